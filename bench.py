@@ -1,0 +1,145 @@
+"""Headline benchmark: AGC logistic regression, synthetic 1e6 x 1e3, 8 workers, s=2, k=6.
+
+Metric (BASELINE.json): "wall-clock sec/iter + iters-to-loss-floor, logistic regression
+n_stragglers=2, 1/2/4/8 MI355X".  One *step* = one full training round of approximate
+gradient coding: master sends beta to every worker rank over RCCL p2p, every logical
+worker computes its (s+1)-replicated gradient with the fused HIP kernel, the master waits
+for the stop rule (k = num_collect arrivals or every FRC group covered), decodes, runs
+the fused combine+AGD update and drains the straggler tail (ref approximate_coding.py).
+The problem is fixed (1e6 x 1e3, W = 8 logical workers) and spread over N GPUs:
+strong scaling.  W % (s+1) != 0 for W=8, s=2, so the FRC groups are {0,1,2},{3,4,5},{6,7}
+(--allow-uneven-groups extension; the reference would refuse this config).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]   (N>1: launched by torchrun)
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+METRIC = "wall-clock sec/iter + iters-to-loss-floor, logistic regression n_stragglers=2, 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n-rows", type=int, default=1_000_000)
+    ap.add_argument("--n-cols", type=int, default=1000)
+    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--stragglers", type=int, default=2)
+    ap.add_argument("--num-collect", type=int, default=6)
+    ap.add_argument("--coded-ver", type=int, default=3)
+    ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32", "bf16"])
+    ap.add_argument("--update-rule", default="AGD")
+    ap.add_argument("--add-delay", type=int, default=0)
+    ap.add_argument("--no-floor", action="store_true", help="skip the 100-round iters-to-loss-floor run")
+    ap.add_argument("--floor-rounds", type=int, default=100)
+    ap.add_argument("--tasks", type=int, default=0)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main() -> int:
+    a = parse()
+    import torch
+
+    from erasurehead_amd.config import RunConfig
+    from erasurehead_amd.engine import Trainer, evaluate
+    from erasurehead_amd.parallel.dist import init_distributed
+
+    env = init_distributed("auto")
+    if env.world != a.gpus and env.is_master:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={env.world}", file=sys.stderr)
+
+    def make_cfg(rounds: int) -> RunConfig:
+        return RunConfig(a.workers + 1, a.n_rows, a.n_cols, "/tmp/erasurehead_bench/", 0, "synthetic", 1,
+                         a.stragglers, 0, a.coded_ver, a.num_collect, a.add_delay, a.update_rule,
+                         num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234, seed=0,
+                         allow_uneven_groups=True, verbose=False, tasks=a.tasks)
+
+    t_setup = time.perf_counter()
+    trainer = Trainer(make_cfg(a.warmup + a.steps), env)
+    setup_s = time.perf_counter() - t_setup
+    res = trainer.run(timed_start=a.warmup)
+    timed = None
+    if env.is_master:
+        timed = res.timed_seconds
+    timed = env.broadcast_object(timed, 0)
+    out = {}
+    if env.is_master:
+        sec_per_iter = timed / a.steps
+        ts = res.timeset[a.warmup:]
+        lt = res.loop_time[a.warmup:]
+        out = {
+            "metric": METRIC,
+            "value": sec_per_iter,
+            "unit": "s/iter",
+            "n_gpus": env.world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": 1e3 * sec_per_iter,
+            "higher_is_better": False,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": a.precision,
+            "data": "synthetic (on-device GMM of ref generate_data.py; random-init beta)",
+            "config": {
+                "model": "L2 logistic regression (d=%d)" % a.n_cols,
+                "scheme": {3: "approx (AGC)", 1: "replication (FRC)", 0: "coded (cyclic MDS)",
+                           2: "avoidstragg"}.get(a.coded_ver, str(a.coded_ver)),
+                "global_batch": a.n_rows,
+                "seq_len": None,
+                "n_rows": a.n_rows, "n_cols": a.n_cols, "workers": a.workers,
+                "n_stragglers": a.stragglers, "num_collect": a.num_collect, "add_delay": a.add_delay,
+                "update_rule": a.update_rule,
+                "parallelism": f"ps-master + {a.workers} logical workers on {env.world} GPU(s) (dp{env.world}, RCCL p2p)",
+            },
+            "time_to_decode_ms_median": float(1e3 * np.median(ts)),
+            "loop_ms_median": float(1e3 * np.median(lt)),
+            "hbm_bytes_per_step_rank0": int(trainer.plan.bytes_per_round) if hasattr(trainer.plan, "bytes_per_round") else None,
+            "setup_s": setup_s,
+            "phases_us": {k: round(v["mean_us"], 1) for k, v in res.phases.items()},
+        }
+        bpr = out["hbm_bytes_per_step_rank0"]
+        if bpr:
+            out["rank0_grad_stream_GBps_at_step_time"] = bpr / sec_per_iter / 1e9
+    # convergence: iterations to the training-loss floor (100-round run, evaluated with the MFMA eval kernel)
+    if not a.no_floor:
+        del trainer
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+        tr2 = Trainer(make_cfg(a.floor_rounds), env)
+        r2 = tr2.run()
+        if env.is_master:
+            tr2.cfg.fix_quirks = True  # evaluate on all partitions
+            ev = evaluate(tr2, r2, write=False)
+            tl = ev.training_loss
+            floor = float(np.min(tl))
+            thr = floor + 0.01 * abs(floor)
+            it = int(np.argmax(tl <= thr))
+            out["iters_to_loss_floor"] = it
+            out["loss_floor"] = floor
+            out["final_train_loss"] = float(tl[-1])
+            out["final_test_auc"] = float(ev.auc[-1])
+            out["floor_run_wallclock_s"] = float(r2.total_time)
+    env.barrier()
+    if env.is_master:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    env.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

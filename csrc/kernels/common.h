@@ -1,0 +1,96 @@
+// Shared device helpers for the ErasureHead MI355X (gfx950 / CDNA4) kernels.
+//
+// Everything here is wave64-native: reductions span 64 lanes, loads are 16 bytes
+// per lane (one dwordx4 per lane = 1 KiB per wave instruction), and storage types
+// are {double, float, bf16} with an fp64 or fp32 accumulator.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace eh {
+
+constexpr int kWave = 64;
+
+// bf16 storage is carried as raw uint16 bits; conversion is a shift (exact).
+struct bf16_t {
+  uint16_t bits;
+};
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t b) {
+  return __uint_as_float(static_cast<uint32_t>(b) << 16);
+}
+
+// Storage-type traits: how many elements fit a 16-byte vector load and how to widen.
+template <typename T> struct Vec16;
+template <> struct Vec16<double> {
+  static constexpr int N = 2;
+  using raw = double2;
+  template <typename A>
+  __device__ __forceinline__ static void load(const double* p, A (&out)[N]) {
+    const double2 v = *reinterpret_cast<const double2*>(p);
+    out[0] = static_cast<A>(v.x);
+    out[1] = static_cast<A>(v.y);
+  }
+};
+template <> struct Vec16<float> {
+  static constexpr int N = 4;
+  template <typename A>
+  __device__ __forceinline__ static void load(const float* p, A (&out)[N]) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    out[0] = static_cast<A>(v.x);
+    out[1] = static_cast<A>(v.y);
+    out[2] = static_cast<A>(v.z);
+    out[3] = static_cast<A>(v.w);
+  }
+};
+template <> struct Vec16<bf16_t> {
+  static constexpr int N = 8;
+  template <typename A>
+  __device__ __forceinline__ static void load(const bf16_t* p, A (&out)[N]) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      out[2 * i] = static_cast<A>(__uint_as_float(w[i] << 16));
+      out[2 * i + 1] = static_cast<A>(__uint_as_float(w[i] & 0xffff0000u));
+    }
+  }
+};
+
+// Full-wave butterfly sum: every lane ends with the total.
+template <typename A>
+__device__ __forceinline__ A wave_allreduce_sum(A v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// Loss epilogues. r is the per-row coefficient that multiplies x_row in the
+// gradient:  g = sum_rows r * x_row.
+//   logistic (ref naive.py:137-139):  g = -X^T( ymod / (exp(y*z) + 1) )  ->  r = -ymod * sigmoid(-y z)
+//   least squares (ref naive.py:345-346): g = -2 X^T (y - z)                ->  r = -2 * c * (y - z)
+enum LossKind : int { kLogistic = 0, kLeastSquares = 1 };
+
+template <typename A>
+__device__ __forceinline__ A sigmoid_neg(A t) {
+  // 1 / (exp(t) + 1), overflow-free in both directions.
+  if (t > A(0)) {
+    const A e = exp(-t);
+    return e / (A(1) + e);
+  }
+  return A(1) / (A(1) + exp(t));
+}
+
+template <int LOSS, typename A>
+__device__ __forceinline__ A residual(A z, A y, A coef) {
+  if constexpr (LOSS == kLogistic) {
+    return -(coef * y) * sigmoid_neg<A>(y * z);
+  } else {
+    return A(-2) * coef * (y - z);
+  }
+}
+
+__host__ __device__ constexpr int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace eh

@@ -1,0 +1,337 @@
+// Fused single-pass worker gradient for dense design matrices (K1+K2+K3+K13 of SURVEY §2.8).
+//
+// Reference semantics (one logical worker, one message):
+//   predy = X_current.dot(beta)                                  ref src/naive.py:137
+//   g = -X_current.T.dot( y_mod / (exp(y * predy) + 1) )         ref src/naive.py:138-139,
+//                                                                 src/coded.py:183-185 (y_mod = B[w,p]*y)
+//   g = -2 X_current.T.dot(y - predy)                             ref src/naive.py:345-346 (least squares)
+//
+// MI355X design: every row of X is read from HBM exactly once.  A wave owns whole
+// rows: its 64 lanes load a row with 16-byte vector loads (1 KiB per wave
+// instruction), form the dot product with beta held in registers, butterfly-reduce
+// it across the wave, apply the loss epilogue (label encoding fused in as a
+// per-segment coefficient) and immediately accumulate r * x_row into a per-lane
+// register slice of g.  Two rows are kept in flight per wave so the reduction
+// latency of one overlaps the loads of the other.  At the end each workgroup
+// folds its 4 waves through LDS and writes one fp64/fp32 slab row; a second tiny
+// kernel sums the slab rows of each output message in a fixed order (bitwise
+// reproducible, no float atomics).
+//
+// The "task" table lets one launch serve every logical worker hosted on this GPU
+// (e.g. all 8 FRC/AGC workers at N=1): task -> (output message slot, segment,
+// row range); segment -> (partition base pointer, labels, encoding coefficient).
+#include "common.h"
+
+namespace eh {
+
+struct Segment {
+  const void* X;      // [nrows, ld] row-major, storage type T
+  const void* y;      // [nrows] labels, accumulator type A
+  double coef;        // label encoding coefficient (cyclic MDS B[w, part]); 1 otherwise
+  long long nrows;
+};
+
+struct Task {
+  int slot;       // output message index
+  int seg;        // segment index
+  int row_begin;  // rows of the segment handled by this workgroup
+  int row_end;
+};
+
+template <typename T, typename A, int CPL, int LOSS>
+__global__ void __launch_bounds__(256)
+grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
+                 const A* __restrict__ beta, A* __restrict__ slab, int ld) {
+  constexpr int VN = Vec16<T>::N;
+  constexpr int NV = CPL / VN;  // vector loads per row per lane
+  static_assert(CPL % VN == 0, "CPL must be a multiple of the vector width");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  A* red = reinterpret_cast<A*>(smem_raw);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+
+  const Task task = tasks[blockIdx.x];
+  const Segment seg = segs[task.seg];
+  const T* __restrict__ X = static_cast<const T*>(seg.X);
+  const A* __restrict__ Y = static_cast<const A*>(seg.y);
+  const A coef = static_cast<A>(seg.coef);
+
+  // Column ownership: vector j of lane l covers columns [(j*64+l)*VN, +VN).
+  bool valid[NV];
+  A b[NV][VN];
+  A g[NV][VN];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * kWave + lane) * VN;
+    valid[j] = c0 < ld;
+#pragma unroll
+    for (int v = 0; v < VN; ++v) {
+      b[j][v] = valid[j] ? beta[c0 + v] : A(0);
+      g[j][v] = A(0);
+    }
+  }
+
+  int r = task.row_begin + wid;
+  // Main loop: two rows per wave per iteration.
+  for (; r + nw < task.row_end; r += 2 * nw) {
+    const T* x0 = X + static_cast<long long>(r) * ld;
+    const T* x1 = X + static_cast<long long>(r + nw) * ld;
+    A a0[NV][VN], a1[NV][VN];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c0 = (j * kWave + lane) * VN;
+      if (valid[j]) {
+        Vec16<T>::load(x0 + c0, a0[j]);
+        Vec16<T>::load(x1 + c0, a1[j]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < VN; ++v) { a0[j][v] = A(0); a1[j][v] = A(0); }
+      }
+    }
+    A z0 = A(0), z1 = A(0);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v) {
+        z0 = fma(a0[j][v], b[j][v], z0);
+        z1 = fma(a1[j][v], b[j][v], z1);
+      }
+    z0 = wave_allreduce_sum(z0);
+    z1 = wave_allreduce_sum(z1);
+    const A r0 = residual<LOSS, A>(z0, Y[r], coef);
+    const A r1 = residual<LOSS, A>(z1, Y[r + nw], coef);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v) g[j][v] = fma(r1, a1[j][v], fma(r0, a0[j][v], g[j][v]));
+  }
+  // Tail: at most one row left for this wave.
+  if (r < task.row_end) {
+    const T* x0 = X + static_cast<long long>(r) * ld;
+    A a0[NV][VN];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c0 = (j * kWave + lane) * VN;
+      if (valid[j]) {
+        Vec16<T>::load(x0 + c0, a0[j]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < VN; ++v) a0[j][v] = A(0);
+      }
+    }
+    A z0 = A(0);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v) z0 = fma(a0[j][v], b[j][v], z0);
+    z0 = wave_allreduce_sum(z0);
+    const A r0 = residual<LOSS, A>(z0, Y[r], coef);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v) g[j][v] = fma(r0, a0[j][v], g[j][v]);
+  }
+
+  // Fold the waves of this workgroup through LDS, then one slab row per workgroup.
+  const int span = kWave * CPL;  // padded columns covered by a wave
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * kWave + lane) * VN;
+#pragma unroll
+    for (int v = 0; v < VN; ++v) red[wid * span + c0 + v] = g[j][v];
+  }
+  __syncthreads();
+  A* out = slab + static_cast<long long>(blockIdx.x) * ld;
+  for (int c = threadIdx.x; c < ld; c += blockDim.x) {
+    A s = A(0);
+    for (int w = 0; w < nw; ++w) s += red[w * span + c];
+    out[c] = s;
+  }
+}
+
+// G[slot, c] = sum over the slot's tasks (in task order) of slab[task, c].
+template <typename A>
+__global__ void __launch_bounds__(256)
+slab_reduce(const A* __restrict__ slab, const int* __restrict__ slot_task_begin,
+            A* __restrict__ G, int ld) {
+  const int slot = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ld) return;
+  const int tb = slot_task_begin[slot];
+  const int te = slot_task_begin[slot + 1];
+  A s0 = A(0), s1 = A(0);
+  int t = tb;
+  for (; t + 1 < te; t += 2) {
+    s0 += slab[static_cast<long long>(t) * ld + c];
+    s1 += slab[static_cast<long long>(t + 1) * ld + c];
+  }
+  if (t < te) s0 += slab[static_cast<long long>(t) * ld + c];
+  G[static_cast<long long>(slot) * ld + c] = s0 + s1;
+}
+
+// ----- Wide-feature fallback (d > 64 * 32): two passes over X, still no atomics. -----
+// Pass 1: one wave per row computes z = x_row . beta and stores the loss residual r.
+template <typename T, typename A, int LOSS>
+__global__ void __launch_bounds__(256)
+rowdot_residual(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
+                const A* __restrict__ beta, const int* __restrict__ task_row_off,
+                A* __restrict__ rbuf, int ld) {
+  constexpr int VN = Vec16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  const Task task = tasks[blockIdx.x];
+  const Segment seg = segs[task.seg];
+  const T* __restrict__ X = static_cast<const T*>(seg.X);
+  const A* __restrict__ Y = static_cast<const A*>(seg.y);
+  const A coef = static_cast<A>(seg.coef);
+  const int off = task_row_off[blockIdx.x];
+  for (int r = task.row_begin + wid; r < task.row_end; r += nw) {
+    const T* x = X + static_cast<long long>(r) * ld;
+    A z = A(0);
+    for (int c0 = lane * VN; c0 < ld; c0 += kWave * VN) {
+      A a[VN];
+      Vec16<T>::load(x + c0, a);
+#pragma unroll
+      for (int v = 0; v < VN; ++v) z = fma(a[v], beta[c0 + v], z);
+    }
+    z = wave_allreduce_sum(z);
+    if (lane == 0) rbuf[off + (r - task.row_begin)] = residual<LOSS, A>(z, Y[r], coef);
+  }
+}
+
+// Pass 2: slab[task, cols] = sum over the task's rows of r_row * x_row[cols].
+template <typename T, typename A>
+__global__ void __launch_bounds__(256)
+xt_r_tiles(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
+           const int* __restrict__ task_row_off, const A* __restrict__ rbuf,
+           A* __restrict__ slab, int ld) {
+  constexpr int VN = Vec16<T>::N;
+  const Task task = tasks[blockIdx.x];
+  const Segment seg = segs[task.seg];
+  const T* __restrict__ X = static_cast<const T*>(seg.X);
+  const int off = task_row_off[blockIdx.x];
+  const int c0 = (blockIdx.y * blockDim.x + threadIdx.x) * VN;
+  if (c0 >= ld) return;
+  A g[VN];
+#pragma unroll
+  for (int v = 0; v < VN; ++v) g[v] = A(0);
+  for (int r = task.row_begin; r < task.row_end; ++r) {
+    A a[VN];
+    Vec16<T>::load(X + static_cast<long long>(r) * ld + c0, a);
+    const A rr = rbuf[off + (r - task.row_begin)];
+#pragma unroll
+    for (int v = 0; v < VN; ++v) g[v] = fma(rr, a[v], g[v]);
+  }
+  A* out = slab + static_cast<long long>(blockIdx.x) * ld + c0;
+#pragma unroll
+  for (int v = 0; v < VN; ++v) out[v] = g[v];
+}
+
+}  // namespace eh
+
+// ---------------------------------------------------------------------------------
+// Host launchers (called from bindings.cpp).
+namespace eh {
+
+template <typename T, typename A, int LOSS>
+static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
+                                   const A* beta, A* slab, int ld, hipStream_t st) {
+  const dim3 block(256);
+  const dim3 grid(ntasks);
+  constexpr int VN = Vec16<T>::N;
+  // CPL (columns per lane) must be a multiple of the 16-byte vector width VN.
+#define EH_IF(C)                                                                          \
+  case C:                                                                                 \
+    if constexpr (C % VN == 0) {                                                          \
+      const size_t sh = 4ull * kWave * C * sizeof(A);                                     \
+      hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS>), grid, block, sh, st, segs,    \
+                         tasks, beta, slab, ld);                                          \
+      return hipGetLastError();                                                           \
+    } else {                                                                              \
+      return hipErrorInvalidValue;                                                        \
+    }
+  switch (cpl) {
+    EH_IF(2)
+    EH_IF(4)
+    EH_IF(8)
+    EH_IF(16)
+    EH_IF(32)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef EH_IF
+}
+
+// dtype codes: 0 = fp64 storage/fp64 acc, 1 = fp32/fp32, 2 = bf16 storage/fp32 acc
+hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
+                             int ntasks, const void* beta, void* slab, const int* slot_task_begin,
+                             int nslots, void* G, int ld, hipStream_t st) {
+  const Segment* S = static_cast<const Segment*>(segs);
+  const Task* Tk = static_cast<const Task*>(tasks);
+  hipError_t e = hipSuccess;
+  if (dtype == 0) {
+    e = loss == kLogistic
+            ? launch_fused_cpl<double, double, kLogistic>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st)
+            : launch_fused_cpl<double, double, kLeastSquares>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st);
+  } else if (dtype == 1) {
+    e = loss == kLogistic
+            ? launch_fused_cpl<float, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st)
+            : launch_fused_cpl<float, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st);
+  } else {
+    e = loss == kLogistic
+            ? launch_fused_cpl<bf16_t, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st)
+            : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st);
+  }
+  if (e != hipSuccess) return e;
+  const dim3 block(256);
+  const dim3 grid(ceil_div(ld, 256), nslots);
+  if (dtype == 0) {
+    hipLaunchKernelGGL(slab_reduce<double>, grid, block, 0, st, (const double*)slab, slot_task_begin, (double*)G, ld);
+  } else {
+    hipLaunchKernelGGL(slab_reduce<float>, grid, block, 0, st, (const float*)slab, slot_task_begin, (float*)G, ld);
+  }
+  return hipGetLastError();
+}
+
+
+hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, const void* tasks,
+                                     int ntasks, const void* beta, const int* task_row_off,
+                                     void* rbuf, void* slab, const int* slot_task_begin,
+                                     int nslots, void* G, int ld, hipStream_t st) {
+  const Segment* S = static_cast<const Segment*>(segs);
+  const Task* Tk = static_cast<const Task*>(tasks);
+  const dim3 block(256);
+  if (dtype == 0) {
+    if (loss == kLogistic)
+      hipLaunchKernelGGL((rowdot_residual<double, double, kLogistic>), dim3(ntasks), block, 0, st, S, Tk, (const double*)beta, task_row_off, (double*)rbuf, ld);
+    else
+      hipLaunchKernelGGL((rowdot_residual<double, double, kLeastSquares>), dim3(ntasks), block, 0, st, S, Tk, (const double*)beta, task_row_off, (double*)rbuf, ld);
+    hipLaunchKernelGGL((xt_r_tiles<double, double>), dim3(ntasks, ceil_div(ld, 256 * 2)), block, 0, st, S, Tk, task_row_off, (const double*)rbuf, (double*)slab, ld);
+  } else if (dtype == 1) {
+    if (loss == kLogistic)
+      hipLaunchKernelGGL((rowdot_residual<float, float, kLogistic>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld);
+    else
+      hipLaunchKernelGGL((rowdot_residual<float, float, kLeastSquares>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld);
+    hipLaunchKernelGGL((xt_r_tiles<float, float>), dim3(ntasks, ceil_div(ld, 256 * 4)), block, 0, st, S, Tk, task_row_off, (const float*)rbuf, (float*)slab, ld);
+  } else {
+    if (loss == kLogistic)
+      hipLaunchKernelGGL((rowdot_residual<bf16_t, float, kLogistic>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld);
+    else
+      hipLaunchKernelGGL((rowdot_residual<bf16_t, float, kLeastSquares>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld);
+    hipLaunchKernelGGL((xt_r_tiles<bf16_t, float>), dim3(ntasks, ceil_div(ld, 256 * 8)), block, 0, st, S, Tk, task_row_off, (const float*)rbuf, (float*)slab, ld);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const dim3 grid(ceil_div(ld, 256), nslots);
+  if (dtype == 0)
+    hipLaunchKernelGGL(slab_reduce<double>, grid, block, 0, st, (const double*)slab, slot_task_begin, (double*)G, ld);
+  else
+    hipLaunchKernelGGL(slab_reduce<float>, grid, block, 0, st, (const float*)slab, slot_task_begin, (float*)G, ld);
+  return hipGetLastError();
+}
+
+}  // namespace eh

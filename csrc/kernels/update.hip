@@ -1,0 +1,78 @@
+// Master-side decode-combine + GD/AGD model update in ONE launch (K5 + K7 + K8 of SURVEY §2.8).
+//
+// Reference semantics:
+//   combine   g = sum_m a_m * msg_m                      ref src/coded.py:147-149 (lstsq decode),
+//                                                        src/approximate_coding.py:150-158 (FRC first-per-group),
+//                                                        src/naive.py:109 (plain sum)
+//   GD        beta = (1 - 2 alpha eta) beta - (eta/n) g   ref src/naive.py:112-115
+//   AGD       theta = 2/(i+2); y = (1-theta) beta + theta u
+//             beta' = y - (eta/n) g - 2 alpha eta beta; u = beta + (beta'-beta)/theta   ref src/naive.py:116-122
+//             (avoidstragg rescales eta/n by W/(W-s): ref src/avoidstragg.py:116)
+//
+// The decode coefficients a_m (fp64, solved on the host) and the message pointers are
+// passed by value in the kernel arguments, so a round's combine+update is a single
+// launch with no host->device copies.  Every column is independent: a thread per
+// column streams the m message rows (coalesced), keeps everything in fp64 registers
+// and writes beta, u, the betaset history row and the worker-dtype copy of beta that
+// the next round's gradient kernels (and the p2p sends) read.
+#include "common.h"
+
+namespace eh {
+
+constexpr int kMaxMsgs = 128;
+
+struct CombineArgs {
+  const void* msg[kMaxMsgs];
+  double coef[kMaxMsgs];
+  int nmsg;
+};
+
+template <typename M, typename W>
+__global__ void __launch_bounds__(256)
+combine_update(const CombineArgs args, double* __restrict__ beta, double* __restrict__ u,
+               double* __restrict__ hist, W* __restrict__ beta_w, double* __restrict__ g_out,
+               int d, int ld, double decay, double gm, double l2, double theta, int rule) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ld) return;
+  if (c >= d) {  // padded columns stay exactly zero
+    if (beta_w) beta_w[c] = W(0);
+    return;
+  }
+  double g = 0.0;
+  for (int m = 0; m < args.nmsg; ++m) {
+    const M* p = static_cast<const M*>(args.msg[m]);
+    g = fma(args.coef[m], static_cast<double>(p[c]), g);
+  }
+  const double b = beta[c];
+  double nb;
+  if (rule == 0) {  // GD
+    nb = decay * b - gm * g;
+  } else {  // AGD (gradient evaluated at beta, exactly as the reference)
+    const double yt = (1.0 - theta) * b + theta * u[c];
+    nb = yt - gm * g - l2 * b;
+    u[c] = b + (nb - b) * (1.0 / theta);
+  }
+  beta[c] = nb;
+  if (hist) hist[c] = nb;
+  if (beta_w) beta_w[c] = static_cast<W>(nb);
+  if (g_out) g_out[c] = g;
+}
+
+// msg dtype: 0 fp64, 1 fp32; worker beta dtype: 0 fp64, 1 fp32
+hipError_t combine_update_launch(const CombineArgs& args, int msg_dtype, int w_dtype,
+                                 double* beta, double* u, double* hist, void* beta_w,
+                                 double* g_out, int d, int ld, double decay, double gm,
+                                 double l2, double theta, int rule, hipStream_t st) {
+  const dim3 block(256), grid(ceil_div(ld, 256));
+  if (msg_dtype == 0 && w_dtype == 0)
+    hipLaunchKernelGGL((combine_update<double, double>), grid, block, 0, st, args, beta, u, hist, (double*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule);
+  else if (msg_dtype == 0 && w_dtype == 1)
+    hipLaunchKernelGGL((combine_update<double, float>), grid, block, 0, st, args, beta, u, hist, (float*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule);
+  else if (msg_dtype == 1 && w_dtype == 0)
+    hipLaunchKernelGGL((combine_update<float, double>), grid, block, 0, st, args, beta, u, hist, (double*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule);
+  else
+    hipLaunchKernelGGL((combine_update<float, float>), grid, block, 0, st, args, beta, u, hist, (float*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule);
+  return hipGetLastError();
+}
+
+}  // namespace eh

@@ -1,0 +1,240 @@
+// Native arrival collector (see collector.h for the reference semantics it reproduces).
+#include "collector.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <limits>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
+namespace eh {
+
+static constexpr double kInf = std::numeric_limits<double>::infinity();
+
+Collector::Collector(int n_workers, std::vector<int> group_of, int n_groups)
+    : W_(n_workers), group_of_(std::move(group_of)), n_groups_(n_groups) {
+  if (W_ <= 0) throw std::invalid_argument("Collector: n_workers must be > 0");
+  if (static_cast<int>(group_of_.size()) != W_) group_of_.assign(W_, 0);
+  for (int g : group_of_)
+    if (g < 0 || g >= std::max(n_groups_, 1)) throw std::invalid_argument("Collector: bad group id");
+  finish_.assign(W_, {});
+  got0_.assign(W_, 0);
+  got1_.assign(W_, 0);
+  group_done_.assign(std::max(n_groups_, 1), 0);
+}
+
+double Collector::now() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+void Collector::begin_round(int round, double t_start, int rule, int k) {
+  if (round <= round_) throw std::invalid_argument("Collector: rounds must increase");
+  round_ = round;
+  t_start_ = t_start;
+  rule_ = rule;
+  k_ = k;
+  stopped_ = false;
+  if (static_cast<int>(round_start_.size()) <= round) round_start_.resize(round + 1, 0.0);
+  round_start_[round] = t_start;
+  cur_.clear();
+  late_.clear();
+  std::fill(got0_.begin(), got0_.end(), 0);
+  std::fill(got1_.begin(), got1_.end(), 0);
+  std::fill(group_done_.begin(), group_done_.end(), 0);
+  cnt0_ = cnt1_ = cnt_groups_ = 0;
+}
+
+int Collector::add_event_probe(int worker, int part, int round, uintptr_t event, double delay) {
+  if (worker < 0 || worker >= W_) throw std::invalid_argument("Collector: bad worker");
+  Probe p{worker, part, round, reinterpret_cast<hipEvent_t>(event), false, false, false, 0.0, delay, kInf};
+  probes_.push_back(p);
+  live_.push_back(static_cast<int>(probes_.size()) - 1);
+  return static_cast<int>(probes_.size()) - 1;
+}
+
+int Collector::add_host_probe(int worker, int part, int round, double delay) {
+  if (worker < 0 || worker >= W_) throw std::invalid_argument("Collector: bad worker");
+  Probe p{worker, part, round, nullptr, true, false, false, 0.0, delay, kInf};
+  probes_.push_back(p);
+  live_.push_back(static_cast<int>(probes_.size()) - 1);
+  return static_cast<int>(probes_.size()) - 1;
+}
+
+double Collector::finish_of(int worker, int round) const {
+  if (round < 0) return -kInf;
+  const auto& f = finish_[worker];
+  if (round >= static_cast<int>(f.size())) return -kInf;
+  return f[round];
+}
+
+void Collector::mark_seen(int id, double t) {
+  Probe& p = probes_.at(id);
+  if (p.seen) return;
+  p.seen = true;
+  p.t_seen = t;
+  const double ts = p.round < static_cast<int>(round_start_.size()) ? round_start_[p.round] : t;
+  const double start = std::max(ts, finish_of(p.worker, p.round - 1));
+  const double compute = std::max(0.0, t - ts);
+  p.ready = start + compute + p.delay;
+  auto& f = finish_[p.worker];
+  if (static_cast<int>(f.size()) <= p.round) f.resize(p.round + 1, -kInf);
+  f[p.round] = std::max(f[p.round], p.ready);
+}
+
+void Collector::poll_events(double t) {
+  for (int id : live_) {
+    Probe& p = probes_[id];
+    if (p.seen || p.host) continue;
+    const hipError_t e = hipEventQuery(p.ev);
+    if (e == hipSuccess) {
+      mark_seen(id, t);
+    } else if (e != hipErrorNotReady) {
+      throw std::runtime_error(std::string("Collector: hipEventQuery failed: ") + hipGetErrorString(e));
+    }
+  }
+}
+
+bool Collector::rule_holds() const {
+  switch (rule_) {
+    case kRuleAll: return cnt0_ >= W_;
+    case kRuleCount: return cnt0_ >= k_;
+    case kRuleFrc: return cnt0_ >= k_ || cnt_groups_ >= n_groups_;
+    case kRulePartialFrc: return cnt1_ >= W_ && cnt_groups_ >= n_groups_;
+    case kRulePartialCount: return cnt1_ >= W_ && cnt0_ >= k_;
+    default: return true;
+  }
+}
+
+bool Collector::process_ready(double t, bool /*stop_at_rule*/) {
+  // Ready probes, in virtual arrival order.
+  std::vector<int> ready;
+  for (int id : live_) {
+    const Probe& p = probes_[id];
+    if (p.seen && p.ready <= t) ready.push_back(id);
+  }
+  if (ready.empty()) return stopped_;
+  std::sort(ready.begin(), ready.end(), [&](int a, int b) {
+    if (probes_[a].ready != probes_[b].ready) return probes_[a].ready < probes_[b].ready;
+    return a < b;
+  });
+  for (int id : ready) {
+    Probe& p = probes_[id];
+    p.arrived = true;
+    const Arrival a{p.worker, p.part, p.round, p.ready - round_start_[p.round], id};
+    if (p.round != round_) continue;  // stale message of an earlier round: drained, ignored
+    if (stopped_) {
+      late_.push_back(a);
+      continue;
+    }
+    cur_.push_back(a);
+    if (p.part == 0) {
+      if (!got0_[p.worker]) {
+        got0_[p.worker] = 1;
+        ++cnt0_;
+        const int g = group_of_[p.worker];
+        if (!group_done_[g]) {
+          group_done_[g] = 1;
+          ++cnt_groups_;
+        }
+      }
+    } else if (!got1_[p.worker]) {
+      got1_[p.worker] = 1;
+      ++cnt1_;
+    }
+    if (rule_holds()) stopped_ = true;
+  }
+  live_.erase(std::remove_if(live_.begin(), live_.end(), [&](int id) { return probes_[id].arrived; }),
+              live_.end());
+  return stopped_;
+}
+
+bool Collector::step() {
+  const double t = now();
+  poll_events(t);
+  return process_ready(t, true);
+}
+
+static void pause_for(double dt) {
+  if (dt > 2e-4) {
+    std::this_thread::sleep_for(std::chrono::duration<double>(std::min(dt - 1e-4, 1e-3)));
+  } else {
+#if defined(__x86_64__)
+    for (int i = 0; i < 32; ++i) _mm_pause();
+#endif
+  }
+}
+
+bool Collector::wait(double timeout) {
+  if (round_ < 0) throw std::logic_error("Collector::wait before begin_round");
+  if (rule_holds()) stopped_ = true;  // e.g. k = 0
+  for (;;) {
+    const double t = now();
+    poll_events(t);
+    if (process_ready(t, true)) return true;
+    if (t - t_start_ > timeout) return false;
+    double next = kInf;
+    for (int id : live_) {
+      const Probe& p = probes_[id];
+      if (p.seen) next = std::min(next, p.ready);
+    }
+    bool unseen_event = false;
+    for (int id : live_)
+      if (!probes_[id].seen && !probes_[id].host) { unseen_event = true; break; }
+    double dt = next - t;
+    if (unseen_event) dt = std::min(dt, 2e-5);  // keep polling hardware events tightly
+    dt = std::min(dt, t_start_ + timeout - t);
+    pause_for(std::max(dt, 0.0));
+  }
+}
+
+bool Collector::drain(int round, double timeout) {
+  const double t0 = now();
+  for (;;) {
+    const double t = now();
+    poll_events(t);
+    process_ready(t, true);
+    bool left = false;
+    double next = kInf;
+    bool unseen_event = false;
+    for (int id : live_) {
+      const Probe& p = probes_[id];
+      if (p.round > round) continue;
+      if (p.seen && std::isinf(p.delay)) continue;  // dead worker: its message was received
+      left = true;
+      if (p.seen) next = std::min(next, p.ready);
+      else if (!p.host) unseen_event = true;
+    }
+    if (!left) return true;
+    if (t - t0 > timeout) return false;
+    double dt = next - t;
+    if (unseen_event) dt = std::min(dt, 2e-5);
+    pause_for(std::max(std::min(dt, t0 + timeout - t), 0.0));
+  }
+}
+
+std::vector<Arrival> Collector::late_arrivals(int round) const {
+  if (round != round_) return {};
+  return late_;
+}
+
+int Collector::pending() const { return static_cast<int>(live_.size()); }
+
+int Collector::pending_upto(int round) const {
+  int n = 0;
+  for (int id : live_) {
+    const Probe& p = probes_[id];
+    if (p.round > round) continue;
+    if (p.seen && std::isinf(p.delay)) continue;
+    ++n;
+  }
+  return n;
+}
+
+}  // namespace eh

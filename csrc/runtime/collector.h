@@ -1,0 +1,111 @@
+// Straggler-aware arrival collector: the native "Waitany" of the engine.
+//
+// Reference: the master's wait-for-the-fastest loop is an MPI Waitany over
+// pre-posted Irecvs plus a per-scheme stop condition
+//   naive         while cnt < W                                   ref src/naive.py:103
+//   cyclic/avoid  while cnt < W - s                               ref src/coded.py:137, src/avoidstragg.py:106
+//   FRC / AGC     while cnt_workers < k and cnt_groups < n_groups  ref src/approximate_coding.py:144
+//   partial_*     first parts from all W AND (groups | W - s)     ref src/partial_replication.py:166,
+//                                                                 src/partial_coded.py:174
+// and an optional Waitall drain (ref src/approximate_coding.py:182-183).
+//
+// Here a "probe" is one expected message (worker, part, round).  GPU probes are HIP
+// events recorded behind the RCCL receive (or behind the local gradient kernel for
+// workers hosted in the master's own process); host probes are completed by the
+// caller (gloo / CPU path).  The poll loop runs in C++ with the GIL released.
+//
+// Straggler model: the reference injects  sleep(Exp(0.5)[w])  on the worker after
+// compute and before the send (ref src/naive.py:141-148).  GPUs never sleep here;
+// the same deterministic delay is applied by the collector as a virtual arrival time
+//     ready = max(t_start(round), finish(w, round-1)) + (t_seen - t_start(round)) + delay
+// which reproduces the reference's arrival order and wall-clock (including the lag a
+// straggler carries into the next round when the scheme does not drain), while the
+// hardware stays busy.  delay = +inf models a dead worker (an erasure that never
+// arrives; bounded by the round timeout instead of hanging like the reference).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace eh {
+
+enum RuleKind : int {
+  kRuleAll = 0,           // every worker's part 0
+  kRuleCount = 1,         // k part-0 arrivals
+  kRuleFrc = 2,           // k workers OR every group covered
+  kRulePartialFrc = 3,    // all part-1 AND every group covered by part 0
+  kRulePartialCount = 4,  // all part-1 AND k part-0 arrivals
+};
+
+struct Arrival {
+  int worker;
+  int part;
+  int round;
+  double t_rel;  // virtual arrival time relative to the round start
+  int probe;
+};
+
+class Collector {
+ public:
+  Collector(int n_workers, std::vector<int> group_of, int n_groups);
+
+  static double now();
+
+  void begin_round(int round, double t_start, int rule, int k);
+  int add_event_probe(int worker, int part, int round, uintptr_t event, double delay);
+  int add_host_probe(int worker, int part, int round, double delay);
+  void mark_seen(int probe, double t);
+
+  // Process everything that is ready; returns true once the current round's stop rule holds.
+  bool step();
+  // Blocking poll until the stop rule holds or `timeout` seconds after the round start.
+  // Returns true when the rule was satisfied, false on timeout.
+  bool wait(double timeout);
+  // Blocking: until every probe of rounds <= `round` has arrived (dead ones: been seen).
+  bool drain(int round, double timeout);
+
+  const std::vector<Arrival>& arrivals() const { return cur_; }
+  std::vector<Arrival> late_arrivals(int round) const;  // arrivals after the stop, this round
+  int pending() const;
+  // Live probes of rounds <= `round` that a drain would still wait for.
+  int pending_upto(int round) const;
+  bool stopped() const { return stopped_; }
+
+ private:
+  struct Probe {
+    int worker, part, round;
+    hipEvent_t ev;
+    bool host;
+    bool seen;
+    bool arrived;
+    double t_seen;
+    double delay;
+    double ready;
+  };
+  void poll_events(double t);
+  bool process_ready(double t, bool stop_at_rule);
+  bool rule_holds() const;
+  double finish_of(int worker, int round) const;
+
+  int W_;
+  std::vector<int> group_of_;
+  int n_groups_;
+  int round_ = -1;
+  double t_start_ = 0.0;
+  int rule_ = kRuleAll;
+  int k_ = 0;
+  bool stopped_ = false;
+  std::vector<double> round_start_;
+  std::vector<std::vector<double>> finish_;  // [worker][round] virtual finish
+  std::vector<Probe> probes_;
+  std::vector<int> live_;  // probe ids not yet arrived
+  std::vector<Arrival> cur_;
+  std::vector<Arrival> late_;
+  // per current round counters
+  std::vector<char> got0_, got1_, group_done_;
+  int cnt0_ = 0, cnt1_ = 0, cnt_groups_ = 0;
+};
+
+}  // namespace eh

@@ -1,0 +1,99 @@
+"""Reference-compatible command line (ref main.py).
+
+    python main.py n_procs n_rows n_cols input_dir is_real dataset is_coded n_stragglers \\
+                   partitions coded_ver num_collect add_delay update_rule  [--extension flags]
+
+Single GPU / CPU: run directly.  Several MI355X of one node: one process per GPU,
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 main.py <13 args> [flags]
+The n_procs argument keeps the reference meaning (1 master + n_procs-1 logical workers);
+the logical workers are spread over however many processes were launched.
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+from typing import List, Optional
+
+from .config import RunConfig
+
+USAGE = ("Usage: python main.py n_procs n_rows n_cols input_dir is_real dataset is_coded n_stragglers "
+         "partial_straggler_partitions coded_ver num_itrs")  # verbatim (stale) reference usage line, ref main.py:21
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="main.py", add_help=True)
+    p.add_argument("positional", nargs="*")
+    g = p.add_argument_group("extensions (defaults reproduce the reference)")
+    g.add_argument("--precision", default="fp64", choices=["fp64", "fp32", "bf16"])
+    g.add_argument("--loss", default="auto", choices=["auto", "logistic", "least_squares"])
+    g.add_argument("--num-itrs", type=int, default=100)
+    g.add_argument("--lr", type=float, default=10.0)
+    g.add_argument("--alpha", type=float, default=None)
+    g.add_argument("--seed", type=int, default=None)
+    g.add_argument("--data", default="files", choices=["files", "synthetic"])
+    g.add_argument("--data-seed", type=int, default=0)
+    g.add_argument("--allow-uneven-groups", action="store_true")
+    g.add_argument("--drain", default=None, choices=["all", "lazy"])
+    g.add_argument("--delay-mode", default="exp", choices=["exp", "fixed", "none"])
+    g.add_argument("--fixed-stragglers", type=int, nargs="*", default=[])
+    g.add_argument("--fixed-sleep", type=float, default=0.5)
+    g.add_argument("--kill-workers", type=int, nargs="*", default=[])
+    g.add_argument("--force-delay", action="store_true")
+    g.add_argument("--round-timeout", type=float, default=600.0)
+    g.add_argument("--fix-quirks", action="store_true")
+    g.add_argument("--save-linear", action="store_true")
+    g.add_argument("--full-precision-outputs", action="store_true")
+    g.add_argument("--no-eval", action="store_true")
+    g.add_argument("--quiet", action="store_true")
+    g.add_argument("--checkpoint-every", type=int, default=0)
+    g.add_argument("--checkpoint-path", default=None)
+    g.add_argument("--trace", action="store_true")
+    g.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
+    return p
+
+
+def parse(argv: List[str]):
+    a = build_parser().parse_args(argv)
+    if len(a.positional) != 13:
+        return None, a
+    (n_procs, n_rows, n_cols, input_dir, is_real, dataset, is_coded, n_stragglers, partitions, coded_ver,
+     num_collect, add_delay, update_rule) = a.positional
+    cfg = RunConfig(int(n_procs), int(n_rows), int(n_cols), input_dir, int(is_real), dataset, int(is_coded),
+                    int(n_stragglers), int(partitions), int(coded_ver), int(num_collect), int(add_delay),
+                    update_rule, num_itrs=a.num_itrs, alpha=a.alpha, lr=a.lr, precision=a.precision, loss=a.loss,
+                    seed=a.seed, data=a.data, data_seed=a.data_seed, allow_uneven_groups=a.allow_uneven_groups,
+                    drain=a.drain, delay_mode=a.delay_mode, fixed_stragglers=a.fixed_stragglers,
+                    fixed_sleep=a.fixed_sleep, kill_workers=a.kill_workers, force_delay=a.force_delay,
+                    round_timeout=a.round_timeout, fix_quirks=a.fix_quirks, save_linear=a.save_linear,
+                    full_precision_outputs=a.full_precision_outputs, evaluate=not a.no_eval, verbose=not a.quiet,
+                    checkpoint_every=a.checkpoint_every, checkpoint_path=a.checkpoint_path, trace=a.trace)
+    return cfg, a
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    cfg, a = parse(argv)
+    if cfg is None:
+        print(USAGE)
+        return 0
+    from .codes.schemes import SchemeError
+    from .engine import Trainer, evaluate
+    from .parallel.dist import init_distributed
+    from .utils import tracing
+
+    tracing.enable(cfg.trace)
+    env = init_distributed(a.device)
+    try:
+        try:
+            trainer = Trainer(cfg, env)
+        except SchemeError as e:  # the reference prints and exits 0 (ref src/replication.py:24-26)
+            if env.is_master:
+                print(str(e))
+            return 0
+        res = trainer.run()
+        if env.is_master and cfg.evaluate:
+            evaluate(trainer, res)
+        env.barrier()
+    finally:
+        env.shutdown()
+    return 0

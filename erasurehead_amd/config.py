@@ -1,0 +1,88 @@
+"""Run configuration: the reference's 13 positional arguments + hard-coded constants + extensions.
+
+Positional CLI (ref main.py:20-27):
+  n_procs n_rows n_cols input_dir is_real dataset is_coded n_stragglers partitions coded_ver
+  num_collect add_delay update_rule
+Constants (ref main.py:31-53): num_itrs = 100, alpha = 1/n_rows, eta_i = 10.0 for every round.
+
+Everything past the 13 positionals is an opt-in extension (``--flags`` in cli.py); the
+defaults reproduce the reference, including its quirks, unless
+``fix_quirks`` is set.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+
+@dataclass
+class RunConfig:
+    n_procs: int
+    n_rows: int
+    n_cols: int
+    input_dir: str
+    is_real: int = 0
+    dataset: str = "synthetic"
+    is_coded: int = 0
+    n_stragglers: int = 0
+    partitions: int = 0
+    coded_ver: int = 0
+    num_collect: int = 0
+    add_delay: int = 0
+    update_rule: str = "GD"
+
+    # ---- reference constants (ref main.py:31-46) ----------------------------------
+    num_itrs: int = 100
+    alpha: Optional[float] = None  # default 1 / n_rows
+    lr: float = 10.0  # learning_rate_schedule = lr * ones(num_itrs)
+    lr_schedule: Optional[List[float]] = None
+
+    # ---- extensions -----------------------------------------------------------------
+    precision: str = "fp64"  # fp64 | fp32 | bf16 worker compute (master state always fp64)
+    loss: str = "auto"  # auto (reference dispatch) | logistic | least_squares
+    seed: Optional[int] = None  # beta_0 / B matrix seed (reference: unseeded)
+    data: str = "files"  # files | synthetic (on-device generator, no files)
+    data_seed: int = 0
+    allow_uneven_groups: bool = False  # FRC with W % (s+1) != 0
+    drain: Optional[str] = None  # None = scheme default; "all" | "lazy"
+    delay_mode: str = "exp"  # exp (reference) | fixed | none
+    delay_mean: float = 0.5
+    fixed_stragglers: List[int] = field(default_factory=list)  # 1-based worker ids (fixed mode)
+    fixed_sleep: float = 0.5
+    kill_workers: List[int] = field(default_factory=list)  # 1-based ids that never arrive
+    force_delay: bool = False  # inject delays even where the reference does not
+    round_timeout: float = 600.0  # master waits at most this long per round (dead worker -> erasure)
+    fix_quirks: bool = False
+    save_linear: bool = False  # reference comments the linear-model outputs out
+    full_precision_outputs: bool = False
+    evaluate: bool = True
+    verbose: bool = True
+    checkpoint_every: int = 0
+    checkpoint_path: Optional[str] = None
+    resume: Optional[str] = None
+    trace: bool = False
+    tasks: int = 0  # override gradient-kernel workgroup count
+
+    def __post_init__(self):
+        self.update_rule = str(self.update_rule)
+        if self.update_rule not in ("GD", "AGD"):
+            raise ValueError("update_rule must be GD or AGD")  # ref src/naive.py:13 assert
+        self.input_dir = self.input_dir if self.input_dir.endswith("/") else self.input_dir + "/"
+
+    @property
+    def n_workers(self) -> int:
+        return self.n_procs - 1
+
+    @property
+    def alpha_value(self) -> float:
+        return 1.0 / self.n_rows if self.alpha is None else self.alpha
+
+    def eta(self) -> np.ndarray:
+        if self.lr_schedule is not None:
+            s = np.asarray(self.lr_schedule, dtype=np.float64)
+            if len(s) < self.num_itrs:
+                raise ValueError("lr_schedule shorter than num_itrs")
+            return s
+        return self.lr * np.ones(self.num_itrs)

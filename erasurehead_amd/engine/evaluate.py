@@ -1,0 +1,76 @@
+"""Master epilogue: evaluate every stored beta, print, save (ref src/naive.py:153-209).
+
+Reference quirks reproduced unless ``fix_quirks``:
+  * the training set is partitions 1..W-1 — partition W is skipped (ref src/naive.py:161,167
+    ``range(2, n_procs-1)``), labels are the matching prefix of label.dat (ref :172);
+  * linear-regression runs print but do not write result files (ref src/naive.py:413-417);
+  * result names follow each scheme's (colliding) prefixes (codes/schemes.py).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..data import io as dio
+from ..models.losses import LOGISTIC
+from ..ops.eval import auc_columns, loss_sums, predictions
+from ..utils import report
+from .trainer import TrainResult, Trainer
+
+
+@dataclass
+class EvalResult:
+    training_loss: np.ndarray
+    testing_loss: np.ndarray
+    auc: np.ndarray
+    n_train: int
+    n_test: int
+    files: Optional[Dict[str, str]] = None
+
+
+def eval_partitions(trainer: Trainer):
+    W = trainer.cfg.n_workers
+    if trainer.cfg.fix_quirks:
+        return list(range(trainer.scheme.n_partition_files))
+    return list(range(max(1, W - 1)))
+
+
+def evaluate(trainer: Trainer, res: TrainResult, log=None, write: bool = True) -> EvalResult:
+    log = log or report.log
+    cfg = trainer.cfg
+    dev = trainer.env.device
+    prec = trainer.prec
+    d, ld = trainer.d, trainer.ld
+    R = res.betaset.shape[0]
+    B = torch.zeros((R, ld), dtype=torch.float64, device=dev)
+    B[:, :d] = torch.from_numpy(res.betaset).to(dev)
+    kind = trainer.loss
+    sums, n_train = loss_sums(trainer.source.train_eval_chunks(eval_partitions(trainer), prec, dev), B, d, kind)
+    Xt, yt = trainer.source.test(prec, dev)
+    P = predictions(Xt, B, d)
+    from ..ops.eval import _loss_torch
+
+    tsum = _loss_torch(kind, yt.to(P.device), P).double().cpu().numpy()
+    n_test = Xt.shape[0]
+    training_loss = sums / max(1, n_train)
+    testing_loss = tsum / max(1, n_test)
+    auc = auc_columns(yt, P) if kind == LOGISTIC else np.zeros(R)
+    if cfg.verbose:
+        log(report.total_time_line(res.total_time))
+        for i in range(R):
+            if kind == LOGISTIC:
+                log(report.logistic_line(i, training_loss[i], testing_loss[i], auc[i], res.timeset[i]))
+            else:
+                log(report.linear_line(i, training_loss[i], testing_loss[i], res.timeset[i]))
+    files = None
+    if write and (kind == LOGISTIC or cfg.save_linear):
+        names = trainer.scheme.output_names(cfg.fix_quirks)
+        data_dir = getattr(trainer.source, "data_dir", None) or cfg.input_dir
+        files = report.write_results(dio.results_dir(data_dir), names, training_loss, testing_loss, auc,
+                                     res.timeset, res.worker_timeset, cfg.full_precision_outputs)
+    if cfg.verbose:
+        log(">>> Done")
+    return EvalResult(training_loss, testing_loss, auc, n_train, n_test, files)

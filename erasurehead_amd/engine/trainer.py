@@ -1,0 +1,426 @@
+"""The generic straggler-tolerant training engine (L4), one loop for every scheme.
+
+Reference skeleton (ref src/naive.py:11-211, repeated in all seven engine files):
+load shard -> warm-up gradient -> pre-post receives -> Barrier -> per round {master:
+Isend beta to all, Waitany until the stop rule, decode, GD/AGD update, record times;
+worker: Wait beta, gradient, optional delay, Isend g} -> Barrier -> master evaluates
+every stored beta and writes results/*.dat.
+
+MI355X design:
+  * one process per GPU; logical workers are placed on ranks (parallel/placement.py) and
+    each rank computes ALL its workers' messages with one fused kernel launch per round
+    (ops/grad.py), reading its resident partitions from HBM exactly once;
+  * rank 0 is also the master: local messages are probed with a HIP event behind the
+    gradient kernel, remote messages with a HIP event behind the RCCL receive on the
+    per-peer stream; the native collector decides arrival order / the stop rule with the
+    GIL released (parallel/collector.py);
+  * decode coefficients are solved on the host in fp64 (codes/), then one
+    ``combine_update`` launch forms g and updates beta/u/betaset/worker-beta on the GPU;
+  * worker ranks never block their host: receive, kernel and sends are stream-ordered,
+    ring buffers are protected by device-side event waits;
+  * every buffer is per (round mod K) — no aliasing of beta or message buffers across
+    rounds (the reference's latent races, SURVEY §5.2, cannot happen);
+  * the injected straggler delay is a virtual arrival time (utils/delay.py), so the
+    same wall-clock semantics as the reference hold while the GPUs never sleep.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..codes.schemes import Scheme, SchemeError, make_scheme, scheme_key
+from ..config import RunConfig
+from ..data import io as dio
+from ..data.source import DataSource, FileSource, SyntheticSource
+from ..models.losses import LEAST_SQUARES, LOGISTIC, UpdateRule
+from ..ops.grad import DenseGradPlan, SparseGradPlan
+from ..ops.precision import get_precision
+from ..ops.update import combine_update
+from ..parallel.collector import ArrivalCollector
+from ..parallel.dist import DistEnv
+from ..parallel.placement import place_workers, workers_by_rank
+from ..utils import report
+from ..utils.delay import DelayModel
+from ..utils.tracing import PhaseTimer, range_
+
+TAG_STRIDE = 1024  # gloo tags: beta of round i = 2*i*S, message j of round i = 2*(i*S+j)+1
+
+
+def _tag_beta(i: int) -> int:
+    return 2 * i * TAG_STRIDE
+
+
+def _tag_msg(i: int, j: int) -> int:
+    return 2 * (i * TAG_STRIDE + j) + 1
+
+
+@dataclass
+class TrainResult:
+    scheme: str
+    betaset: np.ndarray  # [R, d] beta after each round (fp64)
+    timeset: np.ndarray  # [R] time-to-decode per round (reference semantics)
+    worker_timeset: np.ndarray  # [R, W]
+    loop_time: np.ndarray  # [R] true per-round wall-clock incl. drain
+    total_time: float
+    timed_seconds: Optional[float] = None
+    timed_rounds: int = 0
+    timeouts: int = 0
+    phases: Dict[str, Dict[str, float]] = field(default_factory=dict)
+    arrivals: List[List[Tuple[int, int, float]]] = field(default_factory=list)
+
+
+class Trainer:
+    def __init__(self, cfg: RunConfig, env: Optional[DistEnv] = None, source: Optional[DataSource] = None,
+                 scheme: Optional[Scheme] = None):
+        self.cfg = cfg
+        self.env = env or DistEnv()
+        self.timer = PhaseTimer()
+        self._setup_scheme(scheme)
+        self._setup_data(source)
+        self._setup_buffers()
+
+    # ------------------------------------------------------------------------------ setup
+    def _setup_scheme(self, scheme: Optional[Scheme]):
+        cfg, env = self.cfg, self.env
+        W = cfg.n_workers
+        if W < 1:
+            raise SchemeError("n_procs must be >= 2 (one master + at least one worker)")
+        self.key = scheme_key(cfg.is_coded, cfg.partitions, cfg.coded_ver)
+        if scheme is None:
+            rng = np.random.RandomState(cfg.seed) if cfg.seed is not None else None
+            B = None
+            if env.is_master or env.world == 1:
+                scheme = make_scheme(self.key, W, cfg.n_stragglers, cfg.n_rows, cfg.num_collect, cfg.partitions,
+                                     cfg.allow_uneven_groups, rng)
+                B = scheme.B
+            B = env.broadcast_object(B, 0) if env.world > 1 else B
+            if not env.is_master:
+                scheme = make_scheme(self.key, W, cfg.n_stragglers, cfg.n_rows, cfg.num_collect, cfg.partitions,
+                                     cfg.allow_uneven_groups, None, B)
+        self.scheme = scheme
+        if cfg.loss == "auto":
+            self.loss = LEAST_SQUARES if (cfg.dataset == "kc_house_data" and scheme.has_linear) else LOGISTIC
+        else:
+            self.loss = LEAST_SQUARES if cfg.loss == "least_squares" else LOGISTIC
+        self.rule_kind, self.rule_k = scheme.rule()
+        self.update = UpdateRule("AGD" if scheme.fixed_agd else cfg.update_rule, cfg.alpha_value, cfg.n_rows,
+                                 scheme.grad_scale())
+        self.drain = scheme.drain if cfg.drain is None else cfg.drain == "all"
+        inject = cfg.add_delay == 1 and (scheme.has_delay or cfg.force_delay)
+        mode = "none"
+        if inject:
+            mode = cfg.delay_mode if cfg.delay_mode in ("exp", "fixed") else "none"
+        self.delay = DelayModel(W, mode, cfg.delay_mean, [w - 1 for w in cfg.fixed_stragglers], cfg.fixed_sleep,
+                                [w - 1 for w in cfg.kill_workers])
+        # placement
+        rows = scheme.rows_per_partition
+        cost = [0.0] * W
+        for m in scheme.messages:
+            cost[m.worker] += rows * len(m.segments)
+        self.owner = place_workers(cost, env.world)
+        self.by_rank = workers_by_rank(self.owner, env.world)
+        self.msg_index = {(m.worker, m.part): j for j, m in enumerate(scheme.messages)}
+        self.local_msgs = [m for m in scheme.messages if self.owner[m.worker] == env.rank]
+        self.remote_msgs = {r: [m for m in scheme.messages if self.owner[m.worker] == r]
+                            for r in range(1, env.world)} if env.is_master else {}
+
+    def _setup_data(self, source: Optional[DataSource]):
+        cfg, sch = self.cfg, self.scheme
+        self.prec = get_precision(cfg.precision)
+        if source is None:
+            if cfg.data == "synthetic":
+                source = SyntheticSource(cfg.n_rows, cfg.n_cols, sch.n_partition_files, cfg.data_seed)
+            else:
+                data_dir = dio.dataset_dir(cfg.input_dir, cfg.is_real, cfg.dataset, cfg.n_rows, cfg.n_cols)
+                data_dir = data_dir + sch.data_subdir()
+                source = FileSource(data_dir, cfg.is_real, sch.rows_per_partition, cfg.n_cols)
+        self.source = source
+        self.d = cfg.n_cols
+        self.ld = self.prec.ld(self.d)
+        dev = self.env.device
+        needed = sorted({p for m in self.local_msgs for p, _ in m.segments})
+        t0 = time.perf_counter()
+        parts = {p: source.partition(p, self.prec, dev) for p in needed}
+        self.load_seconds = time.perf_counter() - t0
+        segs = [m.segments for m in self.local_msgs]
+        if source.is_sparse:
+            self.plan = SparseGradPlan(segs, parts, self.prec, self.loss, self.d, device=dev)
+        else:
+            kw = {"target_tasks": cfg.tasks} if cfg.tasks else {}
+            self.plan = DenseGradPlan(segs, parts, self.prec, self.loss, self.d, **kw)
+        self._parts = parts
+
+    def _setup_buffers(self):
+        cfg, env = self.cfg, self.env
+        R, ld, acc, dev = cfg.num_itrs, self.ld, self.prec.acc, env.device
+        es = torch.tensor([], dtype=acc).element_size()
+        n_loc = len(self.local_msgs)
+        n_rem = sum(len(v) for v in self.remote_msgs.values())
+        per_round = max(1, (n_loc + n_rem) * ld * es)
+        self.K = int(max(2, min(R, (1 << 30) // per_round)))
+        self.G = torch.zeros((self.K, max(1, n_loc), ld), dtype=acc, device=dev)
+        if env.is_master:
+            self.rem_slot = {}
+            j = 0
+            for r in sorted(self.remote_msgs):
+                for m in self.remote_msgs[r]:
+                    self.rem_slot[(m.worker, m.part)] = j
+                    j += 1
+            self.Rbuf = torch.zeros((self.K, max(1, n_rem), ld), dtype=acc, device=dev)
+            self.beta = torch.zeros(ld, dtype=torch.float64, device=dev)
+            self.u = torch.zeros(ld, dtype=torch.float64, device=dev)
+            self.hist = torch.zeros((R, ld), dtype=torch.float64, device=dev)
+            self.beta_in = torch.zeros((R + 1, ld), dtype=acc, device=dev)
+            self.loc_index = {(m.worker, m.part): j for j, m in enumerate(self.local_msgs)}
+        else:
+            self.bbuf = torch.zeros((2, ld), dtype=acc, device=dev)
+        if env.gpu:
+            self.cs = torch.cuda.current_stream(dev)
+            self.ps = {r: torch.cuda.Stream(dev) for r in (range(1, env.world) if env.is_master else [0])}
+            self.loc_ev = [torch.cuda.Event() for _ in range(self.K)]
+            if env.is_master:
+                self.rem_ev = [[torch.cuda.Event() for _ in range(max(1, n_rem))] for _ in range(self.K)]
+                self.beta_ev = torch.cuda.Event()
+                self.upd_ev = torch.cuda.Event()
+            else:
+                self.bev = torch.cuda.Event()
+                self.gev = torch.cuda.Event()
+                self.send_done = [None] * self.K
+        self._cpu_sends: List[List] = [[] for _ in range(self.K)]
+
+    # --------------------------------------------------------------------------- helpers
+    def _init_beta(self):
+        """beta_0: randn (naive/replication/approx) or zeros (ref §2.2 'Per-scheme beta init')."""
+        d = self.d
+        if self.scheme.init_zero:
+            b0 = np.zeros(d)
+        elif self.cfg.seed is not None:
+            b0 = np.random.RandomState(self.cfg.seed + 1).randn(d)
+        else:
+            b0 = np.random.randn(d)
+        self.beta.zero_()
+        self.beta[:d] = torch.from_numpy(b0).to(self.beta.device)
+        self.u.zero_()
+        self.beta_in[0].zero_()
+        self.beta_in[0, :d] = self.beta[:d].to(self.beta_in.dtype)
+        self.beta0 = b0
+
+    def _sync(self):
+        if self.env.gpu:
+            torch.cuda.synchronize(self.env.device)
+
+    def warmup(self):
+        """Discarded warm-up gradient (ref src/naive.py:39-44); also loads the kernels."""
+        beta = torch.zeros(self.ld, dtype=self.prec.acc, device=self.env.device)
+        if self.local_msgs:
+            self.plan.run(beta, self.G[0])
+        self._sync()
+
+    # ------------------------------------------------------------------------------ run
+    def run(self, timed_start: Optional[int] = None, log=None) -> Optional[TrainResult]:
+        """Train for cfg.num_itrs rounds; returns the master's TrainResult (None on workers).
+
+        timed_start: if set, all ranks synchronise (device sync + barrier) before that round
+        and after the last one, and the result carries the timed wall-clock (bench.py).
+        """
+        log = log or report.log
+        cfg, env = self.cfg, self.env
+        self.warmup()
+        if env.is_master:
+            self._init_beta()
+            for line in self.scheme.setup_lines():
+                if cfg.verbose:
+                    log(line)
+        env.barrier()
+        if env.is_master:
+            res = self._master_loop(timed_start, log)
+        else:
+            res = self._worker_loop(timed_start)
+        return res
+
+    def _timed_fence(self):
+        self._sync()
+        self.env.barrier()
+        return time.perf_counter()
+
+    def _master_loop(self, timed_start, log) -> TrainResult:
+        cfg, env, sch = self.cfg, self.env, self.scheme
+        R, W, K = cfg.num_itrs, cfg.n_workers, self.K
+        eta = cfg.eta()
+        col = ArrivalCollector(W, sch.group_of, sch.n_groups, env.gpu)
+        timeset = np.zeros(R)
+        loop_time = np.zeros(R)
+        worker_timeset = np.zeros((R, W))
+        arrivals_log = []
+        timeouts = 0
+        t_timed0 = t_timed1 = None
+        if cfg.verbose:
+            log(sch.banner(cfg.add_delay))
+        orig_start = time.perf_counter()
+        for i in range(R):
+            if timed_start is not None and i == timed_start:
+                t_timed0 = self._timed_fence()
+            if cfg.verbose and i % 10 == 0:
+                log(report.iteration_tick(i))
+            slot = i % K
+            if i >= K:
+                col.drain(i - K)  # ring slot reuse: round i-K fully received
+            t_start = col.now()
+            col.begin_round(i, t_start, self.rule_kind, self.rule_k)
+            delays = self.delay.delays(i)
+            with self.timer.phase("send_beta"):
+                self._send_beta(i)
+            with self.timer.phase("local_grad"):
+                if self.local_msgs:
+                    self.plan.run(self.beta_in[i], self.G[slot])
+                    if env.gpu:
+                        ev = self.loc_ev[slot]
+                        ev.record(self.cs)
+                        for m in self.local_msgs:
+                            col.add_event(m.worker, m.part, i, ev, delays[m.worker])
+                    else:
+                        for m in self.local_msgs:
+                            col.add_work(m.worker, m.part, i, None, delays[m.worker])
+            with self.timer.phase("post_recv"):
+                self._post_recvs(i, slot, col, delays)
+            with self.timer.phase("wait_k"):
+                arrivals, ok = col.wait(cfg.round_timeout)
+            if not ok:
+                timeouts += 1
+            with self.timer.phase("decode_update"):
+                used = sch.decode(arrivals)
+                msgs, coefs = [], []
+                for (w, part), c in sorted(used.items()):
+                    key = (w, part)
+                    if key in self.loc_index:
+                        msgs.append(self.G[slot, self.loc_index[key]])
+                    else:
+                        j = self.rem_slot[key]
+                        if env.gpu:
+                            self.cs.wait_event(self.rem_ev[slot][j])
+                        msgs.append(self.Rbuf[slot, j])
+                    coefs.append(c)
+                decay, gm, l2, theta, code = self.update.coeffs(i, float(eta[i]))
+                combine_update(msgs, coefs, self.beta, self.u, self.d, decay, gm, l2, theta, code,
+                               hist=self.hist[i], beta_w=self.beta_in[i + 1])
+                if env.gpu:
+                    self.upd_ev.record(self.cs)
+                    self.upd_ev.synchronize()
+            timeset[i] = col.now() - t_start
+            worker_timeset[i] = sch.worker_times(arrivals)
+            arrivals_log.append([(a.worker, a.part, a.t_rel) for a in arrivals])
+            if self.drain:
+                with self.timer.phase("drain"):
+                    col.drain(i, cfg.round_timeout)
+            loop_time[i] = col.now() - t_start
+            if cfg.checkpoint_every and (i + 1) % cfg.checkpoint_every == 0:
+                self._checkpoint(i + 1, timeset, worker_timeset)
+        col.drain(R - 1, max(cfg.round_timeout, 60.0))
+        if timed_start is not None:
+            t_timed1 = self._timed_fence()
+        self._sync()
+        env.barrier()
+        total = time.perf_counter() - orig_start
+        res = TrainResult(self.key, self.hist[:, : self.d].double().cpu().numpy(), timeset, worker_timeset, loop_time,
+                          total, timeouts=timeouts, phases=self.timer.summary(), arrivals=arrivals_log)
+        if t_timed0 is not None:
+            res.timed_seconds = t_timed1 - t_timed0
+            res.timed_rounds = R - timed_start
+        return res
+
+    def _send_beta(self, i: int):
+        env = self.env
+        if env.world == 1:
+            return
+        if env.gpu:
+            self.beta_ev.record(self.cs)
+            for r in range(1, env.world):
+                s = self.ps[r]
+                s.wait_event(self.beta_ev)
+                with torch.cuda.stream(s):
+                    dist.isend(self.beta_in[i], r)
+        else:
+            for r in range(1, env.world):
+                self._cpu_sends[i % self.K].append(dist.isend(self.beta_in[i], r, tag=_tag_beta(i)))
+
+    def _post_recvs(self, i: int, slot: int, col: ArrivalCollector, delays):
+        env = self.env
+        for r in sorted(self.remote_msgs):
+            msgs = self.remote_msgs[r]
+            if env.gpu:
+                s = self.ps[r]
+                with torch.cuda.stream(s):
+                    for jj, m in enumerate(msgs):
+                        j = self.rem_slot[(m.worker, m.part)]
+                        w = dist.irecv(self.Rbuf[slot, j], r)
+                        w.wait()
+                        ev = self.rem_ev[slot][j]
+                        ev.record(s)
+                        col.add_event(m.worker, m.part, i, ev, delays[m.worker])
+            else:
+                for jj, m in enumerate(msgs):
+                    j = self.rem_slot[(m.worker, m.part)]
+                    w = dist.irecv(self.Rbuf[slot, j], r, tag=_tag_msg(i, jj))
+                    col.add_work(m.worker, m.part, i, w, delays[m.worker])
+
+    def _worker_loop(self, timed_start) -> None:
+        cfg, env = self.cfg, self.env
+        R, K = cfg.num_itrs, self.K
+        n = len(self.local_msgs)
+        for i in range(R):
+            if timed_start is not None and i == timed_start:
+                self._timed_fence()
+            slot, bs = i % K, i % 2
+            if env.gpu:
+                with torch.cuda.stream(self.ps[0]):
+                    w = dist.irecv(self.bbuf[bs], 0)
+                    w.wait()
+                    self.bev.record(self.ps[0])
+                self.cs.wait_event(self.bev)
+                if self.send_done[slot] is not None:
+                    self.cs.wait_event(self.send_done[slot])
+                if n:
+                    self.plan.run(self.bbuf[bs], self.G[slot])
+                self.gev.record(self.cs)
+                s = self.ps[0]
+                s.wait_event(self.gev)
+                with torch.cuda.stream(s):
+                    works = [dist.isend(self.G[slot, j], 0) for j in range(n)]
+                    for w in works:
+                        w.wait()
+                    ev = self.send_done[slot] or torch.cuda.Event()
+                    ev.record(s)
+                    self.send_done[slot] = ev
+            else:
+                for w in self._cpu_sends[slot]:
+                    w.wait()
+                self._cpu_sends[slot] = []
+                dist.irecv(self.bbuf[bs], 0, tag=_tag_beta(i)).wait()
+                if n:
+                    self.plan.run(self.bbuf[bs], self.G[slot])
+                self._cpu_sends[slot] = [dist.isend(self.G[slot, j], 0, tag=_tag_msg(i, j)) for j in range(n)]
+        for lst in self._cpu_sends:
+            for w in lst:
+                w.wait()
+        if timed_start is not None:
+            self._timed_fence()
+        self._sync()
+        env.barrier()
+        return None
+
+    # ------------------------------------------------------------------- checkpointing
+    def _checkpoint(self, next_round: int, timeset, worker_timeset):
+        path = self.cfg.checkpoint_path or os.path.join(self.cfg.input_dir, "checkpoint.pt")
+        state = {"next_round": next_round, "beta": self.beta.cpu(), "u": self.u.cpu(),
+                 "hist": self.hist[:next_round].cpu(), "timeset": torch.from_numpy(timeset[:next_round].copy()),
+                 "worker_timeset": torch.from_numpy(worker_timeset[:next_round].copy()), "scheme": self.key}
+        tmp = path + ".tmp"
+        torch.save(state, tmp)
+        os.replace(tmp, path)

@@ -1,0 +1,104 @@
+"""Post-hoc evaluation of every stored beta (K9-K11; ref src/naive.py:186-198).
+
+Dense data: the MFMA GEMM P = X B^T with the loss reduction fused in its epilogue
+(csrc/kernels/eval.hip), streamed partition by partition so the training set never
+has to be resident at once.  Test predictions are materialised for the ROC AUC, which
+is a rank statistic computed on the device with a sort per round (ties count 1/2, i.e.
+exactly sklearn's trapezoidal roc_curve + auc).
+Sparse data: torch CSR x dense products on the device (library SpMM), same epilogues.
+"""
+from __future__ import annotations
+
+from typing import Iterable, Tuple
+
+import numpy as np
+import torch
+
+from .._ext import native
+from ..models.losses import LOGISTIC
+
+
+def _loss_torch(kind: int, y: torch.Tensor, P: torch.Tensor) -> torch.Tensor:
+    y = y.double()[:, None]
+    P = P.double()
+    if kind == LOGISTIC:
+        m = -y * P
+        return (torch.clamp(m, min=0) + torch.log1p(torch.exp(-m.abs()))).sum(0)
+    e = y - P
+    return (e * e).sum(0)
+
+
+def _is_sparse(X) -> bool:
+    return not isinstance(X, torch.Tensor) or X.layout != torch.strided
+
+
+def _to_torch_sparse(X, device, dtype):
+    import scipy.sparse as sps
+
+    X = sps.csr_matrix(X)
+    return torch.sparse_csr_tensor(torch.from_numpy(X.indptr.astype(np.int64)),
+                                   torch.from_numpy(X.indices.astype(np.int64)),
+                                   torch.from_numpy(X.data.astype(np.float64)), size=X.shape,
+                                   dtype=dtype, device=device)
+
+
+def predictions(X, B: torch.Tensor, d: int) -> torch.Tensor:
+    """P = X[:, :d] @ B[:, :d]^T  ([n, R], accumulator dtype of X)."""
+    if _is_sparse(X):
+        Xt = _to_torch_sparse(X, B.device, torch.float64)
+        return (Xt @ B[:, :d].double().t().contiguous())
+    n = X.shape[0]
+    acc = torch.float64 if X.dtype == torch.float64 else torch.float32
+    Bc = B.to(acc).contiguous()
+    if X.is_cuda:
+        P = torch.empty((n, B.shape[0]), dtype=acc, device=X.device)
+        junk = torch.zeros(B.shape[0], dtype=torch.float64, device=X.device)
+        yz = torch.zeros(n, dtype=acc, device=X.device)
+        native().eval_gemm_loss(LOGISTIC, X, n, d, yz, Bc, junk, P)
+        return P
+    return X[:, :d].to(acc) @ Bc[:, :d].t()
+
+
+def loss_sums(chunks: Iterable[Tuple[object, torch.Tensor]], B: torch.Tensor, d: int, kind: int) -> Tuple[np.ndarray, int]:
+    """Sum over all chunk rows of the per-row loss for every beta row of B -> ([R], n)."""
+    R = B.shape[0]
+    total = None
+    n = 0
+    for X, y in chunks:
+        if _is_sparse(X):
+            P = predictions(X, B, d)
+            s = _loss_torch(kind, y.to(P.device), P)
+        elif X.is_cuda:
+            acc = torch.float64 if X.dtype == torch.float64 else torch.float32
+            s = torch.zeros(R, dtype=torch.float64, device=X.device)
+            native().eval_gemm_loss(kind, X, X.shape[0], d, y.to(acc).contiguous(), B.to(acc).contiguous(), s, None)
+        else:
+            P = predictions(X, B, d)
+            s = _loss_torch(kind, y, P)
+        total = s if total is None else total + s.to(total.device)
+        n += X.shape[0]
+    if total is None:
+        return np.zeros(R), 0
+    return total.double().cpu().numpy(), n
+
+
+def auc_columns(y: torch.Tensor, P: torch.Tensor) -> np.ndarray:
+    """ROC AUC of every column of P against labels y in {-1, +1} (ties count 1/2)."""
+    y = y.to(P.device)
+    pos = y == 1
+    n_pos = int(pos.sum().item())
+    n_neg = y.numel() - n_pos
+    out = np.full(P.shape[1], np.nan)
+    if n_pos == 0 or n_neg == 0:
+        return out
+    for j in range(P.shape[1]):
+        s = P[:, j].double()
+        order = torch.argsort(s, stable=True)
+        ss = s[order]
+        _, inv, counts = torch.unique_consecutive(ss, return_inverse=True, return_counts=True)
+        ends = counts.cumsum(0).double()
+        avg = (2 * ends - counts.double() + 1) / 2.0  # mean of ranks start+1 .. end
+        ranks = avg[inv]
+        u = ranks[pos[order]].sum().item() - n_pos * (n_pos + 1) / 2.0
+        out[j] = u / (n_pos * n_neg)
+    return out

@@ -1,0 +1,228 @@
+"""Worker-gradient execution plans (device side of K1-K4/K13).
+
+A *plan* is built once per run for all logical workers hosted on one GPU: every
+message (worker, part) is a list of segments (partition, label coefficient).  Each
+round the plan is executed with one launch set:
+
+  dense  -> ``grad_dense`` (fused single pass over X, slab reduction)   csrc/kernels/grad_dense.hip
+            ``grad_dense_twopass`` when d > 2048                          (same file)
+  sparse -> ``grad_sparse`` (CSR row pass + sorted-COO column pass)      csrc/kernels/grad_sparse.hip
+
+On CPU tensors the same plans run a float64/float32 torch implementation of the
+identical math (the test path and the gloo multi-process path); on GPU tensors the
+native kernels are mandatory (:func:`erasurehead_amd._ext.native` raises if absent).
+"""
+from __future__ import annotations
+
+import struct
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .._ext import native
+from ..models.losses import LEAST_SQUARES, LOGISTIC
+from .precision import Precision
+
+_SEG = struct.Struct("<QQdq")  # csrc Segment {const void* X; const void* y; double coef; long long nrows}
+MAX_CPL = 32
+DEFAULT_TASKS = 2048
+MIN_ROWS_PER_TASK = 32
+
+
+def choose_cpl(ld: int, vec: int) -> Optional[int]:
+    """Columns per lane of the fused kernel (64 * cpl >= ld); None -> two-pass path."""
+    for c in (2, 4, 8, 16, 32):
+        if c % vec == 0 and 64 * c >= ld:
+            return c
+    return None
+
+
+def _residual_torch(kind: int, z, y, coef):
+    if kind == LOGISTIC:
+        return -(coef * y) * torch.sigmoid(-(y * z))
+    return -2.0 * coef * (y - z)
+
+
+class DenseGradPlan:
+    """Gradient of every local message over dense partitions.
+
+    partitions: {partition_index: (X [rows, ld] storage dtype, y [rows] acc dtype)}
+    messages:   sequence of (segments) where segments = [(partition_index, coef), ...]
+    """
+
+    def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]],
+                 partitions: Dict[int, Tuple[torch.Tensor, torch.Tensor]], prec: Precision, loss: int, d: int,
+                 target_tasks: int = DEFAULT_TASKS):
+        self.prec = prec
+        self.loss = loss
+        self.d = d
+        self.ld = prec.ld(d)
+        self.messages = [list(m) for m in messages]
+        self.partitions = partitions
+        self.nslots = len(self.messages)
+        any_t = next(iter(partitions.values()))[0] if partitions else torch.empty(0)
+        self.device = any_t.device
+        for p, (X, y) in partitions.items():
+            if X.dim() != 2 or X.shape[1] != self.ld or X.dtype != prec.storage or not X.is_contiguous():
+                raise ValueError(f"partition {p}: X must be contiguous [rows, {self.ld}] {prec.storage}")
+            if y.shape[0] != X.shape[0] or y.dtype != prec.acc:
+                raise ValueError(f"partition {p}: y must be [{X.shape[0]}] {prec.acc}")
+        self.total_rows = sum(partitions[p][0].shape[0] for m in self.messages for p, _ in m)
+        self.cpl = choose_cpl(self.ld, prec.vec)
+        if self.device.type == "cuda":
+            self._build_tables(target_tasks)
+
+    # ---- device tables ----------------------------------------------------------------
+    def _build_tables(self, target_tasks: int):
+        segs = bytearray()
+        tasks: List[Tuple[int, int, int, int]] = []
+        slot_begin = [0]
+        rows_per_task = max(MIN_ROWS_PER_TASK, -(-self.total_rows // max(1, target_tasks)))
+        seg_id = 0
+        for slot, m in enumerate(self.messages):
+            for p, coef in m:
+                X, y = self.partitions[p]
+                n = X.shape[0]
+                segs += _SEG.pack(X.data_ptr(), y.data_ptr(), float(coef), n)
+                for r0 in range(0, n, rows_per_task):
+                    tasks.append((slot, seg_id, r0, min(n, r0 + rows_per_task)))
+                seg_id += 1
+            slot_begin.append(len(tasks))
+        dev = self.device
+        self.segs = torch.frombuffer(bytes(segs) or b"\0" * 32, dtype=torch.uint8).clone().to(dev)
+        self.ntasks = len(tasks)
+        t = np.asarray(tasks, dtype=np.int32).reshape(-1, 4)
+        self.tasks = torch.from_numpy(t).to(dev)
+        self.slot_task_begin = torch.tensor(slot_begin, dtype=torch.int32, device=dev)
+        self.slab = torch.empty((max(1, self.ntasks), self.ld), dtype=self.prec.acc, device=dev)
+        if self.cpl is None:
+            off = np.zeros(max(1, self.ntasks), dtype=np.int64)
+            if self.ntasks:
+                off[1:] = np.cumsum(t[:, 3] - t[:, 2])[:-1]
+            if off.size and off[-1] + (t[-1, 3] - t[-1, 2] if self.ntasks else 0) >= 2 ** 31:
+                raise ValueError("two-pass plan exceeds int32 row offsets")
+            self.task_row_off = torch.from_numpy(off.astype(np.int32)).to(dev)
+            self.rbuf = torch.empty(max(1, int(self.total_rows)), dtype=self.prec.acc, device=dev)
+
+    def out_buffer(self, n: int = 1) -> torch.Tensor:
+        """Message buffer(s) [n, nslots, ld] in the accumulator dtype."""
+        return torch.zeros((n, self.nslots, self.ld), dtype=self.prec.acc, device=self.device)
+
+    # ---- execution -------------------------------------------------------------------
+    def run(self, beta: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
+        """G[slot] = gradient of message slot at beta (beta: [ld] acc dtype)."""
+        if G.shape != (self.nslots, self.ld):
+            raise ValueError(f"G must be [{self.nslots}, {self.ld}]")
+        if self.device.type == "cuda":
+            C = native()
+            if self.cpl is not None:
+                C.grad_dense(self.prec.code, self.loss, self.cpl, self.segs, self.tasks, beta, self.slab,
+                             self.slot_task_begin, G, self.ld)
+            else:
+                C.grad_dense_twopass(self.prec.code, self.loss, self.segs, self.tasks, beta, self.task_row_off,
+                                     self.rbuf, self.slab, self.slot_task_begin, G, self.ld)
+            return G
+        return self._run_torch(beta, G)
+
+    def _run_torch(self, beta, G):
+        acc = self.prec.acc
+        b = beta.to(acc)
+        for slot, m in enumerate(self.messages):
+            g = torch.zeros(self.ld, dtype=acc)
+            for p, coef in m:
+                X, y = self.partitions[p]
+                Xa = X.to(acc)
+                z = Xa @ b
+                r = _residual_torch(self.loss, z, y, torch.tensor(coef, dtype=acc))
+                g += Xa.t() @ r
+            G[slot].copy_(g)
+        return G
+
+    @property
+    def bytes_per_round(self) -> int:
+        """HBM bytes the fused kernel must stream per round (X once)."""
+        es = torch.tensor([], dtype=self.prec.storage).element_size()
+        return int(self.total_rows) * self.ld * es
+
+
+class SparseGradPlan:
+    """Gradient of every local message over CSR partitions (one-hot / pattern-only aware).
+
+    partitions: {partition_index: (scipy.sparse.csr_matrix, y ndarray float64)}
+    """
+
+    def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]], partitions: Dict[int, Tuple[object, np.ndarray]],
+                 prec: Precision, loss: int, d: int, device="cpu"):
+        import scipy.sparse as sps
+
+        if prec.name == "bf16":
+            raise ValueError("sparse data uses fp64 or fp32 values (bf16 has no benefit for one-hot data)")
+        self.prec, self.loss, self.d = prec, loss, d
+        self.ld = prec.ld(d)
+        self.messages = [list(m) for m in messages]
+        self.nslots = len(self.messages)
+        self.device = torch.device(device)
+        blocks, ys, coefs, slots = [], [], [], []
+        for slot, m in enumerate(self.messages):
+            for p, coef in m:
+                A, y = partitions[p]
+                A = sps.csr_matrix(A)
+                if A.shape[1] > d:
+                    raise ValueError("partition has more columns than d")
+                blocks.append(A)
+                ys.append(np.asarray(y, dtype=np.float64))
+                coefs.append(np.full(A.shape[0], float(coef)))
+                slots.append(np.full(A.shape[0], slot, dtype=np.int64))
+        X = sps.vstack(blocks, format="csr") if blocks else sps.csr_matrix((0, d))
+        X = sps.csr_matrix((X.data, X.indices, X.indptr), shape=(X.shape[0], d))
+        X.sort_indices()
+        self.nrows = X.shape[0]
+        self.nnz = X.nnz
+        row_slot = np.concatenate(slots) if slots else np.zeros(0, dtype=np.int64)
+        self.pattern_only = bool(X.nnz == 0 or np.all(X.data == 1.0))
+        # COO sorted by key = slot * ld + col (the CSC twin across all local messages)
+        coo = X.tocoo()
+        keys = row_slot[coo.row] * self.ld + coo.col.astype(np.int64)
+        order = np.argsort(keys, kind="stable")
+        acc = prec.acc
+        npacc = np.float64 if acc == torch.float64 else np.float32
+        dev = self.device
+        self.row_ptr = torch.from_numpy(X.indptr.astype(np.int64)).to(dev)
+        self.col_idx = torch.from_numpy(X.indices.astype(np.int32)).to(dev)
+        self.vals = None if self.pattern_only else torch.from_numpy(X.data.astype(npacc)).to(dev)
+        self.y = torch.from_numpy((np.concatenate(ys) if ys else np.zeros(0)).astype(npacc)).to(dev)
+        self.coef = torch.from_numpy((np.concatenate(coefs) if coefs else np.zeros(0)).astype(npacc)).to(dev)
+        self.keys = torch.from_numpy(keys[order]).to(dev)
+        self.rows = torch.from_numpy(coo.row[order].astype(np.int32)).to(dev)
+        self.cvals = None if self.pattern_only else torch.from_numpy(coo.data[order].astype(npacc)).to(dev)
+        self.rbuf = torch.empty(max(1, self.nrows), dtype=acc, device=dev)
+        self._row_slot = torch.from_numpy(row_slot).to(dev)
+        self._X_cpu = X if dev.type == "cpu" else None
+
+    def out_buffer(self, n: int = 1) -> torch.Tensor:
+        return torch.zeros((n, self.nslots, self.ld), dtype=self.prec.acc, device=self.device)
+
+    def run(self, beta: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
+        if G.shape != (self.nslots, self.ld):
+            raise ValueError(f"G must be [{self.nslots}, {self.ld}]")
+        if self.device.type == "cuda":
+            native().grad_sparse(self.loss, self.row_ptr, self.col_idx, self.vals, self.y, self.coef, beta,
+                                 self.rbuf, self.keys, self.rows, self.cvals, G, self.ld)
+            return G
+        X = self._X_cpu
+        b = beta.detach().cpu().double().numpy()[: self.d]
+        z = X.dot(b)
+        y = self.y.double().numpy()
+        c = self.coef.double().numpy()
+        if self.loss == LOGISTIC:
+            r = -(c * y) * (1.0 / (1.0 + np.exp(np.clip(y * z, -700, 700))))
+        else:
+            r = -2.0 * c * (y - z)
+        G.zero_()
+        rs = self._row_slot.numpy()
+        for slot in range(self.nslots):
+            sel = rs == slot
+            g = X[sel].T.dot(r[sel]) if sel.any() else np.zeros(self.d)
+            G[slot, : self.d] = torch.from_numpy(np.asarray(g).ravel()).to(G.dtype)
+        return G

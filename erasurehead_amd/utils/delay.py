@@ -1,0 +1,73 @@
+"""Straggler / fault injection model.
+
+Reference (ref src/naive.py:141-148, also coded/replication/approximate_coding):
+    if add_delay == 1:
+        np.random.seed(seed=i); artificial_delays = np.random.exponential(0.5, n_workers)
+        time.sleep(artificial_delays[rank-1])          # after compute, before the send
+Every worker seeds with the round index, so all draw the same vector: the pattern is
+deterministic.  ``RandomState(i).exponential`` reproduces that stream exactly.
+
+Extra modes (opt-in): ``fixed`` (the commented variant at ref src/naive.py:143-145: a
+fixed set of workers sleeps ``fixed_sleep``), ``kill`` (workers that never arrive: the
+master's round timeout turns them into erasures instead of hanging).
+The delay is applied as a virtual arrival time by the native collector (see
+csrc/runtime/collector.h) so the GPUs never idle in ``sleep``.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List
+
+import numpy as np
+
+
+@dataclass
+class DelayModel:
+    n_workers: int
+    mode: str = "none"  # none | exp | fixed
+    mean: float = 0.5
+    fixed_workers: List[int] = field(default_factory=list)  # 0-based
+    fixed_sleep: float = 0.5
+    dead: List[int] = field(default_factory=list)  # 0-based
+
+    def delays(self, i: int) -> np.ndarray:
+        """Delay (seconds) of every worker in round i."""
+        W = self.n_workers
+        if self.mode == "exp":
+            d = np.random.RandomState(seed=i).exponential(self.mean, W)
+        elif self.mode == "fixed":
+            d = np.zeros(W)
+            d[list(self.fixed_workers)] = self.fixed_sleep
+        else:
+            d = np.zeros(W)
+        for w in self.dead:
+            d[w] = math.inf
+        return d
+
+
+def delay_floor(n_workers: int, rounds: int, stop_count=None, groups=None, k=None, mean=0.5) -> float:
+    """Sum over rounds of the injected delay the master must wait for.
+
+    stop_count: wait for the `stop_count`-th smallest delay (naive: W, cyclic: W-s).
+    groups/k:   FRC/AGC rule — stop at k arrivals or when every group is covered.
+    """
+    tot = 0.0
+    for i in range(rounds):
+        d = np.random.RandomState(seed=i).exponential(mean, n_workers)
+        order = np.argsort(d, kind="stable")
+        if groups is None:
+            tot += float(np.sort(d)[stop_count - 1])
+            continue
+        covered = set()
+        cnt = 0
+        t = 0.0
+        n_groups = len(set(groups))
+        for w in order:
+            t = d[w]
+            cnt += 1
+            covered.add(groups[w])
+            if cnt >= k or len(covered) >= n_groups:
+                break
+        tot += float(t)
+    return tot

@@ -1,0 +1,160 @@
+"""Numerics of the gfx950 HIP kernels against fp64 NumPy/PyTorch references (GPU only)."""
+import numpy as np
+import pytest
+import scipy.sparse as sps
+import torch
+
+from erasurehead_amd.models.losses import LEAST_SQUARES, LOGISTIC, least_squares_grad, logistic_grad, logistic_loss, mse
+from erasurehead_amd.ops import DenseGradPlan, SparseGradPlan, auc_columns, combine_update, get_precision, loss_sums, predictions
+from erasurehead_amd.models.losses import roc_auc, UpdateRule
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _parts(rng, sizes, d, prec):
+    parts = {}
+    host = {}
+    for p, n in enumerate(sizes):
+        X = rng.randn(n, d) * 0.3
+        y = rng.choice([-1.0, 1.0], n)
+        Xp = torch.zeros((n, prec.ld(d)), dtype=torch.float64)
+        Xp[:, :d] = torch.from_numpy(X)
+        Xs = Xp.to(prec.storage)
+        host[p] = (Xs[:, :d].double().numpy(), y)  # oracle sees the stored (rounded) values
+        parts[p] = (Xs.to(DEV).contiguous(), torch.from_numpy(y).to(prec.acc).to(DEV))
+    return parts, host
+
+
+@pytest.mark.parametrize("prec_name,tol", [("fp64", 1e-11), ("fp32", 2e-4), ("bf16", 2e-4)])
+@pytest.mark.parametrize("d", [1, 37, 1000, 2048, 2500])
+@pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
+def test_dense_grad(prec_name, tol, d, loss, native):
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(d + loss)
+    parts, host = _parts(rng, [257, 64, 1], d, prec)
+    msgs = [[(0, 1.0), (1, -0.7)], [(2, 2.5)], [(1, 1.0), (0, 0.3), (2, 1.0)]]
+    plan = DenseGradPlan(msgs, parts, prec, loss, d, target_tasks=7)
+    beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
+    b = rng.randn(d) * 0.5
+    beta[:d] = torch.from_numpy(b).to(prec.acc)
+    bh = beta[:d].double().cpu().numpy()
+    G = plan.out_buffer()[0]
+    plan.run(beta, G)
+    torch.cuda.synchronize()
+    f = logistic_grad if loss == LOGISTIC else least_squares_grad
+    for s, m in enumerate(msgs):
+        ref = sum(f(host[p][0], host[p][1], bh, c) for p, c in m)
+        got = G[s, :d].double().cpu().numpy()
+        err = np.max(np.abs(got - ref)) / max(1e-12, np.max(np.abs(ref)))
+        assert err < tol, (s, err)
+        assert torch.all(G[s, d:] == 0)
+
+
+def test_dense_grad_many_tasks_deterministic(native):
+    prec = get_precision("fp64")
+    rng = np.random.RandomState(5)
+    parts, host = _parts(rng, [5000, 3001], 300, prec)
+    plan = DenseGradPlan([[(0, 1.0), (1, 1.0)]], parts, prec, LOGISTIC, 300, target_tasks=100)
+    beta = torch.randn(plan.ld, dtype=torch.float64, device=DEV) * 0.1
+    G1 = plan.out_buffer()[0]
+    G2 = plan.out_buffer()[0]
+    plan.run(beta, G1)
+    plan.run(beta, G2)
+    torch.cuda.synchronize()
+    assert torch.equal(G1, G2)  # slab reduction is order-fixed: bitwise reproducible
+
+
+@pytest.mark.parametrize("prec_name,tol", [("fp64", 1e-11), ("fp32", 1e-4)])
+@pytest.mark.parametrize("pattern_only", [True, False])
+def test_sparse_grad(prec_name, tol, pattern_only, native):
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(3)
+    d = 700
+    parts = {}
+    for p in range(3):
+        n = 400 + 37 * p
+        cols = np.stack([rng.choice(d, 5, replace=False) for _ in range(n)])
+        vals = np.ones(cols.size) if pattern_only else rng.randn(cols.size)
+        X = sps.csr_matrix((vals, cols.ravel(), np.arange(0, cols.size + 1, 5)), shape=(n, d))
+        parts[p] = (X, rng.choice([-1.0, 1.0], n))
+    msgs = [[(0, 1.0), (1, 0.5)], [(2, -1.5)], [(0, 1.0)]]
+    for loss in (LOGISTIC, LEAST_SQUARES):
+        plan = SparseGradPlan(msgs, parts, prec, loss, d, device=DEV)
+        assert plan.pattern_only == pattern_only
+        b = rng.randn(d) * 0.2
+        beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
+        beta[:d] = torch.from_numpy(b).to(prec.acc)
+        bh = beta[:d].double().cpu().numpy()
+        G = plan.out_buffer()[0]
+        plan.run(beta, G)
+        torch.cuda.synchronize()
+        f = logistic_grad if loss == LOGISTIC else least_squares_grad
+        for s, m in enumerate(msgs):
+            ref = sum(f(parts[p][0], parts[p][1], bh, c) for p, c in m)
+            got = G[s, :d].double().cpu().numpy()
+            err = np.max(np.abs(got - ref)) / max(1e-12, np.max(np.abs(ref)))
+            assert err < tol, (loss, s, err)
+
+
+@pytest.mark.parametrize("rule", ["GD", "AGD"])
+@pytest.mark.parametrize("msg_dtype", [torch.float64, torch.float32])
+def test_combine_update(rule, msg_dtype, native):
+    rng = np.random.RandomState(1)
+    d, ld = 1001, 1002
+    msgs_h = [rng.randn(ld) for _ in range(5)]
+    msgs = [torch.from_numpy(m).to(msg_dtype).to(DEV) for m in msgs_h]
+    coefs = [1.0, -0.5, 0.0, 2.0, 0.25]
+    b0 = rng.randn(ld)
+    b0[d:] = 0
+    u0 = rng.randn(ld)
+    u0[d:] = 0
+    beta = torch.from_numpy(b0.copy()).to(DEV)
+    u = torch.from_numpy(u0.copy()).to(DEV)
+    hist = torch.zeros(ld, dtype=torch.float64, device=DEV)
+    bw = torch.full((ld,), 7.0, dtype=torch.float32, device=DEV)
+    g_out = torch.zeros(ld, dtype=torch.float64, device=DEV)
+    up = UpdateRule(rule, 1e-3, 5000)
+    i = 3
+    decay, gm, l2, theta, code = up.coeffs(i, 10.0)
+    combine_update(msgs, coefs, beta, u, d, decay, gm, l2, theta, code, hist=hist, beta_w=bw, g_out=g_out)
+    torch.cuda.synchronize()
+    g = sum(c * torch.from_numpy(m).to(msg_dtype).double().numpy() for c, m in zip(coefs, msgs_h))[:d]
+    bref, uref = b0[:d].copy(), u0[:d].copy()
+    up.apply(i, 10.0, bref, uref, g)
+    np.testing.assert_allclose(g_out[:d].cpu().numpy(), g, rtol=1e-13, atol=1e-12)
+    np.testing.assert_allclose(beta[:d].cpu().numpy(), bref, rtol=1e-13, atol=1e-13)
+    np.testing.assert_allclose(hist[:d].cpu().numpy(), bref, rtol=1e-13, atol=1e-13)
+    if rule == "AGD":
+        np.testing.assert_allclose(u[:d].cpu().numpy(), uref, rtol=1e-12, atol=1e-12)
+    assert torch.all(bw[d:] == 0)
+    np.testing.assert_allclose(bw[:d].cpu().double().numpy(), bref.astype(np.float32), rtol=1e-6)
+
+
+@pytest.mark.parametrize("prec_name,tol", [("fp64", 1e-11), ("fp32", 2e-5), ("bf16", 2e-5)])
+@pytest.mark.parametrize("R", [1, 16, 100, 130])
+def test_eval_gemm_loss(prec_name, tol, R, native):
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(R)
+    n, d = 333, 257
+    X = rng.randn(n, d) * 0.2
+    y = rng.choice([-1.0, 1.0], n)
+    Xp = torch.zeros((n, prec.ld(d)), dtype=torch.float64)
+    Xp[:, :d] = torch.from_numpy(X)
+    Xs = Xp.to(prec.storage)
+    Xh = Xs[:, :d].double().numpy()
+    B = torch.zeros((R, prec.ld(d)), dtype=torch.float64)
+    B[:, :d] = torch.from_numpy(rng.randn(R, d) * 0.3)
+    Bh = B[:, :d].to(prec.acc).double().numpy()
+    Xd = Xs.to(DEV)
+    Bd = B.to(DEV)
+    for kind in (LOGISTIC, LEAST_SQUARES):
+        sums, nn = loss_sums([(Xd, torch.from_numpy(y).to(DEV))], Bd, d, kind)
+        P = Xh @ Bh.T
+        ref = np.array([logistic_loss(y, P[:, j], 1) if kind == LOGISTIC else mse(y, P[:, j]) * n for j in range(R)])
+        assert nn == n
+        np.testing.assert_allclose(sums, ref, rtol=tol * 10, atol=tol)
+    Pd = predictions(Xd, Bd, d).double().cpu().numpy()
+    np.testing.assert_allclose(Pd, Xh @ Bh.T, rtol=tol * 10, atol=tol)
+    auc = auc_columns(torch.from_numpy(y).to(DEV), torch.from_numpy(Xh @ Bh.T).to(DEV))
+    np.testing.assert_allclose(auc, [roc_auc(y, (Xh @ Bh.T)[:, j]) for j in range(R)], rtol=1e-12)

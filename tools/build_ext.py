@@ -1,0 +1,105 @@
+"""In-tree build of the native extension ``erasurehead_amd/_C*.so`` for gfx950.
+
+No hipify, no torch JIT cache: HIP kernels are compiled with ``hipcc --offload-arch=gfx950``
+(device + host code in one fat object), the host-only runtime and the pybind/torch bindings
+with ``g++`` against the HIP runtime headers, then everything is linked with ``hipcc -shared``.
+Objects are cached under ``build/`` and rebuilt only when a source or header changed.
+
+Usage:  python tools/build_ext.py [--force] [-j N]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build", "objs")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    inc = ce.include_paths(device_type="cuda")
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def target_path() -> str:
+    return os.path.join(ROOT, "erasurehead_amd", "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+
+
+def _stale(obj: str, src: str, headers) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(p) > t for p in [src, *headers])
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
+    inc, torchlib, abi = _torch_paths()
+    pyinc = sysconfig.get_paths()["include"]
+    os.makedirs(BUILD, exist_ok=True)
+    headers = _headers()
+    common = ["-O3", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{CSRC}"]
+    hip_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    cpp_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "bindings.cpp")]
+    jobs_list = []
+    for s in hip_srcs:
+        o = os.path.join(BUILD, os.path.basename(s) + ".o")
+        cmd = [os.path.join(ROCM, "bin", "hipcc"), "-c", s, "-o", o, f"--offload-arch={ARCH}",
+               "-munsafe-fp-atomics", *common]
+        jobs_list.append((s, o, cmd))
+    for s in cpp_srcs:
+        o = os.path.join(BUILD, os.path.basename(s) + ".o")
+        cmd = ["g++", "-c", s, "-o", o, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+               f"-I{ROCM}/include", *[f"-I{p}" for p in inc], f"-I{pyinc}",
+               "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-w"]
+        jobs_list.append((s, o, cmd))
+    todo = [(s, o, c) for (s, o, c) in jobs_list if force or _stale(o, s, headers)]
+    n = jobs or min(len(todo), max(1, (os.cpu_count() or 4)), 8) or 1
+    with cf.ThreadPoolExecutor(max_workers=n) as ex:
+        futs = {ex.submit(_run, c): s for (s, o, c) in todo}
+        for f in cf.as_completed(futs):
+            out = f.result()
+            if verbose:
+                print("compiled", os.path.relpath(futs[f], ROOT), out, flush=True)
+    out = target_path()
+    objs = [o for (_, o, _) in jobs_list]
+    if force or todo or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
+        link = [os.path.join(ROCM, "bin", "hipcc"), "-shared", "-fPIC", "-o", out + ".tmp", *objs,
+                f"--offload-arch={ARCH}", f"-L{torchlib}", f"-Wl,-rpath,{torchlib}",
+                "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64"]
+        _run(link)
+        os.replace(out + ".tmp", out)
+        if verbose:
+            print("linked", os.path.relpath(out, ROOT), flush=True)
+    return out
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=0)
+    a = ap.parse_args()
+    print(build(force=a.force, jobs=a.j, verbose=True))
