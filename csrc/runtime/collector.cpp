@@ -89,15 +89,24 @@ void Collector::mark_seen(int id, double t) {
 }
 
 void Collector::poll_events(double t) {
+  // Query every distinct event ONCE per sweep: probes that share an event (all local
+  // messages behind one gradient launch) must become visible together, otherwise an
+  // event completing mid-sweep would order simultaneous messages by sweep position.
+  std::vector<std::pair<hipEvent_t, bool>> done;
   for (int id : live_) {
     Probe& p = probes_[id];
     if (p.seen || p.host) continue;
-    const hipError_t e = hipEventQuery(p.ev);
-    if (e == hipSuccess) {
-      mark_seen(id, t);
-    } else if (e != hipErrorNotReady) {
-      throw std::runtime_error(std::string("Collector: hipEventQuery failed: ") + hipGetErrorString(e));
+    int hit = -1;
+    for (int k = 0; k < static_cast<int>(done.size()); ++k)
+      if (done[k].first == p.ev) { hit = k; break; }
+    if (hit < 0) {
+      const hipError_t e = hipEventQuery(p.ev);
+      if (e != hipSuccess && e != hipErrorNotReady)
+        throw std::runtime_error(std::string("Collector: hipEventQuery failed: ") + hipGetErrorString(e));
+      done.emplace_back(p.ev, e == hipSuccess);
+      hit = static_cast<int>(done.size()) - 1;
     }
+    if (done[hit].second) mark_seen(id, t);
   }
 }
 

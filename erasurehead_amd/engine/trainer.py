@@ -80,7 +80,11 @@ class Trainer:
     def __init__(self, cfg: RunConfig, env: Optional[DistEnv] = None, source: Optional[DataSource] = None,
                  scheme: Optional[Scheme] = None):
         self.cfg = cfg
-        self.env = env or DistEnv()
+        if env is None:
+            from ..parallel.dist import init_distributed
+
+            env = init_distributed("auto")
+        self.env = env
         self.timer = PhaseTimer()
         self._setup_scheme(scheme)
         self._setup_data(source)
@@ -323,6 +327,7 @@ class Trainer:
             if cfg.checkpoint_every and (i + 1) % cfg.checkpoint_every == 0:
                 self._checkpoint(i + 1, timeset, worker_timeset)
         col.drain(R - 1, max(cfg.round_timeout, 60.0))
+        col.close()
         if timed_start is not None:
             t_timed1 = self._timed_fence()
         self._sync()
@@ -368,7 +373,7 @@ class Trainer:
                 for jj, m in enumerate(msgs):
                     j = self.rem_slot[(m.worker, m.part)]
                     w = dist.irecv(self.Rbuf[slot, j], r, tag=_tag_msg(i, jj))
-                    col.add_work(m.worker, m.part, i, w, delays[m.worker])
+                    col.add_work(m.worker, m.part, i, w, delays[m.worker], src=r)
 
     def _worker_loop(self, timed_start) -> None:
         cfg, env = self.cfg, self.env

@@ -3,13 +3,17 @@
 GPU mode: probes are HIP events (torch.cuda.Event) recorded behind an RCCL receive or
 behind the local gradient kernel; the poll loop, virtual straggler delays and stop rule
 all run in C++ with the GIL released (``wait``/``drain``).
-Host mode (CPU tensors, gloo): probes are completed from Python when the gloo ``Work``
-reports completion (or immediately for synchronous CPU compute) and the same native
-state machine decides arrival order and the stop.
+Host mode (CPU tensors, gloo): gloo's p2p ``Work`` objects only complete inside
+``wait()`` (``is_completed()`` never flips), so one waiter thread per source rank waits
+on that rank's receives in FIFO order and reports the completion time; local CPU
+compute completes immediately.  The same native state machine decides arrival order
+and the stop.
 """
 from __future__ import annotations
 
 import math
+import queue
+import threading
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -24,8 +28,26 @@ class ArrivalCollector:
         self.c = C.Collector(int(n_workers), [int(g) for g in group_of], int(n_groups))
         self.gpu = gpu
         self._keep: Dict[int, object] = {}  # probe -> event (kept alive until arrival)
-        self._host: Dict[int, Tuple[object, int]] = {}  # probe -> (work or None, round)
+        self._pending_host = 0
+        self._done: "queue.Queue[Tuple[int, float]]" = queue.Queue()
+        self._waiters: Dict[int, "queue.Queue"] = {}
         self.round = -1
+
+    def _waiter(self, q: "queue.Queue") -> None:
+        while True:
+            item = q.get()
+            if item is None:
+                return
+            pid, work = item
+            try:
+                work.wait()
+            finally:
+                self._done.put((pid, self.now()))
+
+    def close(self) -> None:
+        for q in self._waiters.values():
+            q.put(None)
+        self._waiters.clear()
 
     @staticmethod
     def now() -> float:
@@ -40,26 +62,28 @@ class ArrivalCollector:
         self._keep[pid] = event
         return pid
 
-    def add_work(self, worker: int, part: int, i: int, work, delay: float) -> int:
-        """Host probe completed when ``work.is_completed()`` (None = already complete now)."""
+    def add_work(self, worker: int, part: int, i: int, work, delay: float, src: int = 0) -> int:
+        """Host probe completed when ``work`` finishes (None = already complete now)."""
         pid = self.c.add_host_probe(int(worker), int(part), int(i), float(delay))
         if work is None:
             self.c.mark_seen(pid, self.now())
         else:
-            self._host[pid] = (work, i)
+            q = self._waiters.get(src)
+            if q is None:
+                q = self._waiters[src] = queue.Queue()
+                threading.Thread(target=self._waiter, args=(q,), daemon=True).start()
+            self._pending_host += 1
+            q.put((pid, work))
         return pid
 
     def _poll_host(self) -> None:
-        if not self._host:
-            return
-        done = []
-        t = self.now()
-        for pid, (w, _) in self._host.items():
-            if w.is_completed():
-                self.c.mark_seen(pid, t)
-                done.append(pid)
-        for pid in done:
-            del self._host[pid]
+        while True:
+            try:
+                pid, t = self._done.get_nowait()
+            except queue.Empty:
+                return
+            self._pending_host -= 1
+            self.c.mark_seen(pid, t)
 
     def _arrivals(self) -> List[Arrival]:
         out = []
@@ -70,7 +94,7 @@ class ArrivalCollector:
 
     def wait(self, timeout: float) -> Tuple[List[Arrival], bool]:
         """Block until the round's stop rule holds (True) or the timeout elapses (False)."""
-        if not self._host and self.gpu:
+        if self._pending_host == 0 and self.gpu:
             ok = self.c.wait(float(timeout))
             return self._arrivals(), ok
         t0 = time.perf_counter()
@@ -84,7 +108,7 @@ class ArrivalCollector:
 
     def drain(self, i: int, timeout: float = math.inf) -> bool:
         """Wait until every probe of rounds <= i arrived (the reference's Waitall)."""
-        if not self._host and self.gpu:
+        if self._pending_host == 0 and self.gpu:
             ok = self.c.drain(int(i), float(min(timeout, 1e9)))
         else:
             t0 = time.perf_counter()

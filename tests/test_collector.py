@@ -1,0 +1,109 @@
+"""Native arrival collector: stop rules, virtual straggler delays, lag carry-over, drain."""
+import math
+import time
+
+import pytest
+
+from erasurehead_amd.codes.schemes import RULE_ALL, RULE_COUNT, RULE_FRC, RULE_PARTIAL_COUNT, RULE_PARTIAL_FRC
+
+
+@pytest.fixture
+def C(native):
+    return native
+
+
+def test_frc_stop_on_groups(C):
+    c = C.Collector(6, [0, 0, 0, 1, 1, 1], 2)
+    t0 = C.Collector.now()
+    c.begin_round(0, t0, RULE_FRC, 5)
+    ids = [c.add_host_probe(w, 0, 0, 0.0) for w in range(6)]
+    for w in (1, 2):
+        c.mark_seen(ids[w], t0)
+    assert not c.step()
+    c.mark_seen(ids[4], t0)
+    assert c.step()  # both groups covered after 3 arrivals (k=5 not needed)
+    assert [a.worker for a in c.arrivals()] == [1, 2, 4]
+
+
+def test_count_rule_and_virtual_delay_order(C):
+    c = C.Collector(4, [0, 1, 2, 3], 4)
+    t0 = C.Collector.now()
+    c.begin_round(0, t0, RULE_COUNT, 2)
+    delays = [0.03, 0.0, 0.01, 1.0]
+    ids = [c.add_host_probe(w, 0, 0, delays[w]) for w in range(4)]
+    for i in ids:
+        c.mark_seen(i, t0)
+    assert c.wait(5.0)
+    arr = c.arrivals()
+    assert [a.worker for a in arr] == [1, 2]
+    assert arr[1].t_rel == pytest.approx(0.01, abs=1e-6)
+    assert C.Collector.now() - t0 >= 0.0099
+
+
+def test_all_rule_timeout_dead_worker(C):
+    c = C.Collector(3, [0, 1, 2], 3)
+    t0 = C.Collector.now()
+    c.begin_round(0, t0, RULE_ALL, 3)
+    ids = [c.add_host_probe(w, 0, 0, math.inf if w == 2 else 0.0) for w in range(3)]
+    for i in ids:
+        c.mark_seen(i, t0)
+    assert not c.wait(0.05)  # worker 2 never arrives -> timeout, erasure
+    assert sorted(a.worker for a in c.arrivals()) == [0, 1]
+    assert c.drain(0, 1.0)  # dead worker was seen: drain does not hang
+
+
+def test_partial_rules(C):
+    c = C.Collector(3, [0, 1, 2], 3)
+    t0 = C.Collector.now()
+    c.begin_round(0, t0, RULE_PARTIAL_COUNT, 2)
+    p1 = [c.add_host_probe(w, 1, 0, 0.0) for w in range(3)]
+    p0 = [c.add_host_probe(w, 0, 0, 0.0) for w in range(3)]
+    for w in range(3):
+        c.mark_seen(p0[w], t0)
+    assert not c.step()  # coded parts done but first parts missing
+    for w in range(3):
+        c.mark_seen(p1[w], t0)
+    assert c.step()
+    c2 = C.Collector(4, [0, 0, 1, 1], 2)
+    c2.begin_round(0, t0, RULE_PARTIAL_FRC, 4)
+    q1 = [c2.add_host_probe(w, 1, 0, 0.0) for w in range(4)]
+    q0 = [c2.add_host_probe(w, 0, 0, 0.0) for w in range(4)]
+    for w in range(4):
+        c2.mark_seen(q1[w], t0)
+    c2.mark_seen(q0[1], t0)
+    assert not c2.step()
+    c2.mark_seen(q0[3], t0)
+    assert c2.step()
+
+
+def test_lag_carries_into_next_round(C):
+    """Without a drain, a straggler's virtual finish delays its next-round arrival (reference lag)."""
+    c = C.Collector(2, [0, 1], 2)
+    t0 = C.Collector.now()
+    c.begin_round(0, t0, RULE_COUNT, 1)
+    a = c.add_host_probe(0, 0, 0, 0.0)
+    b = c.add_host_probe(1, 0, 0, 0.2)
+    c.mark_seen(a, t0)
+    c.mark_seen(b, t0)
+    assert c.wait(1.0)
+    assert [x.worker for x in c.arrivals()] == [0]
+    t1 = C.Collector.now()
+    c.begin_round(1, t1, RULE_COUNT, 1)
+    a1 = c.add_host_probe(0, 0, 1, 0.3)
+    b1 = c.add_host_probe(1, 0, 1, 0.0)
+    c.mark_seen(a1, t1)
+    c.mark_seen(b1, t1)
+    assert c.wait(2.0)
+    arr = c.arrivals()
+    # worker 1 finished round 0 at t0+0.2 (virtual), so it arrives ~0.2 - (t1-t0) after round 1 starts
+    assert arr[0].worker == 1
+    assert arr[0].t_rel == pytest.approx(0.2 - (t1 - t0), abs=2e-3)
+    assert c.drain(1, 2.0)
+    assert c.pending() == 0
+
+
+def test_rounds_must_increase(C):
+    c = C.Collector(1, [0], 1)
+    c.begin_round(3, C.Collector.now(), RULE_ALL, 1)
+    with pytest.raises(ValueError):
+        c.begin_round(2, C.Collector.now(), RULE_ALL, 1)

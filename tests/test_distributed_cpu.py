@@ -1,0 +1,67 @@
+"""Multi-process engine over gloo (world 2 and 3): same trajectories as the single-process engine."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from test_engine_cpu import CASES, make
+
+pytestmark = pytest.mark.slow
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, case, rule, out_path, extra):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from erasurehead_amd.engine import Trainer
+    from erasurehead_amd.parallel.dist import init_distributed
+
+    env = init_distributed("cpu")
+    cfg, src, sch, parts = make(case, rule, **extra)
+    if extra.get("delay_mode"):
+        cfg.add_delay = 1
+    tr = Trainer(cfg, env, src, scheme=sch)
+    res = tr.run()
+    if env.is_master:
+        np.savez(out_path, betaset=res.betaset, ws=res.worker_timeset, arrivals=np.array(
+            [[(w, p) for (w, p, _) in a] for a in res.arrivals], dtype=object), beta0=tr.beta0)
+    env.barrier()
+    env.shutdown()
+
+
+def _run(world, case, rule, tmp_path, **extra):
+    out = str(tmp_path / f"res_{world}.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), case, rule, out, extra), nprocs=world, join=True,
+                       start_method="spawn")
+    return np.load(out, allow_pickle=True)  # our own file (contains the arrival lists)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[4], CASES[5], CASES[7]])
+def test_multiprocess_matches_replay(world, case, tmp_path):
+    from erasurehead_amd.codes.schemes import Arrival
+    from oracle import replay
+
+    cfg, src, sch, parts = make(case, "AGD")
+    r = _run(world, case, "AGD", tmp_path)
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, cfg.eta())
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-10, atol=1e-12)
+
+
+def test_multiprocess_delay_straggler_skipped(tmp_path):
+    """AGC with fixed stragglers: the slow workers' messages are never used in the decode."""
+    case = (1, 0, 3, 7, 1, 3)  # W=6, s=1 -> 3 groups of 2, k=3
+    r = _run(3, case, "GD", tmp_path, delay_mode="fixed", fixed_stragglers=[1, 3, 5], fixed_sleep=0.05)
+    for a in r["arrivals"]:
+        assert {w for (w, p) in a} == {1, 3, 5}  # 0-based: workers 2,4,6 are the fast ones

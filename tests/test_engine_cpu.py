@@ -1,0 +1,124 @@
+"""Engine on CPU (torch fp64): every scheme vs the NumPy replay of the reference math."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from erasurehead_amd.codes import make_scheme, scheme_key
+from erasurehead_amd.config import RunConfig
+from erasurehead_amd.data.source import ArraySource
+from erasurehead_amd.engine import Trainer, evaluate
+from erasurehead_amd.models.losses import LEAST_SQUARES, LOGISTIC, logistic_loss, roc_auc
+from erasurehead_amd.parallel.dist import DistEnv
+from oracle import replay
+
+CASES = [  # key args: (is_coded, partitions, coded_ver, n_procs, s, num_collect)
+    (0, 0, 0, 5, 0, 0),
+    (1, 0, 0, 7, 2, 0),
+    (1, 0, 1, 7, 2, 0),
+    (1, 0, 2, 7, 2, 0),
+    (1, 0, 3, 7, 2, 4),
+    (1, 0, 3, 9, 2, 6),  # W=8, s=2: uneven FRC groups (extension)
+    (1, 4, 1, 7, 1, 0),
+    (1, 4, 0, 7, 1, 0),
+]
+
+
+def make(case, rule="AGD", rows=30, d=17, loss="auto", seed=0, precision="fp64", **kw):
+    is_coded, P, ver, n_procs, s, k = case
+    W = n_procs - 1
+    key = scheme_key(is_coded, P, ver)
+    uneven = key in ("approx", "replication") and W % (s + 1) != 0
+    probe = make_scheme(key, W, s, rows * W, k, P, allow_uneven=uneven)
+    n_parts = probe.n_partition_files
+    n = rows * n_parts
+    rng = np.random.RandomState(seed)
+    parts = [(rng.randn(rows, d) * 0.3, rng.choice([-1.0, 1.0], rows)) for _ in range(n_parts)]
+    test = (rng.randn(rows * 2, d) * 0.3, rng.choice([-1.0, 1.0], rows * 2))
+    src = ArraySource(parts, test)
+    cfg = RunConfig(n_procs, n, d, "/tmp/eh_cpu_eng/", 0, "x", is_coded, s, P, ver, k, 0, rule, num_itrs=6, seed=0,
+                    verbose=False, allow_uneven_groups=uneven, loss=loss, precision=precision, **kw)
+    sch = make_scheme(key, W, s, n, k, P, allow_uneven=uneven, rng=np.random.RandomState(7))
+    return cfg, src, sch, parts
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("rule", ["GD", "AGD"])
+def test_engine_matches_numpy_replay(case, rule):
+    cfg, src, sch, parts = make(case, rule)
+    tr = Trainer(cfg, DistEnv(), src, scheme=sch)
+    res = tr.run()
+    ref = replay(sch, parts, tr.beta0, res.arrivals, rule, cfg.alpha_value, cfg.n_rows, cfg.eta())
+    np.testing.assert_allclose(res.betaset, ref, rtol=1e-10, atol=1e-12)
+    assert res.timeset.shape == (6,) and np.all(res.timeset > 0)
+    assert res.worker_timeset.shape == (6, cfg.n_workers)
+
+
+def test_least_squares_engine():
+    cfg, src, sch, parts = make((1, 0, 3, 7, 2, 4), "GD", loss="least_squares")
+    tr = Trainer(cfg, DistEnv(), src, scheme=sch)
+    res = tr.run()
+    ref = replay(sch, parts, tr.beta0, res.arrivals, "GD", cfg.alpha_value, cfg.n_rows, cfg.eta(), LEAST_SQUARES)
+    np.testing.assert_allclose(res.betaset, ref, rtol=1e-10, atol=1e-12)
+
+
+def test_fp32_close_to_fp64():
+    a = make((1, 0, 3, 7, 2, 4), "GD")
+    b = make((1, 0, 3, 7, 2, 4), "GD", precision="fp32")
+    ra = Trainer(a[0], DistEnv(), a[1], scheme=a[2]).run()
+    rb = Trainer(b[0], DistEnv(), b[1], scheme=b[2]).run()
+    np.testing.assert_allclose(rb.betaset, ra.betaset, rtol=1e-4, atol=1e-5)
+
+
+def test_evaluate_matches_reference_epilogue(tmp_path):
+    cfg, src, sch, parts = make((0, 0, 0, 5, 0, 0), "GD")
+    tr = Trainer(cfg, DistEnv(), src, scheme=sch)
+    res = tr.run()
+    lines = []
+    cfg.input_dir = str(tmp_path) + "/"
+    ev = evaluate(tr, res, log=lines.append, write=False)
+    # training set = partitions 1..W-1 (skips partition W, ref src/naive.py:161)
+    Xtr = np.vstack([parts[p][0] for p in range(cfg.n_workers - 1)])
+    ytr = np.concatenate([parts[p][1] for p in range(cfg.n_workers)])[: Xtr.shape[0]]
+    Xte, yte = src._test
+    for i in range(len(res.betaset)):
+        b = res.betaset[i]
+        assert ev.training_loss[i] == pytest.approx(logistic_loss(ytr, Xtr @ b), rel=1e-10)
+        assert ev.testing_loss[i] == pytest.approx(logistic_loss(yte, Xte @ b), rel=1e-10)
+        assert ev.auc[i] == pytest.approx(roc_auc(yte, Xte @ b), rel=1e-12)
+
+
+def test_delay_virtual_floor():
+    """add_delay=1 (scaled mean): AGC time-to-decode sums to the deterministic floor + overhead."""
+    from erasurehead_amd.utils.delay import delay_floor
+
+    cfg, src, sch, parts = make((1, 0, 3, 7, 2, 4), "GD", delay_mean=0.01)
+    cfg.add_delay = 1
+    tr = Trainer(cfg, DistEnv(), src, scheme=sch)
+    res = tr.run()
+    floor = delay_floor(6, 6, groups=sch.group_of, k=4, mean=0.01)
+    assert floor <= res.timeset.sum() < floor + 6 * 0.02
+    # the wall-clock per round includes the drained straggler tail (replication/AGC Waitall)
+    assert np.all(res.loop_time >= res.timeset)
+
+
+def test_killed_worker_becomes_erasure():
+    cfg, src, sch, parts = make((1, 0, 0, 7, 2, 0), "GD", kill_workers=[2], round_timeout=5.0)
+    cfg.add_delay = 1
+    cfg.delay_mode = "none"
+    tr = Trainer(cfg, DistEnv(), src, scheme=sch)
+    res = tr.run()
+    assert res.timeouts == 0  # cyclic tolerates s=2 dead/slow workers
+    assert np.all(res.worker_timeset[:, 1] == -1)
+    ref = replay(sch, parts, tr.beta0, res.arrivals, "GD", cfg.alpha_value, cfg.n_rows, cfg.eta())
+    np.testing.assert_allclose(res.betaset, ref, rtol=1e-10, atol=1e-12)
+
+
+def test_checkpoint_written(tmp_path):
+    cfg, src, sch, parts = make((1, 0, 3, 7, 2, 4), "GD", checkpoint_every=2,
+                                checkpoint_path=str(tmp_path / "ck.pt"))
+    res = Trainer(cfg, DistEnv(), src, scheme=sch).run()
+    st = torch.load(str(tmp_path / "ck.pt"), weights_only=True)
+    assert st["next_round"] == 6
+    np.testing.assert_allclose(st["hist"].numpy()[:, :17], res.betaset)
