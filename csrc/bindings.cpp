@@ -17,11 +17,11 @@
 namespace eh {
 hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
                              int ntasks, const void* beta, void* slab, const int* slot_task_begin,
-                             int nslots, void* G, int ld, hipStream_t st);
+                             int nslots, void* part, void* G, int ld, hipStream_t st);
 hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, const void* tasks,
                                      int ntasks, const void* beta, const int* task_row_off,
                                      void* rbuf, void* slab, const int* slot_task_begin,
-                                     int nslots, void* G, int ld, hipStream_t st);
+                                     int nslots, void* part, void* G, int ld, hipStream_t st);
 hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, const int* col_idx,
                               const void* vals, const void* y, const void* coef,
                               const void* beta, void* rbuf, long long nrows,
@@ -75,8 +75,15 @@ int acc_code(const Tensor& t) {
   throw std::invalid_argument("accumulator tensors must be float64 or float32");
 }
 
+constexpr int64_t kSplits = 16;  // must match csrc/kernels/grad_dense.hip
+
+void need_part(const Tensor& part, int64_t nslots, int64_t ld, int ac) {
+  need_cuda(part, "part");
+  need(part.numel() >= nslots * kSplits * ld && acc_code(part) == ac, "part must be [nslots*16*ld] acc dtype");
+}
+
 void grad_dense(int64_t dtype, int64_t loss, int64_t cpl, const Tensor& segs, const Tensor& tasks,
-                const Tensor& beta, const Tensor& slab, const Tensor& slot_task_begin,
+                const Tensor& beta, const Tensor& slab, const Tensor& slot_task_begin, const Tensor& part,
                 const Tensor& G, int64_t ld) {
   need_cuda(segs, "segs");
   need_cuda(tasks, "tasks");
@@ -95,16 +102,18 @@ void grad_dense(int64_t dtype, int64_t loss, int64_t cpl, const Tensor& segs, co
   need(cpl * 64 >= ld, "cpl * 64 must cover ld");
   const int ac = dtype == 0 ? 0 : 1;
   need(acc_code(beta) == ac && acc_code(slab) == ac && acc_code(G) == ac, "beta/slab/G dtype mismatch");
+  need_part(part, nslots, ld, ac);
   if (ntasks == 0) return;
   check(eh::grad_dense_launch((int)dtype, (int)loss, (int)cpl, segs.data_ptr(), tasks.data_ptr(), (int)ntasks,
                               beta.data_ptr(), slab.data_ptr(), slot_task_begin.data_ptr<int>(), (int)nslots,
-                              G.data_ptr(), (int)ld, stream_of(G)),
+                              part.data_ptr(), G.data_ptr(), (int)ld, stream_of(G)),
         "grad_dense");
 }
 
 void grad_dense_twopass(int64_t dtype, int64_t loss, const Tensor& segs, const Tensor& tasks,
                         const Tensor& beta, const Tensor& task_row_off, const Tensor& rbuf,
-                        const Tensor& slab, const Tensor& slot_task_begin, const Tensor& G, int64_t ld) {
+                        const Tensor& slab, const Tensor& slot_task_begin, const Tensor& part, const Tensor& G,
+                        int64_t ld) {
   need_cuda(segs, "segs");
   need_cuda(tasks, "tasks");
   need_cuda(beta, "beta");
@@ -117,11 +126,13 @@ void grad_dense_twopass(int64_t dtype, int64_t loss, const Tensor& segs, const T
   need(slab.dim() == 2 && slab.size(0) >= ntasks && slab.size(1) == ld, "slab must be [>=ntasks, ld]");
   need(G.dim() == 2 && G.size(0) == nslots && G.size(1) == ld, "G must be [nslots, ld]");
   need(task_row_off.numel() >= ntasks, "task_row_off too small");
+  need_part(part, nslots, ld, acc_code(G));
+  need(rbuf.numel() >= 1 && acc_code(rbuf) == acc_code(G) && acc_code(beta) == acc_code(G), "rbuf/beta dtype");
   if (ntasks == 0) return;
   check(eh::grad_dense_twopass_launch((int)dtype, (int)loss, segs.data_ptr(), tasks.data_ptr(), (int)ntasks,
                                       beta.data_ptr(), task_row_off.data_ptr<int>(), rbuf.data_ptr(),
                                       slab.data_ptr(), slot_task_begin.data_ptr<int>(), (int)nslots,
-                                      G.data_ptr(), (int)ld, stream_of(G)),
+                                      part.data_ptr(), G.data_ptr(), (int)ld, stream_of(G)),
         "grad_dense_twopass");
 }
 

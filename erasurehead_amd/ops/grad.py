@@ -28,6 +28,7 @@ _SEG = struct.Struct("<QQdq")  # csrc Segment {const void* X; const void* y; dou
 MAX_CPL = 32
 DEFAULT_TASKS = 2048
 MIN_ROWS_PER_TASK = 32
+SLAB_SPLITS = 16  # csrc/kernels/grad_dense.hip kSplits
 
 
 def choose_cpl(ld: int, vec: int) -> Optional[int]:
@@ -90,12 +91,13 @@ class DenseGradPlan:
                 seg_id += 1
             slot_begin.append(len(tasks))
         dev = self.device
-        self.segs = torch.frombuffer(bytes(segs) or b"\0" * 32, dtype=torch.uint8).clone().to(dev)
+        self.segs = torch.tensor(list(bytes(segs) or b"\0" * 32), dtype=torch.uint8).to(dev)
         self.ntasks = len(tasks)
         t = np.asarray(tasks, dtype=np.int32).reshape(-1, 4)
         self.tasks = torch.from_numpy(t).to(dev)
         self.slot_task_begin = torch.tensor(slot_begin, dtype=torch.int32, device=dev)
         self.slab = torch.empty((max(1, self.ntasks), self.ld), dtype=self.prec.acc, device=dev)
+        self.part = torch.empty(max(1, self.nslots) * SLAB_SPLITS * self.ld, dtype=self.prec.acc, device=dev)
         if self.cpl is None:
             off = np.zeros(max(1, self.ntasks), dtype=np.int64)
             if self.ntasks:
@@ -118,10 +120,10 @@ class DenseGradPlan:
             C = native()
             if self.cpl is not None:
                 C.grad_dense(self.prec.code, self.loss, self.cpl, self.segs, self.tasks, beta, self.slab,
-                             self.slot_task_begin, G, self.ld)
+                             self.slot_task_begin, self.part, G, self.ld)
             else:
                 C.grad_dense_twopass(self.prec.code, self.loss, self.segs, self.tasks, beta, self.task_row_off,
-                                     self.rbuf, self.slab, self.slot_task_begin, G, self.ld)
+                                     self.rbuf, self.slab, self.slot_task_begin, self.part, G, self.ld)
             return G
         return self._run_torch(beta, G)
 
