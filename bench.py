@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--floor-rounds", type=int, default=100)
     ap.add_argument("--tasks", type=int, default=0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl"])
     return ap.parse_args()
 
 
@@ -63,16 +64,17 @@ def main() -> int:
         return RunConfig(a.workers + 1, a.n_rows, a.n_cols, "/tmp/erasurehead_bench/", 0, "synthetic", 1,
                          a.stragglers, 0, a.coded_ver, a.num_collect, a.add_delay, a.update_rule,
                          num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234, seed=0,
-                         allow_uneven_groups=True, verbose=False, tasks=a.tasks)
+                         allow_uneven_groups=True, verbose=False, tasks=a.tasks,
+                         transport=a.transport)
 
     t_setup = time.perf_counter()
     trainer = Trainer(make_cfg(a.warmup + a.steps), env)
     setup_s = time.perf_counter() - t_setup
     res = trainer.run(timed_start=a.warmup)
-    timed = None
-    if env.is_master:
-        timed = res.timed_seconds
-    timed = env.broadcast_object(timed, 0)
+    # timed region: barrier + device sync on both sides on every rank; MAX over ranks
+    mine = res.timed_seconds if env.is_master else trainer.worker_timed_seconds
+    timed = env.allreduce_max(mine)
+    transport = trainer.transport
     out = {}
     if env.is_master:
         sec_per_iter = timed / a.steps
@@ -100,7 +102,8 @@ def main() -> int:
                 "n_rows": a.n_rows, "n_cols": a.n_cols, "workers": a.workers,
                 "n_stragglers": a.stragglers, "num_collect": a.num_collect, "add_delay": a.add_delay,
                 "update_rule": a.update_rule,
-                "parallelism": f"ps-master + {a.workers} logical workers on {env.world} GPU(s) (dp{env.world}, RCCL p2p)",
+                "parallelism": f"ps-master + {a.workers} logical workers on {env.world} GPU(s) (dp{env.world})",
+                "transport": transport,
             },
             "time_to_decode_ms_median": float(1e3 * np.median(ts)),
             "loop_ms_median": float(1e3 * np.median(lt)),
@@ -112,12 +115,14 @@ def main() -> int:
         if bpr:
             out["rank0_grad_stream_GBps_at_step_time"] = bpr / sec_per_iter / 1e9
     # convergence: iterations to the training-loss floor (100-round run, evaluated with the MFMA eval kernel)
+    trainer.close()
     if not a.no_floor:
         del trainer
         if torch.cuda.is_available():
             torch.cuda.empty_cache()
         tr2 = Trainer(make_cfg(a.floor_rounds), env)
         r2 = tr2.run()
+        tr2.close()
         if env.is_master:
             tr2.cfg.fix_quirks = True  # evaluate on all partitions
             ev = evaluate(tr2, r2, write=False)

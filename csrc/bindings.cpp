@@ -30,6 +30,7 @@ hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, con
 hipError_t eval_gemm_loss_launch(int x_dtype, int loss_kind, const void* X, long long ldx,
                                  long long n, int d, const void* y, const void* B, int ldb,
                                  int R, double* loss, void* P, hipStream_t st);
+void bind_ipc(pybind11::module& m);  // csrc/runtime/ipc.cpp
 }  // namespace eh
 
 // Must match csrc/kernels/update.hip
@@ -223,7 +224,8 @@ void eval_gemm_loss(int64_t loss_kind, const Tensor& X, int64_t n, int64_t d, co
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
-  m.doc() = "ErasureHead MI355X native runtime: gfx950 HIP kernels + arrival collector";
+  m.doc() = "ErasureHead MI355X native runtime: gfx950 HIP kernels + arrival collector + IPC mailbox";
+  eh::bind_ipc(m);
   m.def("grad_dense", &grad_dense);
   m.def("grad_dense_twopass", &grad_dense_twopass);
   m.def("grad_sparse", &grad_sparse);
@@ -248,6 +250,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("begin_round", &eh::Collector::begin_round)
       .def("add_event_probe", &eh::Collector::add_event_probe)
       .def("add_host_probe", &eh::Collector::add_host_probe)
+      .def("add_flag_probe", &eh::Collector::add_flag_probe)
       .def("mark_seen", &eh::Collector::mark_seen)
       .def("step", &eh::Collector::step, py::call_guard<py::gil_scoped_release>())
       .def("wait", &eh::Collector::wait, py::call_guard<py::gil_scoped_release>())

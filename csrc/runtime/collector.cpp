@@ -53,7 +53,7 @@ void Collector::begin_round(int round, double t_start, int rule, int k) {
 
 int Collector::add_event_probe(int worker, int part, int round, uintptr_t event, double delay) {
   if (worker < 0 || worker >= W_) throw std::invalid_argument("Collector: bad worker");
-  Probe p{worker, part, round, reinterpret_cast<hipEvent_t>(event), false, false, false, 0.0, delay, kInf};
+  Probe p{worker, part, round, reinterpret_cast<hipEvent_t>(event), nullptr, 0, false, false, false, 0.0, delay, kInf};
   probes_.push_back(p);
   live_.push_back(static_cast<int>(probes_.size()) - 1);
   return static_cast<int>(probes_.size()) - 1;
@@ -61,7 +61,17 @@ int Collector::add_event_probe(int worker, int part, int round, uintptr_t event,
 
 int Collector::add_host_probe(int worker, int part, int round, double delay) {
   if (worker < 0 || worker >= W_) throw std::invalid_argument("Collector: bad worker");
-  Probe p{worker, part, round, nullptr, true, false, false, 0.0, delay, kInf};
+  Probe p{worker, part, round, nullptr, nullptr, 0, true, false, false, 0.0, delay, kInf};
+  probes_.push_back(p);
+  live_.push_back(static_cast<int>(probes_.size()) - 1);
+  return static_cast<int>(probes_.size()) - 1;
+}
+
+int Collector::add_flag_probe(int worker, int part, int round, uintptr_t flag_addr, uint64_t value, double delay) {
+  if (worker < 0 || worker >= W_) throw std::invalid_argument("Collector: bad worker");
+  if (flag_addr == 0) throw std::invalid_argument("Collector: null flag");
+  Probe p{worker, part, round, nullptr, reinterpret_cast<const uint64_t*>(flag_addr), value, false, false, false,
+          0.0, delay, kInf};
   probes_.push_back(p);
   live_.push_back(static_cast<int>(probes_.size()) - 1);
   return static_cast<int>(probes_.size()) - 1;
@@ -96,6 +106,10 @@ void Collector::poll_events(double t) {
   for (int id : live_) {
     Probe& p = probes_[id];
     if (p.seen || p.host) continue;
+    if (p.flag) {
+      if (__atomic_load_n(p.flag, __ATOMIC_ACQUIRE) >= p.fval) mark_seen(id, t);
+      continue;
+    }
     int hit = -1;
     for (int k = 0; k < static_cast<int>(done.size()); ++k)
       if (done[k].first == p.ev) { hit = k; break; }

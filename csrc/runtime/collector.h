@@ -56,6 +56,9 @@ class Collector {
   void begin_round(int round, double t_start, int rule, int k);
   int add_event_probe(int worker, int part, int round, uintptr_t event, double delay);
   int add_host_probe(int worker, int part, int round, double delay);
+  // IPC mailbox probe: arrived once the 64-bit flag at `flag_addr` (shared host memory,
+  // release-stored by the sending GPU) reaches `value` (csrc/runtime/ipc.cpp).
+  int add_flag_probe(int worker, int part, int round, uintptr_t flag_addr, uint64_t value, double delay);
   void mark_seen(int probe, double t);
 
   // Process everything that is ready; returns true once the current round's stop rule holds.
@@ -77,6 +80,8 @@ class Collector {
   struct Probe {
     int worker, part, round;
     hipEvent_t ev;
+    const uint64_t* flag;  // IPC flag probe (nullptr otherwise)
+    uint64_t fval;
     bool host;
     bool seen;
     bool arrived;

@@ -46,20 +46,10 @@ from ..ops.update import combine_update
 from ..parallel.collector import ArrivalCollector
 from ..parallel.dist import DistEnv
 from ..parallel.placement import place_workers, workers_by_rank
+from ..parallel.transport import make_transport
 from ..utils import report
 from ..utils.delay import DelayModel
 from ..utils.tracing import PhaseTimer, range_
-
-TAG_STRIDE = 1024  # gloo tags: beta of round i = 2*i*S, message j of round i = 2*(i*S+j)+1
-
-
-def _tag_beta(i: int) -> int:
-    return 2 * i * TAG_STRIDE
-
-
-def _tag_msg(i: int, j: int) -> int:
-    return 2 * (i * TAG_STRIDE + j) + 1
-
 
 @dataclass
 class TrainResult:
@@ -170,34 +160,30 @@ class Trainer:
         per_round = max(1, (n_loc + n_rem) * ld * es)
         self.K = int(max(2, min(R, (1 << 30) // per_round)))
         self.G = torch.zeros((self.K, max(1, n_loc), ld), dtype=acc, device=dev)
+        self.n_loc = n_loc
+        remote_counts = {r: len(v) for r, v in self.remote_msgs.items() if v} if env.is_master else {}
+        self.tx = make_transport(cfg.transport, env, R, self.K, ld, acc, n_loc, remote_counts, cfg.round_timeout) \
+            if env.world > 1 else None
         if env.is_master:
             self.rem_slot = {}
-            j = 0
             for r in sorted(self.remote_msgs):
-                for m in self.remote_msgs[r]:
-                    self.rem_slot[(m.worker, m.part)] = j
-                    j += 1
-            self.Rbuf = torch.zeros((self.K, max(1, n_rem), ld), dtype=acc, device=dev)
+                for jj, m in enumerate(self.remote_msgs[r]):
+                    self.rem_slot[(m.worker, m.part)] = self.tx.row0[r] + jj
+            self.Rbuf = self.tx.make_rbuf() if self.tx is not None else None
             self.beta = torch.zeros(ld, dtype=torch.float64, device=dev)
             self.u = torch.zeros(ld, dtype=torch.float64, device=dev)
             self.hist = torch.zeros((R, ld), dtype=torch.float64, device=dev)
             self.beta_in = torch.zeros((R + 1, ld), dtype=acc, device=dev)
             self.loc_index = {(m.worker, m.part): j for j, m in enumerate(self.local_msgs)}
-        else:
-            self.bbuf = torch.zeros((2, ld), dtype=acc, device=dev)
         if env.gpu:
             self.cs = torch.cuda.current_stream(dev)
-            self.ps = {r: torch.cuda.Stream(dev) for r in (range(1, env.world) if env.is_master else [0])}
             self.loc_ev = [torch.cuda.Event() for _ in range(self.K)]
             if env.is_master:
-                self.rem_ev = [[torch.cuda.Event() for _ in range(max(1, n_rem))] for _ in range(self.K)]
-                self.beta_ev = torch.cuda.Event()
                 self.upd_ev = torch.cuda.Event()
-            else:
-                self.bev = torch.cuda.Event()
-                self.gev = torch.cuda.Event()
-                self.send_done = [None] * self.K
-        self._cpu_sends: List[List] = [[] for _ in range(self.K)]
+
+    @property
+    def transport(self) -> str:
+        return self.tx.name if self.tx is not None else "local"
 
     # --------------------------------------------------------------------------- helpers
     def _init_beta(self):
@@ -307,8 +293,7 @@ class Trainer:
                         msgs.append(self.G[slot, self.loc_index[key]])
                     else:
                         j = self.rem_slot[key]
-                        if env.gpu:
-                            self.cs.wait_event(self.rem_ev[slot][j])
+                        self.tx.before_read(slot, j)
                         msgs.append(self.Rbuf[slot, j])
                     coefs.append(c)
                 decay, gm, l2, theta, code = self.update.coeffs(i, float(eta[i]))
@@ -341,84 +326,38 @@ class Trainer:
         return res
 
     def _send_beta(self, i: int):
-        env = self.env
-        if env.world == 1:
-            return
-        if env.gpu:
-            self.beta_ev.record(self.cs)
-            for r in range(1, env.world):
-                s = self.ps[r]
-                s.wait_event(self.beta_ev)
-                with torch.cuda.stream(s):
-                    dist.isend(self.beta_in[i], r)
-        else:
-            for r in range(1, env.world):
-                self._cpu_sends[i % self.K].append(dist.isend(self.beta_in[i], r, tag=_tag_beta(i)))
+        if self.tx is not None:
+            self.tx.send_beta(i, self.beta_in[i])
 
     def _post_recvs(self, i: int, slot: int, col: ArrivalCollector, delays):
-        env = self.env
-        for r in sorted(self.remote_msgs):
-            msgs = self.remote_msgs[r]
-            if env.gpu:
-                s = self.ps[r]
-                with torch.cuda.stream(s):
-                    for jj, m in enumerate(msgs):
-                        j = self.rem_slot[(m.worker, m.part)]
-                        w = dist.irecv(self.Rbuf[slot, j], r)
-                        w.wait()
-                        ev = self.rem_ev[slot][j]
-                        ev.record(s)
-                        col.add_event(m.worker, m.part, i, ev, delays[m.worker])
-            else:
-                for jj, m in enumerate(msgs):
-                    j = self.rem_slot[(m.worker, m.part)]
-                    w = dist.irecv(self.Rbuf[slot, j], r, tag=_tag_msg(i, jj))
-                    col.add_work(m.worker, m.part, i, w, delays[m.worker], src=r)
+        if self.tx is not None:
+            self.tx.post_recvs(i, slot, col, self.Rbuf, self.remote_msgs, delays)
 
     def _worker_loop(self, timed_start) -> None:
-        cfg, env = self.cfg, self.env
-        R, K = cfg.num_itrs, self.K
-        n = len(self.local_msgs)
+        cfg, env, tx = self.cfg, self.env, self.tx
+        R, K, n = cfg.num_itrs, self.K, self.n_loc
+        t0 = None
         for i in range(R):
             if timed_start is not None and i == timed_start:
-                self._timed_fence()
-            slot, bs = i % K, i % 2
-            if env.gpu:
-                with torch.cuda.stream(self.ps[0]):
-                    w = dist.irecv(self.bbuf[bs], 0)
-                    w.wait()
-                    self.bev.record(self.ps[0])
-                self.cs.wait_event(self.bev)
-                if self.send_done[slot] is not None:
-                    self.cs.wait_event(self.send_done[slot])
-                if n:
-                    self.plan.run(self.bbuf[bs], self.G[slot])
-                self.gev.record(self.cs)
-                s = self.ps[0]
-                s.wait_event(self.gev)
-                with torch.cuda.stream(s):
-                    works = [dist.isend(self.G[slot, j], 0) for j in range(n)]
-                    for w in works:
-                        w.wait()
-                    ev = self.send_done[slot] or torch.cuda.Event()
-                    ev.record(s)
-                    self.send_done[slot] = ev
-            else:
-                for w in self._cpu_sends[slot]:
-                    w.wait()
-                self._cpu_sends[slot] = []
-                dist.irecv(self.bbuf[bs], 0, tag=_tag_beta(i)).wait()
-                if n:
-                    self.plan.run(self.bbuf[bs], self.G[slot])
-                self._cpu_sends[slot] = [dist.isend(self.G[slot, j], 0, tag=_tag_msg(i, j)) for j in range(n)]
-        for lst in self._cpu_sends:
-            for w in lst:
-                w.wait()
+                t0 = self._timed_fence()
+            slot = i % K
+            b = tx.recv_beta(i)
+            if n:
+                self.plan.run(b, self.G[slot])
+                tx.send_msgs(i, self.G[slot, :n])
+        tx.finish()
         if timed_start is not None:
-            self._timed_fence()
+            self.worker_timed_seconds = self._timed_fence() - t0
         self._sync()
         env.barrier()
         return None
+
+    def close(self) -> None:
+        """Release transport resources (IPC mappings, shared flags); collective."""
+        if self.tx is not None:
+            self.env.barrier()
+            self.tx.close()
+            self.tx = None
 
     # ------------------------------------------------------------------- checkpointing
     def _checkpoint(self, next_round: int, timeset, worker_timeset):

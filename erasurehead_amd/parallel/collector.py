@@ -62,6 +62,10 @@ class ArrivalCollector:
         self._keep[pid] = event
         return pid
 
+    def add_flag(self, worker: int, part: int, i: int, addr: int, value: int, delay: float) -> int:
+        """IPC mailbox probe: arrived when the shared-host counter at ``addr`` reaches ``value``."""
+        return self.c.add_flag_probe(int(worker), int(part), int(i), int(addr), int(value), float(delay))
+
     def add_work(self, worker: int, part: int, i: int, work, delay: float, src: int = 0) -> int:
         """Host probe completed when ``work`` finishes (None = already complete now)."""
         pid = self.c.add_host_probe(int(worker), int(part), int(i), float(delay))

@@ -92,11 +92,14 @@ def init_distributed(device: str = "auto", timeout_min: float = 60.0) -> DistEnv
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     to = datetime.timedelta(minutes=timeout_min)
     owns = False
+    shared_gpu = want_gpu and world > torch.cuda.device_count()  # several ranks per GPU: RCCL impossible
     if not dist.is_initialized():
-        backend = "nccl" if want_gpu else "gloo"
-        kw = {"device_id": dev} if want_gpu else {}
+        backend = "nccl" if want_gpu and not shared_gpu else "gloo"
+        kw = {"device_id": dev} if backend == "nccl" else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=to, **kw)
         owns = True
     backend = dist.get_backend()
     ctrl = dist.new_group(backend="gloo", timeout=to) if backend != "gloo" else dist.group.WORLD
+    if want_gpu and backend == "gloo":
+        os.environ.setdefault("ERASUREHEAD_TRANSPORT", "ipc")  # device data can only move over IPC
     return DistEnv(rank=rank, world=world, local_rank=local, device=dev, backend=backend, ctrl=ctrl, owns_pg=owns)

@@ -1,0 +1,45 @@
+"""One rank of a multi-process engine run (launched by torchrun from tests/test_multiproc_gpu.py).
+
+python -m torch.distributed.run --nproc-per-node N tests/mp_engine_run.py OUT.npz CASE_INDEX RULE [delay_mean]
+Builds the same seeded ArraySource as tests/test_engine_cpu.py::make, trains on the GPU(s)
+with the ranks' transport (ranks sharing one GPU -> IPC mailboxes) and writes, on rank 0,
+the betaset, beta0 and per-round arrival lists so the test can replay them with the fp64
+NumPy oracle.
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    out, case_i, rule = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+    delay = float(sys.argv[4]) if len(sys.argv) > 4 else 0.0
+    from erasurehead_amd.engine import Trainer
+    from erasurehead_amd.parallel.dist import init_distributed
+    from test_engine_cpu import CASES, make
+
+    env = init_distributed(os.environ.get("EH_TEST_DEVICE", "cuda"))
+    extra = {"delay_mean": delay} if delay else {}
+    cfg, src, sch, parts = make(CASES[case_i], rule, **extra)
+    cfg.num_itrs = 12
+    if delay:
+        cfg.add_delay = 1
+        cfg.force_delay = True
+    tr = Trainer(cfg, env, src, scheme=sch)
+    res = tr.run()
+    if env.is_master:
+        arr = np.array([[(w, p) for (w, p, _) in a] for a in res.arrivals], dtype=object)
+        np.savez(out, betaset=res.betaset, beta0=tr.beta0, arrivals=arr, transport=np.array(tr.transport),
+                 timeset=res.timeset)
+    env.barrier()
+    tr.close()
+    env.shutdown()
+
+
+if __name__ == "__main__":
+    main()

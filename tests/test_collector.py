@@ -1,5 +1,6 @@
 """Native arrival collector: stop rules, virtual straggler delays, lag carry-over, drain."""
 import math
+import os
 import time
 
 import pytest
@@ -107,3 +108,17 @@ def test_rounds_must_increase(C):
     c.begin_round(3, C.Collector.now(), RULE_ALL, 1)
     with pytest.raises(ValueError):
         c.begin_round(2, C.Collector.now(), RULE_ALL, 1)
+
+
+def test_collector_host_asan_ubsan():
+    """The collector state machine under AddressSanitizer + UBSan (host build, tools/sanitize_host.sh)."""
+    import shutil
+    import subprocess
+
+    if shutil.which("g++") is None:
+        pytest.skip("no host compiler")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["bash", os.path.join(root, "tools", "sanitize_host.sh")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "collector selftest ok" in r.stdout

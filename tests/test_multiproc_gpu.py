@@ -1,0 +1,67 @@
+"""Multi-process engine on the GPU: ranks share one MI355X and talk over the IPC mailbox.
+
+Each case is launched with torchrun as child processes (2 and 3 ranks on the one GPU of the
+test box; on an 8-GPU node the same code path runs one rank per GPU over xGMI), and the
+master's trajectory is replayed with the fp64 NumPy oracle on the arrival sets it reports.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(world, case_i, rule, out, delay=0.0):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(HERE, "mp_engine_run.py"),
+           out, str(case_i), rule, str(delay)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return np.load(out, allow_pickle=True)  # our own file (contains the arrival lists)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case_i", [0, 1, 4, 6])
+def test_ipc_multiprocess_matches_replay(world, case_i, tmp_path):
+    from oracle import replay
+    from test_engine_cpu import CASES, make
+
+    r = _launch(world, case_i, "AGD", str(tmp_path / "r.npz"))
+    assert str(r["transport"]) == "ipc"
+    cfg, src, sch, parts = make(CASES[case_i], "AGD")
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    eta = 10.0 * np.ones(len(arrivals))
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, eta)
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+
+
+def test_ipc_multiprocess_delayed_agc(tmp_path):
+    """AGC (W=6, s=2, k=4) with the reference delay model: the decode only uses fast workers."""
+    from oracle import replay
+    from test_engine_cpu import CASES, make
+
+    r = _launch(3, 4, "GD", str(tmp_path / "d.npz"), delay=0.01)
+    cfg, src, sch, parts = make(CASES[4], "GD")
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    for i, a in enumerate(r["arrivals"]):
+        d = np.random.RandomState(i).exponential(0.01, 6)
+        used = {w for (w, p) in a}
+        slowest = int(np.argmax(d))
+        if d[slowest] - np.sort(d)[-2] > 0.004:  # a clear straggler never makes the cut
+            assert slowest not in used or len(used) == 6
+    ref = replay(sch, parts, r["beta0"], arrivals, "GD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)

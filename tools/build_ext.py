@@ -63,7 +63,8 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     headers = _headers()
     common = ["-O3", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{CSRC}"]
     hip_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    cpp_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "bindings.cpp")]
+    cpp_srcs = sorted(p for p in glob.glob(os.path.join(CSRC, "runtime", "*.cpp")) if not p.endswith("_selftest.cpp"))
+    cpp_srcs.append(os.path.join(CSRC, "bindings.cpp"))
     jobs_list = []
     for s in hip_srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")

@@ -18,6 +18,9 @@ tail -2 "$OUT/smoke.log"
 echo "== bench"
 timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 5 --json-out "$OUT/bench.json" > "$OUT/bench.log" 2>&1 || { tail -30 "$OUT/bench.log"; exit 3; }
 tail -1 "$OUT/bench.log"
+echo "== bench, 2 ranks sharing the GPU (IPC transport path)"
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 3 --no-floor --json-out "$OUT/bench_2rank.json" > "$OUT/bench_2rank.log" 2>&1 || { tail -30 "$OUT/bench_2rank.log"; exit 5; }
+tail -c 600 "$OUT/bench_2rank.json"
 echo "== rocprofv3"
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python "$ROOT/bench.py" --steps 10 --warmup 3 --no-floor > "$OUT/prof.log" 2>&1 || { tail -30 "$OUT/prof.log"; exit 4; }
 find "$OUT/prof" -name "*stats*" | head
