@@ -24,7 +24,8 @@ from .synthetic import DeviceGMM
 
 
 def _pad_dense(X, prec: Precision, device) -> torch.Tensor:
-    X = torch.as_tensor(np.asarray(X, dtype=np.float64) if not isinstance(X, torch.Tensor) else X)
+    if not isinstance(X, torch.Tensor):  # memory-mapped .npy twins are read-only: copy those
+        X = torch.from_numpy(np.require(np.asarray(X, dtype=np.float64), requirements=["W", "C"]))
     if X.dim() == 1:
         X = X[None, :]
     n, d = X.shape

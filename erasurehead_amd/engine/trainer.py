@@ -158,7 +158,8 @@ class Trainer:
         n_loc = len(self.local_msgs)
         n_rem = sum(len(v) for v in self.remote_msgs.values())
         per_round = max(1, (n_loc + n_rem) * ld * es)
-        self.K = int(max(2, min(R, (1 << 30) // per_round)))
+        K = int(max(2, min(R, (1 << 30) // per_round)))
+        self.K = int(env.broadcast_object(K, 0)) if env.world > 1 else K  # the mailbox ring is shared: one K
         self.G = torch.zeros((self.K, max(1, n_loc), ld), dtype=acc, device=dev)
         self.n_loc = n_loc
         remote_counts = {r: len(v) for r, v in self.remote_msgs.items() if v} if env.is_master else {}
@@ -223,16 +224,20 @@ class Trainer:
         log = log or report.log
         cfg, env = self.cfg, self.env
         self.warmup()
+        start = 0
         if env.is_master:
             self._init_beta()
+            if cfg.resume:
+                start = self._restore(cfg.resume)
             for line in self.scheme.setup_lines():
                 if cfg.verbose:
                     log(line)
+        start = env.broadcast_object(start, 0)
         env.barrier()
         if env.is_master:
-            res = self._master_loop(timed_start, log)
+            res = self._master_loop(timed_start, log, start)
         else:
-            res = self._worker_loop(timed_start)
+            res = self._worker_loop(timed_start, start)
         return res
 
     def _timed_fence(self):
@@ -240,7 +245,7 @@ class Trainer:
         self.env.barrier()
         return time.perf_counter()
 
-    def _master_loop(self, timed_start, log) -> TrainResult:
+    def _master_loop(self, timed_start, log, start: int = 0) -> TrainResult:
         cfg, env, sch = self.cfg, self.env, self.scheme
         R, W, K = cfg.num_itrs, cfg.n_workers, self.K
         eta = cfg.eta()
@@ -248,13 +253,16 @@ class Trainer:
         timeset = np.zeros(R)
         loop_time = np.zeros(R)
         worker_timeset = np.zeros((R, W))
-        arrivals_log = []
+        arrivals_log: List = [[] for _ in range(start)]
+        if start:
+            timeset[:start] = self._restored["timeset"]
+            worker_timeset[:start] = self._restored["worker_timeset"]
         timeouts = 0
         t_timed0 = t_timed1 = None
         if cfg.verbose:
             log(sch.banner(cfg.add_delay))
         orig_start = time.perf_counter()
-        for i in range(R):
+        for i in range(start, R):
             if timed_start is not None and i == timed_start:
                 t_timed0 = self._timed_fence()
             if cfg.verbose and i % 10 == 0:
@@ -333,11 +341,11 @@ class Trainer:
         if self.tx is not None:
             self.tx.post_recvs(i, slot, col, self.Rbuf, self.remote_msgs, delays)
 
-    def _worker_loop(self, timed_start) -> None:
+    def _worker_loop(self, timed_start, start: int = 0) -> None:
         cfg, env, tx = self.cfg, self.env, self.tx
         R, K, n = cfg.num_itrs, self.K, self.n_loc
         t0 = None
-        for i in range(R):
+        for i in range(start, R):
             if timed_start is not None and i == timed_start:
                 t0 = self._timed_fence()
             slot = i % K
@@ -360,6 +368,30 @@ class Trainer:
             self.tx = None
 
     # ------------------------------------------------------------------- checkpointing
+    def _restore(self, path: str) -> int:
+        """Resume the master from a checkpoint written by :meth:`_checkpoint`; returns the next round.
+
+        Loaded with ``weights_only=True`` (tensors and plain containers only).  The injected
+        delays are seeded by the round index (utils/delay.py), so a resumed run sees the
+        same straggler pattern as an uninterrupted one.
+        """
+        st = torch.load(path, map_location="cpu", weights_only=True)
+        if st.get("scheme") != self.key:
+            raise ValueError(f"checkpoint {path} is for scheme {st.get('scheme')!r}, not {self.key!r}")
+        nxt = int(st["next_round"])
+        if not 0 < nxt <= self.cfg.num_itrs:
+            raise ValueError(f"checkpoint next_round {nxt} outside (0, {self.cfg.num_itrs}]")
+        ld = self.ld
+        if st["beta"].numel() != ld:
+            raise ValueError("checkpoint beta has a different feature dimension")
+        dev = self.beta.device
+        self.beta.copy_(st["beta"].to(dev))
+        self.u.copy_(st["u"].to(dev))
+        self.hist[:nxt].copy_(st["hist"].to(dev))
+        self.beta_in[nxt].copy_(self.beta.to(self.beta_in.dtype))
+        self._restored = {"timeset": st["timeset"].numpy(), "worker_timeset": st["worker_timeset"].numpy()}
+        return nxt
+
     def _checkpoint(self, next_round: int, timeset, worker_timeset):
         path = self.cfg.checkpoint_path or os.path.join(self.cfg.input_dir, "checkpoint.pt")
         state = {"next_round": next_round, "beta": self.beta.cpu(), "u": self.u.cpu(),

@@ -264,7 +264,9 @@ class IpcTransport(Transport):
 
             mine = attempt(_open)
         allh = env.gather_objects(mine)
-        self.my_row0 = env.broadcast_object(self.row0, 0).get(env.rank, 0)
+        row0, n_rem = env.broadcast_object((self.row0, self.n_rem), 0)
+        self.my_row0 = row0.get(env.rank, 0)
+        self.mbox_rows = max(1, n_rem)  # rows per slot of the master's mailbox ring
         if env.is_master:
             self.inbox_remote = {}
 
@@ -372,7 +374,7 @@ class IpcTransport(Transport):
     def send_msgs(self, i, G_slot):
         slot = i % self.K
         n = G_slot.shape[0]
-        off = ((slot * max(1, self.n_rem)) + self.my_row0) * self.ld * self.es
+        off = (slot * self.mbox_rows + self.my_row0) * self.ld * self.es
         dst = self.rremote.view(self.dname, [n, self.ld], off)
         self.C.put_signal([(G_slot, dst, self.flags.dev_addr(self.env.world + self.env.rank), i + 1)],
                           self.counters)

@@ -1,0 +1,76 @@
+"""Golden-format tests of the reference console output and result files (SURVEY §2.5, §4 layer 6).
+
+Runs the 13-argument CLI end to end on a tiny synthetic dataset written in the reference
+text layout and checks every console line against the reference templates
+(ref src/naive.py:86,93,156,198,209; :407) and the ``%5.3f`` result files (ref src/util.py:32-36).
+"""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from erasurehead_amd.cli import main as cli_main
+from erasurehead_amd.data.synthetic import generate_to_disk, synthetic_dir
+
+LOGISTIC_LINE = re.compile(r"^Iteration (\d+): Train Loss = [ \d.]{5,}, Test Loss = [ \d.]{5,}, AUC = [ \d.]{5,}, "
+                           r"Total time taken =[ \d.]{5,}$")
+LINEAR_LINE = re.compile(r"^Iteration (\d+): Train Loss = \d+\.\d{6}, Test Loss = \d+\.\d{6}, Total time taken =[ \d.]{5,}$")
+
+
+def _data(root, n_procs=5, n=200, d=6, partial=(0, 0, 0)):
+    s, P, part = partial
+    out, parts = synthetic_dir(root, n_procs, n, d, s, P, part)
+    generate_to_disk(n, d, parts, out, rng=np.random.RandomState(0), verbose=False)
+    return out
+
+
+@pytest.mark.parametrize("args,prefix", [
+    (("0", "1", "0", "0", "0"), "naive_acc_"),
+    (("1", "1", "0", "0", "0"), "coded_acc_1_"),
+    (("1", "1", "0", "1", "0"), "replication_acc_1_"),
+    (("1", "1", "0", "2", "0"), "avoidstragg_acc_1_"),
+    (("1", "1", "0", "3", "3"), "replication_acc_1_"),  # AGC collides with replication (ref quirk)
+])
+def test_console_and_files(args, prefix, tmp_path, capsys):
+    root = str(tmp_path) + "/"
+    ddir = _data(root)
+    is_coded, s, P, ver, k = args
+    rc = cli_main(["5", "200", "6", root, "0", "artificial", is_coded, s, P, ver, k, "0", "GD", "--num-itrs", "12",
+                   "--device", "cpu", "--seed", "1"])
+    assert rc == 0
+    lines = capsys.readouterr().out.splitlines()
+    assert lines[0].startswith("---- Starting ")
+    assert lines[1] == "\t >>> At Iteration 0" and "\t >>> At Iteration 10" in lines
+    tot = [l for l in lines if l.startswith("Total Time Elapsed: ")]
+    assert len(tot) == 1 and re.match(r"^Total Time Elapsed: \d+\.\d{3}$", tot[0])
+    its = [l for l in lines if l.startswith("Iteration ")]
+    assert [int(LOGISTIC_LINE.match(l).group(1)) for l in its] == list(range(12))
+    assert lines[-1] == ">>> Done"
+    res = os.path.join(ddir, "results")
+    for kind in ("training_loss", "testing_loss", "auc", "timeset"):
+        body = open(os.path.join(res, prefix + kind + ".dat")).read().splitlines()
+        assert len(body) == 12
+        assert all(re.match(r"^ ?-?\d+\.\d{3} $", l) for l in body), body[:2]
+    wt = np.loadtxt(os.path.join(res, prefix + "worker_timeset.dat"))
+    assert wt.shape == (12, 4)
+
+
+def test_least_squares_console(tmp_path, capsys):
+    root = str(tmp_path) + "/"
+    _data(root)
+    rc = cli_main(["5", "200", "6", root, "0", "artificial", "0", "0", "0", "0", "0", "0", "GD", "--num-itrs", "3",
+                   "--device", "cpu", "--loss", "least_squares", "--lr", "0.01"])
+    assert rc == 0
+    its = [l for l in capsys.readouterr().out.splitlines() if l.startswith("Iteration ")]
+    assert len(its) == 3 and all(LINEAR_LINE.match(l) for l in its), its
+
+
+def test_usage_and_rejections(tmp_path, capsys):
+    assert cli_main(["1", "2"]) == 0
+    assert capsys.readouterr().out.startswith("Usage: python main.py")
+    root = str(tmp_path) + "/"
+    _data(root, n_procs=9)
+    # FRC with W % (s+1) != 0 prints the reference error and exits cleanly
+    assert cli_main(["9", "200", "6", root, "0", "x", "1", "2", "0", "1", "0", "0", "GD", "--device", "cpu"]) == 0
+    assert "Error: n_workers must be multiple of n_stragglers+1!" in capsys.readouterr().out

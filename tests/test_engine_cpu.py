@@ -122,3 +122,44 @@ def test_checkpoint_written(tmp_path):
     st = torch.load(str(tmp_path / "ck.pt"), weights_only=True)
     assert st["next_round"] == 6
     np.testing.assert_allclose(st["hist"].numpy()[:, :17], res.betaset)
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[4]])
+def test_resume_continues_trajectory(case, tmp_path):
+    """Checkpoint at round 3, resume in a fresh trainer: the trajectory equals the replay."""
+    ck = str(tmp_path / "ck.pt")
+    cfg, src, sch, parts = make(case, "AGD", checkpoint_every=3, checkpoint_path=ck)
+    tr = Trainer(cfg, DistEnv(), src, scheme=sch)
+    full = tr.run()
+    st = torch.load(ck, weights_only=True)
+    assert st["next_round"] == 6
+    # rewrite a round-3 checkpoint from the full run and resume from it
+    torch.save({**st, "next_round": 3, "hist": st["hist"][:3],
+                "beta": torch.from_numpy(np.pad(full.betaset[2], (0, tr.ld - tr.d))),
+                "timeset": st["timeset"][:3], "worker_timeset": st["worker_timeset"][:3],
+                "u": _u_after(sch, parts, tr.beta0, full.arrivals[:3], cfg, tr.ld)}, ck)
+    cfg2, src2, sch2, _ = make(case, "AGD", resume=ck)
+    tr2 = Trainer(cfg2, DistEnv(), src2, scheme=sch2)
+    res2 = tr2.run()
+    np.testing.assert_allclose(res2.betaset[:3], full.betaset[:3])
+    arr = full.arrivals[:3] + res2.arrivals[3:]
+    ref = replay(sch, parts, tr.beta0, arr, "AGD", cfg.alpha_value, cfg.n_rows, cfg.eta())
+    np.testing.assert_allclose(res2.betaset, ref, rtol=1e-10, atol=1e-12)
+
+
+def _u_after(sch, parts, beta0, arrivals, cfg, ld):
+    """AGD auxiliary vector u after len(arrivals) rounds (NumPy oracle)."""
+    from erasurehead_amd.codes.schemes import Arrival
+    from erasurehead_amd.models.losses import UpdateRule, worker_grad
+
+    up = UpdateRule("AGD", cfg.alpha_value, cfg.n_rows, sch.grad_scale())
+    beta = np.array(beta0, dtype=np.float64)
+    u = np.zeros_like(beta)
+    for i, arr in enumerate(arrivals):
+        used = sch.decode([Arrival(w, p, t) for (w, p, t) in arr])
+        g = np.zeros_like(beta)
+        for (w, part), c in used.items():
+            m = [x for x in sch.messages if x.worker == w and x.part == part][0]
+            g += c * sum(worker_grad(LOGISTIC, parts[p][0], parts[p][1], beta, coef) for p, coef in m.segments)
+        up.apply(i, 10.0, beta, u, g)
+    return torch.from_numpy(np.pad(u, (0, ld - len(u))))
