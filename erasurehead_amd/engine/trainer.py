@@ -254,6 +254,9 @@ class Trainer:
         loop_time = np.zeros(R)
         worker_timeset = np.zeros((R, W))
         arrivals_log: List = [[] for _ in range(start)]
+        upd_events: List = []
+        delay_table = np.stack([self.delay.delays(i) for i in range(R)]) if R else np.zeros((0, W))
+        views: Dict[Tuple[int, int, int], torch.Tensor] = {}  # (slot, worker, part) -> message row
         if start:
             timeset[:start] = self._restored["timeset"]
             worker_timeset[:start] = self._restored["worker_timeset"]
@@ -272,7 +275,7 @@ class Trainer:
                 col.drain(i - K)  # ring slot reuse: round i-K fully received
             t_start = col.now()
             col.begin_round(i, t_start, self.rule_kind, self.rule_k)
-            delays = self.delay.delays(i)
+            delays = delay_table[i]
             with self.timer.phase("send_beta"):
                 self._send_beta(i)
             with self.timer.phase("local_grad"):
@@ -297,19 +300,28 @@ class Trainer:
                 msgs, coefs = [], []
                 for (w, part), c in sorted(used.items()):
                     key = (w, part)
-                    if key in self.loc_index:
-                        msgs.append(self.G[slot, self.loc_index[key]])
-                    else:
-                        j = self.rem_slot[key]
-                        self.tx.before_read(slot, j)
-                        msgs.append(self.Rbuf[slot, j])
+                    v = views.get((slot, w, part))
+                    if v is None:
+                        v = self.G[slot, self.loc_index[key]] if key in self.loc_index else \
+                            self.Rbuf[slot, self.rem_slot[key]]
+                        views[(slot, w, part)] = v
+                    if key not in self.loc_index:
+                        self.tx.before_read(slot, self.rem_slot[key])
+                    msgs.append(v)
                     coefs.append(c)
                 decay, gm, l2, theta, code = self.update.coeffs(i, float(eta[i]))
+                if env.gpu and not cfg.sync_update:
+                    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    ev0.record(self.cs)
                 combine_update(msgs, coefs, self.beta, self.u, self.d, decay, gm, l2, theta, code,
                                hist=self.hist[i], beta_w=self.beta_in[i + 1])
                 if env.gpu:
-                    self.upd_ev.record(self.cs)
-                    self.upd_ev.synchronize()
+                    if cfg.sync_update:
+                        self.upd_ev.record(self.cs)
+                        self.upd_ev.synchronize()
+                    else:  # no host round trip: the next round's sends are stream-ordered behind it
+                        ev1.record(self.cs)
+                        upd_events.append((i, ev0, ev1))
             timeset[i] = col.now() - t_start
             worker_timeset[i] = sch.worker_times(arrivals)
             arrivals_log.append([(a.worker, a.part, a.t_rel) for a in arrivals])
@@ -321,6 +333,10 @@ class Trainer:
                 self._checkpoint(i + 1, timeset, worker_timeset)
         col.drain(R - 1, max(cfg.round_timeout, 60.0))
         col.close()
+        if upd_events:
+            torch.cuda.synchronize(env.device)
+            for i, ev0, ev1 in upd_events:  # + the update kernel's own duration (reference: decode + update)
+                timeset[i] += 1e-3 * ev0.elapsed_time(ev1)
         if timed_start is not None:
             t_timed1 = self._timed_fence()
         self._sync()
