@@ -14,37 +14,11 @@
 
 #include "runtime/collector.h"
 
-namespace eh {
-hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
-                             int ntasks, const void* beta, void* slab, const int* slot_task_begin,
-                             int nslots, void* part, void* G, int ld, hipStream_t st);
-hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, const void* tasks,
-                                     int ntasks, const void* beta, const int* task_row_off,
-                                     void* rbuf, void* slab, const int* slot_task_begin,
-                                     int nslots, void* part, void* G, int ld, hipStream_t st);
-hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, const int* col_idx,
-                              const void* vals, const void* y, const void* coef,
-                              const void* beta, void* rbuf, long long nrows,
-                              const long long* keys, const int* rows, const void* cvals,
-                              long long nnz, void* G, long long gsize, int ld, hipStream_t st);
-hipError_t eval_gemm_loss_launch(int x_dtype, int loss_kind, const void* X, long long ldx,
-                                 long long n, int d, const void* y, const void* B, int ldb,
-                                 int R, double* loss, void* P, hipStream_t st);
-void bind_ipc(pybind11::module& m);  // csrc/runtime/ipc.cpp
-}  // namespace eh
+#include "kernels/launchers.h"
 
-// Must match csrc/kernels/update.hip
 namespace eh {
-constexpr int kMaxMsgs = 128;
-struct CombineArgs {
-  const void* msg[kMaxMsgs];
-  double coef[kMaxMsgs];
-  int nmsg;
-};
-hipError_t combine_update_launch(const CombineArgs& args, int msg_dtype, int w_dtype,
-                                 double* beta, double* u, double* hist, void* beta_w,
-                                 double* g_out, int d, int ld, double decay, double gm,
-                                 double l2, double theta, int rule, hipStream_t st);
+void bind_ipc(pybind11::module& m);     // csrc/runtime/ipc.cpp
+void bind_engine(pybind11::module& m);  // csrc/runtime/engine.cpp
 }  // namespace eh
 
 namespace {
@@ -226,6 +200,7 @@ void eval_gemm_loss(int64_t loss_kind, const Tensor& X, int64_t n, int64_t d, co
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "ErasureHead MI355X native runtime: gfx950 HIP kernels + arrival collector + IPC mailbox";
   eh::bind_ipc(m);
+  eh::bind_engine(m);
   m.def("grad_dense", &grad_dense);
   m.def("grad_dense_twopass", &grad_dense_twopass);
   m.def("grad_sparse", &grad_sparse);

@@ -1,0 +1,62 @@
+// Host-side launch interface of every gfx950 kernel in csrc/kernels/*.hip.
+//
+// Shared by the Python bindings (csrc/bindings.cpp), the IPC runtime (csrc/runtime/ipc.cpp)
+// and the native round executors (csrc/runtime/engine.cpp).  Every launcher enqueues on
+// the given HIP stream and returns the launch error; shapes are validated by the callers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace eh {
+
+// ---- worker gradient (grad_dense.hip, grad_sparse.hip) -------------------------------
+// dtype: 0 fp64 storage/acc, 1 fp32/fp32, 2 bf16 storage/fp32 acc; loss: 0 logistic, 1 least squares
+hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
+                             int ntasks, const void* beta, void* slab, const int* slot_task_begin,
+                             int nslots, void* part, void* G, int ld, hipStream_t st);
+hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, const void* tasks,
+                                     int ntasks, const void* beta, const int* task_row_off,
+                                     void* rbuf, void* slab, const int* slot_task_begin,
+                                     int nslots, void* part, void* G, int ld, hipStream_t st);
+hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, const int* col_idx,
+                              const void* vals, const void* y, const void* coef,
+                              const void* beta, void* rbuf, long long nrows,
+                              const long long* keys, const int* rows, const void* cvals,
+                              long long nnz, void* G, long long gsize, int ld, hipStream_t st);
+
+// ---- post-hoc evaluation GEMM (eval.hip) -----------------------------------------------
+hipError_t eval_gemm_loss_launch(int x_dtype, int loss_kind, const void* X, long long ldx,
+                                 long long n, int d, const void* y, const void* B, int ldb,
+                                 int R, double* loss, void* P, hipStream_t st);
+
+// ---- master combine + update (update.hip) -----------------------------------------------
+constexpr int kMaxMsgs = 128;
+struct CombineArgs {
+  const void* msg[kMaxMsgs];
+  double coef[kMaxMsgs];
+  int nmsg;
+};
+// msg dtype / worker-beta dtype: 0 fp64, 1 fp32; rule 0 GD, 1 AGD
+hipError_t combine_update_launch(const CombineArgs& args, int msg_dtype, int w_dtype,
+                                 double* beta, double* u, double* hist, void* beta_w,
+                                 double* g_out, int d, int ld, double decay, double gm,
+                                 double l2, double theta, int rule, hipStream_t st);
+
+// ---- IPC mailbox put + signal (transport.hip) -------------------------------------------
+constexpr int kMaxPuts = 16;
+struct PutDesc {
+  const void* src;
+  void* dst;
+  long long bytes;            // multiple of 16
+  unsigned long long* flag;   // device-accessible address of the flag (host-registered shm)
+  unsigned long long value;   // flag value announced once the payload is visible
+  unsigned int* counter;      // per-descriptor block counter (device memory, zero between launches)
+};
+struct PutArgs {
+  PutDesc d[kMaxPuts];
+  int n;
+};
+hipError_t put_signal_launch(const PutArgs& args, int blocks, hipStream_t st);
+hipError_t signal_launch(unsigned long long* flag, unsigned long long value, hipStream_t st);
+
+}  // namespace eh

@@ -14,24 +14,9 @@
 // scope.  So a receiver that observes flag >= value also observes the payload, without
 // relying on kernel-boundary cache semantics across devices.
 #include "common.h"
+#include "launchers.h"
 
 namespace eh {
-
-constexpr int kMaxPuts = 16;
-
-struct PutDesc {
-  const void* src;
-  void* dst;
-  long long bytes;        // multiple of 16
-  unsigned long long* flag;     // device-accessible address of the flag (host-registered shm)
-  unsigned long long value;     // flag value announced once the payload is visible
-  unsigned int* counter;  // per-descriptor block counter (device memory, zero between launches)
-};
-
-struct PutArgs {
-  PutDesc d[kMaxPuts];
-  int n;
-};
 
 __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
   const int k = blockIdx.y;

@@ -16,16 +16,9 @@
 // and writes beta, u, the betaset history row and the worker-dtype copy of beta that
 // the next round's gradient kernels (and the p2p sends) read.
 #include "common.h"
+#include "launchers.h"
 
 namespace eh {
-
-constexpr int kMaxMsgs = 128;
-
-struct CombineArgs {
-  const void* msg[kMaxMsgs];
-  double coef[kMaxMsgs];
-  int nmsg;
-};
 
 template <typename M, typename W>
 __global__ void __launch_bounds__(256)

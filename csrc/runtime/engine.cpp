@@ -1,0 +1,615 @@
+// Native round executors: the master's and the IPC workers' per-round hot loops in C++.
+//
+// Reference loop (every engine, ref src/naive.py:88-150, src/approximate_coding.py:136-207):
+//   master: Isend beta to all -> Waitany until the stop rule -> decode -> GD/AGD update
+//   worker: Wait(beta) -> gradient -> [delay] -> Isend(g)
+// On the MI355X the Python engine (erasurehead_amd/engine/trainer.py) owns setup and
+// bookkeeping, while these executors run the latency-critical part of a round with the
+// GIL released and no per-call Python overhead:
+//
+//  MasterPump::finish(i)  wait for the stop rule (Collector) -> decode on the host
+//                         (plain sum / first arrival per FRC group / cyclic-MDS
+//                         coefficients from a bitmask table) -> combine+update launch
+//                         -> [drain] -> begin(i+1): push beta(i+1) to every worker
+//                         inbox (put+signal), launch the master's own workers'
+//                         gradient, register the round's arrival probes.
+//  WorkerPump::run(a, b)  for each round: spin on the beta round counter, launch the
+//                         gradient of every local logical worker, put+signal the
+//                         messages into the master's mailbox ring.
+//
+// Everything is stream-ordered on the rank's compute stream; the only host waits are the
+// collector's poll and the worker's beta counter.
+#include <c10/hip/HIPStream.h>
+#include <pybind11/stl.h>
+#include <torch/extension.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <tuple>
+#include <vector>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
+#include "kernels/launchers.h"
+#include "runtime/collector.h"
+
+namespace {
+namespace py = pybind11;
+using at::Tensor;
+
+void hcheck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void need(bool ok, const std::string& msg) {
+  if (!ok) throw std::invalid_argument(msg);
+}
+
+int acc_code(const Tensor& t) {
+  if (t.scalar_type() == at::kDouble) return 0;
+  if (t.scalar_type() == at::kFloat) return 1;
+  throw std::invalid_argument("accumulator tensors must be float64 or float32");
+}
+
+void need_gpu(const Tensor& t, const char* name) {
+  need(t.is_cuda() && t.is_contiguous(), std::string(name) + " must be a contiguous GPU tensor");
+}
+
+// ------------------------------------------------------------------------ GradLauncher
+// The per-round gradient launch of one rank's local messages, captured once from the
+// Python plan (ops/grad.py).  The plan object keeps every referenced tensor alive; the
+// launcher also holds references.
+struct GradLauncher {
+  int kind = 0;  // 0 dense fused, 1 dense two-pass, 2 sparse
+  int dtype = 0, loss = 0, cpl = 0, ntasks = 0, nslots = 0, ld = 0;
+  const void* segs = nullptr;
+  const void* tasks = nullptr;
+  void* slab = nullptr;
+  const int* stb = nullptr;
+  void* part = nullptr;
+  const int* task_row_off = nullptr;
+  void* rbuf = nullptr;
+  const long long* row_ptr = nullptr;
+  const int* col_idx = nullptr;
+  const void* vals = nullptr;
+  const void* y = nullptr;
+  const void* coef = nullptr;
+  long long nrows = 0;
+  const long long* keys = nullptr;
+  const int* rows = nullptr;
+  const void* cvals = nullptr;
+  long long nnz = 0;
+  int acc = 0;
+  std::vector<Tensor> keep;
+
+  hipError_t launch(const void* beta, void* G, hipStream_t st) const {
+    switch (kind) {
+      case 0:
+        return ntasks ? eh::grad_dense_launch(dtype, loss, cpl, segs, tasks, ntasks, beta, slab, stb, nslots, part, G,
+                                              ld, st)
+                      : hipSuccess;
+      case 1:
+        return ntasks ? eh::grad_dense_twopass_launch(dtype, loss, segs, tasks, ntasks, beta, task_row_off, rbuf, slab,
+                                                      stb, nslots, part, G, ld, st)
+                      : hipSuccess;
+      case 2:
+        return eh::grad_sparse_launch(acc, loss, row_ptr, col_idx, vals, y, coef, beta, rbuf, nrows, keys, rows,
+                                      cvals, nnz, G, static_cast<long long>(nslots) * ld, ld, st);
+      default:
+        return hipErrorInvalidValue;
+    }
+  }
+};
+
+std::shared_ptr<GradLauncher> make_dense(int64_t dtype, int64_t loss, int64_t cpl, const Tensor& segs,
+                                         const Tensor& tasks, const Tensor& slab, const Tensor& stb,
+                                         const Tensor& part, int64_t ld, std::optional<Tensor> task_row_off,
+                                         std::optional<Tensor> rbuf) {
+  for (auto* t : {&segs, &tasks, &slab, &stb, &part}) need_gpu(*t, "dense plan operand");
+  need(tasks.dim() == 2 && tasks.size(1) == 4 && tasks.scalar_type() == at::kInt, "tasks must be int32 [n,4]");
+  need(stb.scalar_type() == at::kInt, "slot_task_begin must be int32");
+  auto g = std::make_shared<GradLauncher>();
+  g->dtype = (int)dtype;
+  g->loss = (int)loss;
+  g->cpl = (int)cpl;
+  g->ld = (int)ld;
+  g->ntasks = (int)tasks.size(0);
+  g->nslots = (int)stb.numel() - 1;
+  g->segs = segs.data_ptr();
+  g->tasks = tasks.data_ptr();
+  g->slab = slab.data_ptr();
+  g->stb = stb.data_ptr<int>();
+  g->part = part.data_ptr();
+  g->keep = {segs, tasks, slab, stb, part};
+  g->acc = dtype == 0 ? 0 : 1;
+  if (task_row_off) {
+    need(rbuf.has_value(), "two-pass plan needs rbuf");
+    need_gpu(*task_row_off, "task_row_off");
+    need_gpu(*rbuf, "rbuf");
+    g->kind = 1;
+    g->task_row_off = task_row_off->data_ptr<int>();
+    g->rbuf = rbuf->data_ptr();
+    g->keep.push_back(*task_row_off);
+    g->keep.push_back(*rbuf);
+  } else {
+    need(cpl * 64 >= ld, "cpl * 64 must cover ld");
+    g->kind = 0;
+  }
+  return g;
+}
+
+std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& row_ptr, const Tensor& col_idx,
+                                          std::optional<Tensor> vals, const Tensor& y, const Tensor& coef,
+                                          const Tensor& rbuf, const Tensor& keys, const Tensor& rows,
+                                          std::optional<Tensor> cvals, int64_t nslots, int64_t ld) {
+  for (auto* t : {&row_ptr, &col_idx, &y, &coef, &rbuf, &keys, &rows}) need_gpu(*t, "sparse plan operand");
+  need(row_ptr.scalar_type() == at::kLong && keys.scalar_type() == at::kLong, "row_ptr/keys must be int64");
+  auto g = std::make_shared<GradLauncher>();
+  g->kind = 2;
+  g->loss = (int)loss;
+  g->acc = acc_code(y);
+  g->ld = (int)ld;
+  g->nslots = (int)nslots;
+  g->row_ptr = (const long long*)row_ptr.data_ptr<int64_t>();
+  g->col_idx = col_idx.data_ptr<int>();
+  g->vals = vals ? vals->data_ptr() : nullptr;
+  g->y = y.data_ptr();
+  g->coef = coef.data_ptr();
+  g->rbuf = rbuf.data_ptr();
+  g->nrows = row_ptr.numel() - 1;
+  g->keys = (const long long*)keys.data_ptr<int64_t>();
+  g->rows = rows.data_ptr<int>();
+  g->cvals = cvals ? cvals->data_ptr() : nullptr;
+  g->nnz = keys.numel();
+  g->keep = {row_ptr, col_idx, y, coef, rbuf, keys, rows};
+  if (vals) g->keep.push_back(*vals);
+  if (cvals) g->keep.push_back(*cvals);
+  return g;
+}
+
+// Decode kinds (codes/schemes.py)
+enum DecodeKind : int {
+  kSumPart0 = 0,       // naive, avoidstragg: every arrived main message, coefficient 1
+  kFirstPerGroup = 1,  // FRC / AGC: first arrival of each group
+  kPartialFrc = 2,     // partial replication: all first parts + first second part per group
+  kTable = 3,          // cyclic MDS: coefficients from the completion-bitmask table
+  kPartialTable = 4,   // partial coded: all first parts + table-decoded coded parts
+};
+
+// ------------------------------------------------------------------------- MasterPump
+class MasterPump {
+ public:
+  MasterPump(eh::Collector* col, int W, int R, int K, int d, int ld, int device, double timeout)
+      : col_(col), W_(W), R_(R), K_(K), d_(d), ld_(ld), device_(device), timeout_(timeout) {
+    need(col != nullptr, "collector required");
+    need(W > 0 && R > 0 && K > 0 && ld >= d && d > 0, "bad pump dimensions");
+    stream_ = c10::hip::getCurrentHIPStream(device).stream();
+    t_start_.assign(R, 0.0);
+    upd_ev_.assign(R, {nullptr, nullptr});
+    loc_ev_.assign(K, nullptr);
+    for (auto& e : loc_ev_) hcheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    index_.assign(2 * W, {-1, -1});
+  }
+  ~MasterPump() {
+    for (auto e : loc_ev_)
+      if (e) hipEventDestroy(e);
+    for (auto& p : upd_ev_) {
+      if (p.first) hipEventDestroy(p.first);
+      if (p.second) hipEventDestroy(p.second);
+    }
+  }
+
+  void set_state(const Tensor& beta, const Tensor& u, const Tensor& hist, const Tensor& beta_in) {
+    need_gpu(beta, "beta");
+    need_gpu(u, "u");
+    need_gpu(hist, "hist");
+    need_gpu(beta_in, "beta_in");
+    need(beta.scalar_type() == at::kDouble && u.scalar_type() == at::kDouble && hist.scalar_type() == at::kDouble,
+         "beta/u/hist must be float64");
+    need(beta.numel() == ld_ && u.numel() == ld_, "beta/u must have ld elements");
+    need(hist.dim() == 2 && hist.size(0) >= R_ && hist.size(1) == ld_, "hist must be [R, ld]");
+    need(beta_in.dim() == 2 && beta_in.size(0) >= R_ + 1 && beta_in.size(1) == ld_, "beta_in must be [R+1, ld]");
+    beta_ = beta;
+    u_ = u;
+    hist_ = hist;
+    beta_in_ = beta_in;
+    acc_ = acc_code(beta_in);
+    es_ = acc_ == 0 ? 8 : 4;
+  }
+
+  // local messages: row order of G ([K, n_loc, ld]); each (worker, part)
+  void set_local(std::shared_ptr<GradLauncher> g, const Tensor& G, const std::vector<std::pair<int, int>>& msgs) {
+    need_gpu(G, "G");
+    need(G.dim() == 3 && G.size(0) == K_ && G.size(2) == ld_, "G must be [K, n_loc, ld]");
+    need(acc_code(G) == acc_, "G dtype must match beta_in");
+    need((int64_t)msgs.size() <= G.size(1), "more local messages than G rows");
+    launcher_ = std::move(g);
+    G_ = G;
+    n_loc_ = (int)msgs.size();
+    g_rows_ = (int)G.size(1);
+    local_.clear();
+    for (int j = 0; j < n_loc_; ++j) {
+      check_wp(msgs[j].first, msgs[j].second);
+      local_.push_back({msgs[j].first, msgs[j].second, j, 0});
+      index_[2 * msgs[j].first + msgs[j].second] = {0, j};
+    }
+  }
+
+  // remote messages: (worker, part, mailbox row, host address of the sender's round counter)
+  void set_remote(const Tensor& rbuf, const std::vector<std::tuple<int, int, int, uintptr_t>>& msgs) {
+    need_gpu(rbuf, "rbuf");
+    need(rbuf.dim() == 3 && rbuf.size(0) == K_ && rbuf.size(2) == ld_, "rbuf must be [K, rows, ld]");
+    need(acc_code(rbuf) == acc_, "rbuf dtype must match beta_in");
+    rbuf_ = rbuf;
+    r_rows_ = (int)rbuf.size(1);
+    remote_.clear();
+    for (const auto& [w, p, row, addr] : msgs) {
+      check_wp(w, p);
+      need(row >= 0 && row < r_rows_, "mailbox row out of range");
+      need(addr != 0, "null flag address");
+      remote_.push_back({w, p, row, addr});
+      index_[2 * w + p] = {1, row};
+    }
+  }
+
+  // beta pushes: (inbox base device pointer [R+1, ld], flag device address) per worker rank
+  void set_puts(const std::vector<std::pair<uintptr_t, uintptr_t>>& targets, const Tensor& counters) {
+    need(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.numel() >= (int64_t)targets.size(),
+         "counters must be int32 GPU [>= n targets]");
+    for (const auto& t : targets) need(t.first != 0 && t.second != 0, "null put target");
+    targets_ = targets;
+    counters_ = counters;
+  }
+
+  void set_schedule(const std::vector<double>& decay, const std::vector<double>& gm, const std::vector<double>& l2,
+                    const std::vector<double>& theta, int update_rule, const std::vector<double>& delays, int stop_rule,
+                    int k, bool drain) {
+    need((int)decay.size() >= R_ && (int)gm.size() >= R_ && (int)l2.size() >= R_ && (int)theta.size() >= R_,
+         "schedule arrays must cover R rounds");
+    need((int64_t)delays.size() >= (int64_t)R_ * W_, "delays must be [R*W]");
+    decay_ = decay;
+    gm_ = gm;
+    l2_ = l2;
+    theta_ = theta;
+    update_rule_ = update_rule;
+    delays_ = delays;
+    stop_rule_ = stop_rule;
+    k_ = k;
+    drain_ = drain;
+  }
+
+  void set_decode(int kind, const std::vector<int>& group_of, int n_groups) {
+    need((int)group_of.size() == W_, "group_of must have W entries");
+    decode_kind_ = kind;
+    group_of_ = group_of;
+    n_groups_ = n_groups;
+  }
+  void add_table(uint64_t mask, const std::vector<double>& coefs) {
+    need((int)coefs.size() == W_, "table row must have W coefficients");
+    table_[mask] = coefs;
+  }
+
+  // ---- round execution ---------------------------------------------------------------
+  void begin(int i) {
+    need(i >= 0 && i < R_, "round out of range");
+    need(beta_in_.defined(), "set_state first");
+    const int slot = i % K_;
+    if (i >= K_) col_->drain(i - K_, timeout_);  // the ring slot's previous round fully received
+    const double t = eh::Collector::now();
+    col_->begin_round(i, t, stop_rule_, k_);
+    t_start_[i] = t;
+    char* bin = static_cast<char*>(beta_in_.data_ptr());
+    const void* src = bin + static_cast<int64_t>(i) * ld_ * es_;
+    // push beta(i) into every worker inbox
+    for (size_t k0 = 0; k0 < targets_.size(); k0 += eh::kMaxPuts) {
+      eh::PutArgs a{};
+      a.n = 0;
+      for (size_t k = k0; k < targets_.size() && a.n < eh::kMaxPuts; ++k) {
+        a.d[a.n] = eh::PutDesc{src, reinterpret_cast<char*>(targets_[k].first) + static_cast<int64_t>(i) * ld_ * es_,
+                               static_cast<long long>(ld_) * es_,
+                               reinterpret_cast<unsigned long long*>(targets_[k].second),
+                               static_cast<unsigned long long>(i + 1),
+                               reinterpret_cast<unsigned int*>(counters_.data_ptr<int>()) + k};
+        ++a.n;
+      }
+      hcheck(eh::put_signal_launch(a, blocks_for(static_cast<long long>(ld_) * es_), stream_), "put_signal(beta)");
+    }
+    const double* dl = delays_.data() + static_cast<int64_t>(i) * W_;
+    if (n_loc_ > 0 && launcher_) {
+      char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
+      hcheck(launcher_->launch(src, g, stream_), "local gradient");
+      hcheck(hipEventRecord(loc_ev_[slot], stream_), "hipEventRecord");
+      for (const auto& m : local_)
+        col_->add_event_probe(m.w, m.p, i, reinterpret_cast<uintptr_t>(loc_ev_[slot]), dl[m.w]);
+    }
+    for (const auto& m : remote_)
+      col_->add_flag_probe(m.w, m.p, i, m.flag, static_cast<uint64_t>(i + 1), dl[m.w]);
+  }
+
+  // Returns (status, arrivals [(worker, part, t_rel)], t_start, t_decoded, t_end):
+  // status 0 ok, 1 timeout (decoded with what arrived), 2 host decode needed (no table
+  // row: call resolve()).
+  py::tuple finish(int i, bool publish_next) {
+    int status;
+    std::vector<eh::Arrival> arr;
+    double t_dec = 0, t_end = 0;
+    {
+      py::gil_scoped_release nogil;
+      const bool ok = col_->wait(timeout_);
+      arr = col_->arrivals();
+      std::vector<std::pair<const void*, double>> used;
+      const bool decoded = decode(i, arr, used);
+      if (!decoded) {
+        status = 2;
+      } else {
+        status = ok ? 0 : 1;
+        combine(i, used);
+        t_dec = eh::Collector::now();
+        t_end = after_combine(i, publish_next);
+      }
+    }
+    return pack(status, arr, i, t_dec, t_end);
+  }
+
+  // Host-decoded fallback: coefs[(w, part)] for the given arrivals.
+  py::tuple resolve(int i, const std::vector<std::tuple<int, int, double>>& coefs, bool publish_next) {
+    std::vector<eh::Arrival> arr = col_->arrivals();
+    double t_dec, t_end;
+    {
+      py::gil_scoped_release nogil;
+      std::vector<std::pair<const void*, double>> used;
+      for (const auto& [w, p, c] : coefs) used.push_back({msg_ptr(i % K_, w, p), c});
+      combine(i, used);
+      t_dec = eh::Collector::now();
+      t_end = after_combine(i, publish_next);
+    }
+    return pack(0, arr, i, t_dec, t_end);
+  }
+
+  // Update-kernel durations (ms) of every round run so far (host sync).
+  std::vector<double> update_ms() {
+    hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    std::vector<double> out(R_, 0.0);
+    for (int i = 0; i < R_; ++i) {
+      auto& p = upd_ev_[i];
+      if (p.first && p.second) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) out[i] = ms;
+      }
+    }
+    return out;
+  }
+
+ private:
+  struct Msg {
+    int w, p, row;
+    uintptr_t flag;
+  };
+
+  void check_wp(int w, int p) const { need(w >= 0 && w < W_ && (p == 0 || p == 1), "bad (worker, part)"); }
+
+  static int blocks_for(long long bytes) {
+    const long long v = bytes / 16;
+    return (int)std::max<long long>(1, std::min<long long>(64, (v + 4095) / 4096));
+  }
+
+  const void* msg_ptr(int slot, int w, int p) const {
+    const auto& ix = index_[2 * w + p];
+    if (ix.first == 0)
+      return static_cast<const char*>(G_.data_ptr()) + (static_cast<int64_t>(slot) * g_rows_ + ix.second) * ld_ * es_;
+    if (ix.first == 1)
+      return static_cast<const char*>(rbuf_.data_ptr()) + (static_cast<int64_t>(slot) * r_rows_ + ix.second) * ld_ * es_;
+    throw std::logic_error("message without a buffer");
+  }
+
+  bool decode(int i, const std::vector<eh::Arrival>& arr, std::vector<std::pair<const void*, double>>& used) const {
+    const int slot = i % K_;
+    std::vector<char> gdone(std::max(n_groups_, 1), 0);
+    uint64_t mask = 0;
+    for (const auto& a : arr) {
+      if (a.part == 1) {
+        if (decode_kind_ == kPartialFrc || decode_kind_ == kPartialTable) used.push_back({msg_ptr(slot, a.worker, 1), 1.0});
+        continue;
+      }
+      switch (decode_kind_) {
+        case kSumPart0:
+          used.push_back({msg_ptr(slot, a.worker, 0), 1.0});
+          break;
+        case kFirstPerGroup:
+        case kPartialFrc: {
+          const int g = group_of_[a.worker];
+          if (!gdone[g]) {
+            gdone[g] = 1;
+            used.push_back({msg_ptr(slot, a.worker, 0), 1.0});
+          }
+          break;
+        }
+        default:
+          mask |= (uint64_t)1 << a.worker;
+      }
+    }
+    if (decode_kind_ == kTable || decode_kind_ == kPartialTable) {
+      auto it = table_.find(mask);
+      if (it == table_.end()) return false;
+      for (int w = 0; w < W_; ++w)
+        if (mask >> w & 1) used.push_back({msg_ptr(slot, w, 0), it->second[w]});
+    }
+    return true;
+  }
+
+  void combine(int i, const std::vector<std::pair<const void*, double>>& used) {
+    need((int)used.size() <= eh::kMaxMsgs, "too many messages for one combine");
+    eh::CombineArgs a{};
+    a.nmsg = (int)used.size();
+    for (int m = 0; m < a.nmsg; ++m) {
+      a.msg[m] = used[m].first;
+      a.coef[m] = used[m].second;
+    }
+    auto& ev = upd_ev_[i];
+    if (!ev.first) hcheck(hipEventCreate(&ev.first), "hipEventCreate");
+    if (!ev.second) hcheck(hipEventCreate(&ev.second), "hipEventCreate");
+    hcheck(hipEventRecord(ev.first, stream_), "hipEventRecord");
+    char* bin = static_cast<char*>(beta_in_.data_ptr());
+    hcheck(eh::combine_update_launch(a, acc_, acc_, beta_.data_ptr<double>(), u_.data_ptr<double>(),
+                                     hist_.data_ptr<double>() + static_cast<int64_t>(i) * ld_,
+                                     bin + static_cast<int64_t>(i + 1) * ld_ * es_, nullptr, d_, ld_, decay_[i], gm_[i],
+                                     l2_[i], theta_[i], update_rule_, stream_),
+           "combine_update");
+    hcheck(hipEventRecord(ev.second, stream_), "hipEventRecord");
+  }
+
+  double after_combine(int i, bool publish_next) {
+    if (drain_) col_->drain(i, timeout_);
+    const double t_end = eh::Collector::now();
+    if (publish_next && i + 1 < R_) begin(i + 1);
+    return t_end;
+  }
+
+  py::tuple pack(int status, const std::vector<eh::Arrival>& arr, int i, double t_dec, double t_end) const {
+    py::list lst;
+    for (const auto& a : arr) lst.append(py::make_tuple(a.worker, a.part, a.t_rel));
+    return py::make_tuple(status, lst, t_start_[i], t_dec, t_end);
+  }
+
+  eh::Collector* col_;
+  int W_, R_, K_, d_, ld_, device_;
+  double timeout_;
+  hipStream_t stream_ = nullptr;
+  int acc_ = 0, es_ = 8;
+  Tensor beta_, u_, hist_, beta_in_, G_, rbuf_, counters_;
+  std::shared_ptr<GradLauncher> launcher_;
+  int n_loc_ = 0, g_rows_ = 1, r_rows_ = 1;
+  std::vector<Msg> local_, remote_;
+  std::vector<std::pair<int, int>> index_;  // [2*w+p] -> (0 local | 1 remote, row)
+  std::vector<std::pair<uintptr_t, uintptr_t>> targets_;
+  std::vector<double> decay_, gm_, l2_, theta_, delays_;
+  int update_rule_ = 0, stop_rule_ = 0, k_ = 0;
+  bool drain_ = false;
+  int decode_kind_ = kSumPart0, n_groups_ = 1;
+  std::vector<int> group_of_;
+  std::map<uint64_t, std::vector<double>> table_;
+  std::vector<double> t_start_;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> upd_ev_;
+  std::vector<hipEvent_t> loc_ev_;
+};
+
+// ------------------------------------------------------------------------- WorkerPump
+class WorkerPump {
+ public:
+  WorkerPump(std::shared_ptr<GradLauncher> g, const Tensor& inbox, const Tensor& G, int n_loc, uintptr_t mbox_base,
+             int mbox_rows, int row0, uintptr_t beta_flag_host, uintptr_t msg_flag_dev, const Tensor& counters,
+             int K, int device, double timeout)
+      : g_(std::move(g)), inbox_(inbox), G_(G), n_(n_loc), mbox_(mbox_base), mbox_rows_(mbox_rows), row0_(row0),
+        bflag_(reinterpret_cast<const uint64_t*>(beta_flag_host)),
+        mflag_(reinterpret_cast<unsigned long long*>(msg_flag_dev)), counters_(counters), K_(K), timeout_(timeout) {
+    need_gpu(inbox, "inbox");
+    need_gpu(G, "G");
+    need(G.dim() == 3 && G.size(0) == K && G.size(2) == inbox.size(1), "G must be [K, n, ld]");
+    need(acc_code(G) == acc_code(inbox), "G/inbox dtype mismatch");
+    need(n_loc >= 0 && n_loc <= G.size(1), "n_loc out of range");
+    need(row0 >= 0 && row0 + n_loc <= mbox_rows, "mailbox rows out of range");
+    need(beta_flag_host != 0 && msg_flag_dev != 0 && mbox_base != 0, "null address");
+    need(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.numel() >= 1, "counters");
+    ld_ = (int)inbox.size(1);
+    R_ = (int)inbox.size(0) - 1;
+    es_ = acc_code(G) == 0 ? 8 : 4;
+    g_rows_ = (int)G.size(1);
+    stream_ = c10::hip::getCurrentHIPStream(device).stream();
+  }
+
+  // Rounds [a, b).  Returns -1 when every round was issued, else the round whose beta
+  // did not arrive within the timeout.
+  int run(int a, int b) {
+    py::gil_scoped_release nogil;
+    using clk = std::chrono::steady_clock;
+    for (int i = a; i < b; ++i) {
+      need(i >= 0 && i < R_, "round out of range");
+      const auto t0 = clk::now();
+      for (int spin = 0; __atomic_load_n(bflag_, __ATOMIC_ACQUIRE) < static_cast<uint64_t>(i + 1); ++spin) {
+        if (spin < 4096) {
+#if defined(__x86_64__)
+          _mm_pause();
+#endif
+          continue;
+        }
+        if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_) return i;
+        std::this_thread::sleep_for(std::chrono::microseconds(5));
+      }
+      if (n_ == 0) continue;
+      const int slot = i % K_;
+      const char* beta = static_cast<const char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * ld_ * es_;
+      char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
+      hcheck(g_->launch(beta, g, stream_), "worker gradient");
+      eh::PutArgs pa{};
+      pa.n = 1;
+      const long long bytes = static_cast<long long>(n_) * ld_ * es_;
+      pa.d[0] = eh::PutDesc{g, reinterpret_cast<char*>(mbox_) + (static_cast<int64_t>(slot) * mbox_rows_ + row0_) * ld_ * es_,
+                            bytes, mflag_, static_cast<unsigned long long>(i + 1),
+                            reinterpret_cast<unsigned int*>(counters_.data_ptr<int>())};
+      const int blocks = (int)std::max<long long>(1, std::min<long long>(64, (bytes / 16 + 4095) / 4096));
+      hcheck(eh::put_signal_launch(pa, blocks, stream_), "put_signal(messages)");
+    }
+    return -1;
+  }
+
+ private:
+  std::shared_ptr<GradLauncher> g_;
+  Tensor inbox_, G_;
+  int n_;
+  uintptr_t mbox_;
+  int mbox_rows_, row0_;
+  const uint64_t* bflag_;
+  unsigned long long* mflag_;
+  Tensor counters_;
+  int K_;
+  double timeout_;
+  int ld_ = 0, R_ = 0, es_ = 8, g_rows_ = 1;
+  hipStream_t stream_ = nullptr;
+};
+
+}  // namespace
+
+namespace eh {
+void bind_engine(py::module& m) {
+  py::class_<GradLauncher, std::shared_ptr<GradLauncher>>(m, "GradLauncher")
+      .def_static("dense", &make_dense, py::arg("dtype"), py::arg("loss"), py::arg("cpl"), py::arg("segs"),
+                  py::arg("tasks"), py::arg("slab"), py::arg("slot_task_begin"), py::arg("part"), py::arg("ld"),
+                  py::arg("task_row_off") = py::none(), py::arg("rbuf") = py::none())
+      .def_static("sparse", &make_sparse, py::arg("loss"), py::arg("row_ptr"), py::arg("col_idx"), py::arg("vals"),
+                  py::arg("y"), py::arg("coef"), py::arg("rbuf"), py::arg("keys"), py::arg("rows"), py::arg("cvals"),
+                  py::arg("nslots"), py::arg("ld"))
+      .def("launch", [](const GradLauncher& g, const Tensor& beta, const Tensor& G) {
+        need_gpu(beta, "beta");
+        need_gpu(G, "G");
+        hcheck(g.launch(beta.data_ptr(), G.data_ptr(), c10::hip::getCurrentHIPStream(G.device().index()).stream()),
+               "GradLauncher.launch");
+      });
+  py::class_<MasterPump>(m, "MasterPump")
+      .def(py::init<eh::Collector*, int, int, int, int, int, int, double>(), py::arg("collector"), py::arg("W"),
+           py::arg("R"), py::arg("K"), py::arg("d"), py::arg("ld"), py::arg("device"), py::arg("timeout"),
+           py::keep_alive<1, 2>())
+      .def("set_state", &MasterPump::set_state)
+      .def("set_local", &MasterPump::set_local)
+      .def("set_remote", &MasterPump::set_remote)
+      .def("set_puts", &MasterPump::set_puts)
+      .def("set_schedule", &MasterPump::set_schedule)
+      .def("set_decode", &MasterPump::set_decode)
+      .def("add_table", &MasterPump::add_table)
+      .def("begin", &MasterPump::begin, py::call_guard<py::gil_scoped_release>())
+      .def("finish", &MasterPump::finish)
+      .def("resolve", &MasterPump::resolve)
+      .def("update_ms", &MasterPump::update_ms);
+  py::class_<WorkerPump>(m, "WorkerPump")
+      .def(py::init<std::shared_ptr<GradLauncher>, const Tensor&, const Tensor&, int, uintptr_t, int, int, uintptr_t,
+                    uintptr_t, const Tensor&, int, int, double>())
+      .def("run", &WorkerPump::run);
+}
+}  // namespace eh

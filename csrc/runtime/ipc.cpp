@@ -32,23 +32,7 @@
 #include <immintrin.h>
 #endif
 
-namespace eh {
-constexpr int kMaxPuts = 16;
-struct PutDesc {
-  const void* src;
-  void* dst;
-  long long bytes;
-  unsigned long long* flag;
-  unsigned long long value;
-  unsigned int* counter;
-};
-struct PutArgs {
-  PutDesc d[kMaxPuts];
-  int n;
-};
-hipError_t put_signal_launch(const PutArgs& args, int blocks, hipStream_t st);
-hipError_t signal_launch(unsigned long long* flag, unsigned long long value, hipStream_t st);
-}  // namespace eh
+#include "kernels/launchers.h"
 
 namespace {
 namespace py = pybind11;

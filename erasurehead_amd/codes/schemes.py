@@ -28,6 +28,8 @@ from .cyclic import DecodeCache, make_cyclic_B
 
 # stop-rule kinds (must match csrc/runtime/collector.h)
 RULE_ALL, RULE_COUNT, RULE_FRC, RULE_PARTIAL_FRC, RULE_PARTIAL_COUNT = range(5)
+# host decode kinds of the native master executor (must match csrc/runtime/engine.cpp DecodeKind)
+DEC_SUM, DEC_FIRST_PER_GROUP, DEC_PARTIAL_FRC, DEC_TABLE, DEC_PARTIAL_TABLE = range(5)
 
 
 class SchemeError(ValueError):
@@ -70,6 +72,7 @@ class Scheme:
     fixed_agd = False  # reference hard-codes AGD regardless of the CLI update rule
     has_linear = False  # reference has a least-squares variant
     needs_B = False
+    decode_kind = DEC_SUM
 
     def __post_init__(self):
         if self.n_workers < 1:
@@ -141,6 +144,24 @@ class Scheme:
     def describe(self) -> str:
         return f"{self.key}(W={self.n_workers}, s={self.n_stragglers})"
 
+    def decode_table(self) -> Dict[int, np.ndarray]:
+        """Completion bitmask -> W decode coefficients (table-decoded schemes only).
+
+        Every pattern the stop rule can produce on time (exactly W - s completed main
+        messages) is solved up front in fp64 (the reference's getA, ref src/util.py:85-103);
+        any other pattern (a round that timed out) is solved on demand by :meth:`decode`.
+        """
+        import itertools
+
+        W, s = self.n_workers, self.n_stragglers
+        out = {}
+        for done in itertools.combinations(range(W), W - s):
+            mask = 0
+            for w in done:
+                mask |= 1 << w
+            out[mask] = self._decoder(done)
+        return out
+
 
 def _names(prefix: str, train_prefix: Optional[str] = None) -> Dict[str, str]:
     return {
@@ -181,6 +202,7 @@ class Cyclic(Scheme):
 
     init_zero = True
     needs_B = True
+    decode_kind = DEC_TABLE
 
     def _build(self):
         self._check_s()
@@ -229,6 +251,7 @@ class FRC(Scheme):
     drain = True
     has_linear = True
     approx = False
+    decode_kind = DEC_FIRST_PER_GROUP
 
     def _build(self):
         self._check_s()
@@ -351,6 +374,8 @@ class _Partial(Scheme):
 class PartialReplication(_Partial):
     """ref src/partial_replication.py:11-286 (first part all W + FRC second part)."""
 
+    decode_kind = DEC_PARTIAL_FRC
+
     def _build(self):
         self._check()
         W, s = self.n_workers, self.n_stragglers
@@ -395,6 +420,7 @@ class PartialCoded(_Partial):
     """ref src/partial_coded.py:12-293 (first part all W + cyclic-coded second part)."""
 
     needs_B = True
+    decode_kind = DEC_PARTIAL_TABLE
 
     def _build(self):
         self._check()

@@ -35,7 +35,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ..codes.schemes import Scheme, SchemeError, make_scheme, scheme_key
+from .._ext import native as native_ext
+from ..codes.schemes import Arrival, Scheme, SchemeError, make_scheme, scheme_key
 from ..config import RunConfig
 from ..data import io as dio
 from ..data.source import DataSource, FileSource, SyntheticSource
@@ -234,11 +235,21 @@ class Trainer:
                     log(line)
         start = env.broadcast_object(start, 0)
         env.barrier()
+        native_loop = self.native_loop
         if env.is_master:
-            res = self._master_loop(timed_start, log, start)
+            res = (self._master_loop_native if native_loop else self._master_loop)(timed_start, log, start)
         else:
-            res = self._worker_loop(timed_start, start)
+            res = (self._worker_loop_native if native_loop else self._worker_loop)(timed_start, start)
         return res
+
+    @property
+    def native_loop(self) -> bool:
+        """Run rounds in the C++ executors (GPU; single process or the IPC transport)."""
+        if not (self.env.gpu and self.cfg.native_loop):
+            return False
+        if self.tx is not None and self.tx.name != "ipc":
+            return False
+        return self.n_loc > 0 or self.env.is_master
 
     def _timed_fence(self):
         self._sync()
@@ -348,6 +359,114 @@ class Trainer:
             res.timed_seconds = t_timed1 - t_timed0
             res.timed_rounds = R - timed_start
         return res
+
+    def _master_loop_native(self, timed_start, log, start: int = 0) -> TrainResult:
+        """Master rounds in csrc/runtime/engine.cpp (MasterPump); Python only keeps the books."""
+        cfg, env, sch = self.cfg, self.env, self.scheme
+        R, W, K = cfg.num_itrs, cfg.n_workers, self.K
+        C = native_ext()
+        col = ArrivalCollector(W, sch.group_of, sch.n_groups, True)
+        dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
+        pump = C.MasterPump(col.c, W, R, K, self.d, self.ld, dev, float(cfg.round_timeout))
+        pump.set_state(self.beta, self.u, self.hist, self.beta_in)
+        if self.local_msgs:
+            pump.set_local(self.plan.native_launcher(), self.G, [(m.worker, m.part) for m in self.local_msgs])
+        tx = self.tx
+        if tx is not None:
+            rem = [(m.worker, m.part, self.rem_slot[(m.worker, m.part)], tx.flags.host_addr(env.world + r))
+                   for r in sorted(self.remote_msgs) for m in self.remote_msgs[r]]
+            pump.set_remote(self.Rbuf, rem)
+            pump.set_puts([(tx.inbox_remote[r].data_ptr(), tx.flags.dev_addr(r)) for r in range(1, env.world)],
+                          tx.counters)
+        eta = cfg.eta()
+        co = [self.update.coeffs(i, float(eta[i])) for i in range(R)]
+        delay_table = np.stack([self.delay.delays(i) for i in range(R)])
+        pump.set_schedule([c[0] for c in co], [c[1] for c in co], [c[2] for c in co], [c[3] for c in co],
+                          co[0][4] if co else 0, [float(x) for x in delay_table.ravel()], self.rule_kind,
+                          self.rule_k, bool(self.drain))
+        pump.set_decode(sch.decode_kind, list(sch.group_of), sch.n_groups)
+        if sch.decode_kind in (3, 4):
+            for mask, a in sch.decode_table().items():
+                pump.add_table(mask, [float(x) for x in a])
+        timeset, loop_time, worker_timeset = np.zeros(R), np.zeros(R), np.zeros((R, W))
+        arrivals_log: List = [[] for _ in range(start)]
+        if start:
+            timeset[:start] = self._restored["timeset"]
+            worker_timeset[:start] = self._restored["worker_timeset"]
+        timeouts = 0
+        t_timed0 = t_timed1 = None
+        if cfg.verbose:
+            log(sch.banner(cfg.add_delay))
+        orig_start = time.perf_counter()
+        begun = False
+        for i in range(start, R):
+            if not begun:
+                if timed_start is not None and i == timed_start:
+                    t_timed0 = self._timed_fence()
+                pump.begin(i)
+            if cfg.verbose and i % 10 == 0:
+                log(report.iteration_tick(i))
+            fence_next = timed_start is not None and i + 1 == timed_start
+            publish = i + 1 < R and not fence_next
+            status, arr, t0, tdec, tend = pump.finish(i, publish)
+            arrivals = [Arrival(w, p, t) for (w, p, t) in arr]
+            if status == 2:  # completion pattern outside the precomputed table (a timed-out round)
+                used = sch.decode(arrivals)
+                status, arr, t0, tdec, tend = pump.resolve(i, [(w, p, float(c)) for (w, p), c in used.items()],
+                                                           publish)
+                timeouts += 1
+            elif status == 1:
+                timeouts += 1
+            begun = publish
+            timeset[i] = tdec - t0
+            loop_time[i] = tend - t0
+            worker_timeset[i] = sch.worker_times(arrivals)
+            arrivals_log.append([(a.worker, a.part, a.t_rel) for a in arrivals])
+            if cfg.checkpoint_every and (i + 1) % cfg.checkpoint_every == 0:
+                self._checkpoint(i + 1, timeset, worker_timeset)
+        col.drain(R - 1, max(cfg.round_timeout, 60.0))
+        upd = pump.update_ms()
+        timeset[start:] += 1e-3 * np.asarray(upd[start:])
+        col.close()
+        if timed_start is not None:
+            t_timed1 = self._timed_fence()
+        self._sync()
+        env.barrier()
+        total = time.perf_counter() - orig_start
+        res = TrainResult(self.key, self.hist[:, : self.d].double().cpu().numpy(), timeset, worker_timeset, loop_time,
+                          total, timeouts=timeouts, phases=self.timer.summary(), arrivals=arrivals_log)
+        if t_timed0 is not None:
+            res.timed_seconds = t_timed1 - t_timed0
+            res.timed_rounds = R - timed_start
+        del pump
+        return res
+
+    def _worker_loop_native(self, timed_start, start: int = 0) -> None:
+        """Worker rounds in csrc/runtime/engine.cpp (WorkerPump) over the IPC mailbox."""
+        cfg, env, tx = self.cfg, self.env, self.tx
+        R, K = cfg.num_itrs, self.K
+        C = native_ext()
+        dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
+        w = env.world
+        pump = C.WorkerPump(self.plan.native_launcher(), tx.inbox, self.G, self.n_loc, tx.rremote.ptr,
+                            tx.mbox_rows, tx.my_row0, tx.flags.host_addr(env.rank), tx.flags.dev_addr(w + env.rank),
+                            tx.counters, K, dev, float(cfg.round_timeout))
+        cut = timed_start if timed_start is not None and start <= timed_start < R else None
+        segments = [(start, cut), (cut, R)] if cut is not None else [(start, R)]
+        t0 = None
+        for k, (a, b) in enumerate(segments):
+            if k == 1:
+                t0 = self._timed_fence()
+            bad = pump.run(a, b)
+            if bad >= 0:
+                raise TimeoutError(f"rank {env.rank}: beta of round {bad} did not arrive within {cfg.round_timeout}s")
+        tx.finish()
+        if timed_start is not None:
+            self.worker_timed_seconds = self._timed_fence() - (t0 if t0 is not None else time.perf_counter())
+        self._sync()
+        env.barrier()
+        del pump
+        return None
 
     def _send_beta(self, i: int):
         if self.tx is not None:

@@ -127,6 +127,17 @@ class DenseGradPlan:
             return G
         return self._run_torch(beta, G)
 
+    def native_launcher(self):
+        """C++ GradLauncher for the native round executors (csrc/runtime/engine.cpp)."""
+        if self.device.type != "cuda":
+            raise RuntimeError("native launchers need GPU tensors")
+        C = native()
+        if self.cpl is not None:
+            return C.GradLauncher.dense(self.prec.code, self.loss, self.cpl, self.segs, self.tasks, self.slab,
+                                        self.slot_task_begin, self.part, self.ld)
+        return C.GradLauncher.dense(self.prec.code, self.loss, 0, self.segs, self.tasks, self.slab,
+                                    self.slot_task_begin, self.part, self.ld, self.task_row_off, self.rbuf)
+
     def _run_torch(self, beta, G):
         acc = self.prec.acc
         b = beta.to(acc)
@@ -204,6 +215,12 @@ class SparseGradPlan:
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:
         return torch.zeros((n, self.nslots, self.ld), dtype=self.prec.acc, device=self.device)
+
+    def native_launcher(self):
+        if self.device.type != "cuda":
+            raise RuntimeError("native launchers need GPU tensors")
+        return native().GradLauncher.sparse(self.loss, self.row_ptr, self.col_idx, self.vals, self.y, self.coef,
+                                            self.rbuf, self.keys, self.rows, self.cvals, self.nslots, self.ld)
 
     def run(self, beta: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
         if G.shape != (self.nslots, self.ld):

@@ -30,7 +30,8 @@ def _source(n_parts, rows, d, seed=0):
 
 @pytest.mark.parametrize("case", CASES)
 @pytest.mark.parametrize("rule", ["GD", "AGD"])
-def test_gpu_matches_cpu(case, rule, native):
+@pytest.mark.parametrize("native_loop", [True, False])
+def test_gpu_matches_cpu(case, rule, native_loop, native):
     is_coded, P, ver, n_procs, s, k = case
     W = n_procs - 1
     d, rows = 33, 40
@@ -44,10 +45,11 @@ def test_gpu_matches_cpu(case, rule, native):
     out = {}
     for dev in ("cpu", "cuda"):
         cfg = RunConfig(n_procs, n, d, "/tmp/eh_gpu_eng/", 0, "x", is_coded, s, P, ver, k, 0, rule, num_itrs=8,
-                        seed=0, verbose=False)
+                        seed=0, verbose=False, native_loop=native_loop)
         env = DistEnv(device=torch.device(dev))
         sch = make_scheme(key, W, s, n, k, P, rng=np.random.RandomState(0))
         tr = Trainer(cfg, env, src, scheme=sch)
+        assert tr.native_loop == (dev == "cuda" and native_loop)
         res = tr.run()
         out[dev] = res.betaset
         if dev == "cuda":
@@ -70,3 +72,19 @@ def test_gpu_delay_semantics(native):
     floor = delay_floor(W, 10, groups=[w // 3 for w in range(W)], k=k, mean=0.02)
     assert res.timeset.sum() >= floor
     assert res.timeset.sum() < floor + 10 * 0.01  # < 10 ms overhead per round
+
+
+def test_native_loop_timeout_falls_back_to_host_decode(native):
+    """Cyclic code with s+1 dead workers: rounds time out, the native executor hands the
+    off-table completion pattern back to the host decode and training continues."""
+    W, s = 6, 1
+    rows, d = 30, 12
+    src = _source(W, rows, d)
+    cfg = RunConfig(W + 1, rows * W, d, "/tmp/eh_gpu_eng/", 0, "x", 1, s, 0, 0, 0, 1, "GD", num_itrs=3, seed=0,
+                    verbose=False, kill_workers=[2, 4], delay_mode="none", round_timeout=0.2)
+    tr = Trainer(cfg, DistEnv(device=torch.device("cuda")), src)
+    assert tr.native_loop
+    res = tr.run()
+    assert res.timeouts == 3
+    assert np.all(res.worker_timeset[:, [1, 3]] == -1)
+    assert np.all(np.isfinite(res.betaset))
