@@ -136,3 +136,55 @@ class DeviceGMM:
         import torch
 
         return self._draw(int(0.2 * self.n_rows), 10 ** 6 + 1, device, dtype or torch.float64)
+
+
+# ------------------------------------------------------------------ one-hot (real-data-shaped)
+REAL_SHAPES = {  # (train rows, one-hot columns, original columns incl. bias) of the prepared datasets
+    "covtype": (396112, 15509, 55),  # ref run_approx_coding.sh:26-28
+    "kc_house_data": (17290, 27654, 19),  # ref run_approx_coding.sh:34-36
+    "amazon-dataset": (26215, 241915, 45),  # ref run_approx_coding.sh:30-32 (9 + 35 interactions + bias)
+}
+
+
+def onehot_partitions(n_rows: int, n_cols: int, n_feat: int, n_partitions: int, seed: int = 0,
+                      least_squares: bool = False, test_frac: float = 0.25):
+    """Synthetic one-hot CSR data with the structure of the prepared real datasets.
+
+    Every row has exactly ``n_feat`` nonzeros (one category of each original column, the
+    last column being the single-category bias), all values 1.0 — the layout
+    ``arrange_real_data.py`` produces.  Labels follow a planted model:
+    logistic ``y = 2 Bernoulli(sigmoid(x . w*)) - 1`` or least squares ``y = x . w* + noise``.
+    Returns (partitions [(csr, y)], (test_csr, y_test)) with ``n_rows // n_partitions`` rows
+    per partition.
+    """
+    from scipy.sparse import csr_matrix
+
+    rng = np.random.RandomState(seed)
+    n_real = n_feat - 1
+    base = max(2, (n_cols - 1) // max(1, n_real))
+    cards = np.full(n_real, base, dtype=np.int64)
+    cards[: max(0, (n_cols - 1) - base * n_real)] += 1  # spread the remainder: sum(cards) = n_cols - 1
+    offs = np.concatenate([[0], np.cumsum(cards)])
+    d = int(offs[-1]) + 1
+    w_star = rng.normal(0, 1.0 / np.sqrt(n_feat), d)
+
+    def draw(n):
+        # skewed category frequencies (Zipf-like), like real categorical columns
+        cols = np.empty((n, n_feat), dtype=np.int64)
+        for j in range(n_real):
+            u = rng.power(3.0, n)
+            cols[:, j] = offs[j] + np.minimum((u * cards[j]).astype(np.int64), cards[j] - 1)
+        cols[:, -1] = d - 1
+        indptr = np.arange(0, n * n_feat + 1, n_feat, dtype=np.int64)
+        X = csr_matrix((np.ones(n * n_feat), cols.ravel().astype(np.int32), indptr), shape=(n, d))
+        z = np.asarray(X @ w_star).ravel()
+        if least_squares:
+            y = z + 0.1 * rng.standard_normal(n)
+        else:
+            y = 2.0 * rng.binomial(1, 1.0 / (1.0 + np.exp(-3.0 * z))) - 1.0
+        return X, y
+
+    rpw = n_rows // n_partitions
+    parts = [draw(rpw) for _ in range(n_partitions)]
+    test = draw(max(1, int(test_frac * n_rows)))
+    return parts, test, d

@@ -1,0 +1,160 @@
+"""Secondary benchmark suite: every config BASELINE.json lists, on one MI355X.
+
+    python tools/bench_suite.py [--quick] [--out DIR]
+
+Configs (BASELINE.json "configs"; synthetic stand-ins where the reference used real data,
+which is not available offline — same shapes and one-hot structure, see
+data/synthetic.py onehot_partitions):
+  naive_dense        naive uncoded logistic, synthetic GMM 1e6 x 1e3, W=8
+  agc_dense          approximate coding (AGC), same data, W=8 s=2 k=6 (uneven groups)
+  cyclic_dense       exact cyclic-MDS (EGC), same data, W=8 s=2
+  frc_dense          exact FRC (replication), same data, W=8 s=1
+  partialrep_covtype partial replication, covtype-shaped one-hot (396112 x 15509), W=8 s=1 P=4,
+                     injected Exp(0.05) delays (forced; the reference only relies on natural stragglers;
+                     mean 0.05 s instead of 0.5 s keeps the run short — floors scale linearly)
+  avoid_covtype      ignore-stragglers, same data, W=8 s=1, forced delays
+  ls_kc_house_*      least squares on kc_house-shaped one-hot (17290 x 27654): naive vs AGC with
+                     num_collect in {4,5,6,7}, W=8 s=1
+
+Per config: seconds per round (timed, device-synchronised), time-to-decode (reference
+``timeset``), iterations to the training-loss floor (within 1 % of the best loss over the
+run), and for delayed runs the deterministic injected-delay floor and the overhead above it
+(SURVEY §6).  Writes suite.jsonl and suite.md.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _floor_iters(tl: np.ndarray) -> int:
+    floor = float(np.min(tl))
+    return int(np.argmax(tl <= floor + 0.01 * abs(floor)))
+
+
+def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_kw=None):
+    import torch
+
+    from erasurehead_amd.config import RunConfig
+    from erasurehead_amd.engine import Trainer, evaluate
+    from erasurehead_amd.parallel.dist import DistEnv
+    from erasurehead_amd.utils.delay import delay_floor
+
+    cfg = RunConfig(**cfg_kw, num_itrs=rounds, verbose=False, seed=0)
+    env = DistEnv(device=torch.device("cuda" if torch.cuda.is_available() else "cpu"))
+    t0 = time.perf_counter()
+    tr = Trainer(cfg, env, source)
+    setup = time.perf_counter() - t0
+    res = tr.run(timed_start=timed_from)
+    ev = evaluate(tr, res, write=False)
+    out = {
+        "config": name,
+        "scheme": tr.key,
+        "loss": "least_squares" if tr.loss else "logistic",
+        "W": cfg.n_workers, "s": cfg.n_stragglers, "num_collect": cfg.num_collect, "partitions": cfg.partitions,
+        "n_rows": cfg.n_rows, "n_cols": cfg.n_cols, "rounds": rounds, "add_delay": cfg.add_delay,
+        "sec_per_round": res.timed_seconds / max(1, res.timed_rounds),
+        "timeset_mean_ms": 1e3 * float(np.mean(res.timeset[timed_from:])),
+        "sum_timeset_s": float(np.sum(res.timeset)),
+        "iters_to_loss_floor": _floor_iters(ev.training_loss),
+        "final_train_loss": float(ev.training_loss[-1]),
+        "final_test_loss": float(ev.testing_loss[-1]),
+        "final_auc": float(ev.auc[-1]) if not tr.loss else None,
+        "setup_s": setup,
+        "native_loop": tr.native_loop,
+        "precision": cfg.precision,
+    }
+    if delay_floor_kw is not None:
+        fl = delay_floor(cfg.n_workers, rounds, mean=cfg.delay_mean, **delay_floor_kw)
+        out["delay_floor_s"] = fl
+        out["overhead_above_floor_ms_per_round"] = 1e3 * (out["sum_timeset_s"] - fl) / rounds
+    tr.close()
+    del tr
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true", help="10x smaller problems (plumbing check)")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--only", default=None, help="comma-separated config names")
+    a = ap.parse_args()
+    from erasurehead_amd.data.source import ArraySource
+    from erasurehead_amd.data.synthetic import REAL_SHAPES, onehot_partitions
+
+    scale = 10 if a.quick else 1
+    n_dense = 1_000_000 // scale
+    dense = dict(n_procs=9, n_rows=n_dense, n_cols=1000, input_dir="/tmp/eh_suite/", is_real=0, dataset="synthetic",
+                 data="synthetic", data_seed=1234, update_rule="AGD")
+    configs = []
+    configs.append(("naive_dense", dict(dense, is_coded=0), None, None))
+    configs.append(("agc_dense", dict(dense, is_coded=1, n_stragglers=2, coded_ver=3, num_collect=6,
+                                      allow_uneven_groups=True), None, None))
+    configs.append(("cyclic_dense", dict(dense, is_coded=1, n_stragglers=2, coded_ver=0), None, None))
+    configs.append(("frc_dense", dict(dense, is_coded=1, n_stragglers=1, coded_ver=1), None, None))
+
+    # covtype-shaped one-hot; partial schemes need (P - s) * W partition files
+    n_cov, d_cov, f_cov = REAL_SHAPES["covtype"]
+    n_cov //= scale
+    W, s, P = 8, 1, 4
+    cov_parts, cov_test, dc = onehot_partitions(n_cov, d_cov, f_cov, (P - s) * W, seed=3)
+    src_pr = ArraySource(cov_parts, cov_test, sparse=True)
+    n_pr = sum(p[0].shape[0] for p in cov_parts)
+    base_cov = dict(n_procs=W + 1, n_rows=n_pr, n_cols=dc, input_dir="/tmp/eh_suite/", is_real=1, dataset="covtype",
+                    update_rule="AGD", add_delay=1, force_delay=True, delay_mean=0.05)
+    configs.append(("partialrep_covtype", dict(base_cov, is_coded=1, n_stragglers=s, partitions=P, coded_ver=1),
+                    src_pr, {"stop_count": W}))
+    cov8, cov8_test, _ = onehot_partitions(n_cov, d_cov, f_cov, W, seed=3)
+    n8 = sum(p[0].shape[0] for p in cov8)
+    configs.append(("avoid_covtype", dict(base_cov, n_rows=n8, is_coded=1, n_stragglers=s, coded_ver=2),
+                    ArraySource(cov8, cov8_test, sparse=True), {"stop_count": W - s}))
+
+    n_kc, d_kc, f_kc = REAL_SHAPES["kc_house_data"]
+    kc, kc_test, dk = onehot_partitions(n_kc, d_kc, f_kc, W, seed=5, least_squares=True)
+    src_kc = ArraySource(kc, kc_test, sparse=True)
+    nk = sum(p[0].shape[0] for p in kc)
+    base_kc = dict(n_procs=W + 1, n_rows=nk, n_cols=dk, input_dir="/tmp/eh_suite/", is_real=1,
+                   dataset="kc_house_data", update_rule="AGD", loss="least_squares", lr=0.2)
+    configs.append(("ls_kc_house_naive", dict(base_kc, is_coded=0), src_kc, None))
+    for k in (4, 5, 6, 7):
+        configs.append((f"ls_kc_house_agc_k{k}", dict(base_kc, is_coded=1, n_stragglers=1, coded_ver=3,
+                                                      num_collect=k), src_kc, None))
+    if a.only:
+        keep = set(a.only.split(","))
+        configs = [c for c in configs if c[0] in keep]
+    os.makedirs(a.out, exist_ok=True)
+    rows = []
+    with open(os.path.join(a.out, "suite.jsonl"), "w") as f:
+        for name, kw, src, floor_kw in configs:
+            r = run_config(name, kw, src, delay_floor_kw=floor_kw)
+            rows.append(r)
+            f.write(json.dumps(r) + "\n")
+            f.flush()
+            print(json.dumps(r), flush=True)
+    hdr = ("| config | scheme | W | s | k | ms/round | timeset ms | iters to floor | final train loss | AUC | "
+           "delay floor s | overhead ms/round |\n|---|---|---|---|---|---|---|---|---|---|---|---|\n")
+    lines = []
+    for r in rows:
+        auc = "%.4f" % r["final_auc"] if r.get("final_auc") is not None else "-"
+        fl = "%.2f" % r["delay_floor_s"] if "delay_floor_s" in r else "-"
+        ov = "%.3f" % r["overhead_above_floor_ms_per_round"] if "delay_floor_s" in r else "-"
+        lines.append(f"| {r['config']} | {r['scheme']} | {r['W']} | {r['s']} | {r['num_collect']} | "
+                     f"{1e3 * r['sec_per_round']:.3f} | {r['timeset_mean_ms']:.3f} | {r['iters_to_loss_floor']} | "
+                     f"{r['final_train_loss']:.5f} | {auc} | {fl} | {ov} |")
+    with open(os.path.join(a.out, "suite.md"), "w") as f:
+        f.write(hdr + "\n".join(lines) + "\n")
+    print(hdr + "\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
