@@ -133,6 +133,28 @@ void grad_sparse(int64_t loss, const Tensor& row_ptr, const Tensor& col_idx, con
         "grad_sparse");
 }
 
+void grad_ell(int64_t loss, const Tensor& idx, const OptT& vals, const Tensor& y, const Tensor& coef,
+              const Tensor& beta, const Tensor& rbuf, const Tensor& chunks, const Tensor& lo, const Tensor& width,
+              int64_t max_width, const Tensor& G, int64_t ld) {
+  for (auto* p : {&idx, &y, &coef, &beta, &rbuf, &chunks, &lo, &width, &G}) need_cuda(*p, "ell operand");
+  need(idx.dim() == 2 && idx.scalar_type() == at::kInt, "idx must be int32 [m, nrows]");
+  need(chunks.dim() == 2 && chunks.size(1) == 4 && chunks.scalar_type() == at::kInt, "chunks must be int32 [n, 4]");
+  need(lo.scalar_type() == at::kInt && width.scalar_type() == at::kInt, "lo/width must be int32");
+  const int64_t m = idx.size(0), nrows = idx.size(1);
+  need(lo.numel() == m && width.numel() == m, "lo/width must have m entries");
+  const int ac = acc_code(G);
+  need(acc_code(y) == ac && acc_code(coef) == ac && acc_code(beta) == ac && acc_code(rbuf) == ac, "dtype mismatch");
+  need(y.numel() == nrows && coef.numel() == nrows && rbuf.numel() >= nrows, "row arrays must match idx");
+  need(G.dim() == 2 && G.size(1) == ld && beta.numel() >= ld, "G must be [nslots, ld]");
+  if (vals) need(vals->is_cuda() && acc_code(*vals) == ac && vals->sizes() == idx.sizes(), "vals must match idx");
+  need(nrows < (int64_t(1) << 31), "ELL rows must fit int32");
+  check(eh::grad_ell_launch(ac, (int)loss, idx.data_ptr<int>(), vals ? vals->data_ptr() : nullptr, y.data_ptr(),
+                            coef.data_ptr(), beta.data_ptr(), rbuf.data_ptr(), (long long)nrows, (int)m,
+                            chunks.data_ptr(), (int)chunks.size(0), lo.data_ptr<int>(), width.data_ptr<int>(),
+                            (int)max_width, G.data_ptr(), (long long)G.numel(), (int)ld, stream_of(G)),
+        "grad_ell");
+}
+
 void combine_update(const std::vector<Tensor>& msgs, const std::vector<double>& coefs, const Tensor& beta,
                     const Tensor& u, const OptT& hist, const OptT& beta_w, const OptT& g_out, int64_t d,
                     double decay, double gm, double l2, double theta, int64_t rule) {
@@ -204,6 +226,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_dense", &grad_dense);
   m.def("grad_dense_twopass", &grad_dense_twopass);
   m.def("grad_sparse", &grad_sparse);
+  m.def("grad_ell", &grad_ell);
   m.def("combine_update", &combine_update);
   m.def("eval_gemm_loss", &eval_gemm_loss);
   m.attr("MAX_MSGS") = eh::kMaxMsgs;

@@ -15,6 +15,8 @@
 //     run issues one float atomic add: one atomic per distinct column per wave
 //     instead of one per nonzero.
 // Pattern-only storage: vals == nullptr means every stored value is 1.0 (one-hot).
+#include <algorithm>
+
 #include "common.h"
 
 namespace eh {
@@ -60,6 +62,113 @@ coo_colpass(const long long* __restrict__ keys, const int* __restrict__ rows,
   const long long kn = __shfl_down(key, 1, kWave);
   const bool last = (lane == kWave - 1) || (kn != key);
   if (live && last) atomicAdd(G + key, v);
+}
+
+// ----- ELL path: constant nnz per row (every one-hot dataset of the reference) -----------
+//
+// idx is column-major [m][nrows]: idx[k][row] = k-th (sorted) column of `row`.  For one-hot
+// data the k-th nonzero of every row falls in original feature k's block of categories, so
+// a wave that handles 64 consecutive rows for one k gathers beta (row pass) or scatters
+// into g (column pass) inside one small window — L1-resident gathers and LDS-resident
+// histograms instead of whole-vector random access.
+//
+// Row pass: one thread per row, z = sum_k v * beta[idx[k][row]], r = loss residual.
+template <typename A, int LOSS, bool VALS>
+__global__ void __launch_bounds__(256)
+ell_rowpass(const int* __restrict__ idx, const A* __restrict__ vals, const A* __restrict__ y,
+            const A* __restrict__ coef, const A* __restrict__ beta, A* __restrict__ rbuf,
+            long long nrows, int m) {
+  const long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (row >= nrows) return;
+  A z0 = A(0), z1 = A(0);
+  int k = 0;
+  for (; k + 1 < m; k += 2) {  // two independent gathers in flight
+    const int c0 = idx[static_cast<long long>(k) * nrows + row];
+    const int c1 = idx[static_cast<long long>(k + 1) * nrows + row];
+    const A v0 = VALS ? vals[static_cast<long long>(k) * nrows + row] : A(1);
+    const A v1 = VALS ? vals[static_cast<long long>(k + 1) * nrows + row] : A(1);
+    z0 = fma(v0, beta[c0], z0);
+    z1 = fma(v1, beta[c1], z1);
+  }
+  if (k < m) {
+    const int c0 = idx[static_cast<long long>(k) * nrows + row];
+    const A v0 = VALS ? vals[static_cast<long long>(k) * nrows + row] : A(1);
+    z0 = fma(v0, beta[c0], z0);
+  }
+  rbuf[row] = residual<LOSS, A>(z0 + z1, y[row], coef[row]);
+}
+
+struct EllChunk {
+  int row_begin;
+  int row_end;
+  int slot;
+  int pad;
+};
+
+// Column pass: block (chunk of rows of one message, feature k).  Features whose column
+// window fits the LDS budget accumulate r * v into an LDS histogram of the window and
+// flush the touched bins with one global atomic each; wider windows add straight into g.
+template <typename A, bool VALS>
+__global__ void __launch_bounds__(256)
+ell_colpass(const int* __restrict__ idx, const A* __restrict__ vals, const A* __restrict__ rbuf,
+            const EllChunk* __restrict__ chunks, const int* __restrict__ lo, const int* __restrict__ width,
+            A* __restrict__ G, long long nrows, int ld, int lds_cap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  A* hist = reinterpret_cast<A*>(smem_raw);
+  const EllChunk ch = chunks[blockIdx.x];
+  const int k = blockIdx.y;
+  const int lo_k = lo[k], w = width[k];
+  const int* __restrict__ ik = idx + static_cast<long long>(k) * nrows;
+  const A* __restrict__ vk = VALS ? vals + static_cast<long long>(k) * nrows : nullptr;
+  A* __restrict__ g = G + static_cast<long long>(ch.slot) * ld;
+  if (w <= lds_cap) {
+    for (int b = threadIdx.x; b < w; b += blockDim.x) hist[b] = A(0);
+    __syncthreads();
+    for (int row = ch.row_begin + threadIdx.x; row < ch.row_end; row += blockDim.x) {
+      const A v = VALS ? rbuf[row] * vk[row] : rbuf[row];
+      atomicAdd(&hist[ik[row] - lo_k], v);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < w; b += blockDim.x) {
+      const A h = hist[b];
+      if (h != A(0)) atomicAdd(&g[lo_k + b], h);
+    }
+  } else {
+    for (int row = ch.row_begin + threadIdx.x; row < ch.row_end; row += blockDim.x) {
+      const A v = VALS ? rbuf[row] * vk[row] : rbuf[row];
+      atomicAdd(&g[ik[row]], v);
+    }
+  }
+}
+
+hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals, const void* y,
+                           const void* coef, const void* beta, void* rbuf, long long nrows, int m,
+                           const void* chunks, int nchunks, const int* lo, const int* width,
+                           int max_width, void* G, long long gsize, int ld, hipStream_t st) {
+  const size_t esz = dtype == 0 ? sizeof(double) : sizeof(float);
+  hipError_t e = hipMemsetAsync(G, 0, gsize * esz, st);
+  if (e != hipSuccess || nrows == 0 || m == 0) return e;
+  constexpr int kLdsBytes = 64 * 1024;
+  const int cap = static_cast<int>(kLdsBytes / esz);
+  const size_t sh = static_cast<size_t>(std::min(max_width, cap)) * esz;
+  const dim3 block(256), grid1(static_cast<unsigned>((nrows + 255) / 256)), grid2(nchunks, m);
+  const EllChunk* C = static_cast<const EllChunk*>(chunks);
+#define EH_ELL(A, VALS)                                                                                  \
+  if (loss == kLogistic)                                                                                 \
+    hipLaunchKernelGGL((ell_rowpass<A, kLogistic, VALS>), grid1, block, 0, st, idx, (const A*)vals,      \
+                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m);                 \
+  else                                                                                                   \
+    hipLaunchKernelGGL((ell_rowpass<A, kLeastSquares, VALS>), grid1, block, 0, st, idx, (const A*)vals,  \
+                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m);                 \
+  hipLaunchKernelGGL((ell_colpass<A, VALS>), grid2, block, sh, st, idx, (const A*)vals, (const A*)rbuf, C, \
+                     lo, width, (A*)G, nrows, ld, cap);
+  if (dtype == 0) {
+    if (vals) { EH_ELL(double, true) } else { EH_ELL(double, false) }
+  } else {
+    if (vals) { EH_ELL(float, true) } else { EH_ELL(float, false) }
+  }
+#undef EH_ELL
+  return hipGetLastError();
 }
 
 hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, const int* col_idx,

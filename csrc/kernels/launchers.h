@@ -24,6 +24,13 @@ hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, con
                               const long long* keys, const int* rows, const void* cvals,
                               long long nnz, void* G, long long gsize, int ld, hipStream_t st);
 
+// ELL (constant nnz per row) variant: idx/vals column-major [m][nrows]; chunks = EllChunk
+// {row_begin, row_end, slot, pad} of rows of one message; lo/width = column window of feature k.
+hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals, const void* y,
+                           const void* coef, const void* beta, void* rbuf, long long nrows, int m,
+                           const void* chunks, int nchunks, const int* lo, const int* width,
+                           int max_width, void* G, long long gsize, int ld, hipStream_t st);
+
 // ---- post-hoc evaluation GEMM (eval.hip) -----------------------------------------------
 hipError_t eval_gemm_loss_launch(int x_dtype, int loss_kind, const void* X, long long ldx,
                                  long long n, int d, const void* y, const void* B, int ldb,

@@ -88,6 +88,13 @@ struct GradLauncher {
   const void* cvals = nullptr;
   long long nnz = 0;
   int acc = 0;
+  // ELL
+  const int* ell_idx = nullptr;
+  const void* ell_vals = nullptr;
+  const void* chunks = nullptr;
+  int nchunks = 0, m = 0, max_width = 0;
+  const int* lo = nullptr;
+  const int* width = nullptr;
   std::vector<Tensor> keep;
 
   hipError_t launch(const void* beta, void* G, hipStream_t st) const {
@@ -103,6 +110,9 @@ struct GradLauncher {
       case 2:
         return eh::grad_sparse_launch(acc, loss, row_ptr, col_idx, vals, y, coef, beta, rbuf, nrows, keys, rows,
                                       cvals, nnz, G, static_cast<long long>(nslots) * ld, ld, st);
+      case 3:
+        return eh::grad_ell_launch(acc, loss, ell_idx, ell_vals, y, coef, beta, rbuf, nrows, m, chunks, nchunks, lo,
+                                   width, max_width, G, static_cast<long long>(nslots) * ld, ld, st);
       default:
         return hipErrorInvalidValue;
     }
@@ -172,6 +182,35 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& row_ptr, c
   g->keep = {row_ptr, col_idx, y, coef, rbuf, keys, rows};
   if (vals) g->keep.push_back(*vals);
   if (cvals) g->keep.push_back(*cvals);
+  return g;
+}
+
+std::shared_ptr<GradLauncher> make_ell(int64_t loss, const Tensor& idx, std::optional<Tensor> vals, const Tensor& y,
+                                       const Tensor& coef, const Tensor& rbuf, const Tensor& chunks, const Tensor& lo,
+                                       const Tensor& width, int64_t max_width, int64_t nslots, int64_t ld) {
+  for (auto* t : {&idx, &y, &coef, &rbuf, &chunks, &lo, &width}) need_gpu(*t, "ell plan operand");
+  need(idx.dim() == 2 && idx.scalar_type() == at::kInt, "idx must be int32 [m, nrows]");
+  need(chunks.dim() == 2 && chunks.size(1) == 4 && chunks.scalar_type() == at::kInt, "chunks must be int32 [n,4]");
+  auto g = std::make_shared<GradLauncher>();
+  g->kind = 3;
+  g->loss = (int)loss;
+  g->acc = acc_code(y);
+  g->ld = (int)ld;
+  g->nslots = (int)nslots;
+  g->m = (int)idx.size(0);
+  g->nrows = idx.size(1);
+  g->ell_idx = idx.data_ptr<int>();
+  g->ell_vals = vals ? vals->data_ptr() : nullptr;
+  g->y = y.data_ptr();
+  g->coef = coef.data_ptr();
+  g->rbuf = rbuf.data_ptr();
+  g->chunks = chunks.data_ptr();
+  g->nchunks = (int)chunks.size(0);
+  g->lo = lo.data_ptr<int>();
+  g->width = width.data_ptr<int>();
+  g->max_width = (int)max_width;
+  g->keep = {idx, y, coef, rbuf, chunks, lo, width};
+  if (vals) g->keep.push_back(*vals);
   return g;
 }
 
@@ -585,6 +624,9 @@ void bind_engine(py::module& m) {
                   py::arg("task_row_off") = py::none(), py::arg("rbuf") = py::none())
       .def_static("sparse", &make_sparse, py::arg("loss"), py::arg("row_ptr"), py::arg("col_idx"), py::arg("vals"),
                   py::arg("y"), py::arg("coef"), py::arg("rbuf"), py::arg("keys"), py::arg("rows"), py::arg("cvals"),
+                  py::arg("nslots"), py::arg("ld"))
+      .def_static("ell", &make_ell, py::arg("loss"), py::arg("idx"), py::arg("vals"), py::arg("y"), py::arg("coef"),
+                  py::arg("rbuf"), py::arg("chunks"), py::arg("lo"), py::arg("width"), py::arg("max_width"),
                   py::arg("nslots"), py::arg("ld"))
       .def("launch", [](const GradLauncher& g, const Tensor& beta, const Tensor& G) {
         need_gpu(beta, "beta");

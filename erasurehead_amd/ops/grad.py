@@ -166,7 +166,7 @@ class SparseGradPlan:
     """
 
     def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]], partitions: Dict[int, Tuple[object, np.ndarray]],
-                 prec: Precision, loss: int, d: int, device="cpu"):
+                 prec: Precision, loss: int, d: int, device="cpu", use_ell: bool = True):
         import scipy.sparse as sps
 
         if prec.name == "bf16":
@@ -212,6 +212,38 @@ class SparseGradPlan:
         self.rbuf = torch.empty(max(1, self.nrows), dtype=acc, device=dev)
         self._row_slot = torch.from_numpy(row_slot).to(dev)
         self._X_cpu = X if dev.type == "cpu" else None
+        self.ell = False
+        if dev.type == "cuda" and use_ell:
+            self._build_ell(X, row_slot, npacc, slots)
+
+    ELL_CHUNK = 4096  # rows per column-pass block
+
+    def _build_ell(self, X, row_slot, npacc, slots):
+        """Column-major ELL twin when every row has the same nnz (one-hot data)."""
+        nnz_row = np.diff(X.indptr)
+        if self.nrows == 0 or not np.all(nnz_row == nnz_row[0]) or nnz_row[0] == 0 or self.nrows >= 2 ** 31:
+            return
+        m = int(nnz_row[0])
+        idx = X.indices.reshape(self.nrows, m).T  # [m, nrows]; rows are sorted -> k-th smallest column
+        lo = idx.min(axis=1).astype(np.int32)
+        width = (idx.max(axis=1) - lo + 1).astype(np.int32)
+        chunks = []
+        r = 0
+        for slot in range(self.nslots):
+            n = int(np.sum(row_slot == slot))
+            for r0 in range(r, r + n, self.ELL_CHUNK):
+                chunks.append((r0, min(r + n, r0 + self.ELL_CHUNK), slot, 0))
+            r += n
+        dev = self.device
+        self.ell = True
+        self.ell_m = m
+        self.ell_idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32)).to(dev)
+        self.ell_vals = None if self.pattern_only else torch.from_numpy(
+            np.ascontiguousarray(X.data.reshape(self.nrows, m).T, dtype=npacc)).to(dev)
+        self.ell_lo = torch.from_numpy(lo).to(dev)
+        self.ell_width = torch.from_numpy(width).to(dev)
+        self.ell_max_width = int(width.max())
+        self.ell_chunks = torch.from_numpy(np.asarray(chunks, dtype=np.int32).reshape(-1, 4)).to(dev)
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:
         return torch.zeros((n, self.nslots, self.ld), dtype=self.prec.acc, device=self.device)
@@ -219,12 +251,20 @@ class SparseGradPlan:
     def native_launcher(self):
         if self.device.type != "cuda":
             raise RuntimeError("native launchers need GPU tensors")
+        if self.ell:
+            return native().GradLauncher.ell(self.loss, self.ell_idx, self.ell_vals, self.y, self.coef, self.rbuf,
+                                             self.ell_chunks, self.ell_lo, self.ell_width, self.ell_max_width,
+                                             self.nslots, self.ld)
         return native().GradLauncher.sparse(self.loss, self.row_ptr, self.col_idx, self.vals, self.y, self.coef,
                                             self.rbuf, self.keys, self.rows, self.cvals, self.nslots, self.ld)
 
     def run(self, beta: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
         if G.shape != (self.nslots, self.ld):
             raise ValueError(f"G must be [{self.nslots}, {self.ld}]")
+        if self.device.type == "cuda" and self.ell:
+            native().grad_ell(self.loss, self.ell_idx, self.ell_vals, self.y, self.coef, beta, self.rbuf,
+                              self.ell_chunks, self.ell_lo, self.ell_width, self.ell_max_width, G, self.ld)
+            return G
         if self.device.type == "cuda":
             native().grad_sparse(self.loss, self.row_ptr, self.col_idx, self.vals, self.y, self.coef, beta,
                                  self.rbuf, self.keys, self.rows, self.cvals, G, self.ld)

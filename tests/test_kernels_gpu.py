@@ -67,7 +67,8 @@ def test_dense_grad_many_tasks_deterministic(native):
 
 @pytest.mark.parametrize("prec_name,tol", [("fp64", 1e-11), ("fp32", 1e-4)])
 @pytest.mark.parametrize("pattern_only", [True, False])
-def test_sparse_grad(prec_name, tol, pattern_only, native):
+@pytest.mark.parametrize("use_ell", [True, False])
+def test_sparse_grad(prec_name, tol, pattern_only, use_ell, native):
     prec = get_precision(prec_name)
     rng = np.random.RandomState(3)
     d = 700
@@ -80,8 +81,8 @@ def test_sparse_grad(prec_name, tol, pattern_only, native):
         parts[p] = (X, rng.choice([-1.0, 1.0], n))
     msgs = [[(0, 1.0), (1, 0.5)], [(2, -1.5)], [(0, 1.0)]]
     for loss in (LOGISTIC, LEAST_SQUARES):
-        plan = SparseGradPlan(msgs, parts, prec, loss, d, device=DEV)
-        assert plan.pattern_only == pattern_only
+        plan = SparseGradPlan(msgs, parts, prec, loss, d, device=DEV, use_ell=use_ell)
+        assert plan.pattern_only == pattern_only and plan.ell == use_ell
         b = rng.randn(d) * 0.2
         beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
         beta[:d] = torch.from_numpy(b).to(prec.acc)
@@ -95,6 +96,47 @@ def test_sparse_grad(prec_name, tol, pattern_only, native):
             got = G[s, :d].double().cpu().numpy()
             err = np.max(np.abs(got - ref)) / max(1e-12, np.max(np.abs(ref)))
             assert err < tol, (loss, s, err)
+
+
+@pytest.mark.parametrize("prec_name,tol", [("fp64", 1e-11), ("fp32", 1e-4)])
+def test_ell_onehot_blocks_and_wide_windows(prec_name, tol, native):
+    """One-hot feature blocks (LDS histogram path) plus one block wider than the LDS budget
+    (global-atomic path), through both the Python binding and the native GradLauncher."""
+    from erasurehead_amd.data.synthetic import onehot_partitions
+
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(9)
+    parts_l, _, d = onehot_partitions(3000, 900, 6, 3, seed=4)
+    wide = 20000  # > 64 KiB / 8 B: that feature's window cannot live in LDS
+    parts = {}
+    for p, (X, y) in enumerate(parts_l):
+        extra = sps.csr_matrix((np.ones(X.shape[0]), d + rng.randint(0, wide, X.shape[0]),
+                                np.arange(X.shape[0] + 1)), shape=(X.shape[0], d + wide))
+        Xw = sps.csr_matrix(sps.hstack([X, sps.csr_matrix((X.shape[0], wide))]) + extra)
+        Xw.sort_indices()
+        parts[p] = (Xw, y)
+    D = d + wide
+    msgs = [[(0, 1.0), (1, 0.5)], [(2, -1.5)]]
+    b = rng.randn(D) * 0.1
+    for loss in (LOGISTIC, LEAST_SQUARES):
+        plan = SparseGradPlan(msgs, parts, prec, loss, D, device=DEV)
+        assert plan.ell and plan.ell_max_width > 8192
+        beta = torch.zeros(prec.ld(D), dtype=prec.acc, device=DEV)
+        beta[:D] = torch.from_numpy(b).to(prec.acc)
+        bh = beta[:D].double().cpu().numpy()
+        f = logistic_grad if loss == LOGISTIC else least_squares_grad
+        for via_launcher in (False, True):
+            G = plan.out_buffer()[0]
+            if via_launcher:
+                plan.native_launcher().launch(beta, G)
+            else:
+                plan.run(beta, G)
+            torch.cuda.synchronize()
+            for s_, m in enumerate(msgs):
+                ref = sum(f(parts[p][0], parts[p][1], bh, c) for p, c in m)
+                got = G[s_, :D].double().cpu().numpy()
+                err = np.max(np.abs(got - ref)) / max(1e-12, np.max(np.abs(ref)))
+                assert err < tol, (loss, via_launcher, s_, err)
 
 
 @pytest.mark.parametrize("rule", ["GD", "AGD"])

@@ -13,6 +13,7 @@ data/synthetic.py onehot_partitions):
                      injected Exp(0.05) delays (forced; the reference only relies on natural stragglers;
                      mean 0.05 s instead of 0.5 s keeps the run short — floors scale linearly)
   avoid_covtype      ignore-stragglers, same data, W=8 s=1, forced delays
+  agc_covtype        AGC on the covtype-shaped data without delays (sparse kernel throughput)
   ls_kc_house_*      least squares on kc_house-shaped one-hot (17290 x 27654): naive vs AGC with
                      num_collect in {4,5,6,7}, W=8 s=1
 
@@ -116,8 +117,11 @@ def main():
                     src_pr, {"stop_count": W}))
     cov8, cov8_test, _ = onehot_partitions(n_cov, d_cov, f_cov, W, seed=3)
     n8 = sum(p[0].shape[0] for p in cov8)
+    src8 = ArraySource(cov8, cov8_test, sparse=True)
     configs.append(("avoid_covtype", dict(base_cov, n_rows=n8, is_coded=1, n_stragglers=s, coded_ver=2),
-                    ArraySource(cov8, cov8_test, sparse=True), {"stop_count": W - s}))
+                    src8, {"stop_count": W - s}))
+    configs.append(("agc_covtype", dict(base_cov, n_rows=n8, is_coded=1, n_stragglers=s, coded_ver=3, num_collect=6,
+                                        add_delay=0, force_delay=False), src8, None))
 
     n_kc, d_kc, f_kc = REAL_SHAPES["kc_house_data"]
     kc, kc_test, dk = onehot_partitions(n_kc, d_kc, f_kc, W, seed=5, least_squares=True)
