@@ -103,19 +103,18 @@ def auc_columns(y: torch.Tensor, P: torch.Tensor, chunk: int = 0) -> np.ndarray:
         chunk = max(1, min(R, (1 << 26) // max(1, n)))
     ar = torch.arange(1, n + 1, dtype=torch.float64, device=P.device)
     for c0 in range(0, R, chunk):
-        S = P[:, c0:c0 + chunk].double()
-        m = S.shape[1]
-        ss, order = torch.sort(S, dim=0, stable=True)
-        pos_s = pos[order]  # [n, m] labels in sorted order
+        S = P[:, c0:c0 + chunk].double().t().contiguous()  # [m, n]: every scan runs along contiguous memory
+        m = S.shape[0]
+        ss, order = torch.sort(S, dim=1, stable=True)
+        pos_s = pos[order]  # [m, n] labels in sorted order
         start = torch.ones_like(ss, dtype=torch.bool)
-        start[1:] = ss[1:] != ss[:-1]
-        seg = torch.cumsum(start.to(torch.int64), dim=0) - 1  # tie-group id within the column
-        flat = seg + torch.arange(m, device=P.device)[None, :] * n
-        ranks = ar[:, None].expand(n, m).reshape(-1)
-        ssum = torch.zeros(n * m, dtype=torch.float64, device=P.device).index_add_(0, flat.reshape(-1), ranks)
-        scnt = torch.zeros(n * m, dtype=torch.float64, device=P.device).index_add_(
-            0, flat.reshape(-1), torch.ones_like(ranks))
-        avg = (ssum / scnt.clamp(min=1))[flat]  # [n, m] average rank of every element
-        u = (avg * pos_s).sum(0) - n_pos * (n_pos + 1) / 2.0
+        start[:, 1:] = ss[:, 1:] != ss[:, :-1]
+        seg = torch.cumsum(start.to(torch.int64), dim=1) - 1  # tie-group id within the column
+        flat = (seg + torch.arange(m, device=P.device)[:, None] * n).reshape(-1)
+        ranks = ar[None, :].expand(m, n).reshape(-1)
+        ssum = torch.zeros(n * m, dtype=torch.float64, device=P.device).index_add_(0, flat, ranks)
+        scnt = torch.zeros(n * m, dtype=torch.float64, device=P.device).index_add_(0, flat, torch.ones_like(ranks))
+        avg = (ssum / scnt.clamp(min=1))[flat].view(m, n)  # average rank of every element
+        u = (avg * pos_s).sum(1) - n_pos * (n_pos + 1) / 2.0
         out[c0:c0 + m] = (u / (n_pos * n_neg)).cpu().numpy()
     return out
