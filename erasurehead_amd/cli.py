@@ -49,6 +49,7 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--checkpoint-path", default=None)
     g.add_argument("--resume", default=None, help="continue from a checkpoint written by --checkpoint-every")
     g.add_argument("--trace", action="store_true")
+    g.add_argument("--verify-beta", action="store_true", help="race detector: checksum beta on every worker")
     g.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     g.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl", "gloo"])
     return p
@@ -68,7 +69,7 @@ def parse(argv: List[str]):
                     fixed_sleep=a.fixed_sleep, kill_workers=a.kill_workers, force_delay=a.force_delay,
                     round_timeout=a.round_timeout, fix_quirks=a.fix_quirks, save_linear=a.save_linear,
                     full_precision_outputs=a.full_precision_outputs, evaluate=not a.no_eval, verbose=not a.quiet,
-                    checkpoint_every=a.checkpoint_every, checkpoint_path=a.checkpoint_path, resume=a.resume, trace=a.trace,
+                    checkpoint_every=a.checkpoint_every, checkpoint_path=a.checkpoint_path, resume=a.resume, trace=a.trace, verify_beta=a.verify_beta,
                     transport=a.transport)
     return cfg, a
 

@@ -64,6 +64,7 @@ class RunConfig:
     resume: Optional[str] = None
     trace: bool = False
     tasks: int = 0  # override gradient-kernel workgroup count
+    verify_beta: bool = False  # race detector: workers checksum beta before/after use (Python loop)
     native_loop: bool = True  # GPU rounds in the C++ executors (csrc/runtime/engine.cpp)
     sync_update: bool = False  # host waits for every round's update kernel (else timed by HIP events)
     transport: str = "auto"  # auto | ipc | rccl | gloo (parallel/transport.py)

@@ -245,7 +245,7 @@ class Trainer:
     @property
     def native_loop(self) -> bool:
         """Run rounds in the C++ executors (GPU; single process or the IPC transport)."""
-        if not (self.env.gpu and self.cfg.native_loop):
+        if not (self.env.gpu and self.cfg.native_loop) or self.cfg.verify_beta:
             return False
         if self.tx is not None and self.tx.name != "ipc":
             return False
@@ -344,6 +344,8 @@ class Trainer:
                 self._checkpoint(i + 1, timeset, worker_timeset)
         col.drain(R - 1, max(cfg.round_timeout, 60.0))
         col.close()
+        if cfg.verify_beta and env.world > 1:
+            self._verify_beta_checksums(start)
         if upd_events:
             torch.cuda.synchronize(env.device)
             for i, ev0, ev1 in upd_events:  # + the update kernel's own duration (reference: decode + update)
@@ -468,6 +470,19 @@ class Trainer:
         del pump
         return None
 
+    def _verify_beta_checksums(self, start: int) -> None:
+        """Race detector: every worker's beta, before and after its gradient read it,
+        must equal the beta the master published for that round."""
+        R = self.cfg.num_itrs
+        want = self.beta_in[:R].double().sum(1).cpu().numpy()
+        got = self.env.gather_objects(None)
+        for r in range(1, self.env.world):
+            sums = got[r]
+            for i in range(start, R):
+                if not (sums[i, 0] == want[i] and sums[i, 1] == want[i]):
+                    raise RuntimeError(f"beta race detected: rank {r} round {i}: master {want[i]!r}, worker "
+                                       f"before/after gradient {sums[i, 0]!r}/{sums[i, 1]!r}")
+
     def _send_beta(self, i: int):
         if self.tx is not None:
             self.tx.send_beta(i, self.beta_in[i])
@@ -480,15 +495,22 @@ class Trainer:
         cfg, env, tx = self.cfg, self.env, self.tx
         R, K, n = cfg.num_itrs, self.K, self.n_loc
         t0 = None
+        bsum = torch.full((R, 2), float("nan"), dtype=torch.float64, device=env.device) if cfg.verify_beta else None
         for i in range(start, R):
             if timed_start is not None and i == timed_start:
                 t0 = self._timed_fence()
             slot = i % K
             b = tx.recv_beta(i)
+            if bsum is not None:
+                bsum[i, 0] = b.double().sum()
             if n:
                 self.plan.run(b, self.G[slot])
                 tx.send_msgs(i, self.G[slot, :n])
+            if bsum is not None:  # beta must be unchanged after the gradient read it
+                bsum[i, 1] = b.double().sum()
         tx.finish()
+        if bsum is not None:
+            env.gather_objects(bsum.cpu().numpy())
         if timed_start is not None:
             self.worker_timed_seconds = self._timed_fence() - t0
         self._sync()

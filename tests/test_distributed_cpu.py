@@ -27,10 +27,15 @@ def _worker(rank, world, port, case, rule, out_path, extra):
     from erasurehead_amd.parallel.dist import init_distributed
 
     env = init_distributed("cpu")
+    extra = dict(extra)
+    corrupt = extra.pop("corrupt", False)
     cfg, src, sch, parts = make(case, rule, **extra)
     if extra.get("delay_mode"):
         cfg.add_delay = 1
     tr = Trainer(cfg, env, src, scheme=sch)
+    if corrupt and not env.is_master:  # simulate a buffer overwritten while the gradient reads it
+        run = tr.plan.run
+        tr.plan.run = lambda b, G: (run(b, G), b.add_(1e-9))[0]
     res = tr.run()
     if env.is_master:
         np.savez(out_path, betaset=res.betaset, ws=res.worker_timeset, arrivals=np.array(
@@ -65,3 +70,12 @@ def test_multiprocess_delay_straggler_skipped(tmp_path):
     r = _run(3, case, "GD", tmp_path, delay_mode="fixed", fixed_stragglers=[1, 3, 5], fixed_sleep=0.05)
     for a in r["arrivals"]:
         assert {w for (w, p) in a} == {1, 3, 5}  # 0-based: workers 2,4,6 are the fast ones
+
+
+def test_multiprocess_verify_beta(tmp_path):
+    """The beta race detector (checksums before/after every worker gradient) passes on a clean run."""
+    case = (1, 0, 3, 7, 2, 4)
+    r = _run(2, case, "AGD", tmp_path, verify_beta=True)
+    assert r["betaset"].shape[0] == 6
+    with pytest.raises(Exception, match="beta race detected"):
+        _run(2, case, "AGD", tmp_path, verify_beta=True, corrupt=True)
