@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import os
 import sys
+import time
 import uuid
 from typing import Dict, List, Optional
 
@@ -206,6 +207,7 @@ class IpcTransport(Transport):
 
     name = "ipc"
     FINE = True  # mailboxes in fine-grained (coherent) device memory
+    HANDSHAKE_TIMEOUT = 30.0  # seconds for the whole setup handshake
 
     def __init__(self, *a, timeout: float = 600.0, **kw):
         super().__init__(*a, **kw)
@@ -312,8 +314,9 @@ class IpcTransport(Transport):
                 self.C.put_signal(puts[k:k + 16], self.counters)
             torch.cuda.synchronize(env.device)
             rbuf = self.make_rbuf()
+            deadline = time.monotonic() + self.HANDSHAKE_TIMEOUT
             for r in range(1, env.world):
-                if not self.flags.wait_ge(env.world + r, 1, 120.0):
+                if not self.flags.wait_ge(env.world + r, 1, max(0.0, deadline - time.monotonic())):
                     ok = False
                     continue
                 n = self.remote_counts.get(r, 0)
@@ -326,7 +329,7 @@ class IpcTransport(Transport):
                 self.flags.store(r, 0)
         else:
             r = env.rank
-            if self.flags.wait_ge(r, 1, 120.0):
+            if self.flags.wait_ge(r, 1, self.HANDSHAKE_TIMEOUT):
                 pat = torch.arange(self.ld, dtype=self.dtype, device=env.device) + 0.5
                 ok = bool(torch.equal(self.inbox[self.R], pat))
                 n = self.n_local
