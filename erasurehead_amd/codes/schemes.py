@@ -73,6 +73,7 @@ class Scheme:
     has_linear = False  # reference has a least-squares variant
     needs_B = False
     decode_kind = DEC_SUM
+    logs_eval_loading = False  # naive/coded print ">> Loaded j" per dense training partition (ref naive.py:160-164)
 
     def __post_init__(self):
         if self.n_workers < 1:
@@ -178,6 +179,7 @@ class Naive(Scheme):
 
     has_linear = True
     marks_unused = False
+    logs_eval_loading = True
 
     def _build(self):
         self.messages = [Message(w, 0, [(w, 1.0)]) for w in range(self.n_workers)]
@@ -203,6 +205,7 @@ class Cyclic(Scheme):
     init_zero = True
     needs_B = True
     decode_kind = DEC_TABLE
+    logs_eval_loading = True
 
     def _build(self):
         self._check_s()

@@ -48,7 +48,13 @@ def evaluate(trainer: Trainer, res: TrainResult, log=None, write: bool = True) -
     B = torch.zeros((R, ld), dtype=torch.float64, device=dev)
     B[:, :d] = torch.from_numpy(res.betaset).to(dev)
     kind = trainer.loss
-    sums, n_train = loss_sums(trainer.source.train_eval_chunks(eval_partitions(trainer), prec, dev), B, d, kind)
+    parts = eval_partitions(trainer)
+    if cfg.verbose:
+        log(report.total_time_line(res.total_time))
+        if trainer.scheme.logs_eval_loading and not trainer.source.is_sparse:
+            for p in parts:
+                log(">> Loaded %d" % (p + 1))
+    sums, n_train = loss_sums(trainer.source.train_eval_chunks(parts, prec, dev), B, d, kind)
     Xt, yt = trainer.source.test(prec, dev)
     P = predictions(Xt, B, d)
     from ..ops.eval import _loss_torch
@@ -59,7 +65,6 @@ def evaluate(trainer: Trainer, res: TrainResult, log=None, write: bool = True) -
     testing_loss = tsum / max(1, n_test)
     auc = auc_columns(yt, P) if kind == LOGISTIC else np.zeros(R)
     if cfg.verbose:
-        log(report.total_time_line(res.total_time))
         for i in range(R):
             if kind == LOGISTIC:
                 log(report.logistic_line(i, training_loss[i], testing_loss[i], auc[i], res.timeset[i]))

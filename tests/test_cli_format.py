@@ -46,6 +46,12 @@ def test_console_and_files(args, prefix, tmp_path, capsys):
     assert len(tot) == 1 and re.match(r"^Total Time Elapsed: \d+\.\d{3}$", tot[0])
     its = [l for l in lines if l.startswith("Iteration ")]
     assert [int(LOGISTIC_LINE.match(l).group(1)) for l in its] == list(range(12))
+    loaded = [l for l in lines if l.startswith(">> Loaded ")]
+    if prefix.startswith(("naive", "coded")):  # ref naive.py:160-164: partitions 1..W-1 (the off-by-one)
+        assert loaded == [">> Loaded %d" % j for j in range(1, 4)]
+        assert lines.index(tot[0]) < lines.index(loaded[0]) < lines.index(its[0])
+    else:
+        assert loaded == []
     assert lines[-1] == ">>> Done"
     res = os.path.join(ddir, "results")
     for kind in ("training_loss", "testing_loss", "auc", "timeset"):
