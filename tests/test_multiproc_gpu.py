@@ -49,6 +49,20 @@ def test_ipc_multiprocess_matches_replay(world, case_i, tmp_path):
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
 
 
+@pytest.mark.parametrize("world,case_i", [(8, 5), (5, 5), (4, 7)])
+def test_ipc_many_ranks(world, case_i, tmp_path):
+    """The 8-GPU layout (one logical worker per rank, 8 ranks) rehearsed on one GPU."""
+    from oracle import replay
+    from test_engine_cpu import CASES, make
+
+    r = _launch(world, case_i, "AGD", str(tmp_path / "m.npz"))
+    assert str(r["transport"]) == "ipc"
+    cfg, src, sch, parts = make(CASES[case_i], "AGD")
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+
+
 def test_ipc_multiprocess_delayed_agc(tmp_path):
     """AGC (W=6, s=2, k=4) with the reference delay model: the decode only uses fast workers."""
     from oracle import replay
