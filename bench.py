@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--tasks", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl"])
+    ap.add_argument("--round-timeout", type=float, default=120.0, help="bounds any hang (a round takes ms)")
     return ap.parse_args()
 
 
@@ -65,7 +66,7 @@ def main() -> int:
                          a.stragglers, 0, a.coded_ver, a.num_collect, a.add_delay, a.update_rule,
                          num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234, seed=0,
                          allow_uneven_groups=True, verbose=False, tasks=a.tasks,
-                         transport=a.transport)
+                         transport=a.transport, round_timeout=a.round_timeout)
 
     t_setup = time.perf_counter()
     trainer = Trainer(make_cfg(a.warmup + a.steps), env)
