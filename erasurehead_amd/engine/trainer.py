@@ -141,6 +141,8 @@ class Trainer:
         self.ld = self.prec.ld(self.d)
         dev = self.env.device
         needed = sorted({p for m in self.local_msgs for p, _ in m.segments})
+        if not source.is_sparse and self.env.gpu:
+            self._check_hbm(len(needed) * sch.rows_per_partition * self.ld * self.prec.storage_bytes)
         t0 = time.perf_counter()
         parts = {p: source.partition(p, self.prec, dev) for p in needed}
         self.load_seconds = time.perf_counter() - t0
@@ -151,6 +153,15 @@ class Trainer:
             kw = {"target_tasks": cfg.tasks} if cfg.tasks else {}
             self.plan = DenseGradPlan(segs, parts, self.prec, self.loss, self.d, **kw)
         self._parts = parts
+
+    def _check_hbm(self, need_bytes: int) -> None:
+        """Fail early (and say what to change) when this rank's resident partitions cannot fit."""
+        free, total = torch.cuda.mem_get_info(self.env.device)
+        if need_bytes > 0.92 * free:
+            raise MemoryError(
+                f"rank {self.env.rank}: its logical workers need {need_bytes / 2**30:.1f} GiB of resident "
+                f"partitions but only {free / 2**30:.1f} of {total / 2**30:.1f} GiB HBM are free; launch more GPU "
+                f"ranks (torchrun --nproc-per-node) or use --precision fp32/bf16")
 
     def _setup_buffers(self):
         cfg, env = self.cfg, self.env

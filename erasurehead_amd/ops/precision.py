@@ -22,6 +22,10 @@ class Precision:
     acc: torch.dtype
     vec: int  # elements per 16-byte vector load
 
+    @property
+    def storage_bytes(self) -> int:
+        return 16 // self.vec
+
     def ld(self, d: int) -> int:
         """Leading dimension: d rounded up to the 16-byte vector width."""
         return ((d + self.vec - 1) // self.vec) * self.vec

@@ -79,3 +79,24 @@ def test_ipc_multiprocess_delayed_agc(tmp_path):
             assert slowest not in used or len(used) == 6
     ref = replay(sch, parts, r["beta0"], arrivals, "GD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+
+
+def test_cli_two_ranks_synthetic(tmp_path):
+    """main.py under torchrun (2 ranks sharing the GPU): reference console lines and result files."""
+    import re
+
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    root = str(tmp_path) + "/"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(os.path.dirname(HERE), "main.py"),
+           "7", "60000", "200", root, "0", "synthetic", "1", "2", "0", "3", "4", "0", "AGD", "--data", "synthetic",
+           "--num-itrs", "20", "--seed", "0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = r.stdout.splitlines()
+    assert any(l.startswith("---- Starting Approx Coding Iterations for 2 stragglers") for l in lines)
+    its = [l for l in lines if re.match(r"^Iteration \d+: Train Loss = ", l)]
+    assert len(its) == 20
+    losses = [float(l.split("Train Loss = ")[1].split(",")[0]) for l in its]
+    assert losses[-1] < losses[0]
+    assert os.path.exists(os.path.join(root, "results", "replication_acc_2_training_loss.dat"))
