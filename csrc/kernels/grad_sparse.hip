@@ -80,21 +80,26 @@ ell_rowpass(const int* __restrict__ idx, const A* __restrict__ vals, const A* __
             long long nrows, int m) {
   const long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (row >= nrows) return;
-  A z0 = A(0), z1 = A(0);
+  // four independent gather chains per thread: enough loads in flight to stream idx at HBM rate
+  A z[4] = {A(0), A(0), A(0), A(0)};
   int k = 0;
-  for (; k + 1 < m; k += 2) {  // two independent gathers in flight
-    const int c0 = idx[static_cast<long long>(k) * nrows + row];
-    const int c1 = idx[static_cast<long long>(k + 1) * nrows + row];
-    const A v0 = VALS ? vals[static_cast<long long>(k) * nrows + row] : A(1);
-    const A v1 = VALS ? vals[static_cast<long long>(k + 1) * nrows + row] : A(1);
-    z0 = fma(v0, beta[c0], z0);
-    z1 = fma(v1, beta[c1], z1);
+  for (; k + 3 < m; k += 4) {
+    int c[4];
+    A v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      c[u] = __builtin_nontemporal_load(idx + static_cast<long long>(k + u) * nrows + row);
+      v[u] = VALS ? vals[static_cast<long long>(k + u) * nrows + row] : A(1);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) z[u] = fma(v[u], beta[c[u]], z[u]);
   }
-  if (k < m) {
+  for (; k < m; ++k) {
     const int c0 = idx[static_cast<long long>(k) * nrows + row];
     const A v0 = VALS ? vals[static_cast<long long>(k) * nrows + row] : A(1);
-    z0 = fma(v0, beta[c0], z0);
+    z[k & 3] = fma(v0, beta[c0], z[k & 3]);
   }
+  const A z0 = (z[0] + z[1]) + (z[2] + z[3]), z1 = A(0);
   rbuf[row] = residual<LOSS, A>(z0 + z1, y[row], coef[row]);
 }
 

@@ -1,0 +1,112 @@
+"""Kernel microbenchmarks on one MI355X: the worker-gradient kernels in isolation.
+
+    python tools/bench_kernels.py [--out FILE]
+
+* dense ``grad_dense`` (fused single pass; two-pass above d = 2048 fp64) at several widths,
+  reported as effective HBM bandwidth over the bytes of X it must stream;
+* sparse one-hot gradients on covtype / kc_house / amazon-shaped data (the reference's real
+  datasets, synthetic stand-ins of the same shape): the ELL path against the generic
+  sorted-COO path.
+
+Times are HIP-event medians over 50 launches after 5 warm-up launches.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _time(fn, reps=50, warm=5):
+    import torch
+
+    for _ in range(warm):
+        fn()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evs:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in evs]))  # ms
+
+
+def dense_cases(out):
+    import torch
+
+    from erasurehead_amd.models.losses import LOGISTIC
+    from erasurehead_amd.ops import DenseGradPlan, get_precision
+
+    for prec_name in ("fp64", "fp32", "bf16"):
+        prec = get_precision(prec_name)
+        for d in (1000, 2048, 4000):
+            rows = max(1, int(2e9 // (d * 8)))  # ~2 GB of fp64 X
+            parts = {}
+            for p in range(4):
+                X = torch.randn(rows // 4, prec.ld(d), device="cuda", dtype=torch.float32).to(prec.storage)
+                y = torch.where(torch.rand(rows // 4, device="cuda") > 0.5, 1.0, -1.0).to(prec.acc)
+                parts[p] = (X.contiguous(), y)
+            plan = DenseGradPlan([[(0, 1.0), (1, 1.0)], [(2, 1.0), (3, 1.0)]], parts, prec, LOGISTIC, d)
+            beta = torch.randn(prec.ld(d), device="cuda", dtype=prec.acc) * 0.01
+            G = plan.out_buffer()[0]
+            ms = _time(lambda: plan.run(beta, G))
+            gb = plan.bytes_per_round / 1e9
+            r = {"kernel": "grad_dense" + ("" if plan.cpl else "_twopass"), "precision": prec_name, "d": d,
+                 "rows": rows, "ms": ms, "x_gbytes": gb, "effective_TBps": gb / ms}
+            out.append(r)
+            print(json.dumps(r), flush=True)
+            del parts, plan
+            torch.cuda.empty_cache()
+
+
+def sparse_cases(out):
+    import torch
+
+    from erasurehead_amd.data.synthetic import REAL_SHAPES, onehot_partitions
+    from erasurehead_amd.models.losses import LOGISTIC
+    from erasurehead_amd.ops import SparseGradPlan, get_precision
+
+    prec = get_precision("fp64")
+    for name in ("covtype", "kc_house_data", "amazon-dataset"):
+        n, d, f = REAL_SHAPES[name]
+        W = 8
+        parts_l, _, dd = onehot_partitions(n, d, f, W, seed=1)
+        parts = {p: xy for p, xy in enumerate(parts_l)}
+        msgs = [[(w, 1.0), ((w + 1) % W, 1.0)] for w in range(W)]  # 8 workers, 2 partitions each (s = 1)
+        for use_ell in (True, False):
+            plan = SparseGradPlan(msgs, parts, prec, LOGISTIC, dd, device="cuda", use_ell=use_ell)
+            beta = torch.randn(prec.ld(dd), device="cuda", dtype=torch.float64) * 0.1
+            G = plan.out_buffer()[0]
+            ms = _time(lambda: plan.run(beta, G))
+            r = {"kernel": "grad_ell" if plan.ell else "grad_sparse_coo", "dataset_shape": name, "rows": plan.nrows,
+                 "nnz": int(plan.nnz), "d": dd, "ms": ms, "nnz_per_us": plan.nnz / (ms * 1e3)}
+            out.append(r)
+            print(json.dumps(r), flush=True)
+            del plan
+            torch.cuda.empty_cache()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "kernels.jsonl"))
+    ap.add_argument("--only", choices=["dense", "sparse"], default=None)
+    a = ap.parse_args()
+    out = []
+    if a.only in (None, "dense"):
+        dense_cases(out)
+    if a.only in (None, "sparse"):
+        sparse_cases(out)
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        for r in out:
+            f.write(json.dumps(r) + "\n")
+
+
+if __name__ == "__main__":
+    main()
