@@ -327,6 +327,7 @@ class MasterPump {
 
   void set_decode(int kind, const std::vector<int>& group_of, int n_groups) {
     need((int)group_of.size() == W_, "group_of must have W entries");
+    need(!((kind == kTable || kind == kPartialTable) && W_ > 64), "table decode supports at most 64 workers");
     decode_kind_ = kind;
     group_of_ = group_of;
     n_groups_ = n_groups;

@@ -260,6 +260,8 @@ class Trainer:
             return False
         if self.tx is not None and self.tx.name != "ipc":
             return False
+        if self.scheme.decode_kind in (3, 4) and self.cfg.n_workers > 64:  # 64-bit completion masks
+            return False
         return self.n_loc > 0 or self.env.is_master
 
     def _timed_fence(self):
@@ -398,7 +400,8 @@ class Trainer:
                           co[0][4] if co else 0, [float(x) for x in delay_table.ravel()], self.rule_kind,
                           self.rule_k, bool(self.drain))
         pump.set_decode(sch.decode_kind, list(sch.group_of), sch.n_groups)
-        if sch.decode_kind in (3, 4):
+        table_decoded = sch.decode_kind in (3, 4)
+        if table_decoded and math.comb(W, sch.n_stragglers) <= 20000:  # else filled on demand below
             for mask, a in sch.decode_table().items():
                 pump.add_table(mask, [float(x) for x in a])
         timeset, loop_time, worker_timeset = np.zeros(R), np.zeros(R), np.zeros((R, W))
@@ -423,11 +426,19 @@ class Trainer:
             publish = i + 1 < R and not fence_next
             status, arr, t0, tdec, tend = pump.finish(i, publish)
             arrivals = [Arrival(w, p, t) for (w, p, t) in arr]
-            if status == 2:  # completion pattern outside the precomputed table (a timed-out round)
+            if status == 2:  # completion pattern not in the table yet (timed-out round or a large C(W, s))
                 used = sch.decode(arrivals)
+                timed_out = len(sch.completed_workers(arrivals)) < self.rule_k
+                if table_decoded and not timed_out:
+                    mask = sum(1 << w for w in sch.completed_workers(arrivals))
+                    coefs = [0.0] * W
+                    for (w, p), c in used.items():
+                        if p == 0:
+                            coefs[w] = float(c)
+                    pump.add_table(mask, coefs)
                 status, arr, t0, tdec, tend = pump.resolve(i, [(w, p, float(c)) for (w, p), c in used.items()],
                                                            publish)
-                timeouts += 1
+                timeouts += int(timed_out)
             elif status == 1:
                 timeouts += 1
             begun = publish

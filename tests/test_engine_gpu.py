@@ -88,3 +88,22 @@ def test_native_loop_timeout_falls_back_to_host_decode(native):
     assert res.timeouts == 3
     assert np.all(res.worker_timeset[:, [1, 3]] == -1)
     assert np.all(np.isfinite(res.betaset))
+
+
+def test_native_loop_large_cyclic_table_on_demand(native):
+    """C(20, 8) = 125970 completion patterns: the native executor fills its decode table on demand."""
+    from erasurehead_amd.codes import make_scheme
+
+    W, s, rows, d = 20, 8, 12, 9
+    src = _source(W, rows, d)
+    out = {}
+    for dev in ("cpu", "cuda"):
+        cfg = RunConfig(W + 1, rows * W, d, "/tmp/eh_gpu_eng/", 0, "x", 1, s, 0, 0, 0, 0, "GD", num_itrs=4, seed=0,
+                        verbose=False)
+        sch = make_scheme("coded", W, s, rows * W, rng=np.random.RandomState(0))
+        tr = Trainer(cfg, DistEnv(device=torch.device(dev)), src, scheme=sch)
+        assert tr.native_loop == (dev == "cuda")
+        res = tr.run()
+        assert res.timeouts == 0
+        out[dev] = res.betaset
+    np.testing.assert_allclose(out["cuda"], out["cpu"], rtol=1e-7, atol=1e-9)
