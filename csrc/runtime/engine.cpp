@@ -374,7 +374,7 @@ class MasterPump {
       col_->add_flag_probe(m.w, m.p, i, m.flag, static_cast<uint64_t>(i + 1), dl[m.w]);
   }
 
-  // Returns (status, arrivals [(worker, part, t_rel)], t_start, t_decoded, t_end):
+  // Returns (status, arrivals [(worker, part, t_rel)], t_start, t_decoded, t_end, t_waited):
   // status 0 ok, 1 timeout (decoded with what arrived), 2 host decode needed (no table
   // row: call resolve()).
   py::tuple finish(int i, bool publish_next) {
@@ -384,6 +384,7 @@ class MasterPump {
     {
       py::gil_scoped_release nogil;
       const bool ok = col_->wait(timeout_);
+      t_waited_ = eh::Collector::now();
       arr = col_->arrivals();
       std::vector<std::pair<const void*, double>> used;
       const bool decoded = decode(i, arr, used);
@@ -516,7 +517,7 @@ class MasterPump {
   py::tuple pack(int status, const std::vector<eh::Arrival>& arr, int i, double t_dec, double t_end) const {
     py::list lst;
     for (const auto& a : arr) lst.append(py::make_tuple(a.worker, a.part, a.t_rel));
-    return py::make_tuple(status, lst, t_start_[i], t_dec, t_end);
+    return py::make_tuple(status, lst, t_start_[i], t_dec, t_end, t_waited_);
   }
 
   eh::Collector* col_;
@@ -537,6 +538,7 @@ class MasterPump {
   std::vector<int> group_of_;
   std::map<uint64_t, std::vector<double>> table_;
   std::vector<double> t_start_;
+  double t_waited_ = 0.0;  // host time the last wait() returned (phase timing)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> upd_ev_;
   std::vector<hipEvent_t> loc_ev_;
 };

@@ -424,7 +424,7 @@ class Trainer:
                 log(report.iteration_tick(i))
             fence_next = timed_start is not None and i + 1 == timed_start
             publish = i + 1 < R and not fence_next
-            status, arr, t0, tdec, tend = pump.finish(i, publish)
+            status, arr, t0, tdec, tend, twait = pump.finish(i, publish)
             arrivals = [Arrival(w, p, t) for (w, p, t) in arr]
             if status == 2:  # completion pattern not in the table yet (timed-out round or a large C(W, s))
                 used = sch.decode(arrivals)
@@ -436,12 +436,15 @@ class Trainer:
                         if p == 0:
                             coefs[w] = float(c)
                     pump.add_table(mask, coefs)
-                status, arr, t0, tdec, tend = pump.resolve(i, [(w, p, float(c)) for (w, p), c in used.items()],
-                                                           publish)
+                status, arr, t0, tdec, tend, _ = pump.resolve(i, [(w, p, float(c)) for (w, p), c in used.items()],
+                                                              publish)
                 timeouts += int(timed_out)
             elif status == 1:
                 timeouts += 1
             begun = publish
+            self.timer.add("wait_k", twait - t0)
+            self.timer.add("decode_update", tdec - twait)
+            self.timer.add("drain", tend - tdec)
             timeset[i] = tdec - t0
             loop_time[i] = tend - t0
             worker_timeset[i] = sch.worker_times(arrivals)
