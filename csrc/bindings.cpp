@@ -253,6 +253,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("step", &eh::Collector::step, py::call_guard<py::gil_scoped_release>())
       .def("wait", &eh::Collector::wait, py::call_guard<py::gil_scoped_release>())
       .def("drain", &eh::Collector::drain, py::call_guard<py::gil_scoped_release>())
+      .def("wait_seen", &eh::Collector::wait_seen, py::call_guard<py::gil_scoped_release>())
       .def("arrivals", &eh::Collector::arrivals)
       .def("late_arrivals", &eh::Collector::late_arrivals)
       .def("pending", &eh::Collector::pending)

@@ -242,6 +242,26 @@ bool Collector::drain(int round, double timeout) {
   }
 }
 
+bool Collector::wait_seen(int round, double timeout) {
+  const double t0 = now();
+  for (;;) {
+    const double t = now();
+    poll_events(t);
+    process_ready(t, true);
+    bool left = false;
+    for (int id : live_) {
+      const Probe& p = probes_[id];
+      if (p.round <= round && !p.seen) {
+        left = true;
+        break;
+      }
+    }
+    if (!left) return true;
+    if (t - t0 > timeout) return false;
+    pause_for(2e-5);
+  }
+}
+
 std::vector<Arrival> Collector::late_arrivals(int round) const {
   if (round != round_) return {};
   return late_;

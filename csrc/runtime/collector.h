@@ -68,6 +68,9 @@ class Collector {
   bool wait(double timeout);
   // Blocking: until every probe of rounds <= `round` has arrived (dead ones: been seen).
   bool drain(int round, double timeout);
+  // Blocking: until every probe of rounds <= `round` has been SEEN (its data landed), whatever
+  // its virtual arrival time — the condition for reusing that round's mailbox slot.
+  bool wait_seen(int round, double timeout);
 
   const std::vector<Arrival>& arrivals() const { return cur_; }
   std::vector<Arrival> late_arrivals(int round) const;  // arrivals after the stop, this round

@@ -342,7 +342,7 @@ class MasterPump {
     need(i >= 0 && i < R_, "round out of range");
     need(beta_in_.defined(), "set_state first");
     const int slot = i % K_;
-    if (i >= K_) col_->drain(i - K_, timeout_);  // the ring slot's previous round fully received
+    if (i >= K_) col_->wait_seen(i - K_, timeout_);  // the ring slot's previous round has landed
     const double t = eh::Collector::now();
     col_->begin_round(i, t, stop_rule_, k_);
     t_start_[i] = t;

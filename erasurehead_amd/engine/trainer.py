@@ -170,7 +170,7 @@ class Trainer:
         n_loc = len(self.local_msgs)
         n_rem = sum(len(v) for v in self.remote_msgs.values())
         per_round = max(1, (n_loc + n_rem) * ld * es)
-        K = int(max(2, min(R, (1 << 30) // per_round)))
+        K = int(max(2, min(R, (4 << 30) // per_round)))  # <= 4 GiB of message ring (288 GB HBM)
         self.K = int(env.broadcast_object(K, 0)) if env.world > 1 else K  # the mailbox ring is shared: one K
         self.G = torch.zeros((self.K, max(1, n_loc), ld), dtype=acc, device=dev)
         self.n_loc = n_loc
@@ -296,7 +296,7 @@ class Trainer:
                 log(report.iteration_tick(i))
             slot = i % K
             if i >= K:
-                col.drain(i - K)  # ring slot reuse: round i-K fully received
+                col.wait_seen(i - K, cfg.round_timeout)  # ring slot reuse: round i-K's data has landed
             t_start = col.now()
             col.begin_round(i, t_start, self.rule_kind, self.rule_k)
             delays = delay_table[i]

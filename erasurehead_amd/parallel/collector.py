@@ -128,5 +128,18 @@ class ArrivalCollector:
             self._keep.clear()
         return ok
 
+    def wait_seen(self, i: int, timeout: float = math.inf) -> bool:
+        """Wait until the data of every message of rounds <= i has landed (mailbox slot reuse)."""
+        if self._pending_host == 0 and self.gpu:
+            return self.c.wait_seen(int(i), float(min(timeout, 1e9)))
+        t0 = time.perf_counter()
+        while True:
+            self._poll_host()
+            if self.c.wait_seen(int(i), 0.0):
+                return True
+            if time.perf_counter() - t0 > timeout:
+                return False
+            time.sleep(1e-4)
+
     def late(self) -> List[Arrival]:
         return [Arrival(a.worker, a.part, a.t_rel) for a in self.c.late_arrivals(self.round)]

@@ -122,3 +122,20 @@ def test_collector_host_asan_ubsan():
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "collector selftest ok" in r.stdout
+
+
+def test_wait_seen_ignores_virtual_delay(C):
+    """Slot reuse needs the data, not the virtual arrival: a straggler seen long before its
+    virtual arrival does not block wait_seen."""
+    col = C.Collector(2, [0, 1], 2)
+    t0 = C.Collector.now()
+    col.begin_round(0, t0, RULE_COUNT, 1)
+    a = col.add_host_probe(0, 0, 0, 0.0)
+    b = col.add_host_probe(1, 0, 0, 30.0)  # arrives (virtually) 30 s later
+    col.mark_seen(a, t0)
+    assert not col.wait_seen(0, 0.0)
+    col.mark_seen(b, t0)
+    t = time.perf_counter()
+    assert col.wait_seen(0, 5.0)
+    assert time.perf_counter() - t < 1.0
+    assert not col.drain(0, 0.01)  # the reference Waitall still waits for the virtual arrival
