@@ -74,7 +74,9 @@ void grad_dense(int64_t dtype, int64_t loss, int64_t cpl, const Tensor& segs, co
   need(G.dim() == 2 && G.size(0) == nslots && G.size(1) == ld, "G must be [nslots, ld]");
   need(beta.numel() >= ld, "beta must have >= ld elements");
   need(ld % (dtype == 0 ? 2 : dtype == 1 ? 4 : 8) == 0, "ld must be a multiple of the 16-byte vector width");
-  need(cpl * 64 >= ld, "cpl * 64 must cover ld");
+  need(cpl <= 32 ? cpl * 64 >= ld
+                   : ((cpl == 256 || cpl == 512) && cpl * (dtype == 0 ? 16 : 32) >= ld),
+         "cpl (narrow: columns per lane, wide: block size) must cover ld");
   const int ac = dtype == 0 ? 0 : 1;
   need(acc_code(beta) == ac && acc_code(slab) == ac && acc_code(G) == ac, "beta/slab/G dtype mismatch");
   need_part(part, nslots, ld, ac);

@@ -152,6 +152,97 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
   }
 }
 
+// ----- Wide rows (2048 < d <= 8192 fp64 / 16384 fp32,bf16): still ONE pass over X. -----
+// A whole workgroup owns each row: thread t holds columns (j*BS + t)*VN + [0, VN) for the
+// NV 16-byte vectors j, so every load instruction of the block is fully coalesced and each
+// thread keeps its slice of beta and of the gradient in registers.  The row dot product is
+// finished across the block through LDS once per PAIR of rows (double-buffered LDS slots,
+// one barrier per pair); the loss residual is then applied from registers, so X is read
+// from HBM exactly once.  Columns are disjoint per thread: the slab row is written
+// directly, no LDS fold.
+template <typename T, typename A, int NV, int BS, int LOSS>
+__global__ void __launch_bounds__(BS)
+grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
+                const A* __restrict__ beta, A* __restrict__ slab, int ld) {
+  constexpr int VN = Vec16<T>::N;
+  constexpr int NW = BS / kWave;
+  __shared__ A part[2][2][NW];  // [buffer][row of the pair][wave]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const Task task = tasks[blockIdx.x];
+  const Segment seg = segs[task.seg];
+  const T* __restrict__ X = static_cast<const T*>(seg.X);
+  const A* __restrict__ Y = static_cast<const A*>(seg.y);
+  const A coef = static_cast<A>(seg.coef);
+
+  bool valid[NV];
+  A b[NV][VN], g[NV][VN];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * BS + tid) * VN;
+    valid[j] = c0 < ld;
+#pragma unroll
+    for (int v = 0; v < VN; ++v) {
+      b[j][v] = valid[j] ? beta[c0 + v] : A(0);
+      g[j][v] = A(0);
+    }
+  }
+  int buf = 0;
+  for (int r = task.row_begin; r < task.row_end; r += 2) {
+    const bool two = r + 1 < task.row_end;
+    const T* x0 = X + static_cast<long long>(r) * ld;
+    const T* x1 = X + static_cast<long long>(two ? r + 1 : r) * ld;
+    A a0[NV][VN], a1[NV][VN];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c0 = (j * BS + tid) * VN;
+      if (valid[j]) {
+        Vec16<T>::load(x0 + c0, a0[j]);
+        Vec16<T>::load(x1 + c0, a1[j]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < VN; ++v) { a0[j][v] = A(0); a1[j][v] = A(0); }
+      }
+    }
+    A z0 = A(0), z1 = A(0);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v) {
+        z0 = fma(a0[j][v], b[j][v], z0);
+        z1 = fma(a1[j][v], b[j][v], z1);
+      }
+    z0 = wave_allreduce_sum(z0);
+    z1 = wave_allreduce_sum(z1);
+    if (lane == 0) {
+      part[buf][0][wid] = z0;
+      part[buf][1][wid] = z1;
+    }
+    __syncthreads();
+    A s0 = A(0), s1 = A(0);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {  // fixed order: every thread gets the bitwise-same sums
+      s0 += part[buf][0][w];
+      s1 += part[buf][1][w];
+    }
+    buf ^= 1;  // the next pair writes the other buffer: no second barrier needed
+    const A r0 = residual<LOSS, A>(s0, Y[r], coef);
+    const A r1 = two ? residual<LOSS, A>(s1, Y[r + 1], coef) : A(0);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v) g[j][v] = fma(r1, a1[j][v], fma(r0, a0[j][v], g[j][v]));
+  }
+  A* out = slab + static_cast<long long>(blockIdx.x) * ld;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * BS + tid) * VN;
+    if (valid[j]) {
+#pragma unroll
+      for (int v = 0; v < VN; ++v) out[c0 + v] = g[j][v];
+    }
+  }
+}
+
 // Slab reduction, two fixed-order stages (bitwise reproducible, no atomics):
 //   stage 1: block (64-column chunk, slot, split) — 4 waves stride over the split's tasks,
 //            lane = column, then fold the waves in LDS -> part[slot][split][c]
@@ -267,9 +358,31 @@ xt_r_tiles(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
 // Host launchers (called from bindings.cpp).
 namespace eh {
 
+// Wide kernel: 16 elements per thread per row for fp64 (NV = 8), 32 for fp32 (NV = 8) and
+// bf16 (NV = 4); the block size BS (256 / 512) covers ld.  (1024-thread blocks would cap a
+// wave at 128 VGPRs and spill the two-row register tiles, so wider rows take the two-pass path.)
+template <typename T, typename A, int LOSS>
+static hipError_t launch_wide(int bs, const Segment* segs, const Task* tasks, int ntasks, const A* beta,
+                              A* slab, int ld, hipStream_t st) {
+  constexpr int NV = Vec16<T>::N == 8 ? 4 : 8;
+  const dim3 grid(ntasks);
+  switch (bs) {
+    case 256:
+      hipLaunchKernelGGL((grad_dense_wide<T, A, NV, 256, LOSS>), grid, dim3(256), 0, st, segs, tasks, beta, slab, ld);
+      break;
+    case 512:
+      hipLaunchKernelGGL((grad_dense_wide<T, A, NV, 512, LOSS>), grid, dim3(512), 0, st, segs, tasks, beta, slab, ld);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 template <typename T, typename A, int LOSS>
 static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
                                    const A* beta, A* slab, int ld, hipStream_t st) {
+  if (cpl >= 256) return launch_wide<T, A, LOSS>(cpl, segs, tasks, ntasks, beta, slab, ld, st);
   const dim3 block(256);
   const dim3 grid(ntasks);
   constexpr int VN = Vec16<T>::N;

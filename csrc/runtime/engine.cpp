@@ -150,7 +150,9 @@ std::shared_ptr<GradLauncher> make_dense(int64_t dtype, int64_t loss, int64_t cp
     g->keep.push_back(*task_row_off);
     g->keep.push_back(*rbuf);
   } else {
-    need(cpl * 64 >= ld, "cpl * 64 must cover ld");
+    need(cpl <= 32 ? cpl * 64 >= ld
+                   : ((cpl == 256 || cpl == 512) && cpl * (dtype == 0 ? 16 : 32) >= ld),
+         "cpl (narrow: columns per lane, wide: block size) must cover ld");
     g->kind = 0;
   }
   return g;

@@ -5,7 +5,8 @@ message (worker, part) is a list of segments (partition, label coefficient).  Ea
 round the plan is executed with one launch set:
 
   dense  -> ``grad_dense`` (fused single pass over X, slab reduction)   csrc/kernels/grad_dense.hip
-            ``grad_dense_twopass`` when d > 2048                          (same file)
+            ``grad_dense_wide`` (a workgroup per row) when d > 2048 fp64       (same file)
+            ``grad_dense_twopass`` beyond 8192 fp64 / 16384 fp32 columns
   sparse -> ``grad_sparse`` (CSR row pass + sorted-COO column pass)      csrc/kernels/grad_sparse.hip
 
 On CPU tensors the same plans run a float64/float32 torch implementation of the
@@ -31,11 +32,22 @@ MIN_ROWS_PER_TASK = 32
 SLAB_SPLITS = 16  # csrc/kernels/grad_dense.hip kSplits
 
 
+WIDE_EPT = {2: 16, 4: 32, 8: 32}  # elements per thread per row of grad_dense_wide (by vector width)
+
+
 def choose_cpl(ld: int, vec: int) -> Optional[int]:
-    """Columns per lane of the fused kernel (64 * cpl >= ld); None -> two-pass path."""
+    """Kernel selector of the single-pass dense gradient.
+
+    2..32       grad_dense_fused: a wave owns a row, ``cpl`` columns per lane (64 * cpl >= ld)
+    256, 512    grad_dense_wide: a workgroup of that many threads owns a row (wide d)
+    None        two-pass path (rows wider than 8192 fp64 / 16384 fp32, bf16 elements)
+    """
     for c in (2, 4, 8, 16, 32):
         if c % vec == 0 and 64 * c >= ld:
             return c
+    for bs in (256, 512):
+        if bs * WIDE_EPT[vec] >= ld:
+            return bs
     return None
 
 

@@ -27,9 +27,10 @@ def _parts(rng, sizes, d, prec):
 
 
 @pytest.mark.parametrize("prec_name,tol", [("fp64", 1e-11), ("fp32", 2e-4), ("bf16", 2e-4)])
-@pytest.mark.parametrize("d", [1, 37, 1000, 2048, 2500])
+@pytest.mark.parametrize("d", [1, 37, 1000, 2048, 2500, 5000, 9000, 17000])
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
 def test_dense_grad(prec_name, tol, d, loss, native):
+    """Narrow fused (d <= 2048), wide single-pass (d <= 8192 fp64 / 16384 fp32) and two-pass kernels."""
     prec = get_precision(prec_name)
     rng = np.random.RandomState(d + loss)
     parts, host = _parts(rng, [257, 64, 1], d, prec)
@@ -49,6 +50,10 @@ def test_dense_grad(prec_name, tol, d, loss, native):
         err = np.max(np.abs(got - ref)) / max(1e-12, np.max(np.abs(ref)))
         assert err < tol, (s, err)
         assert torch.all(G[s, d:] == 0)
+    G2 = plan.out_buffer()[0]
+    plan.native_launcher().launch(beta, G2)  # the native executors' launch path
+    torch.cuda.synchronize()
+    assert torch.equal(G, G2)
 
 
 def test_dense_grad_many_tasks_deterministic(native):
