@@ -33,9 +33,17 @@ def _is_sparse(X) -> bool:
 
 
 def _to_torch_sparse(X, device, dtype):
+    import warnings
+
     import scipy.sparse as sps
 
     X = sps.csr_matrix(X)
+    with warnings.catch_warnings():
+        warnings.filterwarnings("ignore", message="Sparse CSR tensor support is in beta state")
+        return _csr(X, device, dtype)
+
+
+def _csr(X, device, dtype):
     return torch.sparse_csr_tensor(torch.from_numpy(X.indptr.astype(np.int64)),
                                    torch.from_numpy(X.indices.astype(np.int64)),
                                    torch.from_numpy(X.data.astype(np.float64)), size=X.shape,

@@ -119,3 +119,23 @@ def test_generate_cli(tmp_path, capsys):
     X = dio.load_data(os.path.join(d, "1.dat"))
     assert X.shape == (20, 5)
     assert gen_main([]) == 0 and "Usage" in capsys.readouterr().out
+
+
+@pytest.mark.parametrize("coded_ver,prefix", [(1, "partialreplication_1_3_"), (0, "partialcoded_1_3_")])
+def test_partial_schemes_on_prepared_real_data(coded_ver, prefix, tmp_path, capsys):
+    """arrange_real_data with partial_coded=1 -> main.py partial schemes on the partial/ layout."""
+    from erasurehead_amd.cli import main as cli_main
+
+    root = str(tmp_path) + "/"
+    # W = 4, s = 1, P = 3  ->  (P - s) * W = 8 partition files under covtype/partial/8/
+    assert prep_main(["5", root, "covtype", "1", "3", "1", "--make-raw", "1500"]) == 0
+    line = [l for l in capsys.readouterr().out.splitlines() if l.startswith("No. of training samples")][0]
+    n_rows, n_cols = [int(t) for t in line.replace(",", " ").split() if t.isdigit()]
+    rc = cli_main(["5", str(n_rows), str(n_cols), root, "1", "covtype", "1", "1", "3", str(coded_ver), "0", "0", "AGD",
+                   "--num-itrs", "4", "--device", "cpu", "--seed", "0"])
+    assert rc == 0
+    out = capsys.readouterr().out
+    assert "Stragglers are allowed to be atmost 3.00 times slower" in out
+    assert "Iteration 3: Train Loss" in out
+    res = os.path.join(root, "covtype", "partial", "8", "results")
+    assert os.path.exists(os.path.join(res, prefix + "auc.dat"))
