@@ -163,3 +163,42 @@ def _u_after(sch, parts, beta0, arrivals, cfg, ld):
             g += c * sum(worker_grad(LOGISTIC, parts[p][0], parts[p][1], beta, coef) for p, coef in m.segments)
         up.apply(i, 10.0, beta, u, g)
     return torch.from_numpy(np.pad(u, (0, ld - len(u))))
+
+
+@pytest.mark.parametrize("case,k", [((1, 0, 3, 7, 1, 2), 2), ((1, 0, 0, 7, 2, 0), 4), ((0, 0, 0, 5, 0, 0), 4)])
+def test_arrival_sets_replay_reference_delays(case, k):
+    """Scheduler replay (SURVEY §4 layer 3): with the reference's seeded Exp delays, the workers
+    used each round and the -1 marks of worker_timeset follow the stop rule applied to
+    RandomState(i).exponential(mean, W) (rounds whose delays are too close to call are skipped)."""
+    mean = 0.02
+    cfg, src, sch, parts = make(case, "GD", delay_mean=mean)
+    cfg.add_delay = 1
+    cfg.num_itrs = 8
+    tr = Trainer(cfg, DistEnv(), src, scheme=sch)
+    res = tr.run()
+    W = cfg.n_workers
+    T, fin = 0.0, np.zeros(W)  # virtual round start and per-worker finish (non-draining schemes carry lag)
+    for i in range(cfg.num_itrs):
+        d = np.random.RandomState(i).exponential(mean, W)
+        ready = np.maximum(T, fin) + d
+        order = list(np.argsort(ready, kind="stable"))
+        close = np.min(np.diff(np.sort(ready))) < 2e-3  # too close for wall-clock scheduling noise
+        # the oracle stop rule on the arrival order
+        got_groups, used = set(), []
+        for w in order:
+            used.append(w)
+            got_groups.add(sch.group_of[w])
+            if sch.key == "naive" and len(used) == W:
+                break
+            if sch.key == "coded" and len(used) == W - cfg.n_stragglers:
+                break
+            if sch.key == "approx" and (len(used) >= k or len(got_groups) == sch.n_groups):
+                break
+        fin = ready
+        T = float(np.max(ready)) if tr.drain else float(ready[used[-1]])
+        if close:
+            continue
+        arrived = [w for (w, p, _) in res.arrivals[i]]
+        assert arrived == used, (i, arrived, used)
+        if sch.marks_unused:
+            assert set(np.where(res.worker_timeset[i] == -1)[0]) == set(range(W)) - set(used)
