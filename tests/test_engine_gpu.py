@@ -107,3 +107,48 @@ def test_native_loop_large_cyclic_table_on_demand(native):
         assert res.timeouts == 0
         out[dev] = res.betaset
     np.testing.assert_allclose(out["cuda"], out["cpu"], rtol=1e-7, atol=1e-9)
+
+
+@pytest.mark.parametrize("ver,k", [(3, 4), (0, 0), (2, 0)])
+@pytest.mark.parametrize("native_loop", [True, False])
+def test_gpu_sparse_onehot_matches_cpu(ver, k, native_loop, native):
+    """One-hot CSR data (the real datasets' layout) through the ELL path vs the CPU engine."""
+    from erasurehead_amd.codes import make_scheme, scheme_key
+    from erasurehead_amd.data.synthetic import onehot_partitions
+
+    W, s = 6, 2
+    parts, test, d = onehot_partitions(6 * 150, 400, 8, W, seed=11)
+    src = ArraySource(parts, test, sparse=True)
+    n = sum(p[0].shape[0] for p in parts)
+    key = scheme_key(1, 0, ver)
+    out = {}
+    for dev in ("cpu", "cuda"):
+        cfg = RunConfig(W + 1, n, d, "/tmp/eh_gpu_eng/", 1, "covtype", 1, s, 0, ver, k, 0, "AGD", num_itrs=6,
+                        seed=0, verbose=False, native_loop=native_loop)
+        sch = make_scheme(key, W, s, n, k, 0, rng=np.random.RandomState(0))
+        tr = Trainer(cfg, DistEnv(device=torch.device(dev)), src, scheme=sch)
+        if dev == "cuda":
+            assert tr.plan.ell
+        res = tr.run()
+        out[dev] = res.betaset
+    np.testing.assert_allclose(out["cuda"], out["cpu"], rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-4), ("bf16", 2e-2)])
+def test_gpu_reduced_precision_tracks_fp64(precision, tol, native):
+    """fp32 / bf16 worker storage: the trajectory stays close to the fp64 engine."""
+    case = (1, 0, 3, 7, 2, 4)
+    is_coded, P, ver, n_procs, s, k = case
+    W, d, rows = n_procs - 1, 64, 200
+    src = _source(W, rows, d)
+    out = {}
+    for prec in ("fp64", precision):
+        cfg = RunConfig(n_procs, rows * W, d, "/tmp/eh_gpu_eng/", 0, "x", is_coded, s, P, ver, k, 0, "AGD",
+                        num_itrs=10, seed=0, verbose=False, precision=prec, lr=1.0)
+        from erasurehead_amd.codes import make_scheme
+
+        sch = make_scheme("approx", W, s, rows * W, k, P, rng=np.random.RandomState(0))
+        res = Trainer(cfg, DistEnv(device=torch.device("cuda")), src, scheme=sch).run()
+        out[prec] = res.betaset
+    err = np.max(np.abs(out[precision] - out["fp64"])) / np.max(np.abs(out["fp64"]))
+    assert err < tol, err
