@@ -28,6 +28,10 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--loss", default="auto", choices=["auto", "logistic", "least_squares"])
     g.add_argument("--num-itrs", type=int, default=100)
     g.add_argument("--lr", type=float, default=10.0)
+    g.add_argument("--lr-schedule", default="const", choices=["const", "invscaling", "exponential"],
+                   help="the reference's commented alternatives (ref main.py:40-46)")
+    g.add_argument("--lr-t0", type=float, default=90.0)
+    g.add_argument("--lr-decay", type=float, default=0.98)
     g.add_argument("--alpha", type=float, default=None)
     g.add_argument("--seed", type=int, default=None)
     g.add_argument("--data", default="files", choices=["files", "synthetic"])
@@ -63,7 +67,8 @@ def parse(argv: List[str]):
      num_collect, add_delay, update_rule) = a.positional
     cfg = RunConfig(int(n_procs), int(n_rows), int(n_cols), input_dir, int(is_real), dataset, int(is_coded),
                     int(n_stragglers), int(partitions), int(coded_ver), int(num_collect), int(add_delay),
-                    update_rule, num_itrs=a.num_itrs, alpha=a.alpha, lr=a.lr, precision=a.precision, loss=a.loss,
+                    update_rule, num_itrs=a.num_itrs, alpha=a.alpha, lr=a.lr,
+                    lr_kind=a.lr_schedule, lr_t0=a.lr_t0, lr_decay=a.lr_decay, precision=a.precision, loss=a.loss,
                     seed=a.seed, data=a.data, data_seed=a.data_seed, allow_uneven_groups=a.allow_uneven_groups,
                     drain=a.drain, delay_mode=a.delay_mode, fixed_stragglers=a.fixed_stragglers,
                     fixed_sleep=a.fixed_sleep, kill_workers=a.kill_workers, force_delay=a.force_delay,

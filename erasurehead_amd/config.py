@@ -38,6 +38,9 @@ class RunConfig:
     alpha: Optional[float] = None  # default 1 / n_rows
     lr: float = 10.0  # learning_rate_schedule = lr * ones(num_itrs)
     lr_schedule: Optional[List[float]] = None
+    lr_kind: str = "const"  # const (ref default) | invscaling | exponential (ref main.py:40-46, commented there)
+    lr_t0: float = 90.0  # invscaling: eta_i = lr * t0 / (i + t0), i = 1..R
+    lr_decay: float = 0.98  # exponential: eta_i = lr * decay**i, i = 1..R (the regression schedule)
 
     # ---- extensions -----------------------------------------------------------------
     precision: str = "fp64"  # fp64 | fp32 | bf16 worker compute (master state always fp64)
@@ -89,4 +92,11 @@ class RunConfig:
             if len(s) < self.num_itrs:
                 raise ValueError("lr_schedule shorter than num_itrs")
             return s
-        return self.lr * np.ones(self.num_itrs)
+        i = np.arange(1, self.num_itrs + 1, dtype=np.float64)
+        if self.lr_kind == "const":
+            return self.lr * np.ones(self.num_itrs)
+        if self.lr_kind == "invscaling":
+            return self.lr * self.lr_t0 / (i + self.lr_t0)
+        if self.lr_kind == "exponential":
+            return self.lr * self.lr_decay ** i
+        raise ValueError(f"unknown lr schedule {self.lr_kind!r}")

@@ -92,7 +92,8 @@ def init_distributed(device: str = "auto", timeout_min: float = 60.0) -> DistEnv
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     to = datetime.timedelta(minutes=timeout_min)
     owns = False
-    shared_gpu = want_gpu and world > torch.cuda.device_count()  # several ranks per GPU: RCCL impossible
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))  # ranks on this node (torchrun)
+    shared_gpu = want_gpu and local_world > torch.cuda.device_count()  # several ranks per GPU: RCCL impossible
     if not dist.is_initialized():
         backend = "nccl" if want_gpu and not shared_gpu else "gloo"
         kw = {"device_id": dev} if backend == "nccl" else {}

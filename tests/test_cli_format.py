@@ -80,3 +80,14 @@ def test_usage_and_rejections(tmp_path, capsys):
     # FRC with W % (s+1) != 0 prints the reference error and exits cleanly
     assert cli_main(["9", "200", "6", root, "0", "x", "1", "2", "0", "1", "0", "0", "GD", "--device", "cpu"]) == 0
     assert "Error: n_workers must be multiple of n_stragglers+1!" in capsys.readouterr().out
+
+
+def test_lr_schedules():
+    from erasurehead_amd.config import RunConfig
+
+    c = RunConfig(3, 10, 2, "/tmp", num_itrs=4)
+    np.testing.assert_allclose(c.eta(), [10.0] * 4)
+    c = RunConfig(3, 10, 2, "/tmp", num_itrs=4, lr_kind="invscaling")  # ref main.py:42-44
+    np.testing.assert_allclose(c.eta(), [10.0 * 90.0 / (i + 90.0) for i in range(1, 5)])
+    c = RunConfig(3, 10, 2, "/tmp", num_itrs=4, lr=0.1, lr_kind="exponential")  # ref main.py:46
+    np.testing.assert_allclose(c.eta(), [0.1 * 0.98 ** i for i in range(1, 5)])
