@@ -50,7 +50,7 @@ from ..parallel.placement import place_workers, workers_by_rank
 from ..parallel.transport import make_transport
 from ..utils import report
 from ..utils.delay import DelayModel
-from ..utils.tracing import PhaseTimer, range_
+from ..utils.tracing import PhaseTimer
 
 @dataclass
 class TrainResult:

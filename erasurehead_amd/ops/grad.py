@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from .._ext import native
-from ..models.losses import LEAST_SQUARES, LOGISTIC
+from ..models.losses import LOGISTIC
 from .precision import Precision
 
 _SEG = struct.Struct("<QQdq")  # csrc Segment {const void* X; const void* y; double coef; long long nrows}

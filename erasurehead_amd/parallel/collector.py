@@ -15,7 +15,7 @@ import math
 import queue
 import threading
 import time
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Sequence, Tuple
 
 from .._ext import native
 from ..codes.schemes import Arrival
