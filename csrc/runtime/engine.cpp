@@ -38,10 +38,34 @@
 #include <immintrin.h>
 #endif
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <cstdlib>
+
 #include "kernels/launchers.h"
 #include "runtime/collector.h"
 
 namespace {
+
+// roctx ranges for rocprofv3 --marker-trace, enabled by ERASUREHEAD_TRACE=1.
+bool trace_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("ERASUREHEAD_TRACE");
+    return e && e[0] && e[0] != '0';
+  }();
+  return on;
+}
+
+struct Range {
+  explicit Range(const char* name) : on(trace_enabled()) {
+    if (on) roctxRangePushA(name);
+  }
+  ~Range() {
+    if (on) roctxRangePop();
+  }
+  bool on;
+};
+
 namespace py = pybind11;
 using at::Tensor;
 
@@ -341,6 +365,7 @@ class MasterPump {
 
   // ---- round execution ---------------------------------------------------------------
   void begin(int i) {
+    Range tr("eh.master.begin");
     need(i >= 0 && i < R_, "round out of range");
     need(beta_in_.defined(), "set_state first");
     const int slot = i % K_;
@@ -385,10 +410,15 @@ class MasterPump {
     double t_dec = 0, t_end = 0;
     {
       py::gil_scoped_release nogil;
-      const bool ok = col_->wait(timeout_);
+      bool ok;
+      {
+        Range tr("eh.master.wait");
+        ok = col_->wait(timeout_);
+      }
       t_waited_ = eh::Collector::now();
       arr = col_->arrivals();
       std::vector<std::pair<const void*, double>> used;
+      Range tr("eh.master.decode_update");
       const bool decoded = decode(i, arr, used);
       if (!decoded) {
         status = 2;
@@ -510,7 +540,10 @@ class MasterPump {
   }
 
   double after_combine(int i, bool publish_next) {
-    if (drain_) col_->drain(i, timeout_);
+    if (drain_) {
+      Range tr("eh.master.drain");
+      col_->drain(i, timeout_);
+    }
     const double t_end = eh::Collector::now();
     if (publish_next && i + 1 < R_) begin(i + 1);
     return t_end;
@@ -576,6 +609,7 @@ class WorkerPump {
     using clk = std::chrono::steady_clock;
     for (int i = a; i < b; ++i) {
       need(i >= 0 && i < R_, "round out of range");
+      Range tr("eh.worker.round");
       const auto t0 = clk::now();
       for (int spin = 0; __atomic_load_n(bflag_, __ATOMIC_ACQUIRE) < static_cast<uint64_t>(i + 1); ++spin) {
         if (spin < 4096) {

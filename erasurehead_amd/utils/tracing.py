@@ -17,8 +17,12 @@ _ENABLED = os.environ.get("ERASUREHEAD_TRACE", "0") not in ("0", "", "false")
 
 
 def enable(flag: bool = True) -> None:
+    """Turn roctx ranges on for the Python engine and (via the environment, read once) the
+    native executors in csrc/runtime/engine.cpp."""
     global _ENABLED
     _ENABLED = flag
+    if flag:
+        os.environ["ERASUREHEAD_TRACE"] = "1"
 
 
 @contextlib.contextmanager

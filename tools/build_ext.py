@@ -90,7 +90,8 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     if force or todo or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
         link = [os.path.join(ROCM, "bin", "hipcc"), "-shared", "-fPIC", "-o", out + ".tmp", *objs,
                 f"--offload-arch={ARCH}", f"-L{torchlib}", f"-Wl,-rpath,{torchlib}",
-                "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64"]
+                "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64",
+                f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx"]
         _run(link)
         os.replace(out + ".tmp", out)
         if verbose:
