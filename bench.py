@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl"])
     ap.add_argument("--round-timeout", type=float, default=120.0, help="bounds any hang (a round takes ms)")
+    ap.add_argument("--share-partitions", action="store_true",
+                    help="co-located workers stream each distinct partition once (not the headline)")
     return ap.parse_args()
 
 
@@ -66,7 +68,8 @@ def main() -> int:
                          a.stragglers, 0, a.coded_ver, a.num_collect, a.add_delay, a.update_rule,
                          num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234, seed=0,
                          allow_uneven_groups=True, verbose=False, tasks=a.tasks,
-                         transport=a.transport, round_timeout=a.round_timeout)
+                         transport=a.transport, round_timeout=a.round_timeout,
+                         share_partitions=a.share_partitions)
 
     t_setup = time.perf_counter()
     trainer = Trainer(make_cfg(a.warmup + a.steps), env)
@@ -112,6 +115,15 @@ def main() -> int:
             "setup_s": setup_s,
             "phases_us": {k: round(v["mean_us"], 1) for k, v in res.phases.items()},
         }
+        if a.share_partitions:
+            out["config"]["share_partitions"] = True
+        ref = _ref_cpu_equiv()
+        if ref and (a.n_rows, a.n_cols, a.workers, a.stragglers) == (ref["n_rows"], ref["n_cols"], ref["workers"],
+                                                                       ref["stragglers"]):
+            # reference per-iteration math on 8 host CPU threads (tools/reference_cpu_equiv.py);
+            # BASELINE.md publishes no sec/iter, so vs_baseline stays null
+            out["ref_cpu_equiv_s_per_iter"] = ref["sec_per_iter_lower_bound"]
+            out["speedup_vs_ref_cpu_equiv"] = ref["sec_per_iter_lower_bound"] / sec_per_iter
         bpr = out["hbm_bytes_per_step_rank0"]
         if bpr:
             out["rank0_grad_stream_GBps_at_step_time"] = bpr / sec_per_iter / 1e9
@@ -148,6 +160,17 @@ def main() -> int:
                 f.write(line + "\n")
     env.shutdown()
     return 0
+
+
+def _ref_cpu_equiv():
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "reference_cpu_equiv.json")
+    try:
+        with open(path) as f:
+            r = json.loads(f.readline())
+        r.setdefault("n_rows", 1_000_000)
+        return r
+    except (OSError, ValueError):
+        return None
 
 
 if __name__ == "__main__":

@@ -135,6 +135,19 @@ void grad_sparse(int64_t loss, const Tensor& row_ptr, const Tensor& col_idx, con
         "grad_sparse");
 }
 
+void encode_messages(const Tensor& Gb, const Tensor& ptr, const Tensor& idx, const Tensor& coef, const Tensor& G) {
+  for (auto* p : {&Gb, &ptr, &idx, &coef, &G}) need_cuda(*p, "encode operand");
+  need(ptr.scalar_type() == at::kInt && idx.scalar_type() == at::kInt, "ptr/idx must be int32");
+  need(coef.scalar_type() == at::kDouble && coef.numel() == idx.numel(), "coef must be fp64, one per idx");
+  const int ac = acc_code(G);
+  need(acc_code(Gb) == ac && Gb.dim() == 2 && G.dim() == 2 && Gb.size(1) == G.size(1), "Gb/G mismatch");
+  need(ptr.numel() == G.size(0) + 1, "ptr must have nslots + 1 entries");
+  check(eh::encode_messages_launch(ac, Gb.data_ptr(), ptr.data_ptr<int>(), idx.data_ptr<int>(),
+                                   coef.data_ptr<double>(), G.data_ptr(), (int)G.size(0), (int)G.size(1),
+                                   stream_of(G)),
+        "encode_messages");
+}
+
 void grad_ell(int64_t loss, const Tensor& idx, const OptT& vals, const Tensor& y, const Tensor& coef,
               const Tensor& beta, const Tensor& rbuf, const Tensor& chunks, const Tensor& lo, const Tensor& width,
               int64_t max_width, const Tensor& G, int64_t ld) {
@@ -229,6 +242,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_dense_twopass", &grad_dense_twopass);
   m.def("grad_sparse", &grad_sparse);
   m.def("grad_ell", &grad_ell);
+  m.def("encode_messages", &encode_messages);
   m.def("combine_update", &combine_update);
   m.def("eval_gemm_loss", &eval_gemm_loss);
   m.attr("MAX_MSGS") = eh::kMaxMsgs;

@@ -1,0 +1,45 @@
+// Gradient-code encoding on the device: messages = E . per-partition gradients (K13 of SURVEY §2.8).
+//
+// Reference: every coded worker evaluates its own message over its (s+1) partitions,
+//   cyclic MDS   g_w = sum_p B[w, p] * grad_p      (label encoding y_mod = B[w,p] * y,
+//                                                  ref src/coded.py:92-95, 183-185)
+//   FRC / AGC    g_w = sum_{p in group(w)} grad_p  (ref src/replication.py:56-68, 191-193)
+// which on one machine per worker is the only option.  When several logical workers share
+// a GPU they also share partitions (all members of an FRC group hold the same ones, cyclic
+// neighbours overlap in s of s+1), so the GPU can stream every distinct partition from HBM
+// once, produce grad_p with coefficient 1, and encode all local messages here with the sparse
+// encoding matrix E (rows = local messages, CSR over the distinct partitions).  The
+// residual is linear in the label coefficient, so the messages are the same sums.
+//
+// One thread per (message, column): a fixed-order fp64/fp32 dot over the message's few
+// nonzeros of E — deterministic, no atomics, coalesced rows of grad_p.
+#include "common.h"
+#include "launchers.h"
+
+namespace eh {
+
+template <typename A>
+__global__ void __launch_bounds__(256)
+encode_messages(const A* __restrict__ Gb, const int* __restrict__ ptr, const int* __restrict__ idx,
+                const double* __restrict__ coef, A* __restrict__ G, int ld) {
+  const int slot = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ld) return;
+  const int b = ptr[slot], e = ptr[slot + 1];
+  A s = A(0);
+  for (int k = b; k < e; ++k) s = fma(static_cast<A>(coef[k]), Gb[static_cast<long long>(idx[k]) * ld + c], s);
+  G[static_cast<long long>(slot) * ld + c] = s;
+}
+
+hipError_t encode_messages_launch(int dtype, const void* Gb, const int* ptr, const int* idx, const double* coef,
+                                  void* G, int nslots, int ld, hipStream_t st) {
+  if (nslots == 0) return hipSuccess;
+  const dim3 block(256), grid(ceil_div(ld, 256), nslots);
+  if (dtype == 0)
+    hipLaunchKernelGGL(encode_messages<double>, grid, block, 0, st, (const double*)Gb, ptr, idx, coef, (double*)G, ld);
+  else
+    hipLaunchKernelGGL(encode_messages<float>, grid, block, 0, st, (const float*)Gb, ptr, idx, coef, (float*)G, ld);
+  return hipGetLastError();
+}
+
+}  // namespace eh

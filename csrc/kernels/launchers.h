@@ -31,6 +31,11 @@ hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals
                            const void* chunks, int nchunks, const int* lo, const int* width,
                            int max_width, void* G, long long gsize, int ld, hipStream_t st);
 
+// ---- device encoding of shared-partition gradients (encode.hip) ---------------------------
+// G[slot] = sum_{k in [ptr[slot], ptr[slot+1])} coef[k] * Gb[idx[k]]; dtype 0 fp64, 1 fp32
+hipError_t encode_messages_launch(int dtype, const void* Gb, const int* ptr, const int* idx, const double* coef,
+                                  void* G, int nslots, int ld, hipStream_t st);
+
 // ---- post-hoc evaluation GEMM (eval.hip) -----------------------------------------------
 hipError_t eval_gemm_loss_launch(int x_dtype, int loss_kind, const void* X, long long ldx,
                                  long long n, int d, const void* y, const void* B, int ldb,

@@ -119,9 +119,23 @@ struct GradLauncher {
   int nchunks = 0, m = 0, max_width = 0;
   const int* lo = nullptr;
   const int* width = nullptr;
+  // optional device encoding (csrc/kernels/encode.hip): the kernels above write the distinct
+  // partitions' gradients into Gb, then G[slot] = sum_k coef * Gb[idx] for the enc_slots messages
+  void* Gb = nullptr;
+  const int* enc_ptr = nullptr;
+  const int* enc_idx = nullptr;
+  const double* enc_coef = nullptr;
+  int enc_slots = 0;
   std::vector<Tensor> keep;
 
   hipError_t launch(const void* beta, void* G, hipStream_t st) const {
+    if (!Gb) return launch_raw(beta, G, st);
+    const hipError_t e = launch_raw(beta, Gb, st);
+    if (e != hipSuccess) return e;
+    return eh::encode_messages_launch(acc, Gb, enc_ptr, enc_idx, enc_coef, G, enc_slots, ld, st);
+  }
+
+  hipError_t launch_raw(const void* beta, void* G, hipStream_t st) const {
     switch (kind) {
       case 0:
         return ntasks ? eh::grad_dense_launch(dtype, loss, cpl, segs, tasks, ntasks, beta, slab, stb, nslots, part, G,
@@ -667,6 +681,21 @@ void bind_engine(py::module& m) {
       .def_static("ell", &make_ell, py::arg("loss"), py::arg("idx"), py::arg("vals"), py::arg("y"), py::arg("coef"),
                   py::arg("rbuf"), py::arg("chunks"), py::arg("lo"), py::arg("width"), py::arg("max_width"),
                   py::arg("nslots"), py::arg("ld"))
+      .def("set_encode",
+           [](GradLauncher& g, const Tensor& ptr, const Tensor& idx, const Tensor& coef, const Tensor& Gb) {
+             for (auto* t : {&ptr, &idx, &coef, &Gb}) need_gpu(*t, "encode operand");
+             need(ptr.scalar_type() == at::kInt && idx.scalar_type() == at::kInt, "encode ptr/idx must be int32");
+             need(coef.scalar_type() == at::kDouble, "encode coefficients must be fp64");
+             need(Gb.dim() == 2 && Gb.size(0) == g.nslots && Gb.size(1) == g.ld && acc_code(Gb) == g.acc,
+                  "Gb must be [distinct partitions, ld] in the accumulator dtype");
+             need(idx.numel() == coef.numel(), "encode idx/coef size mismatch");
+             g.enc_slots = (int)ptr.numel() - 1;
+             g.Gb = Gb.data_ptr();
+             g.enc_ptr = ptr.data_ptr<int>();
+             g.enc_idx = idx.data_ptr<int>();
+             g.enc_coef = coef.data_ptr<double>();
+             for (auto* t : {&ptr, &idx, &coef, &Gb}) g.keep.push_back(*t);
+           })
       .def("launch", [](const GradLauncher& g, const Tensor& beta, const Tensor& G) {
         need_gpu(beta, "beta");
         need_gpu(G, "G");

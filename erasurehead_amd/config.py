@@ -71,6 +71,7 @@ class RunConfig:
     native_loop: bool = True  # GPU rounds in the C++ executors (csrc/runtime/engine.cpp)
     sync_update: bool = False  # host waits for every round's update kernel (else timed by HIP events)
     transport: str = "auto"  # auto | ipc | rccl | gloo (parallel/transport.py)
+    share_partitions: bool = False  # co-located workers: distinct partitions once + device encode (ops/grad.py)
 
     def __post_init__(self):
         self.update_rule = str(self.update_rule)

@@ -41,7 +41,7 @@ from ..config import RunConfig
 from ..data import io as dio
 from ..data.source import DataSource, FileSource, SyntheticSource
 from ..models.losses import LEAST_SQUARES, LOGISTIC, UpdateRule
-from ..ops.grad import DenseGradPlan, SparseGradPlan
+from ..ops.grad import DenseGradPlan, SharedGradPlan, SparseGradPlan
 from ..ops.precision import get_precision
 from ..ops.update import combine_update
 from ..parallel.collector import ArrivalCollector
@@ -147,11 +147,17 @@ class Trainer:
         parts = {p: source.partition(p, self.prec, dev) for p in needed}
         self.load_seconds = time.perf_counter() - t0
         segs = [m.segments for m in self.local_msgs]
-        if source.is_sparse:
-            self.plan = SparseGradPlan(segs, parts, self.prec, self.loss, self.d, device=dev)
-        else:
+
+        def make_plan(messages):
+            if source.is_sparse:
+                return SparseGradPlan(messages, parts, self.prec, self.loss, self.d, device=dev)
             kw = {"target_tasks": cfg.tasks} if cfg.tasks else {}
-            self.plan = DenseGradPlan(segs, parts, self.prec, self.loss, self.d, **kw)
+            return DenseGradPlan(messages, parts, self.prec, self.loss, self.d, **kw)
+
+        if cfg.share_partitions and SharedGradPlan.worthwhile(segs, lambda p: parts[p][0].shape[0]):
+            self.plan = SharedGradPlan(segs, make_plan)
+        else:
+            self.plan = make_plan(segs)
         self._parts = parts
 
     def _check_hbm(self, need_bytes: int) -> None:

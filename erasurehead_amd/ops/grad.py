@@ -297,3 +297,73 @@ class SparseGradPlan:
             g = X[sel].T.dot(r[sel]) if sel.any() else np.zeros(self.d)
             G[slot, : self.d] = torch.from_numpy(np.asarray(g).ravel()).to(G.dtype)
         return G
+
+
+class SharedGradPlan:
+    """Distinct partitions once, then device encoding of every local message (``--share-partitions``).
+
+    Logical workers placed on one GPU share partitions: all members of an FRC/AGC group hold
+    the same (s+1) partitions (ref src/replication.py:56-68) and cyclic neighbours overlap in s
+    of them (ref src/coded.py:31-50).  The faithful plans above compute every message from its
+    own rows, streaming (s+1)-replicated X; this plan streams each distinct partition once
+    (coefficient 1) into ``Gb`` and encodes ``G = E . Gb`` (csrc/kernels/encode.hip), E being
+    the [messages x partitions] matrix of label-encoding coefficients.  The residual is linear
+    in the coefficient, so every message is the same sum (up to fp rounding order).
+
+    ``make_inner(messages)`` builds the dense or sparse plan over the basis messages.
+    """
+
+    def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]], make_inner):
+        self.messages = [list(m) for m in messages]
+        self.nslots = len(self.messages)
+        self.basis = sorted({p for m in self.messages for p, _ in m})
+        pos = {p: j for j, p in enumerate(self.basis)}
+        self.inner = make_inner([[(p, 1.0)] for p in self.basis])
+        self.prec, self.loss, self.d, self.ld = self.inner.prec, self.inner.loss, self.inner.d, self.inner.ld
+        self.device = self.inner.device
+        ptr, idx, coef = [0], [], []
+        for m in self.messages:
+            for p, c in m:
+                idx.append(pos[p])
+                coef.append(float(c))
+            ptr.append(len(idx))
+        if idx and (min(idx) < 0 or max(idx) >= len(self.basis)):
+            raise ValueError("encoding index out of range")
+        self.E = torch.zeros((self.nslots, len(self.basis)), dtype=torch.float64)
+        for s in range(self.nslots):
+            for k in range(ptr[s], ptr[s + 1]):
+                self.E[s, idx[k]] += coef[k]
+        dev = self.device
+        self.enc_ptr = torch.tensor(ptr, dtype=torch.int32, device=dev)
+        self.enc_idx = torch.tensor(idx or [0], dtype=torch.int32, device=dev)[: len(idx)]
+        self.enc_coef = torch.tensor(coef or [0.0], dtype=torch.float64, device=dev)[: len(coef)]
+        self.Gb = self.inner.out_buffer()[0]
+
+    @staticmethod
+    def worthwhile(messages: Sequence[Sequence[Tuple[int, float]]], rows_of) -> bool:
+        """True when the local messages stream some partition more than once."""
+        total = sum(rows_of(p) for m in messages for p, _ in m)
+        distinct = sum(rows_of(p) for p in {p for m in messages for p, _ in m})
+        return distinct < total
+
+    def out_buffer(self, n: int = 1) -> torch.Tensor:
+        return torch.zeros((n, self.nslots, self.ld), dtype=self.prec.acc, device=self.device)
+
+    @property
+    def bytes_per_round(self) -> int:
+        return getattr(self.inner, "bytes_per_round", 0)
+
+    def run(self, beta: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
+        if G.shape != (self.nslots, self.ld):
+            raise ValueError(f"G must be [{self.nslots}, {self.ld}]")
+        self.inner.run(beta, self.Gb)
+        if self.device.type == "cuda":
+            native().encode_messages(self.Gb, self.enc_ptr, self.enc_idx, self.enc_coef, G)
+        else:
+            G.copy_((self.E.to(self.Gb.dtype) @ self.Gb).to(G.dtype))
+        return G
+
+    def native_launcher(self):
+        L = self.inner.native_launcher()
+        L.set_encode(self.enc_ptr, self.enc_idx, self.enc_coef, self.Gb)
+        return L

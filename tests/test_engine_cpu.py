@@ -202,3 +202,44 @@ def test_arrival_sets_replay_reference_delays(case, k):
         assert arrived == used, (i, arrived, used)
         if sch.marks_unused:
             assert set(np.where(res.worker_timeset[i] == -1)[0]) == set(range(W)) - set(used)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_share_partitions_matches_numpy_replay(case):
+    """--share-partitions: distinct partitions once + encode, same trajectory as the reference math."""
+    cfg, src, sch, parts = make(case, "AGD", share_partitions=True)
+    tr = Trainer(cfg, DistEnv(), src, scheme=sch)
+    from erasurehead_amd.ops.grad import SharedGradPlan
+
+    shared = SharedGradPlan.worthwhile([m.segments for m in sch.messages], lambda p: 1)
+    assert isinstance(tr.plan, SharedGradPlan) == shared
+    assert shared == (case[4] > 0 and case[2] != 2)  # every scheme but naive / avoidstragg replicates
+    res = tr.run()
+    ref = replay(sch, parts, tr.beta0, res.arrivals, "AGD", cfg.alpha_value, cfg.n_rows, cfg.eta())
+    np.testing.assert_allclose(res.betaset, ref, rtol=1e-10, atol=1e-12)
+
+
+def test_shared_plan_encoding_matrix():
+    from erasurehead_amd.ops.grad import SharedGradPlan
+
+    msgs = [[(0, 1.0), (1, -2.0)], [(1, 0.5), (2, 1.0)], [(2, 3.0)]]
+    seen = []
+
+    class Inner:
+        prec, loss, d, ld, device = None, 0, 4, 4, torch.device("cpu")
+
+        def __init__(self, ms):
+            seen.append(ms)
+
+        def out_buffer(self, n=1):
+            return torch.zeros((n, 3, 4), dtype=torch.float64)
+
+    class P:
+        acc = torch.float64
+
+    Inner.prec = P
+    sp = SharedGradPlan(msgs, Inner)
+    assert seen == [[[(0, 1.0)], [(1, 1.0)], [(2, 1.0)]]]
+    np.testing.assert_array_equal(sp.E.numpy(), [[1, -2, 0], [0, 0.5, 1], [0, 0, 3]])
+    assert SharedGradPlan.worthwhile(msgs, lambda p: 10)
+    assert not SharedGradPlan.worthwhile([[(0, 1.0)], [(1, 1.0)]], lambda p: 10)

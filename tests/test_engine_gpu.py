@@ -152,3 +152,49 @@ def test_gpu_reduced_precision_tracks_fp64(precision, tol, native):
         out[prec] = res.betaset
     err = np.max(np.abs(out[precision] - out["fp64"])) / np.max(np.abs(out["fp64"]))
     assert err < tol, err
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[4] > 0 and c[2] != 2])
+@pytest.mark.parametrize("native_loop", [True, False])
+def test_gpu_share_partitions_matches_cpu(case, native_loop, native):
+    """--share-partitions on the GPU (distinct partitions once + encode.hip) vs the faithful CPU engine."""
+    from erasurehead_amd.codes import make_scheme, scheme_key
+    from erasurehead_amd.ops.grad import SharedGradPlan
+
+    is_coded, P, ver, n_procs, s, k = case
+    W, d, rows = n_procs - 1, 33, 40
+    key = scheme_key(is_coded, P, ver)
+    n_parts = make_scheme(key, W, s, rows * W, k, P, rng=np.random.RandomState(0)).n_partition_files
+    src = _source(n_parts, rows, d)
+    out = {}
+    for dev, share in (("cpu", False), ("cuda", True)):
+        cfg = RunConfig(n_procs, rows * n_parts, d, "/tmp/eh_gpu_eng/", 0, "x", is_coded, s, P, ver, k, 0, "AGD",
+                        num_itrs=8, seed=0, verbose=False, native_loop=native_loop, share_partitions=share)
+        sch = make_scheme(key, W, s, rows * n_parts, k, P, rng=np.random.RandomState(0))
+        tr = Trainer(cfg, DistEnv(device=torch.device(dev)), src, scheme=sch)
+        assert isinstance(tr.plan, SharedGradPlan) == share
+        out[dev] = tr.run().betaset
+    np.testing.assert_allclose(out["cuda"], out["cpu"], rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.parametrize("ver,k", [(3, 4), (0, 0)])
+def test_gpu_share_partitions_sparse(ver, k, native):
+    """Shared partitions over the one-hot ELL path."""
+    from erasurehead_amd.codes import make_scheme, scheme_key
+    from erasurehead_amd.data.synthetic import onehot_partitions
+    from erasurehead_amd.ops.grad import SharedGradPlan
+
+    W, s = 6, 2
+    parts, test, d = onehot_partitions(6 * 150, 400, 8, W, seed=11)
+    src = ArraySource(parts, test, sparse=True)
+    n = sum(p[0].shape[0] for p in parts)
+    out = {}
+    for dev, share in (("cpu", False), ("cuda", True)):
+        cfg = RunConfig(W + 1, n, d, "/tmp/eh_gpu_eng/", 1, "covtype", 1, s, 0, ver, k, 0, "AGD", num_itrs=6,
+                        seed=0, verbose=False, share_partitions=share)
+        sch = make_scheme(scheme_key(1, 0, ver), W, s, n, k, 0, rng=np.random.RandomState(0))
+        tr = Trainer(cfg, DistEnv(device=torch.device(dev)), src, scheme=sch)
+        if share:
+            assert isinstance(tr.plan, SharedGradPlan) and tr.plan.inner.ell
+        out[dev] = tr.run().betaset
+    np.testing.assert_allclose(out["cuda"], out["cpu"], rtol=1e-9, atol=1e-11)

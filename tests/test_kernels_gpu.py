@@ -205,3 +205,27 @@ def test_eval_gemm_loss(prec_name, tol, R, native):
     np.testing.assert_allclose(Pd, Xh @ Bh.T, rtol=tol * 10, atol=tol)
     auc = auc_columns(torch.from_numpy(y).to(DEV), torch.from_numpy(Xh @ Bh.T).to(DEV))
     np.testing.assert_allclose(auc, [roc_auc(y, (Xh @ Bh.T)[:, j]) for j in range(R)], rtol=1e-12)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_encode_messages(dtype, native):
+    """encode.hip: G = E . Gb over a sparse E, against the fp64 torch product."""
+    rng = np.random.RandomState(3)
+    nb, ns, ld = 5, 7, 1003
+    Gb = torch.from_numpy(rng.randn(nb, ld)).to(dtype).cuda()
+    ptr, idx, coef = [0], [], []
+    E = np.zeros((ns, nb))
+    for s in range(ns):
+        for b in rng.choice(nb, size=1 + s % 3, replace=False):
+            c = rng.randn()
+            idx.append(int(b))
+            coef.append(c)
+            E[s, b] = c
+        ptr.append(len(idx))
+    G = torch.full((ns, ld), float("nan"), dtype=dtype, device="cuda")
+    native.encode_messages(Gb, torch.tensor(ptr, dtype=torch.int32, device="cuda"),
+                           torch.tensor(idx, dtype=torch.int32, device="cuda"),
+                           torch.tensor(coef, dtype=torch.float64, device="cuda"), G)
+    ref = E @ Gb.double().cpu().numpy()
+    tol = 1e-13 if dtype == torch.float64 else 1e-5
+    np.testing.assert_allclose(G.double().cpu().numpy(), ref, rtol=tol, atol=tol)
