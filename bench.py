@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl"])
     ap.add_argument("--round-timeout", type=float, default=120.0, help="bounds any hang (a round takes ms)")
+    ap.add_argument("--device-loop", default="auto", choices=["auto", "graph", "stream", "off"])
     ap.add_argument("--share-partitions", action="store_true",
                     help="co-located workers stream each distinct partition once (not the headline)")
     return ap.parse_args()
@@ -69,7 +70,7 @@ def main() -> int:
                          num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234, seed=0,
                          allow_uneven_groups=True, verbose=False, tasks=a.tasks,
                          transport=a.transport, round_timeout=a.round_timeout,
-                         share_partitions=a.share_partitions)
+                         share_partitions=a.share_partitions, device_loop=a.device_loop)
 
     t_setup = time.perf_counter()
     trainer = Trainer(make_cfg(a.warmup + a.steps), env)
@@ -115,6 +116,8 @@ def main() -> int:
             "setup_s": setup_s,
             "phases_us": {k: round(v["mean_us"], 1) for k, v in res.phases.items()},
         }
+        out["config"]["round_loop"] = {"graph": "device-driven, hipGraph", "stream": "device-driven"}.get(
+            trainer.device_loop, "host-driven (native pump)")
         if a.share_partitions:
             out["config"]["share_partitions"] = True
         ref = _ref_cpu_equiv()

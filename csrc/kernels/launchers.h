@@ -52,7 +52,10 @@ struct CombineArgs {
 hipError_t combine_update_launch(const CombineArgs& args, int msg_dtype, int w_dtype,
                                  double* beta, double* u, double* hist, void* beta_w,
                                  double* g_out, int d, int ld, double decay, double gm,
-                                 double l2, double theta, int rule, hipStream_t st);
+                                 double l2, double theta, int rule, hipStream_t st,
+                                 long long* stamp = nullptr);
+// one device timestamp (wall_clock64, hipDeviceAttributeWallClockRate kHz) into *out
+hipError_t stamp_launch(long long* out, hipStream_t st);
 
 // ---- IPC mailbox put + signal (transport.hip) -------------------------------------------
 constexpr int kMaxPuts = 16;

@@ -24,8 +24,10 @@ template <typename M, typename W>
 __global__ void __launch_bounds__(256)
 combine_update(const CombineArgs args, double* __restrict__ beta, double* __restrict__ u,
                double* __restrict__ hist, W* __restrict__ beta_w, double* __restrict__ g_out,
-               int d, int ld, double decay, double gm, double l2, double theta, int rule) {
+               int d, int ld, double decay, double gm, double l2, double theta, int rule,
+               long long* __restrict__ stamp) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (stamp && c == 0) *stamp = wall_clock64();  // device time the round's messages were all ready
   if (c >= ld) return;
   if (c >= d) {  // padded columns stay exactly zero
     if (beta_w) beta_w[c] = W(0);
@@ -55,16 +57,25 @@ combine_update(const CombineArgs args, double* __restrict__ beta, double* __rest
 hipError_t combine_update_launch(const CombineArgs& args, int msg_dtype, int w_dtype,
                                  double* beta, double* u, double* hist, void* beta_w,
                                  double* g_out, int d, int ld, double decay, double gm,
-                                 double l2, double theta, int rule, hipStream_t st) {
+                                 double l2, double theta, int rule, hipStream_t st, long long* stamp) {
   const dim3 block(256), grid(ceil_div(ld, 256));
   if (msg_dtype == 0 && w_dtype == 0)
-    hipLaunchKernelGGL((combine_update<double, double>), grid, block, 0, st, args, beta, u, hist, (double*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule);
+    hipLaunchKernelGGL((combine_update<double, double>), grid, block, 0, st, args, beta, u, hist, (double*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule, stamp);
   else if (msg_dtype == 0 && w_dtype == 1)
-    hipLaunchKernelGGL((combine_update<double, float>), grid, block, 0, st, args, beta, u, hist, (float*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule);
+    hipLaunchKernelGGL((combine_update<double, float>), grid, block, 0, st, args, beta, u, hist, (float*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule, stamp);
   else if (msg_dtype == 1 && w_dtype == 0)
-    hipLaunchKernelGGL((combine_update<float, double>), grid, block, 0, st, args, beta, u, hist, (double*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule);
+    hipLaunchKernelGGL((combine_update<float, double>), grid, block, 0, st, args, beta, u, hist, (double*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule, stamp);
   else
-    hipLaunchKernelGGL((combine_update<float, float>), grid, block, 0, st, args, beta, u, hist, (float*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule);
+    hipLaunchKernelGGL((combine_update<float, float>), grid, block, 0, st, args, beta, u, hist, (float*)beta_w, g_out, d, ld, decay, gm, l2, theta, rule, stamp);
+  return hipGetLastError();
+}
+
+__global__ void stamp_kernel(long long* out) {
+  if (threadIdx.x == 0) *out = wall_clock64();
+}
+
+hipError_t stamp_launch(long long* out, hipStream_t st) {
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, st, out);
   return hipGetLastError();
 }
 

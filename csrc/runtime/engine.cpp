@@ -278,6 +278,12 @@ class MasterPump {
     index_.assign(2 * W, {-1, -1});
   }
   ~MasterPump() {
+    if (dev_stream_) {
+      hipStreamSynchronize(dev_stream_);
+      for (auto g : graphs_) hipGraphExecDestroy(g);
+      hipStreamDestroy(dev_stream_);
+      hipEventDestroy(join_ev_);
+    }
     for (auto e : loc_ev_)
       if (e) hipEventDestroy(e);
     for (auto& p : upd_ev_) {
@@ -461,6 +467,111 @@ class MasterPump {
     return pack(0, arr, i, t_dec, t_end);
   }
 
+  // ---- device-driven rounds (single process, no injected delay) -------------------------
+  // Every message is local and finishes with the one gradient launch, so the arrival order
+  // (and with it the decode) is fixed before the GPU runs: the collector still decides it,
+  // from host probes seen at the round start (ties break by probe order, exactly like the
+  // simultaneous HIP-event probes of begin()).  The host decodes rounds [a, b) up front and
+  // enqueues  grad(i) -> combine_update(i)  back to back, so the device never waits for the
+  // host between rounds.  With `graph` the whole segment is captured into hipGraphs (at most
+  // kGraphRounds rounds each) and replayed with one launch per graph.
+  // stamps: int64 GPU [R + 1]; stamps[a] = device time before round a, stamps[i + 1] = start
+  // of round i's update (its messages are done).  Returns the arrivals of every round.
+  static constexpr int kGraphRounds = 256;
+
+  py::list run_local(int a, int b, bool graph, const Tensor& stamps) {
+    need(a >= 0 && a <= b && b <= R_, "round range out of bounds");
+    need(remote_.empty() && targets_.empty(), "device-driven rounds need every message local");
+    need(n_loc_ > 0 && launcher_ != nullptr, "no local messages");
+    need(stamps.is_cuda() && stamps.scalar_type() == at::kLong && stamps.numel() >= R_ + 1, "stamps: int64 [R+1]");
+    for (int i = a; i < b; ++i)
+      for (int w = 0; w < W_; ++w) need(delays_[static_cast<int64_t>(i) * W_ + w] == 0.0, "injected delay present");
+    std::vector<std::vector<eh::Arrival>> arrs;
+    std::vector<std::vector<std::pair<const void*, double>>> useds;
+    {
+      Range tr("eh.master.decode_ahead");
+      for (int i = a; i < b; ++i) {
+        const double t = eh::Collector::now();
+        col_->begin_round(i, t, stop_rule_, k_);
+        t_start_[i] = t;
+        for (const auto& m : local_) col_->mark_seen(col_->add_host_probe(m.w, m.p, i, 0.0), t);
+        need(col_->wait(timeout_), "local arrivals did not satisfy the stop rule");
+        std::vector<std::pair<const void*, double>> used;
+        need(decode(i, col_->arrivals(), used), "completion pattern missing from the decode table");
+        arrs.push_back(col_->arrivals());
+        useds.push_back(std::move(used));
+        if (drain_) col_->drain(i, timeout_);
+      }
+    }
+    long long* st = reinterpret_cast<long long*>(stamps.data_ptr<int64_t>());
+    char* bin = static_cast<char*>(beta_in_.data_ptr());
+    // The rounds run on the pump's own stream (the legacy default stream cannot be captured),
+    // ordered after everything already on the caller's stream and before anything after.
+    if (!dev_stream_) {
+      hcheck(hipStreamCreateWithFlags(&dev_stream_, hipStreamNonBlocking), "hipStreamCreate");
+      hcheck(hipEventCreateWithFlags(&join_ev_, hipEventDisableTiming), "hipEventCreate");
+    }
+    hcheck(hipEventRecord(join_ev_, stream_), "hipEventRecord");
+    hcheck(hipStreamWaitEvent(dev_stream_, join_ev_, 0), "hipStreamWaitEvent");
+    const hipStream_t caller = stream_;
+    stream_ = dev_stream_;  // launcher_/combine() enqueue on stream_
+    struct Restore {
+      hipStream_t& s;
+      hipStream_t v;
+      ~Restore() { s = v; }
+    } restore{stream_, caller};
+    auto enqueue = [&](int i0, int i1) {
+      for (int i = i0; i < i1; ++i) {
+        const int slot = i % K_;
+        char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
+        hcheck(launcher_->launch(bin + static_cast<int64_t>(i) * ld_ * es_, g, stream_), "local gradient");
+        combine(i, useds[i - a], false, st + i + 1);
+      }
+    };
+    Range tr("eh.master.device_rounds");
+    hcheck(eh::stamp_launch(st + a, stream_), "stamp");
+    if (!graph) {
+      enqueue(a, b);
+    } else {
+      for (int c0 = a; c0 < b; c0 += kGraphRounds) {
+        const int c1 = std::min(b, c0 + kGraphRounds);
+        hipGraph_t gr = nullptr;
+        hipGraphExec_t ex = nullptr;
+        hcheck(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+        try {
+          enqueue(c0, c1);
+        } catch (...) {
+          hipStreamEndCapture(stream_, &gr);
+          if (gr) hipGraphDestroy(gr);
+          throw;
+        }
+        hcheck(hipStreamEndCapture(stream_, &gr), "hipStreamEndCapture");
+        hcheck(hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0), "hipGraphInstantiate");
+        hipGraphDestroy(gr);
+        hcheck(hipGraphLaunch(ex, stream_), "hipGraphLaunch");
+        graphs_.push_back(ex);
+      }
+      ++graph_segments_;
+    }
+    hcheck(hipEventRecord(join_ev_, dev_stream_), "hipEventRecord");
+    hcheck(hipStreamWaitEvent(caller, join_ev_, 0), "hipStreamWaitEvent");
+    py::list out;
+    for (const auto& arr : arrs) {
+      py::list lst;
+      for (const auto& x : arr) lst.append(py::make_tuple(x.worker, x.part, x.t_rel));
+      out.append(lst);
+    }
+    return out;
+  }
+
+  // Wall-clock rate of the device timestamps (Hz).
+  double stamp_hz() const {
+    int khz = 0;
+    hcheck(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_), "hipDeviceGetAttribute");
+    return 1e3 * khz;
+  }
+  int graphs_launched() const { return (int)graphs_.size(); }
+
   // Update-kernel durations (ms) of every round run so far (host sync).
   std::vector<double> update_ms() {
     hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
@@ -532,7 +643,10 @@ class MasterPump {
     return true;
   }
 
-  void combine(int i, const std::vector<std::pair<const void*, double>>& used) {
+  // events: time the update with HIP events (host-driven rounds); stamp: device timestamp
+  // written by the update kernel at its start (device-driven rounds, graph capture).
+  void combine(int i, const std::vector<std::pair<const void*, double>>& used, bool events = true,
+               long long* stamp = nullptr) {
     need((int)used.size() <= eh::kMaxMsgs, "too many messages for one combine");
     eh::CombineArgs a{};
     a.nmsg = (int)used.size();
@@ -541,16 +655,18 @@ class MasterPump {
       a.coef[m] = used[m].second;
     }
     auto& ev = upd_ev_[i];
-    if (!ev.first) hcheck(hipEventCreate(&ev.first), "hipEventCreate");
-    if (!ev.second) hcheck(hipEventCreate(&ev.second), "hipEventCreate");
-    hcheck(hipEventRecord(ev.first, stream_), "hipEventRecord");
+    if (events) {
+      if (!ev.first) hcheck(hipEventCreate(&ev.first), "hipEventCreate");
+      if (!ev.second) hcheck(hipEventCreate(&ev.second), "hipEventCreate");
+      hcheck(hipEventRecord(ev.first, stream_), "hipEventRecord");
+    }
     char* bin = static_cast<char*>(beta_in_.data_ptr());
     hcheck(eh::combine_update_launch(a, acc_, acc_, beta_.data_ptr<double>(), u_.data_ptr<double>(),
                                      hist_.data_ptr<double>() + static_cast<int64_t>(i) * ld_,
                                      bin + static_cast<int64_t>(i + 1) * ld_ * es_, nullptr, d_, ld_, decay_[i], gm_[i],
-                                     l2_[i], theta_[i], update_rule_, stream_),
+                                     l2_[i], theta_[i], update_rule_, stream_, stamp),
            "combine_update");
-    hcheck(hipEventRecord(ev.second, stream_), "hipEventRecord");
+    if (events) hcheck(hipEventRecord(ev.second, stream_), "hipEventRecord");
   }
 
   double after_combine(int i, bool publish_next) {
@@ -590,6 +706,10 @@ class MasterPump {
   double t_waited_ = 0.0;  // host time the last wait() returned (phase timing)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> upd_ev_;
   std::vector<hipEvent_t> loc_ev_;
+  std::vector<hipGraphExec_t> graphs_;  // device-driven segments (destroyed after a sync)
+  hipStream_t dev_stream_ = nullptr;     // stream of the device-driven rounds (capturable)
+  hipEvent_t join_ev_ = nullptr;
+  int graph_segments_ = 0;
 };
 
 // ------------------------------------------------------------------------- WorkerPump
@@ -716,7 +836,10 @@ void bind_engine(py::module& m) {
       .def("begin", &MasterPump::begin, py::call_guard<py::gil_scoped_release>())
       .def("finish", &MasterPump::finish)
       .def("resolve", &MasterPump::resolve)
-      .def("update_ms", &MasterPump::update_ms);
+      .def("update_ms", &MasterPump::update_ms)
+      .def("run_local", &MasterPump::run_local, py::arg("a"), py::arg("b"), py::arg("graph"), py::arg("stamps"))
+      .def("stamp_hz", &MasterPump::stamp_hz)
+      .def("graphs_launched", &MasterPump::graphs_launched);
   py::class_<WorkerPump>(m, "WorkerPump")
       .def(py::init<std::shared_ptr<GradLauncher>, const Tensor&, const Tensor&, int, uintptr_t, int, int, uintptr_t,
                     uintptr_t, const Tensor&, int, int, double>())

@@ -56,6 +56,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--verify-beta", action="store_true", help="race detector: checksum beta on every worker")
     g.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     g.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl", "gloo"])
+    g.add_argument("--device-loop", default="auto", choices=["auto", "graph", "stream", "off"],
+                   help="single-process runs without injected delay: rounds captured in hipGraphs (auto/graph), "
+                        "enqueued back to back (stream) or host-driven (off)")
     g.add_argument("--share-partitions", action="store_true",
                    help="stream each distinct partition once per GPU and encode the local messages on the device")
     return p
@@ -77,7 +80,7 @@ def parse(argv: List[str]):
                     round_timeout=a.round_timeout, fix_quirks=a.fix_quirks, save_linear=a.save_linear,
                     full_precision_outputs=a.full_precision_outputs, evaluate=not a.no_eval, verbose=not a.quiet,
                     checkpoint_every=a.checkpoint_every, checkpoint_path=a.checkpoint_path, resume=a.resume, trace=a.trace, verify_beta=a.verify_beta,
-                    transport=a.transport, share_partitions=a.share_partitions)
+                    transport=a.transport, share_partitions=a.share_partitions, device_loop=a.device_loop)
     return cfg, a
 
 

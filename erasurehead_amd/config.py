@@ -71,6 +71,7 @@ class RunConfig:
     native_loop: bool = True  # GPU rounds in the C++ executors (csrc/runtime/engine.cpp)
     sync_update: bool = False  # host waits for every round's update kernel (else timed by HIP events)
     transport: str = "auto"  # auto | ipc | rccl | gloo (parallel/transport.py)
+    device_loop: str = "auto"  # auto|graph|stream|off: device-driven rounds when eligible (trainer._device_loop_mode)
     share_partitions: bool = False  # co-located workers: distinct partitions once + device encode (ops/grad.py)
 
     def __post_init__(self):

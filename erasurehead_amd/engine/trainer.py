@@ -77,6 +77,7 @@ class Trainer:
             env = init_distributed("auto")
         self.env = env
         self.timer = PhaseTimer()
+        self.device_loop: Optional[str] = None  # set by the native master loop when rounds ran device-driven
         self._setup_scheme(scheme)
         self._setup_data(source)
         self._setup_buffers()
@@ -420,8 +421,32 @@ class Trainer:
         if cfg.verbose:
             log(sch.banner(cfg.add_delay))
         orig_start = time.perf_counter()
-        begun = False
-        for i in range(start, R):
+        device_mode = self._device_loop_mode(start, delay_table, table_decoded)
+        if device_mode:
+            stamps = torch.zeros(R + 1, dtype=torch.int64, device=env.device)
+            hz = pump.stamp_hz()
+            cuts = [start] + ([timed_start] if timed_start is not None and start < timed_start < R else []) + [R]
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                if timed_start is not None and a == timed_start:
+                    t_timed0 = self._timed_fence()
+                if cfg.verbose:
+                    for i in range(a, b):
+                        if i % 10 == 0:
+                            log(report.iteration_tick(i))
+                arrs = pump.run_local(a, b, device_mode == "graph", stamps)
+                arrivals_log.extend(arrs)
+            self._sync()
+            st = stamps.cpu().numpy().astype(np.float64)
+            for i in range(start, R):
+                dt = (st[i + 1] - st[i]) / hz  # device time: round i's gradients + the previous update
+                timeset[i] = loop_time[i] = dt
+                arrivals = [Arrival(w, p, dt) for (w, p, _t) in arrivals_log[i]]
+                arrivals_log[i] = [(a.worker, a.part, a.t_rel) for a in arrivals]
+                worker_timeset[i] = sch.worker_times(arrivals)
+                self.timer.add("device_round", dt)
+            self.device_loop = device_mode
+        begun = device_mode is not None
+        for i in range(start, R if not device_mode else start):
             if not begun:
                 if timed_start is not None and i == timed_start:
                     t_timed0 = self._timed_fence()
@@ -459,7 +484,8 @@ class Trainer:
                 self._checkpoint(i + 1, timeset, worker_timeset)
         col.drain(R - 1, max(cfg.round_timeout, 60.0))
         upd = pump.update_ms()
-        timeset[start:] += 1e-3 * np.asarray(upd[start:])
+        if not device_mode:
+            timeset[start:] += 1e-3 * np.asarray(upd[start:])
         col.close()
         if timed_start is not None:
             t_timed1 = self._timed_fence()
@@ -473,6 +499,23 @@ class Trainer:
             res.timed_rounds = R - timed_start
         del pump
         return res
+
+    def _device_loop_mode(self, start: int, delay_table: np.ndarray, table_decoded: bool) -> Optional[str]:
+        """'graph' | 'stream' when the rounds can run device-driven (MasterPump.run_local), else None.
+
+        Eligible: one process (every message local), no injected delay in any remaining round
+        (the arrival order is then fixed before the GPU runs), every decode pattern already
+        in the table, no per-round checkpoints.
+        """
+        mode = self.cfg.device_loop
+        if mode == "off" or self.tx is not None or not self.local_msgs or self.cfg.checkpoint_every:
+            return None
+        if delay_table.size and np.any(delay_table[start:] != 0.0):
+            return None
+        W, s = self.cfg.n_workers, self.scheme.n_stragglers
+        if table_decoded and math.comb(W, s) > 20000:
+            return None
+        return "graph" if mode == "graph" else "stream"
 
     def _worker_loop_native(self, timed_start, start: int = 0) -> None:
         """Worker rounds in csrc/runtime/engine.cpp (WorkerPump) over the IPC mailbox."""

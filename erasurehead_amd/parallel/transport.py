@@ -419,6 +419,9 @@ def make_transport(kind: str, env, R: int, K: int, ld: int, dtype, n_local: int,
         raise ValueError("gloo transport is the CPU path; GPU ranks use ipc or rccl")
     if kind == "rccl":
         return RcclTransport(*args)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(env.world)))
+    if kind == "auto" and local_world < env.world and env.backend != "gloo":
+        return RcclTransport(*args)  # multi-node (torchrun --nnodes > 1): IPC mailboxes are node-local
     if kind in ("ipc", "auto"):
         try:
             return IpcTransport(*args, timeout=timeout)

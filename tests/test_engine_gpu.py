@@ -30,8 +30,8 @@ def _source(n_parts, rows, d, seed=0):
 
 @pytest.mark.parametrize("case", CASES)
 @pytest.mark.parametrize("rule", ["GD", "AGD"])
-@pytest.mark.parametrize("native_loop", [True, False])
-def test_gpu_matches_cpu(case, rule, native_loop, native):
+@pytest.mark.parametrize("native_loop,device_loop", [(True, "graph"), (True, "stream"), (True, "off"), (False, "off")])
+def test_gpu_matches_cpu(case, rule, native_loop, device_loop, native):
     is_coded, P, ver, n_procs, s, k = case
     W = n_procs - 1
     d, rows = 33, 40
@@ -45,17 +45,43 @@ def test_gpu_matches_cpu(case, rule, native_loop, native):
     out = {}
     for dev in ("cpu", "cuda"):
         cfg = RunConfig(n_procs, n, d, "/tmp/eh_gpu_eng/", 0, "x", is_coded, s, P, ver, k, 0, rule, num_itrs=8,
-                        seed=0, verbose=False, native_loop=native_loop)
+                        seed=0, verbose=False, native_loop=native_loop, device_loop=device_loop)
         env = DistEnv(device=torch.device(dev))
         sch = make_scheme(key, W, s, n, k, P, rng=np.random.RandomState(0))
         tr = Trainer(cfg, env, src, scheme=sch)
         assert tr.native_loop == (dev == "cuda" and native_loop)
         res = tr.run()
+        if dev == "cuda":
+            assert tr.device_loop == (None if device_loop == "off" else device_loop)
+            assert np.all(res.timeset > 0) and np.all(np.isfinite(res.timeset))
+            out["arr_" + dev] = res.arrivals
+        else:
+            out["arr_" + dev] = res.arrivals
         out[dev] = res.betaset
         if dev == "cuda":
             ev = evaluate(tr, res, write=False)
             assert np.all(np.isfinite(ev.training_loss))
     np.testing.assert_allclose(out["cuda"], out["cpu"], rtol=1e-9, atol=1e-11)
+    # same arrival sets and order, round by round
+    assert [[(w, p) for (w, p, _t) in r] for r in out["arr_cuda"]] == \
+        [[(w, p) for (w, p, _t) in r] for r in out["arr_cpu"]]
+
+
+def test_gpu_device_loop_timed_segments(native):
+    """bench-style timed fence inside a device-driven run: two graph segments, same betas as host-driven."""
+    src = _source(6, 40, 33)
+    out = {}
+    for mode in ("graph", "off"):
+        cfg = RunConfig(7, 240, 33, "/tmp/eh_gpu_eng/", 0, "x", 1, 2, 0, 3, 4, 0, "AGD", num_itrs=12, seed=0,
+                        verbose=False, device_loop=mode)
+        from erasurehead_amd.codes import make_scheme
+
+        sch = make_scheme("approx", 6, 2, 240, 4, 0, rng=np.random.RandomState(0))
+        tr = Trainer(cfg, DistEnv(device=torch.device("cuda")), src, scheme=sch)
+        res = tr.run(timed_start=5)
+        assert res.timed_rounds == 7 and res.timed_seconds > 0
+        out[mode] = res.betaset
+    np.testing.assert_allclose(out["graph"], out["off"], rtol=1e-12, atol=1e-14)
 
 
 def test_gpu_delay_semantics(native):

@@ -65,6 +65,40 @@ def dense_cases(out):
             torch.cuda.empty_cache()
 
 
+def scale_cases(out):
+    """fp64 d = 1000 at the per-rank sizes of the headline at N = 8/4/2/1 GPUs, task-count sweep.
+
+    Also times torch's sum over the same bytes as a read-bandwidth reference.
+    """
+    import torch
+
+    from erasurehead_amd.models.losses import LOGISTIC
+    from erasurehead_amd.ops import DenseGradPlan, get_precision
+
+    prec = get_precision("fp64")
+    d, rpp = 1000, 125000  # headline partition: 1e6 / 8 rows
+    parts = {}
+    for p in range(22):
+        X = torch.randn(rpp, prec.ld(d), device="cuda", dtype=torch.float64)
+        y = torch.where(torch.rand(rpp, device="cuda") > 0.5, 1.0, -1.0).double()
+        parts[p] = (X, y)
+    beta = torch.randn(prec.ld(d), device="cuda", dtype=torch.float64) * 0.01
+    for nparts in (3, 6, 11, 22):
+        msgs = [[(p, 1.0) for p in range(q, min(nparts, q + 3))] for q in range(0, nparts, 3)]
+        X0 = parts[0][0]
+        ref_ms = _time(lambda: [parts[p][0].sum() for p in range(nparts)], reps=10)
+        for tasks in (1280, 2048, 2560, 3840, 5120):
+            plan = DenseGradPlan(msgs, {p: parts[p] for p in range(nparts)}, prec, LOGISTIC, d, target_tasks=tasks)
+            G = plan.out_buffer()[0]
+            ms = _time(lambda: plan.run(beta, G), reps=20)
+            gb = plan.bytes_per_round / 1e9
+            r = {"kernel": "grad_dense_scale", "parts": nparts, "tasks": plan.ntasks, "ms": ms, "x_gbytes": gb,
+                 "effective_TBps": gb / ms, "torch_sum_ms": ref_ms, "torch_sum_TBps": gb / ref_ms}
+            out.append(r)
+            print(json.dumps(r), flush=True)
+            del plan
+
+
 def sparse_cases(out):
     import torch
 
@@ -95,11 +129,13 @@ def sparse_cases(out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "kernels.jsonl"))
-    ap.add_argument("--only", choices=["dense", "sparse"], default=None)
+    ap.add_argument("--only", choices=["dense", "sparse", "scale"], default=None)
     a = ap.parse_args()
     out = []
     if a.only in (None, "dense"):
         dense_cases(out)
+    if a.only == "scale":
+        scale_cases(out)
     if a.only in (None, "sparse"):
         sparse_cases(out)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)

@@ -41,7 +41,7 @@ def _floor_iters(tl: np.ndarray) -> int:
     return int(np.argmax(tl <= floor + 0.01 * abs(floor)))
 
 
-def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_kw=None):
+def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_kw=None, device_loop="auto"):
     import torch
 
     from erasurehead_amd.config import RunConfig
@@ -49,7 +49,7 @@ def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_
     from erasurehead_amd.parallel.dist import DistEnv
     from erasurehead_amd.utils.delay import delay_floor
 
-    cfg = RunConfig(**cfg_kw, num_itrs=rounds, verbose=False, seed=0)
+    cfg = RunConfig(**cfg_kw, num_itrs=rounds, verbose=False, seed=0, device_loop=device_loop)
     env = DistEnv(device=torch.device("cuda" if torch.cuda.is_available() else "cpu"))
     t0 = time.perf_counter()
     tr = Trainer(cfg, env, source)
@@ -71,6 +71,7 @@ def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_
         "final_auc": float(ev.auc[-1]) if not tr.loss else None,
         "setup_s": setup,
         "native_loop": tr.native_loop,
+        "round_loop": tr.device_loop or ("host-native" if tr.native_loop else "host-python"),
         "precision": cfg.precision,
     }
     if delay_floor_kw is not None:
@@ -89,6 +90,7 @@ def main():
     ap.add_argument("--quick", action="store_true", help="10x smaller problems (plumbing check)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out"))
     ap.add_argument("--only", default=None, help="comma-separated config names")
+    ap.add_argument("--device-loop", default="auto", choices=["auto", "graph", "stream", "off"])
     a = ap.parse_args()
     from erasurehead_amd.data.source import ArraySource
     from erasurehead_amd.data.synthetic import REAL_SHAPES, onehot_partitions
@@ -140,19 +142,19 @@ def main():
     rows = []
     with open(os.path.join(a.out, "suite.jsonl"), "w") as f:
         for name, kw, src, floor_kw in configs:
-            r = run_config(name, kw, src, delay_floor_kw=floor_kw)
+            r = run_config(name, kw, src, delay_floor_kw=floor_kw, device_loop=a.device_loop)
             rows.append(r)
             f.write(json.dumps(r) + "\n")
             f.flush()
             print(json.dumps(r), flush=True)
-    hdr = ("| config | scheme | W | s | k | ms/round | timeset ms | iters to floor | final train loss | AUC | "
-           "delay floor s | overhead ms/round |\n|---|---|---|---|---|---|---|---|---|---|---|---|\n")
+    hdr = ("| config | scheme | W | s | k | loop | ms/round | timeset ms | iters to floor | final train loss | AUC | "
+           "delay floor s | overhead ms/round |\n|---|---|---|---|---|---|---|---|---|---|---|---|---|\n")
     lines = []
     for r in rows:
         auc = "%.4f" % r["final_auc"] if r.get("final_auc") is not None else "-"
         fl = "%.2f" % r["delay_floor_s"] if "delay_floor_s" in r else "-"
         ov = "%.3f" % r["overhead_above_floor_ms_per_round"] if "delay_floor_s" in r else "-"
-        lines.append(f"| {r['config']} | {r['scheme']} | {r['W']} | {r['s']} | {r['num_collect']} | "
+        lines.append(f"| {r['config']} | {r['scheme']} | {r['W']} | {r['s']} | {r['num_collect']} | {r['round_loop']} | "
                      f"{1e3 * r['sec_per_round']:.3f} | {r['timeset_mean_ms']:.3f} | {r['iters_to_loss_floor']} | "
                      f"{r['final_train_loss']:.5f} | {auc} | {fl} | {ov} |")
     with open(os.path.join(a.out, "suite.md"), "w") as f:
