@@ -110,6 +110,8 @@ struct EllChunk {
   int pad;
 };
 
+constexpr int kSmallW = 8;  // features with at most this many categories accumulate in registers
+
 // Column pass: block (chunk of rows of one message, feature k).  Features whose column
 // window fits the LDS budget accumulate r * v into an LDS histogram of the window and
 // flush the touched bins with one global atomic each; wider windows add straight into g.
@@ -126,7 +128,34 @@ ell_colpass(const int* __restrict__ idx, const A* __restrict__ vals, const A* __
   const int* __restrict__ ik = idx + static_cast<long long>(k) * nrows;
   const A* __restrict__ vk = VALS ? vals + static_cast<long long>(k) * nrows : nullptr;
   A* __restrict__ g = G + static_cast<long long>(ch.slot) * ld;
-  if (w <= lds_cap) {
+  if (w <= kSmallW) {
+    // Few categories (the bias column, binary columns): every lane of a wave would hit the
+    // same one or two LDS bins, serialising the atomics 32-64 ways.  Each thread keeps one
+    // register accumulator per category instead (compare-select), then the block reduces
+    // them with wave shuffles and one LDS fold: no atomics until the w global adds.
+    A acc[kSmallW];
+#pragma unroll
+    for (int b = 0; b < kSmallW; ++b) acc[b] = A(0);
+    for (int row = ch.row_begin + threadIdx.x; row < ch.row_end; row += blockDim.x) {
+      const A v = VALS ? rbuf[row] * vk[row] : rbuf[row];
+      const int bin = ik[row] - lo_k;
+#pragma unroll
+      for (int b = 0; b < kSmallW; ++b) acc[b] += bin == b ? v : A(0);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int b = 0; b < kSmallW; ++b) {
+      if (b >= w) break;  // w is uniform over the block
+      const A sb = wave_allreduce_sum(acc[b]);
+      if (lane == 0) hist[wid * kSmallW + b] = sb;
+    }
+    __syncthreads();
+    if (threadIdx.x < w) {
+      A sb = A(0);
+      for (int q = 0; q < nw; ++q) sb += hist[q * kSmallW + threadIdx.x];
+      if (sb != A(0)) atomicAdd(&g[lo_k + threadIdx.x], sb);
+    }
+  } else if (w <= lds_cap) {
     for (int b = threadIdx.x; b < w; b += blockDim.x) hist[b] = A(0);
     __syncthreads();
     for (int row = ch.row_begin + threadIdx.x; row < ch.row_end; row += blockDim.x) {
@@ -155,7 +184,7 @@ hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals
   if (e != hipSuccess || nrows == 0 || m == 0) return e;
   constexpr int kLdsBytes = 64 * 1024;
   const int cap = static_cast<int>(kLdsBytes / esz);
-  const size_t sh = static_cast<size_t>(std::min(max_width, cap)) * esz;
+  const size_t sh = static_cast<size_t>(std::max(std::min(max_width, cap), 4 * kSmallW)) * esz;
   const dim3 block(256), grid1(static_cast<unsigned>((nrows + 255) / 256)), grid2(nchunks, m);
   const EllChunk* C = static_cast<const EllChunk*>(chunks);
 #define EH_ELL(A, VALS)                                                                                  \
