@@ -20,7 +20,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd "$(dirname "$0")/.."
 ARGS="${N_PROCS} ${N_ROWS} ${N_COLS} ${DATA_FOLDER} ${IS_REAL} ${DATASET} ${MODE%% *} ${N_STRAGGLERS} ${N_PARTITIONS} ${MODE##* } ${N_COLLECT} ${ADD_DELAY} ${UPDATE_RULE}"
 if [ "$NGPUS" -gt 1 ]; then
-  python -m torch.distributed.run --nnodes=1 --nproc-per-node "$NGPUS" --master-addr 127.0.0.1 \
+  exec python -m torch.distributed.run --nnodes=1 --nproc-per-node "$NGPUS" --master-addr 127.0.0.1 \
        --master-port "${PORT:-29500}" main.py $ARGS "$@"
 fi
-python main.py $ARGS "$@"
+exec python main.py $ARGS "$@"
