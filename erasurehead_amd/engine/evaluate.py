@@ -16,7 +16,7 @@ import torch
 
 from ..data import io as dio
 from ..models.losses import LOGISTIC
-from ..ops.eval import auc_columns, loss_sums, predictions
+from ..ops.eval import auc_columns, loss_sums, predictions_and_loss
 from ..utils import report
 from .trainer import TrainResult, Trainer
 
@@ -56,10 +56,7 @@ def evaluate(trainer: Trainer, res: TrainResult, log=None, write: bool = True) -
                 log(">> Loaded %d" % (p + 1))
     sums, n_train = loss_sums(trainer.source.train_eval_chunks(parts, prec, dev), B, d, kind)
     Xt, yt = trainer.source.test(prec, dev)
-    P = predictions(Xt, B, d)
-    from ..ops.eval import _loss_torch
-
-    tsum = _loss_torch(kind, yt.to(P.device), P).double().cpu().numpy()
+    P, tsum = predictions_and_loss(Xt, yt, B, d, kind)
     n_test = Xt.shape[0]
     training_loss = sums / max(1, n_train)
     testing_loss = tsum / max(1, n_test)

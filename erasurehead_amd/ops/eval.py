@@ -67,6 +67,19 @@ def predictions(X, B: torch.Tensor, d: int) -> torch.Tensor:
     return X[:, :d].to(acc) @ Bc[:, :d].t()
 
 
+def predictions_and_loss(X, y: torch.Tensor, B: torch.Tensor, d: int, kind: int) -> Tuple[torch.Tensor, np.ndarray]:
+    """(P = X B^T, per-beta loss sums) — on the GPU one MFMA GEMM with the loss fused in its epilogue."""
+    if not _is_sparse(X) and X.is_cuda:
+        n = X.shape[0]
+        acc = torch.float64 if X.dtype == torch.float64 else torch.float32
+        P = torch.empty((n, B.shape[0]), dtype=acc, device=X.device)
+        s = torch.zeros(B.shape[0], dtype=torch.float64, device=X.device)
+        native().eval_gemm_loss(kind, X, n, d, y.to(acc).contiguous(), B.to(acc).contiguous(), s, P)
+        return P, s.cpu().numpy()
+    P = predictions(X, B, d)
+    return P, _loss_torch(kind, y.to(P.device), P).double().cpu().numpy()
+
+
 def loss_sums(chunks: Iterable[Tuple[object, torch.Tensor]], B: torch.Tensor, d: int, kind: int) -> Tuple[np.ndarray, int]:
     """Sum over all chunk rows of the per-row loss for every beta row of B -> ([R], n)."""
     R = B.shape[0]
