@@ -99,6 +99,29 @@ def scale_cases(out):
             del plan
 
 
+def eval_cases(out):
+    """Post-hoc evaluation GEMM (MFMA, loss fused): X [n, 1000] . B[100, 1000]^T, fp64 / fp32."""
+    import torch
+
+    from erasurehead_amd._ext import native
+    from erasurehead_amd.models.losses import LOGISTIC
+
+    for dt, n in ((torch.float64, 1_000_000), (torch.float32, 1_000_000)):
+        d, R = 1000, 100
+        X = torch.randn(n, d, device="cuda", dtype=dt)
+        y = torch.where(torch.rand(n, device="cuda") > 0.5, 1.0, -1.0).to(dt)
+        B = (torch.randn(R, d, device="cuda", dtype=dt) * 0.01).contiguous()
+        s = torch.zeros(R, dtype=torch.float64, device="cuda")
+        ms = _time(lambda: native().eval_gemm_loss(LOGISTIC, X, n, d, y, B, s, None), reps=10, warm=2)
+        flops = 2.0 * n * d * R
+        r = {"kernel": "eval_gemm_loss", "dtype": str(dt), "n": n, "d": d, "R": R, "ms": ms,
+             "TFLOPs": flops / ms / 1e9, "x_TBps": n * d * X.element_size() / ms / 1e9,
+             "v1": bool(os.environ.get("ERASUREHEAD_EVAL_V1"))}
+        out.append(r)
+        print(json.dumps(r), flush=True)
+        del X
+
+
 def sparse_cases(out):
     import torch
 
@@ -129,13 +152,15 @@ def sparse_cases(out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "kernels.jsonl"))
-    ap.add_argument("--only", choices=["dense", "sparse", "scale"], default=None)
+    ap.add_argument("--only", choices=["dense", "sparse", "scale", "eval"], default=None)
     a = ap.parse_args()
     out = []
     if a.only in (None, "dense"):
         dense_cases(out)
     if a.only == "scale":
         scale_cases(out)
+    if a.only == "eval":
+        eval_cases(out)
     if a.only in (None, "sparse"):
         sparse_cases(out)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
