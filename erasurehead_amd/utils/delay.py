@@ -46,12 +46,19 @@ class DelayModel:
         return d
 
 
-def delay_floor(n_workers: int, rounds: int, stop_count=None, groups=None, k=None, mean=0.5) -> float:
+def delay_floor(n_workers: int, rounds: int, stop_count=None, groups=None, k=None, mean=0.5,
+                carry: bool = False) -> float:
     """Sum over rounds of the injected delay the master must wait for.
 
     stop_count: wait for the `stop_count`-th smallest delay (naive: W, cyclic: W-s).
     groups/k:   FRC/AGC rule — stop at k arrivals or when every group is covered.
+    carry:      schemes that do not drain (cyclic, avoidstragg): a straggler still busy with
+                round i-1 starts round i late (the collector's
+                ready = max(t_start, finish(w, i-1)) + delay), so the floor is the exact
+                zero-compute replay of that timeline instead of the per-round order statistic.
     """
+    if carry:
+        return _carried_floor(n_workers, rounds, stop_count, groups, k, mean)
     tot = 0.0
     for i in range(rounds):
         d = np.random.RandomState(seed=i).exponential(mean, n_workers)
@@ -70,4 +77,29 @@ def delay_floor(n_workers: int, rounds: int, stop_count=None, groups=None, k=Non
             if cnt >= k or len(covered) >= n_groups:
                 break
         tot += float(t)
+    return tot
+
+
+def _carried_floor(n_workers, rounds, stop_count, groups, k, mean) -> float:
+    finish = np.zeros(n_workers)  # virtual finish of every worker's latest message
+    t = 0.0  # start of the current round (= decode of the previous one, zero compute)
+    tot = 0.0
+    n_groups = len(set(groups)) if groups is not None else 0
+    for i in range(rounds):
+        d = np.random.RandomState(seed=i).exponential(mean, n_workers)
+        ready = np.maximum(t, finish) + d
+        finish = ready
+        order = np.argsort(ready, kind="stable")
+        if groups is None:
+            t_stop = float(ready[order[stop_count - 1]])
+        else:
+            covered, cnt = set(), 0
+            for w in order:
+                t_stop = float(ready[w])
+                cnt += 1
+                covered.add(groups[w])
+                if cnt >= k or len(covered) >= n_groups:
+                    break
+        tot += t_stop - t
+        t = t_stop
     return tot

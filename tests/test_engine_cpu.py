@@ -243,3 +243,19 @@ def test_shared_plan_encoding_matrix():
     np.testing.assert_array_equal(sp.E.numpy(), [[1, -2, 0], [0, 0.5, 1], [0, 0, 3]])
     assert SharedGradPlan.worthwhile(msgs, lambda p: 10)
     assert not SharedGradPlan.worthwhile([[(0, 1.0)], [(1, 1.0)]], lambda p: 10)
+
+
+def test_delay_floor_with_carried_lag():
+    """avoidstragg does not drain: Σtimeset follows the carried-lag replay, which exceeds the
+    independent per-round order statistic."""
+    from erasurehead_amd.utils.delay import delay_floor
+
+    cfg, src, sch, parts = make((1, 0, 2, 7, 2, 0), "AGD", delay_mean=0.01)
+    cfg.add_delay = 1
+    cfg.force_delay = True
+    tr = Trainer(cfg, DistEnv(), src, scheme=sch)
+    res = tr.run()
+    plain = delay_floor(6, 6, stop_count=4, mean=0.01)
+    carried = delay_floor(6, 6, stop_count=4, mean=0.01, carry=True)
+    assert carried >= plain
+    assert carried <= res.timeset.sum() < carried + 6 * 0.02

@@ -121,7 +121,7 @@ def main():
     n8 = sum(p[0].shape[0] for p in cov8)
     src8 = ArraySource(cov8, cov8_test, sparse=True)
     configs.append(("avoid_covtype", dict(base_cov, n_rows=n8, is_coded=1, n_stragglers=s, coded_ver=2),
-                    src8, {"stop_count": W - s}))
+                    src8, {"stop_count": W - s, "carry": True}))
     configs.append(("agc_covtype", dict(base_cov, n_rows=n8, is_coded=1, n_stragglers=s, coded_ver=3, num_collect=6,
                                         add_delay=0, force_delay=False), src8, None))
 
