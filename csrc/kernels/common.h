@@ -26,6 +26,9 @@ template <typename T> struct Vec16;
 template <> struct Vec16<double> {
   static constexpr int N = 2;
   using raw = double2;
+  __device__ __forceinline__ static raw load_raw(const double* p) { return *reinterpret_cast<const raw*>(p); }
+  template <typename A>
+  __device__ __forceinline__ static A elem(const raw& v, int i) { return static_cast<A>(i == 0 ? v.x : v.y); }
   template <typename A>
   __device__ __forceinline__ static void load(const double* p, A (&out)[N]) {
     const double2 v = *reinterpret_cast<const double2*>(p);
@@ -35,6 +38,12 @@ template <> struct Vec16<double> {
 };
 template <> struct Vec16<float> {
   static constexpr int N = 4;
+  using raw = float4;
+  __device__ __forceinline__ static raw load_raw(const float* p) { return *reinterpret_cast<const raw*>(p); }
+  template <typename A>
+  __device__ __forceinline__ static A elem(const raw& v, int i) {
+    return static_cast<A>(i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
+  }
   template <typename A>
   __device__ __forceinline__ static void load(const float* p, A (&out)[N]) {
     const float4 v = *reinterpret_cast<const float4*>(p);
@@ -46,6 +55,13 @@ template <> struct Vec16<float> {
 };
 template <> struct Vec16<bf16_t> {
   static constexpr int N = 8;
+  using raw = uint4;
+  __device__ __forceinline__ static raw load_raw(const bf16_t* p) { return *reinterpret_cast<const raw*>(p); }
+  template <typename A>
+  __device__ __forceinline__ static A elem(const raw& v, int i) {  // i is a compile-time constant after unrolling
+    const uint32_t w = (i >> 1) == 0 ? v.x : (i >> 1) == 1 ? v.y : (i >> 1) == 2 ? v.z : v.w;
+    return static_cast<A>(__uint_as_float((i & 1) ? (w & 0xffff0000u) : (w << 16)));
+  }
   template <typename A>
   __device__ __forceinline__ static void load(const bf16_t* p, A (&out)[N]) {
     const uint4 v = *reinterpret_cast<const uint4*>(p);

@@ -11,8 +11,9 @@
 // instruction), form the dot product with beta held in registers, butterfly-reduce
 // it across the wave, apply the loss epilogue (label encoding fused in as a
 // per-segment coefficient) and immediately accumulate r * x_row into a per-lane
-// register slice of g.  Two rows are kept in flight per wave so the reduction
-// latency of one overlaps the loads of the other.  At the end each workgroup
+// register slice of g.  ROWS rows are loaded per wave iteration as raw 16-byte tiles (every
+// load issues before the first conversion waits), so the reduction latency of one row
+// overlaps the loads of the others; the rows-in-flight count is tuned per storage type.  At the end each workgroup
 // folds its 4 waves through LDS and writes one fp64/fp32 slab row; a second tiny
 // kernel sums the slab rows of each output message in a fixed order (bitwise
 // reproducible, no float atomics).
@@ -20,6 +21,9 @@
 // The "task" table lets one launch serve every logical worker hosted on this GPU
 // (e.g. all 8 FRC/AGC workers at N=1): task -> (output message slot, segment,
 // row range); segment -> (partition base pointer, labels, encoding coefficient).
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 
 namespace eh {
@@ -38,9 +42,126 @@ struct Task {
   int row_end;
 };
 
-template <typename T, typename A, int CPL, int LOSS>
+template <typename T, typename A, int CPL, int LOSS, int ROWS>
 __global__ void __launch_bounds__(256)
 grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
+                 const A* __restrict__ beta, A* __restrict__ slab, int ld) {
+  constexpr int VN = Vec16<T>::N;
+  constexpr int NV = CPL / VN;  // vector loads per row per lane
+  static_assert(CPL % VN == 0, "CPL must be a multiple of the vector width");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  A* red = reinterpret_cast<A*>(smem_raw);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+
+  const Task task = tasks[blockIdx.x];
+  const Segment seg = segs[task.seg];
+  const T* __restrict__ X = static_cast<const T*>(seg.X);
+  const A* __restrict__ Y = static_cast<const A*>(seg.y);
+  const A coef = static_cast<A>(seg.coef);
+
+  // Column ownership: vector j of lane l covers columns [(j*64+l)*VN, +VN).
+  bool valid[NV];
+  A b[NV][VN];
+  A g[NV][VN];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * kWave + lane) * VN;
+    valid[j] = c0 < ld;
+#pragma unroll
+    for (int v = 0; v < VN; ++v) {
+      b[j][v] = valid[j] ? beta[c0 + v] : A(0);
+      g[j][v] = A(0);
+    }
+  }
+
+  int r = task.row_begin + wid;
+  // Main loop: ROWS rows per wave per iteration, all loads issued before the first reduction
+  // (ROWS * NV 16-byte loads in flight per lane).
+  for (; r + (ROWS - 1) * nw < task.row_end; r += ROWS * nw) {
+    // raw 16-byte tiles: every load of the iteration issues before any conversion waits on one
+    typename Vec16<T>::raw xr[ROWS][NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int q = 0; q < ROWS; ++q) {
+        const int c0 = (j * kWave + lane) * VN;
+        if (valid[j]) xr[q][j] = Vec16<T>::load_raw(X + static_cast<long long>(r + q * nw) * ld + c0);
+        else xr[q][j] = typename Vec16<T>::raw{};
+      }
+    A z[ROWS];
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q) z[q] = A(0);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v)
+#pragma unroll
+        for (int q = 0; q < ROWS; ++q) z[q] = fma(Vec16<T>::template elem<A>(xr[q][j], v), b[j][v], z[q]);
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q) z[q] = wave_allreduce_sum(z[q]);
+    A rq[ROWS];
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q) rq[q] = residual<LOSS, A>(z[q], Y[r + q * nw], coef);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v)
+#pragma unroll
+        for (int q = 0; q < ROWS; ++q) g[j][v] = fma(rq[q], Vec16<T>::template elem<A>(xr[q][j], v), g[j][v]);
+  }
+  // Tail: fewer than ROWS rows left for this wave, one at a time.
+  for (; r < task.row_end; r += nw) {
+    const T* x0 = X + static_cast<long long>(r) * ld;
+    A a0[NV][VN];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c0 = (j * kWave + lane) * VN;
+      if (valid[j]) {
+        Vec16<T>::load(x0 + c0, a0[j]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < VN; ++v) a0[j][v] = A(0);
+      }
+    }
+    A z0 = A(0);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v) z0 = fma(a0[j][v], b[j][v], z0);
+    z0 = wave_allreduce_sum(z0);
+    const A r0 = residual<LOSS, A>(z0, Y[r], coef);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v) g[j][v] = fma(r0, a0[j][v], g[j][v]);
+  }
+
+  // Fold the waves of this workgroup through LDS, then one slab row per workgroup.
+  const int span = kWave * CPL;  // padded columns covered by a wave
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * kWave + lane) * VN;
+#pragma unroll
+    for (int v = 0; v < VN; ++v) red[wid * span + c0 + v] = g[j][v];
+  }
+  __syncthreads();
+  A* out = slab + static_cast<long long>(blockIdx.x) * ld;
+  for (int c = threadIdx.x; c < ld; c += blockDim.x) {
+    A s = A(0);
+    for (int w = 0; w < nw; ++w) s += red[w * span + c];
+    out[c] = s;
+  }
+}
+
+// Two rows per wave per iteration, loads of both rows interleaved per vector (the layout
+// that measured fastest for bf16 and fp32).
+template <typename T, typename A, int CPL, int LOSS>
+__global__ void __launch_bounds__(256)
+grad_dense_fused_pair(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                  const A* __restrict__ beta, A* __restrict__ slab, int ld) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;  // vector loads per row per lane
@@ -379,6 +500,19 @@ static hipError_t launch_wide(int bs, const Segment* segs, const Task* tasks, in
   return hipGetLastError();
 }
 
+// Rows in flight per wave (tools/sweep_grad_rows.sh, docs/PERF_NOTES.md): the generic kernel
+// with 1 row for fp64 and bf16 and 4 rows for fp32, measured at full headline scale against
+// the interleaved pair kernel (2).  ERASUREHEAD_GRAD_ROWS = 1 | 2 | 4 overrides (sweeps only).
+template <typename T>
+static int fused_rows() {
+  static const int env = [] {
+    const char* e = std::getenv("ERASUREHEAD_GRAD_ROWS");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (env == 1 || env == 2 || env == 4) return env;
+  return std::is_same<T, float>::value ? 4 : 1;
+}
+
 template <typename T, typename A, int LOSS>
 static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
                                    const A* beta, A* slab, int ld, hipStream_t st) {
@@ -387,12 +521,20 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
   const dim3 grid(ntasks);
   constexpr int VN = Vec16<T>::N;
   // CPL (columns per lane) must be a multiple of the 16-byte vector width VN.
+  const int rows = fused_rows<T>();
 #define EH_IF(C)                                                                          \
   case C:                                                                                 \
     if constexpr (C % VN == 0) {                                                          \
       const size_t sh = 4ull * kWave * C * sizeof(A);                                     \
-      hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS>), grid, block, sh, st, segs,    \
-                         tasks, beta, slab, ld);                                          \
+      if (rows == 1)                                                                      \
+        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1>), grid, block, sh, st,     \
+                           segs, tasks, beta, slab, ld);                                  \
+      else if (rows == 4)                                                                 \
+        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 4>), grid, block, sh, st,     \
+                           segs, tasks, beta, slab, ld);                                  \
+      else                                                                                \
+        hipLaunchKernelGGL((grad_dense_fused_pair<T, A, C, LOSS>), grid, block, sh, st,   \
+                           segs, tasks, beta, slab, ld);                                  \
       return hipGetLastError();                                                           \
     } else {                                                                              \
       return hipErrorInvalidValue;                                                        \
