@@ -42,7 +42,7 @@ struct Task {
   int row_end;
 };
 
-template <typename T, typename A, int CPL, int LOSS, int ROWS>
+template <typename T, typename A, int CPL, int LOSS, int ROWS, bool BL = false>
 __global__ void __launch_bounds__(256)
 grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                  const A* __restrict__ beta, A* __restrict__ slab, int ld) {
@@ -64,24 +64,36 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
   const A coef = static_cast<A>(seg.coef);
 
   // Column ownership: vector j of lane l covers columns [(j*64+l)*VN, +VN).
+  // BL: beta lives in LDS (after the fold area) and is re-read every row instead of pinning
+  // NV*VN registers, so more rows fit in flight at the same occupancy.
+  A* bl = red + 4 * kWave * CPL;
   bool valid[NV];
-  A b[NV][VN];
+  A b[BL ? 1 : NV][VN];
   A g[NV][VN];
+  if constexpr (BL) {
+    for (int c = threadIdx.x; c < kWave * CPL; c += blockDim.x) bl[c] = c < ld ? beta[c] : A(0);
+    __syncthreads();
+  }
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int c0 = (j * kWave + lane) * VN;
     valid[j] = c0 < ld;
 #pragma unroll
     for (int v = 0; v < VN; ++v) {
-      b[j][v] = valid[j] ? beta[c0 + v] : A(0);
+      if constexpr (!BL) b[j][v] = valid[j] ? beta[c0 + v] : A(0);
       g[j][v] = A(0);
     }
   }
+  auto bval = [&](int j, int v) -> A {
+    if constexpr (BL) return bl[(j * kWave + lane) * VN + v];
+    else return b[j][v];
+  };
 
   int r = task.row_begin + wid;
   // Main loop: ROWS rows per wave per iteration, all loads issued before the first reduction
   // (ROWS * NV 16-byte loads in flight per lane).
   for (; r + (ROWS - 1) * nw < task.row_end; r += ROWS * nw) {
+    if constexpr (BL) asm volatile("" ::: "memory");  // keep the beta reads inside the loop
     // raw 16-byte tiles: every load of the iteration issues before any conversion waits on one
     typename Vec16<T>::raw xr[ROWS][NV];
 #pragma unroll
@@ -100,7 +112,7 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
 #pragma unroll
       for (int v = 0; v < VN; ++v)
 #pragma unroll
-        for (int q = 0; q < ROWS; ++q) z[q] = fma(Vec16<T>::template elem<A>(xr[q][j], v), b[j][v], z[q]);
+        for (int q = 0; q < ROWS; ++q) z[q] = fma(Vec16<T>::template elem<A>(xr[q][j], v), bval(j, v), z[q]);
 #pragma unroll
     for (int q = 0; q < ROWS; ++q) z[q] = wave_allreduce_sum(z[q]);
     A rq[ROWS];
@@ -131,7 +143,7 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
 #pragma unroll
     for (int j = 0; j < NV; ++j)
 #pragma unroll
-      for (int v = 0; v < VN; ++v) z0 = fma(a0[j][v], b[j][v], z0);
+      for (int v = 0; v < VN; ++v) z0 = fma(a0[j][v], bval(j, v), z0);
     z0 = wave_allreduce_sum(z0);
     const A r0 = residual<LOSS, A>(z0, Y[r], coef);
 #pragma unroll
@@ -500,16 +512,20 @@ static hipError_t launch_wide(int bs, const Segment* segs, const Task* tasks, in
   return hipGetLastError();
 }
 
-// Rows in flight per wave (tools/sweep_grad_rows.sh, docs/PERF_NOTES.md): the generic kernel
-// with 1 row for fp64 and bf16 and 4 rows for fp32, measured at full headline scale against
-// the interleaved pair kernel (2).  ERASUREHEAD_GRAD_ROWS = 1 | 2 | 4 overrides (sweeps only).
+// Kernel variant of grad_dense_fused per storage type (tools/sweep_grad_rows.sh,
+// docs/PERF_NOTES.md), measured at full headline scale:
+//   1 / 2 / 4  beta in registers, 1 row / the interleaved pair kernel / 4 rows in flight
+//   5 / 6 / 7  beta in LDS, 1 / 2 / 4 rows in flight
+// fp64 -> 6 (frees 32 VGPRs: 2 rows at 3 waves/SIMD), fp32 -> 4, bf16 -> 1.
+// ERASUREHEAD_GRAD_ROWS overrides (sweeps only).
 template <typename T>
 static int fused_rows() {
   static const int env = [] {
     const char* e = std::getenv("ERASUREHEAD_GRAD_ROWS");
     return e ? std::atoi(e) : 0;
   }();
-  if (env == 1 || env == 2 || env == 4) return env;
+  if (env >= 1 && env <= 7 && env != 3) return env;
+  if (std::is_same<T, double>::value) return 6;
   return std::is_same<T, float>::value ? 4 : 1;
 }
 
@@ -526,7 +542,17 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
   case C:                                                                                 \
     if constexpr (C % VN == 0) {                                                          \
       const size_t sh = 4ull * kWave * C * sizeof(A);                                     \
-      if (rows == 1)                                                                      \
+      const size_t shb = sh + kWave * C * sizeof(A);                                      \
+      if (rows == 5)                                                                      \
+        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1, true>), grid, block, shb,  \
+                           st, segs, tasks, beta, slab, ld);                              \
+      else if (rows == 6)                                                                 \
+        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 2, true>), grid, block, shb,  \
+                           st, segs, tasks, beta, slab, ld);                              \
+      else if (rows == 7)                                                                 \
+        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 4, true>), grid, block, shb,  \
+                           st, segs, tasks, beta, slab, ld);                              \
+      else if (rows == 1)                                                                 \
         hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1>), grid, block, sh, st,     \
                            segs, tasks, beta, slab, ld);                                  \
       else if (rows == 4)                                                                 \
