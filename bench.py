@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--stragglers", type=int, default=2)
     ap.add_argument("--num-collect", type=int, default=6)
     ap.add_argument("--coded-ver", type=int, default=3)
+    ap.add_argument("--naive", action="store_true", help="uncoded baseline (is_coded=0), not the headline")
     ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32", "bf16"])
     ap.add_argument("--update-rule", default="AGD")
     ap.add_argument("--add-delay", type=int, default=0)
@@ -65,7 +66,8 @@ def main() -> int:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={env.world}", file=sys.stderr)
 
     def make_cfg(rounds: int) -> RunConfig:
-        return RunConfig(a.workers + 1, a.n_rows, a.n_cols, "/tmp/erasurehead_bench/", 0, "synthetic", 1,
+        return RunConfig(a.workers + 1, a.n_rows, a.n_cols, "/tmp/erasurehead_bench/", 0, "synthetic",
+                         0 if a.naive else 1,
                          a.stragglers, 0, a.coded_ver, a.num_collect, a.add_delay, a.update_rule,
                          num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234, seed=0,
                          allow_uneven_groups=True, verbose=False, tasks=a.tasks,
@@ -100,8 +102,9 @@ def main() -> int:
             "data": "synthetic (on-device GMM of ref generate_data.py; random-init beta)",
             "config": {
                 "model": "L2 logistic regression (d=%d)" % a.n_cols,
-                "scheme": {3: "approx (AGC)", 1: "replication (FRC)", 0: "coded (cyclic MDS)",
-                           2: "avoidstragg"}.get(a.coded_ver, str(a.coded_ver)),
+                "scheme": "naive (uncoded)" if a.naive else {3: "approx (AGC)", 1: "replication (FRC)",
+                                                            0: "coded (cyclic MDS)",
+                                                            2: "avoidstragg"}.get(a.coded_ver, str(a.coded_ver)),
                 "global_batch": a.n_rows,
                 "seq_len": None,
                 "n_rows": a.n_rows, "n_cols": a.n_cols, "workers": a.workers,

@@ -59,7 +59,7 @@ void need_part(const Tensor& part, int64_t nslots, int64_t ld, int ac) {
 
 void grad_dense(int64_t dtype, int64_t loss, int64_t cpl, const Tensor& segs, const Tensor& tasks,
                 const Tensor& beta, const Tensor& slab, const Tensor& slot_task_begin, const Tensor& part,
-                const Tensor& G, int64_t ld) {
+                const Tensor& G, int64_t ld, int64_t variant) {
   need_cuda(segs, "segs");
   need_cuda(tasks, "tasks");
   need_cuda(beta, "beta");
@@ -68,7 +68,7 @@ void grad_dense(int64_t dtype, int64_t loss, int64_t cpl, const Tensor& segs, co
   need_cuda(G, "G");
   const int64_t ntasks = tasks.size(0);
   const int64_t nslots = slot_task_begin.numel() - 1;
-  need(tasks.dim() == 2 && tasks.size(1) == 4 && tasks.scalar_type() == at::kInt, "tasks must be int32 [ntasks, 4]");
+  need(tasks.dim() == 2 && tasks.size(1) == 5 && tasks.scalar_type() == at::kInt, "tasks must be int32 [ntasks, 5]");
   need(segs.scalar_type() == at::kByte && segs.numel() % 32 == 0, "segs must be packed uint8 [nseg*32]");
   need(slab.dim() == 2 && slab.size(0) >= ntasks && slab.size(1) == ld, "slab must be [>=ntasks, ld]");
   need(G.dim() == 2 && G.size(0) == nslots && G.size(1) == ld, "G must be [nslots, ld]");
@@ -83,7 +83,7 @@ void grad_dense(int64_t dtype, int64_t loss, int64_t cpl, const Tensor& segs, co
   if (ntasks == 0) return;
   check(eh::grad_dense_launch((int)dtype, (int)loss, (int)cpl, segs.data_ptr(), tasks.data_ptr(), (int)ntasks,
                               beta.data_ptr(), slab.data_ptr(), slot_task_begin.data_ptr<int>(), (int)nslots,
-                              part.data_ptr(), G.data_ptr(), (int)ld, stream_of(G)),
+                              part.data_ptr(), G.data_ptr(), (int)ld, stream_of(G), (int)variant),
         "grad_dense");
 }
 

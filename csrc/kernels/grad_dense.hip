@@ -40,6 +40,8 @@ struct Task {
   int seg;        // segment index
   int row_begin;  // rows of the segment handled by this workgroup
   int row_end;
+  int slab;       // slab row of this task's partial sum (tasks are dispatched in replica-
+                  // interleaved order; slab rows stay contiguous per message slot)
 };
 
 template <typename T, typename A, int CPL, int LOSS, int ROWS, bool BL = false>
@@ -161,7 +163,7 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
     for (int v = 0; v < VN; ++v) red[wid * span + c0 + v] = g[j][v];
   }
   __syncthreads();
-  A* out = slab + static_cast<long long>(blockIdx.x) * ld;
+  A* out = slab + static_cast<long long>(task.slab) * ld;
   for (int c = threadIdx.x; c < ld; c += blockDim.x) {
     A s = A(0);
     for (int w = 0; w < nw; ++w) s += red[w * span + c];
@@ -277,7 +279,7 @@ grad_dense_fused_pair(const Segment* __restrict__ segs, const Task* __restrict__
     for (int v = 0; v < VN; ++v) red[wid * span + c0 + v] = g[j][v];
   }
   __syncthreads();
-  A* out = slab + static_cast<long long>(blockIdx.x) * ld;
+  A* out = slab + static_cast<long long>(task.slab) * ld;
   for (int c = threadIdx.x; c < ld; c += blockDim.x) {
     A s = A(0);
     for (int w = 0; w < nw; ++w) s += red[w * span + c];
@@ -365,7 +367,7 @@ grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks
 #pragma unroll
       for (int v = 0; v < VN; ++v) g[j][v] = fma(r1, a1[j][v], fma(r0, a0[j][v], g[j][v]));
   }
-  A* out = slab + static_cast<long long>(blockIdx.x) * ld;
+  A* out = slab + static_cast<long long>(task.slab) * ld;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int c0 = (j * BS + tid) * VN;
@@ -480,7 +482,7 @@ xt_r_tiles(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
 #pragma unroll
     for (int v = 0; v < VN; ++v) g[v] = fma(rr, a[v], g[v]);
   }
-  A* out = slab + static_cast<long long>(blockIdx.x) * ld + c0;
+  A* out = slab + static_cast<long long>(task.slab) * ld + c0;
 #pragma unroll
   for (int v = 0; v < VN; ++v) out[v] = g[v];
 }
@@ -518,26 +520,29 @@ static hipError_t launch_wide(int bs, const Segment* segs, const Task* tasks, in
 //   5 / 6 / 7  beta in LDS, 1 / 2 / 4 rows in flight
 // fp64 -> 6 (frees 32 VGPRs: 2 rows at 3 waves/SIMD), fp32 -> 4, bf16 -> 1.
 // ERASUREHEAD_GRAD_ROWS overrides (sweeps only).
+// The plan may request a variant (DenseGradPlan.variant: replica-shared vs distinct rows).
 template <typename T>
-static int fused_rows() {
+static int fused_rows(int requested) {
   static const int env = [] {
     const char* e = std::getenv("ERASUREHEAD_GRAD_ROWS");
     return e ? std::atoi(e) : 0;
   }();
-  if (env >= 1 && env <= 7 && env != 3) return env;
+  auto ok = [](int v) { return v >= 1 && v <= 7 && v != 3; };
+  if (ok(env)) return env;
+  if (ok(requested)) return requested;
   if (std::is_same<T, double>::value) return 6;
   return std::is_same<T, float>::value ? 4 : 1;
 }
 
 template <typename T, typename A, int LOSS>
 static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
-                                   const A* beta, A* slab, int ld, hipStream_t st) {
+                                   const A* beta, A* slab, int ld, hipStream_t st, int variant) {
   if (cpl >= 256) return launch_wide<T, A, LOSS>(cpl, segs, tasks, ntasks, beta, slab, ld, st);
   const dim3 block(256);
   const dim3 grid(ntasks);
   constexpr int VN = Vec16<T>::N;
   // CPL (columns per lane) must be a multiple of the 16-byte vector width VN.
-  const int rows = fused_rows<T>();
+  const int rows = fused_rows<T>(variant);
 #define EH_IF(C)                                                                          \
   case C:                                                                                 \
     if constexpr (C % VN == 0) {                                                          \
@@ -580,22 +585,22 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
 // dtype codes: 0 = fp64 storage/fp64 acc, 1 = fp32/fp32, 2 = bf16 storage/fp32 acc
 hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
                              int ntasks, const void* beta, void* slab, const int* slot_task_begin,
-                             int nslots, void* part, void* G, int ld, hipStream_t st) {
+                             int nslots, void* part, void* G, int ld, hipStream_t st, int variant) {
   const Segment* S = static_cast<const Segment*>(segs);
   const Task* Tk = static_cast<const Task*>(tasks);
   hipError_t e = hipSuccess;
   if (dtype == 0) {
     e = loss == kLogistic
-            ? launch_fused_cpl<double, double, kLogistic>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st)
-            : launch_fused_cpl<double, double, kLeastSquares>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st);
+            ? launch_fused_cpl<double, double, kLogistic>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, variant)
+            : launch_fused_cpl<double, double, kLeastSquares>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, variant);
   } else if (dtype == 1) {
     e = loss == kLogistic
-            ? launch_fused_cpl<float, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st)
-            : launch_fused_cpl<float, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st);
+            ? launch_fused_cpl<float, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant)
+            : launch_fused_cpl<float, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant);
   } else {
     e = loss == kLogistic
-            ? launch_fused_cpl<bf16_t, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st)
-            : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st);
+            ? launch_fused_cpl<bf16_t, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant)
+            : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant);
   }
   if (e != hipSuccess) return e;
   if (dtype == 0) return slab_reduce_launch<double>((const double*)slab, slot_task_begin, (double*)part, (double*)G, nslots, ld, st);

@@ -11,9 +11,10 @@ namespace eh {
 
 // ---- worker gradient (grad_dense.hip, grad_sparse.hip) -------------------------------
 // dtype: 0 fp64 storage/acc, 1 fp32/fp32, 2 bf16 storage/fp32 acc; loss: 0 logistic, 1 least squares
+// variant: 0 = per-dtype default, else the grad_dense_fused variant (grad_dense.hip fused_rows)
 hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
                              int ntasks, const void* beta, void* slab, const int* slot_task_begin,
-                             int nslots, void* part, void* G, int ld, hipStream_t st);
+                             int nslots, void* part, void* G, int ld, hipStream_t st, int variant = 0);
 hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, const void* tasks,
                                      int ntasks, const void* beta, const int* task_row_off,
                                      void* rbuf, void* slab, const int* slot_task_begin,

@@ -93,7 +93,7 @@ void need_gpu(const Tensor& t, const char* name) {
 // launcher also holds references.
 struct GradLauncher {
   int kind = 0;  // 0 dense fused, 1 dense two-pass, 2 sparse
-  int dtype = 0, loss = 0, cpl = 0, ntasks = 0, nslots = 0, ld = 0;
+  int dtype = 0, loss = 0, cpl = 0, ntasks = 0, nslots = 0, ld = 0, variant = 0;
   const void* segs = nullptr;
   const void* tasks = nullptr;
   void* slab = nullptr;
@@ -139,7 +139,7 @@ struct GradLauncher {
     switch (kind) {
       case 0:
         return ntasks ? eh::grad_dense_launch(dtype, loss, cpl, segs, tasks, ntasks, beta, slab, stb, nslots, part, G,
-                                              ld, st)
+                                              ld, st, variant)
                       : hipSuccess;
       case 1:
         return ntasks ? eh::grad_dense_twopass_launch(dtype, loss, segs, tasks, ntasks, beta, task_row_off, rbuf, slab,
@@ -160,14 +160,15 @@ struct GradLauncher {
 std::shared_ptr<GradLauncher> make_dense(int64_t dtype, int64_t loss, int64_t cpl, const Tensor& segs,
                                          const Tensor& tasks, const Tensor& slab, const Tensor& stb,
                                          const Tensor& part, int64_t ld, std::optional<Tensor> task_row_off,
-                                         std::optional<Tensor> rbuf) {
+                                         std::optional<Tensor> rbuf, int64_t variant) {
   for (auto* t : {&segs, &tasks, &slab, &stb, &part}) need_gpu(*t, "dense plan operand");
-  need(tasks.dim() == 2 && tasks.size(1) == 4 && tasks.scalar_type() == at::kInt, "tasks must be int32 [n,4]");
+  need(tasks.dim() == 2 && tasks.size(1) == 5 && tasks.scalar_type() == at::kInt, "tasks must be int32 [n,5]");
   need(stb.scalar_type() == at::kInt, "slot_task_begin must be int32");
   auto g = std::make_shared<GradLauncher>();
   g->dtype = (int)dtype;
   g->loss = (int)loss;
   g->cpl = (int)cpl;
+  g->variant = (int)variant;
   g->ld = (int)ld;
   g->ntasks = (int)tasks.size(0);
   g->nslots = (int)stb.numel() - 1;
@@ -794,7 +795,7 @@ void bind_engine(py::module& m) {
   py::class_<GradLauncher, std::shared_ptr<GradLauncher>>(m, "GradLauncher")
       .def_static("dense", &make_dense, py::arg("dtype"), py::arg("loss"), py::arg("cpl"), py::arg("segs"),
                   py::arg("tasks"), py::arg("slab"), py::arg("slot_task_begin"), py::arg("part"), py::arg("ld"),
-                  py::arg("task_row_off") = py::none(), py::arg("rbuf") = py::none())
+                  py::arg("task_row_off") = py::none(), py::arg("rbuf") = py::none(), py::arg("variant") = 0)
       .def_static("sparse", &make_sparse, py::arg("loss"), py::arg("row_ptr"), py::arg("col_idx"), py::arg("vals"),
                   py::arg("y"), py::arg("coef"), py::arg("rbuf"), py::arg("keys"), py::arg("rows"), py::arg("cvals"),
                   py::arg("nslots"), py::arg("ld"))

@@ -15,6 +15,7 @@ native kernels are mandatory (:func:`erasurehead_amd._ext.native` raises if abse
 """
 from __future__ import annotations
 
+import os
 import struct
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -28,6 +29,7 @@ from .precision import Precision
 _SEG = struct.Struct("<QQdq")  # csrc Segment {const void* X; const void* y; double coef; long long nrows}
 MAX_CPL = 32
 DEFAULT_TASKS = 2048
+REPLICA_TASKS = 4096
 MIN_ROWS_PER_TASK = 32
 SLAB_SPLITS = 16  # csrc/kernels/grad_dense.hip kSplits
 
@@ -51,6 +53,39 @@ def choose_cpl(ld: int, vec: int) -> Optional[int]:
     return None
 
 
+XCDS = 8  # MI355X: workgroups are dealt round-robin over the 8 XCDs (block b -> XCD b % 8)
+
+
+def replica_dispatch_order(keys: Sequence[Tuple[int, int]]) -> List[int]:
+    """Dispatch order of the gradient tasks that co-schedules replicas on one XCD.
+
+    Co-located logical workers of a replicated scheme read identical rows: every member of an
+    FRC/AGC group holds the same partitions, cyclic neighbours share s of their s+1.  In
+    message-major order those reads are hundreds of workgroups apart and each streams the rows
+    from HBM again.  Here the tasks that read the same (partition, row range) — a *bundle* —
+    are placed 8 dispatch slots apart, so (blocks being dealt round-robin over the XCDs) they
+    start together on the same XCD and walk the same rows in step: one HBM read feeds the
+    others from that XCD's L2 / the Infinity Cache.  Every task still runs in full; only the
+    order changes, and slab rows stay message-major, so results are bitwise unchanged.
+
+    keys[i] = (partition, first row) of task i (message-major order).  Returns a permutation.
+    """
+    bundles: Dict[Tuple[int, int], List[int]] = {}
+    for i, k in enumerate(keys):
+        bundles.setdefault(k, []).append(i)
+    by_size: Dict[int, List[List[int]]] = {}
+    for b in bundles.values():  # first-appearance order
+        by_size.setdefault(len(b), []).append(b)
+    order: List[int] = []
+    for size in sorted(by_size, reverse=True):
+        group = by_size[size]
+        for c in range(0, len(group), XCDS):
+            chunk = group[c:c + XCDS]
+            for m in range(size):  # member m of bundle j at offset m * len(chunk) + j
+                order.extend(b[m] for b in chunk)
+    return order
+
+
 def _residual_torch(kind: int, z, y, coef):
     if kind == LOGISTIC:
         return -(coef * y) * torch.sigmoid(-(y * z))
@@ -66,7 +101,9 @@ class DenseGradPlan:
 
     def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]],
                  partitions: Dict[int, Tuple[torch.Tensor, torch.Tensor]], prec: Precision, loss: int, d: int,
-                 target_tasks: int = DEFAULT_TASKS):
+                 target_tasks: Optional[int] = None, interleave: Optional[bool] = None):
+        # replica-interleaved dispatch (see replica_dispatch_order); ERASUREHEAD_NO_INTERLEAVE=1 for A/B runs
+        self.interleave = (not os.environ.get("ERASUREHEAD_NO_INTERLEAVE")) if interleave is None else interleave
         self.prec = prec
         self.loss = loss
         self.d = d
@@ -83,6 +120,14 @@ class DenseGradPlan:
                 raise ValueError(f"partition {p}: y must be [{X.shape[0]}] {prec.acc}")
         self.total_rows = sum(partitions[p][0].shape[0] for m in self.messages for p, _ in m)
         self.cpl = choose_cpl(self.ld, prec.vec)
+        # co-located replicas (a partition in several local messages) read shared rows
+        self.replicated = len({p for m in self.messages for p, _ in m}) < sum(len(m) for m in self.messages)
+        shared = self.replicated and self.interleave
+        if target_tasks is None:  # measured: smaller tasks keep interleaved replicas in step
+            target_tasks = REPLICA_TASKS if shared else DEFAULT_TASKS
+        # grad_dense_fused variant (csrc/kernels/grad_dense.hip fused_rows), measured per case:
+        # fp64 1 row for interleaved replicas (L2-fed), the interleaved pair kernel for distinct rows
+        self.variant = {0: 1 if shared else 2, 1: 4, 2: 1}[prec.code]
         if self.device.type == "cuda":
             self._build_tables(target_tasks)
 
@@ -93,19 +138,23 @@ class DenseGradPlan:
         slot_begin = [0]
         rows_per_task = max(MIN_ROWS_PER_TASK, -(-self.total_rows // max(1, target_tasks)))
         seg_id = 0
+        keys = []  # (partition, first row) of every task: equal keys read identical rows
         for slot, m in enumerate(self.messages):
             for p, coef in m:
                 X, y = self.partitions[p]
                 n = X.shape[0]
                 segs += _SEG.pack(X.data_ptr(), y.data_ptr(), float(coef), n)
                 for r0 in range(0, n, rows_per_task):
-                    tasks.append((slot, seg_id, r0, min(n, r0 + rows_per_task)))
+                    tasks.append((slot, seg_id, r0, min(n, r0 + rows_per_task), len(tasks)))
+                    keys.append((p, r0))
                 seg_id += 1
             slot_begin.append(len(tasks))
+        if self.interleave and self.cpl is not None:
+            tasks = [tasks[i] for i in replica_dispatch_order(keys)]
         dev = self.device
         self.segs = torch.tensor(list(bytes(segs) or b"\0" * 32), dtype=torch.uint8).to(dev)
         self.ntasks = len(tasks)
-        t = np.asarray(tasks, dtype=np.int32).reshape(-1, 4)
+        t = np.asarray(tasks, dtype=np.int32).reshape(-1, 5)
         self.tasks = torch.from_numpy(t).to(dev)
         self.slot_task_begin = torch.tensor(slot_begin, dtype=torch.int32, device=dev)
         self.slab = torch.empty((max(1, self.ntasks), self.ld), dtype=self.prec.acc, device=dev)
@@ -132,7 +181,7 @@ class DenseGradPlan:
             C = native()
             if self.cpl is not None:
                 C.grad_dense(self.prec.code, self.loss, self.cpl, self.segs, self.tasks, beta, self.slab,
-                             self.slot_task_begin, self.part, G, self.ld)
+                             self.slot_task_begin, self.part, G, self.ld, self.variant)
             else:
                 C.grad_dense_twopass(self.prec.code, self.loss, self.segs, self.tasks, beta, self.task_row_off,
                                      self.rbuf, self.slab, self.slot_task_begin, self.part, G, self.ld)
@@ -146,7 +195,7 @@ class DenseGradPlan:
         C = native()
         if self.cpl is not None:
             return C.GradLauncher.dense(self.prec.code, self.loss, self.cpl, self.segs, self.tasks, self.slab,
-                                        self.slot_task_begin, self.part, self.ld)
+                                        self.slot_task_begin, self.part, self.ld, variant=self.variant)
         return C.GradLauncher.dense(self.prec.code, self.loss, 0, self.segs, self.tasks, self.slab,
                                     self.slot_task_begin, self.part, self.ld, self.task_row_off, self.rbuf)
 

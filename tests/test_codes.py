@@ -129,3 +129,27 @@ def test_banners_verbatim():
     assert make_scheme("avoidstragg", 4, 1, 40).banner(0) == "---- Starting AvoidStragg Iterations with 1 stragglers ----"
     assert make_scheme("partial_replication", 4, 1, 40, n_partitions=3).setup_lines() == \
         ["Stragglers are allowed to be atmost 3.00 times slower"]
+
+
+def test_replica_dispatch_order_coschedules_replicas_on_one_xcd():
+    """Tasks that read identical rows are placed 8 dispatch slots apart (same XCD), none is lost."""
+    from erasurehead_amd.ops.grad import XCDS, replica_dispatch_order
+
+    # headline-like layout: 3 replicas of partitions 0..5, 2 replicas of 6..7, 10 row chunks each
+    keys = []
+    groups = [[0, 1, 2]] * 3 + [[3, 4, 5]] * 3 + [[6, 7]] * 2
+    for parts in groups:
+        for p in parts:
+            keys += [(p, r) for r in range(10)]
+    order = replica_dispatch_order(keys)
+    assert sorted(order) == list(range(len(keys)))
+    pos = {t: i for i, t in enumerate(order)}
+    by_key = {}
+    for i, k in enumerate(keys):
+        by_key.setdefault(k, []).append(pos[i])
+    aligned = sum(1 for v in by_key.values() if len({x % XCDS for x in v}) == 1)
+    assert aligned >= 0.9 * len(by_key)  # only the partial last chunk of each size class can break the stride
+    for v in by_key.values():
+        assert max(v) - min(v) <= XCDS * (len(v) - 1)  # replicas start within a few slots of each other
+    # no replicas at all: identity
+    assert replica_dispatch_order([(p, 0) for p in range(5)]) == list(range(5))

@@ -229,3 +229,21 @@ def test_encode_messages(dtype, native):
     ref = E @ Gb.double().cpu().numpy()
     tol = 1e-13 if dtype == torch.float64 else 1e-5
     np.testing.assert_allclose(G.double().cpu().numpy(), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
+def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native):
+    """Replica-interleaved task order + per-case kernel variant: same bits as message-major order."""
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(11)
+    parts, _ = _parts(rng, [3000, 2000, 1000], 1000, prec)
+    msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
+    a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, target_tasks=256, interleave=True)
+    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, target_tasks=256, interleave=False)
+    assert a.replicated and not torch.equal(a.tasks, b.tasks)
+    beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
+    Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
+    a.native_launcher().launch(beta, Ga)
+    b.run(beta, Gb)
+    torch.cuda.synchronize()
+    assert torch.equal(Ga, Gb)

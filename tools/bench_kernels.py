@@ -83,6 +83,20 @@ def scale_cases(out):
         y = torch.where(torch.rand(rpp, device="cuda") > 0.5, 1.0, -1.0).double()
         parts[p] = (X, y)
     beta = torch.randn(prec.ld(d), device="cuda", dtype=torch.float64) * 0.01
+    # FRC-style replicas on one GPU (headline layout: groups {0,1,2} x3, {3,4,5} x3, {6,7} x2): 22 GB of
+    # message rows over 8 GB of distinct partitions; concurrently running replica tasks share L2/MALL lines
+    frc = [[0, 1, 2]] * 3 + [[3, 4, 5]] * 3 + [[6, 7]] * 2
+    for tasks in (2048, 5120):
+        plan = DenseGradPlan([[(p, 1.0) for p in m] for m in frc], {p: parts[p] for p in range(8)}, prec, LOGISTIC,
+                             d, target_tasks=tasks)
+        G = plan.out_buffer()[0]
+        ms = _time(lambda: plan.run(beta, G), reps=20)
+        gb = plan.bytes_per_round / 1e9
+        r = {"kernel": "grad_dense_scale_frc_replicas", "message_gbytes": gb, "distinct_gbytes": 8.0,
+             "tasks": plan.ntasks, "ms": ms, "effective_TBps": gb / ms, "distinct_TBps": 8.0 / ms}
+        out.append(r)
+        print(json.dumps(r), flush=True)
+        del plan
     for nparts in (3, 6, 11, 22):
         msgs = [[(p, 1.0) for p in range(q, min(nparts, q + 3))] for q in range(0, nparts, 3)]
         X0 = parts[0][0]
