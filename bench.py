@@ -115,7 +115,10 @@ def main() -> int:
             },
             "time_to_decode_ms_median": float(1e3 * np.median(ts)),
             "loop_ms_median": float(1e3 * np.median(lt)),
-            "hbm_bytes_per_step_rank0": int(trainer.plan.bytes_per_round) if hasattr(trainer.plan, "bytes_per_round") else None,
+            # X bytes the rank-0 messages read per round (replicas counted each time) and the bytes of
+            # the distinct partitions behind them; co-located replicas share reads through L2
+            "x_message_bytes_per_step_rank0": int(getattr(trainer.plan, "bytes_per_round", 0)) or None,
+            "x_distinct_bytes_rank0": int(getattr(trainer.plan, "distinct_bytes", 0)) or None,
             "setup_s": setup_s,
             "phases_us": {k: round(v["mean_us"], 1) for k, v in res.phases.items()},
         }
@@ -130,9 +133,11 @@ def main() -> int:
             # BASELINE.md publishes no sec/iter, so vs_baseline stays null
             out["ref_cpu_equiv_s_per_iter"] = ref["sec_per_iter_lower_bound"]
             out["speedup_vs_ref_cpu_equiv"] = ref["sec_per_iter_lower_bound"] / sec_per_iter
-        bpr = out["hbm_bytes_per_step_rank0"]
+        bpr = out["x_message_bytes_per_step_rank0"]
         if bpr:
-            out["rank0_grad_stream_GBps_at_step_time"] = bpr / sec_per_iter / 1e9
+            out["rank0_message_rows_GBps"] = bpr / sec_per_iter / 1e9
+        if out["x_distinct_bytes_rank0"]:
+            out["rank0_distinct_rows_GBps"] = out["x_distinct_bytes_rank0"] / sec_per_iter / 1e9
     # convergence: iterations to the training-loss floor (100-round run, evaluated with the MFMA eval kernel)
     trainer.close()
     if not a.no_floor:

@@ -215,9 +215,16 @@ class DenseGradPlan:
 
     @property
     def bytes_per_round(self) -> int:
-        """HBM bytes the fused kernel must stream per round (X once)."""
+        """Bytes of X the messages read per round (every message's rows; replicas counted each time)."""
         es = torch.tensor([], dtype=self.prec.storage).element_size()
         return int(self.total_rows) * self.ld * es
+
+    @property
+    def distinct_bytes(self) -> int:
+        """Bytes of the distinct partitions behind those rows (the HBM floor when replicas share reads)."""
+        es = torch.tensor([], dtype=self.prec.storage).element_size()
+        rows = sum(self.partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
+        return int(rows) * self.ld * es
 
 
 class SparseGradPlan:
@@ -401,6 +408,10 @@ class SharedGradPlan:
     @property
     def bytes_per_round(self) -> int:
         return getattr(self.inner, "bytes_per_round", 0)
+
+    @property
+    def distinct_bytes(self) -> int:
+        return getattr(self.inner, "distinct_bytes", 0)
 
     def run(self, beta: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
         if G.shape != (self.nslots, self.ld):
