@@ -56,7 +56,7 @@ def choose_cpl(ld: int, vec: int) -> Optional[int]:
 XCDS = 8  # MI355X: workgroups are dealt round-robin over the 8 XCDs (block b -> XCD b % 8)
 
 
-def replica_dispatch_order(keys: Sequence[Tuple[int, int]]) -> List[int]:
+def replica_dispatch_order(keys: Sequence[Tuple[int, int]], stride: int = 0) -> List[int]:
     """Dispatch order of the gradient tasks that co-schedules replicas on one XCD.
 
     Co-located logical workers of a replicated scheme read identical rows: every member of an
@@ -69,7 +69,10 @@ def replica_dispatch_order(keys: Sequence[Tuple[int, int]]) -> List[int]:
     order changes, and slab rows stay message-major, so results are bitwise unchanged.
 
     keys[i] = (partition, first row) of task i (message-major order).  Returns a permutation.
+    stride: dispatch distance between bundle members (default XCDS: same XCD; 1: adjacent
+    slots, i.e. different XCDs sharing through the Infinity Cache — A/B runs only).
     """
+    stride = stride or int(os.environ.get("ERASUREHEAD_REPLICA_STRIDE", XCDS))
     bundles: Dict[Tuple[int, int], List[int]] = {}
     for i, k in enumerate(keys):
         bundles.setdefault(k, []).append(i)
@@ -79,8 +82,8 @@ def replica_dispatch_order(keys: Sequence[Tuple[int, int]]) -> List[int]:
     order: List[int] = []
     for size in sorted(by_size, reverse=True):
         group = by_size[size]
-        for c in range(0, len(group), XCDS):
-            chunk = group[c:c + XCDS]
+        for c in range(0, len(group), stride):
+            chunk = group[c:c + stride]
             for m in range(size):  # member m of bundle j at offset m * len(chunk) + j
                 order.extend(b[m] for b in chunk)
     return order
