@@ -21,6 +21,37 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
   return __uint_as_float(static_cast<uint32_t>(b) << 16);
 }
 
+// Loads of data reached through a pointer table (Segment.X / .y) compile to flat_load, and
+// flat loads count in lgkmcnt as well as vmcnt: the LDS / cross-lane waits of a row's wave
+// reduction would then also wait for every row tile still in flight.  Buffer loads count in
+// vmcnt only, and the descriptor's range check returns zeros past the row end (no per-vector
+// bounds branches).  The descriptor base must be wave-uniform (a row, a label array).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+template <typename V>
+__device__ __forceinline__ V buf_load16(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  static_assert(sizeof(V) == 16, "16-byte vector");
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0);
+  V out;
+  __builtin_memcpy(&out, &v, 16);
+  return out;
+}
+template <typename A>
+__device__ __forceinline__ A buf_load_scalar(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  if constexpr (sizeof(A) == 8) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, byte_off, 0, 0);
+    A out;
+    __builtin_memcpy(&out, &v, 8);
+    return out;
+  } else {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b32(rs, byte_off, 0, 0);
+    A out;
+    __builtin_memcpy(&out, &v, 4);
+    return out;
+  }
+}
+
 // Storage-type traits: how many elements fit a 16-byte vector load and how to widen.
 template <typename T> struct Vec16;
 template <> struct Vec16<double> {

@@ -93,18 +93,23 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
 
   int r = task.row_begin + wid;
   // Main loop: ROWS rows per wave per iteration, all loads issued before the first reduction
-  // (ROWS * NV 16-byte loads in flight per lane).
+  // (ROWS * NV 16-byte loads in flight per lane).  A software-pipelined variant (the next
+  // row in flight while this one is reduced) measured no faster: docs/PERF_NOTES.md.
   for (; r + (ROWS - 1) * nw < task.row_end; r += ROWS * nw) {
     if constexpr (BL) asm volatile("" ::: "memory");  // keep the beta reads inside the loop
     // raw 16-byte tiles: every load of the iteration issues before any conversion waits on one
+    // (buffer loads: vmcnt only, zeros past the row end; see common.h make_rsrc)
     typename Vec16<T>::raw xr[ROWS][NV];
+    __amdgpu_buffer_rsrc_t rsq[ROWS];
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q)
+      rsq[q] = make_rsrc(X + static_cast<long long>(r + q * nw) * ld, ld * static_cast<int>(sizeof(T)));
 #pragma unroll
     for (int j = 0; j < NV; ++j)
 #pragma unroll
       for (int q = 0; q < ROWS; ++q) {
         const int c0 = (j * kWave + lane) * VN;
-        if (valid[j]) xr[q][j] = Vec16<T>::load_raw(X + static_cast<long long>(r + q * nw) * ld + c0);
-        else xr[q][j] = typename Vec16<T>::raw{};
+        xr[q][j] = buf_load16<typename Vec16<T>::raw>(rsq[q], c0 * static_cast<int>(sizeof(T)));
       }
     A z[ROWS];
 #pragma unroll

@@ -129,8 +129,9 @@ class DenseGradPlan:
         if target_tasks is None:  # measured: smaller tasks keep interleaved replicas in step
             target_tasks = REPLICA_TASKS if shared else DEFAULT_TASKS
         # grad_dense_fused variant (csrc/kernels/grad_dense.hip fused_rows), measured per case:
-        # fp64 1 row for interleaved replicas (L2-fed), the interleaved pair kernel for distinct rows
-        self.variant = {0: 1 if shared else 2, 1: 4, 2: 1}[prec.code]
+        # one row in flight for interleaved replicas (L2-fed) in every precision; for distinct
+        # rows the interleaved pair kernel (fp64), 4 rows (fp32), 1 row (bf16)
+        self.variant = 1 if shared else {0: 2, 1: 4, 2: 1}[prec.code]
         if self.device.type == "cuda":
             self._build_tables(target_tasks)
 
