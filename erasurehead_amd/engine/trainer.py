@@ -46,7 +46,12 @@ from ..ops.precision import get_precision
 from ..ops.update import combine_update
 from ..parallel.collector import ArrivalCollector
 from ..parallel.dist import DistEnv
-from ..parallel.placement import place_workers, workers_by_rank
+from ..parallel.placement import place_workers_shared, workers_by_rank
+
+# Cost of re-reading a partition row that a co-located replica already streams, relative to a
+# distinct row (dense fp64 on MI355X: (1.84 - 1.29) ms for 14 GB of replica rows against
+# 1.29 ms for 8 GB of distinct rows, docs/PERF_NOTES.md).
+REPLICA_WEIGHT_DENSE = 0.25
 from ..parallel.transport import make_transport
 from ..utils import report
 from ..utils.delay import DelayModel
@@ -78,12 +83,12 @@ class Trainer:
         self.env = env
         self.timer = PhaseTimer()
         self.device_loop: Optional[str] = None  # set by the native master loop when rounds ran device-driven
-        self._setup_scheme(scheme)
+        self._setup_scheme(scheme, source)
         self._setup_data(source)
         self._setup_buffers()
 
     # ------------------------------------------------------------------------------ setup
-    def _setup_scheme(self, scheme: Optional[Scheme]):
+    def _setup_scheme(self, scheme: Optional[Scheme], source: Optional[DataSource] = None):
         cfg, env = self.cfg, self.env
         W = cfg.n_workers
         if W < 1:
@@ -115,12 +120,19 @@ class Trainer:
             mode = cfg.delay_mode if cfg.delay_mode in ("exp", "fixed") else "none"
         self.delay = DelayModel(W, mode, cfg.delay_mean, [w - 1 for w in cfg.fixed_stragglers], cfg.fixed_sleep,
                                 [w - 1 for w in cfg.kill_workers])
-        # placement
+        # placement: sharing-aware on GPUs (co-located replicas share HBM reads)
         rows = scheme.rows_per_partition
-        cost = [0.0] * W
+        parts: List[List[Tuple[int, int]]] = [[] for _ in range(W)]
         for m in scheme.messages:
-            cost[m.worker] += rows * len(m.segments)
-        self.owner = place_workers(cost, env.world)
+            parts[m.worker] += [(p, rows) for p, _ in m.segments]
+        sparse = source.is_sparse if source is not None else bool(cfg.is_real)
+        if cfg.share_partitions:
+            replica_weight = 0.0
+        elif env.gpu and not sparse:
+            replica_weight = REPLICA_WEIGHT_DENSE
+        else:
+            replica_weight = 1.0
+        self.owner = place_workers_shared(parts, env.world, replica_weight)
         self.by_rank = workers_by_rank(self.owner, env.world)
         self.msg_index = {(m.worker, m.part): j for j, m in enumerate(scheme.messages)}
         self.local_msgs = [m for m in scheme.messages if self.owner[m.worker] == env.rank]

@@ -153,3 +153,26 @@ def test_replica_dispatch_order_coschedules_replicas_on_one_xcd():
         assert max(v) - min(v) <= XCDS * (len(v) - 1)  # replicas start within a few slots of each other
     # no replicas at all: identity
     assert replica_dispatch_order([(p, 0) for p in range(5)]) == list(range(5))
+
+
+def test_sharing_aware_placement_keeps_replicas_together():
+    """GPU placement: co-located replicas share HBM reads, so groups stay together when that lowers
+    the slowest rank; with weight 1 (nothing shared) it balances message rows like LPT."""
+    from erasurehead_amd.parallel.placement import place_workers, place_workers_shared, rank_cost, workers_by_rank
+
+    parts = [[(p, 1) for p in ([0, 1, 2] if w < 3 else [3, 4, 5] if w < 6 else [6, 7])] for w in range(8)]
+
+    def slowest(owner, N, wt):
+        by = workers_by_rank(owner, N)
+        return max(rank_cost(by[r], parts, wt) for r in range(N))
+
+    for N in (2, 4, 8):
+        lpt = place_workers([float(len(p)) for p in parts], N)
+        shared = place_workers_shared(parts, N, 0.25)
+        assert slowest(shared, N, 0.25) <= slowest(lpt, N, 0.25)
+        assert all(workers_by_rank(shared, N)[r] for r in range(N))  # no idle GPU
+        assert place_workers_shared(parts, N, 0.25) == shared  # deterministic
+    assert slowest(place_workers_shared(parts, 4, 0.25), 4, 0.25) == 4.5  # vs 6.0 for LPT pairs
+    flat = place_workers_shared(parts, 2, 1.0)
+    assert slowest(flat, 2, 1.0) == 11.0  # 22 message rows over 2 ranks
+    assert place_workers_shared(parts, 1, 0.25) == [0] * 8
