@@ -176,6 +176,65 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
   }
 }
 
+// ----- Replica bundles: one wave per co-located replica, all in one workgroup. -----
+// A workgroup holds R = blockDim/64 task slots (tasks[blockIdx.x * R + q] for wave q); the
+// tasks of a bundle read the SAME rows of the same partition for different messages (FRC group
+// members, cyclic neighbours).  Each wave walks every row of the range for its own message —
+// its own loads, dot product, residual with its own coefficient, gradient accumulation — and
+// writes its own slab row.  Because the replicas of a row are requested by waves of one CU at
+// nearly the same time, the repeated requests hit in that CU's L1 / merge in flight instead of
+// crossing to L2.  Unused slots have seg < 0 (the wave exits; no barrier is used).
+template <typename T, typename A, int CPL, int LOSS>
+__global__ void __launch_bounds__(512)
+grad_dense_bundle(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
+                  const A* __restrict__ beta, A* __restrict__ slab, int ld) {
+  constexpr int VN = Vec16<T>::N;
+  constexpr int NV = CPL / VN;
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6, R = blockDim.x >> 6;
+  const Task task = tasks[blockIdx.x * R + q];
+  if (task.seg < 0) return;
+  const Segment seg = segs[task.seg];
+  const T* __restrict__ X = static_cast<const T*>(seg.X);
+  const A* __restrict__ Y = static_cast<const A*>(seg.y);
+  const A coef = static_cast<A>(seg.coef);
+  A b[NV][VN], g[NV][VN];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * kWave + lane) * VN;
+#pragma unroll
+    for (int v = 0; v < VN; ++v) {
+      b[j][v] = c0 < ld ? beta[c0 + v] : A(0);
+      g[j][v] = A(0);
+    }
+  }
+  for (int r = task.row_begin; r < task.row_end; ++r) {
+    using Rw = typename Vec16<T>::raw;
+    Rw xr[NV];
+    const auto rs = make_rsrc(X + static_cast<long long>(r) * ld, ld * static_cast<int>(sizeof(T)));
+#pragma unroll
+    for (int j = 0; j < NV; ++j) xr[j] = buf_load16<Rw>(rs, (j * kWave + lane) * VN * static_cast<int>(sizeof(T)));
+    A z = A(0);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v) z = fma(Vec16<T>::template elem<A>(xr[j], v), b[j][v], z);
+    z = wave_allreduce_sum(z);
+    const A rr = residual<LOSS, A>(z, Y[r], coef);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v) g[j][v] = fma(rr, Vec16<T>::template elem<A>(xr[j], v), g[j][v]);
+  }
+  A* out = slab + static_cast<long long>(task.slab) * ld;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * kWave + lane) * VN;
+#pragma unroll
+    for (int v = 0; v < VN; ++v)
+      if (c0 + v < ld) out[c0 + v] = g[j][v];
+  }
+}
+
 // Two rows per wave per iteration, loads of both rows interleaved per vector (the layout
 // that measured fastest for bf16 and fp32).
 template <typename T, typename A, int CPL, int LOSS>
@@ -548,9 +607,17 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
   constexpr int VN = Vec16<T>::N;
   // CPL (columns per lane) must be a multiple of the 16-byte vector width VN.
   const int rows = fused_rows<T>(variant);
+  // variant 10 + R (R = 1..8): replica-bundle kernel, R task slots (waves) per workgroup
+  const int bundle_r = variant > 10 && variant <= 18 ? variant - 10 : 0;
+  if (bundle_r && ntasks % bundle_r != 0) return hipErrorInvalidValue;
 #define EH_IF(C)                                                                          \
   case C:                                                                                 \
     if constexpr (C % VN == 0) {                                                          \
+      if (bundle_r) {                                                                     \
+        hipLaunchKernelGGL((grad_dense_bundle<T, A, C, LOSS>), dim3(ntasks / bundle_r),   \
+                           dim3(64 * bundle_r), 0, st, segs, tasks, beta, slab, ld);       \
+        return hipGetLastError();                                                         \
+      }                                                                                   \
       const size_t sh = 4ull * kWave * C * sizeof(A);                                     \
       const size_t shb = sh + kWave * C * sizeof(A);                                      \
       if (rows == 5)                                                                      \

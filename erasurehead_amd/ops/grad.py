@@ -30,6 +30,7 @@ _SEG = struct.Struct("<QQdq")  # csrc Segment {const void* X; const void* y; dou
 MAX_CPL = 32
 DEFAULT_TASKS = 2048
 REPLICA_TASKS = 4096
+MAX_BUNDLE = 8  # replica task slots (waves) per workgroup of grad_dense_bundle
 MIN_ROWS_PER_TASK = 32
 SLAB_SPLITS = 16  # csrc/kernels/grad_dense.hip kSplits
 
@@ -132,6 +133,11 @@ class DenseGradPlan:
         # one row in flight for interleaved replicas (L2-fed) in every precision; for distinct
         # rows the interleaved pair kernel (fp64), 4 rows (fp32), 1 row (bf16)
         self.variant = 1 if shared else {0: 2, 1: 4, 2: 1}[prec.code]
+        # replica bundles (one wave per replica in one workgroup): rows per bundle task, 0 = off
+        self.bundle_rows = int(os.environ.get("ERASUREHEAD_BUNDLE_ROWS", "0")) if (
+            shared and self.cpl is not None and self.cpl <= MAX_CPL) else 0
+        if self.bundle_rows:
+            target_tasks = max(1, -(-self.total_rows // self.bundle_rows))
         if self.device.type == "cuda":
             self._build_tables(target_tasks)
 
@@ -153,7 +159,9 @@ class DenseGradPlan:
                     keys.append((p, r0))
                 seg_id += 1
             slot_begin.append(len(tasks))
-        if self.interleave and self.cpl is not None:
+        if self.bundle_rows:
+            tasks = self._bundle_table(tasks, keys)
+        elif self.interleave and self.cpl is not None:
             tasks = [tasks[i] for i in replica_dispatch_order(keys)]
         dev = self.device
         self.segs = torch.tensor(list(bytes(segs) or b"\0" * 32), dtype=torch.uint8).to(dev)
@@ -171,6 +179,22 @@ class DenseGradPlan:
                 raise ValueError("two-pass plan exceeds int32 row offsets")
             self.task_row_off = torch.from_numpy(off.astype(np.int32)).to(dev)
             self.rbuf = torch.empty(max(1, int(self.total_rows)), dtype=self.prec.acc, device=dev)
+
+    def _bundle_table(self, tasks, keys):
+        """Replica-bundle layout for grad_dense_bundle: R task slots per workgroup, one wave each."""
+        bundles: Dict[Tuple[int, int], List[int]] = {}
+        for i, k in enumerate(keys):
+            bundles.setdefault(k, []).append(i)
+        groups: List[List[int]] = []
+        for b in bundles.values():
+            groups += [b[i:i + MAX_BUNDLE] for i in range(0, len(b), MAX_BUNDLE)]
+        R = max(len(g) for g in groups)
+        pad = (0, -1, 0, 0, 0)
+        table = []
+        for g in groups:
+            table += [tasks[i] for i in g] + [pad] * (R - len(g))
+        self.variant = 10 + R
+        return table
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:
         """Message buffer(s) [n, nslots, ld] in the accumulator dtype."""
