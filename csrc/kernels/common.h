@@ -105,12 +105,51 @@ template <> struct Vec16<bf16_t> {
   }
 };
 
-// Full-wave butterfly sum: every lane ends with the total.
+// Full-wave sum, every lane ends with the bitwise-same total, in VALU cross-lane moves only
+// (no LDS crossbar, no lgkmcnt waits): DPP quad_perm xor 1 and 2, row_half_mirror and
+// row_mirror (pairs the quads and half-rows of each 16-lane row), then gfx950's
+// v_permlane16_swap / v_permlane32_swap (exchange rows 0<->1, 2<->3, then the two halves).
+// Each step adds the partner's value in the same operand order on both partners, so all
+// lanes hold identical bits.  fp64 moves its two dwords separately.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), CTRL, 0xf, 0xf, true));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) { return __uint_as_float(dpp_u32<CTRL>(__float_as_uint(x))); }
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double x) {
+  const unsigned long long u = static_cast<unsigned long long>(__double_as_longlong(x));
+  const uint32_t lo = dpp_u32<CTRL>(static_cast<uint32_t>(u)), hi = dpp_u32<CTRL>(static_cast<uint32_t>(u >> 32));
+  return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+}
+template <bool ROW16>
+__device__ __forceinline__ float swap_sum(float x) {
+  const uint32_t u = __float_as_uint(x);
+  const auto s = ROW16 ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
+                       : __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+template <bool ROW16>
+__device__ __forceinline__ double swap_sum(double x) {
+  const unsigned long long u = static_cast<unsigned long long>(__double_as_longlong(x));
+  const uint32_t l = static_cast<uint32_t>(u), h = static_cast<uint32_t>(u >> 32);
+  const auto lo = ROW16 ? __builtin_amdgcn_permlane16_swap(l, l, false, false)
+                        : __builtin_amdgcn_permlane32_swap(l, l, false, false);
+  const auto hi = ROW16 ? __builtin_amdgcn_permlane16_swap(h, h, false, false)
+                        : __builtin_amdgcn_permlane32_swap(h, h, false, false);
+  const double a = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi[0]) << 32) | lo[0]));
+  const double b = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi[1]) << 32) | lo[1]));
+  return a + b;
+}
 template <typename A>
 __device__ __forceinline__ A wave_allreduce_sum(A v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
-  return v;
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  v = swap_sum<true>(v);   // rows 0<->1, 2<->3
+  return swap_sum<false>(v);  // lanes 0-31 <-> 32-63
 }
 
 // Loss epilogues. r is the per-row coefficient that multiplies x_row in the
