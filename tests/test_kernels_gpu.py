@@ -247,3 +247,38 @@ def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native)
     b.run(beta, Gb)
     torch.cuda.synchronize()
     assert torch.equal(Ga, Gb)
+
+
+def test_eval_gemm_unaligned_rows_use_scalar_staging(native):
+    """Rows whose stride is not a 16-byte multiple take the scalar-staging eval kernel (v1)."""
+    rng = np.random.RandomState(9)
+    n, d, R = 301, 257, 37
+    X = torch.from_numpy(rng.randn(n, d) * 0.2).to(DEV)  # ld = 257 doubles: rows not 16-B aligned
+    y = torch.from_numpy(rng.choice([-1.0, 1.0], n)).to(DEV)
+    B = torch.from_numpy(rng.randn(R, d) * 0.3).to(DEV)
+    s = torch.zeros(R, dtype=torch.float64, device=DEV)
+    P = torch.empty((n, R), dtype=torch.float64, device=DEV)
+    native.eval_gemm_loss(LOGISTIC, X, n, d, y, B, s, P)
+    Ph = X.cpu().numpy() @ B.cpu().numpy().T
+    np.testing.assert_allclose(P.cpu().numpy(), Ph, rtol=1e-11, atol=1e-11)
+    ref = [logistic_loss(y.cpu().numpy(), Ph[:, j], 1) for j in range(R)]
+    np.testing.assert_allclose(s.cpu().numpy(), ref, rtol=1e-10)
+
+
+def test_dense_grad_replica_bundle_kernel(monkeypatch, native):
+    """Opt-in bundle kernel (one wave per replica per workgroup) against the fp64 oracle."""
+    monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", "64")
+    prec = get_precision("fp64")
+    rng = np.random.RandomState(21)
+    parts, host = _parts(rng, [700, 500, 300], 1000, prec)
+    msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
+    plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
+    assert plan.bundle_rows == 64 and plan.variant > 10
+    beta = torch.randn(plan.ld, dtype=torch.float64, device=DEV) * 0.05
+    G = plan.out_buffer()[0]
+    plan.native_launcher().launch(beta, G)
+    torch.cuda.synchronize()
+    bh = beta[:1000].cpu().numpy()
+    for s, m in enumerate(msgs):
+        ref = sum(logistic_grad(host[p][0], host[p][1], bh, c) for p, c in m)
+        np.testing.assert_allclose(G[s, :1000].cpu().numpy(), ref, rtol=1e-10, atol=1e-12)
