@@ -91,3 +91,23 @@ def test_lr_schedules():
     np.testing.assert_allclose(c.eta(), [10.0 * 90.0 / (i + 90.0) for i in range(1, 5)])
     c = RunConfig(3, 10, 2, "/tmp", num_itrs=4, lr=0.1, lr_kind="exponential")  # ref main.py:46
     np.testing.assert_allclose(c.eta(), [0.1 * 0.98 ** i for i in range(1, 5)])
+
+
+def test_extension_flags_parse_and_run(tmp_path, capsys):
+    """--share-partitions / --device-loop reach RunConfig; shared partitions train identically."""
+    from erasurehead_amd.cli import parse
+
+    cfg, _ = parse(["5", "200", "6", "/d/", "0", "artificial", "1", "1", "0", "1", "0", "0", "GD",
+                    "--share-partitions", "--device-loop", "graph"])
+    assert cfg.share_partitions and cfg.device_loop == "graph"
+    cfg, _ = parse(["5", "200", "6", "/d/", "0", "artificial", "1", "1", "0", "1", "0", "0", "GD"])
+    assert not cfg.share_partitions and cfg.device_loop == "auto"
+    root = str(tmp_path) + "/"
+    _data(root)
+    outs = []
+    for extra in ([], ["--share-partitions"]):
+        assert cli_main(["5", "200", "6", root, "0", "artificial", "1", "1", "0", "1", "0", "0", "GD",
+                         "--num-itrs", "4", "--seed", "3", *extra]) == 0
+        outs.append([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("Iteration")])
+    strip = [[ln.split(", Total time")[0] for ln in o] for o in outs]
+    assert strip[0] == strip[1] and len(strip[0]) == 4
