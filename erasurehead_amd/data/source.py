@@ -79,13 +79,13 @@ class FileSource(DataSource):
         for p in parts:
             X = dio.load_partition(self.data_dir, p, self.is_real)
             n = X.shape[0]
-            yy = torch.as_tensor(np.asarray(y[off:off + n]), dtype=torch.float64, device=device)
+            yy = torch.tensor(np.asarray(y[off:off + n]), dtype=torch.float64, device=device)
             off += n
             yield (X if self.is_sparse else _pad_dense(X, prec, device)), yy
 
     def test(self, prec, device):
         X = dio.load_test(self.data_dir, self.is_real)
-        y = torch.as_tensor(np.asarray(dio.load_labels(self.data_dir, test=True)), dtype=torch.float64, device=device)
+        y = torch.tensor(np.asarray(dio.load_labels(self.data_dir, test=True)), dtype=torch.float64, device=device)
         return (X if self.is_sparse else _pad_dense(X, prec, device)), y
 
 
