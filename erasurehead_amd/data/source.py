@@ -71,7 +71,7 @@ class FileSource(DataSource):
             raise ValueError(f"partition {p + 1}: {X.shape[0]} rows but {len(y)} labels; check n_rows")
         if self.is_sparse:
             return X, np.asarray(y, dtype=np.float64)
-        return _pad_dense(X, prec, device), torch.as_tensor(np.asarray(y), dtype=prec.acc, device=device)
+        return _pad_dense(X, prec, device), torch.tensor(np.asarray(y), dtype=prec.acc, device=device)
 
     def train_eval_chunks(self, parts, prec, device):
         y = self.labels()
@@ -126,7 +126,7 @@ class ArraySource(DataSource):
         X, y = self.parts[p]
         if self.is_sparse:
             return X, np.asarray(y, dtype=np.float64)
-        return _pad_dense(X, prec, device), torch.as_tensor(np.asarray(y), dtype=prec.acc, device=device)
+        return _pad_dense(X, prec, device), torch.tensor(np.asarray(y), dtype=prec.acc, device=device)
 
     def train_eval_chunks(self, parts, prec, device):
         ys = np.concatenate([np.asarray(y) for _, y in self.parts])
