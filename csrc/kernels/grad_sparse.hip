@@ -77,8 +77,11 @@ template <typename A, int LOSS, bool VALS>
 __global__ void __launch_bounds__(256)
 ell_rowpass(const int* __restrict__ idx, const A* __restrict__ vals, const A* __restrict__ y,
             const A* __restrict__ coef, const A* __restrict__ beta, A* __restrict__ rbuf,
-            long long nrows, int m) {
+            long long nrows, int m, A* __restrict__ G, long long gsize) {
   const long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  // the column pass accumulates into G: zero it here (stream order) instead of a memset launch
+  const long long nthreads = static_cast<long long>(gridDim.x) * blockDim.x;
+  for (long long i = row; i < gsize; i += nthreads) G[i] = A(0);
   if (row >= nrows) return;
   // four independent gather chains per thread: enough loads in flight to stream idx at HBM rate
   A z[4] = {A(0), A(0), A(0), A(0)};
@@ -180,8 +183,7 @@ hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals
                            const void* chunks, int nchunks, const int* lo, const int* width,
                            int max_width, void* G, long long gsize, int ld, hipStream_t st) {
   const size_t esz = dtype == 0 ? sizeof(double) : sizeof(float);
-  hipError_t e = hipMemsetAsync(G, 0, gsize * esz, st);
-  if (e != hipSuccess || nrows == 0 || m == 0) return e;
+  if (nrows == 0 || m == 0) return hipMemsetAsync(G, 0, gsize * esz, st);
   constexpr int kLdsBytes = 64 * 1024;
   const int cap = static_cast<int>(kLdsBytes / esz);
   const size_t sh = static_cast<size_t>(std::max(std::min(max_width, cap), 4 * kSmallW)) * esz;
@@ -190,10 +192,10 @@ hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals
 #define EH_ELL(A, VALS)                                                                                  \
   if (loss == kLogistic)                                                                                 \
     hipLaunchKernelGGL((ell_rowpass<A, kLogistic, VALS>), grid1, block, 0, st, idx, (const A*)vals,      \
-                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m);                 \
+                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m, (A*)G, gsize);   \
   else                                                                                                   \
     hipLaunchKernelGGL((ell_rowpass<A, kLeastSquares, VALS>), grid1, block, 0, st, idx, (const A*)vals,  \
-                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m);                 \
+                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m, (A*)G, gsize);   \
   hipLaunchKernelGGL((ell_colpass<A, VALS>), grid2, block, sh, st, idx, (const A*)vals, (const A*)rbuf, C, \
                      lo, width, (A*)G, nrows, ld, cap);
   if (dtype == 0) {
