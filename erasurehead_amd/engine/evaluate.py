@@ -38,6 +38,22 @@ def eval_partitions(trainer: Trainer):
     return list(range(max(1, W - 1)))
 
 
+def _train_chunks(trainer: Trainer, parts, prec, dev):
+    """Training partitions for the evaluation, in order.
+
+    Dense partitions this rank already holds in HBM (all of them on one GPU) are evaluated in
+    place instead of being re-read from disk or regenerated.  The reference reloads every file
+    (ref src/naive.py:161-172).  Its labels are the prefix of label.dat, which for partitions
+    taken in order 0..k is exactly each partition's own labels.
+    """
+    resident = getattr(trainer, "_parts", None) or {}
+    if trainer.source.is_sparse or not all(p in resident for p in parts) or list(parts) != sorted(parts):
+        yield from trainer.source.train_eval_chunks(parts, prec, dev)
+        return
+    for p in parts:
+        yield resident[p]
+
+
 def evaluate(trainer: Trainer, res: TrainResult, log=None, write: bool = True) -> EvalResult:
     log = log or report.log
     cfg = trainer.cfg
@@ -54,7 +70,7 @@ def evaluate(trainer: Trainer, res: TrainResult, log=None, write: bool = True) -
         if trainer.scheme.logs_eval_loading and not trainer.source.is_sparse:
             for p in parts:
                 log(">> Loaded %d" % (p + 1))
-    sums, n_train = loss_sums(trainer.source.train_eval_chunks(parts, prec, dev), B, d, kind)
+    sums, n_train = loss_sums(_train_chunks(trainer, parts, prec, dev), B, d, kind)
     Xt, yt = trainer.source.test(prec, dev)
     P, tsum = predictions_and_loss(Xt, yt, B, d, kind)
     n_test = Xt.shape[0]
