@@ -35,6 +35,9 @@ __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
     if (prev == gridDim.x - 1) {
       __hip_atomic_store(p.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __threadfence_system();
+      // ROCm 7.2 / gfx950: after a returned atomic the compiler may drop the wait that follows
+      // the fence's write-back, letting the flag overtake it; keep the wait explicitly.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(p.flag, p.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
@@ -43,6 +46,7 @@ __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
 // Signal only (no payload): flag = value once all prior work on the stream is done.
 __global__ void signal_only(unsigned long long* flag, unsigned long long value) {
   __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
