@@ -100,3 +100,29 @@ def test_cli_two_ranks_synthetic(tmp_path):
     losses = [float(l.split("Train Loss = ")[1].split(",")[0]) for l in its]
     assert losses[-1] < losses[0]
     assert os.path.exists(os.path.join(root, "results", "replication_acc_2_training_loss.dat"))
+
+
+def _gpu_count():
+    import torch
+
+    return torch.cuda.device_count()
+
+
+@pytest.mark.parametrize("transport", ["ipc", "rccl"])
+@pytest.mark.parametrize("case_i", [4, 1])
+def test_one_rank_per_gpu_matches_replay(transport, case_i, tmp_path, monkeypatch):
+    """SURVEY §4 layer 5: one rank per MI355X (2-4 GPUs), IPC over xGMI and RCCL p2p, against the
+    fp64 oracle.  Skipped on one-GPU boxes (there RCCL cannot run two ranks on one device)."""
+    from oracle import replay
+    from test_engine_cpu import CASES, make
+
+    n = _gpu_count()
+    if n < 2:
+        pytest.skip("needs >= 2 GPUs")
+    monkeypatch.setenv("ERASUREHEAD_TRANSPORT", transport)
+    r = _launch(min(4, n), case_i, "AGD", str(tmp_path / "g.npz"))
+    assert str(r["transport"]) == transport
+    cfg, src, sch, parts = make(CASES[case_i], "AGD")
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
