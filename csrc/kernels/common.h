@@ -152,6 +152,37 @@ __device__ __forceinline__ A wave_allreduce_sum(A v) {
   return swap_sum<false>(v);  // lanes 0-31 <-> 32-63
 }
 
+// Two-row reduce-scatter: lanes 0-31 end with the full sum of z0, lanes 32-63 with that of z1
+// (one permlane32 exchange, then the within-half steps of wave_allreduce_sum).
+__device__ __forceinline__ uint32_t partner32(uint32_t u, bool hi) {
+  const auto s = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return hi ? s[0] : s[1];  // lanes 0-31: s = {self, partner}; lanes 32-63: {partner, self}
+}
+__device__ __forceinline__ float partner32(float x, bool hi) { return __uint_as_float(partner32(__float_as_uint(x), hi)); }
+__device__ __forceinline__ double partner32(double x, bool hi) {
+  const unsigned long long u = static_cast<unsigned long long>(__double_as_longlong(x));
+  const uint32_t l = partner32(static_cast<uint32_t>(u), hi), h = partner32(static_cast<uint32_t>(u >> 32), hi);
+  return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(h) << 32) | l));
+}
+template <typename A>
+__device__ __forceinline__ A wave_pair_reduce(A z0, A z1, bool hi) {
+  A v = (hi ? z1 : z0) + partner32(hi ? z0 : z1, hi);
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0x141>(v);
+  v += dpp_mov<0x140>(v);
+  return swap_sum<true>(v);
+}
+__device__ __forceinline__ float readlane_a(float x, int l) {
+  return __uint_as_float(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(__float_as_uint(x)), l)));
+}
+__device__ __forceinline__ double readlane_a(double x, int l) {
+  const unsigned long long u = static_cast<unsigned long long>(__double_as_longlong(x));
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(u)), l));
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(u >> 32)), l));
+  return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+}
+
 // Loss epilogues. r is the per-row coefficient that multiplies x_row in the
 // gradient:  g = sum_rows r * x_row.
 //   logistic (ref naive.py:137-139):  g = -X^T( ymod / (exp(y*z) + 1) )  ->  r = -ymod * sigmoid(-y z)
@@ -166,6 +197,19 @@ __device__ __forceinline__ A sigmoid_neg(A t) {
     return e / (A(1) + e);
   }
   return A(1) / (A(1) + exp(t));
+}
+
+// Branch-free form for waves whose lanes hold different rows (one exp either way).
+template <int LOSS, typename A>
+__device__ __forceinline__ A residual_branchfree(A z, A y, A coef) {
+  if constexpr (LOSS == kLogistic) {
+    const A t = y * z;
+    const A e = exp(-fabs(t));
+    const A q = A(1) / (A(1) + e);
+    return -(coef * y) * (t > A(0) ? e * q : q);
+  } else {
+    return A(-2) * coef * (y - z);
+  }
 }
 
 template <int LOSS, typename A>

@@ -21,6 +21,7 @@
 // The "task" table lets one launch serve every logical worker hosted on this GPU
 // (e.g. all 8 FRC/AGC workers at N=1): task -> (output message slot, segment,
 // row range); segment -> (partition base pointer, labels, encoding coefficient).
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -233,6 +234,237 @@ grad_dense_bundle(const Segment* __restrict__ segs, const Task* __restrict__ tas
     for (int v = 0; v < VN; ++v)
       if (c0 + v < ld) out[c0 + v] = g[j][v];
   }
+}
+
+// ----- Replica bundles staged through LDS: one HBM read per row, one wave per replica. -----
+// Same task table as grad_dense_bundle (R slots per workgroup, all reading the same rows of one
+// partition).  The workgroup streams its row range through an NS-stage LDS ring with
+// global_load_lds (16-byte LDS-DMA, no staging registers): NS-1 stages are in flight while every
+// replica wave computes the oldest one from LDS — its own dot product against beta, residual with
+// its own coefficient, and gradient accumulation — and writes its own slab row.  The rows of a
+// stage are contiguous in HBM, so a stage is one flat copy split into 1 KiB wave pieces (lane-
+// linear LDS image).  Labels ride along as one 4-byte-per-lane LDS-DMA piece.
+// The LDS-DMA loads are issued by inline asm: through the builtin, hipcc cannot tell the stage
+// being filled from the one being read and waits vmcnt(0) before every ds_read, which drains the
+// prefetch (checked in the .s).  The kernel counts and waits for its own loads instead: "stage t
+// landed" is vmcnt <= the loads this wave issued for the stages after t.
+__device__ __forceinline__ void glds16(const void* g, unsigned lds, bool nt = false) {
+  int keep;
+  if (nt)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* g, unsigned lds) {
+  int keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant; n > 63 waits
+// for 63, which is stricter and therefore safe).
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+#define EH_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); return;
+#define EH_W8(k) EH_W(k) EH_W(k + 1) EH_W(k + 2) EH_W(k + 3) EH_W(k + 4) EH_W(k + 5) EH_W(k + 6) EH_W(k + 7)
+    EH_W8(0) EH_W8(8) EH_W8(16) EH_W8(24) EH_W8(32) EH_W8(40) EH_W8(48) EH_W8(56)
+#undef EH_W8
+#undef EH_W
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+  }
+}
+
+template <typename T, typename A, int CPL, int LOSS, bool PAIR>
+__global__ void __launch_bounds__(512)
+grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
+                  const A* __restrict__ beta, A* __restrict__ slab, int ld, int srows, int pieces, int nstage,
+                  int nload, int flags) {
+  constexpr int VN = Vec16<T>::N;
+  constexpr int NV = CPL / VN;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int lane = threadIdx.x & 63, R = blockDim.x >> 6;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const unsigned lds_base = static_cast<unsigned>(
+      reinterpret_cast<size_t>((__attribute__((address_space(3))) unsigned char*)smem_raw));
+  const Task lead = tasks[blockIdx.x * R];  // slot 0 of a bundle is always a real task
+  const Task task = tasks[blockIdx.x * R + q];
+  const bool active = task.seg >= 0;
+  const Segment ls = segs[lead.seg];
+  const unsigned char* __restrict__ X = static_cast<const unsigned char*>(ls.X);
+  const unsigned char* __restrict__ Y = static_cast<const unsigned char*>(ls.y);
+  const A coef = active ? static_cast<A>(segs[task.seg].coef) : A(0);
+  const int rowbytes = ld * static_cast<int>(sizeof(T));
+  const int data_bytes = (nload > 0 ? nload : R) * pieces * 1024;  // one stage: data, then 256 B of labels
+  const int buf_bytes = data_bytes + 256;
+  const int nrows = lead.row_end - lead.row_begin;
+  const int nst = (nrows + srows - 1) / srows;
+
+  // LDS-DMA loads wave q issues for stage t: its 1 KiB pieces of the stage's bytes (+ labels: wave 0)
+  // issuing waves: all R, or the last nload (dedicated loader slots, seg < 0)
+  const int LR = nload > 0 ? nload : R;
+  const int lq = nload > 0 ? q - (R - nload) : q;
+  const bool nt = flags & 1;  // non-temporal loads (rows are read once)
+  auto count = [&](int t) {
+    if (lq < 0) return 0;
+    const int nb = (min(srows, nrows - t * srows) * rowbytes + 1023) >> 10;
+    return (nb > lq ? (nb - lq + LR - 1) / LR : 0) + (lq == 0 ? 1 : 0);
+  };
+  auto issue = [&](int t) {
+    if (lq < 0) return;
+    const unsigned dst = lds_base + (t % nstage) * buf_bytes;
+    const long long r0 = lead.row_begin + static_cast<long long>(t) * srows;
+    const int ns = min(srows, static_cast<int>(lead.row_end - r0));
+    const int bytes = ns * rowbytes;
+    const unsigned char* src = X + r0 * rowbytes;
+    for (int blk = lq; blk * 1024 < bytes; blk += LR)
+      glds16(src + min(blk * 1024 + lane * 16, bytes - 16), dst + blk * 1024, nt);
+    if (lq == 0) {
+      const int lb = ns * static_cast<int>(sizeof(A));
+      glds4(Y + r0 * sizeof(A) + min(lane * 4, lb - 4), dst + data_bytes);
+    }
+  };
+
+  A b[NV][VN], g[NV][VN];
+  bool valid[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * kWave + lane) * VN;
+    valid[j] = c0 < ld;
+#pragma unroll
+    for (int v = 0; v < VN; ++v) {
+      b[j][v] = valid[j] ? beta[c0 + v] : A(0);
+      g[j][v] = A(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // beta in registers before the counted loads
+  using Rw = typename Vec16<T>::raw;
+  for (int t = 0; t < nstage - 1 && t < nst; ++t) issue(t);
+  for (int t = 0; t < nst; ++t) {
+    int later = 0;  // loads this wave issued after stage t
+    for (int u = t + 1; u <= min(t + nstage - 2, nst - 1); ++u) later += count(u);
+    wait_vmcnt(later);  // this wave's pieces of stage t landed
+    __syncthreads();    // every wave's pieces of stage t; stage t-1 consumed by every wave
+    if (t + nstage - 1 < nst) issue(t + nstage - 1);  // into the buffer stage t-1 used
+    if (!active) continue;
+    const unsigned char* buf = smem_raw + (t % nstage) * buf_bytes;
+    const A* lab = reinterpret_cast<const A*>(buf + data_bytes);
+    const int ns = min(srows, nrows - t * srows);
+    if constexpr (PAIR) {
+      // Two rows per step with ONE reduction and ONE residual evaluation between them: the two
+      // partial dot products are reduce-scattered (lanes 0-31 finish row i, lanes 32-63 row i+1),
+      // each lane evaluates the loss epilogue of its half's row (one exp for two rows), and the
+      // two residuals are broadcast by readlane.  The rows are re-read from LDS for the update
+      // rather than held in registers across the reduction.  A lone last row is paired with
+      // itself and weighted 0.
+      const bool hi = lane >= 32;
+      for (int i = 0; i < ns; i += 2) {
+        const bool two = i + 1 < ns;
+        const unsigned char* row0 = buf + i * rowbytes;
+        const unsigned char* row1 = two ? row0 + rowbytes : row0;
+        A z0 = A(0), z1 = A(0);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
+          const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
+          const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
+#pragma unroll
+          for (int v = 0; v < VN; ++v) {
+            z0 = fma(valid[j] ? Vec16<T>::template elem<A>(v0, v) : A(0), b[j][v], z0);
+            z1 = fma(valid[j] ? Vec16<T>::template elem<A>(v1, v) : A(0), b[j][v], z1);
+          }
+        }
+        const A zs = wave_pair_reduce(z0, z1, hi);
+        const A rr = residual_branchfree<LOSS, A>(zs, lab[two && hi ? i + 1 : i], coef);
+        const A r0 = readlane_a(rr, 0);
+        const A r1 = two ? readlane_a(rr, 32) : A(0);
+        asm volatile("" ::: "memory");  // re-read the rows from LDS below
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
+          const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
+          const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
+#pragma unroll
+          for (int v = 0; v < VN; ++v) {
+            const A e0 = valid[j] ? Vec16<T>::template elem<A>(v0, v) : A(0);
+            const A e1 = valid[j] ? Vec16<T>::template elem<A>(v1, v) : A(0);
+            g[j][v] = fma(r1, e1, fma(r0, e0, g[j][v]));
+          }
+        }
+      }
+    } else {
+      // one row at a time
+      for (int i = 0; i < ns; ++i) {
+        const unsigned char* row = buf + i * rowbytes;
+        Rw xr[NV];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {  // clamped read, masked to zero past the row end
+          const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
+          const Rw v = *reinterpret_cast<const Rw*>(row + c0);
+          xr[j] = valid[j] ? v : Rw{};
+        }
+        A z = A(0);  // one accumulator: four independent chains measured no faster
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+#pragma unroll
+          for (int v = 0; v < VN; ++v) z = fma(Vec16<T>::template elem<A>(xr[j], v), b[j][v], z);
+        const A rr = residual<LOSS, A>(wave_allreduce_sum(z), lab[i], coef);
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+#pragma unroll
+          for (int v = 0; v < VN; ++v) g[j][v] = fma(rr, Vec16<T>::template elem<A>(xr[j], v), g[j][v]);
+      }
+    }
+  }
+  if (!active) return;
+  A* out = slab + static_cast<long long>(task.slab) * ld;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * kWave + lane) * VN;
+#pragma unroll
+    for (int v = 0; v < VN; ++v)
+      if (c0 + v < ld) out[c0 + v] = g[j][v];
+  }
+}
+
+// Stage geometry of grad_dense_staged: rows per stage, 1 KiB pieces per wave and ring depth.
+// Defaults measured at the headline (tools/sweep_staged.sh); ERASUREHEAD_STAGE_ROWS and
+// ERASUREHEAD_STAGES override them for sweeps.  Rows shrink until the ring fits kStagedLds.
+constexpr int kStagedLds = 160 * 1024;
+struct StagedGeom {
+  int srows, pieces, nstage;
+  size_t lds;
+  int nload, flags;
+};
+static inline int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+static inline bool staged_geometry(int R, int rowbytes, StagedGeom* g) {
+  // dedicated loader waves (the last slots of every bundle; DenseGradPlan pads the table for them)
+  static const int nload = env_int("ERASUREHEAD_STAGED_LOADERS", 0);
+  static const int flags = env_int("ERASUREHEAD_STAGED_NT", 0) ? 1 : 0;
+  if (nload >= R) return false;
+  const int LR = nload > 0 ? nload : R;
+  static const int env_rows = [] {
+    const char* e = std::getenv("ERASUREHEAD_STAGE_ROWS");
+    return e ? std::atoi(e) : 0;
+  }();
+  static const int env_stages = [] {
+    const char* e = std::getenv("ERASUREHEAD_STAGES");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int ns = env_stages >= 2 && env_stages <= 8 ? env_stages : 2;
+  int s = env_rows > 0 ? std::min(env_rows, 32) : 2;
+  for (; s >= 1; --s) {
+    const int p = (s * rowbytes + LR * 1024 - 1) / (LR * 1024);
+    const size_t bytes = static_cast<size_t>(ns) * (static_cast<size_t>(LR) * p * 1024 + 256);
+    if (bytes <= kStagedLds) {
+      *g = StagedGeom{s, p, ns, bytes, nload, flags};
+      return true;
+    }
+  }
+  return false;
 }
 
 // Two rows per wave per iteration, loads of both rows interleaved per vector (the layout
@@ -608,11 +840,30 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
   // CPL (columns per lane) must be a multiple of the 16-byte vector width VN.
   const int rows = fused_rows<T>(variant);
   // variant 10 + R (R = 1..8): replica-bundle kernel, R task slots (waves) per workgroup
-  const int bundle_r = variant > 10 && variant <= 18 ? variant - 10 : 0;
+  // variant 20 + R / 30 + R: the same bundle table, rows staged through LDS (grad_dense_staged,
+  // one row per wave step / two rows sharing one reduction and residual evaluation)
+  const bool staged_pair = variant > 30 && variant <= 38;
+  const int staged_r = variant > 20 && variant <= 28 ? variant - 20 : staged_pair ? variant - 30 : 0;
+  const int bundle_r = variant > 10 && variant <= 18 ? variant - 10 : staged_r;
   if (bundle_r && ntasks % bundle_r != 0) return hipErrorInvalidValue;
+  StagedGeom sg{};
+  if (staged_r && !staged_geometry(staged_r, ld * static_cast<int>(sizeof(T)), &sg)) return hipErrorInvalidValue;
 #define EH_IF(C)                                                                          \
   case C:                                                                                 \
     if constexpr (C % VN == 0) {                                                          \
+      if (staged_r) {                                                                     \
+        auto kern = staged_pair ? grad_dense_staged<T, A, C, LOSS, true>                  \
+                                : grad_dense_staged<T, A, C, LOSS, false>;                \
+        if (sg.lds > 65536) {                                                             \
+          const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),   \
+              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sg.lds));      \
+          if (ea != hipSuccess) return ea;                                                \
+        }                                                                                 \
+        hipLaunchKernelGGL(kern, dim3(ntasks / staged_r), dim3(64 * staged_r), sg.lds, st, \
+                           segs, tasks, beta, slab, ld, sg.srows, sg.pieces, sg.nstage,   \
+                           sg.nload, sg.flags);                                           \
+        return hipGetLastError();                                                         \
+      }                                                                                   \
       if (bundle_r) {                                                                     \
         hipLaunchKernelGGL((grad_dense_bundle<T, A, C, LOSS>), dim3(ntasks / bundle_r),   \
                            dim3(64 * bundle_r), 0, st, segs, tasks, beta, slab, ld);       \

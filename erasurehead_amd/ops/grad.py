@@ -30,7 +30,8 @@ _SEG = struct.Struct("<QQdq")  # csrc Segment {const void* X; const void* y; dou
 MAX_CPL = 32
 DEFAULT_TASKS = 2048
 REPLICA_TASKS = 4096
-MAX_BUNDLE = 8  # replica task slots (waves) per workgroup of grad_dense_bundle
+MAX_BUNDLE = 8  # replica task slots (waves) per workgroup of grad_dense_bundle / _staged
+STAGED_ROWS = 512  # rows per bundle task of grad_dense_staged (measured: 512 > 256, 1024; 2048 leaves CUs idle)
 MIN_ROWS_PER_TASK = 32
 SLAB_SPLITS = 16  # csrc/kernels/grad_dense.hip kSplits
 
@@ -133,8 +134,19 @@ class DenseGradPlan:
         # one row in flight for interleaved replicas (L2-fed) in every precision; for distinct
         # rows the interleaved pair kernel (fp64), 4 rows (fp32), 1 row (bf16)
         self.variant = 1 if shared else {0: 2, 1: 4, 2: 1}[prec.code]
-        # replica bundles (one wave per replica in one workgroup): rows per bundle task, 0 = off
-        self.bundle_rows = int(os.environ.get("ERASUREHEAD_BUNDLE_ROWS", "0")) if (
+        # Replica bundles: the tasks that read the same rows run in one workgroup, one wave per
+        # replica.  Default for fp64/fp32 replicas: grad_dense_staged streams each bundle's rows
+        # from HBM once through LDS and every replica wave computes its own message from there
+        # (measured 1.58 vs 1.80 ms fp64, 0.89 vs 0.99 ms fp32 at the headline; bf16 rows are
+        # too short to pay for the staging: 0.70 vs 0.66 ms, docs/PERF_NOTES.md).
+        # ERASUREHEAD_STAGED=0 / 1 / pair overrides (pair: two rows share one reduction and one
+        # residual evaluation — measured slower, kept for sweeps).
+        staged_env = os.environ.get("ERASUREHEAD_STAGED", "")
+        staged_ok = shared and self.cpl is not None and self.cpl <= MAX_CPL
+        self.staged = staged_ok and (staged_env in ("1", "pair") or (staged_env == "" and prec.code in (0, 1)))
+        self.staged_pair = self.staged and staged_env == "pair"
+        default_rows = str(STAGED_ROWS) if self.staged else "0"
+        self.bundle_rows = int(os.environ.get("ERASUREHEAD_BUNDLE_ROWS", default_rows)) if (
             shared and self.cpl is not None and self.cpl <= MAX_CPL) else 0
         if self.bundle_rows:
             target_tasks = max(1, -(-self.total_rows // self.bundle_rows))
@@ -188,12 +200,13 @@ class DenseGradPlan:
         groups: List[List[int]] = []
         for b in bundles.values():
             groups += [b[i:i + MAX_BUNDLE] for i in range(0, len(b), MAX_BUNDLE)]
-        R = max(len(g) for g in groups)
+        # + dedicated loader slots of grad_dense_staged (ERASUREHEAD_STAGED_LOADERS, sweeps only)
+        R = max(len(g) for g in groups) + (int(os.environ.get("ERASUREHEAD_STAGED_LOADERS", "0")) if self.staged else 0)
         pad = (0, -1, 0, 0, 0)
         table = []
         for g in groups:
             table += [tasks[i] for i in g] + [pad] * (R - len(g))
-        self.variant = 10 + R
+        self.variant = (30 if self.staged_pair else 20 if self.staged else 10) + R
         return table
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:

@@ -232,8 +232,9 @@ def test_encode_messages(dtype, native):
 
 
 @pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
-def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native):
+def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native, monkeypatch):
     """Replica-interleaved task order + per-case kernel variant: same bits as message-major order."""
+    monkeypatch.setenv("ERASUREHEAD_STAGED", "0")  # the interleaved dispatch, not the LDS-staged bundles
     prec = get_precision(prec_name)
     rng = np.random.RandomState(11)
     parts, _ = _parts(rng, [3000, 2000, 1000], 1000, prec)
@@ -247,6 +248,30 @@ def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native)
     b.run(beta, Gb)
     torch.cuda.synchronize()
     assert torch.equal(Ga, Gb)
+
+
+@pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
+def test_dense_grad_staged_is_the_replica_default(prec_name, native, monkeypatch):
+    """Co-located replicas default to the LDS-staged bundles for fp64/fp32 (interleaved dispatch
+    for bf16), and the staged messages match message-major order to rounding."""
+    monkeypatch.delenv("ERASUREHEAD_STAGED", raising=False)
+    monkeypatch.delenv("ERASUREHEAD_BUNDLE_ROWS", raising=False)
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(12)
+    parts, _ = _parts(rng, [3000, 2000, 1000], 1000, prec)
+    msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
+    a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
+    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, interleave=False)
+    assert a.staged == (prec_name != "bf16") and not b.staged
+    if a.staged:
+        assert 20 < a.variant <= 28 and a.bundle_rows == 512
+    beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
+    Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
+    a.native_launcher().launch(beta, Ga)
+    b.run(beta, Gb)
+    torch.cuda.synchronize()
+    tol = 1e-12 if prec_name == "fp64" else 1e-4
+    torch.testing.assert_close(Ga, Gb, rtol=tol, atol=tol)
 
 
 def test_eval_gemm_unaligned_rows_use_scalar_staging(native):
@@ -265,20 +290,30 @@ def test_eval_gemm_unaligned_rows_use_scalar_staging(native):
     np.testing.assert_allclose(s.cpu().numpy(), ref, rtol=1e-10)
 
 
-def test_dense_grad_replica_bundle_kernel(monkeypatch, native):
-    """Opt-in bundle kernel (one wave per replica per workgroup) against the fp64 oracle."""
-    monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", "64")
-    prec = get_precision("fp64")
+@pytest.mark.parametrize("pair", [False, True])
+@pytest.mark.parametrize("staged,rows,d,prec_name", [(False, "64", 1000, "fp64"), (True, "64", 1000, "fp64"),
+                                                     (True, "37", 1000, "fp64"), (True, "100", 250, "fp64"),
+                                                     (True, "64", 1000, "fp32"), (True, "64", 1000, "bf16")])
+def test_dense_grad_replica_bundle_kernel(monkeypatch, native, staged, rows, d, prec_name, pair):
+    """Opt-in bundle kernels (one wave per replica per workgroup; rows loaded per wave, or staged
+    once through LDS by LDS-DMA) against the fp64 oracle.  Row counts that leave partial stages
+    and partial bundles are included."""
+    monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", rows)
+    if pair and not staged:
+        pytest.skip("pair applies to the staged kernel")
+    monkeypatch.setenv("ERASUREHEAD_STAGED", ("pair" if pair else "1") if staged else "0")
+    prec = get_precision(prec_name)
     rng = np.random.RandomState(21)
-    parts, host = _parts(rng, [700, 500, 300], 1000, prec)
+    parts, host = _parts(rng, [700, 500, 301], d, prec)
     msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
-    plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
-    assert plan.bundle_rows == 64 and plan.variant > 10
-    beta = torch.randn(plan.ld, dtype=torch.float64, device=DEV) * 0.05
+    plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, d)
+    assert plan.bundle_rows == int(rows) and plan.variant > (30 if pair else 20 if staged else 10)
+    beta = torch.randn(plan.ld, dtype=prec.acc, device=DEV) * 0.05
     G = plan.out_buffer()[0]
     plan.native_launcher().launch(beta, G)
     torch.cuda.synchronize()
-    bh = beta[:1000].cpu().numpy()
+    bh = beta[:d].double().cpu().numpy()
+    tol = 1e-10 if prec_name == "fp64" else 2e-4
     for s, m in enumerate(msgs):
         ref = sum(logistic_grad(host[p][0], host[p][1], bh, c) for p, c in m)
-        np.testing.assert_allclose(G[s, :1000].cpu().numpy(), ref, rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=tol * 1e-2)
