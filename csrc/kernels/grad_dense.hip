@@ -248,14 +248,10 @@ grad_dense_bundle(const Segment* __restrict__ segs, const Task* __restrict__ tas
 // being filled from the one being read and waits vmcnt(0) before every ds_read, which drains the
 // prefetch (checked in the .s).  The kernel counts and waits for its own loads instead: "stage t
 // landed" is vmcnt <= the loads this wave issued for the stages after t.
-__device__ __forceinline__ void glds16(const void* g, unsigned lds, bool nt = false) {
+__device__ __forceinline__ void glds16(const void* g, unsigned lds) {
   int keep;
-  if (nt)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-  else
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
 }
 __device__ __forceinline__ void glds4(const void* g, unsigned lds) {
   int keep;
@@ -279,12 +275,14 @@ template <typename T, typename A, int CPL, int LOSS, bool PAIR>
 __global__ void __launch_bounds__(512)
 grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                   const A* __restrict__ beta, A* __restrict__ slab, int ld, int srows, int pieces, int nstage,
-                  int nload, int flags) {
+                  int wpr) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  const int lane = threadIdx.x & 63, R = blockDim.x >> 6;
-  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // W waves = R task slots x wpr waves per slot; slot q's waves split each stage's rows
+  const int lane = threadIdx.x & 63, W = blockDim.x >> 6, R = W / wpr;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = w % R, sub = w / R;
   const unsigned lds_base = static_cast<unsigned>(
       reinterpret_cast<size_t>((__attribute__((address_space(3))) unsigned char*)smem_raw));
   const Task lead = tasks[blockIdx.x * R];  // slot 0 of a bundle is always a real task
@@ -295,31 +293,25 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
   const unsigned char* __restrict__ Y = static_cast<const unsigned char*>(ls.y);
   const A coef = active ? static_cast<A>(segs[task.seg].coef) : A(0);
   const int rowbytes = ld * static_cast<int>(sizeof(T));
-  const int data_bytes = (nload > 0 ? nload : R) * pieces * 1024;  // one stage: data, then 256 B of labels
+  const int data_bytes = W * pieces * 1024;  // one stage buffer: data, then 256 B of labels
   const int buf_bytes = data_bytes + 256;
   const int nrows = lead.row_end - lead.row_begin;
   const int nst = (nrows + srows - 1) / srows;
 
-  // LDS-DMA loads wave q issues for stage t: its 1 KiB pieces of the stage's bytes (+ labels: wave 0)
-  // issuing waves: all R, or the last nload (dedicated loader slots, seg < 0)
-  const int LR = nload > 0 ? nload : R;
-  const int lq = nload > 0 ? q - (R - nload) : q;
-  const bool nt = flags & 1;  // non-temporal loads (rows are read once)
+  // LDS-DMA loads wave w issues for stage t: its 1 KiB pieces of the stage's bytes (+ labels: wave 0)
   auto count = [&](int t) {
-    if (lq < 0) return 0;
     const int nb = (min(srows, nrows - t * srows) * rowbytes + 1023) >> 10;
-    return (nb > lq ? (nb - lq + LR - 1) / LR : 0) + (lq == 0 ? 1 : 0);
+    return (nb > w ? (nb - w + W - 1) / W : 0) + (w == 0 ? 1 : 0);
   };
   auto issue = [&](int t) {
-    if (lq < 0) return;
     const unsigned dst = lds_base + (t % nstage) * buf_bytes;
     const long long r0 = lead.row_begin + static_cast<long long>(t) * srows;
     const int ns = min(srows, static_cast<int>(lead.row_end - r0));
     const int bytes = ns * rowbytes;
     const unsigned char* src = X + r0 * rowbytes;
-    for (int blk = lq; blk * 1024 < bytes; blk += LR)
-      glds16(src + min(blk * 1024 + lane * 16, bytes - 16), dst + blk * 1024, nt);
-    if (lq == 0) {
+    for (int blk = w; blk * 1024 < bytes; blk += W)
+      glds16(src + min(blk * 1024 + lane * 16, bytes - 16), dst + blk * 1024);
+    if (w == 0) {
       const int lb = ns * static_cast<int>(sizeof(A));
       glds4(Y + r0 * sizeof(A) + min(lane * 4, lb - 4), dst + data_bytes);
     }
@@ -358,7 +350,7 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
       // rather than held in registers across the reduction.  A lone last row is paired with
       // itself and weighted 0.
       const bool hi = lane >= 32;
-      for (int i = 0; i < ns; i += 2) {
+      for (int i = 2 * sub; i < ns; i += 2 * wpr) {
         const bool two = i + 1 < ns;
         const unsigned char* row0 = buf + i * rowbytes;
         const unsigned char* row1 = two ? row0 + rowbytes : row0;
@@ -394,7 +386,7 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
       }
     } else {
       // one row at a time
-      for (int i = 0; i < ns; ++i) {
+      for (int i = sub; i < ns; i += wpr) {
         const unsigned char* row = buf + i * rowbytes;
         Rw xr[NV];
 #pragma unroll
@@ -416,7 +408,25 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
       }
     }
   }
-  if (!active) return;
+  if (wpr > 1) {  // fold the slot's waves through LDS (the ring is free after this barrier)
+    A* fold = reinterpret_cast<A*>(smem_raw);
+    __syncthreads();
+    if (active && sub > 0) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+#pragma unroll
+        for (int v = 0; v < VN; ++v) fold[(((sub - 1) * R + q) * NV * VN + j * VN + v) * kWave + lane] = g[j][v];
+    }
+    __syncthreads();
+    if (active && sub == 0) {
+      for (int k = 0; k < wpr - 1; ++k)
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+#pragma unroll
+          for (int v = 0; v < VN; ++v) g[j][v] += fold[((k * R + q) * NV * VN + j * VN + v) * kWave + lane];
+    }
+  }
+  if (!active || sub > 0) return;
   A* out = slab + static_cast<long long>(task.slab) * ld;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
@@ -432,35 +442,30 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
 // ERASUREHEAD_STAGES override them for sweeps.  Rows shrink until the ring fits kStagedLds.
 constexpr int kStagedLds = 160 * 1024;
 struct StagedGeom {
-  int srows, pieces, nstage;
+  int srows, pieces, nstage, wpr;
   size_t lds;
-  int nload, flags;
 };
 static inline int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
-static inline bool staged_geometry(int R, int rowbytes, StagedGeom* g) {
-  // dedicated loader waves (the last slots of every bundle; DenseGradPlan pads the table for them)
-  static const int nload = env_int("ERASUREHEAD_STAGED_LOADERS", 0);
-  static const int flags = env_int("ERASUREHEAD_STAGED_NT", 0) ? 1 : 0;
-  if (nload >= R) return false;
-  const int LR = nload > 0 ? nload : R;
-  static const int env_rows = [] {
-    const char* e = std::getenv("ERASUREHEAD_STAGE_ROWS");
-    return e ? std::atoi(e) : 0;
-  }();
-  static const int env_stages = [] {
-    const char* e = std::getenv("ERASUREHEAD_STAGES");
-    return e ? std::atoi(e) : 0;
-  }();
+// R task slots; fold_bytes_per_wave: one wave's gradient slice (64 * CPL accumulators)
+static inline bool staged_geometry(int R, int rowbytes, size_t fold_bytes_per_wave, StagedGeom* g) {
+  static const int env_rows = env_int("ERASUREHEAD_STAGE_ROWS", 0);
+  static const int env_stages = env_int("ERASUREHEAD_STAGES", 0);
+  static const int env_wpr = env_int("ERASUREHEAD_STAGED_WPR", 0);  // waves per replica slot
+  // defaults (tools/ab_staged_loss.sh): about 4 waves per workgroup and 2 rows per wave per
+  // stage — R = 3: 1 wave per replica, 2 rows; R = 2: 2 waves per replica, 4 rows
   const int ns = env_stages >= 2 && env_stages <= 8 ? env_stages : 2;
-  int s = env_rows > 0 ? std::min(env_rows, 32) : 2;
+  const int wpr = env_wpr >= 1 && env_wpr <= 4 && R * env_wpr <= 8 ? env_wpr : std::max(1, 4 / R);
+  const int W = R * wpr;
+  const size_t fold = static_cast<size_t>(wpr - 1) * R * fold_bytes_per_wave;
+  int s = env_rows > 0 ? std::min(env_rows, 32) : 2 * wpr;
   for (; s >= 1; --s) {
-    const int p = (s * rowbytes + LR * 1024 - 1) / (LR * 1024);
-    const size_t bytes = static_cast<size_t>(ns) * (static_cast<size_t>(LR) * p * 1024 + 256);
+    const int p = (s * rowbytes + W * 1024 - 1) / (W * 1024);
+    const size_t bytes = std::max(fold, static_cast<size_t>(ns) * (static_cast<size_t>(W) * p * 1024 + 256));
     if (bytes <= kStagedLds) {
-      *g = StagedGeom{s, p, ns, bytes, nload, flags};
+      *g = StagedGeom{s, p, ns, wpr, bytes};
       return true;
     }
   }
@@ -847,7 +852,8 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
   const int bundle_r = variant > 10 && variant <= 18 ? variant - 10 : staged_r;
   if (bundle_r && ntasks % bundle_r != 0) return hipErrorInvalidValue;
   StagedGeom sg{};
-  if (staged_r && !staged_geometry(staged_r, ld * static_cast<int>(sizeof(T)), &sg)) return hipErrorInvalidValue;
+  if (staged_r && !staged_geometry(staged_r, ld * static_cast<int>(sizeof(T)), 64ull * cpl * sizeof(A), &sg))
+    return hipErrorInvalidValue;
 #define EH_IF(C)                                                                          \
   case C:                                                                                 \
     if constexpr (C % VN == 0) {                                                          \
@@ -859,9 +865,9 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sg.lds));      \
           if (ea != hipSuccess) return ea;                                                \
         }                                                                                 \
-        hipLaunchKernelGGL(kern, dim3(ntasks / staged_r), dim3(64 * staged_r), sg.lds, st, \
-                           segs, tasks, beta, slab, ld, sg.srows, sg.pieces, sg.nstage,   \
-                           sg.nload, sg.flags);                                           \
+        hipLaunchKernelGGL(kern, dim3(ntasks / staged_r), dim3(64 * staged_r * sg.wpr),   \
+                           sg.lds, st, segs, tasks, beta, slab, ld, sg.srows, sg.pieces,  \
+                           sg.nstage, sg.wpr);                                            \
         return hipGetLastError();                                                         \
       }                                                                                   \
       if (bundle_r) {                                                                     \

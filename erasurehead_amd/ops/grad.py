@@ -200,8 +200,7 @@ class DenseGradPlan:
         groups: List[List[int]] = []
         for b in bundles.values():
             groups += [b[i:i + MAX_BUNDLE] for i in range(0, len(b), MAX_BUNDLE)]
-        # + dedicated loader slots of grad_dense_staged (ERASUREHEAD_STAGED_LOADERS, sweeps only)
-        R = max(len(g) for g in groups) + (int(os.environ.get("ERASUREHEAD_STAGED_LOADERS", "0")) if self.staged else 0)
+        R = max(len(g) for g in groups)
         pad = (0, -1, 0, 0, 0)
         table = []
         for g in groups:

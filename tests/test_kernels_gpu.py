@@ -290,14 +290,16 @@ def test_eval_gemm_unaligned_rows_use_scalar_staging(native):
     np.testing.assert_allclose(s.cpu().numpy(), ref, rtol=1e-10)
 
 
+@pytest.mark.parametrize("layout", ["mixed", "pairs"])
 @pytest.mark.parametrize("pair", [False, True])
 @pytest.mark.parametrize("staged,rows,d,prec_name", [(False, "64", 1000, "fp64"), (True, "64", 1000, "fp64"),
                                                      (True, "37", 1000, "fp64"), (True, "100", 250, "fp64"),
                                                      (True, "64", 1000, "fp32"), (True, "64", 1000, "bf16")])
-def test_dense_grad_replica_bundle_kernel(monkeypatch, native, staged, rows, d, prec_name, pair):
-    """Opt-in bundle kernels (one wave per replica per workgroup; rows loaded per wave, or staged
-    once through LDS by LDS-DMA) against the fp64 oracle.  Row counts that leave partial stages
-    and partial bundles are included."""
+def test_dense_grad_replica_bundle_kernel(monkeypatch, native, staged, rows, d, prec_name, pair, layout):
+    """Bundle kernels (one wave per replica per workgroup; rows loaded per wave, or staged once
+    through LDS by LDS-DMA) against the fp64 oracle.  Row counts that leave partial stages and
+    partial bundles are included.  "mixed": bundles of 5 and 3 replicas (one wave per replica);
+    "pairs": bundles of 2 (the staged kernel then runs two waves per replica and folds them)."""
     monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", rows)
     if pair and not staged:
         pytest.skip("pair applies to the staged kernel")
@@ -305,7 +307,10 @@ def test_dense_grad_replica_bundle_kernel(monkeypatch, native, staged, rows, d, 
     prec = get_precision(prec_name)
     rng = np.random.RandomState(21)
     parts, host = _parts(rng, [700, 500, 301], d, prec)
-    msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
+    if layout == "mixed":
+        msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
+    else:
+        msgs = [[(0, 1.0)]] * 2 + [[(1, 1.0), (2, 0.5)], [(1, -1.0), (2, 2.0)]]
     plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, d)
     assert plan.bundle_rows == int(rows) and plan.variant > (30 if pair else 20 if staged else 10)
     beta = torch.randn(plan.ld, dtype=prec.acc, device=DEV) * 0.05

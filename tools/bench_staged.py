@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--precision", default="fp64")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--layout", choices=["agc", "frc1"], default="agc")
     a = ap.parse_args()
     import torch
 
@@ -34,7 +35,9 @@ def main():
         y = torch.where(torch.rand(rpp, device="cuda", generator=g) > 0.5, 1.0, -1.0).to(prec.acc)
         parts[p] = (X, y)
     beta = torch.randn(prec.ld(d), device="cuda", dtype=prec.acc, generator=g) * 0.01
-    frc = [[0, 1, 2]] * 3 + [[3, 4, 5]] * 3 + [[6, 7]] * 2
+    frc = [[0, 1, 2]] * 3 + [[3, 4, 5]] * 3 + [[6, 7]] * 2  # AGC W=8 s=2 (--layout agc)
+    if a.layout == "frc1":  # exact FRC W=8 s=1: four groups of 2
+        frc = [[0, 1]] * 2 + [[2, 3]] * 2 + [[4, 5]] * 2 + [[6, 7]] * 2
     loss = LOGISTIC if a.loss == "logistic" else LEAST_SQUARES
     plan = DenseGradPlan([[(p, 1.0) for p in m] for m in frc], parts, prec, loss, d)
     G = plan.out_buffer()[0]
@@ -50,7 +53,7 @@ def main():
         e.synchronize()
         times.append(s.elapsed_time(e))
     times.sort()
-    print(json.dumps({"tag": a.tag, "loss": a.loss, "precision": a.precision, "variant": plan.variant,
+    print(json.dumps({"tag": a.tag, "layout": a.layout, "loss": a.loss, "precision": a.precision, "variant": plan.variant,
                       "ms_median": times[len(times) // 2], "ms_min": times[0],
                       "distinct_TBps": plan.distinct_bytes / 1e9 / times[len(times) // 2]}), flush=True)
 
