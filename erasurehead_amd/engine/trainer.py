@@ -48,10 +48,11 @@ from ..parallel.collector import ArrivalCollector
 from ..parallel.dist import DistEnv
 from ..parallel.placement import place_workers_shared, workers_by_rank
 
-# Cost of re-reading a partition row that a co-located replica already streams, relative to a
-# distinct row (dense fp64 on MI355X: (1.84 - 1.29) ms for 14 GB of replica rows against
-# 1.29 ms for 8 GB of distinct rows, docs/PERF_NOTES.md).
-REPLICA_WEIGHT_DENSE = 0.25
+# Cost of a replica's message rows whose HBM reads a co-located replica already streams, relative
+# to a distinct row (dense fp64 on MI355X with the LDS-staged bundles: (1.56 - 1.29) ms for 14 GB
+# of replica rows against 1.29 ms for 8 GB of distinct rows; FRC s = 1 gives the same 0.11,
+# docs/PERF_NOTES.md).
+REPLICA_WEIGHT_DENSE = 0.12
 from ..parallel.transport import make_transport
 from ..utils import report
 from ..utils.delay import DelayModel

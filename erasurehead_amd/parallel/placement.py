@@ -8,7 +8,7 @@ workers and computes all of their messages in one kernel launch per round.
 Assignment (deterministic on every rank): `place_workers` is longest-processing-time greedy
 on each worker's rows-per-round (the coded schemes replicate data unevenly, e.g. FRC with a
 short last group).  `place_workers_shared` refines it for GPUs, where workers that read the
-same partitions share HBM reads (replica-interleaved dispatch), so keeping an FRC group or
+same partitions share HBM reads (LDS-staged bundles / interleaved dispatch), so keeping an FRC group or
 cyclic neighbours together costs less than their message rows suggest.
 """
 from __future__ import annotations
@@ -39,10 +39,11 @@ def rank_cost(workers: Sequence[int], parts: Sequence[Sequence[Tuple[int, int]]]
     """Estimated per-round work of one rank hosting `workers`.
 
     parts[w] = [(partition, rows), ...] read by worker w's messages.  Rows of a partition read
-    by several co-located messages are streamed from HBM once when the replicas' tasks are
-    co-scheduled (ops/grad.py:replica_dispatch_order); each further read costs
-    `replica_weight` of a distinct row (measured ≈ 0.25 for dense fp64 on MI355X, 1 where
-    nothing is shared, 0 with --share-partitions).
+    by several co-located messages are streamed from HBM once (LDS-staged replica bundles, or
+    replica tasks co-scheduled on one XCD: ops/grad.py); each further message over them costs
+    `replica_weight` of a distinct row (measured ≈ 0.12 for dense fp64 on MI355X with the staged
+    bundles, 0.25 with the interleaved dispatch, 1 where nothing is shared, 0 with
+    --share-partitions).
     """
     distinct: Dict[int, int] = {}
     total = 0
