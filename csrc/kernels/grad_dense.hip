@@ -261,6 +261,12 @@ __device__ __forceinline__ void glds4(const void* g, unsigned lds) {
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant; n > 63 waits
 // for 63, which is stricter and therefore safe).
 __device__ __forceinline__ void wait_vmcnt(int n) {
+  // The two-stage ring (the default) always waits for everything: test that first.  Testing a
+  // readfirstlane copy keeps the compiler from folding it into the switch's compare tree.
+  if (__builtin_amdgcn_readfirstlane(n) <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
   switch (n) {
 #define EH_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); return;
 #define EH_W8(k) EH_W(k) EH_W(k + 1) EH_W(k + 2) EH_W(k + 3) EH_W(k + 4) EH_W(k + 5) EH_W(k + 6) EH_W(k + 7)
@@ -298,11 +304,15 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
   const int nrows = lead.row_end - lead.row_begin;
   const int nst = (nrows + srows - 1) / srows;
 
-  // LDS-DMA loads wave w issues for stage t: its 1 KiB pieces of the stage's bytes (+ labels: wave 0)
-  auto count = [&](int t) {
-    const int nb = (min(srows, nrows - t * srows) * rowbytes + 1023) >> 10;
+  // LDS-DMA loads wave w issues for a stage of nbytes: its 1 KiB pieces (+ labels: wave 0).  Every
+  // stage but the last is full, so two counts cover the ring; computing them once keeps integer
+  // divisions (and the loop the vectorizer made of a per-stage sum) out of the stage loop.
+  auto count_bytes = [&](int nbytes) {
+    const int nb = (nbytes + 1023) >> 10;
     return (nb > w ? (nb - w + W - 1) / W : 0) + (w == 0 ? 1 : 0);
   };
+  const int cnt_full = count_bytes(srows * rowbytes);
+  const int cnt_last = count_bytes((nrows - (nst - 1) * srows) * rowbytes);
   auto issue = [&](int t) {
     const unsigned dst = lds_base + (t % nstage) * buf_bytes;
     const long long r0 = lead.row_begin + static_cast<long long>(t) * srows;
@@ -333,8 +343,9 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
   using Rw = typename Vec16<T>::raw;
   for (int t = 0; t < nstage - 1 && t < nst; ++t) issue(t);
   for (int t = 0; t < nst; ++t) {
-    int later = 0;  // loads this wave issued after stage t
-    for (int u = t + 1; u <= min(t + nstage - 2, nst - 1); ++u) later += count(u);
+    // loads this wave issued after stage t: stages t+1 .. hi, only stage nst-1 can be partial
+    const int hi = min(t + nstage - 2, nst - 1);
+    const int later = hi > t ? (hi - t) * cnt_full + (hi == nst - 1 ? cnt_last - cnt_full : 0) : 0;
     wait_vmcnt(later);  // this wave's pieces of stage t landed
     __syncthreads();    // every wave's pieces of stage t; stage t-1 consumed by every wave
     if (t + nstage - 1 < nst) issue(t + nstage - 1);  // into the buffer stage t-1 used
