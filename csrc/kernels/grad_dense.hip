@@ -373,8 +373,8 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
           const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
 #pragma unroll
           for (int v = 0; v < VN; ++v) {
-            z0 = fma(valid[j] ? Vec16<T>::template elem<A>(v0, v) : A(0), b[j][v], z0);
-            z1 = fma(valid[j] ? Vec16<T>::template elem<A>(v1, v) : A(0), b[j][v], z1);
+            z0 = fma(Vec16<T>::template elem<A>(v0, v), b[j][v], z0);  // beta is 0 past the row end
+            z1 = fma(Vec16<T>::template elem<A>(v1, v), b[j][v], z1);
           }
         }
         const A zs = wave_pair_reduce(z0, z1, hi);
@@ -389,8 +389,8 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
           const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
 #pragma unroll
           for (int v = 0; v < VN; ++v) {
-            const A e0 = valid[j] ? Vec16<T>::template elem<A>(v0, v) : A(0);
-            const A e1 = valid[j] ? Vec16<T>::template elem<A>(v1, v) : A(0);
+            const A e0 = Vec16<T>::template elem<A>(v0, v);  // columns past the row end: never written
+            const A e1 = Vec16<T>::template elem<A>(v1, v);
             g[j][v] = fma(r1, e1, fma(r0, e0, g[j][v]));
           }
         }
@@ -401,10 +401,13 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
         const unsigned char* row = buf + i * rowbytes;
         Rw xr[NV];
 #pragma unroll
-        for (int j = 0; j < NV; ++j) {  // clamped read, masked to zero past the row end
+        for (int j = 0; j < NV; ++j) {
+          // Clamped read: past the row end a lane re-reads the row's last vector.  It is not
+          // masked: beta is 0 there, so its dot-product terms add exactly 0 (finite data), and the
+          // gradient columns it pollutes are never written.  A per-vector select compiled to exec
+          // branches and 64-bit moves that cost as much as the row's FMAs.
           const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
-          const Rw v = *reinterpret_cast<const Rw*>(row + c0);
-          xr[j] = valid[j] ? v : Rw{};
+          xr[j] = *reinterpret_cast<const Rw*>(row + c0);
         }
         A z = A(0);  // one accumulator: four independent chains measured no faster
 #pragma unroll
