@@ -4,6 +4,14 @@ The extension (gfx950 HIP kernels + the C++ arrival collector) is built in-tree 
 ``tools/build_ext.py``; if it is missing it is built on first use (hipcc cross-compiles
 without a GPU).  GPU code paths call :func:`native` and fail loudly when the extension
 cannot be loaded — there is no silent eager fallback on a GPU.
+
+Build provenance: the library carries the SHA-256 of the ``csrc/`` tree it was compiled
+from (``EH_SOURCE_HASH:<hex>``, see ``tools/build_ext.py``).  Before importing it,
+:func:`native` reads that hash straight from the ``.so`` file and compares it with the
+sources next to it.  A mismatch rebuilds (``build_if_missing=True``) or raises
+:class:`StaleBuildError`; a library that was shipped from elsewhere can therefore never
+run kernels other than the ones in this tree.  ``ERASUREHEAD_CSRC_DIR`` points the
+check at another source tree (tests).
 """
 from __future__ import annotations
 
@@ -17,21 +25,54 @@ _mod = None
 _err = None
 
 
+class StaleBuildError(RuntimeError):
+    """The built ``_C`` library does not match the ``csrc/`` sources of this tree."""
+
+
 def _root() -> str:
     return os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def _build_ext():
     tools = os.path.join(_root(), "tools")
     if tools not in sys.path:
         sys.path.insert(0, tools)
     import build_ext  # type: ignore
 
-    return build_ext.build(force=force, verbose=verbose)
+    return build_ext
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    return _build_ext().build(force=force, verbose=verbose)
+
+
+def csrc_dir() -> str:
+    return os.environ.get("ERASUREHEAD_CSRC_DIR") or os.path.join(_root(), "csrc")
+
+
+def provenance() -> dict:
+    """{'so': path, 'built_from': hash in the .so (None if missing), 'tree': hash of csrc/, 'fresh': bool}."""
+    be = _build_ext()
+    so = be.target_path()
+    built = be.embedded_hash(so) if os.path.exists(so) else None
+    tree = be.source_hash(csrc_dir())
+    return {"so": so, "built_from": built, "tree": tree, "fresh": built is not None and built == tree}
+
+
+def check_fresh() -> dict:
+    """Raise :class:`StaleBuildError` unless the built library matches the source tree."""
+    p = provenance()
+    if not os.path.exists(p["so"]):
+        raise StaleBuildError(f"native extension not built ({p['so']} missing): run python tools/build_ext.py")
+    if not p["fresh"]:
+        raise StaleBuildError(
+            f"stale native build: {os.path.basename(p['so'])} was compiled from csrc/ hash "
+            f"{(p['built_from'] or 'unknown')[:16]}, the tree is {p['tree'][:16]}; run python tools/build_ext.py")
+    return p
 
 
 def native(build_if_missing: bool = True):
-    """Return the loaded ``_C`` module (building it if needed); raise if impossible."""
+    """Return the loaded ``_C`` module (building it if missing or stale); raise if impossible."""
     global _mod, _err
     if _mod is not None:
         return _mod
@@ -39,15 +80,23 @@ def native(build_if_missing: bool = True):
         if _mod is not None:
             return _mod
         try:
-            _mod = importlib.import_module("erasurehead_amd._C")
-            return _mod
-        except ImportError as e:  # not built yet
+            check_fresh()
+        except StaleBuildError as e:
+            if not build_if_missing or os.environ.get("ERASUREHEAD_NO_BUILD"):
+                raise
             _err = e
-        if not build_if_missing or os.environ.get("ERASUREHEAD_NO_BUILD"):
-            raise RuntimeError(f"erasurehead_amd native extension not available: {_err}")
-        build()
-        importlib.invalidate_caches()
-        _mod = importlib.import_module("erasurehead_amd._C")
+            build()
+            importlib.invalidate_caches()
+            check_fresh()
+        try:
+            mod = importlib.import_module("erasurehead_amd._C")
+        except ImportError as e:
+            raise RuntimeError(f"erasurehead_amd native extension not loadable: {e}") from e
+        tree = provenance()["tree"]
+        if getattr(mod, "SOURCE_HASH", None) != tree:
+            raise StaleBuildError(f"loaded _C reports SOURCE_HASH {getattr(mod, 'SOURCE_HASH', None)!r}, "
+                                  f"tree is {tree}")
+        _mod = mod
         return _mod
 
 

@@ -5,6 +5,14 @@ No hipify, no torch JIT cache: HIP kernels are compiled with ``hipcc --offload-a
 with ``g++`` against the HIP runtime headers, then everything is linked with ``hipcc -shared``.
 Objects are cached under ``build/`` and rebuilt only when a source or header changed.
 
+Provenance: a SHA-256 over every ``csrc/`` source and header plus this build script
+(:func:`source_hash`) is compiled into the library as the string ``EH_SOURCE_HASH:<hex>``
+and exposed as ``_C.SOURCE_HASH``.  ``erasurehead_amd._ext.native()`` reads it from the
+``.so`` file BEFORE loading it and rebuilds (or, with ``build_if_missing=False``, refuses
+with :class:`StaleBuildError`) when it differs from the tree, so a shipped ``.so`` can
+never silently run code other than the sources next to it.  A hash mismatch forces a
+full rebuild regardless of file mtimes.
+
 Usage:  python tools/build_ext.py [--force] [-j N]
 """
 from __future__ import annotations
@@ -12,6 +20,7 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -22,6 +31,49 @@ CSRC = os.path.join(ROOT, "csrc")
 BUILD = os.path.join(ROOT, "build", "objs")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+HASH_MARKER = b"EH_SOURCE_HASH:"
+
+
+def _hash_inputs(csrc: str = CSRC):
+    files = []
+    for ext in ("*.hip", "*.cpp", "*.h"):
+        files += glob.glob(os.path.join(csrc, "**", ext), recursive=True)
+    files = sorted(files, key=lambda p: os.path.relpath(p, csrc))
+    return files
+
+
+def source_hash(csrc: str = CSRC) -> str:
+    """SHA-256 over the native sources (relative path + bytes) and the build script."""
+    h = hashlib.sha256()
+    for p in _hash_inputs(csrc):
+        if p.endswith("_selftest.cpp"):
+            continue
+        h.update(os.path.relpath(p, csrc).replace(os.sep, "/").encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    with open(os.path.abspath(__file__), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()
+
+
+def embedded_hash(so_path: str):
+    """The source hash compiled into a built library (read from the file; nothing is loaded)."""
+    try:
+        with open(so_path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    k = data.find(HASH_MARKER)
+    if k < 0:
+        return None
+    v = data[k + len(HASH_MARKER): k + len(HASH_MARKER) + 64]
+    try:
+        return v.decode("ascii")
+    except UnicodeDecodeError:
+        return None
 
 
 def _torch_paths():
@@ -77,15 +129,25 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
                f"-I{ROCM}/include", *[f"-I{p}" for p in inc], f"-I{pyinc}",
                "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-w"]
         jobs_list.append((s, o, cmd))
+    out = target_path()
+    want = source_hash()
+    if embedded_hash(out) not in (None, want) and os.path.exists(out):
+        force = True  # the library was built from other sources: never trust mtimes then
+    hsrc = os.path.join(BUILD, "source_hash.cpp")
+    text = ('// generated by tools/build_ext.py: hash of the csrc/ tree this library was built from\n'
+            f'extern "C" __attribute__((used)) const char eh_source_hash[] = "{HASH_MARKER.decode()}{want}";\n')
+    if not os.path.exists(hsrc) or open(hsrc).read() != text:
+        with open(hsrc, "w") as f:
+            f.write(text)
+    jobs_list.append((hsrc, hsrc + ".o", ["g++", "-c", hsrc, "-o", hsrc + ".o", "-O2", "-fPIC"]))
     todo = [(s, o, c) for (s, o, c) in jobs_list if force or _stale(o, s, headers)]
     n = jobs or min(len(todo), max(1, (os.cpu_count() or 4)), 8) or 1
     with cf.ThreadPoolExecutor(max_workers=n) as ex:
         futs = {ex.submit(_run, c): s for (s, o, c) in todo}
         for f in cf.as_completed(futs):
-            out = f.result()
+            log = f.result()
             if verbose:
-                print("compiled", os.path.relpath(futs[f], ROOT), out, flush=True)
-    out = target_path()
+                print("compiled", os.path.relpath(futs[f], ROOT), log, flush=True)
     objs = [o for (_, o, _) in jobs_list]
     if force or todo or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
         link = [os.path.join(ROCM, "bin", "hipcc"), "-shared", "-fPIC", "-o", out + ".tmp", *objs,
@@ -93,6 +155,8 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
                 "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64",
                 f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx"]
         _run(link)
+        if embedded_hash(out + ".tmp") != want:
+            raise RuntimeError("build: linked library does not carry the tree's source hash")
         os.replace(out + ".tmp", out)
         if verbose:
             print("linked", os.path.relpath(out, ROOT), flush=True)
