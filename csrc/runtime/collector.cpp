@@ -29,6 +29,17 @@ Collector::Collector(int n_workers, std::vector<int> group_of, int n_groups)
   group_done_.assign(std::max(n_groups_, 1), 0);
 }
 
+uint64_t Collector::tie_key(int64_t seed, int round, int worker) {
+  // splitmix64 of (seed, round, worker): distinct workers get independent uniform keys, so the
+  // sort below orders tied workers by a uniformly random permutation that changes every round
+  uint64_t z = static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ull ^ (static_cast<uint64_t>(round) << 32) ^
+               static_cast<uint64_t>(worker);
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
 double Collector::now() {
   using namespace std::chrono;
   return duration<double>(steady_clock::now().time_since_epoch()).count();
@@ -49,6 +60,9 @@ void Collector::begin_round(int round, double t_start, int rule, int k) {
   std::fill(got1_.begin(), got1_.end(), 0);
   std::fill(group_done_.begin(), group_done_.end(), 0);
   cnt0_ = cnt1_ = cnt_groups_ = 0;
+  tie_.assign(W_, 0);
+  if (tie_seed_ >= 0)
+    for (int w = 0; w < W_; ++w) tie_[w] = tie_key(tie_seed_, round, w);
 }
 
 int Collector::add_event_probe(int worker, int part, int round, uintptr_t event, double delay) {
@@ -144,7 +158,11 @@ bool Collector::process_ready(double t, bool /*stop_at_rule*/) {
   }
   if (ready.empty()) return stopped_;
   std::sort(ready.begin(), ready.end(), [&](int a, int b) {
-    if (probes_[a].ready != probes_[b].ready) return probes_[a].ready < probes_[b].ready;
+    const Probe& pa = probes_[a];
+    const Probe& pb = probes_[b];
+    if (pa.ready != pb.ready) return pa.ready < pb.ready;
+    if (pa.round == round_ && pb.round == round_ && tie_[pa.worker] != tie_[pb.worker])
+      return tie_[pa.worker] < tie_[pb.worker];  // seeded per-round tie permutation
     return a < b;
   });
   for (int id : ready) {

@@ -22,6 +22,14 @@
 // straggler carries into the next round when the scheme does not drain), while the
 // hardware stays busy.  delay = +inf models a dead worker (an erasure that never
 // arrives; bounded by the round timeout instead of hanging like the reference).
+//
+// Tie model: messages that become ready at the same instant (every local message of one
+// process shares the gradient kernel's HIP event; with add_delay = 0 nothing separates
+// them) are ordered by a per-round permutation of the workers seeded by (tie_seed, round)
+// — the stand-in for the reference's Waitany order, which varies with real timing from
+// round to round.  Ordering such ties by worker id instead would let AGC stop on the same
+// k workers every round and never cover the last FRC groups' partitions.  tie_seed < 0
+// restores the plain probe (worker) order.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -54,6 +62,11 @@ class Collector {
   static double now();
 
   void begin_round(int round, double t_start, int rule, int k);
+  // Seed of the per-round tie permutation (< 0: ties keep probe order); see the tie model above.
+  void set_tie_seed(int64_t seed) { tie_seed_ = seed; }
+  int64_t tie_seed() const { return tie_seed_; }
+  // Tie rank of `worker` in `round` (smaller first); the permutation any host code can replay.
+  static uint64_t tie_key(int64_t seed, int round, int worker);
   int add_event_probe(int worker, int part, int round, uintptr_t event, double delay);
   int add_host_probe(int worker, int part, int round, double delay);
   // IPC mailbox probe: arrived once the 64-bit flag at `flag_addr` (shared host memory,
@@ -105,6 +118,8 @@ class Collector {
   int rule_ = kRuleAll;
   int k_ = 0;
   bool stopped_ = false;
+  int64_t tie_seed_ = -1;
+  std::vector<uint64_t> tie_;  // [worker] tie key of the current round
   std::vector<double> round_start_;
   std::vector<std::vector<double>> finish_;  // [worker][round] virtual finish
   std::vector<Probe> probes_;

@@ -390,7 +390,10 @@ class MasterPump {
     need(i >= 0 && i < R_, "round out of range");
     need(beta_in_.defined(), "set_state first");
     const int slot = i % K_;
-    if (i >= K_) col_->wait_seen(i - K_, timeout_);  // the ring slot's previous round has landed
+    if (i >= K_ && !col_->wait_seen(i - K_, timeout_))  // the ring slot's previous round must have landed
+      throw std::runtime_error("MasterPump round " + std::to_string(i) + ": messages of round " +
+                               std::to_string(i - K_) + " still in flight after the round timeout; mailbox slot " +
+                               std::to_string(slot) + " cannot be reused");
     const double t = eh::Collector::now();
     col_->begin_round(i, t, stop_rule_, k_);
     t_start_[i] = t;
@@ -471,8 +474,8 @@ class MasterPump {
   // ---- device-driven rounds (single process, no injected delay) -------------------------
   // Every message is local and finishes with the one gradient launch, so the arrival order
   // (and with it the decode) is fixed before the GPU runs: the collector still decides it,
-  // from host probes seen at the round start (ties break by probe order, exactly like the
-  // simultaneous HIP-event probes of begin()).  The host decodes rounds [a, b) up front and
+  // from host probes seen at the round start (ties break by the collector's seeded per-round
+  // permutation, exactly like the simultaneous HIP-event probes of begin()).  The host decodes rounds [a, b) up front and
   // enqueues  grad(i) -> combine_update(i)  back to back, so the device never waits for the
   // host between rounds.  With `graph` the whole segment is captured into hipGraphs (at most
   // kGraphRounds rounds each) and replayed with one launch per graph.

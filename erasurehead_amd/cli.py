@@ -61,6 +61,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "enqueued back to back (stream) or host-driven (off)")
     g.add_argument("--share-partitions", action="store_true",
                    help="stream each distinct partition once per GPU and encode the local messages on the device")
+    g.add_argument("--tie-break", default="permute", choices=["permute", "worker"],
+                   help="order of simultaneous arrivals: seeded per-round worker permutation (default) or worker id")
+    g.add_argument("--tie-seed", type=int, default=0)
     return p
 
 
@@ -80,7 +83,8 @@ def parse(argv: List[str]):
                     round_timeout=a.round_timeout, fix_quirks=a.fix_quirks, save_linear=a.save_linear,
                     full_precision_outputs=a.full_precision_outputs, evaluate=not a.no_eval, verbose=not a.quiet,
                     checkpoint_every=a.checkpoint_every, checkpoint_path=a.checkpoint_path, resume=a.resume, trace=a.trace, verify_beta=a.verify_beta,
-                    transport=a.transport, share_partitions=a.share_partitions, device_loop=a.device_loop)
+                    transport=a.transport, share_partitions=a.share_partitions, device_loop=a.device_loop,
+                    tie_break=a.tie_break, tie_seed=a.tie_seed)
     return cfg, a
 
 

@@ -73,12 +73,23 @@ class RunConfig:
     transport: str = "auto"  # auto | ipc | rccl | gloo (parallel/transport.py)
     device_loop: str = "auto"  # auto|graph|stream|off: device-driven rounds when eligible (trainer._device_loop_mode)
     share_partitions: bool = False  # co-located workers: distinct partitions once + device encode (ops/grad.py)
+    # simultaneous arrivals (add_delay = 0, or one kernel finishing several local workers): "permute"
+    # orders them by a per-round permutation seeded by (tie_seed, round) (csrc/runtime/collector.h,
+    # tie model); "worker" keeps worker-id order (AGC then stops on the same k workers every round)
+    tie_break: str = "permute"
+    tie_seed: int = 0
 
     def __post_init__(self):
         self.update_rule = str(self.update_rule)
         if self.update_rule not in ("GD", "AGD"):
             raise ValueError("update_rule must be GD or AGD")  # ref src/naive.py:13 assert
         self.input_dir = self.input_dir if self.input_dir.endswith("/") else self.input_dir + "/"
+        if self.tie_break not in ("permute", "worker"):
+            raise ValueError("tie_break must be permute or worker")
+
+    @property
+    def tie_seed_value(self) -> int:
+        return int(self.tie_seed) if self.tie_break == "permute" else -1
 
     @property
     def n_workers(self) -> int:

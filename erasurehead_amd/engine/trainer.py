@@ -99,8 +99,9 @@ class Trainer:
             rng = np.random.RandomState(cfg.seed) if cfg.seed is not None else None
             B = None
             if env.is_master or env.world == 1:
+                B0 = self._checkpoint_B(cfg.resume) if cfg.resume else None  # a resumed run keeps its code
                 scheme = make_scheme(self.key, W, cfg.n_stragglers, cfg.n_rows, cfg.num_collect, cfg.partitions,
-                                     cfg.allow_uneven_groups, rng)
+                                     cfg.allow_uneven_groups, rng if B0 is None else None, B0)
                 B = scheme.B
             B = env.broadcast_object(B, 0) if env.world > 1 else B
             if not env.is_master:
@@ -293,7 +294,7 @@ class Trainer:
         cfg, env, sch = self.cfg, self.env, self.scheme
         R, W, K = cfg.num_itrs, cfg.n_workers, self.K
         eta = cfg.eta()
-        col = ArrivalCollector(W, sch.group_of, sch.n_groups, env.gpu)
+        col = ArrivalCollector(W, sch.group_of, sch.n_groups, env.gpu, cfg.tie_seed_value)
         timeset = np.zeros(R)
         loop_time = np.zeros(R)
         worker_timeset = np.zeros((R, W))
@@ -315,8 +316,9 @@ class Trainer:
             if cfg.verbose and i % 10 == 0:
                 log(report.iteration_tick(i))
             slot = i % K
-            if i >= K:
-                col.wait_seen(i - K, cfg.round_timeout)  # ring slot reuse: round i-K's data has landed
+            if i >= K and not col.wait_seen(i - K, cfg.round_timeout):  # ring slot reuse: round i-K landed
+                raise TimeoutError(f"round {i}: messages of round {i - K} still in flight after "
+                                   f"{cfg.round_timeout}s; cannot reuse mailbox slot {i % K}")
             t_start = col.now()
             col.begin_round(i, t_start, self.rule_kind, self.rule_k)
             delays = delay_table[i]
@@ -330,9 +332,10 @@ class Trainer:
                         ev.record(self.cs)
                         for m in self.local_msgs:
                             col.add_event(m.worker, m.part, i, ev, delays[m.worker])
-                    else:
+                    else:  # one compute call finished every local message: they are seen together
+                        t_done = col.now()
                         for m in self.local_msgs:
-                            col.add_work(m.worker, m.part, i, None, delays[m.worker])
+                            col.add_work(m.worker, m.part, i, None, delays[m.worker], t_seen=t_done)
             with self.timer.phase("post_recv"):
                 self._post_recvs(i, slot, col, delays)
             with self.timer.phase("wait_k"):
@@ -400,7 +403,7 @@ class Trainer:
         cfg, env, sch = self.cfg, self.env, self.scheme
         R, W, K = cfg.num_itrs, cfg.n_workers, self.K
         C = native_ext()
-        col = ArrivalCollector(W, sch.group_of, sch.n_groups, True)
+        col = ArrivalCollector(W, sch.group_of, sch.n_groups, True, cfg.tie_seed_value)
         dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
         pump = C.MasterPump(col.c, W, R, K, self.d, self.ld, dev, float(cfg.round_timeout))
         pump.set_state(self.beta, self.u, self.hist, self.beta_in)
@@ -616,8 +619,12 @@ class Trainer:
         """Resume the master from a checkpoint written by :meth:`_checkpoint`; returns the next round.
 
         Loaded with ``weights_only=True`` (tensors and plain containers only).  The injected
-        delays are seeded by the round index (utils/delay.py), so a resumed run sees the
-        same straggler pattern as an uninterrupted one.
+        delays are seeded by the round index (utils/delay.py) and the cyclic code B is
+        restored from the checkpoint (:meth:`_checkpoint_B`), so a resumed run draws the same
+        delays and decodes with the same code as an uninterrupted one.  What is NOT carried
+        over is the virtual lag a straggler carries between rounds in schemes without a drain
+        (cyclic, avoidstragg, partial_*): the collector's finish times are wall-clock instants
+        of the interrupted process, so the first resumed round starts every worker fresh.
         """
         st = torch.load(path, map_location="cpu", weights_only=True)
         if st.get("scheme") != self.key:
@@ -636,11 +643,19 @@ class Trainer:
         self._restored = {"timeset": st["timeset"].numpy(), "worker_timeset": st["worker_timeset"].numpy()}
         return nxt
 
+    @staticmethod
+    def _checkpoint_B(path: str) -> Optional[np.ndarray]:
+        st = torch.load(path, map_location="cpu", weights_only=True)
+        B = st.get("B")
+        return None if B is None else B.numpy().astype(np.float64)
+
     def _checkpoint(self, next_round: int, timeset, worker_timeset):
         path = self.cfg.checkpoint_path or os.path.join(self.cfg.input_dir, "checkpoint.pt")
         state = {"next_round": next_round, "beta": self.beta.cpu(), "u": self.u.cpu(),
                  "hist": self.hist[:next_round].cpu(), "timeset": torch.from_numpy(timeset[:next_round].copy()),
                  "worker_timeset": torch.from_numpy(worker_timeset[:next_round].copy()), "scheme": self.key}
+        if getattr(self.scheme, "B", None) is not None:
+            state["B"] = torch.from_numpy(np.ascontiguousarray(self.scheme.B, dtype=np.float64))
         tmp = path + ".tmp"
         torch.save(state, tmp)
         os.replace(tmp, path)

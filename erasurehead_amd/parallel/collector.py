@@ -22,10 +22,11 @@ from ..codes.schemes import Arrival
 
 
 class ArrivalCollector:
-    def __init__(self, n_workers: int, group_of: Sequence[int], n_groups: int, gpu: bool):
+    def __init__(self, n_workers: int, group_of: Sequence[int], n_groups: int, gpu: bool, tie_seed: int = -1):
         C = native()
         self._C = C
         self.c = C.Collector(int(n_workers), [int(g) for g in group_of], int(n_groups))
+        self.c.set_tie_seed(int(tie_seed))  # simultaneous arrivals: seeded per-round worker permutation
         self.gpu = gpu
         self._keep: Dict[int, object] = {}  # probe -> event (kept alive until arrival)
         self._pending_host = 0
@@ -66,11 +67,12 @@ class ArrivalCollector:
         """IPC mailbox probe: arrived when the shared-host counter at ``addr`` reaches ``value``."""
         return self.c.add_flag_probe(int(worker), int(part), int(i), int(addr), int(value), float(delay))
 
-    def add_work(self, worker: int, part: int, i: int, work, delay: float, src: int = 0) -> int:
-        """Host probe completed when ``work`` finishes (None = already complete now)."""
+    def add_work(self, worker: int, part: int, i: int, work, delay: float, src: int = 0,
+                 t_seen: float = None) -> int:
+        """Host probe completed when ``work`` finishes (None = already complete at ``t_seen``, default now)."""
         pid = self.c.add_host_probe(int(worker), int(part), int(i), float(delay))
         if work is None:
-            self.c.mark_seen(pid, self.now())
+            self.c.mark_seen(pid, self.now() if t_seen is None else float(t_seen))
         else:
             q = self._waiters.get(src)
             if q is None:

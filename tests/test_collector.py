@@ -139,3 +139,58 @@ def test_wait_seen_ignores_virtual_delay(C):
     assert col.wait_seen(0, 5.0)
     assert time.perf_counter() - t < 1.0
     assert not col.drain(0, 0.01)  # the reference Waitall still waits for the virtual arrival
+
+
+def _tied_round_order(C, seed, rnd, W=8):
+    c = C.Collector(W, list(range(W)), W)
+    c.set_tie_seed(seed)
+    t0 = C.Collector.now()
+    c.begin_round(rnd, t0, RULE_ALL, 0)
+    for w in range(W):
+        c.mark_seen(c.add_host_probe(w, 0, rnd, 0.0), t0)  # all at the same instant
+    assert c.step()
+    return [a.worker for a in c.arrivals()]
+
+
+def test_simultaneous_arrivals_use_seeded_round_permutation(C):
+    orders = [_tied_round_order(C, 0, r) for r in range(12)]
+    for r, o in enumerate(orders):
+        assert sorted(o) == list(range(8))
+        keys = [C.Collector.tie_key(0, r, w) for w in o]
+        assert keys == sorted(keys)  # the documented, replayable permutation
+    assert len({tuple(o) for o in orders}) > 6  # changes from round to round
+    assert _tied_round_order(C, 0, 3) == orders[3]  # deterministic
+    assert _tied_round_order(C, -1, 3) == list(range(8))  # tie_seed < 0: worker order
+
+
+def test_agc_zero_delay_covers_every_group_across_rounds():
+    """W=8, s=2, k=6 (uneven groups {0,1,2},{3,4,5},{6,7}) with add_delay=0: the stop rule fires
+    after 6 simultaneous arrivals; with the seeded tie permutation every group, and so every
+    partition, reaches the decoded gradient in some round (worker order would drop {6,7} forever)."""
+    import numpy as np
+    import torch
+
+    from erasurehead_amd.codes import make_scheme
+    from erasurehead_amd.config import RunConfig
+    from erasurehead_amd.data.source import ArraySource
+    from erasurehead_amd.engine import Trainer
+    from erasurehead_amd.parallel.dist import DistEnv
+
+    rows, d, W = 12, 5, 8
+    rng = np.random.RandomState(0)
+    parts = [(rng.randn(rows, d), rng.choice([-1.0, 1.0], rows)) for _ in range(W)]
+    src = ArraySource(parts, (rng.randn(4, d), np.ones(4)))
+    covered = {}
+    for tie in ("permute", "worker"):
+        cfg = RunConfig(9, rows * W, d, "/tmp/eh_tie/", 0, "x", 1, 2, 0, 3, 6, 0, "AGD", num_itrs=16, seed=0,
+                        verbose=False, allow_uneven_groups=True, tie_break=tie)
+        sch = make_scheme("approx", W, 2, rows * W, 6, 0, allow_uneven=True)
+        res = Trainer(cfg, DistEnv(), src, scheme=sch).run()
+        used = set()
+        for arr in res.arrivals:
+            from erasurehead_amd.codes.schemes import Arrival
+            for (w, p) in sch.decode([Arrival(*a) for a in arr]):
+                used.add(sch.group_of[w])
+        covered[tie] = used
+    assert covered["permute"] == {0, 1, 2}
+    assert covered["worker"] == {0, 1}  # the degenerate order the default avoids

@@ -259,3 +259,17 @@ def test_delay_floor_with_carried_lag():
     carried = delay_floor(6, 6, stop_count=4, mean=0.01, carry=True)
     assert carried >= plain
     assert carried <= res.timeset.sum() < carried + 6 * 0.02
+
+
+def test_checkpoint_restores_cyclic_code(tmp_path):
+    """A resumed cyclic-MDS run decodes with the checkpoint's B, not a freshly drawn one."""
+    ck = str(tmp_path / "ck.pt")
+    cfg, src, sch, parts = make(CASES[1], "AGD", checkpoint_every=3, checkpoint_path=ck)
+    tr = Trainer(cfg, DistEnv(), src)  # B drawn from cfg.seed
+    tr.run()
+    st = torch.load(ck, weights_only=True)
+    np.testing.assert_array_equal(st["B"].numpy(), tr.scheme.B)
+    cfg2, src2, _, _ = make(CASES[1], "AGD", resume=ck)
+    cfg2.seed = None  # unseeded: without the checkpoint's B a new random code would be drawn
+    tr2 = Trainer(cfg2, DistEnv(), src2)
+    np.testing.assert_array_equal(tr2.scheme.B, tr.scheme.B)
