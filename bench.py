@@ -2,22 +2,40 @@
 
 Metric (BASELINE.json): "wall-clock sec/iter + iters-to-loss-floor, logistic regression
 n_stragglers=2, 1/2/4/8 MI355X".  One *step* = one full training round of approximate
-gradient coding: master sends beta to every worker rank over RCCL p2p, every logical
-worker computes its (s+1)-replicated gradient with the fused HIP kernel, the master waits
-for the stop rule (k = num_collect arrivals or every FRC group covered), decodes, runs
-the fused combine+AGD update and drains the straggler tail (ref approximate_coding.py).
-The problem is fixed (1e6 x 1e3, W = 8 logical workers) and spread over N GPUs:
-strong scaling.  W % (s+1) != 0 for W=8, s=2, so the FRC groups are {0,1,2},{3,4,5},{6,7}
-(--allow-uneven-groups extension; the reference would refuse this config).
+gradient coding: the master pushes beta to every worker rank (IPC mailbox over xGMI),
+every logical worker computes its (s+1)-replicated gradient with the fused HIP kernel,
+the master waits for the stop rule (k = num_collect arrivals or every FRC group covered),
+decodes, runs the fused combine+AGD update and drains the straggler tail
+(ref src/approximate_coding.py:136-207).  The problem is fixed (1e6 x 1e3, W = 8 logical
+workers) and spread over N GPUs: strong scaling.  W % (s+1) != 0 for W=8, s=2, so the FRC
+groups are {0,1,2},{3,4,5},{6,7} (--allow-uneven-groups extension; the reference would
+refuse this config, ref src/approximate_coding.py:25-27).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]   (N>1: launched by torchrun)
-Prints ONE JSON line on rank 0.
+Launch (ref run_approx_coding.sh:47-49 starts every rank from one mpirun command):
+  python bench.py --gpus N ...        N > 1 without torchrun: relaunches itself under
+                                      torch.distributed.run --nproc-per-node N (before any
+                                      GPU call) and exits with its status
+  torchrun --nproc-per-node N bench.py --gpus N ...   used as is; WORLD_SIZE must equal N
+
+Reported on rank 0 as ONE JSON line:
+  value / ms_per_step     timed rounds (barrier + device sync on both sides, MAX over ranks)
+  host_driven_ms_per_step the same rounds driven by the host collector's real wait-for-k
+                          path (HIP-event instrumented run; equals the headline path at N > 1)
+  hbm_distinct_TBps       distinct X bytes rank 0 streams per round / round time
+  fraction_of_rows_used_in_decode   mean over rounds of the training rows whose partitions
+                          reach the decoded gradient (AGC < 1; exact codes = 1)
+  iters_to_loss_floor     rounds until the AGC training loss reaches the COMMON target
+                          loss_target = naive (exact, uncoded GD) 100-round loss + 1 %
+  ranks                   per-rank breakdown: hosted workers, transport, kernel / put /
+                          wait / decode+update microseconds (Trainer.rank_report)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,7 +44,7 @@ import numpy as np
 METRIC = "wall-clock sec/iter + iters-to-loss-floor, logistic regression n_stragglers=2, 1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -41,52 +59,88 @@ def parse():
     ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32", "bf16"])
     ap.add_argument("--update-rule", default="AGD")
     ap.add_argument("--add-delay", type=int, default=0)
-    ap.add_argument("--no-floor", action="store_true", help="skip the 100-round iters-to-loss-floor run")
+    ap.add_argument("--no-floor", action="store_true", help="skip the 100-round convergence runs")
+    ap.add_argument("--no-breakdown", action="store_true", help="skip the instrumented host-driven run")
     ap.add_argument("--floor-rounds", type=int, default=100)
     ap.add_argument("--tasks", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl"])
     ap.add_argument("--round-timeout", type=float, default=120.0, help="bounds any hang (a round takes ms)")
     ap.add_argument("--device-loop", default="auto", choices=["auto", "graph", "stream", "off"])
+    ap.add_argument("--tie-break", default="permute", choices=["permute", "worker"])
     ap.add_argument("--share-partitions", action="store_true",
                     help="co-located workers stream each distinct partition once (not the headline)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def main() -> int:
-    a = parse()
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch(gpus: int, argv) -> int:
+    """Start N ranks of this script under torch.distributed.run as a CHILD process (never exec:
+    nothing here has touched the GPU, and the children own it) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    print(f"[bench] launching {gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return relaunch(a.gpus, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"error: --gpus {a.gpus} but WORLD_SIZE={world}: the measurement would not be the one "
+              f"labelled; launch with --nproc-per-node {a.gpus} or drop torchrun", file=sys.stderr)
+        return 2
+
     import torch
 
+    from erasurehead_amd.codes.schemes import Arrival
     from erasurehead_amd.config import RunConfig
     from erasurehead_amd.engine import Trainer, evaluate
     from erasurehead_amd.parallel.dist import init_distributed
 
     env = init_distributed("auto")
-    if env.world != a.gpus and env.is_master:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={env.world}", file=sys.stderr)
 
-    def make_cfg(rounds: int) -> RunConfig:
+    def make_cfg(rounds: int, naive: bool = a.naive, **kw) -> RunConfig:
         return RunConfig(a.workers + 1, a.n_rows, a.n_cols, "/tmp/erasurehead_bench/", 0, "synthetic",
-                         0 if a.naive else 1,
+                         0 if naive else 1,
                          a.stragglers, 0, a.coded_ver, a.num_collect, a.add_delay, a.update_rule,
                          num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234, seed=0,
                          allow_uneven_groups=True, verbose=False, tasks=a.tasks,
                          transport=a.transport, round_timeout=a.round_timeout,
-                         share_partitions=a.share_partitions, device_loop=a.device_loop)
+                         share_partitions=a.share_partitions, device_loop=kw.pop("device_loop", a.device_loop),
+                         tie_break=a.tie_break, **kw)
 
+    def free(tr):
+        tr.close()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+
+    # ---- 1. headline: timed rounds --------------------------------------------------------------
     t_setup = time.perf_counter()
     trainer = Trainer(make_cfg(a.warmup + a.steps), env)
     setup_s = time.perf_counter() - t_setup
     res = trainer.run(timed_start=a.warmup)
-    # timed region: barrier + device sync on both sides on every rank; MAX over ranks
     mine = res.timed_seconds if env.is_master else trainer.worker_timed_seconds
     timed = env.allreduce_max(mine)
-    transport = trainer.transport
+    sch = trainer.scheme
     out = {}
     if env.is_master:
         sec_per_iter = timed / a.steps
         ts = res.timeset[a.warmup:]
         lt = res.loop_time[a.warmup:]
+        n_gpu_dev = torch.cuda.device_count() if torch.cuda.is_available() else 0
         out = {
             "metric": METRIC,
             "value": sec_per_iter,
@@ -110,20 +164,24 @@ def main() -> int:
                 "n_rows": a.n_rows, "n_cols": a.n_cols, "workers": a.workers,
                 "n_stragglers": a.stragglers, "num_collect": a.num_collect, "add_delay": a.add_delay,
                 "update_rule": a.update_rule,
-                "parallelism": f"ps-master + {a.workers} logical workers on {env.world} GPU(s) (dp{env.world})",
-                "transport": transport,
+                "parallelism": f"ps-master + {a.workers} logical workers on {env.world} GPU rank(s) (dp{env.world})",
+                "transport": trainer.transport,
+                "tie_break": a.tie_break,
             },
             "time_to_decode_ms_median": float(1e3 * np.median(ts)),
             "loop_ms_median": float(1e3 * np.median(lt)),
-            # X bytes the rank-0 messages read per round (replicas counted each time) and the bytes of
-            # the distinct partitions behind them; co-located replicas share reads through L2
+            # X bytes rank 0's messages read per round (replicas counted each time) and the distinct
+            # partitions behind them; co-located replicas share those reads (LDS-staged bundles)
             "x_message_bytes_per_step_rank0": int(getattr(trainer.plan, "bytes_per_round", 0)) or None,
             "x_distinct_bytes_rank0": int(getattr(trainer.plan, "distinct_bytes", 0)) or None,
             "setup_s": setup_s,
             "phases_us": {k: round(v["mean_us"], 1) for k, v in res.phases.items()},
+            "placement": {str(r): [int(w) for w in ws] for r, ws in sorted(trainer.by_rank.items())},
         }
+        if n_gpu_dev and env.world > n_gpu_dev:
+            out["config"]["ranks_per_gpu"] = env.world / n_gpu_dev  # rehearsal: ranks time-share GPUs
         out["config"]["round_loop"] = {"graph": "device-driven, hipGraph", "stream": "device-driven"}.get(
-            trainer.device_loop, "host-driven (native pump)")
+            trainer.device_loop, "host-driven (native pump)" if trainer.native_loop else "host-driven (python)")
         if a.share_partitions:
             out["config"]["share_partitions"] = True
         ref = _ref_cpu_equiv()
@@ -133,33 +191,66 @@ def main() -> int:
             # BASELINE.md publishes no sec/iter, so vs_baseline stays null
             out["ref_cpu_equiv_s_per_iter"] = ref["sec_per_iter_lower_bound"]
             out["speedup_vs_ref_cpu_equiv"] = ref["sec_per_iter_lower_bound"] / sec_per_iter
-        bpr = out["x_message_bytes_per_step_rank0"]
-        if bpr:
-            out["rank0_message_rows_GBps"] = bpr / sec_per_iter / 1e9
         if out["x_distinct_bytes_rank0"]:
-            out["rank0_distinct_rows_GBps"] = out["x_distinct_bytes_rank0"] / sec_per_iter / 1e9
-    # convergence: iterations to the training-loss floor (100-round run, evaluated with the MFMA eval kernel)
-    trainer.close()
-    if not a.no_floor:
-        del trainer
-        if torch.cuda.is_available():
-            torch.cuda.empty_cache()
-        tr2 = Trainer(make_cfg(a.floor_rounds), env)
-        r2 = tr2.run()
-        tr2.close()
+            out["hbm_distinct_TBps"] = out["x_distinct_bytes_rank0"] / sec_per_iter / 1e12
+        out["fraction_of_rows_used_in_decode"] = decode_row_fraction(sch, res.arrivals[a.warmup:], Arrival)
+    reports = env.gather_objects(trainer.rank_report())
+    kernel_iso = trainer.time_local_grad() if trainer.local_msgs else None
+    kernel_iso = env.gather_objects(kernel_iso)
+    free(trainer)
+    del trainer, res
+
+    # ---- 2. the same rounds host-driven, instrumented: real wait-for-k path + per-rank breakdown -----
+    if not a.no_breakdown:
+        tr = Trainer(make_cfg(a.warmup + a.steps, device_loop="off", instrument=True), env)
+        r = tr.run(timed_start=a.warmup)
+        t = env.allreduce_max(r.timed_seconds if env.is_master else tr.worker_timed_seconds)
+        reports = env.gather_objects(tr.rank_report())
         if env.is_master:
-            tr2.cfg.fix_quirks = True  # evaluate on all partitions
-            torch.cuda.synchronize() if torch.cuda.is_available() else None
-            t_ev = time.perf_counter()
-            ev = evaluate(tr2, r2, write=False)
-            out["eval_s"] = time.perf_counter() - t_ev  # 100 betas x (train 1e6 + test 2e5 rows): MFMA GEMM + AUC
+            out["host_driven_ms_per_step"] = 1e3 * t / a.steps
+            out["host_driven_instrumented"] = True
+        free(tr)
+        del tr, r
+    if env.is_master:
+        for rep, k in zip(reports, kernel_iso):
+            if k is not None:
+                rep["kernel_us_isolated"] = round(k, 1)
+        out["ranks"] = reports
+
+    # ---- 3. convergence: naive (exact GD) sets the common loss target, then the scheme -------------
+    if not a.no_floor:
+        curves = {}
+        for name, naive in (("naive", True), ("scheme", a.naive)):
+            if name == "scheme" and a.naive:
+                curves["scheme"] = curves["naive"]
+                continue
+            tr2 = Trainer(make_cfg(a.floor_rounds, naive=naive), env)
+            r2 = tr2.run()
+            free(tr2)
+            if env.is_master:
+                tr2.cfg.fix_quirks = True  # evaluate on every partition
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
+                t_ev = time.perf_counter()
+                ev = evaluate(tr2, r2, write=False)
+                curves[name] = (ev, r2, time.perf_counter() - t_ev)
+            del tr2, r2
+        if env.is_master:
+            ev_n, r_n, _ = curves["naive"]
+            ev, r2, eval_s = curves["scheme"]
+            target = float(ev_n.training_loss[-1]) * 1.01
             tl = ev.training_loss
-            floor = float(np.min(tl))
-            thr = floor + 0.01 * abs(floor)
-            it = int(np.argmax(tl <= thr))
-            out["iters_to_loss_floor"] = it
-            out["loss_floor"] = floor
+            hit = np.nonzero(tl <= target)[0]
+            hit_n = np.nonzero(ev_n.training_loss <= target)[0]
+            out["eval_s"] = eval_s  # 100 betas x (train 1e6 + test 2e5 rows): MFMA GEMM + AUC
+            out["loss_target"] = target
+            out["loss_target_definition"] = "naive (exact uncoded GD) training loss after %d rounds + 1%%" % (
+                a.floor_rounds)
+            out["iters_to_loss_floor"] = int(hit[0]) + 1 if hit.size else None
+            out["naive_iters_to_loss_floor"] = int(hit_n[0]) + 1 if hit_n.size else None
+            out["seconds_to_loss_floor"] = float(np.sum(r2.loop_time[: hit[0] + 1])) if hit.size else None
             out["final_train_loss"] = float(tl[-1])
+            out["naive_final_train_loss"] = float(ev_n.training_loss[-1])
             out["final_test_auc"] = float(ev.auc[-1])
             out["floor_run_wallclock_s"] = float(r2.total_time)
     env.barrier()
@@ -171,6 +262,20 @@ def main() -> int:
                 f.write(line + "\n")
     env.shutdown()
     return 0
+
+
+def decode_row_fraction(scheme, arrivals_log, Arrival) -> float:
+    """Mean over rounds of the fraction of partitions (= of training rows: equal-sized partitions)
+    that reach the decoded gradient.  AGC covers fewer groups than it has (ref
+    src/approximate_coding.py:144-158); exact codes always cover everything."""
+    seg = {(m.worker, m.part): [p for p, _ in m.segments] for m in scheme.messages}
+    n = scheme.n_partition_files
+    fr = []
+    for arr in arrivals_log:
+        used = scheme.decode([Arrival(*x) for x in arr])
+        parts = {p for key in used for p in seg[key]}
+        fr.append(len(parts) / n)
+    return float(np.mean(fr)) if fr else None
 
 
 def _ref_cpu_equiv():

@@ -23,6 +23,7 @@
 #include <pybind11/stl.h>
 #include <torch/extension.h>
 
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -291,6 +292,28 @@ class MasterPump {
       if (p.first) hipEventDestroy(p.first);
       if (p.second) hipEventDestroy(p.second);
     }
+    for (auto& t : tev_)
+      for (auto e : t)
+        if (e) hipEventDestroy(e);
+  }
+
+  // Per-round HIP-event timing of the beta puts and the local gradient launch (bench.py's
+  // per-rank breakdown); off by default: each record costs the host about a microsecond.
+  void set_timing(bool on) {
+    timing_ = on;
+    if (on && tev_.empty()) tev_.assign(R_, {nullptr, nullptr, nullptr, nullptr});
+  }
+  // (put_ms [R], kernel_ms [R]); -1 where a round was not timed.  Syncs the stream.
+  std::pair<std::vector<double>, std::vector<double>> timing_ms() {
+    hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    std::vector<double> put(R_, -1.0), ker(R_, -1.0);
+    for (int i = 0; i < (int)tev_.size(); ++i) {
+      const auto& t = tev_[i];
+      float ms = 0.f;
+      if (t[0] && t[1] && hipEventElapsedTime(&ms, t[0], t[1]) == hipSuccess) put[i] = ms;
+      if (t[2] && t[3] && hipEventElapsedTime(&ms, t[2], t[3]) == hipSuccess) ker[i] = ms;
+    }
+    return {put, ker};
   }
 
   void set_state(const Tensor& beta, const Tensor& u, const Tensor& hist, const Tensor& beta_in) {
@@ -399,6 +422,7 @@ class MasterPump {
     t_start_[i] = t;
     char* bin = static_cast<char*>(beta_in_.data_ptr());
     const void* src = bin + static_cast<int64_t>(i) * ld_ * es_;
+    if (timing_ && !targets_.empty()) record_t(i, 0);
     // push beta(i) into every worker inbox
     for (size_t k0 = 0; k0 < targets_.size(); k0 += eh::kMaxPuts) {
       eh::PutArgs a{};
@@ -413,10 +437,13 @@ class MasterPump {
       }
       hcheck(eh::put_signal_launch(a, blocks_for(static_cast<long long>(ld_) * es_), stream_), "put_signal(beta)");
     }
+    if (timing_ && !targets_.empty()) record_t(i, 1);
     const double* dl = delays_.data() + static_cast<int64_t>(i) * W_;
     if (n_loc_ > 0 && launcher_) {
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
+      if (timing_) record_t(i, 2);
       hcheck(launcher_->launch(src, g, stream_), "local gradient");
+      if (timing_) record_t(i, 3);
       hcheck(hipEventRecord(loc_ev_[slot], stream_), "hipEventRecord");
       for (const auto& m : local_)
         col_->add_event_probe(m.w, m.p, i, reinterpret_cast<uintptr_t>(loc_ev_[slot]), dl[m.w]);
@@ -598,6 +625,12 @@ class MasterPump {
 
   void check_wp(int w, int p) const { need(w >= 0 && w < W_ && (p == 0 || p == 1), "bad (worker, part)"); }
 
+  void record_t(int i, int which) {
+    hipEvent_t& e = tev_[i][which];
+    if (!e) hcheck(hipEventCreate(&e), "hipEventCreate");
+    hcheck(hipEventRecord(e, stream_), "hipEventRecord");
+  }
+
   static int blocks_for(long long bytes) {
     const long long v = bytes / 16;
     return (int)std::max<long long>(1, std::min<long long>(64, (v + 4095) / 4096));
@@ -714,6 +747,8 @@ class MasterPump {
   hipStream_t dev_stream_ = nullptr;     // stream of the device-driven rounds (capturable)
   hipEvent_t join_ev_ = nullptr;
   int graph_segments_ = 0;
+  bool timing_ = false;
+  std::vector<std::array<hipEvent_t, 4>> tev_;  // [round] put start/end, gradient start/end
 };
 
 // ------------------------------------------------------------------------- WorkerPump
@@ -738,6 +773,29 @@ class WorkerPump {
     es_ = acc_code(G) == 0 ? 8 : 4;
     g_rows_ = (int)G.size(1);
     stream_ = c10::hip::getCurrentHIPStream(device).stream();
+    wait_s_.assign(R_, -1.0);
+  }
+  ~WorkerPump() {
+    for (auto& t : tev_)
+      for (auto e : t)
+        if (e) hipEventDestroy(e);
+  }
+
+  void set_timing(bool on) {
+    timing_ = on;
+    if (on && tev_.empty()) tev_.assign(R_, {nullptr, nullptr, nullptr});
+  }
+  // (beta_wait_s [R], kernel_ms [R], put_ms [R]); -1 where a round was not timed.  Syncs the stream.
+  std::tuple<std::vector<double>, std::vector<double>, std::vector<double>> timing() {
+    hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    std::vector<double> ker(R_, -1.0), put(R_, -1.0);
+    for (int i = 0; i < (int)tev_.size(); ++i) {
+      const auto& t = tev_[i];
+      float ms = 0.f;
+      if (t[0] && t[1] && hipEventElapsedTime(&ms, t[0], t[1]) == hipSuccess) ker[i] = ms;
+      if (t[1] && t[2] && hipEventElapsedTime(&ms, t[1], t[2]) == hipSuccess) put[i] = ms;
+    }
+    return {wait_s_, ker, put};
   }
 
   // Rounds [a, b).  Returns -1 when every round was issued, else the round whose beta
@@ -759,11 +817,14 @@ class WorkerPump {
         if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_) return i;
         std::this_thread::sleep_for(std::chrono::microseconds(5));
       }
+      wait_s_[i] = std::chrono::duration<double>(clk::now() - t0).count();
       if (n_ == 0) continue;
       const int slot = i % K_;
       const char* beta = static_cast<const char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * ld_ * es_;
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
+      if (timing_) record_t(i, 0);
       hcheck(g_->launch(beta, g, stream_), "worker gradient");
+      if (timing_) record_t(i, 1);
       eh::PutArgs pa{};
       pa.n = 1;
       const long long bytes = static_cast<long long>(n_) * ld_ * es_;
@@ -772,11 +833,18 @@ class WorkerPump {
                             reinterpret_cast<unsigned int*>(counters_.data_ptr<int>())};
       const int blocks = (int)std::max<long long>(1, std::min<long long>(64, (bytes / 16 + 4095) / 4096));
       hcheck(eh::put_signal_launch(pa, blocks, stream_), "put_signal(messages)");
+      if (timing_) record_t(i, 2);
     }
     return -1;
   }
 
  private:
+  void record_t(int i, int which) {
+    hipEvent_t& e = tev_[i][which];
+    if (!e) hcheck(hipEventCreate(&e), "hipEventCreate");
+    hcheck(hipEventRecord(e, stream_), "hipEventRecord");
+  }
+
   std::shared_ptr<GradLauncher> g_;
   Tensor inbox_, G_;
   int n_;
@@ -789,6 +857,9 @@ class WorkerPump {
   double timeout_;
   int ld_ = 0, R_ = 0, es_ = 8, g_rows_ = 1;
   hipStream_t stream_ = nullptr;
+  bool timing_ = false;
+  std::vector<std::array<hipEvent_t, 3>> tev_;  // [round] gradient start, gradient end = put start, put end
+  std::vector<double> wait_s_;                  // [round] host seconds spent waiting for beta
 };
 
 }  // namespace
@@ -843,10 +914,14 @@ void bind_engine(py::module& m) {
       .def("update_ms", &MasterPump::update_ms)
       .def("run_local", &MasterPump::run_local, py::arg("a"), py::arg("b"), py::arg("graph"), py::arg("stamps"))
       .def("stamp_hz", &MasterPump::stamp_hz)
+      .def("set_timing", &MasterPump::set_timing)
+      .def("timing_ms", &MasterPump::timing_ms)
       .def("graphs_launched", &MasterPump::graphs_launched);
   py::class_<WorkerPump>(m, "WorkerPump")
       .def(py::init<std::shared_ptr<GradLauncher>, const Tensor&, const Tensor&, int, uintptr_t, int, int, uintptr_t,
                     uintptr_t, const Tensor&, int, int, double>())
-      .def("run", &WorkerPump::run);
+      .def("run", &WorkerPump::run)
+      .def("set_timing", &WorkerPump::set_timing)
+      .def("timing", &WorkerPump::timing);
 }
 }  // namespace eh

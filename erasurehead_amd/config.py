@@ -78,6 +78,7 @@ class RunConfig:
     # tie model); "worker" keeps worker-id order (AGC then stops on the same k workers every round)
     tie_break: str = "permute"
     tie_seed: int = 0
+    instrument: bool = False  # per-round HIP-event timing of puts / gradient launches (Trainer.rank_report)
 
     def __post_init__(self):
         self.update_rule = str(self.update_rule)

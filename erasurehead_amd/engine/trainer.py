@@ -73,6 +73,12 @@ class TrainResult:
     arrivals: List[List[Tuple[int, int, float]]] = field(default_factory=list)
 
 
+def _mean_us(ms, a0: int = 0) -> Optional[float]:
+    """Mean (microseconds) of the non-negative millisecond entries from round a0 on; None if none."""
+    v = [x for x in list(ms)[a0:] if x is not None and x >= 0]
+    return 1e3 * float(np.mean(v)) if v else None
+
+
 class Trainer:
     def __init__(self, cfg: RunConfig, env: Optional[DistEnv] = None, source: Optional[DataSource] = None,
                  scheme: Optional[Scheme] = None):
@@ -84,6 +90,7 @@ class Trainer:
         self.env = env
         self.timer = PhaseTimer()
         self.device_loop: Optional[str] = None  # set by the native master loop when rounds ran device-driven
+        self.rank_stats: Dict[str, float] = {}  # per-rank breakdown of the last run (rank_report)
         self._setup_scheme(scheme, source)
         self._setup_data(source)
         self._setup_buffers()
@@ -247,6 +254,27 @@ class Trainer:
             self.plan.run(beta, self.G[0])
         self._sync()
 
+    def time_local_grad(self, reps: int = 5) -> Optional[float]:
+        """Mean microseconds of this rank's gradient launch run on its own (no transport, no
+        other rank's traffic); HIP events on a GPU, host time on the CPU."""
+        if not self.local_msgs:
+            return None
+        beta = torch.zeros(self.ld, dtype=self.prec.acc, device=self.env.device)
+        beta[: self.d] = 1e-3
+        self.plan.run(beta, self.G[0])
+        if self.env.gpu:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                self.plan.run(beta, self.G[0])
+            e1.record()
+            e1.synchronize()
+            return 1e3 * e0.elapsed_time(e1) / reps
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            self.plan.run(beta, self.G[0])
+        return 1e6 * (time.perf_counter() - t0) / reps
+
     # ------------------------------------------------------------------------------ run
     def run(self, timed_start: Optional[int] = None, log=None) -> Optional[TrainResult]:
         """Train for cfg.num_itrs rounds; returns the master's TrainResult (None on workers).
@@ -391,12 +419,35 @@ class Trainer:
         self._sync()
         env.barrier()
         total = time.perf_counter() - orig_start
+        a0 = (timed_start or start) - start
+        self.rank_stats.update({f"{k}_us": float(1e6 * np.mean(v[a0:])) for k, v in self.timer.t.items()
+                                if len(v) > a0})
         res = TrainResult(self.key, self.hist[:, : self.d].double().cpu().numpy(), timeset, worker_timeset, loop_time,
                           total, timeouts=timeouts, phases=self.timer.summary(), arrivals=arrivals_log)
         if t_timed0 is not None:
             res.timed_seconds = t_timed1 - t_timed0
             res.timed_rounds = R - timed_start
         return res
+
+    def rank_report(self) -> Dict[str, object]:
+        """This rank's share of the job and where its round time went (bench.py per-rank breakdown).
+
+        Times are means over the timed rounds, in microseconds: ``kernel_us`` the local gradient
+        launch (HIP events; cfg.instrument), ``beta_put_us`` / ``msg_put_us`` the put+signal
+        launches, ``beta_wait_us`` a worker's host wait for beta, ``wait_k_us`` the master's wait
+        for the stop rule, ``decode_update_us`` its host decode + combine/update enqueue and
+        ``update_kernel_us`` the combine+update kernel itself.
+        """
+        env = self.env
+        role = ("master+workers" if self.local_msgs else "master") if env.is_master else "workers"
+        rep: Dict[str, object] = {"rank": env.rank, "role": role, "device": str(env.device),
+                                  "transport": self.transport,
+                                  "round_loop": self.device_loop or ("native pump" if self.native_loop else "python"),
+                                  "workers": sorted({int(m.worker) for m in self.local_msgs}),
+                                  "messages": len(self.local_msgs),
+                                  "partitions": len({p for m in self.local_msgs for p, _ in m.segments})}
+        rep.update({k: round(float(v), 2) for k, v in self.rank_stats.items() if v is not None})
+        return rep
 
     def _master_loop_native(self, timed_start, log, start: int = 0) -> TrainResult:
         """Master rounds in csrc/runtime/engine.cpp (MasterPump); Python only keeps the books."""
@@ -423,6 +474,7 @@ class Trainer:
                           co[0][4] if co else 0, [float(x) for x in delay_table.ravel()], self.rule_kind,
                           self.rule_k, bool(self.drain))
         pump.set_decode(sch.decode_kind, list(sch.group_of), sch.n_groups)
+        pump.set_timing(bool(cfg.instrument))
         table_decoded = sch.decode_kind in (3, 4)
         if table_decoded and math.comb(W, sch.n_stragglers) <= 20000:  # else filled on demand below
             for mask, a in sch.decode_table().items():
@@ -502,6 +554,13 @@ class Trainer:
         upd = pump.update_ms()
         if not device_mode:
             timeset[start:] += 1e-3 * np.asarray(upd[start:])
+        a0 = timed_start if timed_start is not None else start
+        if cfg.instrument:
+            put_ms, ker_ms = pump.timing_ms()
+            self.rank_stats.update(beta_put_us=_mean_us(put_ms, a0), kernel_us=_mean_us(ker_ms, a0))
+        self.rank_stats.update(update_kernel_us=_mean_us(upd, a0),
+                               **{f"{k}_us": float(1e6 * np.mean(v[a0 - start:]))
+                                  for k, v in self.timer.t.items() if len(v) > a0 - start})
         col.close()
         if timed_start is not None:
             t_timed1 = self._timed_fence()
@@ -543,6 +602,7 @@ class Trainer:
         pump = C.WorkerPump(self.plan.native_launcher(), tx.inbox, self.G, self.n_loc, tx.rremote.ptr,
                             tx.mbox_rows, tx.my_row0, tx.flags.host_addr(env.rank), tx.flags.dev_addr(w + env.rank),
                             tx.counters, K, dev, float(cfg.round_timeout))
+        pump.set_timing(bool(cfg.instrument))
         cut = timed_start if timed_start is not None and start <= timed_start < R else None
         segments = [(start, cut), (cut, R)] if cut is not None else [(start, R)]
         t0 = None
@@ -556,6 +616,11 @@ class Trainer:
         if timed_start is not None:
             self.worker_timed_seconds = self._timed_fence() - (t0 if t0 is not None else time.perf_counter())
         self._sync()
+        a0 = cut if cut is not None else start
+        wait_s, ker_ms, put_ms = pump.timing()
+        self.rank_stats.update(beta_wait_us=_mean_us([1e3 * x if x >= 0 else -1.0 for x in wait_s], a0))
+        if cfg.instrument:
+            self.rank_stats.update(kernel_us=_mean_us(ker_ms, a0), msg_put_us=_mean_us(put_ms, a0))
         env.barrier()
         del pump
         return None
@@ -590,12 +655,15 @@ class Trainer:
             if timed_start is not None and i == timed_start:
                 t0 = self._timed_fence()
             slot = i % K
-            b = tx.recv_beta(i)
+            with self.timer.phase("recv_beta"):
+                b = tx.recv_beta(i)
             if bsum is not None:
                 bsum[i, 0] = b.double().sum()
             if n:
-                self.plan.run(b, self.G[slot])
-                tx.send_msgs(i, self.G[slot, :n])
+                with self.timer.phase("local_grad"):
+                    self.plan.run(b, self.G[slot])
+                with self.timer.phase("send_msgs"):
+                    tx.send_msgs(i, self.G[slot, :n])
             if bsum is not None:  # beta must be unchanged after the gradient read it
                 bsum[i, 1] = b.double().sum()
         tx.finish()
@@ -603,6 +671,9 @@ class Trainer:
             env.gather_objects(bsum.cpu().numpy())
         if timed_start is not None:
             self.worker_timed_seconds = self._timed_fence() - t0
+        a0 = (timed_start or 0) - start
+        self.rank_stats.update({f"{k}_us": float(1e6 * np.mean(v[a0:])) for k, v in self.timer.t.items()
+                                if len(v) > a0})
         self._sync()
         env.barrier()
         return None

@@ -1,0 +1,49 @@
+"""bench.py launch contract: `python bench.py --gpus N` measures N ranks from one plain command
+(ref run_approx_coding.sh:47-49 starts every rank with one mpirun), and a WORLD_SIZE that
+disagrees with --gpus is an error, never a silently mislabelled measurement."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = ["--steps", "3", "--warmup", "1", "--n-rows", "2400", "--n-cols", "20", "--floor-rounds", "8"]
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["CUDA_VISIBLE_DEVICES"] = ""  # CPU / gloo ranks
+    env["HIP_VISIBLE_DEVICES"] = ""
+    return env
+
+
+def test_bench_gpus3_relaunches_three_ranks(tmp_path):
+    out = tmp_path / "b.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", *TINY, "--json-out", str(out)],
+                       cwd=str(tmp_path), env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["n_gpus"] == 3
+    assert [x["rank"] for x in d["ranks"]] == [0, 1, 2]
+    assert d["ranks"][0]["role"].startswith("master")
+    hosted = sorted(w for x in d["ranks"] for w in x["workers"])
+    assert hosted == list(range(8))  # every logical worker placed exactly once
+    assert sorted(int(w) for ws in d["placement"].values() for w in ws) == list(range(8))
+    for x in d["ranks"]:
+        assert x["transport"] == "gloo"
+        assert x["local_grad_us"] > 0
+    assert d["ranks"][1]["recv_beta_us"] >= 0
+    assert 0 < d["fraction_of_rows_used_in_decode"] <= 1
+    assert d["host_driven_ms_per_step"] > 0
+    assert d["loss_target"] > 0 and d["naive_iters_to_loss_floor"] is not None
+
+
+def test_bench_world_size_mismatch_fails(tmp_path):
+    env = _env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *TINY, "--no-floor"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=1" in r.stderr
