@@ -86,7 +86,6 @@ def relaunch(gpus: int, argv) -> int:
            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    env.setdefault("OMP_NUM_THREADS", "4")
     print(f"[bench] launching {gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
     return subprocess.call(cmd, env=env)
 
