@@ -175,7 +175,12 @@ def main(argv=None) -> int:
             "x_distinct_bytes_rank0": int(getattr(trainer.plan, "distinct_bytes", 0)) or None,
             "setup_s": setup_s,
             "phases_us": {k: round(v["mean_us"], 1) for k, v in res.phases.items()},
-            "placement": {str(r): [int(w) for w in ws] for r, ws in sorted(trainer.by_rank.items())},
+            # rank -> the (worker, partition) shards it computes ("w3" = worker 3's whole message)
+            "placement": {str(r): [f"w{u.worker}" + (f":p{u.segments[0][0]}" if u.n_shards > 1 else "")
+                                   + (":part1" if u.part else "")
+                                   for u, o in zip(trainer.shards, trainer.owner) if o == r]
+                          for r in range(env.world)},
+            "shard": trainer.shard_mode,
         }
         if n_gpu_dev and env.world > n_gpu_dev:
             out["config"]["ranks_per_gpu"] = env.world / n_gpu_dev  # rehearsal: ranks time-share GPUs

@@ -27,6 +27,14 @@ Collector::Collector(int n_workers, std::vector<int> group_of, int n_groups)
   got0_.assign(W_, 0);
   got1_.assign(W_, 0);
   group_done_.assign(std::max(n_groups_, 1), 0);
+  nsh_.assign(2 * W_, 1);
+  got_sh_.assign(2 * W_, 0);
+}
+
+void Collector::set_shards(int worker, int part, int n) {
+  if (worker < 0 || worker >= W_ || part < 0 || part > 1 || n < 1)
+    throw std::invalid_argument("Collector::set_shards: bad (worker, part, n)");
+  nsh_[2 * worker + part] = n;
 }
 
 uint64_t Collector::tie_key(int64_t seed, int round, int worker) {
@@ -60,6 +68,7 @@ void Collector::begin_round(int round, double t_start, int rule, int k) {
   std::fill(got1_.begin(), got1_.end(), 0);
   std::fill(group_done_.begin(), group_done_.end(), 0);
   cnt0_ = cnt1_ = cnt_groups_ = 0;
+  std::fill(got_sh_.begin(), got_sh_.end(), 0);
   tie_.assign(W_, 0);
   if (tie_seed_ >= 0)
     for (int w = 0; w < W_; ++w) tie_[w] = tie_key(tie_seed_, round, w);
@@ -170,6 +179,8 @@ bool Collector::process_ready(double t, bool /*stop_at_rule*/) {
     p.arrived = true;
     const Arrival a{p.worker, p.part, p.round, p.ready - round_start_[p.round], id};
     if (p.round != round_) continue;  // stale message of an earlier round: drained, ignored
+    const int mi = 2 * p.worker + (p.part ? 1 : 0);
+    if (++got_sh_[mi] < nsh_[mi]) continue;  // more shards of this message still to come
     if (stopped_) {
       late_.push_back(a);
       continue;

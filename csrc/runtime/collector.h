@@ -23,6 +23,11 @@
 // hardware stays busy.  delay = +inf models a dead worker (an erasure that never
 // arrives; bounded by the round timeout instead of hanging like the reference).
 //
+// Shards: with partition sharding (engine/trainer.py) one logical message (worker, part) is
+// computed as n shards on possibly different ranks (one per partition it reads) and the master
+// sums them.  The message arrives when its LAST shard is ready; its arrival time is that
+// shard's (the max over shards, since ready probes are processed in time order).
+//
 // Tie model: messages that become ready at the same instant (every local message of one
 // process shares the gradient kernel's HIP event; with add_delay = 0 nothing separates
 // them) are ordered by a per-round permutation of the workers seeded by (tie_seed, round)
@@ -67,6 +72,8 @@ class Collector {
   int64_t tie_seed() const { return tie_seed_; }
   // Tie rank of `worker` in `round` (smaller first); the permutation any host code can replay.
   static uint64_t tie_key(int64_t seed, int round, int worker);
+  // Message (worker, part) is delivered as n >= 1 shards (probes); default 1.
+  void set_shards(int worker, int part, int n);
   int add_event_probe(int worker, int part, int round, uintptr_t event, double delay);
   int add_host_probe(int worker, int part, int round, double delay);
   // IPC mailbox probe: arrived once the 64-bit flag at `flag_addr` (shared host memory,
@@ -120,6 +127,8 @@ class Collector {
   bool stopped_ = false;
   int64_t tie_seed_ = -1;
   std::vector<uint64_t> tie_;  // [worker] tie key of the current round
+  std::vector<int> nsh_;       // [2 * worker + part] shards per message
+  std::vector<int> got_sh_;    // [2 * worker + part] shards of the current round ready so far
   std::vector<double> round_start_;
   std::vector<std::vector<double>> finish_;  // [worker][round] virtual finish
   std::vector<Probe> probes_;

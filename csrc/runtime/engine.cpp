@@ -23,6 +23,7 @@
 #include <pybind11/stl.h>
 #include <torch/extension.h>
 
+#include <algorithm>
 #include <array>
 #include <chrono>
 #include <cmath>
@@ -277,7 +278,7 @@ class MasterPump {
     upd_ev_.assign(R, {nullptr, nullptr});
     loc_ev_.assign(K, nullptr);
     for (auto& e : loc_ev_) hcheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-    index_.assign(2 * W, {-1, -1});
+    index_.assign(2 * W, {});
   }
   ~MasterPump() {
     if (dev_stream_) {
@@ -334,7 +335,8 @@ class MasterPump {
     es_ = acc_ == 0 ? 8 : 4;
   }
 
-  // local messages: row order of G ([K, n_loc, ld]); each (worker, part)
+  // local messages: row order of G ([K, n_loc, ld]); each (worker, part).  A (worker, part) may
+  // appear several times (partition shards of one message): decode sums all its rows.
   void set_local(std::shared_ptr<GradLauncher> g, const Tensor& G, const std::vector<std::pair<int, int>>& msgs) {
     need_gpu(G, "G");
     need(G.dim() == 3 && G.size(0) == K_ && G.size(2) == ld_, "G must be [K, n_loc, ld]");
@@ -345,10 +347,13 @@ class MasterPump {
     n_loc_ = (int)msgs.size();
     g_rows_ = (int)G.size(1);
     local_.clear();
+    for (auto& ix : index_)
+      ix.erase(std::remove_if(ix.begin(), ix.end(), [](const std::pair<int, int>& e) { return e.first == 0; }),
+               ix.end());
     for (int j = 0; j < n_loc_; ++j) {
       check_wp(msgs[j].first, msgs[j].second);
       local_.push_back({msgs[j].first, msgs[j].second, j, 0});
-      index_[2 * msgs[j].first + msgs[j].second] = {0, j};
+      index_[2 * msgs[j].first + msgs[j].second].push_back({0, j});
     }
   }
 
@@ -360,12 +365,15 @@ class MasterPump {
     rbuf_ = rbuf;
     r_rows_ = (int)rbuf.size(1);
     remote_.clear();
+    for (auto& ix : index_)
+      ix.erase(std::remove_if(ix.begin(), ix.end(), [](const std::pair<int, int>& e) { return e.first == 1; }),
+               ix.end());
     for (const auto& [w, p, row, addr] : msgs) {
       check_wp(w, p);
       need(row >= 0 && row < r_rows_, "mailbox row out of range");
       need(addr != 0, "null flag address");
       remote_.push_back({w, p, row, addr});
-      index_[2 * w + p] = {1, row};
+      index_[2 * w + p].push_back({1, row});
     }
   }
 
@@ -490,7 +498,7 @@ class MasterPump {
     {
       py::gil_scoped_release nogil;
       std::vector<std::pair<const void*, double>> used;
-      for (const auto& [w, p, c] : coefs) used.push_back({msg_ptr(i % K_, w, p), c});
+      for (const auto& [w, p, c] : coefs) push_msg(used, i % K_, w, p, c);
       combine(i, used);
       t_dec = eh::Collector::now();
       t_end = after_combine(i, publish_next);
@@ -636,13 +644,15 @@ class MasterPump {
     return (int)std::max<long long>(1, std::min<long long>(64, (v + 4095) / 4096));
   }
 
-  const void* msg_ptr(int slot, int w, int p) const {
+  // every buffer row (one per shard) of message (w, p) in ring slot `slot`, each with coefficient c
+  void push_msg(std::vector<std::pair<const void*, double>>& used, int slot, int w, int p, double c) const {
     const auto& ix = index_[2 * w + p];
-    if (ix.first == 0)
-      return static_cast<const char*>(G_.data_ptr()) + (static_cast<int64_t>(slot) * g_rows_ + ix.second) * ld_ * es_;
-    if (ix.first == 1)
-      return static_cast<const char*>(rbuf_.data_ptr()) + (static_cast<int64_t>(slot) * r_rows_ + ix.second) * ld_ * es_;
-    throw std::logic_error("message without a buffer");
+    if (ix.empty()) throw std::logic_error("message without a buffer");
+    for (const auto& [kind, row] : ix) {
+      const char* base = kind == 0 ? static_cast<const char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_
+                                   : static_cast<const char*>(rbuf_.data_ptr()) + static_cast<int64_t>(slot) * r_rows_ * ld_ * es_;
+      used.push_back({base + static_cast<int64_t>(row) * ld_ * es_, c});
+    }
   }
 
   bool decode(int i, const std::vector<eh::Arrival>& arr, std::vector<std::pair<const void*, double>>& used) const {
@@ -651,19 +661,19 @@ class MasterPump {
     uint64_t mask = 0;
     for (const auto& a : arr) {
       if (a.part == 1) {
-        if (decode_kind_ == kPartialFrc || decode_kind_ == kPartialTable) used.push_back({msg_ptr(slot, a.worker, 1), 1.0});
+        if (decode_kind_ == kPartialFrc || decode_kind_ == kPartialTable) push_msg(used, slot, a.worker, 1, 1.0);
         continue;
       }
       switch (decode_kind_) {
         case kSumPart0:
-          used.push_back({msg_ptr(slot, a.worker, 0), 1.0});
+          push_msg(used, slot, a.worker, 0, 1.0);
           break;
         case kFirstPerGroup:
         case kPartialFrc: {
           const int g = group_of_[a.worker];
           if (!gdone[g]) {
             gdone[g] = 1;
-            used.push_back({msg_ptr(slot, a.worker, 0), 1.0});
+            push_msg(used, slot, a.worker, 0, 1.0);
           }
           break;
         }
@@ -675,7 +685,7 @@ class MasterPump {
       auto it = table_.find(mask);
       if (it == table_.end()) return false;
       for (int w = 0; w < W_; ++w)
-        if (mask >> w & 1) used.push_back({msg_ptr(slot, w, 0), it->second[w]});
+        if (mask >> w & 1) push_msg(used, slot, w, 0, it->second[w]);
     }
     return true;
   }
@@ -731,7 +741,7 @@ class MasterPump {
   std::shared_ptr<GradLauncher> launcher_;
   int n_loc_ = 0, g_rows_ = 1, r_rows_ = 1;
   std::vector<Msg> local_, remote_;
-  std::vector<std::pair<int, int>> index_;  // [2*w+p] -> (0 local | 1 remote, row)
+  std::vector<std::vector<std::pair<int, int>>> index_;  // [2*w+p] -> (0 local | 1 remote, row) per shard
   std::vector<std::pair<uintptr_t, uintptr_t>> targets_;
   std::vector<double> decay_, gm_, l2_, theta_, delays_;
   int update_rule_ = 0, stop_rule_ = 0, k_ = 0;

@@ -64,6 +64,8 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--tie-break", default="permute", choices=["permute", "worker"],
                    help="order of simultaneous arrivals: seeded per-round worker permutation (default) or worker id")
     g.add_argument("--tie-seed", type=int, default=0)
+    g.add_argument("--shard", default="auto", choices=["auto", "message", "partition"],
+                   help="placement unit on several ranks: whole messages or partition shards (auto: shards)")
     return p
 
 
@@ -84,7 +86,7 @@ def parse(argv: List[str]):
                     full_precision_outputs=a.full_precision_outputs, evaluate=not a.no_eval, verbose=not a.quiet,
                     checkpoint_every=a.checkpoint_every, checkpoint_path=a.checkpoint_path, resume=a.resume, trace=a.trace, verify_beta=a.verify_beta,
                     transport=a.transport, share_partitions=a.share_partitions, device_loop=a.device_loop,
-                    tie_break=a.tie_break, tie_seed=a.tie_seed)
+                    tie_break=a.tie_break, tie_seed=a.tie_seed, shard=a.shard)
     return cfg, a
 
 

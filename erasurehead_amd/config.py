@@ -78,6 +78,10 @@ class RunConfig:
     # tie model); "worker" keeps worker-id order (AGC then stops on the same k workers every round)
     tie_break: str = "permute"
     tie_seed: int = 0
+    # placement unit: "message" (a logical worker's whole message on one rank), "partition" (one
+    # shard per (message, partition): each partition's replicas on one rank; parallel/placement.py)
+    # or "auto" (partition when there are several ranks)
+    shard: str = "auto"
     instrument: bool = False  # per-round HIP-event timing of puts / gradient launches (Trainer.rank_report)
 
     def __post_init__(self):

@@ -46,7 +46,7 @@ from ..ops.precision import get_precision
 from ..ops.update import combine_update
 from ..parallel.collector import ArrivalCollector
 from ..parallel.dist import DistEnv
-from ..parallel.placement import place_workers_shared, workers_by_rank
+from ..parallel.placement import make_shards, place_units, place_workers_shared
 
 # Cost of a replica's message rows whose HBM reads a co-located replica already streams, relative
 # to a distinct row (dense fp64 on MI355X with the LDS-staged bundles: (1.56 - 1.29) ms for 14 GB
@@ -129,11 +129,11 @@ class Trainer:
             mode = cfg.delay_mode if cfg.delay_mode in ("exp", "fixed") else "none"
         self.delay = DelayModel(W, mode, cfg.delay_mean, [w - 1 for w in cfg.fixed_stragglers], cfg.fixed_sleep,
                                 [w - 1 for w in cfg.kill_workers])
-        # placement: sharing-aware on GPUs (co-located replicas share HBM reads)
+        # placement: sharing-aware on GPUs (co-located replicas share HBM reads).  The placed units
+        # are whole messages, or with partition sharding (default for multi-rank runs) one shard
+        # per (message, partition): each partition's replicas then live on one rank
+        # (parallel/placement.py).
         rows = scheme.rows_per_partition
-        parts: List[List[Tuple[int, int]]] = [[] for _ in range(W)]
-        for m in scheme.messages:
-            parts[m.worker] += [(p, rows) for p, _ in m.segments]
         sparse = source.is_sparse if source is not None else bool(cfg.is_real)
         if cfg.share_partitions:
             replica_weight = 0.0
@@ -141,12 +141,19 @@ class Trainer:
             replica_weight = REPLICA_WEIGHT_DENSE
         else:
             replica_weight = 1.0
-        self.owner = place_workers_shared(parts, env.world, replica_weight)
-        self.by_rank = workers_by_rank(self.owner, env.world)
-        self.msg_index = {(m.worker, m.part): j for j, m in enumerate(scheme.messages)}
-        self.local_msgs = [m for m in scheme.messages if self.owner[m.worker] == env.rank]
-        self.remote_msgs = {r: [m for m in scheme.messages if self.owner[m.worker] == r]
+        self.shard_mode = cfg.shard if cfg.shard != "auto" else ("partition" if env.world > 1 else "message")
+        self.shards = make_shards(scheme.messages, self.shard_mode)
+        parts = [[(p, rows) for p, _ in u.segments] for u in self.shards]
+        if self.shard_mode == "partition":
+            self.owner = place_units(parts, env.world, replica_weight)
+        else:
+            self.owner = place_workers_shared(parts, env.world, replica_weight)
+        self.by_rank = {r: sorted({u.worker for u, o in zip(self.shards, self.owner) if o == r})
+                        for r in range(env.world)}
+        self.local_msgs = [u for u, o in zip(self.shards, self.owner) if o == env.rank]
+        self.remote_msgs = {r: [u for u, o in zip(self.shards, self.owner) if o == r]
                             for r in range(1, env.world)} if env.is_master else {}
+        self.n_shards = {(u.worker, u.part): u.n_shards for u in self.shards}
 
     def _setup_data(self, source: Optional[DataSource]):
         cfg, sch = self.cfg, self.scheme
@@ -209,13 +216,13 @@ class Trainer:
             self.rem_slot = {}
             for r in sorted(self.remote_msgs):
                 for jj, m in enumerate(self.remote_msgs[r]):
-                    self.rem_slot[(m.worker, m.part)] = self.tx.row0[r] + jj
+                    self.rem_slot[(m.worker, m.part, m.shard)] = self.tx.row0[r] + jj
             self.Rbuf = self.tx.make_rbuf() if self.tx is not None else None
             self.beta = torch.zeros(ld, dtype=torch.float64, device=dev)
             self.u = torch.zeros(ld, dtype=torch.float64, device=dev)
             self.hist = torch.zeros((R, ld), dtype=torch.float64, device=dev)
             self.beta_in = torch.zeros((R + 1, ld), dtype=acc, device=dev)
-            self.loc_index = {(m.worker, m.part): j for j, m in enumerate(self.local_msgs)}
+            self.loc_index = {(m.worker, m.part, m.shard): j for j, m in enumerate(self.local_msgs)}
         if env.gpu:
             self.cs = torch.cuda.current_stream(dev)
             self.loc_ev = [torch.cuda.Event() for _ in range(self.K)]
@@ -323,6 +330,7 @@ class Trainer:
         R, W, K = cfg.num_itrs, cfg.n_workers, self.K
         eta = cfg.eta()
         col = ArrivalCollector(W, sch.group_of, sch.n_groups, env.gpu, cfg.tie_seed_value)
+        col.set_shards(self.n_shards)
         timeset = np.zeros(R)
         loop_time = np.zeros(R)
         worker_timeset = np.zeros((R, W))
@@ -374,16 +382,17 @@ class Trainer:
                 used = sch.decode(arrivals)
                 msgs, coefs = [], []
                 for (w, part), c in sorted(used.items()):
-                    key = (w, part)
-                    v = views.get((slot, w, part))
-                    if v is None:
-                        v = self.G[slot, self.loc_index[key]] if key in self.loc_index else \
-                            self.Rbuf[slot, self.rem_slot[key]]
-                        views[(slot, w, part)] = v
-                    if key not in self.loc_index:
-                        self.tx.before_read(slot, self.rem_slot[key])
-                    msgs.append(v)
-                    coefs.append(c)
+                    for k in range(self.n_shards[(w, part)]):  # a message = the sum of its shards
+                        key = (w, part, k)
+                        v = views.get((slot, key))
+                        if v is None:
+                            v = self.G[slot, self.loc_index[key]] if key in self.loc_index else \
+                                self.Rbuf[slot, self.rem_slot[key]]
+                            views[(slot, key)] = v
+                        if key not in self.loc_index:
+                            self.tx.before_read(slot, self.rem_slot[key])
+                        msgs.append(v)
+                        coefs.append(c)
                 decay, gm, l2, theta, code = self.update.coeffs(i, float(eta[i]))
                 if env.gpu and not cfg.sync_update:
                     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -455,6 +464,7 @@ class Trainer:
         R, W, K = cfg.num_itrs, cfg.n_workers, self.K
         C = native_ext()
         col = ArrivalCollector(W, sch.group_of, sch.n_groups, True, cfg.tie_seed_value)
+        col.set_shards(self.n_shards)
         dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
         pump = C.MasterPump(col.c, W, R, K, self.d, self.ld, dev, float(cfg.round_timeout))
         pump.set_state(self.beta, self.u, self.hist, self.beta_in)
@@ -462,7 +472,7 @@ class Trainer:
             pump.set_local(self.plan.native_launcher(), self.G, [(m.worker, m.part) for m in self.local_msgs])
         tx = self.tx
         if tx is not None:
-            rem = [(m.worker, m.part, self.rem_slot[(m.worker, m.part)], tx.flags.host_addr(env.world + r))
+            rem = [(m.worker, m.part, self.rem_slot[(m.worker, m.part, m.shard)], tx.flags.host_addr(env.world + r))
                    for r in sorted(self.remote_msgs) for m in self.remote_msgs[r]]
             pump.set_remote(self.Rbuf, rem)
             pump.set_puts([(tx.inbox_remote[r].data_ptr(), tx.flags.dev_addr(r)) for r in range(1, env.world)],

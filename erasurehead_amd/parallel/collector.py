@@ -54,6 +54,12 @@ class ArrivalCollector:
     def now() -> float:
         return native().Collector.now()
 
+    def set_shards(self, n_shards) -> None:
+        """{(worker, part): n} — messages computed as n partition shards (arrive with the last one)."""
+        for (w, p), n in n_shards.items():
+            if n != 1:
+                self.c.set_shards(int(w), int(p), int(n))
+
     def begin_round(self, i: int, t_start: float, rule: int, k: int) -> None:
         self.round = i
         self.c.begin_round(int(i), float(t_start), int(rule), int(k))

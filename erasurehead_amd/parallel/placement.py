@@ -10,10 +10,68 @@ on each worker's rows-per-round (the coded schemes replicate data unevenly, e.g.
 short last group).  `place_workers_shared` refines it for GPUs, where workers that read the
 same partitions share HBM reads (LDS-staged bundles / interleaved dispatch), so keeping an FRC group or
 cyclic neighbours together costs less than their message rows suggest.
+
+Partition shards (multi-rank runs): a logical message (worker, part) reads s+1 partitions.
+Placing whole messages caps strong scaling — at W = 8 on 8 GPUs every GPU still streams its
+worker's 3 partitions per round.  ``make_shards(messages, "partition")`` splits every message
+into one shard per partition; ``place_units`` then keeps the shards of one partition (all its
+replicas) together, so each GPU streams its partitions once and computes every replica's
+segment gradient from those rows (no replica's work is skipped).  The master sums a message's
+shards with the decode coefficient, and the collector counts the message as arrived when its
+last shard is ready (csrc/runtime/collector.h).
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+
+@dataclass(frozen=True)
+class Shard:
+    """A placed unit of work: all (shard = 0, n_shards = 1) or one partition of message (worker, part)."""
+    worker: int
+    part: int
+    segments: Tuple[Tuple[int, float], ...]
+    shard: int = 0
+    n_shards: int = 1
+
+
+def make_shards(messages, mode: str = "message") -> List[Shard]:
+    """One Shard per message ("message") or per (message, partition) ("partition")."""
+    out: List[Shard] = []
+    for m in messages:
+        segs = tuple((int(p), float(c)) for p, c in m.segments)
+        if mode == "partition" and len(segs) > 1:
+            out += [Shard(m.worker, m.part, (sg,), k, len(segs)) for k, sg in enumerate(segs)]
+        elif mode in ("message", "partition"):
+            out.append(Shard(m.worker, m.part, segs))
+        else:
+            raise ValueError(f"unknown shard mode {mode!r}")
+    return out
+
+
+def place_units(parts: Sequence[Sequence[Tuple[int, int]]], world: int, replica_weight: float) -> List[int]:
+    """owner[u] for placement units (messages or shards), sharing-aware.
+
+    Starts from an LPT placement of *partition bundles* (the units whose first partition is the
+    same, costed with the sharing model) so replicas start out together, then refines with
+    :func:`place_workers_shared`'s moves and swaps.
+    """
+    U = len(parts)
+    if world <= 1:
+        return [0] * U
+    bundles: Dict[int, List[int]] = {}
+    for u in range(U):
+        key = parts[u][0][0] if parts[u] else -1 - u
+        bundles.setdefault(key, []).append(u)
+    keys = list(bundles)
+    bcost = [rank_cost(bundles[k], parts, replica_weight) for k in keys]
+    border = place_workers(bcost, world)
+    init = [0] * U
+    for b, k in enumerate(keys):
+        for u in bundles[k]:
+            init[u] = border[b]
+    return place_workers_shared(parts, world, replica_weight, init=init)
 
 
 def place_workers(costs: Sequence[float], world: int) -> List[int]:
@@ -56,7 +114,7 @@ def rank_cost(workers: Sequence[int], parts: Sequence[Sequence[Tuple[int, int]]]
 
 
 def place_workers_shared(parts: Sequence[Sequence[Tuple[int, int]]], world: int,
-                         replica_weight: float) -> List[int]:
+                         replica_weight: float, init: Optional[Sequence[int]] = None) -> List[int]:
     """owner[w] minimising (max rank cost, idle ranks, total cost) with the sharing-aware cost model.
 
     Starts from the LPT placement on message rows and improves it by single-worker moves and
@@ -66,7 +124,8 @@ def place_workers_shared(parts: Sequence[Sequence[Tuple[int, int]]], world: int,
     W = len(parts)
     if world <= 1:
         return [0] * W
-    owner = place_workers([float(sum(n for _, n in parts[w])) for w in range(W)], world)
+    owner = list(init) if init is not None else place_workers([float(sum(n for _, n in parts[w])) for w in range(W)],
+                                                             world)
 
     def costs(own):
         by = workers_by_rank(own, world)

@@ -28,9 +28,16 @@ def test_bench_gpus3_relaunches_three_ranks(tmp_path):
     assert d["n_gpus"] == 3
     assert [x["rank"] for x in d["ranks"]] == [0, 1, 2]
     assert d["ranks"][0]["role"].startswith("master")
-    hosted = sorted(w for x in d["ranks"] for w in x["workers"])
-    assert hosted == list(range(8))  # every logical worker placed exactly once
-    assert sorted(int(w) for ws in d["placement"].values() for w in ws) == list(range(8))
+    assert sorted({w for x in d["ranks"] for w in x["workers"]}) == list(range(8))
+    # partition shards (default on several ranks): every (worker, partition) of the W=8, s=2
+    # uneven-FRC messages is computed on exactly one rank: 3*3 + 3*3 + 2*2 = 22 shards
+    assert d["shard"] == "partition"
+    units = [u for us in d["placement"].values() for u in us]
+    assert len(units) == len(set(units)) == 22
+    for r, us in d["placement"].items():  # a partition's replicas share one rank
+        for u in us:
+            p = u.split(":")[1]
+            assert all(p not in v for rr, vs in d["placement"].items() if rr != r for v in vs)
     for x in d["ranks"]:
         assert x["transport"] == "gloo"
         assert x["local_grad_us"] > 0

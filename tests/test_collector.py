@@ -194,3 +194,18 @@ def test_agc_zero_delay_covers_every_group_across_rounds():
         covered[tie] = used
     assert covered["permute"] == {0, 1, 2}
     assert covered["worker"] == {0, 1}  # the degenerate order the default avoids
+
+
+def test_sharded_message_arrives_with_its_last_shard(C):
+    c = C.Collector(3, [0, 1, 2], 3)
+    c.set_shards(0, 0, 3)  # worker 0's message is computed as 3 partition shards
+    t0 = C.Collector.now()
+    c.begin_round(0, t0, RULE_COUNT, 2)
+    sh = [c.add_host_probe(0, 0, 0, d) for d in (0.0, 0.02, 0.0)]
+    w1 = c.add_host_probe(1, 0, 0, 0.01)
+    for i in sh + [w1]:
+        c.mark_seen(i, t0)
+    assert c.wait(5.0)
+    arr = c.arrivals()
+    assert [a.worker for a in arr] == [1, 0]  # worker 0 counts once, at its slowest shard
+    assert arr[1].t_rel == pytest.approx(0.02, abs=1e-6)

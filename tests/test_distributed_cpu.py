@@ -79,3 +79,20 @@ def test_multiprocess_verify_beta(tmp_path):
     assert r["betaset"].shape[0] == 6
     with pytest.raises(Exception, match="beta race detected"):
         _run(2, case, "AGD", tmp_path, verify_beta=True, corrupt=True)
+
+
+@pytest.mark.parametrize("shard", ["partition", "message"])
+def test_world8_headline_placement_matches_replay(shard, tmp_path):
+    """The 8-GPU code path on gloo: W=8, s=2, k=6 (uneven FRC groups) over 8 ranks, with partition
+    shards (each rank streams one partition for all its replicas; the master sums a message's
+    shards) and with whole messages (one logical worker per rank)."""
+    from oracle import replay
+
+    case = CASES[5]
+    cfg, src, sch, parts = make(case, "AGD", shard=shard)
+    r = _run(8, case, "AGD", tmp_path, shard=shard)
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, cfg.eta())
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-10, atol=1e-12)
+    for a in r["arrivals"]:  # every message counted once, after all its shards
+        assert len({(w, p) for (w, p) in a}) == len(a)
