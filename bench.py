@@ -199,7 +199,11 @@ def main(argv=None) -> int:
             out["hbm_distinct_TBps"] = out["x_distinct_bytes_rank0"] / sec_per_iter / 1e12
         out["fraction_of_rows_used_in_decode"] = decode_row_fraction(sch, res.arrivals[a.warmup:], Arrival)
     reports = env.gather_objects(trainer.rank_report())
-    kernel_iso = trainer.time_local_grad() if trainer.local_msgs else None
+    kernel_iso = None
+    for r in range(env.world):  # one rank at a time: ranks may share a GPU (rehearsals)
+        if r == env.rank and trainer.local_msgs:
+            kernel_iso = trainer.time_local_grad()
+        env.barrier()
     kernel_iso = env.gather_objects(kernel_iso)
     free(trainer)
     del trainer, res
