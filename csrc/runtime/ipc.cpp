@@ -254,6 +254,25 @@ void signal(uintptr_t flag, uint64_t value, int64_t device) {
          "signal");
 }
 
+// Topology probes for the IPC handshake: which local device index a PCI bus id maps to (ranks
+// may see different HIP_VISIBLE_DEVICES sets) and whether one device can map the other's memory.
+std::string pci_bus_id(int device) {
+  char buf[64] = {0};
+  hcheck(hipDeviceGetPCIBusId(buf, sizeof(buf), device), "hipDeviceGetPCIBusId");
+  return std::string(buf);
+}
+int device_by_pci(const std::string& bus) {
+  int dev = -1;
+  if (hipDeviceGetByPCIBusId(&dev, bus.c_str()) != hipSuccess) return -1;
+  return dev;
+}
+bool can_access_peer(int device, int peer) {
+  if (device == peer) return true;
+  int ok = 0;
+  hcheck(hipDeviceCanAccessPeer(&ok, device, peer), "hipDeviceCanAccessPeer");
+  return ok != 0;
+}
+
 }  // namespace
 
 namespace eh {
@@ -279,5 +298,8 @@ void bind_ipc(py::module& m) {
       .def_property_readonly("size", &ShmFlags::size);
   m.def("put_signal", &put_signal, py::arg("puts"), py::arg("counters"), py::arg("blocks") = 0);
   m.def("signal", &signal, py::arg("flag"), py::arg("value"), py::arg("device"));
+  m.def("pci_bus_id", &pci_bus_id, py::arg("device"));
+  m.def("device_by_pci", &device_by_pci, py::arg("bus_id"));
+  m.def("can_access_peer", &can_access_peer, py::arg("device"), py::arg("peer"));
 }
 }  // namespace eh

@@ -456,6 +456,11 @@ class Trainer:
                                   "messages": len(self.local_msgs),
                                   "partitions": len({p for m in self.local_msgs for p, _ in m.segments})}
         rep.update({k: round(float(v), 2) for k, v in self.rank_stats.items() if v is not None})
+        if self.tx is not None and self.tx.fallback_reason:
+            rep["transport_fallback"] = self.tx.fallback_reason
+        if self.tx is not None and env.is_master and self.tx.pairs:
+            rep["peer_access"] = [{k: x[k] for k in ("rank", "same_gpu", "master_to_rank", "rank_to_master")}
+                                  for x in self.tx.pairs]
         return rep
 
     def _master_loop_native(self, timed_start, log, start: int = 0) -> TrainResult:

@@ -46,6 +46,8 @@ class Transport:
     """Interface used by engine/trainer.py (see the module docstring)."""
 
     name = "base"
+    fallback_reason: Optional[str] = None  # why the preferred transport was not used (loud fallback)
+    pairs: List[dict] = []  # IPC: per worker rank peer-access record (IpcTransport._check_topology)
 
     def __init__(self, env, R: int, K: int, ld: int, dtype: torch.dtype, n_local: int,
                  remote_counts: Dict[int, int]):
@@ -207,7 +209,7 @@ class IpcTransport(Transport):
 
     name = "ipc"
     FINE = True  # mailboxes in fine-grained (coherent) device memory
-    HANDSHAKE_TIMEOUT = 30.0  # seconds for the whole setup handshake
+    HANDSHAKE_TIMEOUT = float(os.environ.get("ERASUREHEAD_HANDSHAKE_TIMEOUT", "30"))  # whole setup handshake
 
     def __init__(self, *a, timeout: float = 600.0, **kw):
         super().__init__(*a, **kw)
@@ -222,6 +224,7 @@ class IpcTransport(Transport):
         self.dname = dname
         self.counters = torch.zeros(64, dtype=torch.int32, device=env.device)
         self._imports = []
+        self.pairs = self._check_topology()  # collective; raises TransportError naming the pairs
         # Every step is attempted on every rank and the verdict is collective, so a failure
         # on one rank (e.g. hipIpcOpenMemHandle between two GPUs) never strands the others
         # inside a collective.
@@ -292,6 +295,39 @@ class IpcTransport(Transport):
             self.flags.unlink()  # every rank has it mapped now
         self._verify()
 
+    def _check_topology(self) -> List[dict]:
+        """Peer access between the master GPU and every worker GPU, checked per pair BEFORE any
+        IPC handle is opened: ranks exchange PCI bus ids (device indices need not agree across
+        processes), each side asks hipDeviceCanAccessPeer for its direction.  Returns one record
+        per worker rank: {rank, bus, master_bus, same_gpu, master_to_rank, rank_to_master}
+        (None = the peer GPU is not visible to that process: the handshake decides)."""
+        env, C = self.env, self.C
+        mine = (env.rank, self.dev, C.pci_bus_id(self.dev))
+        allv = env.broadcast_object(env.gather_objects(mine), 0)
+        mbus = allv[0][2]
+        rec = None
+        if not env.is_master:
+            md = C.device_by_pci(mbus)
+            rec = {"rank": env.rank, "bus": mine[2], "master_bus": mbus, "same_gpu": mine[2] == mbus,
+                   "rank_to_master": C.can_access_peer(self.dev, md) if md >= 0 else None}
+        recs = env.gather_objects(rec)
+        pairs: List[dict] = []
+        if env.is_master:
+            for r in range(1, env.world):
+                x = dict(recs[r])
+                rd = C.device_by_pci(x["bus"])
+                x["master_to_rank"] = C.can_access_peer(self.dev, rd) if rd >= 0 else None
+                pairs.append(x)
+        pairs = env.broadcast_object(pairs, 0)
+        bad = [x for x in pairs if x["master_to_rank"] is False or x["rank_to_master"] is False]
+        if bad:
+            raise TransportError("IPC mailbox needs peer access between the master GPU and every worker GPU; "
+                                 "missing for: " + "; ".join(
+                                     f"rank {x['rank']} ({x['bus']}) <-> rank 0 ({x['master_bus']}): "
+                                     f"master->rank {x['master_to_rank']}, rank->master {x['rank_to_master']}"
+                                     for x in bad))
+        return pairs
+
     def make_rbuf(self):
         if not self.env.is_master:
             return torch.zeros((1, 1, self.ld), dtype=self.dtype, device=self.env.device)
@@ -306,7 +342,7 @@ class IpcTransport(Transport):
         RCCL) instead of training on garbage.
         """
         env = self.env
-        ok = True
+        errs: List[str] = []
         if env.is_master:
             pat = torch.arange(self.ld, dtype=self.dtype, device=env.device) + 0.5
             puts = [(pat, self.inbox_remote[r][self.R], self.flags.dev_addr(r), 1) for r in range(1, env.world)]
@@ -317,13 +353,16 @@ class IpcTransport(Transport):
             deadline = time.monotonic() + self.HANDSHAKE_TIMEOUT
             for r in range(1, env.world):
                 if not self.flags.wait_ge(env.world + r, 1, max(0.0, deadline - time.monotonic())):
-                    ok = False
+                    errs.append(f"rank {r} -> rank 0: message flag never signalled within {self.HANDSHAKE_TIMEOUT:.0f}s "
+                                f"(step: worker put+signal into the master mailbox)")
                     continue
                 n = self.remote_counts.get(r, 0)
                 if n:
                     got = rbuf[0, self.row0[r]:self.row0[r] + n]
                     want = pat.unsqueeze(0) * (r + 1)
-                    ok = ok and bool(torch.equal(got, want.expand_as(got)))
+                    if not bool(torch.equal(got, want.expand_as(got))):
+                        errs.append(f"rank {r} -> rank 0: payload in mailbox rows {self.row0[r]}..{self.row0[r] + n - 1} "
+                                    f"differs from the pattern sent (step: worker put over xGMI)")
             for r in range(1, env.world):
                 self.flags.store(env.world + r, 0)
                 self.flags.store(r, 0)
@@ -331,9 +370,13 @@ class IpcTransport(Transport):
             r = env.rank
             if self.flags.wait_ge(r, 1, self.HANDSHAKE_TIMEOUT):
                 pat = torch.arange(self.ld, dtype=self.dtype, device=env.device) + 0.5
-                ok = bool(torch.equal(self.inbox[self.R], pat))
+                if not bool(torch.equal(self.inbox[self.R], pat)):
+                    errs.append(f"rank 0 -> rank {r}: beta payload in the inbox differs from the pattern sent "
+                                f"(step: master put over xGMI)")
                 n = self.n_local
-                if n:
+                if os.environ.get("ERASUREHEAD_IPC_SABOTAGE") == str(r):  # test hook: this rank never answers
+                    pass
+                elif n:
                     src = (pat * (r + 1)).unsqueeze(0).repeat(n, 1).contiguous()
                     dst = self.rremote.view(self.dname, [n, self.ld], self.my_row0 * self.ld * self.es)
                     self.C.put_signal([(src, dst, self.flags.dev_addr(env.world + r), 1)], self.counters)
@@ -341,14 +384,14 @@ class IpcTransport(Transport):
                     self.C.signal(self.flags.dev_addr(env.world + r), 1, self.dev)
                 torch.cuda.synchronize(env.device)
             else:
-                ok = False
+                errs.append(f"rank 0 -> rank {r}: beta flag never signalled within {self.HANDSHAKE_TIMEOUT:.0f}s "
+                            f"(step: master put+signal into the worker inbox)")
         env.barrier()  # master resets the flags only after everyone saw its pattern
-        oks = env.gather_objects(ok)
-        verdict = all(oks) if env.is_master else None
-        verdict = env.broadcast_object(verdict, 0)
-        if not verdict:
+        allerr = env.gather_objects(errs)
+        allerr = env.broadcast_object([e for es in allerr for e in es] if env.is_master else None, 0)
+        if allerr:
             self.close()
-            raise TransportError("IPC mailbox handshake failed (payload or flag not visible across processes)")
+            raise TransportError("IPC mailbox handshake failed: " + "; ".join(allerr))
         if env.is_master:
             rbuf = self.make_rbuf()
             rbuf.zero_()
@@ -428,7 +471,15 @@ def make_transport(kind: str, env, R: int, K: int, ld: int, dtype, n_local: int,
         except TransportError as e:
             if kind == "ipc" or env.backend == "gloo":
                 raise
+            if os.environ.get("ERASUREHEAD_NO_FALLBACK"):
+                raise TransportError(f"{e} (ERASUREHEAD_NO_FALLBACK set: not falling back to RCCL)") from e
+            # loud, recorded degradation: the RCCL path runs the Python round loop (parallel/transport.py
+            # RcclTransport), not the native pumps; bench.py reports transport + reason per rank
             if env.is_master:
-                print(f"[erasurehead] {e}; falling back to RCCL p2p", file=sys.stderr, flush=True)
-            return RcclTransport(*args)
+                print("[erasurehead] WARNING: " + str(e) + "\n[erasurehead] WARNING: falling back to RCCL p2p "
+                      "with the Python round loop (slower; set ERASUREHEAD_NO_FALLBACK=1 or --transport ipc to fail "
+                      "instead)", file=sys.stderr, flush=True)
+            tx = RcclTransport(*args)
+            tx.fallback_reason = str(e)
+            return tx
     raise ValueError(f"unknown transport {kind!r}")

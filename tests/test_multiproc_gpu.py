@@ -126,3 +126,19 @@ def test_one_rank_per_gpu_matches_replay(transport, case_i, tmp_path, monkeypatc
     arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
     ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+
+
+def test_ipc_handshake_failure_names_pair_and_step(tmp_path, monkeypatch):
+    """A worker rank that never answers the setup handshake: --transport ipc fails with an error
+    naming the pair and the step instead of training on garbage or hanging."""
+    monkeypatch.setenv("ERASUREHEAD_TRANSPORT", "ipc")
+    monkeypatch.setenv("ERASUREHEAD_IPC_SABOTAGE", "1")
+    monkeypatch.setenv("ERASUREHEAD_HANDSHAKE_TIMEOUT", "3")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(HERE, "mp_engine_run.py"),
+           str(tmp_path / "x.npz"), "4", "AGD"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    err = r.stdout + r.stderr
+    assert "IPC mailbox handshake failed" in err and "rank 1 -> rank 0: message flag never signalled" in err, err[-3000:]
