@@ -32,6 +32,8 @@ DEFAULT_TASKS = 2048
 REPLICA_TASKS = 4096
 MAX_BUNDLE = 8  # replica task slots (waves) per workgroup of grad_dense_bundle / _staged
 STAGED_ROWS = 512  # rows per bundle task of grad_dense_staged (measured: 512 > 256, 1024; 2048 leaves CUs idle)
+SHARD_STAGED_ROWS = 128  # rows per bundle task when a rank holds < SHARD_ROWS distinct rows (multi-GPU shards)
+SHARD_ROWS = 800_000
 MIN_ROWS_PER_TASK = 32
 SLAB_SPLITS = 16  # csrc/kernels/grad_dense.hip kSplits
 
@@ -145,7 +147,12 @@ class DenseGradPlan:
         staged_ok = shared and self.cpl is not None and self.cpl <= MAX_CPL
         self.staged = staged_ok and (staged_env in ("1", "pair") or (staged_env == "" and prec.code in (0, 1)))
         self.staged_pair = self.staged and staged_env == "pair"
-        default_rows = str(STAGED_ROWS) if self.staged else "0"
+        # rows per bundle task: 512 at the one-GPU headline (1e6 distinct rows); a rank holding the
+        # partition shards of an N-GPU run (500k / 250k / 125k rows at N = 2 / 4 / 8) is fastest with
+        # 128-row bundles (profiles/r2_shapes: N=8 0.238 vs 0.415 ms, N=2 0.80 vs 0.99 ms at 512)
+        distinct_rows = sum(partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
+        staged_rows = STAGED_ROWS if distinct_rows >= SHARD_ROWS else SHARD_STAGED_ROWS
+        default_rows = str(staged_rows) if self.staged else "0"
         self.bundle_rows = int(os.environ.get("ERASUREHEAD_BUNDLE_ROWS", default_rows)) if (
             shared and self.cpl is not None and self.cpl <= MAX_CPL) else 0
         if self.bundle_rows:

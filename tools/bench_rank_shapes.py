@@ -1,0 +1,98 @@
+"""Per-rank gradient work of the headline at N = 1/2/4/8 GPUs, timed on one MI355X.
+
+    python tools/bench_rank_shapes.py [--rows-sweep] [--out FILE]
+
+With partition shards (parallel/placement.py) the rank of an N-GPU headline run (AGC W=8, s=2,
+k=6, 1e6 x 1e3 fp64) holds 8/N partitions of 125k rows, each with its 2-3 replica messages.
+This builds exactly that local plan (DenseGradPlan over the rank's shards) and times one
+gradient launch with HIP events: the compute floor of one round at that N.  --rows-sweep also
+times the staged bundle task sizes (ERASUREHEAD_BUNDLE_ROWS) at each shape.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def one(n_gpus: int, precision: str) -> dict:
+    import numpy as np
+    import torch
+
+    from erasurehead_amd.codes import make_scheme
+    from erasurehead_amd.data.source import SyntheticSource
+    from erasurehead_amd.models.losses import LOGISTIC
+    from erasurehead_amd.ops import DenseGradPlan, get_precision
+    from erasurehead_amd.parallel.placement import make_shards, place_units
+
+    prec = get_precision(precision)
+    sch = make_scheme("approx", 8, 2, 1_000_000, 6, 0, allow_uneven=True)
+    rows = sch.rows_per_partition
+    shards = make_shards(sch.messages, "partition" if n_gpus > 1 else "message")
+    owner = place_units([[(p, rows) for p, _ in u.segments] for u in shards], n_gpus, 0.12)
+    costs = []
+    for r in range(n_gpus):  # time the heaviest rank
+        mine = [u for u, o in zip(shards, owner) if o == r]
+        costs.append((len({p for u in mine for p, _ in u.segments}), len(mine), r))
+    _, _, r = max(costs)
+    mine = [u for u, o in zip(shards, owner) if o == r]
+    src = SyntheticSource(1_000_000, 1000, sch.n_partition_files, 1234)
+    need = sorted({p for u in mine for p, _ in u.segments})
+    parts = {p: src.partition(p, prec, torch.device("cuda")) for p in need}
+    plan = DenseGradPlan([list(u.segments) for u in mine], parts, prec, LOGISTIC, 1000)
+    beta = torch.randn(prec.ld(1000), device="cuda", dtype=prec.acc) * 0.01
+    G = plan.out_buffer()[0]
+    for _ in range(5):
+        plan.run(beta, G)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(30)]
+    for a, b in evs:
+        a.record()
+        plan.run(beta, G)
+        b.record()
+    torch.cuda.synchronize()
+    ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    return {"n_gpus": n_gpus, "precision": precision, "rank": r, "partitions": len(need), "shards": len(mine),
+            "bundle_rows": plan.bundle_rows, "variant": plan.variant, "ntasks": plan.ntasks,
+            "kernel_ms": ms, "distinct_TBps": plan.distinct_bytes / ms / 1e9}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--rows-sweep", action="store_true")
+    ap.add_argument("--precision", default="fp64")
+    ap.add_argument("--one", type=int, default=0, help=argparse.SUPPRESS)
+    a = ap.parse_args()
+    if a.one:
+        print(json.dumps(one(a.one, a.precision)), flush=True)
+        return 0
+    lines = []
+    sweeps = [None] + ([64, 128, 256, 512] if a.rows_sweep else [])
+    for n in (1, 2, 4, 8):
+        for rows in sweeps:
+            env = dict(os.environ)
+            if rows:
+                env["ERASUREHEAD_BUNDLE_ROWS"] = str(rows)
+            out = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", str(n), "--precision",
+                                  a.precision], env=env, capture_output=True, text=True, timeout=300)
+            if out.returncode != 0:
+                print(out.stdout[-2000:], out.stderr[-2000:], file=sys.stderr)
+                return 1
+            rec = json.loads(out.stdout.strip().splitlines()[-1])
+            rec["rows_env"] = rows
+            print(json.dumps(rec), flush=True)
+            lines.append(rec)
+    if a.out:
+        with open(a.out, "w") as f:
+            for r in lines:
+                f.write(json.dumps(r) + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
