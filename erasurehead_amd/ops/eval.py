@@ -103,6 +103,18 @@ def loss_sums(chunks: Iterable[Tuple[object, torch.Tensor]], B: torch.Tensor, d:
     return total.double().cpu().numpy(), n
 
 
+def warm_auc(device) -> None:
+    """Load the code objects of the AUC path (torch's segmented sort, scans, index_add) once.
+
+    Measured (profiles/r2_eval): the first auc_columns call of a process costs 0.6 s, all of it
+    first-use code-object loading (the same call warm: 4.5 ms for 100 x 2e5).  The trainer runs
+    this on the master while it generates / loads the training data, so the post-hoc evaluation
+    does not pay it."""
+    y = torch.tensor([1.0, -1.0, 1.0, -1.0], dtype=torch.float64, device=device)
+    P = torch.tensor([[0.1, 0.2], [0.3, 0.1], [0.3, 0.4], [0.0, 0.4]], dtype=torch.float64, device=device)
+    auc_columns(y, P)
+
+
 def auc_columns(y: torch.Tensor, P: torch.Tensor, chunk: int = 0) -> np.ndarray:
     """ROC AUC of every column of P against labels y in {-1, +1} (ties count 1/2).
 
