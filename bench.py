@@ -79,11 +79,11 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def relaunch(gpus: int, argv) -> int:
+def relaunch(gpus: int, argv, script: str = None) -> int:
     """Start N ranks of this script under torch.distributed.run as a CHILD process (never exec:
     nothing here has touched the GPU, and the children own it) and return its exit status."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
-           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", script or os.path.abspath(__file__), *argv]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     print(f"[bench] launching {gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)

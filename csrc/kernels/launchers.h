@@ -42,6 +42,12 @@ hipError_t eval_gemm_loss_launch(int x_dtype, int loss_kind, const void* X, long
                                  long long n, int d, const void* y, const void* B, int ldb,
                                  int R, double* loss, void* P, hipStream_t st);
 
+// ---- post-hoc evaluation over CSR / one-hot rows (eval_sparse.hip) ---------------------------
+// Bt: betas transposed [ld, R] (R <= 256); vals == nullptr: pattern-only; dtype 0 fp64, 1 fp32
+hipError_t eval_csr_loss_launch(int dtype, int loss_kind, const long long* row_ptr, const int* col, const void* vals,
+                                long long n, const void* y, const void* Bt, int R, double* loss, void* P,
+                                hipStream_t st);
+
 // ---- master combine + update (update.hip) -----------------------------------------------
 constexpr int kMaxMsgs = 128;
 struct CombineArgs {

@@ -5,7 +5,10 @@ Dense data: the MFMA GEMM P = X B^T with the loss reduction fused in its epilogu
 has to be resident at once.  Test predictions are materialised for the ROC AUC, which
 is a rank statistic computed on the device with a sort per round (ties count 1/2, i.e.
 exactly sklearn's trapezoidal roc_curve + auc).
-Sparse data: torch CSR x dense products on the device (library SpMM), same epilogues.
+Sparse data (the reference's one-hot real datasets): the hand-written CSR kernel
+(csrc/kernels/eval_sparse.hip) gathers rows of the transposed betas Bt [ld, R] per non-zero and
+fuses the same loss epilogue; pattern-only rows (every value 1) carry no value array.  CPU
+tensors use torch CSR products (tests).
 """
 from __future__ import annotations
 
@@ -50,6 +53,49 @@ def _csr(X, device, dtype):
                                    dtype=dtype, device=device)
 
 
+def _csr_operands(X, device, acc):
+    """(row_ptr int64, col int32, vals or None if pattern-only, n) of a scipy CSR matrix on the device."""
+    import scipy.sparse as sps
+
+    X = sps.csr_matrix(X)
+    npacc = np.float64 if acc == torch.float64 else np.float32
+    pattern = X.nnz == 0 or bool(np.all(X.data == 1.0))
+    row_ptr = torch.from_numpy(X.indptr.astype(np.int64)).to(device)
+    col = torch.from_numpy(X.indices.astype(np.int32)).to(device)
+    vals = None if pattern else torch.from_numpy(X.data.astype(npacc)).to(device)
+    return row_ptr, col, vals, X.shape[0], (int(X.indices.max()) + 1 if X.nnz else 0)
+
+
+def sparse_eval_device(X, y: torch.Tensor, Bt: torch.Tensor, kind: int, want_P: bool):
+    """(P [n, R] or None, per-beta loss sums [R] fp64 on the device) with the native CSR kernel.
+
+    Bt: the betas transposed, [ld, R] in the accumulator dtype (R > 256 runs in column passes)."""
+    acc = Bt.dtype
+    row_ptr, col, vals, n, maxc = _csr_operands(X, Bt.device, acc)
+    if maxc > Bt.shape[0]:
+        raise ValueError(f"sparse eval: column index {maxc - 1} outside the {Bt.shape[0]} beta features")
+    R = Bt.shape[1]
+    yd = y.to(device=Bt.device, dtype=acc).contiguous()
+    s = torch.zeros(R, dtype=torch.float64, device=Bt.device)
+    P = torch.empty((n, R), dtype=acc, device=Bt.device) if want_P else None
+    C = native()
+    for c0 in range(0, R, 256):
+        c1 = min(R, c0 + 256)
+        Bc = Bt[:, c0:c1].contiguous()
+        Pc = torch.empty((n, c1 - c0), dtype=acc, device=Bt.device) if want_P and (c0 or c1 < R) else P
+        sc = s[c0:c1] if (c0 == 0 and c1 == R) else torch.zeros(c1 - c0, dtype=torch.float64, device=Bt.device)
+        C.eval_csr_loss(kind, row_ptr, col, vals, n, yd, Bc, sc, Pc)
+        if sc is not s:
+            s[c0:c1] = sc
+        if want_P and Pc is not P:
+            P[:, c0:c1] = Pc
+    return P, s
+
+
+def _transposed(B: torch.Tensor, acc) -> torch.Tensor:
+    return B.to(acc).t().contiguous()
+
+
 def predictions(X, B: torch.Tensor, d: int) -> torch.Tensor:
     """P = X[:, :d] @ B[:, :d]^T  ([n, R], accumulator dtype of X)."""
     if _is_sparse(X):
@@ -69,6 +115,9 @@ def predictions(X, B: torch.Tensor, d: int) -> torch.Tensor:
 
 def predictions_and_loss(X, y: torch.Tensor, B: torch.Tensor, d: int, kind: int) -> Tuple[torch.Tensor, np.ndarray]:
     """(P = X B^T, per-beta loss sums) — on the GPU one MFMA GEMM with the loss fused in its epilogue."""
+    if _is_sparse(X) and B.is_cuda:
+        P, s = sparse_eval_device(X, y, _transposed(B, torch.float64), kind, True)
+        return P, s.cpu().numpy()
     if not _is_sparse(X) and X.is_cuda:
         n = X.shape[0]
         acc = torch.float64 if X.dtype == torch.float64 else torch.float32
@@ -85,8 +134,13 @@ def loss_sums(chunks: Iterable[Tuple[object, torch.Tensor]], B: torch.Tensor, d:
     R = B.shape[0]
     total = None
     n = 0
+    Bt = None
     for X, y in chunks:
-        if _is_sparse(X):
+        if _is_sparse(X) and B.is_cuda:
+            if Bt is None:
+                Bt = _transposed(B, torch.float64)
+            _, s = sparse_eval_device(X, y, Bt, kind, False)
+        elif _is_sparse(X):
             P = predictions(X, B, d)
             s = _loss_torch(kind, y.to(P.device), P)
         elif X.is_cuda:

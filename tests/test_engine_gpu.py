@@ -224,3 +224,33 @@ def test_gpu_share_partitions_sparse(ver, k, native):
             assert isinstance(tr.plan, SharedGradPlan) and tr.plan.inner.ell
         out[dev] = tr.run().betaset
     np.testing.assert_allclose(out["cuda"], out["cpu"], rtol=1e-9, atol=1e-11)
+
+
+def test_gpu_amazon_scale_onehot(native):
+    """Amazon-shaped stand-in (26215 x 241915 one-hot, 45 nnz per row; ref run_approx_coding.sh:30-32,
+    src/arrange_real_data.py:34-91; synthetic, parity unpinned): AGC W=8, s=1, k=6 through the
+    native launcher (ELL gradient, 1.94 MB messages, 242k-column combine+update) and the native
+    sparse evaluation, against the fp64 CPU engine + scipy/torch evaluation."""
+    from erasurehead_amd.codes import make_scheme
+    from erasurehead_amd.data.synthetic import REAL_SHAPES, onehot_partitions
+
+    n_am, d_am, f_am = REAL_SHAPES["amazon-dataset"]
+    W, s, k = 8, 1, 6
+    parts, test, d = onehot_partitions(n_am, d_am, f_am, W, seed=21)
+    assert d == d_am
+    src = ArraySource(parts, test, sparse=True)
+    n = sum(p[0].shape[0] for p in parts)
+    out = {}
+    for dev in ("cpu", "cuda"):
+        cfg = RunConfig(W + 1, n, d, "/tmp/eh_gpu_amazon/", 1, "amazon-dataset", 1, s, 0, 3, k, 0, "AGD", num_itrs=5,
+                        seed=0, verbose=False, fix_quirks=True)
+        sch = make_scheme("approx", W, s, n, k, 0)
+        tr = Trainer(cfg, DistEnv(device=torch.device(dev)), src, scheme=sch)
+        if dev == "cuda":
+            assert tr.plan.ell and tr.native_loop
+        res = tr.run()
+        ev = evaluate(tr, res, write=False)
+        out[dev] = (res.betaset, ev.training_loss, ev.testing_loss, ev.auc)
+    np.testing.assert_allclose(out["cuda"][0], out["cpu"][0], rtol=1e-9, atol=1e-11)
+    for a, b in zip(out["cuda"][1:], out["cpu"][1:]):
+        np.testing.assert_allclose(a, b, rtol=1e-9, atol=1e-12)

@@ -322,3 +322,35 @@ def test_dense_grad_replica_bundle_kernel(monkeypatch, native, staged, rows, d, 
     for s, m in enumerate(msgs):
         ref = sum(logistic_grad(host[p][0], host[p][1], bh, c) for p, c in m)
         np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=tol * 1e-2)
+
+
+@pytest.mark.parametrize("shape", [(20000, 15509, 55), (17290, 27654, 19), (6000, 241915, 45)])
+@pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
+@pytest.mark.parametrize("R,valued", [(100, False), (300, True), (7, True)])
+def test_sparse_eval_kernel(shape, loss, R, valued, native):
+    """Hand CSR evaluation kernel (eval_sparse.hip) vs the fp64 scipy oracle on one-hot data shaped
+    like covtype / kc_house / amazon (ref src/naive.py:166-169,190-193): predictions and the fused
+    loss sums, pattern-only and valued rows, R > 256 column passes."""
+    from erasurehead_amd.data.synthetic import onehot_partitions
+    from erasurehead_amd.ops.eval import sparse_eval_device
+
+    n, d, m = shape
+    parts, test, dd = onehot_partitions(n, d, m, 1, seed=R + loss, least_squares=loss == LEAST_SQUARES)
+    X, y = parts[0]
+    X = X.tocsr()
+    if valued:
+        X.data = np.random.RandomState(1).uniform(0.5, 1.5, X.nnz)
+    rng = np.random.RandomState(3)
+    B = rng.randn(R, dd) * 0.2
+    Bt = torch.from_numpy(np.ascontiguousarray(B.T)).to(DEV)
+    P, s = sparse_eval_device(X, torch.from_numpy(y), Bt, loss, True)
+    Pref = np.asarray(X @ B.T)
+    np.testing.assert_allclose(P.cpu().numpy(), Pref, rtol=1e-12, atol=1e-12)
+    if loss == LOGISTIC:
+        mref = -y[:, None] * Pref
+        sref = (np.maximum(mref, 0) + np.log1p(np.exp(-np.abs(mref)))).sum(0)
+    else:
+        sref = ((y[:, None] - Pref) ** 2).sum(0)
+    np.testing.assert_allclose(s.cpu().numpy(), sref, rtol=1e-11)
+    _, s2 = sparse_eval_device(X, torch.from_numpy(y), Bt, loss, False)  # loss only, no P
+    np.testing.assert_allclose(s2.cpu().numpy(), sref, rtol=1e-11)

@@ -16,6 +16,9 @@ data/synthetic.py onehot_partitions):
   agc_covtype        AGC on the covtype-shaped data without delays (sparse kernel throughput)
   ls_kc_house_*      least squares on kc_house-shaped one-hot (17290 x 27654): naive vs AGC with
                      num_collect in {4,5,6,7}, W=8 s=1
+  agc_amazon         AGC W=8 s=1 k=6 on amazon-shaped one-hot (26215 x 241915, 45 nnz/row; 1.94 MB
+                     messages), host-driven with HIP-event instrumentation (gradient / combine+update
+                     kernel microseconds).  Synthetic stand-in: parity unpinned.
 
 Per config: seconds per round (timed, device-synchronised), time-to-decode (reference
 ``timeset``), iterations to the training-loss floor (within 1 % of the best loss over the
@@ -41,7 +44,8 @@ def _floor_iters(tl: np.ndarray) -> int:
     return int(np.argmax(tl <= floor + 0.01 * abs(floor)))
 
 
-def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_kw=None, device_loop="auto"):
+def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_kw=None, device_loop="auto",
+               instrument=False):
     import torch
 
     from erasurehead_amd.config import RunConfig
@@ -49,13 +53,18 @@ def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_
     from erasurehead_amd.parallel.dist import DistEnv
     from erasurehead_amd.utils.delay import delay_floor
 
-    cfg = RunConfig(**cfg_kw, num_itrs=rounds, verbose=False, seed=0, device_loop=device_loop)
+    cfg = RunConfig(**cfg_kw, num_itrs=rounds, verbose=False, seed=0, device_loop="off" if instrument else device_loop,
+                    instrument=instrument)
     env = DistEnv(device=torch.device("cuda" if torch.cuda.is_available() else "cpu"))
     t0 = time.perf_counter()
     tr = Trainer(cfg, env, source)
     setup = time.perf_counter() - t0
     res = tr.run(timed_start=timed_from)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t_ev = time.perf_counter()
     ev = evaluate(tr, res, write=False)
+    eval_s = time.perf_counter() - t_ev
     out = {
         "config": name,
         "scheme": tr.key,
@@ -73,7 +82,14 @@ def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_
         "native_loop": tr.native_loop,
         "round_loop": tr.device_loop or ("host-native" if tr.native_loop else "host-python"),
         "precision": cfg.precision,
+        "message_bytes": int(tr.ld * torch.tensor([], dtype=tr.prec.acc).element_size()),
+        "eval_s": eval_s,
+        "grad_kernel_us_isolated": tr.time_local_grad(),
     }
+    rep = tr.rank_report()
+    for k in ("kernel_us", "update_kernel_us", "wait_k_us", "decode_update_us"):
+        if k in rep:
+            out[k] = rep[k]
     if delay_floor_kw is not None:
         fl = delay_floor(cfg.n_workers, rounds, mean=cfg.delay_mean, **delay_floor_kw)
         out["delay_floor_s"] = fl
@@ -135,20 +151,29 @@ def main():
     for k in (4, 5, 6, 7):
         configs.append((f"ls_kc_house_agc_k{k}", dict(base_kc, is_coded=1, n_stragglers=1, coded_ver=3,
                                                       num_collect=k), src_kc, None))
+    n_am, d_am, f_am = REAL_SHAPES["amazon-dataset"]
+    am, am_test, da = onehot_partitions(n_am // scale, d_am, f_am, W, seed=21)
+    src_am = ArraySource(am, am_test, sparse=True)
+    na = sum(p[0].shape[0] for p in am)
+    configs.append(("agc_amazon", dict(n_procs=W + 1, n_rows=na, n_cols=da, input_dir="/tmp/eh_suite/", is_real=1,
+                                       dataset="amazon-dataset", update_rule="AGD", is_coded=1, n_stragglers=1,
+                                       coded_ver=3, num_collect=6), src_am, None, True))
     if a.only:
         keep = set(a.only.split(","))
         configs = [c for c in configs if c[0] in keep]
     os.makedirs(a.out, exist_ok=True)
     rows = []
     with open(os.path.join(a.out, "suite.jsonl"), "w") as f:
-        for name, kw, src, floor_kw in configs:
-            r = run_config(name, kw, src, delay_floor_kw=floor_kw, device_loop=a.device_loop)
+        for name, kw, src, floor_kw, *inst in configs:
+            r = run_config(name, kw, src, delay_floor_kw=floor_kw, device_loop=a.device_loop,
+                           instrument=bool(inst and inst[0]))
             rows.append(r)
             f.write(json.dumps(r) + "\n")
             f.flush()
             print(json.dumps(r), flush=True)
     hdr = ("| config | scheme | W | s | k | loop | ms/round | timeset ms | iters to floor | final train loss | AUC | "
-           "delay floor s | overhead ms/round |\n|---|---|---|---|---|---|---|---|---|---|---|---|---|\n")
+           "delay floor s | overhead ms/round | msg KB | grad µs | combine µs | eval s |\n"
+           "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|\n")
     lines = []
     for r in rows:
         auc = "%.4f" % r["final_auc"] if r.get("final_auc") is not None else "-"
@@ -156,7 +181,9 @@ def main():
         ov = "%.3f" % r["overhead_above_floor_ms_per_round"] if "delay_floor_s" in r else "-"
         lines.append(f"| {r['config']} | {r['scheme']} | {r['W']} | {r['s']} | {r['num_collect']} | {r['round_loop']} | "
                      f"{1e3 * r['sec_per_round']:.3f} | {r['timeset_mean_ms']:.3f} | {r['iters_to_loss_floor']} | "
-                     f"{r['final_train_loss']:.5f} | {auc} | {fl} | {ov} |")
+                     f"{r['final_train_loss']:.5f} | {auc} | {fl} | {ov} | {r['message_bytes'] / 1024:.0f} | "
+                     f"{r.get('kernel_us', r.get('grad_kernel_us_isolated') or 0):.0f} | "
+                     f"{r.get('update_kernel_us', float('nan')):.1f} | {r['eval_s']:.3f} |")
     with open(os.path.join(a.out, "suite.md"), "w") as f:
         f.write(hdr + "\n".join(lines) + "\n")
     print(hdr + "\n".join(lines))
