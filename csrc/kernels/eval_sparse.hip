@@ -42,7 +42,26 @@ eval_csr_loss(const long long* __restrict__ row_ptr, const int* __restrict__ col
       const int my = lane < cnt ? col[k0 + lane] : 0;
       A mv = A(1);
       if constexpr (VALS) mv = lane < cnt ? vals[k0 + lane] : A(0);
-      for (int k = 0; k < cnt; ++k) {
+      // 8 features per step: their gathers are all issued before the first is consumed (a row
+      // is a chain of dependent L2 / Infinity-Cache hits otherwise)
+      int k = 0;
+      for (; k + 8 <= cnt; k += 8) {
+        A g[8][NC];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const A* __restrict__ bt = Bt + static_cast<long long>(__builtin_amdgcn_readlane(my, k + u)) * R;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) g[u][c] = lane + 64 * c < R ? bt[lane + 64 * c] : A(0);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          A v = A(1);
+          if constexpr (VALS) v = readlane_a(mv, k + u);
+#pragma unroll
+          for (int c = 0; c < NC; ++c) p[c] = fma(v, g[u][c], p[c]);
+        }
+      }
+      for (; k < cnt; ++k) {
         const int f = __builtin_amdgcn_readlane(my, k);  // wave-uniform feature index
         const A* __restrict__ bt = Bt + static_cast<long long>(f) * R;
         A v = A(1);

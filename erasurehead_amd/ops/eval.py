@@ -54,21 +54,27 @@ def _csr(X, device, dtype):
 
 
 def _csr_operands(X, device, acc):
-    """(row_ptr int64, col int32, vals or None if pattern-only, n) of a scipy CSR matrix on the device."""
+    """(row_ptr int64, col int32, vals or None if pattern-only, n, max column + 1) of a scipy CSR
+    matrix on the device (a tuple already in this form is passed through)."""
+    if isinstance(X, tuple):
+        return X
     import scipy.sparse as sps
 
-    X = sps.csr_matrix(X)
+    X = X if sps.isspmatrix_csr(X) else sps.csr_matrix(X)
     npacc = np.float64 if acc == torch.float64 else np.float32
-    pattern = X.nnz == 0 or bool(np.all(X.data == 1.0))
-    row_ptr = torch.from_numpy(X.indptr.astype(np.int64)).to(device)
-    col = torch.from_numpy(X.indices.astype(np.int32)).to(device)
-    vals = None if pattern else torch.from_numpy(X.data.astype(npacc)).to(device)
-    return row_ptr, col, vals, X.shape[0], (int(X.indices.max()) + 1 if X.nnz else 0)
+    pattern = X.nnz == 0 or (X.data.min() == 1.0 and X.data.max() == 1.0)
+    ind = X.indices if X.indices.dtype == np.int32 else X.indices.astype(np.int32)
+    row_ptr = torch.from_numpy(np.asarray(X.indptr, dtype=np.int64)).to(device)
+    col = torch.from_numpy(ind).to(device)
+    vals = None if pattern else torch.from_numpy(np.asarray(X.data, dtype=npacc)).to(device)
+    # the kernel gathers Bt[col]: bound every index on the host (scipy does not validate them)
+    return row_ptr, col, vals, X.shape[0], (int(ind.max()) + 1 if X.nnz else 0)
 
 
 def sparse_eval_device(X, y: torch.Tensor, Bt: torch.Tensor, kind: int, want_P: bool):
     """(P [n, R] or None, per-beta loss sums [R] fp64 on the device) with the native CSR kernel.
 
+    X: scipy CSR, or the operands of :func:`_csr_operands` (already on the device).
     Bt: the betas transposed, [ld, R] in the accumulator dtype (R > 256 runs in column passes)."""
     acc = Bt.dtype
     row_ptr, col, vals, n, maxc = _csr_operands(X, Bt.device, acc)
