@@ -1,0 +1,23 @@
+// Task tables of the dense worker-gradient kernels (grad_dense.hip, grad_mfma.hip); built on the
+// host by erasurehead_amd/ops/grad.py (DenseGradPlan) with the same byte layout.
+#pragma once
+
+namespace eh {
+
+struct Segment {
+  const void* X;      // [nrows, ld] row-major, storage type T
+  const void* y;      // [nrows] labels, accumulator type A
+  double coef;        // label encoding coefficient (cyclic MDS B[w, part]); 1 otherwise
+  long long nrows;
+};
+
+struct Task {
+  int slot;       // output message index
+  int seg;        // segment index
+  int row_begin;  // rows of the segment handled by this workgroup
+  int row_end;
+  int slab;       // slab row of this task's partial sum (tasks are dispatched in replica-
+                  // interleaved order; slab rows stay contiguous per message slot)
+};
+
+}  // namespace eh

@@ -26,24 +26,10 @@
 #include <type_traits>
 
 #include "common.h"
+#include "grad_dense.h"
+#include "lds_dma.h"
 
 namespace eh {
-
-struct Segment {
-  const void* X;      // [nrows, ld] row-major, storage type T
-  const void* y;      // [nrows] labels, accumulator type A
-  double coef;        // label encoding coefficient (cyclic MDS B[w, part]); 1 otherwise
-  long long nrows;
-};
-
-struct Task {
-  int slot;       // output message index
-  int seg;        // segment index
-  int row_begin;  // rows of the segment handled by this workgroup
-  int row_end;
-  int slab;       // slab row of this task's partial sum (tasks are dispatched in replica-
-                  // interleaved order; slab rows stay contiguous per message slot)
-};
 
 template <typename T, typename A, int CPL, int LOSS, int ROWS, bool BL = false>
 __global__ void __launch_bounds__(256)
@@ -244,39 +230,6 @@ grad_dense_bundle(const Segment* __restrict__ segs, const Task* __restrict__ tas
 // its own coefficient, and gradient accumulation — and writes its own slab row.  The rows of a
 // stage are contiguous in HBM, so a stage is one flat copy split into 1 KiB wave pieces (lane-
 // linear LDS image).  Labels ride along as one 4-byte-per-lane LDS-DMA piece.
-// The LDS-DMA loads are issued by inline asm: through the builtin, hipcc cannot tell the stage
-// being filled from the one being read and waits vmcnt(0) before every ds_read, which drains the
-// prefetch (checked in the .s).  The kernel counts and waits for its own loads instead: "stage t
-// landed" is vmcnt <= the loads this wave issued for the stages after t.
-__device__ __forceinline__ void glds16(const void* g, unsigned lds) {
-  int keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
-__device__ __forceinline__ void glds4(const void* g, unsigned lds) {
-  int keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant; n > 63 waits
-// for 63, which is stricter and therefore safe).
-__device__ __forceinline__ void wait_vmcnt(int n) {
-  // The two-stage ring (the default) always waits for everything: test that first.  Testing a
-  // readfirstlane copy keeps the compiler from folding it into the switch's compare tree.
-  if (__builtin_amdgcn_readfirstlane(n) <= 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
-  }
-  switch (n) {
-#define EH_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); return;
-#define EH_W8(k) EH_W(k) EH_W(k + 1) EH_W(k + 2) EH_W(k + 3) EH_W(k + 4) EH_W(k + 5) EH_W(k + 6) EH_W(k + 7)
-    EH_W8(0) EH_W8(8) EH_W8(16) EH_W8(24) EH_W8(32) EH_W8(40) EH_W8(48) EH_W8(56)
-#undef EH_W8
-#undef EH_W
-    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-  }
-}
-
 template <typename T, typename A, int CPL, int LOSS, bool PAIR>
 __global__ void __launch_bounds__(512)
 grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tasks,

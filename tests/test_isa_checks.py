@@ -1,0 +1,53 @@
+"""Static checks on the built gfx950 code objects (no GPU needed).
+
+The LDS-staged gradient kernels (grad_dense_staged, grad_staged_mfma) wait for their own LDS-DMA
+loads with a hand-counted ``s_waitcnt vmcnt(n)`` (csrc/kernels/lds_dma.h): the count is only right
+if the compiler issues no vector-memory LOAD of its own once the stage pipeline has started.  This
+disassembles every instantiation from the built library and checks exactly that, so a compiler
+change that breaks the assumption fails here instead of racing intermittently on the GPU
+(tools/build_ext.py ERASUREHEAD_FULL_VMCNT=1 builds the vmcnt(0) variant for A/B runs).
+"""
+import glob
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+VMEM_LOAD = re.compile(r"^(global_load|buffer_load|flat_load|global_atomic|flat_atomic|buffer_atomic)")
+
+
+def _code_objects(tmp_path):
+    from erasurehead_amd._ext import check_fresh
+
+    so = check_fresh()["so"]
+    dst = tmp_path / "c.so"
+    shutil.copy(so, dst)
+    subprocess.run([OBJDUMP, "--offloading", str(dst)], cwd=str(tmp_path), capture_output=True, check=True)
+    return sorted(glob.glob(str(tmp_path / "c.so.*gfx950")))
+
+
+def _functions(path):
+    out = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", path], capture_output=True, text=True, check=True).stdout
+    for chunk in re.split(r"\n(?=[0-9a-f]+ <)", out):
+        m = re.match(r"[0-9a-f]+ <([^>]+)>", chunk)
+        if m:
+            yield m.group(1), [l.strip() for l in chunk.splitlines()[1:] if l.strip()]
+
+
+@pytest.mark.skipif(not os.path.exists(OBJDUMP), reason="llvm-objdump not installed")
+def test_staged_kernels_issue_no_compiler_loads_inside_the_stage_pipeline(tmp_path):
+    checked = 0
+    for co in _code_objects(tmp_path):
+        for name, body in _functions(co):
+            if "grad_dense_staged" not in name and "grad_staged_mfma" not in name:
+                continue
+            checked += 1
+            first = next((i for i, l in enumerate(body) if "global_load_lds" in l.split()[0]), None)
+            assert first is not None, f"{name}: no LDS-DMA loads found"
+            bad = [l for l in body[first:] if VMEM_LOAD.match(l.split()[0]) and "_lds" not in l.split()[0]]
+            assert not bad, f"{name}: compiler-emitted vector loads inside the counted stage loop: {bad[:4]}"
+    assert checked >= 48, f"only {checked} staged kernel instantiations found"

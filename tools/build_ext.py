@@ -44,9 +44,15 @@ def _hash_inputs(csrc: str = CSRC):
     return files
 
 
+def _defines():
+    """Build-time debug switches (part of the provenance hash)."""
+    return ["-DEH_FULL_VMCNT"] if os.environ.get("ERASUREHEAD_FULL_VMCNT") == "1" else []
+
+
 def source_hash(csrc: str = CSRC) -> str:
-    """SHA-256 over the native sources (relative path + bytes) and the build script."""
+    """SHA-256 over the native sources (relative path + bytes), the build script and its defines."""
     h = hashlib.sha256()
+    h.update(" ".join(_defines()).encode() + b"\0")
     for p in _hash_inputs(csrc):
         if p.endswith("_selftest.cpp"):
             continue
@@ -121,7 +127,7 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     for s in hip_srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         cmd = [os.path.join(ROCM, "bin", "hipcc"), "-c", s, "-o", o, f"--offload-arch={ARCH}",
-               "-munsafe-fp-atomics", *common]
+               "-munsafe-fp-atomics", *common, *_defines()]
         jobs_list.append((s, o, cmd))
     for s in cpp_srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
