@@ -2,6 +2,10 @@
 // host by erasurehead_amd/ops/grad.py (DenseGradPlan) with the same byte layout.
 #pragma once
 
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
 namespace eh {
 
 struct Segment {
@@ -19,5 +23,10 @@ struct Task {
   int slab;       // slab row of this task's partial sum (tasks are dispatched in replica-
                   // interleaved order; slab rows stay contiguous per message slot)
 };
+
+// grad_mfma.hip: bf16 replica bundles on the matrix cores (R task slots per workgroup, ld <= 1024)
+hipError_t grad_mfma_launch(int loss, const Segment* segs, const Task* tasks, int ntasks, int R, const float* beta,
+                            float* slab, int ld, hipStream_t st);
+bool mfma_geometry(int ld, int* pieces, int* nstage, size_t* lds);
 
 }  // namespace eh

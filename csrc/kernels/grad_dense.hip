@@ -805,6 +805,11 @@ static int fused_rows(int requested) {
 template <typename T, typename A, int LOSS>
 static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
                                    const A* beta, A* slab, int ld, hipStream_t st, int variant) {
+  if (variant > 40 && variant <= 56) {  // bf16 replica bundles on MFMA (grad_mfma.hip), R = variant - 40
+    if constexpr (std::is_same<T, bf16_t>::value)
+      return grad_mfma_launch(LOSS, segs, tasks, ntasks, variant - 40, beta, slab, ld, st);
+    return hipErrorInvalidValue;
+  }
   if (cpl >= 256) return launch_wide<T, A, LOSS>(cpl, segs, tasks, ntasks, beta, slab, ld, st);
   const dim3 block(256);
   const dim3 grid(ntasks);

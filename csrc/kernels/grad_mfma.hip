@@ -1,0 +1,286 @@
+// MFMA worker gradient for bf16-stored design matrices: replica bundles on the matrix cores.
+//
+// Reference math per logical worker (ref src/approximate_coding.py:194-196, src/coded.py:183-185):
+//   z = X·beta;  r = -(coef * y) / (exp(y * z) + 1)   (least squares: r = -2 coef (y - z));  g = Xᵀ·r
+// A bundle (ops/grad.py) is the R <= 16 co-located messages that read the same rows of one
+// partition (FRC/AGC group members, cyclic neighbours): every replica computes its OWN z, residual
+// (own coefficient) and gradient.  grad_dense_staged does that on the VALU, one wave per replica;
+// for bf16 storage it is compute-bound (0.68 ms for 2 GB at the headline).  Here the R replicas are
+// the 16-wide M dimension of two GEMMs per 32-row stage, on v_mfma_f32_16x16x32_bf16:
+//
+//   GEMM1  Zᵀ[16 replicas x 32 rows] = Bm[16 x d] · X_stageᵀ     Bm row q = beta (q < R), 0 otherwise
+//   GEMM2  G[16 replicas x d]       += Rm[16 x 32 rows] · X_stage  Rm[q][row] = residual of replica q
+//
+// so no replica's work is skipped (each owns a row of Zᵀ, Rm and G).  beta and the residuals are
+// fp32: each is split into bf16 hi + lo (v = hi + lo + O(2^-17 v)) and fed as two MFMAs, so the
+// products keep ~fp32 accuracy while X stays exact bf16; accumulation is fp32 in the MFMA.
+//
+// Data movement: the workgroup (8 waves) streams its row range through a 2-stage LDS ring with
+// 16-byte LDS-DMA (global_load_lds, lds_dma.h) exactly like grad_dense_staged; a stage is 32 rows
+// (64 KB at d = 1000) + their labels.  GEMM1 reads its B operand (X rows, k = columns) with
+// ds_read_b128; GEMM2 needs X with k = rows, read through gfx950's transposing ds_read_b64_tr_b16
+// from the same row-major image.  GEMM1's K (columns) is split over the 8 waves and the partial
+// Zᵀ tiles are summed through LDS; the residual is evaluated once per (replica, row) by the 512
+// threads; GEMM2's N (columns) is split over the waves, each keeping its G tiles in AGPR/VGPRs for
+// the whole row range.  Supports ld <= 1024 (K steps per wave KPW = 4, column tiles TPW = 8).
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+#include "grad_dense.h"
+#include "lds_dma.h"
+
+namespace eh {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kMfS = 32;   // rows per stage = K of GEMM2
+constexpr int kMfNW = 8;   // waves per workgroup
+constexpr int kMfKPW = 4;  // GEMM1 K steps (32 columns) per wave  -> ld <= 8 * 4 * 32 = 1024
+constexpr int kMfTPW = 8;  // GEMM2 column tiles (16 columns) per wave
+
+__device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
+  hi = static_cast<__bf16>(v);
+  lo = static_cast<__bf16>(v - static_cast<float>(hi));
+}
+
+__device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// LDS transposing read: lane 4q+p of each 16-lane group passes the address of block row q,
+// columns 4p..4p+3; lane i of the group receives column i of the 4 rows (row q in element q).
+__device__ __forceinline__ bf16x4 tr_read(const unsigned char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (__attribute__((address_space(3))) bf16x4*)(reinterpret_cast<size_t>(p)));
+}
+
+template <int LOSS>
+__global__ void __launch_bounds__(512)
+grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ tasks, const float* __restrict__ beta,
+                 float* __restrict__ slab, int ld, int R, int pieces, int nstage) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const unsigned lds_base = static_cast<unsigned>(
+      reinterpret_cast<size_t>((__attribute__((address_space(3))) unsigned char*)smem_raw));
+  const Task lead = tasks[blockIdx.x * R];  // slot 0 of a bundle is always a real task
+  const Segment ls = segs[lead.seg];
+  const unsigned char* __restrict__ X = static_cast<const unsigned char*>(ls.X);
+  const unsigned char* __restrict__ Y = static_cast<const unsigned char*>(ls.y);
+  const int rowbytes = ld * 2;
+  const int data_bytes = kMfNW * pieces * 1024;
+  const int buf_bytes = data_bytes + 256;
+  const int nrows = lead.row_end - lead.row_begin;
+  const int nst = (nrows + kMfS - 1) / kMfS;
+  float* zred = reinterpret_cast<float*>(smem_raw + nstage * buf_bytes);  // [wave][16][32] partial Zᵀ
+  __bf16* rhi = reinterpret_cast<__bf16*>(zred + kMfNW * 16 * kMfS);       // [16][32] residual hi
+  __bf16* rlo = rhi + 16 * kMfS;                                            // [16][32] residual lo
+
+  // Zero the ring once: rows past the end of a partial stage then hold finite stale data, which
+  // GEMM1 may read (its residual is forced to 0) and GEMM2 multiplies by that 0.
+  for (int i = tid * 16; i < nstage * buf_bytes; i += 512 * 16)
+    *reinterpret_cast<uint4*>(smem_raw + i) = make_uint4(0u, 0u, 0u, 0u);
+
+  // residual role of this thread: (replica rm, stage row rn)
+  const int rm = tid >> 5, rn = tid & 31;
+  float rcoef = 0.f;
+  if (rm < R) {
+    const Task tq = tasks[blockIdx.x * R + rm];
+    if (tq.seg >= 0) rcoef = static_cast<float>(segs[tq.seg].coef);
+  }
+  // GEMM1 A fragments: A[m = lane & 15][k = 8 (lane >> 4) + j] = beta[k] for replica rows m < R
+  const bool rep_ok = (lane & 15) < R;
+  bf16x8 bhi[kMfKPW], blo[kMfKPW];
+#pragma unroll
+  for (int kk = 0; kk < kMfKPW; ++kk) {
+    const int k0 = (w * kMfKPW + kk) * 32 + 8 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float b = rep_ok && k0 + j < ld ? beta[k0 + j] : 0.f;
+      __bf16 h, l;
+      split_bf16(b, h, l);
+      bhi[kk][j] = h;
+      blo[kk][j] = l;
+    }
+  }
+  f32x4 g[kMfTPW];
+#pragma unroll
+  for (int t = 0; t < kMfTPW; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // slab rows of the replicas whose G elements this lane holds (m = 4 (lane >> 4) + reg); looked up
+  // before the stage pipeline so no vector load is issued inside it (lds_dma.h, vmcnt counting)
+  int slab_row[4];
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    const int m = 4 * (lane >> 4) + reg;
+    slab_row[reg] = -1;
+    if (m < R) {
+      const Task tq = tasks[blockIdx.x * R + m];
+      if (tq.seg >= 0) slab_row[reg] = tq.slab;
+    }
+  }
+
+  auto count_bytes = [&](int nbytes) {
+    const int nb = (nbytes + 1023) >> 10;
+    return (nb > w ? (nb - w + kMfNW - 1) / kMfNW : 0) + (w == 0 ? 1 : 0);
+  };
+  const int cnt_full = count_bytes(kMfS * rowbytes);
+  const int cnt_last = count_bytes((nrows - (nst - 1) * kMfS) * rowbytes);
+  auto issue = [&](int t) {
+    const unsigned dst = lds_base + (t % nstage) * buf_bytes;
+    const long long r0 = lead.row_begin + static_cast<long long>(t) * kMfS;
+    const int ns = min(kMfS, static_cast<int>(lead.row_end - r0));
+    const int bytes = ns * rowbytes;
+    const unsigned char* src = X + r0 * rowbytes;
+    for (int blk = w; blk * 1024 < bytes; blk += kMfNW)
+      glds16(src + min(blk * 1024 + lane * 16, bytes - 16), dst + blk * 1024);
+    if (w == 0) glds4(Y + r0 * 4 + min(lane * 4, ns * 4 - 4), dst + data_bytes);
+  };
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // beta / table loads done before the counted loads
+  __syncthreads();                                   // the zero fill lands before any LDS-DMA write
+  for (int t = 0; t < nstage - 1 && t < nst; ++t) issue(t);
+  const int fi = lane & 15, fq = fi >> 2, fp = fi & 3, fg = lane >> 4;
+  for (int t = 0; t < nst; ++t) {
+    const int hi = min(t + nstage - 2, nst - 1);
+    const int later = hi > t ? (hi - t) * cnt_full + (hi == nst - 1 ? cnt_last - cnt_full : 0) : 0;
+    wait_vmcnt(later);  // this wave's pieces of stage t landed
+    __syncthreads();    // every wave's pieces; stage t-1, zred and the residuals fully consumed
+    if (t + nstage - 1 < nst) issue(t + nstage - 1);
+    const unsigned char* buf = smem_raw + (t % nstage) * buf_bytes;
+    const float* lab = reinterpret_cast<const float*>(buf + data_bytes);
+    const int ns = min(kMfS, nrows - t * kMfS);
+
+    // ---- GEMM1: this wave's K slice of Zᵀ (two 16-row n-tiles of the stage)
+    f32x4 z0 = f32x4{0.f, 0.f, 0.f, 0.f}, z1 = z0;
+#pragma unroll
+    for (int kk = 0; kk < kMfKPW; ++kk) {
+      const int kstep = w * kMfKPW + kk;
+      if (kstep * 32 >= ld) break;  // wave-uniform
+      // B[k = column][n = row]: 8 consecutive columns of row (lane & 15); columns past ld are
+      // clamped onto the row's last 8 (their beta is 0, the data finite)
+      const int col = min(kstep * 32 + 8 * fg, ld - 8);
+      const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(buf + fi * rowbytes + col * 2);
+      const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(buf + (16 + fi) * rowbytes + col * 2);
+      z0 = mma(bhi[kk], x0, z0);
+      z1 = mma(bhi[kk], x1, z1);
+      z0 = mma(blo[kk], x0, z0);
+      z1 = mma(blo[kk], x1, z1);
+    }
+    // C layout: lane holds C[m = 4 (lane >> 4) + reg][n = lane & 15]  (replica m, stage row n)
+    float* zw = zred + w * 16 * kMfS;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      zw[(4 * fg + reg) * kMfS + fi] = z0[reg];
+      zw[(4 * fg + reg) * kMfS + 16 + fi] = z1[reg];
+    }
+    __syncthreads();
+    // ---- residual of (replica rm, row rn): fixed-order sum of the waves' K slices
+    {
+      float zs = 0.f;
+#pragma unroll
+      for (int v = 0; v < kMfNW; ++v) zs += zred[(v * 16 + rm) * kMfS + rn];
+      const float r = rm < R && rn < ns ? residual<LOSS, float>(zs, lab[rn], rcoef) : 0.f;
+      __bf16 h, l;
+      split_bf16(r, h, l);
+      rhi[rm * kMfS + rn] = h;
+      rlo[rm * kMfS + rn] = l;
+    }
+    __syncthreads();
+    // ---- GEMM2: G[replica][column] += Rm · X_stage over this wave's column tiles
+    // A[m = replica lane & 15][k = row 8 (lane >> 4) + j]
+    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rhi + fi * kMfS + 8 * fg);
+    const bf16x8 al = *reinterpret_cast<const bf16x8*>(rlo + fi * kMfS + 8 * fg);
+#pragma unroll
+    for (int tt = 0; tt < kMfTPW; ++tt) {
+      const int c0 = (w * kMfTPW + tt) * 16;
+      if (c0 >= ld) break;  // wave-uniform
+      // B[k = row 8 g + j][n = column c0 + i]: rows 8g..8g+3 and 8g+4..8g+7 by two transposing
+      // reads (columns past ld land in G columns that are never written)
+      const unsigned char* a0 = buf + (8 * fg + fq) * rowbytes + (c0 + 4 * fp) * 2;
+      const bf16x4 t0 = tr_read(a0);
+      const bf16x4 t1 = tr_read(a0 + 4 * rowbytes);
+      const bf16x8 xb = bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+      g[tt] = mma(ah, xb, g[tt]);
+      g[tt] = mma(al, xb, g[tt]);
+    }
+  }
+  // lane holds G[m = 4 (lane >> 4) + reg][column c0 + (lane & 15)]
+#pragma unroll
+  for (int tt = 0; tt < kMfTPW; ++tt) {
+    const int c0 = (w * kMfTPW + tt) * 16;
+    if (c0 >= ld) break;
+    const int col = c0 + fi;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg)
+      if (slab_row[reg] >= 0 && col < ld) slab[static_cast<long long>(slab_row[reg]) * ld + col] = g[tt][reg];
+  }
+}
+
+// ---- layout probes (tests/test_kernels_gpu.py checks them with exact integer data) ---------------
+// C[16][16] = A[16][32] · B[32][16] through one v_mfma_f32_16x16x32_bf16 with the fragment maps
+// the kernel above assumes.
+__global__ void mfma_probe_kernel(const float* A, const float* B, float* C) {
+  const int l = threadIdx.x;
+  bf16x8 a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = static_cast<__bf16>(A[(l & 15) * 32 + 8 * (l >> 4) + j]);
+    b[j] = static_cast<__bf16>(B[(8 * (l >> 4) + j) * 16 + (l & 15)]);
+  }
+  const f32x4 c = mma(a, b, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) C[(4 * (l >> 4) + reg) * 16 + (l & 15)] = c[reg];
+}
+// tile: [8 rows][rowlen] bf16 (rowlen % 4 == 0, >= 32).  Group g of 16 lanes reads block rows
+// 4 (g & 1) .. +3, columns 16 (g >> 1) .. +15; out[lane][q] = what lane received in element q.
+__global__ void tr_probe_kernel(const float* tile, int rowlen, float* out) {
+  __shared__ __attribute__((aligned(16))) __bf16 sm[8 * 64];
+  const int l = threadIdx.x;
+  for (int i = l; i < 8 * rowlen; i += 64) sm[i] = static_cast<__bf16>(tile[i]);
+  __syncthreads();
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const unsigned char* base = reinterpret_cast<const unsigned char*>(sm);
+  const bf16x4 v = tr_read(base + (4 * (g & 1) + q) * rowlen * 2 + (16 * (g >> 1) + 4 * p) * 2);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) out[l * 4 + e] = static_cast<float>(v[e]);
+}
+
+hipError_t mfma_probe_launch(const float* A, const float* B, float* C, hipStream_t st) {
+  hipLaunchKernelGGL(mfma_probe_kernel, dim3(1), dim3(64), 0, st, A, B, C);
+  return hipGetLastError();
+}
+hipError_t tr_probe_launch(const float* tile, int rowlen, float* out, hipStream_t st) {
+  if (rowlen % 4 || rowlen < 32 || rowlen > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tr_probe_kernel, dim3(1), dim3(64), 0, st, tile, rowlen, out);
+  return hipGetLastError();
+}
+
+// Geometry of grad_staged_mfma: 2-stage ring of 32-row stages; false when ld does not fit.
+bool mfma_geometry(int ld, int* pieces, int* nstage, size_t* lds) {
+  if (ld < 8 || ld > kMfNW * kMfKPW * 32 || ld % 8) return false;
+  const int rowbytes = ld * 2;
+  *pieces = (kMfS * rowbytes + kMfNW * 1024 - 1) / (kMfNW * 1024);
+  *nstage = 2;
+  *lds = static_cast<size_t>(*nstage) * (kMfNW * *pieces * 1024 + 256) + kMfNW * 16 * kMfS * 4 + 2 * 16 * kMfS * 2;
+  return *lds <= 160 * 1024;
+}
+
+hipError_t grad_mfma_launch(int loss, const Segment* segs, const Task* tasks, int ntasks, int R, const float* beta,
+                            float* slab, int ld, hipStream_t st) {
+  if (R < 1 || R > 16 || ntasks % R) return hipErrorInvalidValue;
+  int pieces = 0, nstage = 0;
+  size_t lds = 0;
+  if (!mfma_geometry(ld, &pieces, &nstage, &lds)) return hipErrorInvalidValue;
+  auto kern = loss == kLogistic ? grad_staged_mfma<kLogistic> : grad_staged_mfma<kLeastSquares>;
+  const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  if (ea != hipSuccess) return ea;
+  hipLaunchKernelGGL(kern, dim3(ntasks / R), dim3(64 * kMfNW), lds, st, segs, tasks, beta, slab, ld, R, pieces,
+                     nstage);
+  return hipGetLastError();
+}
+
+}  // namespace eh

@@ -32,6 +32,10 @@ hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals
                            const void* chunks, int nchunks, const int* lo, const int* width,
                            int max_width, void* G, long long gsize, int ld, hipStream_t st);
 
+// layout probes of the bf16 MFMA gradient (grad_mfma.hip): one 16x16x32 product; one transposing read
+hipError_t mfma_probe_launch(const float* A, const float* B, float* C, hipStream_t st);
+hipError_t tr_probe_launch(const float* tile, int rowlen, float* out, hipStream_t st);
+
 // ---- device encoding of shared-partition gradients (encode.hip) ---------------------------
 // G[slot] = sum_{k in [ptr[slot], ptr[slot+1])} coef[k] * Gb[idx[k]]; dtype 0 fp64, 1 fp32
 hipError_t encode_messages_launch(int dtype, const void* Gb, const int* ptr, const int* idx, const double* coef,

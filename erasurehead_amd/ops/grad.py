@@ -147,12 +147,17 @@ class DenseGradPlan:
         staged_ok = shared and self.cpl is not None and self.cpl <= MAX_CPL
         self.staged = staged_ok and (staged_env in ("1", "pair") or (staged_env == "" and prec.code in (0, 1)))
         self.staged_pair = self.staged and staged_env == "pair"
+        # bf16 replica bundles on the matrix cores (csrc/kernels/grad_mfma.hip): the R replicas of a
+        # bundle are the M dimension of X·beta and Xᵀ·r per 32-row LDS stage.  ERASUREHEAD_MFMA=0
+        # keeps the VALU kernels (A/B runs).
+        self.mfma = (prec.code == 2 and staged_ok and self.ld <= 1024 and self.ld % 8 == 0
+                     and os.environ.get("ERASUREHEAD_MFMA", "1") != "0")
         # rows per bundle task: 512 at the one-GPU headline (1e6 distinct rows); a rank holding the
         # partition shards of an N-GPU run (500k / 250k / 125k rows at N = 2 / 4 / 8) is fastest with
         # 128-row bundles (profiles/r2_shapes: N=8 0.238 vs 0.415 ms, N=2 0.80 vs 0.99 ms at 512)
         distinct_rows = sum(partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
         staged_rows = STAGED_ROWS if distinct_rows >= SHARD_ROWS else SHARD_STAGED_ROWS
-        default_rows = str(staged_rows) if self.staged else "0"
+        default_rows = str(staged_rows) if (self.staged or self.mfma) else "0"
         self.bundle_rows = int(os.environ.get("ERASUREHEAD_BUNDLE_ROWS", default_rows)) if (
             shared and self.cpl is not None and self.cpl <= MAX_CPL) else 0
         if self.bundle_rows:
@@ -212,7 +217,9 @@ class DenseGradPlan:
         table = []
         for g in groups:
             table += [tasks[i] for i in g] + [pad] * (R - len(g))
-        self.variant = (30 if self.staged_pair else 20 if self.staged else 10) + R
+        if self.mfma and R > 16:
+            raise ValueError("MFMA bundles hold at most 16 replicas")
+        self.variant = (40 if self.mfma else 30 if self.staged_pair else 20 if self.staged else 10) + R
         return table
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:

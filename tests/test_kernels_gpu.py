@@ -354,3 +354,63 @@ def test_sparse_eval_kernel(shape, loss, R, valued, native):
     np.testing.assert_allclose(s.cpu().numpy(), sref, rtol=1e-11)
     _, s2 = sparse_eval_device(X, torch.from_numpy(y), Bt, loss, False)  # loss only, no P
     np.testing.assert_allclose(s2.cpu().numpy(), sref, rtol=1e-11)
+
+
+def test_mfma_bf16_fragment_maps(native):
+    """The lane maps grad_mfma.hip assumes for v_mfma_f32_16x16x32_bf16, checked with exact integers:
+    A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15], C[row 4(l>>4)+reg][col l&15]."""
+    rng = np.random.RandomState(0)
+    A = rng.randint(-4, 5, (16, 32)).astype(np.float32)
+    B = rng.randint(-4, 5, (32, 16)).astype(np.float32)
+    C = torch.zeros(256, dtype=torch.float32, device=DEV)
+    native._mfma_probe(torch.from_numpy(A).to(DEV), torch.from_numpy(B).to(DEV), C)
+    np.testing.assert_array_equal(C.cpu().numpy().reshape(16, 16), A @ B)
+
+
+@pytest.mark.parametrize("rowlen", [32, 40, 64])
+def test_lds_transpose_read_map(rowlen, native):
+    """ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses block row q, columns 4p..4p+3;
+    lane i receives column i of the 4 rows (row q in element q)."""
+    tile = (np.arange(8)[:, None] * 100 + np.arange(rowlen)[None, :]).astype(np.float32)
+    out = torch.zeros(256, dtype=torch.float32, device=DEV)
+    native._tr_probe(torch.from_numpy(tile).reshape(-1).to(DEV), rowlen, out)
+    got = out.cpu().numpy().reshape(64, 4)
+    for l in range(64):
+        g, i = l >> 4, l & 15
+        want = [tile[4 * (g & 1) + q, 16 * (g >> 1) + i] for q in range(4)]
+        np.testing.assert_array_equal(got[l], want)
+
+
+@pytest.mark.parametrize("d", [1000, 1024, 333, 8])
+@pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
+def test_mfma_bf16_replica_bundles(d, loss, native, monkeypatch):
+    """bf16 replica bundles on MFMA (grad_mfma.hip) at the staged geometry: the headline's uneven FRC
+    layout (bundles of 3 and 2 replicas) plus cyclic-style distinct coefficients, every message
+    against the fp64 oracle on the stored bf16 values; and close to the VALU kernels."""
+    prec = get_precision("bf16")
+    rng = np.random.RandomState(d + 7 * loss)
+    parts, host = _parts(rng, [1500, 1501, 777], d, prec)
+    msgs = [[(0, 1.0), (1, 1.0)], [(1, 1.0), (0, 1.0)], [(0, 1.0), (1, 1.0)],  # group of 3, rotated
+            [(2, 1.0)], [(2, 1.0)],  # group of 2
+            [(0, 0.5), (2, -1.25)], [(1, 2.0)]]  # distinct coefficients
+    plan = DenseGradPlan(msgs, parts, prec, loss, d)
+    assert plan.mfma and plan.variant > 40
+    beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
+    b = rng.randn(d) * 0.3
+    beta[:d] = torch.from_numpy(b).to(prec.acc)
+    G = plan.out_buffer()[0]
+    plan.run(beta, G)
+    grad = logistic_grad if loss == LOGISTIC else least_squares_grad
+    bref = beta[:d].double().cpu().numpy()
+    for slot, m in enumerate(msgs):
+        ref = sum(grad(host[p][0], host[p][1], bref, c) for p, c in m)
+        got = G[slot, :d].double().cpu().numpy()
+        err = np.max(np.abs(got - ref)) / max(1e-30, np.max(np.abs(ref)))
+        assert err < 2e-4, (slot, err)
+    monkeypatch.setenv("ERASUREHEAD_MFMA", "0")
+    valu = DenseGradPlan(msgs, parts, prec, loss, d)
+    assert not valu.mfma
+    G2 = valu.out_buffer()[0]
+    valu.run(beta, G2)
+    np.testing.assert_allclose(G[:, :d].cpu().numpy(), G2[:, :d].cpu().numpy(), rtol=2e-4,
+                               atol=2e-4 * float(G2.abs().max()))
