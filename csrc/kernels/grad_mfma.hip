@@ -12,8 +12,9 @@
 //   GEMM2  G[16 replicas x d]       += Rm[16 x 32 rows] · X_stage  Rm[q][row] = residual of replica q
 //
 // so no replica's work is skipped (each owns a row of Zᵀ, Rm and G).  beta and the residuals are
-// fp32: each is split into bf16 hi + lo (v = hi + lo + O(2^-17 v)) and fed as two MFMAs, so the
-// products keep ~fp32 accuracy while X stays exact bf16; accumulation is fp32 in the MFMA.
+// fp32: each is split into three bf16 terms (v = v0 + v1 + v2 + O(2^-25 v)) fed as three MFMAs,
+// so the products keep fp32 accuracy while X stays exact bf16; accumulation is fp32 in the MFMA.
+// (A two-term split measured ~1e-5 absolute error on O(10) gradients: 10x the VALU kernel's.)
 //
 // Data movement: the workgroup (8 waves) streams its row range through a 2-stage LDS ring with
 // 16-byte LDS-DMA (global_load_lds, lds_dma.h) exactly like grad_dense_staged; a stage is 32 rows
@@ -41,9 +42,14 @@ constexpr int kMfNW = 8;   // waves per workgroup
 constexpr int kMfKPW = 4;  // GEMM1 K steps (32 columns) per wave  -> ld <= 8 * 4 * 32 = 1024
 constexpr int kMfTPW = 8;  // GEMM2 column tiles (16 columns) per wave
 
-__device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
-  hi = static_cast<__bf16>(v);
-  lo = static_cast<__bf16>(v - static_cast<float>(hi));
+constexpr int kMfSplit = 3;  // bf16 terms per fp32 operand
+
+__device__ __forceinline__ void split_bf16(float v, __bf16 (&t)[kMfSplit]) {
+#pragma unroll
+  for (int s = 0; s < kMfSplit; ++s) {
+    t[s] = static_cast<__bf16>(v);
+    v -= static_cast<float>(t[s]);  // exact: the remainder of a round-to-nearest is representable
+  }
 }
 
 __device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -76,8 +82,7 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
   const int nrows = lead.row_end - lead.row_begin;
   const int nst = (nrows + kMfS - 1) / kMfS;
   float* zred = reinterpret_cast<float*>(smem_raw + nstage * buf_bytes);  // [wave][16][32] partial Zᵀ
-  __bf16* rhi = reinterpret_cast<__bf16*>(zred + kMfNW * 16 * kMfS);       // [16][32] residual hi
-  __bf16* rlo = rhi + 16 * kMfS;                                            // [16][32] residual lo
+  __bf16* rres = reinterpret_cast<__bf16*>(zred + kMfNW * 16 * kMfS);      // [split][16][32] residual terms
 
   // Zero the ring once: rows past the end of a partial stage then hold finite stale data, which
   // GEMM1 may read (its residual is forced to 0) and GEMM2 multiplies by that 0.
@@ -93,17 +98,16 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
   }
   // GEMM1 A fragments: A[m = lane & 15][k = 8 (lane >> 4) + j] = beta[k] for replica rows m < R
   const bool rep_ok = (lane & 15) < R;
-  bf16x8 bhi[kMfKPW], blo[kMfKPW];
+  bf16x8 bfr[kMfKPW][kMfSplit];
 #pragma unroll
   for (int kk = 0; kk < kMfKPW; ++kk) {
     const int k0 = (w * kMfKPW + kk) * 32 + 8 * (lane >> 4);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float b = rep_ok && k0 + j < ld ? beta[k0 + j] : 0.f;
-      __bf16 h, l;
-      split_bf16(b, h, l);
-      bhi[kk][j] = h;
-      blo[kk][j] = l;
+      __bf16 t[kMfSplit];
+      split_bf16(rep_ok && k0 + j < ld ? beta[k0 + j] : 0.f, t);
+#pragma unroll
+      for (int s = 0; s < kMfSplit; ++s) bfr[kk][s][j] = t[s];
     }
   }
   f32x4 g[kMfTPW];
@@ -164,10 +168,11 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
       const int col = min(kstep * 32 + 8 * fg, ld - 8);
       const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(buf + fi * rowbytes + col * 2);
       const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(buf + (16 + fi) * rowbytes + col * 2);
-      z0 = mma(bhi[kk], x0, z0);
-      z1 = mma(bhi[kk], x1, z1);
-      z0 = mma(blo[kk], x0, z0);
-      z1 = mma(blo[kk], x1, z1);
+#pragma unroll
+      for (int s = kMfSplit - 1; s >= 0; --s) {  // small terms first
+        z0 = mma(bfr[kk][s], x0, z0);
+        z1 = mma(bfr[kk][s], x1, z1);
+      }
     }
     // C layout: lane holds C[m = 4 (lane >> 4) + reg][n = lane & 15]  (replica m, stage row n)
     float* zw = zred + w * 16 * kMfS;
@@ -183,16 +188,17 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
 #pragma unroll
       for (int v = 0; v < kMfNW; ++v) zs += zred[(v * 16 + rm) * kMfS + rn];
       const float r = rm < R && rn < ns ? residual<LOSS, float>(zs, lab[rn], rcoef) : 0.f;
-      __bf16 h, l;
-      split_bf16(r, h, l);
-      rhi[rm * kMfS + rn] = h;
-      rlo[rm * kMfS + rn] = l;
+      __bf16 t[kMfSplit];
+      split_bf16(r, t);
+#pragma unroll
+      for (int s = 0; s < kMfSplit; ++s) rres[(s * 16 + rm) * kMfS + rn] = t[s];
     }
     __syncthreads();
     // ---- GEMM2: G[replica][column] += Rm · X_stage over this wave's column tiles
     // A[m = replica lane & 15][k = row 8 (lane >> 4) + j]
-    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rhi + fi * kMfS + 8 * fg);
-    const bf16x8 al = *reinterpret_cast<const bf16x8*>(rlo + fi * kMfS + 8 * fg);
+    bf16x8 ar[kMfSplit];
+#pragma unroll
+    for (int s = 0; s < kMfSplit; ++s) ar[s] = *reinterpret_cast<const bf16x8*>(rres + (s * 16 + fi) * kMfS + 8 * fg);
 #pragma unroll
     for (int tt = 0; tt < kMfTPW; ++tt) {
       const int c0 = (w * kMfTPW + tt) * 16;
@@ -203,8 +209,8 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
       const bf16x4 t0 = tr_read(a0);
       const bf16x4 t1 = tr_read(a0 + 4 * rowbytes);
       const bf16x8 xb = bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
-      g[tt] = mma(ah, xb, g[tt]);
-      g[tt] = mma(al, xb, g[tt]);
+#pragma unroll
+      for (int s = kMfSplit - 1; s >= 0; --s) g[tt] = mma(ar[s], xb, g[tt]);
     }
   }
   // lane holds G[m = 4 (lane >> 4) + reg][column c0 + (lane & 15)]
@@ -264,7 +270,8 @@ bool mfma_geometry(int ld, int* pieces, int* nstage, size_t* lds) {
   const int rowbytes = ld * 2;
   *pieces = (kMfS * rowbytes + kMfNW * 1024 - 1) / (kMfNW * 1024);
   *nstage = 2;
-  *lds = static_cast<size_t>(*nstage) * (kMfNW * *pieces * 1024 + 256) + kMfNW * 16 * kMfS * 4 + 2 * 16 * kMfS * 2;
+  *lds = static_cast<size_t>(*nstage) * (kMfNW * *pieces * 1024 + 256) + kMfNW * 16 * kMfS * 4 +
+         kMfSplit * 16 * kMfS * 2;
   return *lds <= 160 * 1024;
 }
 

@@ -235,6 +235,7 @@ def test_encode_messages(dtype, native):
 def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native, monkeypatch):
     """Replica-interleaved task order + per-case kernel variant: same bits as message-major order."""
     monkeypatch.setenv("ERASUREHEAD_STAGED", "0")  # the interleaved dispatch, not the LDS-staged bundles
+    monkeypatch.setenv("ERASUREHEAD_MFMA", "0")  # nor the bf16 MFMA bundles
     prec = get_precision(prec_name)
     rng = np.random.RandomState(11)
     parts, _ = _parts(rng, [3000, 2000, 1000], 1000, prec)
@@ -369,16 +370,19 @@ def test_mfma_bf16_fragment_maps(native):
 
 @pytest.mark.parametrize("rowlen", [32, 40, 64])
 def test_lds_transpose_read_map(rowlen, native):
-    """ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses block row q, columns 4p..4p+3;
-    lane i receives column i of the 4 rows (row q in element q)."""
-    tile = (np.arange(8)[:, None] * 100 + np.arange(rowlen)[None, :]).astype(np.float32)
-    out = torch.zeros(256, dtype=torch.float32, device=DEV)
-    native._tr_probe(torch.from_numpy(tile).reshape(-1).to(DEV), rowlen, out)
-    got = out.cpu().numpy().reshape(64, 4)
+    lane i receives column i of the 4 rows (row q in element q).  Two tiles of bf16-exact integers:
+    one holding each element's row index, one its column index."""
+    rows = np.repeat(np.arange(8, dtype=np.float32)[:, None], rowlen, 1)
+    cols = np.repeat(np.arange(rowlen, dtype=np.float32)[None, :], 8, 0)
+    got = {}
+    for name, tile in (("row", rows), ("col", cols)):
+        out = torch.zeros(256, dtype=torch.float32, device=DEV)
+        native._tr_probe(torch.from_numpy(np.ascontiguousarray(tile)).reshape(-1).to(DEV), rowlen, out)
+        got[name] = out.cpu().numpy().reshape(64, 4)
     for l in range(64):
         g, i = l >> 4, l & 15
-        want = [tile[4 * (g & 1) + q, 16 * (g >> 1) + i] for q in range(4)]
-        np.testing.assert_array_equal(got[l], want)
+        np.testing.assert_array_equal(got["row"][l], [4 * (g & 1) + q for q in range(4)])
+        np.testing.assert_array_equal(got["col"][l], [16 * (g >> 1) + i] * 4)
 
 
 @pytest.mark.parametrize("d", [1000, 1024, 333, 8])
