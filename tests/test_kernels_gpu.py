@@ -370,6 +370,7 @@ def test_mfma_bf16_fragment_maps(native):
 
 @pytest.mark.parametrize("rowlen", [32, 40, 64])
 def test_lds_transpose_read_map(rowlen, native):
+    """ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses block row q, columns 4p..4p+3;
     lane i receives column i of the 4 rows (row q in element q).  Two tiles of bf16-exact integers:
     one holding each element's row index, one its column index."""
     rows = np.repeat(np.arange(8, dtype=np.float32)[:, None], rowlen, 1)
