@@ -37,7 +37,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kMfS = 32;   // rows per stage = K of GEMM2
 constexpr int kMfNW = 8;   // waves per workgroup
 constexpr int kMfKPW = 4;  // GEMM1 K steps (32 columns) per wave  -> ld <= 8 * 4 * 32 = 1024
 constexpr int kMfTPW = 8;  // GEMM2 column tiles (16 columns) per wave
@@ -55,6 +54,10 @@ __device__ __forceinline__ void split_bf16(float v, __bf16 (&t)[kMfSplit]) {
 __device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+// K = 16 form (16-row stages): A[m = l & 15][k = 4 (l >> 4) + j], B[k][n = l & 15], same C map
+__device__ __forceinline__ f32x4 mma(bf16x4 a, bf16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
 
 // LDS transposing read: lane 4q+p of each 16-lane group passes the address of block row q,
 // columns 4p..4p+3; lane i of the group receives column i of the 4 rows (row q in element q).
@@ -63,7 +66,10 @@ __device__ __forceinline__ bf16x4 tr_read(const unsigned char* p) {
       (__attribute__((address_space(3))) bf16x4*)(reinterpret_cast<size_t>(p)));
 }
 
-template <int LOSS>
+// S = rows per stage = K of GEMM2: 32 (v_mfma_f32_16x16x32_bf16, two transposing reads per
+// fragment) or 16 (v_mfma_f32_16x16x16_bf16, one read): 16-row stages fit a 4-deep ring, so three
+// stages (96 KB at d = 1000) are in flight per CU instead of one 64 KB stage.
+template <int LOSS, int kMfS>
 __global__ void __launch_bounds__(512)
 grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ tasks, const float* __restrict__ beta,
                  float* __restrict__ slab, int ld, int R, int pieces, int nstage) {
@@ -89,10 +95,11 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
   for (int i = tid * 16; i < nstage * buf_bytes; i += 512 * 16)
     *reinterpret_cast<uint4*>(smem_raw + i) = make_uint4(0u, 0u, 0u, 0u);
 
-  // residual role of this thread: (replica rm, stage row rn)
-  const int rm = tid >> 5, rn = tid & 31;
+  // residual role of this thread: (replica rm, stage row rn); threads past 16 * S idle there
+  const int rm = tid / kMfS, rn = tid % kMfS;
+  const bool rrole = tid < 16 * kMfS;
   float rcoef = 0.f;
-  if (rm < R) {
+  if (rrole && rm < R) {
     const Task tq = tasks[blockIdx.x * R + rm];
     if (tq.seg >= 0) rcoef = static_cast<float>(segs[tq.seg].coef);
   }
@@ -157,8 +164,11 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
     const float* lab = reinterpret_cast<const float*>(buf + data_bytes);
     const int ns = min(kMfS, nrows - t * kMfS);
 
-    // ---- GEMM1: this wave's K slice of Zᵀ (two 16-row n-tiles of the stage)
-    f32x4 z0 = f32x4{0.f, 0.f, 0.f, 0.f}, z1 = z0;
+    // ---- GEMM1: this wave's K slice of Zᵀ (S / 16 n-tiles of 16 stage rows)
+    constexpr int NT = kMfS / 16;
+    f32x4 z[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) z[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < kMfKPW; ++kk) {
       const int kstep = w * kMfKPW + kk;
@@ -166,24 +176,22 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
       // B[k = column][n = row]: 8 consecutive columns of row (lane & 15); columns past ld are
       // clamped onto the row's last 8 (their beta is 0, the data finite)
       const int col = min(kstep * 32 + 8 * fg, ld - 8);
-      const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(buf + fi * rowbytes + col * 2);
-      const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(buf + (16 + fi) * rowbytes + col * 2);
 #pragma unroll
-      for (int s = kMfSplit - 1; s >= 0; --s) {  // small terms first
-        z0 = mma(bfr[kk][s], x0, z0);
-        z1 = mma(bfr[kk][s], x1, z1);
+      for (int nt = 0; nt < NT; ++nt) {
+        const bf16x8 x = *reinterpret_cast<const bf16x8*>(buf + (16 * nt + fi) * rowbytes + col * 2);
+#pragma unroll
+        for (int s = kMfSplit - 1; s >= 0; --s) z[nt] = mma(bfr[kk][s], x, z[nt]);  // small terms first
       }
     }
     // C layout: lane holds C[m = 4 (lane >> 4) + reg][n = lane & 15]  (replica m, stage row n)
     float* zw = zred + w * 16 * kMfS;
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      zw[(4 * fg + reg) * kMfS + fi] = z0[reg];
-      zw[(4 * fg + reg) * kMfS + 16 + fi] = z1[reg];
-    }
+    for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) zw[(4 * fg + reg) * kMfS + 16 * nt + fi] = z[nt][reg];
     __syncthreads();
     // ---- residual of (replica rm, row rn): fixed-order sum of the waves' K slices
-    {
+    if (rrole) {
       float zs = 0.f;
 #pragma unroll
       for (int v = 0; v < kMfNW; ++v) zs += zred[(v * 16 + rm) * kMfS + rn];
@@ -195,22 +203,38 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
     }
     __syncthreads();
     // ---- GEMM2: G[replica][column] += Rm · X_stage over this wave's column tiles
-    // A[m = replica lane & 15][k = row 8 (lane >> 4) + j]
-    bf16x8 ar[kMfSplit];
+    if constexpr (kMfS == 32) {
+      // A[m = replica lane & 15][k = row 8 (lane >> 4) + j]
+      bf16x8 ar[kMfSplit];
 #pragma unroll
-    for (int s = 0; s < kMfSplit; ++s) ar[s] = *reinterpret_cast<const bf16x8*>(rres + (s * 16 + fi) * kMfS + 8 * fg);
+      for (int s = 0; s < kMfSplit; ++s) ar[s] = *reinterpret_cast<const bf16x8*>(rres + (s * 16 + fi) * kMfS + 8 * fg);
 #pragma unroll
-    for (int tt = 0; tt < kMfTPW; ++tt) {
-      const int c0 = (w * kMfTPW + tt) * 16;
-      if (c0 >= ld) break;  // wave-uniform
-      // B[k = row 8 g + j][n = column c0 + i]: rows 8g..8g+3 and 8g+4..8g+7 by two transposing
-      // reads (columns past ld land in G columns that are never written)
-      const unsigned char* a0 = buf + (8 * fg + fq) * rowbytes + (c0 + 4 * fp) * 2;
-      const bf16x4 t0 = tr_read(a0);
-      const bf16x4 t1 = tr_read(a0 + 4 * rowbytes);
-      const bf16x8 xb = bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+      for (int tt = 0; tt < kMfTPW; ++tt) {
+        const int c0 = (w * kMfTPW + tt) * 16;
+        if (c0 >= ld) break;  // wave-uniform
+        // B[k = row 8 g + j][n = column c0 + i]: rows 8g..8g+3 and 8g+4..8g+7 by two transposing
+        // reads (columns past ld land in G columns that are never written)
+        const unsigned char* a0 = buf + (8 * fg + fq) * rowbytes + (c0 + 4 * fp) * 2;
+        const bf16x4 t0 = tr_read(a0);
+        const bf16x4 t1 = tr_read(a0 + 4 * rowbytes);
+        const bf16x8 xb = bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
 #pragma unroll
-      for (int s = kMfSplit - 1; s >= 0; --s) g[tt] = mma(ar[s], xb, g[tt]);
+        for (int s = kMfSplit - 1; s >= 0; --s) g[tt] = mma(ar[s], xb, g[tt]);
+      }
+    } else {
+      // A[m = replica lane & 15][k = row 4 (lane >> 4) + j]
+      bf16x4 ar[kMfSplit];
+#pragma unroll
+      for (int s = 0; s < kMfSplit; ++s) ar[s] = *reinterpret_cast<const bf16x4*>(rres + (s * 16 + fi) * kMfS + 4 * fg);
+#pragma unroll
+      for (int tt = 0; tt < kMfTPW; ++tt) {
+        const int c0 = (w * kMfTPW + tt) * 16;
+        if (c0 >= ld) break;  // wave-uniform
+        // B[k = row 4 g + q][n = column c0 + i]: one transposing read of rows 4g..4g+3
+        const bf16x4 xb = tr_read(buf + (4 * fg + fq) * rowbytes + (c0 + 4 * fp) * 2);
+#pragma unroll
+        for (int s = kMfSplit - 1; s >= 0; --s) g[tt] = mma(ar[s], xb, g[tt]);
+      }
     }
   }
   // lane holds G[m = 4 (lane >> 4) + reg][column c0 + (lane & 15)]
@@ -264,24 +288,40 @@ hipError_t tr_probe_launch(const float* tile, int rowlen, float* out, hipStream_
   return hipGetLastError();
 }
 
-// Geometry of grad_staged_mfma: 2-stage ring of 32-row stages; false when ld does not fit.
-bool mfma_geometry(int ld, int* pieces, int* nstage, size_t* lds) {
+// Geometry of grad_staged_mfma: rows per stage S (16: as deep a ring as fits, up to 4 stages;
+// 32: 2 stages), LDS-DMA pieces per wave per stage, ring depth and LDS bytes; false when ld does
+// not fit.  ERASUREHEAD_MFMA_ROWS=16|32 overrides S (A/B runs).
+bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds) {
   if (ld < 8 || ld > kMfNW * kMfKPW * 32 || ld % 8) return false;
+  static const int env_rows = [] {
+    const char* e = std::getenv("ERASUREHEAD_MFMA_ROWS");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int S = env_rows == 32 ? 32 : 16;
   const int rowbytes = ld * 2;
-  *pieces = (kMfS * rowbytes + kMfNW * 1024 - 1) / (kMfNW * 1024);
-  *nstage = 2;
-  *lds = static_cast<size_t>(*nstage) * (kMfNW * *pieces * 1024 + 256) + kMfNW * 16 * kMfS * 4 +
-         kMfSplit * 16 * kMfS * 2;
-  return *lds <= 160 * 1024;
+  *rows = S;
+  *pieces = (S * rowbytes + kMfNW * 1024 - 1) / (kMfNW * 1024);
+  const size_t fixed = static_cast<size_t>(kMfNW) * 16 * S * 4 + static_cast<size_t>(kMfSplit) * 16 * S * 2;
+  const size_t stage = static_cast<size_t>(kMfNW) * *pieces * 1024 + 256;
+  const int maxst = S == 16 ? 4 : 2;
+  *nstage = 0;
+  for (int ns = maxst; ns >= 2; --ns)
+    if (ns * stage + fixed <= 160 * 1024) {
+      *nstage = ns;
+      break;
+    }
+  *lds = *nstage * stage + fixed;
+  return *nstage >= 2;
 }
 
 hipError_t grad_mfma_launch(int loss, const Segment* segs, const Task* tasks, int ntasks, int R, const float* beta,
                             float* slab, int ld, hipStream_t st) {
   if (R < 1 || R > 16 || ntasks % R) return hipErrorInvalidValue;
-  int pieces = 0, nstage = 0;
+  int rows = 0, pieces = 0, nstage = 0;
   size_t lds = 0;
-  if (!mfma_geometry(ld, &pieces, &nstage, &lds)) return hipErrorInvalidValue;
-  auto kern = loss == kLogistic ? grad_staged_mfma<kLogistic> : grad_staged_mfma<kLeastSquares>;
+  if (!mfma_geometry(ld, &rows, &pieces, &nstage, &lds)) return hipErrorInvalidValue;
+  auto kern = rows == 32 ? (loss == kLogistic ? grad_staged_mfma<kLogistic, 32> : grad_staged_mfma<kLeastSquares, 32>)
+                         : (loss == kLogistic ? grad_staged_mfma<kLogistic, 16> : grad_staged_mfma<kLeastSquares, 16>);
   const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
   if (ea != hipSuccess) return ea;
