@@ -90,11 +90,6 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
   float* zred = reinterpret_cast<float*>(smem_raw + nstage * buf_bytes);  // [wave][16][32] partial Zᵀ
   __bf16* rres = reinterpret_cast<__bf16*>(zred + kMfNW * 16 * kMfS);      // [split][16][32] residual terms
 
-  // Zero the ring once: rows past the end of a partial stage then hold finite stale data, which
-  // GEMM1 may read (its residual is forced to 0) and GEMM2 multiplies by that 0.
-  for (int i = tid * 16; i < nstage * buf_bytes; i += 512 * 16)
-    *reinterpret_cast<uint4*>(smem_raw + i) = make_uint4(0u, 0u, 0u, 0u);
-
   // residual role of this thread: (replica rm, stage row rn); threads past 16 * S idle there
   const int rm = tid / kMfS, rn = tid % kMfS;
   const bool rrole = tid < 16 * kMfS;
@@ -133,30 +128,29 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
     }
   }
 
-  auto count_bytes = [&](int nbytes) {
-    const int nb = (nbytes + 1023) >> 10;
-    return (nb > w ? (nb - w + kMfNW - 1) / kMfNW : 0) + (w == 0 ? 1 : 0);
-  };
-  const int cnt_full = count_bytes(kMfS * rowbytes);
-  const int cnt_last = count_bytes((nrows - (nst - 1) * kMfS) * rowbytes);
+  // Every stage, a partial last one included, is DMA'd in full: sources past the task's rows are
+  // clamped onto its last 16 valid bytes, so every LDS byte the GEMMs read (rows past the end:
+  // residual 0 / beta 0 there; columns past ld: discarded G columns) holds finite data without a
+  // per-workgroup zero fill, and every stage costs each wave the same number of loads.
+  const int full_bytes = kMfS * rowbytes;
+  const int nblk = (full_bytes + 1023) >> 10;
+  const int cnt_stage = (nblk > w ? (nblk - w + kMfNW - 1) / kMfNW : 0) + (w == 0 ? 1 : 0);
   auto issue = [&](int t) {
     const unsigned dst = lds_base + (t % nstage) * buf_bytes;
     const long long r0 = lead.row_begin + static_cast<long long>(t) * kMfS;
     const int ns = min(kMfS, static_cast<int>(lead.row_end - r0));
     const int bytes = ns * rowbytes;
     const unsigned char* src = X + r0 * rowbytes;
-    for (int blk = w; blk * 1024 < bytes; blk += kMfNW)
+    for (int blk = w; blk < nblk; blk += kMfNW)
       glds16(src + min(blk * 1024 + lane * 16, bytes - 16), dst + blk * 1024);
     if (w == 0) glds4(Y + r0 * 4 + min(lane * 4, ns * 4 - 4), dst + data_bytes);
   };
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // beta / table loads done before the counted loads
-  __syncthreads();                                   // the zero fill lands before any LDS-DMA write
   for (int t = 0; t < nstage - 1 && t < nst; ++t) issue(t);
   const int fi = lane & 15, fq = fi >> 2, fp = fi & 3, fg = lane >> 4;
   for (int t = 0; t < nst; ++t) {
-    const int hi = min(t + nstage - 2, nst - 1);
-    const int later = hi > t ? (hi - t) * cnt_full + (hi == nst - 1 ? cnt_last - cnt_full : 0) : 0;
+    const int later = (min(t + nstage - 2, nst - 1) - t) * cnt_stage;
     wait_vmcnt(later);  // this wave's pieces of stage t landed
     __syncthreads();    // every wave's pieces; stage t-1, zred and the residuals fully consumed
     if (t + nstage - 1 < nst) issue(t + nstage - 1);
@@ -288,16 +282,17 @@ hipError_t tr_probe_launch(const float* tile, int rowlen, float* out, hipStream_
   return hipGetLastError();
 }
 
-// Geometry of grad_staged_mfma: rows per stage S (16: as deep a ring as fits, up to 4 stages;
-// 32: 2 stages), LDS-DMA pieces per wave per stage, ring depth and LDS bytes; false when ld does
-// not fit.  ERASUREHEAD_MFMA_ROWS=16|32 overrides S (A/B runs).
+// Geometry of grad_staged_mfma: rows per stage S (32, 2-stage ring, the default: 0.48 vs 0.59 ms
+// for 16-row stages in a 4-deep ring at the bf16 headline, profiles/r2_mfma), LDS-DMA pieces per
+// wave per stage, ring depth and LDS bytes; false when ld does not fit.
+// ERASUREHEAD_MFMA_ROWS=16 selects the 16-row form (A/B runs).
 bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds) {
   if (ld < 8 || ld > kMfNW * kMfKPW * 32 || ld % 8) return false;
   static const int env_rows = [] {
     const char* e = std::getenv("ERASUREHEAD_MFMA_ROWS");
     return e ? std::atoi(e) : 0;
   }();
-  const int S = env_rows == 32 ? 32 : 16;
+  const int S = env_rows == 16 ? 16 : 32;  // measured: 32-row stages (fewer barriers per byte) win
   const int rowbytes = ld * 2;
   *rows = S;
   *pieces = (S * rowbytes + kMfNW * 1024 - 1) / (kMfNW * 1024);
