@@ -18,3 +18,7 @@ for rows in 32; do
     python -c "import json; d=json.load(open('$OUT/r${rows}_b${br}.json')); print('stage rows $rows bundle rows $br:', round(d['ms_per_step'], 4), 'ms', round(d['hbm_distinct_TBps'], 2), 'TB/s')"
   done
 done
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -m gpu -q --timeout 120 --timeout-method thread -k "fp32" > "$OUT/pytest_fp32.log" 2>&1 || { grep -E "FAIL|Error" "$OUT/pytest_fp32.log" | head -20; exit 3; }
+tail -1 "$OUT/pytest_fp32.log"
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-floor --no-breakdown --precision fp32 --json-out "$OUT/fp32.json" > "$OUT/fp32.log" 2>&1 || { tail -20 "$OUT/fp32.log"; exit 4; }
+python -c "import json; d=json.load(open('$OUT/fp32.json')); print('fp32 packed:', round(d['ms_per_step'], 4), 'ms', round(d['hbm_distinct_TBps'], 2), 'TB/s')"
