@@ -71,6 +71,22 @@ def main():
 
     cold = phases()
     warm_runs = [phases() for _ in range(5)]
+    # the same training GEMM as ONE launch over a contiguous 1e6-row copy (launch count / tail effects)
+    from erasurehead_amd._ext import native as _nat
+
+    Xall = torch.cat([x for x, _ in parts])
+    yall = torch.cat([y for _, y in parts])
+    s1 = torch.zeros(R, dtype=torch.float64, device=dev)
+    ts1 = []
+    for _ in range(6):
+        s1.zero_()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        _nat().eval_gemm_loss(LOGISTIC, Xall, Xall.shape[0], d, yall, B, s1, None)
+        torch.cuda.synchronize()
+        ts1.append(time.perf_counter() - t)
+    one_launch_s = float(np.median(ts1[1:]))
+    del Xall, yall
     warm = {k: float(np.median([w[k] for w in warm_runs])) for k in warm_runs[0]}
     flop_train = 2.0 * a.n_rows * d * R
     flop_test = 2.0 * Xt.shape[0] * d * R
@@ -79,7 +95,9 @@ def main():
            "train_gemm_TFps_warm": flop_train / warm["train_loss_gemm_s"] / 1e12,
            "test_gemm_TFps_warm": flop_test / warm["test_gemm_s"] / 1e12,
            "fp64_peak_TF": 78.6,
-           "cold_minus_warm_s": cold["total_s"] - warm["total_s"]}
+           "cold_minus_warm_s": cold["total_s"] - warm["total_s"],
+           "train_gemm_one_launch_s": one_launch_s,
+           "train_gemm_one_launch_TFps": flop_train / one_launch_s / 1e12}
     rec["train_gemm_frac_of_peak"] = rec["train_gemm_TFps_warm"] / 78.6
     print(json.dumps(rec), flush=True)
     if a.out:
