@@ -157,6 +157,13 @@ class DenseGradPlan:
         # 128-row bundles (profiles/r2_shapes: N=8 0.238 vs 0.415 ms, N=2 0.80 vs 0.99 ms at 512)
         distinct_rows = sum(partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
         staged_rows = STAGED_ROWS if distinct_rows >= SHARD_ROWS else SHARD_STAGED_ROWS
+        if self.mfma:
+            # MFMA bundles run one 8-wave workgroup per CU (150 KB of LDS): long bundles amortise its
+            # prologue (profiles/r2_mfma_ab2: 512 / 1024 / 2048 rows -> 0.458 / 0.440 / 0.430 ms at
+            # the bf16 headline); about two bundles per CU, 256..2048 rows
+            staged_rows = 256
+            while staged_rows < 2048 and staged_rows * 512 < distinct_rows:
+                staged_rows *= 2
         default_rows = str(staged_rows) if (self.staged or self.mfma) else "0"
         self.bundle_rows = int(os.environ.get("ERASUREHEAD_BUNDLE_ROWS", default_rows)) if (
             shared and self.cpl is not None and self.cpl <= MAX_CPL) else 0

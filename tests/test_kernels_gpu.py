@@ -263,9 +263,12 @@ def test_dense_grad_staged_is_the_replica_default(prec_name, native, monkeypatch
     msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
     a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
     b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, interleave=False)
+    from erasurehead_amd.ops.grad import SHARD_STAGED_ROWS
+
     assert a.staged == (prec_name != "bf16") and not b.staged
-    if a.staged:
-        assert 20 < a.variant <= 28 and a.bundle_rows == 512
+    assert a.mfma == (prec_name == "bf16")
+    if a.staged:  # 6000 distinct rows: the small-rank bundle size
+        assert 20 < a.variant <= 28 and a.bundle_rows == SHARD_STAGED_ROWS
     beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
     Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
     a.native_launcher().launch(beta, Ga)

@@ -22,3 +22,11 @@ for n in 2 4; do
   timeout -k 10 600 python bench.py --gpus $n --steps 10 --warmup 3 --no-floor --json-out "$OUT/bench_${n}rank.json" > "$OUT/bench_${n}rank.log" 2>&1 || { tail -30 "$OUT/bench_${n}rank.log"; exit 5; }
   python -c "import json; d=json.load(open('$OUT/bench_${n}rank.json')); print({k: d.get(k) for k in ('ms_per_step','host_driven_ms_per_step','shard')}); [print(r) for r in d['ranks']]"
 done
+echo "== precision modes (headline shape)"
+for p in fp32 bf16; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-floor --no-breakdown --precision $p --json-out "$OUT/bench_$p.json" > "$OUT/bench_$p.log" 2>&1 || { tail -20 "$OUT/bench_$p.log"; exit 6; }
+  python -c "import json; d=json.load(open('$OUT/bench_$p.json')); print('$p', round(d['ms_per_step'], 4), 'ms', round(d['hbm_distinct_TBps'], 2), 'TB/s distinct')"
+done
+echo "== eval profile"
+timeout -k 10 300 python tools/profile_eval.py --out "$OUT/eval.json" > "$OUT/eval.log" 2>&1 || { tail -20 "$OUT/eval.log"; exit 7; }
+tail -c 700 "$OUT/eval.json"
