@@ -319,15 +319,33 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
         const unsigned char* row0 = buf + i * rowbytes;
         const unsigned char* row1 = two ? row0 + rowbytes : row0;
         A z0 = A(0), z1 = A(0);
+        if constexpr (std::is_same<T, float>::value) {
+          // fp32: both rows' dot products in one packed accumulator {z0, z1} (v_pk_fma_f32)
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          f2 z01 = f2{0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
-          const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
-          const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
+          for (int j = 0; j < NV; ++j) {
+            const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
+            const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
+            const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
+            z01 = __builtin_elementwise_fma(f2{v0.x, v1.x}, f2{b[j][0], b[j][0]}, z01);
+            z01 = __builtin_elementwise_fma(f2{v0.y, v1.y}, f2{b[j][1], b[j][1]}, z01);
+            z01 = __builtin_elementwise_fma(f2{v0.z, v1.z}, f2{b[j][2], b[j][2]}, z01);
+            z01 = __builtin_elementwise_fma(f2{v0.w, v1.w}, f2{b[j][3], b[j][3]}, z01);
+          }
+          z0 = z01.x;
+          z1 = z01.y;
+        } else {
 #pragma unroll
-          for (int v = 0; v < VN; ++v) {
-            z0 = fma(Vec16<T>::template elem<A>(v0, v), b[j][v], z0);  // beta is 0 past the row end
-            z1 = fma(Vec16<T>::template elem<A>(v1, v), b[j][v], z1);
+          for (int j = 0; j < NV; ++j) {
+            const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
+            const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
+            const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
+#pragma unroll
+            for (int v = 0; v < VN; ++v) {
+              z0 = fma(Vec16<T>::template elem<A>(v0, v), b[j][v], z0);  // beta is 0 past the row end
+              z1 = fma(Vec16<T>::template elem<A>(v1, v), b[j][v], z1);
+            }
           }
         }
         const A zs = wave_pair_reduce(z0, z1, hi);
@@ -340,11 +358,24 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
           const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
           const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
           const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
+          if constexpr (std::is_same<T, float>::value) {
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 rr0 = f2{r0, r0}, rr1 = f2{r1, r1};
+            f2 lo = __builtin_elementwise_fma(rr0, f2{v0.x, v0.y}, f2{g[j][0], g[j][1]});
+            f2 hi2 = __builtin_elementwise_fma(rr0, f2{v0.z, v0.w}, f2{g[j][2], g[j][3]});
+            lo = __builtin_elementwise_fma(rr1, f2{v1.x, v1.y}, lo);
+            hi2 = __builtin_elementwise_fma(rr1, f2{v1.z, v1.w}, hi2);
+            g[j][0] = lo.x;
+            g[j][1] = lo.y;
+            g[j][2] = hi2.x;
+            g[j][3] = hi2.y;
+          } else {
 #pragma unroll
-          for (int v = 0; v < VN; ++v) {
-            const A e0 = Vec16<T>::template elem<A>(v0, v);  // columns past the row end: never written
-            const A e1 = Vec16<T>::template elem<A>(v1, v);
-            g[j][v] = fma(r1, e1, fma(r0, e0, g[j][v]));
+            for (int v = 0; v < VN; ++v) {
+              const A e0 = Vec16<T>::template elem<A>(v0, v);  // columns past the row end: never written
+              const A e1 = Vec16<T>::template elem<A>(v1, v);
+              g[j][v] = fma(r1, e1, fma(r0, e0, g[j][v]));
+            }
           }
         }
       }

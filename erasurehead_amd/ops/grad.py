@@ -146,7 +146,9 @@ class DenseGradPlan:
         staged_env = os.environ.get("ERASUREHEAD_STAGED", "")
         staged_ok = shared and self.cpl is not None and self.cpl <= MAX_CPL
         self.staged = staged_ok and (staged_env in ("1", "pair") or (staged_env == "" and prec.code in (0, 1)))
-        self.staged_pair = self.staged and staged_env == "pair"
+        # two rows per step sharing one reduction: the fp32 default (0.790 vs 0.862 ms at the
+        # headline, profiles/r2_fp32), slower for fp64
+        self.staged_pair = self.staged and (staged_env == "pair" or (staged_env == "" and prec.code == 1))
         # bf16 replica bundles on the matrix cores (csrc/kernels/grad_mfma.hip): the R replicas of a
         # bundle are the M dimension of X·beta and Xᵀ·r per 32-row LDS stage.  ERASUREHEAD_MFMA=0
         # keeps the VALU kernels (A/B runs).
