@@ -478,15 +478,18 @@ static inline int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
-// R task slots; fold_bytes_per_wave: one wave's gradient slice (64 * CPL accumulators)
-static inline bool staged_geometry(int R, int rowbytes, size_t fold_bytes_per_wave, StagedGeom* g) {
+// R task slots; fold_bytes_per_wave: one wave's gradient slice (64 * CPL accumulators);
+// want_wpr > 0: waves per replica requested by the plan (variant / 100), else the default below
+static inline bool staged_geometry(int R, int rowbytes, size_t fold_bytes_per_wave, StagedGeom* g, int want_wpr = 0) {
   static const int env_rows = env_int("ERASUREHEAD_STAGE_ROWS", 0);
   static const int env_stages = env_int("ERASUREHEAD_STAGES", 0);
   static const int env_wpr = env_int("ERASUREHEAD_STAGED_WPR", 0);  // waves per replica slot
   // defaults (tools/ab_staged_loss.sh): about 4 waves per workgroup and 2 rows per wave per
   // stage — R = 3: 1 wave per replica, 2 rows; R = 2: 2 waves per replica, 4 rows
   const int ns = env_stages >= 2 && env_stages <= 8 ? env_stages : 2;
-  const int wpr = env_wpr >= 1 && env_wpr <= 4 && R * env_wpr <= 8 ? env_wpr : std::max(1, 4 / R);
+  const int wpr = env_wpr >= 1 && env_wpr <= 4 && R * env_wpr <= 8 ? env_wpr
+                  : want_wpr >= 1 && want_wpr <= 4 && R * want_wpr <= 8 ? want_wpr
+                                                                       : std::max(1, 4 / R);
   const int W = R * wpr;
   const size_t fold = static_cast<size_t>(wpr - 1) * R * fold_bytes_per_wave;
   int s = env_rows > 0 ? std::min(env_rows, 32) : 2 * wpr;
@@ -867,6 +870,8 @@ static int fused_rows(int requested) {
 template <typename T, typename A, int LOSS>
 static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
                                    const A* beta, A* slab, int ld, hipStream_t st, int variant) {
+  const int want_wpr = variant / 100;  // staged bundles: waves per replica requested by the plan
+  variant %= 100;
   if (variant > 40 && variant <= 56) {  // bf16 replica bundles on MFMA (grad_mfma.hip), R = variant - 40
     if constexpr (std::is_same<T, bf16_t>::value)
       return grad_mfma_launch(LOSS, segs, tasks, ntasks, variant - 40, beta, slab, ld, st);
@@ -886,7 +891,7 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
   const int bundle_r = variant > 10 && variant <= 18 ? variant - 10 : staged_r;
   if (bundle_r && ntasks % bundle_r != 0) return hipErrorInvalidValue;
   StagedGeom sg{};
-  if (staged_r && !staged_geometry(staged_r, ld * static_cast<int>(sizeof(T)), 64ull * cpl * sizeof(A), &sg))
+  if (staged_r && !staged_geometry(staged_r, ld * static_cast<int>(sizeof(T)), 64ull * cpl * sizeof(A), &sg, want_wpr))
     return hipErrorInvalidValue;
 #define EH_IF(C)                                                                          \
   case C:                                                                                 \

@@ -147,8 +147,13 @@ class DenseGradPlan:
         staged_ok = shared and self.cpl is not None and self.cpl <= MAX_CPL
         self.staged = staged_ok and (staged_env in ("1", "pair") or (staged_env == "" and prec.code in (0, 1)))
         # two rows per step sharing one reduction: the fp32 default (0.790 vs 0.862 ms at the
-        # headline, profiles/r2_fp32), slower for fp64
-        self.staged_pair = self.staged and (staged_env == "pair" or (staged_env == "" and prec.code == 1))
+        # headline, profiles/r2_fp32) and the default on sharded ranks of a multi-GPU run, where it
+        # also wins for fp64 with one wave per replica (N=8 rank 0.213 vs 0.238 ms, N=4 0.407 vs
+        # 0.429, profiles/r2_rank_sweep); slower for the one-GPU fp64 headline
+        distinct_rows = sum(partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
+        sharded = distinct_rows < SHARD_ROWS
+        self.staged_pair = self.staged and (staged_env == "pair" or (staged_env == "" and (prec.code == 1 or sharded)))
+        self.staged_wpr = 1 if (self.staged and sharded and staged_env == "") else 0  # 0: kernel default
         # bf16 replica bundles on the matrix cores (csrc/kernels/grad_mfma.hip): the R replicas of a
         # bundle are the M dimension of X·beta and Xᵀ·r per 32-row LDS stage.  ERASUREHEAD_MFMA=0
         # keeps the VALU kernels (A/B runs).
@@ -157,7 +162,6 @@ class DenseGradPlan:
         # rows per bundle task: 512 at the one-GPU headline (1e6 distinct rows); a rank holding the
         # partition shards of an N-GPU run (500k / 250k / 125k rows at N = 2 / 4 / 8) is fastest with
         # 128-row bundles (profiles/r2_shapes: N=8 0.238 vs 0.415 ms, N=2 0.80 vs 0.99 ms at 512)
-        distinct_rows = sum(partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
         staged_rows = STAGED_ROWS if distinct_rows >= SHARD_ROWS else SHARD_STAGED_ROWS
         if self.mfma:
             # MFMA bundles run one 8-wave workgroup per CU (150 KB of LDS): long bundles amortise its
@@ -229,6 +233,8 @@ class DenseGradPlan:
         if self.mfma and R > 16:
             raise ValueError("MFMA bundles hold at most 16 replicas")
         self.variant = (40 if self.mfma else 30 if self.staged_pair else 20 if self.staged else 10) + R
+        if self.staged and self.staged_wpr:
+            self.variant += 100 * self.staged_wpr  # csrc: variant / 100 = waves per replica
         return table
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:

@@ -268,7 +268,7 @@ def test_dense_grad_staged_is_the_replica_default(prec_name, native, monkeypatch
     assert a.staged == (prec_name != "bf16") and not b.staged
     assert a.mfma == (prec_name == "bf16")
     if a.staged:  # 6000 distinct rows: the small-rank bundle size
-        assert 20 < a.variant <= 38 and a.bundle_rows == SHARD_STAGED_ROWS  # fp32: the pair form (3x)
+        assert 20 < a.variant % 100 <= 38 and a.bundle_rows == SHARD_STAGED_ROWS  # small rank: pair form
     beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
     Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
     a.native_launcher().launch(beta, Ga)
