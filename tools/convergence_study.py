@@ -150,6 +150,7 @@ def main():
     ap.add_argument("--n-cols", type=int, default=1000)
     ap.add_argument("--only", default=None, help="comma-separated scheme names")
     ap.add_argument("--serial", action="store_true")
+    ap.add_argument("--naive-from", default=None, help="reuse a naive.json of an earlier run (split runs)")
     ap.add_argument("--one", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--one-out", default=None, help=argparse.SUPPRESS)
     a = ap.parse_args()
@@ -158,7 +159,12 @@ def main():
         return 0
     os.makedirs(a.out, exist_ok=True)
     names = a.only.split(",") if a.only else list(SCHEMES)
-    if "naive" not in names:
+    if a.naive_from:
+        import shutil
+
+        shutil.copy(a.naive_from, os.path.join(a.out, "naive.json"))
+        names = [n for n in names if n != "naive"]
+    elif "naive" not in names:
         names = ["naive"] + names
     procs = []
     for n in names:
@@ -174,7 +180,7 @@ def main():
     if any(bad):
         print("some scheme runs failed:", bad, file=sys.stderr)
     recs = {}
-    for n in names:
+    for n in (["naive"] if a.naive_from else []) + names:
         path = os.path.join(a.out, f"{n}.json")
         if os.path.exists(path):
             with open(path) as f:
