@@ -54,3 +54,19 @@ def test_bench_world_size_mismatch_fails(tmp_path):
                        cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 2
     assert "WORLD_SIZE=1" in r.stderr
+
+
+def test_decode_row_fraction_counts_covered_partitions():
+    """bench.py's fraction_of_rows_used_in_decode: AGC (W=8, s=2, k=6, uneven groups) stopping on
+    groups {0,1,2} and {3,4,5} decodes 6 of the 8 partitions; every group covered -> 1."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from erasurehead_amd.codes import make_scheme
+    from erasurehead_amd.codes.schemes import Arrival
+
+    sch = make_scheme("approx", 8, 2, 8000, 6, 0, allow_uneven=True)
+    two_groups = [(w, 0, 0.0) for w in (0, 1, 2, 3, 4, 5)]
+    all_groups = [(w, 0, 0.0) for w in (0, 3, 6)]
+    assert bench.decode_row_fraction(sch, [two_groups], Arrival) == 0.75
+    assert bench.decode_row_fraction(sch, [all_groups], Arrival) == 1.0
+    assert bench.decode_row_fraction(sch, [two_groups, all_groups], Arrival) == 0.875
