@@ -176,3 +176,28 @@ def test_sharing_aware_placement_keeps_replicas_together():
     flat = place_workers_shared(parts, 2, 1.0)
     assert slowest(flat, 2, 1.0) == 11.0  # 22 message rows over 2 ranks
     assert place_workers_shared(parts, 1, 0.25) == [0] * 8
+
+
+def test_partition_shards_keep_each_partitions_replicas_on_one_rank():
+    """Partition shards (multi-rank default): the headline's 22 (worker, partition) shards over N
+    ranks; every partition's replicas share a rank, the slowest rank streams ceil(8/N) partitions,
+    and at N = 8 each GPU holds one partition (1 + 2 x 0.12 replica units)."""
+    from erasurehead_amd.codes import make_scheme
+    from erasurehead_amd.parallel.placement import make_shards, place_units, rank_cost, workers_by_rank
+
+    sch = make_scheme("approx", 8, 2, 8000, 6, 0, allow_uneven=True)
+    shards = make_shards(sch.messages, "partition")
+    assert len(shards) == 22 and all(len(u.segments) == 1 for u in shards)
+    assert {(u.worker, u.part): u.n_shards for u in shards}[(6, 0)] == 2
+    parts = [[(u.segments[0][0], 1)] for u in shards]
+    for N in (1, 2, 4, 8):
+        own = place_units(parts, N, 0.12)
+        home = {}
+        for u, o in zip(shards, own):
+            assert home.setdefault(u.segments[0][0], o) == o  # one rank per partition
+        by = workers_by_rank(own, N)
+        cost = [rank_cost(by[r], parts, 0.12) for r in range(N)]
+        assert max(len({parts[i][0][0] for i in by[r]}) for r in range(N)) == -(-8 // N)
+        assert place_units(parts, N, 0.12) == own  # deterministic on every rank
+    assert abs(max(cost) - 1.24) < 1e-9
+    assert make_shards(sch.messages, "message")[0].segments == tuple(sch.messages[0].segments)
