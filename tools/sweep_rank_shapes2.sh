@@ -18,3 +18,12 @@ for n in 8 4; do
     done
   done
 done
+echo "== one-GPU headline, one wave per replica for every bundle (R=2 bundles default to two)"
+for p in fp64 fp32; do
+  for w in 0 1; do
+    if [ "$w" = 1 ]; then export ERASUREHEAD_STAGED_WPR=1; else unset ERASUREHEAD_STAGED_WPR; fi
+    unset ERASUREHEAD_STAGED ERASUREHEAD_STAGE_ROWS ERASUREHEAD_STAGES ERASUREHEAD_BUNDLE_ROWS
+    timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-floor --no-breakdown --precision $p --json-out "$OUT/n1_${p}_w$w.json" > "$OUT/n1_${p}_w$w.log" 2>&1 || { tail -5 "$OUT/n1_${p}_w$w.log"; exit 2; }
+    python -c "import json; d=json.load(open('$OUT/n1_${p}_w$w.json')); print('N=1 $p wpr_forced=$w:', round(d['ms_per_step'], 4))"
+  done
+done
