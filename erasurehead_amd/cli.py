@@ -4,6 +4,9 @@
                    partitions coded_ver num_collect add_delay update_rule  [--extension flags]
 
 Single GPU / CPU: run directly.  Several MI355X of one node: one process per GPU,
+    python main.py <13 args> --gpus N      (relaunches itself under torch.distributed.run, like
+                                            the reference's single mpirun command, ref
+                                            run_approx_coding.sh:47-49)
     torchrun --nproc-per-node N --master-addr 127.0.0.1 main.py <13 args> [flags]
 The n_procs argument keeps the reference meaning (1 master + n_procs-1 logical workers);
 the logical workers are spread over however many processes were launched.
@@ -55,6 +58,8 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--trace", action="store_true")
     g.add_argument("--verify-beta", action="store_true", help="race detector: checksum beta on every worker")
     g.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
+    g.add_argument("--gpus", type=int, default=0,
+                   help="N > 1: start N ranks (one per GPU) under torch.distributed.run from this command")
     g.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl", "gloo"])
     g.add_argument("--device-loop", default="auto", choices=["auto", "graph", "stream", "off"],
                    help="single-process runs without injected delay: rounds captured in hipGraphs (auto/graph), "
@@ -90,12 +95,33 @@ def parse(argv: List[str]):
     return cfg, a
 
 
+def relaunch(n: int, argv: List[str]) -> int:
+    """Start n ranks of main.py as a child torch.distributed.run (before anything touches the GPU)."""
+    import os
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    main_py = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "main.py")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", main_py, *argv]
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv: Optional[List[str]] = None) -> int:
+    import os
+
     argv = sys.argv[1:] if argv is None else argv
     cfg, a = parse(argv)
     if cfg is None:
         print(USAGE)
         return 0
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return relaunch(a.gpus, argv)
     from .codes.schemes import SchemeError
     from .engine import Trainer, evaluate
     from .parallel.dist import init_distributed

@@ -111,3 +111,21 @@ def test_extension_flags_parse_and_run(tmp_path, capsys):
         outs.append([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("Iteration")])
     strip = [[ln.split(", Total time")[0] for ln in o] for o in outs]
     assert strip[0] == strip[1] and len(strip[0]) == 4
+
+
+def test_main_gpus_flag_launches_ranks(tmp_path):
+    """`python main.py <13 args> --gpus 2` starts two ranks from one command (CPU / gloo here) and
+    prints the reference console lines once (rank 0)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = str(tmp_path) + "/"
+    r = subprocess.run([sys.executable, os.path.join(root, "main.py"), "5", "2000", "20", out, "0", "synthetic", "1", "1",
+                        "0", "3", "2", "0", "AGD", "--data", "synthetic", "--num-itrs", "4", "--seed", "0",
+                        "--gpus", "2"], cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert sum(l.startswith("Iteration ") and "Train Loss" in l for l in r.stdout.splitlines()) == 4
