@@ -27,6 +27,7 @@
 
 #include "common.h"
 #include "grad_dense.h"
+#include "launchers.h"
 #include "lds_dma.h"
 
 namespace eh {
@@ -752,12 +753,47 @@ slab_reduce_final(const A* __restrict__ part, A* __restrict__ G, int ld) {
   G[static_cast<long long>(slot) * ld + c] = s;
 }
 
+// Stage 2 fused with the worker's message put (transport.hip's put + signal protocol): every
+// block also stores its sums straight into the receiver's mailbox rows (put.dst, the same
+// [slot][ld] layout as G), fences at system scope and counts itself done; the last block
+// resets the counter and release-stores the flag.  Saves the separate put_signal launch on
+// every worker round's critical path.  No early return: every thread reaches the barrier.
+template <typename A>
+__global__ void __launch_bounds__(256)
+slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, PutDesc put) {
+  const int slot = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < ld) {
+    A s = A(0);
+#pragma unroll
+    for (int k = 0; k < kSplits; ++k) s += part[(static_cast<long long>(slot) * kSplits + k) * ld + c];
+    const long long o = static_cast<long long>(slot) * ld + c;
+    G[o] = s;
+    static_cast<A*>(put.dst)[o] = s;
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int total = gridDim.x * gridDim.y;
+    const unsigned int prev = __hip_atomic_fetch_add(put.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == total - 1) {
+      __hip_atomic_store(put.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // see transport.hip: keep the flag behind the fence
+      __hip_atomic_store(put.flag, put.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 template <typename A>
 static hipError_t slab_reduce_launch(const A* slab, const int* stb, A* part, A* G, int nslots, int ld,
-                                     hipStream_t st) {
+                                     hipStream_t st, const PutDesc* put = nullptr) {
   hipLaunchKernelGGL(slab_reduce_partial<A>, dim3(ceil_div(ld, kWave), nslots, kSplits), dim3(256), 0, st,
                      slab, stb, part, ld);
-  hipLaunchKernelGGL(slab_reduce_final<A>, dim3(ceil_div(ld, 256), nslots), dim3(256), 0, st, part, G, ld);
+  if (put)
+    hipLaunchKernelGGL(slab_reduce_final_put<A>, dim3(ceil_div(ld, 256), nslots), dim3(256), 0, st, part, G, ld, *put);
+  else
+    hipLaunchKernelGGL(slab_reduce_final<A>, dim3(ceil_div(ld, 256), nslots), dim3(256), 0, st, part, G, ld);
   return hipGetLastError();
 }
 
@@ -953,7 +989,8 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
 // dtype codes: 0 = fp64 storage/fp64 acc, 1 = fp32/fp32, 2 = bf16 storage/fp32 acc
 hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
                              int ntasks, const void* beta, void* slab, const int* slot_task_begin,
-                             int nslots, void* part, void* G, int ld, hipStream_t st, int variant) {
+                             int nslots, void* part, void* G, int ld, hipStream_t st, int variant,
+                             const PutDesc* put) {
   const Segment* S = static_cast<const Segment*>(segs);
   const Task* Tk = static_cast<const Task*>(tasks);
   hipError_t e = hipSuccess;
@@ -971,8 +1008,8 @@ hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, con
             : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant);
   }
   if (e != hipSuccess) return e;
-  if (dtype == 0) return slab_reduce_launch<double>((const double*)slab, slot_task_begin, (double*)part, (double*)G, nslots, ld, st);
-  return slab_reduce_launch<float>((const float*)slab, slot_task_begin, (float*)part, (float*)G, nslots, ld, st);
+  if (dtype == 0) return slab_reduce_launch<double>((const double*)slab, slot_task_begin, (double*)part, (double*)G, nslots, ld, st, put);
+  return slab_reduce_launch<float>((const float*)slab, slot_task_begin, (float*)part, (float*)G, nslots, ld, st, put);
 }
 
 

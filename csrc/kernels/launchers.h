@@ -12,9 +12,13 @@ namespace eh {
 // ---- worker gradient (grad_dense.hip, grad_sparse.hip) -------------------------------
 // dtype: 0 fp64 storage/acc, 1 fp32/fp32, 2 bf16 storage/fp32 acc; loss: 0 logistic, 1 least squares
 // variant: 0 = per-dtype default, else the grad_dense_fused variant (grad_dense.hip fused_rows)
+struct PutDesc;
+// put (optional): fuse the message put + signal into the final slab reduction; put->dst
+// receives the nslots x ld result rows, put->bytes is ignored.
 hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
                              int ntasks, const void* beta, void* slab, const int* slot_task_begin,
-                             int nslots, void* part, void* G, int ld, hipStream_t st, int variant = 0);
+                             int nslots, void* part, void* G, int ld, hipStream_t st, int variant = 0,
+                             const PutDesc* put = nullptr);
 hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, const void* tasks,
                                      int ntasks, const void* beta, const int* task_row_off,
                                      void* rbuf, void* slab, const int* slot_task_begin,

@@ -137,6 +137,14 @@ struct GradLauncher {
     return eh::encode_messages_launch(acc, Gb, enc_ptr, enc_idx, enc_coef, G, enc_slots, ld, st);
   }
 
+  // Dense fused plans without device encoding can hand their result rows straight to the
+  // receiver's mailbox from the final reduction kernel (grad_dense.hip slab_reduce_final_put).
+  bool can_fuse_put(int rows) const { return kind == 0 && !Gb && ntasks > 0 && nslots == rows; }
+  hipError_t launch_put(const void* beta, void* G, const eh::PutDesc& put, hipStream_t st) const {
+    return eh::grad_dense_launch(dtype, loss, cpl, segs, tasks, ntasks, beta, slab, stb, nslots, part, G, ld, st,
+                                 variant, &put);
+  }
+
   hipError_t launch_raw(const void* beta, void* G, hipStream_t st) const {
     switch (kind) {
       case 0:
@@ -784,7 +792,10 @@ class WorkerPump {
     g_rows_ = (int)G.size(1);
     stream_ = c10::hip::getCurrentHIPStream(device).stream();
     wait_s_.assign(R_, -1.0);
+    const char* e = std::getenv("ERASUREHEAD_FUSED_PUT");
+    fuse_put_ = g_->can_fuse_put(n_loc) && !(e && e[0] == '0');
   }
+  bool fused_put() const { return fuse_put_; }
   ~WorkerPump() {
     for (auto& t : tev_)
       for (auto e : t)
@@ -832,17 +843,23 @@ class WorkerPump {
       const int slot = i % K_;
       const char* beta = static_cast<const char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * ld_ * es_;
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
-      if (timing_) record_t(i, 0);
-      hcheck(g_->launch(beta, g, stream_), "worker gradient");
-      if (timing_) record_t(i, 1);
-      eh::PutArgs pa{};
-      pa.n = 1;
       const long long bytes = static_cast<long long>(n_) * ld_ * es_;
-      pa.d[0] = eh::PutDesc{g, reinterpret_cast<char*>(mbox_) + (static_cast<int64_t>(slot) * mbox_rows_ + row0_) * ld_ * es_,
-                            bytes, mflag_, static_cast<unsigned long long>(i + 1),
-                            reinterpret_cast<unsigned int*>(counters_.data_ptr<int>())};
-      const int blocks = (int)std::max<long long>(1, std::min<long long>(64, (bytes / 16 + 4095) / 4096));
-      hcheck(eh::put_signal_launch(pa, blocks, stream_), "put_signal(messages)");
+      const eh::PutDesc pd{g, reinterpret_cast<char*>(mbox_) + (static_cast<int64_t>(slot) * mbox_rows_ + row0_) * ld_ * es_,
+                           bytes, mflag_, static_cast<unsigned long long>(i + 1),
+                           reinterpret_cast<unsigned int*>(counters_.data_ptr<int>())};
+      if (timing_) record_t(i, 0);
+      if (fuse_put_) {  // gradient + put + signal in one stream order, no separate put kernel
+        hcheck(g_->launch_put(beta, g, pd, stream_), "worker gradient + put");
+        if (timing_) record_t(i, 1);
+      } else {
+        hcheck(g_->launch(beta, g, stream_), "worker gradient");
+        if (timing_) record_t(i, 1);
+        eh::PutArgs pa{};
+        pa.n = 1;
+        pa.d[0] = pd;
+        const int blocks = (int)std::max<long long>(1, std::min<long long>(64, (bytes / 16 + 4095) / 4096));
+        hcheck(eh::put_signal_launch(pa, blocks, stream_), "put_signal(messages)");
+      }
       if (timing_) record_t(i, 2);
     }
     return -1;
@@ -868,6 +885,7 @@ class WorkerPump {
   int ld_ = 0, R_ = 0, es_ = 8, g_rows_ = 1;
   hipStream_t stream_ = nullptr;
   bool timing_ = false;
+  bool fuse_put_ = false;
   std::vector<std::array<hipEvent_t, 3>> tev_;  // [round] gradient start, gradient end = put start, put end
   std::vector<double> wait_s_;                  // [round] host seconds spent waiting for beta
 };
@@ -931,6 +949,7 @@ void bind_engine(py::module& m) {
       .def(py::init<std::shared_ptr<GradLauncher>, const Tensor&, const Tensor&, int, uintptr_t, int, int, uintptr_t,
                     uintptr_t, const Tensor&, int, int, double>())
       .def("run", &WorkerPump::run)
+      .def_property_readonly("fused_put", &WorkerPump::fused_put)
       .def("set_timing", &WorkerPump::set_timing)
       .def("timing", &WorkerPump::timing);
 }

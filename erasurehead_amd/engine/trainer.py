@@ -465,7 +465,8 @@ class Trainer:
 
         Times are means over the timed rounds, in microseconds: ``kernel_us`` the local gradient
         launch (HIP events; cfg.instrument), ``beta_put_us`` / ``msg_put_us`` the put+signal
-        launches, ``beta_wait_us`` a worker's host wait for beta, ``wait_k_us`` the master's wait
+        launches (a worker with ``fused_put`` issues its message put + signal from the final
+        reduction kernel, so ``kernel_us`` includes it and ``msg_put_us`` is ~0), ``beta_wait_us`` a worker's host wait for beta, ``wait_k_us`` the master's wait
         for the stop rule, ``decode_update_us`` its host decode + combine/update enqueue and
         ``update_kernel_us`` the combine+update kernel itself.
         """
@@ -640,6 +641,7 @@ class Trainer:
                             tx.mbox_rows, tx.my_row0, tx.flags.host_addr(env.rank), tx.flags.dev_addr(w + env.rank),
                             tx.counters, K, dev, float(cfg.round_timeout))
         pump.set_timing(bool(cfg.instrument))
+        self.rank_stats["fused_put"] = bool(pump.fused_put)
         cut = timed_start if timed_start is not None and start <= timed_start < R else None
         segments = [(start, cut), (cut, R)] if cut is not None else [(start, R)]
         t0 = None
