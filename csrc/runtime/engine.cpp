@@ -774,9 +774,9 @@ class WorkerPump {
  public:
   WorkerPump(std::shared_ptr<GradLauncher> g, const Tensor& inbox, const Tensor& G, int n_loc, uintptr_t mbox_base,
              int mbox_rows, int row0, uintptr_t beta_flag_host, uintptr_t msg_flag_dev, const Tensor& counters,
-             int K, int device, double timeout)
+             int K, int device, double timeout, uintptr_t beta_flag_dev)
       : g_(std::move(g)), inbox_(inbox), G_(G), n_(n_loc), mbox_(mbox_base), mbox_rows_(mbox_rows), row0_(row0),
-        bflag_(reinterpret_cast<const uint64_t*>(beta_flag_host)),
+        bflag_(reinterpret_cast<uint64_t*>(beta_flag_host)), bflag_dev_(reinterpret_cast<void*>(beta_flag_dev)),
         mflag_(reinterpret_cast<unsigned long long*>(msg_flag_dev)), counters_(counters), K_(K), timeout_(timeout) {
     need_gpu(inbox, "inbox");
     need_gpu(G, "G");
@@ -794,8 +794,16 @@ class WorkerPump {
     wait_s_.assign(R_, -1.0);
     const char* e = std::getenv("ERASUREHEAD_FUSED_PUT");
     fuse_put_ = g_->can_fuse_put(n_loc) && !(e && e[0] == '0');
+    // Device-side beta wait: the stream itself waits for the flag (hipStreamWaitValue64 on the
+    // host-registered shared flag), so round i's kernels are already queued when beta(i) lands
+    // instead of after a host wake-up + launch.  The host stays one round ahead and keeps the
+    // timeout.  beta_flag_dev = 0 selects the host-side wait (the caller's policy).
+    int can = 0;
+    if (bflag_dev_ && hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess)
+      dwait_ = can != 0;
   }
   bool fused_put() const { return fuse_put_; }
+  bool device_wait() const { return dwait_; }
   ~WorkerPump() {
     for (auto& t : tev_)
       for (auto e : t)
@@ -823,23 +831,19 @@ class WorkerPump {
   // did not arrive within the timeout.
   int run(int a, int b) {
     py::gil_scoped_release nogil;
-    using clk = std::chrono::steady_clock;
     for (int i = a; i < b; ++i) {
       need(i >= 0 && i < R_, "round out of range");
       Range tr("eh.worker.round");
-      const auto t0 = clk::now();
-      for (int spin = 0; __atomic_load_n(bflag_, __ATOMIC_ACQUIRE) < static_cast<uint64_t>(i + 1); ++spin) {
-        if (spin < 4096) {
-#if defined(__x86_64__)
-          _mm_pause();
-#endif
-          continue;
-        }
-        if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_) return i;
-        std::this_thread::sleep_for(std::chrono::microseconds(5));
+      if (dwait_) {
+        // enqueue round i once beta(i-1) is in: one round of lookahead, host timeout kept
+        if (i > a && !host_wait(i, i - 1)) return release(i - 1, b);
+        if (n_ == 0) continue;
+        hcheck(hipStreamWaitValue64(stream_, bflag_dev_, static_cast<uint64_t>(i + 1), hipStreamWaitValueGte),
+               "hipStreamWaitValue64(beta flag)");
+      } else {
+        if (!host_wait(i + 1, i)) return i;
+        if (n_ == 0) continue;
       }
-      wait_s_[i] = std::chrono::duration<double>(clk::now() - t0).count();
-      if (n_ == 0) continue;
       const int slot = i % K_;
       const char* beta = static_cast<const char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * ld_ * es_;
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
@@ -862,10 +866,37 @@ class WorkerPump {
       }
       if (timing_) record_t(i, 2);
     }
+    if (dwait_ && b > a && !host_wait(b, b - 1)) return release(b - 1, b);
     return -1;
   }
 
  private:
+  // Host poll until the beta flag reaches `target`; records the wait under round `rec`.
+  bool host_wait(uint64_t target, int rec) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (int spin = 0; __atomic_load_n(bflag_, __ATOMIC_ACQUIRE) < target; ++spin) {
+      if (spin < 4096) {
+#if defined(__x86_64__)
+        _mm_pause();
+#endif
+        continue;
+      }
+      if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(5));
+    }
+    wait_s_[rec] = std::chrono::duration<double>(clk::now() - t0).count();
+    return true;
+  }
+  // Timeout with device-side waits queued: the master is gone, so release this rank's own
+  // stream waits (store the flag value they wait for) and let the queued rounds drain on
+  // stale data instead of leaving a wait on the GPU.  Returns the round that timed out.
+  int release(int bad, int b) {
+    __atomic_store_n(bflag_, static_cast<uint64_t>(b), __ATOMIC_RELEASE);
+    hipStreamSynchronize(stream_);
+    return bad;
+  }
+
   void record_t(int i, int which) {
     hipEvent_t& e = tev_[i][which];
     if (!e) hcheck(hipEventCreate(&e), "hipEventCreate");
@@ -877,7 +908,8 @@ class WorkerPump {
   int n_;
   uintptr_t mbox_;
   int mbox_rows_, row0_;
-  const uint64_t* bflag_;
+  uint64_t* bflag_;
+  void* bflag_dev_ = nullptr;
   unsigned long long* mflag_;
   Tensor counters_;
   int K_;
@@ -886,6 +918,7 @@ class WorkerPump {
   hipStream_t stream_ = nullptr;
   bool timing_ = false;
   bool fuse_put_ = false;
+  bool dwait_ = false;
   std::vector<std::array<hipEvent_t, 3>> tev_;  // [round] gradient start, gradient end = put start, put end
   std::vector<double> wait_s_;                  // [round] host seconds spent waiting for beta
 };
@@ -947,9 +980,13 @@ void bind_engine(py::module& m) {
       .def("graphs_launched", &MasterPump::graphs_launched);
   py::class_<WorkerPump>(m, "WorkerPump")
       .def(py::init<std::shared_ptr<GradLauncher>, const Tensor&, const Tensor&, int, uintptr_t, int, int, uintptr_t,
-                    uintptr_t, const Tensor&, int, int, double>())
+                    uintptr_t, const Tensor&, int, int, double, uintptr_t>(),
+           py::arg("g"), py::arg("inbox"), py::arg("G"), py::arg("n_loc"), py::arg("mbox_base"), py::arg("mbox_rows"),
+           py::arg("row0"), py::arg("beta_flag_host"), py::arg("msg_flag_dev"), py::arg("counters"), py::arg("K"),
+           py::arg("device"), py::arg("timeout"), py::arg("beta_flag_dev") = 0)
       .def("run", &WorkerPump::run)
       .def_property_readonly("fused_put", &WorkerPump::fused_put)
+      .def_property_readonly("device_wait", &WorkerPump::device_wait)
       .def("set_timing", &WorkerPump::set_timing)
       .def("timing", &WorkerPump::timing);
 }

@@ -637,11 +637,20 @@ class Trainer:
         C = native_ext()
         dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
         w = env.world
+        # beta wait on the device stream (hipStreamWaitValue64) when this rank has its GPU to itself;
+        # ranks time-sharing one GPU keep the host wait (a queued wait competes with the other ranks'
+        # kernels there: profiles/r2_worker_wait/).  ERASUREHEAD_WORKER_WAIT=host|device|auto.
+        mode = os.environ.get("ERASUREHEAD_WORKER_WAIT", "auto")
+        buses = [p.get("master_bus") for p in tx.pairs[:1]] + [p.get("bus") for p in tx.pairs]
+        shared = len(set(buses)) < len(buses)
+        dwait = mode == "device" or (mode == "auto" and not shared)
         pump = C.WorkerPump(self.plan.native_launcher(), tx.inbox, self.G, self.n_loc, tx.rremote.ptr,
                             tx.mbox_rows, tx.my_row0, tx.flags.host_addr(env.rank), tx.flags.dev_addr(w + env.rank),
-                            tx.counters, K, dev, float(cfg.round_timeout))
+                            tx.counters, K, dev, float(cfg.round_timeout),
+                            tx.flags.dev_addr(env.rank) if dwait else 0)
         pump.set_timing(bool(cfg.instrument))
         self.rank_stats["fused_put"] = bool(pump.fused_put)
+        self.rank_stats["device_wait"] = bool(pump.device_wait)
         cut = timed_start if timed_start is not None and start <= timed_start < R else None
         segments = [(start, cut), (cut, R)] if cut is not None else [(start, R)]
         t0 = None

@@ -182,7 +182,6 @@ def test_arrival_sets_replay_reference_delays(case, k):
         d = np.random.RandomState(i).exponential(mean, W)
         ready = np.maximum(T, fin) + d
         order = list(np.argsort(ready, kind="stable"))
-        close = np.min(np.diff(np.sort(ready))) < 2e-3  # too close for wall-clock scheduling noise
         # the oracle stop rule on the arrival order
         got_groups, used = set(), []
         for w in order:
@@ -196,10 +195,14 @@ def test_arrival_sets_replay_reference_delays(case, k):
                 break
         fin = ready
         T = float(np.max(ready)) if tr.drain else float(ready[used[-1]])
-        if close:
+        # the used SET is decided at the stop boundary: skip rounds where the last used and the
+        # first unused worker are too close for wall-clock scheduling noise (a loaded CPU)
+        nxt = ready[order[len(used)]] if len(used) < W else np.inf
+        if nxt - ready[used[-1]] < 3e-3:
             continue
         arrived = [w for (w, p, _) in res.arrivals[i]]
-        assert arrived == used, (i, arrived, used)
+        assert sorted(arrived) == sorted(used), (i, arrived, used)
+        assert arrived[-1] in {w for w in used if ready[used[-1]] - ready[w] < 3e-3}, (i, arrived, used)
         if sch.marks_unused:
             assert set(np.where(res.worker_timeset[i] == -1)[0]) == set(range(W)) - set(used)
 

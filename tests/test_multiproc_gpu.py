@@ -24,8 +24,8 @@ def _port():
     return p
 
 
-def _launch(world, case_i, rule, out, delay=0.0):
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+def _launch(world, case_i, rule, out, delay=0.0, **extra_env):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", **extra_env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(HERE, "mp_engine_run.py"),
            out, str(case_i), rule, str(delay)]
@@ -58,6 +58,22 @@ def test_ipc_many_ranks(world, case_i, tmp_path):
     r = _launch(world, case_i, "AGD", str(tmp_path / "m.npz"))
     assert str(r["transport"]) == "ipc"
     cfg, src, sch, parts = make(CASES[case_i], "AGD")
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.parametrize("wait,fused", [("device", "1"), ("host", "0"), ("device", "0")])
+def test_ipc_worker_wait_and_put_modes(wait, fused, tmp_path):
+    """Worker rounds with the beta wait on the device stream (hipStreamWaitValue64; the default
+    when a rank has its GPU to itself) or on the host, and with the message put fused into the
+    final reduction or as its own kernel: every combination matches the oracle replay."""
+    from oracle import replay
+    from test_engine_cpu import CASES, make
+
+    r = _launch(3, 1, "AGD", str(tmp_path / "w.npz"), ERASUREHEAD_WORKER_WAIT=wait, ERASUREHEAD_FUSED_PUT=fused)
+    assert str(r["transport"]) == "ipc"
+    cfg, src, sch, parts = make(CASES[1], "AGD")
     arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
     ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
