@@ -518,9 +518,9 @@ class MasterPump {
   // Every message is local and finishes with the one gradient launch, so the arrival order
   // (and with it the decode) is fixed before the GPU runs: the collector still decides it,
   // from host probes seen at the round start (ties break by the collector's seeded per-round
-  // permutation, exactly like the simultaneous HIP-event probes of begin()).  The host decodes rounds [a, b) up front and
-  // enqueues  grad(i) -> combine_update(i)  back to back, so the device never waits for the
-  // host between rounds.  With `graph` the whole segment is captured into hipGraphs (at most
+  // permutation, exactly like the simultaneous HIP-event probes of begin()).  The host decodes round i and
+  // enqueues  grad(i) -> combine_update(i)  while the GPU still runs earlier rounds, so the
+  // device never waits for the host between rounds.  With `graph` the whole segment is captured into hipGraphs (at most
   // kGraphRounds rounds each) and replayed with one launch per graph.
   // stamps: int64 GPU [R + 1]; stamps[a] = device time before round a, stamps[i + 1] = start
   // of round i's update (its messages are done).  Returns the arrivals of every round.
@@ -535,20 +535,23 @@ class MasterPump {
       for (int w = 0; w < W_; ++w) need(delays_[static_cast<int64_t>(i) * W_ + w] == 0.0, "injected delay present");
     std::vector<std::vector<eh::Arrival>> arrs;
     std::vector<std::vector<std::pair<const void*, double>>> useds;
-    {
+    arrs.reserve(b - a);
+    useds.reserve(b - a);
+    auto decode_round = [&](int i) {
+      const double t = eh::Collector::now();
+      col_->begin_round(i, t, stop_rule_, k_);
+      t_start_[i] = t;
+      for (const auto& m : local_) col_->mark_seen(col_->add_host_probe(m.w, m.p, i, 0.0), t);
+      need(col_->wait(timeout_), "local arrivals did not satisfy the stop rule");
+      std::vector<std::pair<const void*, double>> used;
+      need(decode(i, col_->arrivals(), used), "completion pattern missing from the decode table");
+      arrs.push_back(col_->arrivals());
+      useds.push_back(std::move(used));
+      if (drain_) col_->drain(i, timeout_);
+    };
+    if (graph) {  // a captured segment needs every round decoded before the capture
       Range tr("eh.master.decode_ahead");
-      for (int i = a; i < b; ++i) {
-        const double t = eh::Collector::now();
-        col_->begin_round(i, t, stop_rule_, k_);
-        t_start_[i] = t;
-        for (const auto& m : local_) col_->mark_seen(col_->add_host_probe(m.w, m.p, i, 0.0), t);
-        need(col_->wait(timeout_), "local arrivals did not satisfy the stop rule");
-        std::vector<std::pair<const void*, double>> used;
-        need(decode(i, col_->arrivals(), used), "completion pattern missing from the decode table");
-        arrs.push_back(col_->arrivals());
-        useds.push_back(std::move(used));
-        if (drain_) col_->drain(i, timeout_);
-      }
+      for (int i = a; i < b; ++i) decode_round(i);
     }
     long long* st = reinterpret_cast<long long*>(stamps.data_ptr<int64_t>());
     char* bin = static_cast<char*>(beta_in_.data_ptr());
@@ -569,6 +572,9 @@ class MasterPump {
     } restore{stream_, caller};
     auto enqueue = [&](int i0, int i1) {
       for (int i = i0; i < i1; ++i) {
+        // stream mode: decode round i just before enqueueing it, so the host decodes round i + 1
+        // while the GPU runs round i (no host-only stretch at the start of a timed segment)
+        if (!graph) decode_round(i);
         const int slot = i % K_;
         char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
         hcheck(launcher_->launch(bin + static_cast<int64_t>(i) * ld_ * es_, g, stream_), "local gradient");

@@ -437,6 +437,8 @@ class Trainer:
             loop_time[i] = col.now() - t_start
             if cfg.checkpoint_every and (i + 1) % cfg.checkpoint_every == 0:
                 self._checkpoint(i + 1, timeset, worker_timeset)
+        if timed_start is not None:  # rounds complete on every rank at the fence (see the native loop)
+            t_timed1 = self._timed_fence()
         col.drain(R - 1, max(cfg.round_timeout, 60.0))
         col.close()
         if cfg.verify_beta and env.world > 1:
@@ -445,8 +447,6 @@ class Trainer:
             torch.cuda.synchronize(env.device)
             for i, ev0, ev1 in upd_events:  # + the update kernel's own duration (reference: decode + update)
                 timeset[i] += 1e-3 * ev0.elapsed_time(ev1)
-        if timed_start is not None:
-            t_timed1 = self._timed_fence()
         self._sync()
         env.barrier()
         total = time.perf_counter() - orig_start
@@ -541,6 +541,8 @@ class Trainer:
                             log(report.iteration_tick(i))
                 arrs = pump.run_local(a, b, device_mode == "graph", stamps)
                 arrivals_log.extend(arrs)
+            if timed_start is not None:  # the rounds are done: stop the clock before the host bookkeeping
+                t_timed1 = self._timed_fence()
             self._sync()
             st = stamps.cpu().numpy().astype(np.float64)
             for i in range(start, R):
@@ -588,6 +590,10 @@ class Trainer:
             arrivals_log.append([(a.worker, a.part, a.t_rel) for a in arrivals])
             if cfg.checkpoint_every and (i + 1) % cfg.checkpoint_every == 0:
                 self._checkpoint(i + 1, timeset, worker_timeset)
+        if timed_start is not None and not device_mode:
+            # every rank's rounds are complete once all ranks pass the fence (workers' puts have landed
+            # before their barrier); the straggler drain and bookkeeping below are not round time
+            t_timed1 = self._timed_fence()
         col.drain(R - 1, max(cfg.round_timeout, 60.0))
         upd = pump.update_ms()
         if not device_mode:
@@ -600,8 +606,6 @@ class Trainer:
                                **{f"{k}_us": float(1e6 * np.mean(v[a0 - start:]))
                                   for k, v in self.timer.t.items() if len(v) > a0 - start})
         col.close()
-        if timed_start is not None:
-            t_timed1 = self._timed_fence()
         self._sync()
         env.barrier()
         total = time.perf_counter() - orig_start
@@ -715,10 +719,10 @@ class Trainer:
             if bsum is not None:  # beta must be unchanged after the gradient read it
                 bsum[i, 1] = b.double().sum()
         tx.finish()
+        if timed_start is not None:  # same collective order as the master: fence, then the race check
+            self.worker_timed_seconds = self._timed_fence() - t0
         if bsum is not None:
             env.gather_objects(bsum.cpu().numpy())
-        if timed_start is not None:
-            self.worker_timed_seconds = self._timed_fence() - t0
         a0 = (timed_start or 0) - start
         self.rank_stats.update({f"{k}_us": float(1e6 * np.mean(v[a0:])) for k, v in self.timer.t.items()
                                 if len(v) > a0})

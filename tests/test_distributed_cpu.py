@@ -29,6 +29,7 @@ def _worker(rank, world, port, case, rule, out_path, extra):
     env = init_distributed("cpu")
     extra = dict(extra)
     corrupt = extra.pop("corrupt", False)
+    timed_start = extra.pop("timed_start", None)
     cfg, src, sch, parts = make(case, rule, **extra)
     if extra.get("delay_mode"):
         cfg.add_delay = 1
@@ -36,10 +37,11 @@ def _worker(rank, world, port, case, rule, out_path, extra):
     if corrupt and not env.is_master:  # simulate a buffer overwritten while the gradient reads it
         run = tr.plan.run
         tr.plan.run = lambda b, G: (run(b, G), b.add_(1e-9))[0]
-    res = tr.run()
+    res = tr.run(timed_start=timed_start)
     if env.is_master:
         np.savez(out_path, betaset=res.betaset, ws=res.worker_timeset, arrivals=np.array(
-            [[(w, p) for (w, p, _) in a] for a in res.arrivals], dtype=object), beta0=tr.beta0)
+            [[(w, p) for (w, p, _) in a] for a in res.arrivals], dtype=object), beta0=tr.beta0,
+            timed=np.array(res.timed_seconds if res.timed_seconds is not None else -1.0))
     env.barrier()
     env.shutdown()
 
@@ -96,3 +98,11 @@ def test_world8_headline_placement_matches_replay(shard, tmp_path):
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-10, atol=1e-12)
     for a in r["arrivals"]:  # every message counted once, after all its shards
         assert len({(w, p) for (w, p) in a}) == len(a)
+
+
+def test_multiprocess_timed_rounds_with_race_check(tmp_path):
+    """Timed rounds (the bench's fence: sync + barrier right after the last round) together with the
+    beta race detector's gather: master and workers issue the collectives in the same order."""
+    case = (1, 0, 3, 7, 2, 4)
+    r = _run(2, case, "AGD", tmp_path, verify_beta=True, timed_start=2)
+    assert r["betaset"].shape[0] == 6 and float(r["timed"]) > 0
