@@ -6,6 +6,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 namespace eh {
@@ -197,6 +198,25 @@ __device__ __forceinline__ A sigmoid_neg(A t) {
     return e / (A(1) + e);
   }
   return A(1) / (A(1) + exp(t));
+}
+
+// Branch-free fp32 sigmoid on the hardware exp2 and reciprocal (each within ~1 ulp): e =
+// exp(-|t|) is in (0, 1], so 1 + e is in [1, 2] and neither can overflow.  Used where a wave's
+// lanes hold different rows (the MFMA bundles: 0.382 -> 0.371 ms at the bf16 headline).  The
+// fp32 staged pair kernel measured SLOWER with it (0.737 -> 0.81 ms, same box,
+// profiles/r2_ab_fastsig), so the library form stays the default elsewhere.
+__device__ __forceinline__ float sigmoid_neg_hw(float t) {
+  const float e = __builtin_amdgcn_exp2f(-__builtin_fabsf(t) * 1.4426950408889634f);
+  const float q = __builtin_amdgcn_rcpf(1.0f + e);
+  return t > 0.f ? e * q : q;
+}
+template <int LOSS>
+__device__ __forceinline__ float residual_hw(float z, float y, float coef) {
+  if constexpr (LOSS == kLogistic) {
+    return -(coef * y) * sigmoid_neg_hw(y * z);
+  } else {
+    return -2.f * coef * (y - z);
+  }
 }
 
 // Branch-free form for waves whose lanes hold different rows (one exp either way).

@@ -189,7 +189,7 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
       float zs = 0.f;
 #pragma unroll
       for (int v = 0; v < kMfNW; ++v) zs += zred[(v * 16 + rm) * kMfS + rn];
-      const float r = rm < R && rn < ns ? residual<LOSS, float>(zs, lab[rn], rcoef) : 0.f;
+      const float r = rm < R && rn < ns ? residual_hw<LOSS>(zs, lab[rn], rcoef) : 0.f;
       __bf16 t[kMfSplit];
       split_bf16(r, t);
 #pragma unroll

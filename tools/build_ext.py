@@ -45,8 +45,11 @@ def _hash_inputs(csrc: str = CSRC):
 
 
 def _defines():
-    """Build-time debug switches (part of the provenance hash)."""
-    return ["-DEH_FULL_VMCNT"] if os.environ.get("ERASUREHEAD_FULL_VMCNT") == "1" else []
+    """Build-time debug / A-B switches (part of the provenance hash)."""
+    d = []
+    if os.environ.get("ERASUREHEAD_FULL_VMCNT") == "1":
+        d.append("-DEH_FULL_VMCNT")
+    return d
 
 
 def source_hash(csrc: str = CSRC) -> str:
