@@ -385,6 +385,17 @@ class MasterPump {
     }
   }
 
+  // Device-side drain (after_combine): (host address, device address) of every worker rank's
+  // message flag.  Empty = the host drains before pushing the next beta.
+  void set_drain_flags(const std::vector<std::pair<uintptr_t, uintptr_t>>& flags) {
+    for (const auto& f : flags) need(f.first != 0 && f.second != 0, "null drain flag");
+    int can = 0;
+    need(flags.empty() ||
+             (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device_) == hipSuccess && can),
+         "device-side drain needs hipStreamWaitValue64 support");
+    drain_flags_ = flags;
+  }
+
   // beta pushes: (inbox base device pointer [R+1, ld], flag device address) per worker rank
   void set_puts(const std::vector<std::pair<uintptr_t, uintptr_t>>& targets, const Tensor& counters) {
     need(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.numel() >= (int64_t)targets.size(),
@@ -438,22 +449,7 @@ class MasterPump {
     t_start_[i] = t;
     char* bin = static_cast<char*>(beta_in_.data_ptr());
     const void* src = bin + static_cast<int64_t>(i) * ld_ * es_;
-    if (timing_ && !targets_.empty()) record_t(i, 0);
-    // push beta(i) into every worker inbox
-    for (size_t k0 = 0; k0 < targets_.size(); k0 += eh::kMaxPuts) {
-      eh::PutArgs a{};
-      a.n = 0;
-      for (size_t k = k0; k < targets_.size() && a.n < eh::kMaxPuts; ++k) {
-        a.d[a.n] = eh::PutDesc{src, reinterpret_cast<char*>(targets_[k].first) + static_cast<int64_t>(i) * ld_ * es_,
-                               static_cast<long long>(ld_) * es_,
-                               reinterpret_cast<unsigned long long*>(targets_[k].second),
-                               static_cast<unsigned long long>(i + 1),
-                               reinterpret_cast<unsigned int*>(counters_.data_ptr<int>()) + k};
-        ++a.n;
-      }
-      hcheck(eh::put_signal_launch(a, blocks_for(static_cast<long long>(ld_) * es_), stream_), "put_signal(beta)");
-    }
-    if (timing_ && !targets_.empty()) record_t(i, 1);
+    if (i != prepub_) put_beta(i);  // else already queued behind the device-side drain of round i-1
     const double* dl = delays_.data() + static_cast<int64_t>(i) * W_;
     if (n_loc_ > 0 && launcher_) {
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
@@ -730,13 +726,61 @@ class MasterPump {
     if (events) hcheck(hipEventRecord(ev.second, stream_), "hipEventRecord");
   }
 
+  // push beta(j) into every worker inbox (put + signal kernels on the pump stream)
+  void put_beta(int j) {
+    if (targets_.empty()) return;
+    const void* src = static_cast<const char*>(beta_in_.data_ptr()) + static_cast<int64_t>(j) * ld_ * es_;
+    if (timing_) record_t(j, 0);
+    for (size_t k0 = 0; k0 < targets_.size(); k0 += eh::kMaxPuts) {
+      eh::PutArgs a{};
+      a.n = 0;
+      for (size_t k = k0; k < targets_.size() && a.n < eh::kMaxPuts; ++k) {
+        a.d[a.n] = eh::PutDesc{src, reinterpret_cast<char*>(targets_[k].first) + static_cast<int64_t>(j) * ld_ * es_,
+                               static_cast<long long>(ld_) * es_,
+                               reinterpret_cast<unsigned long long*>(targets_[k].second),
+                               static_cast<unsigned long long>(j + 1),
+                               reinterpret_cast<unsigned int*>(counters_.data_ptr<int>()) + k};
+        ++a.n;
+      }
+      hcheck(eh::put_signal_launch(a, blocks_for(static_cast<long long>(ld_) * es_), stream_), "put_signal(beta)");
+    }
+    if (timing_) record_t(j, 1);
+  }
+
+  bool no_delay(int i) const {
+    const double* dl = delays_.data() + static_cast<int64_t>(i) * W_;
+    return std::all_of(dl, dl + W_, [](double x) { return x == 0.0; });
+  }
+
   double after_combine(int i, bool publish_next) {
-    if (drain_) {
+    const bool next = publish_next && i + 1 < R_;
+    if (drain_ && next && !drain_flags_.empty() && no_delay(i) && no_delay(i + 1)) {
+      // Device-side drain: the pump stream waits until every worker rank's round-i flag is set
+      // (hipStreamWaitValue64 on the shared flags), then pushes beta(i+1) — queued now, so the
+      // put leaves as soon as the last message lands instead of after a host wake-up + launch.
+      // The host drain below still gates the round's bookkeeping (t_start of round i+1).
+      for (const auto& f : drain_flags_)
+        hcheck(hipStreamWaitValue64(stream_, reinterpret_cast<void*>(f.second), static_cast<uint64_t>(i + 1),
+                                    hipStreamWaitValueGte),
+               "hipStreamWaitValue64(message flag)");
+      put_beta(i + 1);
+      prepub_ = i + 1;
+      Range tr("eh.master.drain");
+      if (!col_->drain(i, timeout_)) {
+        // a worker rank is gone: release the queued waits (store the value they wait for) so no
+        // wait is left on the GPU; its late message, if any, lands in a slot nobody reads
+        for (const auto& f : drain_flags_) {
+          auto* h = reinterpret_cast<uint64_t*>(f.first);
+          if (__atomic_load_n(h, __ATOMIC_ACQUIRE) < static_cast<uint64_t>(i + 1))
+            __atomic_store_n(h, static_cast<uint64_t>(i + 1), __ATOMIC_RELEASE);
+        }
+      }
+    } else if (drain_) {
       Range tr("eh.master.drain");
       col_->drain(i, timeout_);
     }
     const double t_end = eh::Collector::now();
-    if (publish_next && i + 1 < R_) begin(i + 1);
+    if (next) begin(i + 1);
     return t_end;
   }
 
@@ -757,6 +801,8 @@ class MasterPump {
   std::vector<Msg> local_, remote_;
   std::vector<std::vector<std::pair<int, int>>> index_;  // [2*w+p] -> (0 local | 1 remote, row) per shard
   std::vector<std::pair<uintptr_t, uintptr_t>> targets_;
+  std::vector<std::pair<uintptr_t, uintptr_t>> drain_flags_;
+  int prepub_ = -1;  // round whose beta after_combine already queued behind the device-side drain
   std::vector<double> decay_, gm_, l2_, theta_, delays_;
   int update_rule_ = 0, stop_rule_ = 0, k_ = 0;
   bool drain_ = false;
@@ -972,6 +1018,7 @@ void bind_engine(py::module& m) {
       .def("set_local", &MasterPump::set_local)
       .def("set_remote", &MasterPump::set_remote)
       .def("set_puts", &MasterPump::set_puts)
+      .def("set_drain_flags", &MasterPump::set_drain_flags)
       .def("set_schedule", &MasterPump::set_schedule)
       .def("set_decode", &MasterPump::set_decode)
       .def("add_table", &MasterPump::add_table)

@@ -505,6 +505,9 @@ class Trainer:
             pump.set_remote(self.Rbuf, rem)
             pump.set_puts([(tx.inbox_remote[r].data_ptr(), tx.flags.dev_addr(r)) for r in range(1, env.world)],
                           tx.counters)
+            if self._device_waits(tx):  # drain on the device: beta(i+1) leaves as the last message lands
+                pump.set_drain_flags([(tx.flags.host_addr(env.world + r), tx.flags.dev_addr(env.world + r))
+                                      for r in sorted(self.remote_msgs) if self.remote_msgs[r]])
         eta = cfg.eta()
         co = [self.update.coeffs(i, float(eta[i])) for i in range(R)]
         delay_table = np.stack([self.delay.delays(i) for i in range(R)])
@@ -634,6 +637,17 @@ class Trainer:
             return None
         return "graph" if mode == "graph" else "stream"
 
+    @staticmethod
+    def _device_waits(tx) -> bool:
+        """Stream-side waits on the shared flags (hipStreamWaitValue64): a worker's wait for beta and
+        the master's drain before the next beta.  On when every rank has its GPU to itself; ranks
+        time-sharing one GPU keep host waits (a queued wait competes with the other ranks' kernels
+        there: profiles/r2_worker_wait/).  ERASUREHEAD_WORKER_WAIT=host|device|auto."""
+        mode = os.environ.get("ERASUREHEAD_WORKER_WAIT", "auto")
+        buses = [p.get("master_bus") for p in tx.pairs[:1]] + [p.get("bus") for p in tx.pairs]
+        shared = len(set(buses)) < len(buses)
+        return mode == "device" or (mode == "auto" and not shared)
+
     def _worker_loop_native(self, timed_start, start: int = 0) -> None:
         """Worker rounds in csrc/runtime/engine.cpp (WorkerPump) over the IPC mailbox."""
         cfg, env, tx = self.cfg, self.env, self.tx
@@ -641,13 +655,7 @@ class Trainer:
         C = native_ext()
         dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
         w = env.world
-        # beta wait on the device stream (hipStreamWaitValue64) when this rank has its GPU to itself;
-        # ranks time-sharing one GPU keep the host wait (a queued wait competes with the other ranks'
-        # kernels there: profiles/r2_worker_wait/).  ERASUREHEAD_WORKER_WAIT=host|device|auto.
-        mode = os.environ.get("ERASUREHEAD_WORKER_WAIT", "auto")
-        buses = [p.get("master_bus") for p in tx.pairs[:1]] + [p.get("bus") for p in tx.pairs]
-        shared = len(set(buses)) < len(buses)
-        dwait = mode == "device" or (mode == "auto" and not shared)
+        dwait = self._device_waits(tx)
         pump = C.WorkerPump(self.plan.native_launcher(), tx.inbox, self.G, self.n_loc, tx.rremote.ptr,
                             tx.mbox_rows, tx.my_row0, tx.flags.host_addr(env.rank), tx.flags.dev_addr(w + env.rank),
                             tx.counters, K, dev, float(cfg.round_timeout),

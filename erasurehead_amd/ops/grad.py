@@ -142,7 +142,7 @@ class DenseGradPlan:
         # (measured 1.58 vs 1.80 ms fp64, 0.89 vs 0.99 ms fp32 at the headline; bf16 rows are
         # too short to pay for the staging: 0.70 vs 0.66 ms, docs/PERF_NOTES.md).
         # ERASUREHEAD_STAGED=0 / 1 / pair overrides (pair: two rows share one reduction and one
-        # residual evaluation — measured slower, kept for sweeps).
+        # residual evaluation; the default for fp32 and sharded ranks, see below).
         staged_env = os.environ.get("ERASUREHEAD_STAGED", "")
         staged_ok = shared and self.cpl is not None and self.cpl <= MAX_CPL
         self.staged = staged_ok and (staged_env in ("1", "pair") or (staged_env == "" and prec.code in (0, 1)))
