@@ -33,10 +33,19 @@ combine_update(const CombineArgs args, double* __restrict__ beta, double* __rest
     if (beta_w) beta_w[c] = W(0);
     return;
   }
+  // The message rows are independent loads (remote ones in fine-grained memory, ~µs each): issue
+  // them eight at a time, then accumulate in message order (the same fma chain, bitwise, as a
+  // one-at-a-time loop).
   double g = 0.0;
-  for (int m = 0; m < args.nmsg; ++m) {
-    const M* p = static_cast<const M*>(args.msg[m]);
-    g = fma(args.coef[m], static_cast<double>(p[c]), g);
+  constexpr int kBatch = 8;
+  for (int m0 = 0; m0 < args.nmsg; m0 += kBatch) {
+    double v[kBatch];
+#pragma unroll
+    for (int k = 0; k < kBatch; ++k)
+      v[k] = m0 + k < args.nmsg ? static_cast<double>(static_cast<const M*>(args.msg[m0 + k])[c]) : 0.0;
+#pragma unroll
+    for (int k = 0; k < kBatch; ++k)
+      if (m0 + k < args.nmsg) g = fma(args.coef[m0 + k], v[k], g);
   }
   const double b = beta[c];
   double nb;
