@@ -13,16 +13,20 @@ data/synthetic.py onehot_partitions):
                      injected Exp(0.05) delays (forced; the reference only relies on natural stragglers;
                      mean 0.05 s instead of 0.5 s keeps the run short — floors scale linearly)
   avoid_covtype      ignore-stragglers, same data, W=8 s=1, forced delays
+  naive_covtype      naive on the same 8-partition covtype-shaped data (the family's loss target)
   agc_covtype        AGC on the covtype-shaped data without delays (sparse kernel throughput)
   ls_kc_house_*      least squares on kc_house-shaped one-hot (17290 x 27654): naive vs AGC with
                      num_collect in {4,5,6,7}, W=8 s=1
   agc_amazon         AGC W=8 s=1 k=6 on amazon-shaped one-hot (26215 x 241915, 45 nnz/row; 1.94 MB
                      messages), host-driven with HIP-event instrumentation (gradient / combine+update
-                     kernel microseconds).  Synthetic stand-in: parity unpinned.
+                     kernel microseconds), and naive on the same data (the family's loss target).
+                     Synthetic stand-in: parity unpinned.
 
 Per config: seconds per round (timed, device-synchronised), time-to-decode (reference
-``timeset``), iterations to the training-loss floor (within 1 % of the best loss over the
-run), and for delayed runs the deterministic injected-delay floor and the overhead above it
+``timeset``), iterations to the COMMON loss target of its data family (the naive run on the same
+data: final training loss + 1 %; "-" if never reached or the family has no naive run), the
+iterations to the run's own floor (within 1 % of its best loss; not comparable across schemes),
+and for delayed runs the deterministic injected-delay floor and the overhead above it
 (SURVEY §6).  Writes suite.jsonl and suite.md.
 """
 from __future__ import annotations
@@ -42,6 +46,11 @@ sys.path.insert(0, ROOT)
 def _floor_iters(tl: np.ndarray) -> int:
     floor = float(np.min(tl))
     return int(np.argmax(tl <= floor + 0.01 * abs(floor)))
+
+
+def _target_iters(tl, target):
+    hit = np.nonzero(np.asarray(tl) <= target)[0]
+    return int(hit[0]) + 1 if hit.size else None
 
 
 def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_kw=None, device_loop="auto",
@@ -76,6 +85,7 @@ def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_
         "sum_timeset_s": float(np.sum(res.timeset)),
         "iters_to_loss_floor": _floor_iters(ev.training_loss),
         "final_train_loss": float(ev.training_loss[-1]),
+        "train_loss": [float(x) for x in ev.training_loss],
         "final_test_loss": float(ev.testing_loss[-1]),
         "final_auc": float(ev.auc[-1]) if not tr.loss else None,
         "setup_s": setup,
@@ -116,11 +126,12 @@ def main():
     dense = dict(n_procs=9, n_rows=n_dense, n_cols=1000, input_dir="/tmp/eh_suite/", is_real=0, dataset="synthetic",
                  data="synthetic", data_seed=1234, update_rule="AGD")
     configs = []
-    configs.append(("naive_dense", dict(dense, is_coded=0), None, None))
+    # (name, RunConfig kwargs, data source, delay-floor kwargs, instrumented, data family)
+    configs.append(("naive_dense", dict(dense, is_coded=0), None, None, False, "dense"))
     configs.append(("agc_dense", dict(dense, is_coded=1, n_stragglers=2, coded_ver=3, num_collect=6,
-                                      allow_uneven_groups=True), None, None))
-    configs.append(("cyclic_dense", dict(dense, is_coded=1, n_stragglers=2, coded_ver=0), None, None))
-    configs.append(("frc_dense", dict(dense, is_coded=1, n_stragglers=1, coded_ver=1), None, None))
+                                      allow_uneven_groups=True), None, None, False, "dense"))
+    configs.append(("cyclic_dense", dict(dense, is_coded=1, n_stragglers=2, coded_ver=0), None, None, False, "dense"))
+    configs.append(("frc_dense", dict(dense, is_coded=1, n_stragglers=1, coded_ver=1), None, None, False, "dense"))
 
     # covtype-shaped one-hot; partial schemes need (P - s) * W partition files
     n_cov, d_cov, f_cov = REAL_SHAPES["covtype"]
@@ -132,14 +143,16 @@ def main():
     base_cov = dict(n_procs=W + 1, n_rows=n_pr, n_cols=dc, input_dir="/tmp/eh_suite/", is_real=1, dataset="covtype",
                     update_rule="AGD", add_delay=1, force_delay=True, delay_mean=0.05)
     configs.append(("partialrep_covtype", dict(base_cov, is_coded=1, n_stragglers=s, partitions=P, coded_ver=1),
-                    src_pr, {"stop_count": W}))
+                    src_pr, {"stop_count": W}, False, "covtype_24parts"))
     cov8, cov8_test, _ = onehot_partitions(n_cov, d_cov, f_cov, W, seed=3)
     n8 = sum(p[0].shape[0] for p in cov8)
     src8 = ArraySource(cov8, cov8_test, sparse=True)
+    configs.append(("naive_covtype", dict(base_cov, n_rows=n8, is_coded=0, add_delay=0, force_delay=False), src8,
+                    None, False, "covtype"))
     configs.append(("avoid_covtype", dict(base_cov, n_rows=n8, is_coded=1, n_stragglers=s, coded_ver=2),
-                    src8, {"stop_count": W - s, "carry": True}))
+                    src8, {"stop_count": W - s, "carry": True}, False, "covtype"))
     configs.append(("agc_covtype", dict(base_cov, n_rows=n8, is_coded=1, n_stragglers=s, coded_ver=3, num_collect=6,
-                                        add_delay=0, force_delay=False), src8, None))
+                                        add_delay=0, force_delay=False), src8, None, False, "covtype"))
 
     n_kc, d_kc, f_kc = REAL_SHAPES["kc_house_data"]
     kc, kc_test, dk = onehot_partitions(n_kc, d_kc, f_kc, W, seed=5, least_squares=True)
@@ -147,43 +160,56 @@ def main():
     nk = sum(p[0].shape[0] for p in kc)
     base_kc = dict(n_procs=W + 1, n_rows=nk, n_cols=dk, input_dir="/tmp/eh_suite/", is_real=1,
                    dataset="kc_house_data", update_rule="AGD", loss="least_squares", lr=0.2)
-    configs.append(("ls_kc_house_naive", dict(base_kc, is_coded=0), src_kc, None))
+    configs.append(("ls_kc_house_naive", dict(base_kc, is_coded=0), src_kc, None, False, "kc_house"))
     for k in (4, 5, 6, 7):
         configs.append((f"ls_kc_house_agc_k{k}", dict(base_kc, is_coded=1, n_stragglers=1, coded_ver=3,
-                                                      num_collect=k), src_kc, None))
+                                                      num_collect=k), src_kc, None, False, "kc_house"))
     n_am, d_am, f_am = REAL_SHAPES["amazon-dataset"]
     am, am_test, da = onehot_partitions(n_am // scale, d_am, f_am, W, seed=21)
     src_am = ArraySource(am, am_test, sparse=True)
     na = sum(p[0].shape[0] for p in am)
-    configs.append(("agc_amazon", dict(n_procs=W + 1, n_rows=na, n_cols=da, input_dir="/tmp/eh_suite/", is_real=1,
-                                       dataset="amazon-dataset", update_rule="AGD", is_coded=1, n_stragglers=1,
-                                       coded_ver=3, num_collect=6), src_am, None, True))
+    base_am = dict(n_procs=W + 1, n_rows=na, n_cols=da, input_dir="/tmp/eh_suite/", is_real=1,
+                   dataset="amazon-dataset", update_rule="AGD")
+    configs.append(("naive_amazon", dict(base_am, is_coded=0), src_am, None, False, "amazon"))
+    configs.append(("agc_amazon", dict(base_am, is_coded=1, n_stragglers=1, coded_ver=3, num_collect=6), src_am, None,
+                    True, "amazon"))
     if a.only:
         keep = set(a.only.split(","))
         configs = [c for c in configs if c[0] in keep]
     os.makedirs(a.out, exist_ok=True)
     rows = []
     with open(os.path.join(a.out, "suite.jsonl"), "w") as f:
-        for name, kw, src, floor_kw, *inst in configs:
-            r = run_config(name, kw, src, delay_floor_kw=floor_kw, device_loop=a.device_loop,
-                           instrument=bool(inst and inst[0]))
+        for name, kw, src, floor_kw, inst, fam in configs:
+            r = run_config(name, kw, src, delay_floor_kw=floor_kw, device_loop=a.device_loop, instrument=inst)
+            r["family"] = fam
             rows.append(r)
             f.write(json.dumps(r) + "\n")
             f.flush()
             print(json.dumps(r), flush=True)
-    hdr = ("| config | scheme | W | s | k | loop | ms/round | timeset ms | iters to floor | final train loss | AUC | "
-           "delay floor s | overhead ms/round | msg KB | grad µs | combine µs | eval s |\n"
-           "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|\n")
+    # common target per data family: the naive run's final training loss + 1 %
+    targets = {r["family"]: r["final_train_loss"] + 0.01 * abs(r["final_train_loss"])
+               for r in rows if r["scheme"] == "naive"}
+    for r in rows:
+        t = targets.get(r["family"])
+        r["loss_target"] = t
+        r["iters_to_target"] = _target_iters(r["train_loss"], t) if t is not None else None
+    hdr = ("| config | scheme | W | s | k | loop | ms/round | timeset ms | iters to naive target | iters to own floor | "
+           "final train loss | AUC | delay floor s | overhead ms/round | msg KB | grad µs | combine µs | eval s |\n"
+           "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|\n")
     lines = []
     for r in rows:
+        tgt = "-" if r["iters_to_target"] is None else str(r["iters_to_target"])
         auc = "%.4f" % r["final_auc"] if r.get("final_auc") is not None else "-"
         fl = "%.2f" % r["delay_floor_s"] if "delay_floor_s" in r else "-"
         ov = "%.3f" % r["overhead_above_floor_ms_per_round"] if "delay_floor_s" in r else "-"
         lines.append(f"| {r['config']} | {r['scheme']} | {r['W']} | {r['s']} | {r['num_collect']} | {r['round_loop']} | "
-                     f"{1e3 * r['sec_per_round']:.3f} | {r['timeset_mean_ms']:.3f} | {r['iters_to_loss_floor']} | "
+                     f"{1e3 * r['sec_per_round']:.3f} | {r['timeset_mean_ms']:.3f} | {tgt} | {r['iters_to_loss_floor']} | "
                      f"{r['final_train_loss']:.5f} | {auc} | {fl} | {ov} | {r['message_bytes'] / 1024:.0f} | "
                      f"{r.get('kernel_us', r.get('grad_kernel_us_isolated') or 0):.0f} | "
                      f"{r.get('update_kernel_us', float('nan')):.1f} | {r['eval_s']:.3f} |")
+    with open(os.path.join(a.out, "suite.jsonl"), "w") as f:  # again, with the targets filled in
+        for r in rows:
+            f.write(json.dumps(r) + "\n")
     with open(os.path.join(a.out, "suite.md"), "w") as f:
         f.write(hdr + "\n".join(lines) + "\n")
     print(hdr + "\n".join(lines))
