@@ -387,13 +387,13 @@ class MasterPump {
 
   // Device-side drain (after_combine): (host address, device address) of every worker rank's
   // message flag.  Empty = the host drains before pushing the next beta.
-  void set_drain_flags(const std::vector<std::pair<uintptr_t, uintptr_t>>& flags) {
+  // Returns whether the device-side drain is on (off when the device cannot wait on a value).
+  bool set_drain_flags(const std::vector<std::pair<uintptr_t, uintptr_t>>& flags) {
     for (const auto& f : flags) need(f.first != 0 && f.second != 0, "null drain flag");
     int can = 0;
-    need(flags.empty() ||
-             (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device_) == hipSuccess && can),
-         "device-side drain needs hipStreamWaitValue64 support");
-    drain_flags_ = flags;
+    const bool ok = hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device_) == hipSuccess && can;
+    drain_flags_ = ok ? flags : std::vector<std::pair<uintptr_t, uintptr_t>>{};
+    return ok && !flags.empty();
   }
 
   // beta pushes: (inbox base device pointer [R+1, ld], flag device address) per worker rank

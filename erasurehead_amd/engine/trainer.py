@@ -506,8 +506,9 @@ class Trainer:
             pump.set_puts([(tx.inbox_remote[r].data_ptr(), tx.flags.dev_addr(r)) for r in range(1, env.world)],
                           tx.counters)
             if self._device_waits(tx):  # drain on the device: beta(i+1) leaves as the last message lands
-                pump.set_drain_flags([(tx.flags.host_addr(env.world + r), tx.flags.dev_addr(env.world + r))
-                                      for r in sorted(self.remote_msgs) if self.remote_msgs[r]])
+                self.rank_stats["device_drain"] = bool(pump.set_drain_flags(
+                    [(tx.flags.host_addr(env.world + r), tx.flags.dev_addr(env.world + r))
+                     for r in sorted(self.remote_msgs) if self.remote_msgs[r]]))
         eta = cfg.eta()
         co = [self.update.coeffs(i, float(eta[i])) for i in range(R)]
         delay_table = np.stack([self.delay.delays(i) for i in range(R)])
