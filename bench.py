@@ -184,7 +184,8 @@ def main(argv=None) -> int:
         }
         if n_gpu_dev and env.world > n_gpu_dev:
             out["config"]["ranks_per_gpu"] = env.world / n_gpu_dev  # rehearsal: ranks time-share GPUs
-        out["config"]["round_loop"] = {"graph": "device-driven, hipGraph", "stream": "device-driven"}.get(
+        out["config"]["round_loop"] = {"graph": "device-driven, hipGraph", "stream": "device-driven",
+                                          "arbiter": "device-driven (arbiter kernel polls the workers)"}.get(
             trainer.device_loop, "host-driven (native pump)" if trainer.native_loop else "host-driven (python)")
         if a.share_partitions:
             out["config"]["share_partitions"] = True

@@ -1,0 +1,305 @@
+// Device-side master round (see arbiter.h): poll -> stop rule -> decode -> combine + update ->
+// beta(i+1) into the worker inboxes -> drain -> release the workers' beta counters.
+//
+// Reference loop replaced (per round, ref src/approximate_coding.py:131-183, src/naive.py:97-123):
+// Isend beta to every worker; Waitany until the stop rule; decode; GD/AGD update; Waitall.
+//
+// One workgroup of 256 threads.  Wave 0 polls the workers' shared 64-bit round counters (one
+// lane per worker rank, system-scope acquire loads of host memory); thread 0 keeps the
+// collector's books in LDS.  Probes that complete in the same poll are ordered by the round's
+// tie permutation, then by probe id, exactly like Collector::process_ready for delay-free
+// rounds (csrc/runtime/collector.cpp), so a replay of the logged arrivals reproduces the update.
+// Every spin has a deadline (a.deadline_ticks): a round that times out sets a.abort, skips its
+// update and its broadcast, and every later arbiter returns at once, so the grid always drains.
+#include "arbiter.h"
+#include "common.h"
+#include "launchers.h"
+
+namespace eh {
+
+namespace {
+
+__device__ __forceinline__ bool rule_holds(int rule, int k, int W, int G, int cnt0, int cnt1, int cntg) {
+  switch (rule) {
+    case 0: return cnt0 >= W;                    // kRuleAll
+    case 1: return cnt0 >= k;                    // kRuleCount
+    case 2: return cnt0 >= k || cntg >= G;       // kRuleFrc
+    case 3: return cnt1 >= W && cntg >= G;       // kRulePartialFrc
+    case 4: return cnt1 >= W && cnt0 >= k;       // kRulePartialCount
+    default: return true;
+  }
+}
+
+__device__ __forceinline__ unsigned long long load_counter(const unsigned long long* p) {
+  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace
+
+template <typename M>
+__global__ void __launch_bounds__(256) arbiter_round(const ArbArgs a, int i) {
+  __shared__ int s_pw[kArbMaxProbes], s_pp[kArbMaxProbes], s_ps[kArbMaxProbes];
+  __shared__ int batch[kArbMaxProbes];
+  __shared__ int got_sh[2 * kArbMaxW];
+  __shared__ int arr_w[2 * kArbMaxW], arr_p[2 * kArbMaxW];
+  __shared__ long long arr_t[2 * kArbMaxW];
+  __shared__ const void* mptr[kMaxMsgs];
+  __shared__ double mcoef[kMaxMsgs];
+  __shared__ int s_narr, s_nmsg, s_status;
+  const int tid = threadIdx.x;
+  int* lg = a.log + static_cast<long long>(i) * kArbLogInts;
+  long long* tl = a.tlog + static_cast<long long>(i) * kArbLogTicks;
+  if (__hip_atomic_load(a.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {  // an earlier round failed
+    if (tid == 0) lg[0] = 3;
+    return;
+  }
+  for (int q = tid; q < a.nprobe; q += blockDim.x) {
+    s_pw[q] = a.probe_w[q];
+    s_pp[q] = a.probe_p[q];
+    s_ps[q] = a.probe_src[q];
+  }
+  for (int m = tid; m < 2 * a.W; m += blockDim.x) got_sh[m] = 0;
+  if (tid == 0) {
+    s_narr = 0;
+    s_nmsg = 0;
+    s_status = 0;
+  }
+  __syncthreads();
+
+  // ---- 1. poll until the stop rule holds (wave 0) -------------------------------------------
+  const int* tie = a.tie + static_cast<long long>(i) * a.W;
+  unsigned long long seen = 0;  // sources seen so far (wave-uniform)
+  if (tid < 64) {
+    const long long t0 = wall_clock64();
+    const unsigned long long all_src = a.nsrc >= 64 ? ~0ull : ((1ull << a.nsrc) - 1);
+    unsigned long long got0 = 0, got1 = 0, gdone = 0;
+    int cnt0 = 0, cnt1 = 0, cntg = 0, stopped = 0;
+    for (int it = 0;; ++it) {
+      const long long t = wall_clock64();
+      const bool mine = tid < a.nsrc && !(seen >> tid & 1) && load_counter(reinterpret_cast<const unsigned long long*>(a.src_flag[tid])) >= static_cast<unsigned long long>(i + 1);
+      const unsigned long long nm = __ballot(mine);
+      if (it == 0 || nm) {
+        if (tid == 0) {
+          int nb = 0;
+          for (int q = 0; q < a.nprobe; ++q) {
+            const int s = s_ps[q];
+            if ((s < 0 && it == 0) || (s >= 0 && (nm >> s & 1))) batch[nb++] = q;
+          }
+          for (int x = 1; x < nb; ++x) {  // (tie rank, probe id) order
+            const int q = batch[x];
+            const int kq = tie[s_pw[q]];
+            int y = x - 1;
+            while (y >= 0 && (tie[s_pw[batch[y]]] > kq || (tie[s_pw[batch[y]]] == kq && batch[y] > q))) {
+              batch[y + 1] = batch[y];
+              --y;
+            }
+            batch[y + 1] = q;
+          }
+          for (int x = 0; x < nb; ++x) {
+            const int q = batch[x];
+            const int w = s_pw[q], p = s_pp[q];
+            const int mi = 2 * w + p;
+            if (++got_sh[mi] < a.nsh[mi] || stopped) continue;  // more shards to come / late
+            arr_w[s_narr] = w;
+            arr_p[s_narr] = p;
+            arr_t[s_narr] = t;
+            ++s_narr;
+            if (p == 0) {
+              if (!(got0 >> w & 1)) {
+                got0 |= 1ull << w;
+                ++cnt0;
+                const int g = a.group_of[w];
+                if (!(gdone >> g & 1)) {
+                  gdone |= 1ull << g;
+                  ++cntg;
+                }
+              }
+            } else if (!(got1 >> w & 1)) {
+              got1 |= 1ull << w;
+              ++cnt1;
+            }
+            if (rule_holds(a.rule, a.k, a.W, a.n_groups, cnt0, cnt1, cntg)) stopped = 1;
+          }
+        }
+        seen |= nm;
+      }
+      stopped = __builtin_amdgcn_readfirstlane(stopped);
+      if (stopped) break;
+      if ((seen & all_src) == all_src && a.nsrc > 0 && it > 0) {  // everything is in and the rule never held
+        if (tid == 0) s_status = 2;
+        break;
+      }
+      if (t - t0 > a.deadline_ticks) {
+        if (tid == 0) s_status = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  if (s_status != 0) {
+    if (tid == 0) {
+      __hip_atomic_store(a.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lg[0] = s_status;
+      lg[1] = s_narr;
+    }
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the workers' message rows behind their counters
+
+  // ---- 2. decode (thread 0; MasterPump::decode) -----------------------------------------------
+  const int slot = i % a.K;
+  if (tid == 0) {
+    auto push = [&](int w, int p, double c) {
+      const int mi = 2 * w + p;
+      for (int r = 0; r < a.msg_nrows[mi]; ++r) {
+        const int e = a.msg_rows[mi * kArbMaxRows + r];
+        const int row = e & 0xffffff;
+        const M* base = (e >> 24) == 0
+                            ? static_cast<const M*>(a.G) + (static_cast<long long>(slot) * a.g_rows + row) * a.ld
+                            : static_cast<const M*>(a.rbuf) + (static_cast<long long>(slot) * a.r_rows + row) * a.ld;
+        if (s_nmsg < kMaxMsgs) {
+          mptr[s_nmsg] = base;
+          mcoef[s_nmsg] = c;
+        }
+        ++s_nmsg;
+      }
+    };
+    unsigned long long gd = 0, mask = 0;
+    for (int x = 0; x < s_narr; ++x) {
+      const int w = arr_w[x], p = arr_p[x];
+      if (p == 1) {
+        if (a.decode == 2 || a.decode == 4) push(w, 1, 1.0);
+        continue;
+      }
+      if (a.decode == 0) {
+        push(w, 0, 1.0);
+      } else if (a.decode == 1 || a.decode == 2) {
+        const int g = a.group_of[w];
+        if (!(gd >> g & 1)) {
+          gd |= 1ull << g;
+          push(w, 0, 1.0);
+        }
+      } else {
+        mask |= 1ull << w;
+      }
+    }
+    if (a.decode == 3 || a.decode == 4) {
+      const double* row = a.table ? a.table + static_cast<long long>(mask) * a.W : nullptr;
+      for (int w = 0; w < a.W && row; ++w) {
+        if (!(mask >> w & 1)) continue;
+        if (row[w] != row[w]) {  // NaN: completion pattern without a table row
+          s_status = 2;
+          break;
+        }
+        push(w, 0, row[w]);
+      }
+      if (!row) s_status = 2;
+    }
+    if (s_nmsg > kMaxMsgs) s_status = 2;
+  }
+  __syncthreads();
+  if (s_status != 0) {
+    if (tid == 0) {
+      __hip_atomic_store(a.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lg[0] = s_status;
+      lg[1] = s_narr;
+    }
+    return;
+  }
+
+  // ---- 3. combine + update, beta(i+1) into beta_in and every worker inbox -------------------
+  const double decay = a.decay[i], gm = a.gm[i], l2 = a.l2[i], theta = a.theta[i];
+  M* bin_next = static_cast<M*>(a.beta_in) + static_cast<long long>(i + 1) * a.ld;
+  for (int c = tid; c < a.ld; c += blockDim.x) {
+    M out = M(0);
+    if (c < a.d) {
+      double g = 0.0;
+      constexpr int kB = 8;  // independent loads first, then the fma chain in message order
+      for (int m0 = 0; m0 < s_nmsg; m0 += kB) {
+        double v[kB];
+#pragma unroll
+        for (int q = 0; q < kB; ++q) v[q] = m0 + q < s_nmsg ? static_cast<double>(static_cast<const M*>(mptr[m0 + q])[c]) : 0.0;
+#pragma unroll
+        for (int q = 0; q < kB; ++q)
+          if (m0 + q < s_nmsg) g = fma(mcoef[m0 + q], v[q], g);
+      }
+      const double b = a.beta[c];
+      double nb;
+      if (a.update_rule == 0) {
+        nb = decay * b - gm * g;
+      } else {
+        const double yt = (1.0 - theta) * b + theta * a.u[c];
+        nb = yt - gm * g - l2 * b;
+        a.u[c] = b + (nb - b) * (1.0 / theta);
+      }
+      a.beta[c] = nb;
+      a.hist[static_cast<long long>(i) * a.ld + c] = nb;
+      out = static_cast<M>(nb);
+    }
+    if (i + 1 <= a.R) bin_next[c] = out;
+    for (int t = 0; t < a.ntarget && i + 1 < a.R; ++t)
+      reinterpret_cast<M*>(a.targets[2 * t])[static_cast<long long>(i + 1) * a.ld + c] = out;
+  }
+  __syncthreads();
+  if (tid == 0) tl[1] = wall_clock64();
+
+  // ---- 4. drain: every worker rank's round-i message has landed ------------------------------
+  if (a.drain && tid < 64) {
+    const long long t0 = wall_clock64();
+    const unsigned long long all_src = a.nsrc >= 64 ? ~0ull : ((1ull << a.nsrc) - 1);
+    for (;;) {
+      const bool mine = tid < a.nsrc && !(seen >> tid & 1) && load_counter(reinterpret_cast<const unsigned long long*>(a.src_flag[tid])) >= static_cast<unsigned long long>(i + 1);
+      seen |= __ballot(mine);
+      if ((seen & all_src) == all_src) break;
+      if (wall_clock64() - t0 > a.deadline_ticks) {
+        if (tid == 0) s_status = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  if (s_status != 0) {  // a worker rank is gone: do not release the next round
+    if (tid == 0) {
+      __hip_atomic_store(a.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lg[0] = s_status;
+      lg[1] = s_narr;
+    }
+    return;
+  }
+
+  // ---- 5. release beta(i+1): the inbox rows are visible before every worker's counter -------
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) {
+    if (i + 1 < a.R) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // see transport.hip: keep the counters behind the fence
+      for (int t = 0; t < a.ntarget; ++t)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.targets[2 * t + 1]),
+                           static_cast<unsigned long long>(i + 2), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const long long te = wall_clock64();
+    tl[2] = te;
+    if (i + 1 < a.R) a.tlog[static_cast<long long>(i + 1) * kArbLogTicks] = te;  // next round's start
+    lg[0] = 0;
+    lg[1] = s_narr;
+    lg[2] = s_nmsg;
+    for (int x = 0; x < s_narr; ++x) {
+      lg[4 + 2 * x] = arr_w[x];
+      lg[5 + 2 * x] = arr_p[x];
+      tl[4 + x] = arr_t[x];
+    }
+  }
+}
+
+hipError_t arbiter_round_launch(const ArbArgs& a, int round, int msg_dtype, hipStream_t st) {
+  if (a.W > kArbMaxW || a.nprobe > kArbMaxProbes || a.nsrc > kArbMaxSrc || a.nsrc > 64) return hipErrorInvalidValue;
+  if (msg_dtype == 0)
+    hipLaunchKernelGGL(arbiter_round<double>, dim3(1), dim3(256), 0, st, a, round);
+  else
+    hipLaunchKernelGGL(arbiter_round<float>, dim3(1), dim3(256), 0, st, a, round);
+  return hipGetLastError();
+}
+
+}  // namespace eh

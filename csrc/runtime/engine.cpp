@@ -44,6 +44,7 @@
 
 #include <cstdlib>
 
+#include "kernels/arbiter.h"
 #include "kernels/launchers.h"
 #include "runtime/collector.h"
 
@@ -613,6 +614,84 @@ class MasterPump {
     return out;
   }
 
+  // ---- device-driven rounds with remote workers (csrc/kernels/arbiter.hip) -----------------
+  // sources: (host address, device address) of every worker rank's message counter; a remote
+  // message belongs to the source with its flag's host address.
+  void set_sources(const std::vector<std::pair<uintptr_t, uintptr_t>>& srcs) {
+    for (const auto& f : srcs) need(f.first != 0 && f.second != 0, "null source counter");
+    arb_src_ = srcs;
+    arb_ready_ = false;
+  }
+
+  // Why rounds [a, b) cannot run on the device arbiter ("" = they can).
+  std::string device_blocker(int a, int b) const {
+    if (remote_.empty() || arb_src_.empty()) return "no remote workers";
+    if ((int)arb_src_.size() > eh::kArbMaxSrc) return "more than 64 worker ranks";
+    if (W_ > eh::kArbMaxW) return "more than 64 workers";
+    if ((int)(local_.size() + remote_.size()) > eh::kArbMaxProbes) return "too many message shards";
+    if (!drain_ && stop_rule_ != eh::kRuleAll) return "scheme without a drain (late messages cross rounds)";
+    if ((decode_kind_ == kTable || decode_kind_ == kPartialTable) && W_ > 16) return "decode table too large";
+    for (const auto& ix : index_)
+      if ((int)ix.size() > eh::kArbMaxRows) return "message with more than 16 shards";
+    for (const auto& m : remote_) {
+      bool found = false;
+      for (const auto& f : arb_src_) found |= f.first == m.flag;
+      if (!found) return "remote message without a source counter";
+    }
+    for (int i = a; i < b; ++i)
+      if (!no_delay(i)) return "injected delays (virtual arrival times live on the host)";
+    return "";
+  }
+
+  // Enqueue rounds [a, b): the master's own gradient, then one arbiter kernel per round that
+  // polls the workers' counters, decides, updates and releases the next beta.  Nothing waits on
+  // the host; device_log() reads the rounds back.
+  void run_device(int a, int b, double deadline_s) {
+    need(a >= 0 && a <= b && b <= R_, "round range out of bounds");
+    const std::string why = device_blocker(a, b);
+    need(why.empty(), "device-driven rounds: " + why);
+    if (!arb_ready_) arb_prepare();
+    eh::ArbArgs args = arb_args_;
+    args.deadline_ticks = static_cast<long long>(std::max(0.001, deadline_s) * stamp_hz());
+    long long* tlog = reinterpret_cast<long long*>(arb_tlog_.data_ptr<int64_t>());
+    char* bin = static_cast<char*>(beta_in_.data_ptr());
+    if (a < b && a != prepub_) {  // beta(a) was not released by an earlier arbiter
+      put_beta(a);
+      hcheck(eh::stamp_launch(tlog + static_cast<int64_t>(a) * eh::kArbLogTicks, stream_), "stamp");
+    }
+    for (int i = a; i < b; ++i) {
+      if (n_loc_ > 0 && launcher_) {
+        char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(i % K_) * g_rows_ * ld_ * es_;
+        hcheck(launcher_->launch(bin + static_cast<int64_t>(i) * ld_ * es_, g, stream_), "local gradient");
+      }
+      hcheck(eh::arbiter_round_launch(args, i, acc_, stream_), "arbiter_round");
+    }
+    if (b > a) prepub_ = b;
+  }
+
+  // Rounds [a, b) of run_device: (status, arrivals [(worker, part, t_rel)], t_decoded, t_end), times
+  // in seconds from the round's beta release.  status 0 ok, 1 timeout, 2 not decodable on the
+  // device, 3 skipped after an earlier failure.  Syncs the pump stream.
+  py::list device_log(int a, int b) {
+    need(arb_ready_, "run_device first");
+    hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    const Tensor lg = arb_log_.cpu(), tl = arb_tlog_.cpu();
+    const int* L = lg.data_ptr<int>();
+    const int64_t* T = tl.data_ptr<int64_t>();
+    const double hz = stamp_hz();
+    py::list out;
+    for (int i = a; i < b; ++i) {
+      const int* l = L + static_cast<int64_t>(i) * eh::kArbLogInts;
+      const int64_t* t = T + static_cast<int64_t>(i) * eh::kArbLogTicks;
+      py::list arr;
+      const int n = std::min(l[1], 2 * eh::kArbMaxW);
+      for (int x = 0; x < n && l[0] == 0; ++x)
+        arr.append(py::make_tuple(l[4 + 2 * x], l[5 + 2 * x], (t[4 + x] - t[0]) / hz));
+      out.append(py::make_tuple(l[0], arr, (t[1] - t[0]) / hz, (t[2] - t[0]) / hz));
+    }
+    return out;
+  }
+
   // Wall-clock rate of the device timestamps (Hz).
   double stamp_hz() const {
     int khz = 0;
@@ -726,6 +805,116 @@ class MasterPump {
     if (events) hcheck(hipEventRecord(ev.second, stream_), "hipEventRecord");
   }
 
+  // Device copies of everything the arbiter reads (arbiter.h ArbArgs); built once.
+  void arb_prepare() {
+    const auto dev = beta_.device();
+    auto ints = [&](const std::vector<int>& v) {
+      return at::from_blob(const_cast<int*>(v.data()), {(int64_t)v.size()}, at::kInt).clone().to(dev);
+    };
+    auto dbl = [&](const std::vector<double>& v) {
+      return at::from_blob(const_cast<double*>(v.data()), {(int64_t)v.size()}, at::kDouble).clone().to(dev);
+    };
+    auto u64 = [&](const std::vector<int64_t>& v) {
+      return at::from_blob(const_cast<int64_t*>(v.data()), {(int64_t)v.size()}, at::kLong).clone().to(dev);
+    };
+    std::vector<int> pw, pp, ps;
+    for (const auto& m : local_) {  // probe order = begin(): local event probes, then the flag probes
+      pw.push_back(m.w);
+      pp.push_back(m.p);
+      ps.push_back(-1);
+    }
+    for (const auto& m : remote_) {
+      int src = -1;
+      for (int j = 0; j < (int)arb_src_.size(); ++j)
+        if (arb_src_[j].first == m.flag) src = j;
+      pw.push_back(m.w);
+      pp.push_back(m.p);
+      ps.push_back(src);
+    }
+    std::vector<int> nsh(2 * W_, 0), nrows(2 * W_, 0), rows(2 * W_ * eh::kArbMaxRows, 0);
+    for (int q = 0; q < (int)pw.size(); ++q) ++nsh[2 * pw[q] + pp[q]];
+    for (int mi = 0; mi < 2 * W_; ++mi) {
+      nrows[mi] = (int)index_[mi].size();
+      for (int r = 0; r < nrows[mi]; ++r) rows[mi * eh::kArbMaxRows + r] = (index_[mi][r].first << 24) | index_[mi][r].second;
+    }
+    std::vector<int> tie(static_cast<size_t>(R_) * W_, 0);
+    const int64_t seed = col_->tie_seed();
+    if (seed >= 0) {
+      std::vector<int> ord(W_);
+      for (int i = 0; i < R_; ++i) {
+        for (int w = 0; w < W_; ++w) ord[w] = w;
+        std::sort(ord.begin(), ord.end(), [&](int x, int y) {
+          const uint64_t kx = eh::Collector::tie_key(seed, i, x), ky = eh::Collector::tie_key(seed, i, y);
+          return kx != ky ? kx < ky : x < y;
+        });
+        for (int r = 0; r < W_; ++r) tie[static_cast<size_t>(i) * W_ + ord[r]] = r;
+      }
+    }
+    std::vector<double> table;
+    if (decode_kind_ == kTable || decode_kind_ == kPartialTable) {
+      table.assign((size_t{1} << W_) * W_, std::nan(""));
+      for (const auto& [mask, coefs] : table_)
+        if (mask < (uint64_t{1} << W_))
+          for (int w = 0; w < W_; ++w) table[mask * W_ + w] = coefs[w];
+    }
+    std::vector<int64_t> src, tgt;
+    for (const auto& f : arb_src_) src.push_back(static_cast<int64_t>(f.second));
+    for (const auto& t : targets_) {
+      tgt.push_back(static_cast<int64_t>(t.first));
+      tgt.push_back(static_cast<int64_t>(t.second));
+    }
+    arb_keep_ = {ints(group_of_), ints(pw), ints(pp), ints(ps), ints(nsh), ints(nrows), ints(rows), ints(tie),
+                 dbl(decay_), dbl(gm_), dbl(l2_), dbl(theta_), u64(src.empty() ? std::vector<int64_t>{0} : src),
+                 u64(tgt.empty() ? std::vector<int64_t>{0, 0} : tgt),
+                 table.empty() ? at::Tensor() : dbl(table)};
+    arb_log_ = at::zeros({static_cast<int64_t>(R_) * eh::kArbLogInts}, at::TensorOptions().dtype(at::kInt).device(dev));
+    arb_tlog_ = at::zeros({static_cast<int64_t>(R_) * eh::kArbLogTicks}, at::TensorOptions().dtype(at::kLong).device(dev));
+    arb_abort_ = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(dev));
+    eh::ArbArgs g{};
+    g.W = W_;
+    g.n_groups = n_groups_;
+    g.rule = stop_rule_;
+    g.k = k_;
+    g.decode = decode_kind_;
+    g.drain = drain_ ? 1 : 0;
+    g.nprobe = (int)pw.size();
+    g.nsrc = (int)arb_src_.size();
+    g.ntarget = (int)targets_.size();
+    g.K = K_;
+    g.ld = ld_;
+    g.d = d_;
+    g.g_rows = g_rows_;
+    g.r_rows = r_rows_;
+    g.R = R_;
+    g.update_rule = update_rule_;
+    g.group_of = arb_keep_[0].data_ptr<int>();
+    g.probe_w = arb_keep_[1].data_ptr<int>();
+    g.probe_p = arb_keep_[2].data_ptr<int>();
+    g.probe_src = arb_keep_[3].data_ptr<int>();
+    g.nsh = arb_keep_[4].data_ptr<int>();
+    g.msg_nrows = arb_keep_[5].data_ptr<int>();
+    g.msg_rows = arb_keep_[6].data_ptr<int>();
+    g.tie = arb_keep_[7].data_ptr<int>();
+    g.decay = arb_keep_[8].data_ptr<double>();
+    g.gm = arb_keep_[9].data_ptr<double>();
+    g.l2 = arb_keep_[10].data_ptr<double>();
+    g.theta = arb_keep_[11].data_ptr<double>();
+    g.src_flag = reinterpret_cast<const unsigned long long*>(arb_keep_[12].data_ptr<int64_t>());
+    g.targets = reinterpret_cast<const unsigned long long*>(arb_keep_[13].data_ptr<int64_t>());
+    g.table = arb_keep_[14].defined() ? arb_keep_[14].data_ptr<double>() : nullptr;
+    g.beta = beta_.data_ptr<double>();
+    g.u = u_.data_ptr<double>();
+    g.hist = hist_.data_ptr<double>();
+    g.beta_in = beta_in_.data_ptr();
+    g.G = G_.defined() ? G_.data_ptr() : nullptr;
+    g.rbuf = rbuf_.defined() ? rbuf_.data_ptr() : nullptr;
+    g.log = arb_log_.data_ptr<int>();
+    g.tlog = reinterpret_cast<long long*>(arb_tlog_.data_ptr<int64_t>());
+    g.abort = arb_abort_.data_ptr<int>();
+    arb_args_ = g;
+    arb_ready_ = true;
+  }
+
   // push beta(j) into every worker inbox (put + signal kernels on the pump stream)
   void put_beta(int j) {
     if (targets_.empty()) return;
@@ -802,7 +991,12 @@ class MasterPump {
   std::vector<std::vector<std::pair<int, int>>> index_;  // [2*w+p] -> (0 local | 1 remote, row) per shard
   std::vector<std::pair<uintptr_t, uintptr_t>> targets_;
   std::vector<std::pair<uintptr_t, uintptr_t>> drain_flags_;
-  int prepub_ = -1;  // round whose beta after_combine already queued behind the device-side drain
+  int prepub_ = -1;  // round whose beta is already queued (device-side drain / the arbiter)
+  std::vector<std::pair<uintptr_t, uintptr_t>> arb_src_;
+  bool arb_ready_ = false;
+  eh::ArbArgs arb_args_{};
+  std::vector<Tensor> arb_keep_;
+  Tensor arb_log_, arb_tlog_, arb_abort_;
   std::vector<double> decay_, gm_, l2_, theta_, delays_;
   int update_rule_ = 0, stop_rule_ = 0, k_ = 0;
   bool drain_ = false;
@@ -1019,6 +1213,10 @@ void bind_engine(py::module& m) {
       .def("set_remote", &MasterPump::set_remote)
       .def("set_puts", &MasterPump::set_puts)
       .def("set_drain_flags", &MasterPump::set_drain_flags)
+      .def("set_sources", &MasterPump::set_sources)
+      .def("device_blocker", &MasterPump::device_blocker)
+      .def("run_device", &MasterPump::run_device, py::arg("a"), py::arg("b"), py::arg("deadline_s"))
+      .def("device_log", &MasterPump::device_log)
       .def("set_schedule", &MasterPump::set_schedule)
       .def("set_decode", &MasterPump::set_decode)
       .def("add_table", &MasterPump::add_table)

@@ -505,10 +505,11 @@ class Trainer:
             pump.set_remote(self.Rbuf, rem)
             pump.set_puts([(tx.inbox_remote[r].data_ptr(), tx.flags.dev_addr(r)) for r in range(1, env.world)],
                           tx.counters)
+            srcs = [(tx.flags.host_addr(env.world + r), tx.flags.dev_addr(env.world + r))
+                    for r in sorted(self.remote_msgs) if self.remote_msgs[r]]
+            pump.set_sources(srcs)
             if self._device_waits(tx):  # drain on the device: beta(i+1) leaves as the last message lands
-                self.rank_stats["device_drain"] = bool(pump.set_drain_flags(
-                    [(tx.flags.host_addr(env.world + r), tx.flags.dev_addr(env.world + r))
-                     for r in sorted(self.remote_msgs) if self.remote_msgs[r]]))
+                self.rank_stats["device_drain"] = bool(pump.set_drain_flags(srcs))
         eta = cfg.eta()
         co = [self.update.coeffs(i, float(eta[i])) for i in range(R)]
         delay_table = np.stack([self.delay.delays(i) for i in range(R)])
@@ -532,6 +533,30 @@ class Trainer:
             log(sch.banner(cfg.add_delay))
         orig_start = time.perf_counter()
         device_mode = self._device_loop_mode(start, delay_table, table_decoded)
+        arb_mode = not device_mode and self._arbiter_mode(pump, start)
+        if arb_mode:
+            # every round on the device: the master's gradient, then csrc/kernels/arbiter.hip polls the
+            # workers' counters, decodes, updates and releases the next beta; the host only reads back
+            cuts = [start] + ([timed_start] if timed_start is not None and start < timed_start < R else []) + [R]
+            deadline = min(float(cfg.round_timeout), 60.0)
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                if timed_start is not None and a == timed_start:
+                    t_timed0 = self._timed_fence()
+                pump.run_device(a, b, deadline)
+            if timed_start is not None:
+                t_timed1 = self._timed_fence()
+            for i, (status, arr, tdec, tend) in zip(range(start, R), pump.device_log(start, R)):
+                if status:
+                    why = {1: f"a worker rank's message did not arrive within {deadline:.0f} s",
+                           2: "the arrivals could not be decoded on the device",
+                           3: "an earlier round failed"}.get(status, f"status {status}")
+                    raise RuntimeError(f"device-driven round {i}: {why}")
+                arrivals = [Arrival(w, p, t) for (w, p, t) in arr]
+                timeset[i], loop_time[i] = tdec, tend
+                worker_timeset[i] = sch.worker_times(arrivals)
+                arrivals_log.append([(a.worker, a.part, a.t_rel) for a in arrivals])
+                self.timer.add("device_round", tend)
+            self.device_loop = "arbiter"
         if device_mode:
             stamps = torch.zeros(R + 1, dtype=torch.int64, device=env.device)
             hz = pump.stamp_hz()
@@ -557,8 +582,8 @@ class Trainer:
                 worker_timeset[i] = sch.worker_times(arrivals)
                 self.timer.add("device_round", dt)
             self.device_loop = device_mode
-        begun = device_mode is not None
-        for i in range(start, R if not device_mode else start):
+        begun = device_mode is not None or arb_mode
+        for i in range(start, start if (device_mode or arb_mode) else R):
             if not begun:
                 if timed_start is not None and i == timed_start:
                     t_timed0 = self._timed_fence()
@@ -594,13 +619,13 @@ class Trainer:
             arrivals_log.append([(a.worker, a.part, a.t_rel) for a in arrivals])
             if cfg.checkpoint_every and (i + 1) % cfg.checkpoint_every == 0:
                 self._checkpoint(i + 1, timeset, worker_timeset)
-        if timed_start is not None and not device_mode:
+        if timed_start is not None and not device_mode and not arb_mode:
             # every rank's rounds are complete once all ranks pass the fence (workers' puts have landed
             # before their barrier); the straggler drain and bookkeeping below are not round time
             t_timed1 = self._timed_fence()
         col.drain(R - 1, max(cfg.round_timeout, 60.0))
         upd = pump.update_ms()
-        if not device_mode:
+        if not device_mode and not arb_mode:
             timeset[start:] += 1e-3 * np.asarray(upd[start:])
         a0 = timed_start if timed_start is not None else start
         if cfg.instrument:
@@ -620,6 +645,24 @@ class Trainer:
             res.timed_rounds = R - timed_start
         del pump
         return res
+
+    def _arbiter_mode(self, pump, start: int) -> bool:
+        """Multi-rank rounds on the device arbiter (MasterPump.run_device)?  ERASUREHEAD_DEVICE_MASTER =
+        auto | on | off.  auto: when the ranks own their GPUs (a spinning arbiter would compete with
+        the other ranks' kernels on a shared one), the rounds are delay-free and drain, and nothing
+        needs the host between rounds (checkpoints, the beta race check, HIP-event instrumentation,
+        --device-loop off)."""
+        mode = os.environ.get("ERASUREHEAD_DEVICE_MASTER", "auto")
+        cfg, tx = self.cfg, self.tx
+        if mode == "off" or tx is None or cfg.device_loop == "off" or cfg.instrument or cfg.verify_beta \
+                or cfg.checkpoint_every or start:
+            return False
+        why = pump.device_blocker(start, cfg.num_itrs)
+        if why:
+            if mode == "on":
+                raise RuntimeError(f"ERASUREHEAD_DEVICE_MASTER=on, but the rounds cannot run on the device: {why}")
+            return False
+        return mode == "on" or self._device_waits(tx)
 
     def _device_loop_mode(self, start: int, delay_table: np.ndarray, table_decoded: bool) -> Optional[str]:
         """'graph' | 'stream' when the rounds can run device-driven (MasterPump.run_local), else None.

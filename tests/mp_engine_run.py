@@ -27,6 +27,8 @@ def main():
     extra = {"delay_mean": delay} if delay else {}
     cfg, src, sch, parts = make(CASES[case_i], rule, **extra)
     cfg.num_itrs = 12
+    if os.environ.get("EH_TEST_ROUND_TIMEOUT"):
+        cfg.round_timeout = float(os.environ["EH_TEST_ROUND_TIMEOUT"])
     if delay:
         cfg.add_delay = 1
         cfg.force_delay = True
@@ -35,7 +37,7 @@ def main():
     if env.is_master:
         arr = np.array([[(w, p) for (w, p, _) in a] for a in res.arrivals], dtype=object)
         np.savez(out, betaset=res.betaset, beta0=tr.beta0, arrivals=arr, transport=np.array(tr.transport),
-                 timeset=res.timeset)
+                 timeset=res.timeset, round_loop=np.array(tr.device_loop or "host"))
     env.barrier()
     tr.close()
     env.shutdown()

@@ -79,6 +79,25 @@ def test_ipc_worker_wait_and_put_modes(wait, fused, tmp_path):
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
 
 
+@pytest.mark.parametrize("world,case_i,wait", [(2, 2, "device"), (3, 4, "host"), (3, 5, "device"), (3, 0, "device")])
+def test_device_arbiter_rounds(world, case_i, wait, tmp_path):
+    """Multi-rank rounds driven by the arbiter kernel (csrc/kernels/arbiter.hip: the master GPU polls the
+    workers' counters, applies the stop rule, decodes, updates and releases the next beta): the
+    trajectory replays exactly from the arrivals it logged (FRC, AGC, uneven AGC groups, naive)."""
+    from oracle import replay
+    from test_engine_cpu import CASES, make
+
+    r = _launch(world, case_i, "AGD", str(tmp_path / "a.npz"), ERASUREHEAD_DEVICE_MASTER="on",
+                ERASUREHEAD_WORKER_WAIT=wait, EH_TEST_ROUND_TIMEOUT="20")
+    assert str(r["transport"]) == "ipc" and str(r["round_loop"]) == "arbiter"
+    cfg, src, sch, parts = make(CASES[case_i], "AGD")
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    assert all(len(a) for a in arrivals)
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+    assert np.all(r["timeset"] > 0)
+
+
 def test_ipc_multiprocess_delayed_agc(tmp_path):
     """AGC (W=6, s=2, k=4) with the reference delay model: the decode only uses fast workers."""
     from oracle import replay
