@@ -4,7 +4,8 @@
 // Reference loop replaced (per round, ref src/approximate_coding.py:131-183, src/naive.py:97-123):
 // Isend beta to every worker; Waitany until the stop rule; decode; GD/AGD update; Waitall.
 //
-// One workgroup of 256 threads.  Wave 0 polls the workers' shared 64-bit round counters (one
+// One workgroup of 1024 threads (one column each at d <= 1024, so the combine is a couple of
+// batches of independent message loads).  Wave 0 polls the workers' shared 64-bit round counters (one
 // lane per worker rank, system-scope acquire loads of host memory); thread 0 keeps the
 // collector's books in LDS.  Probes that complete in the same poll are ordered by the round's
 // tie permutation, then by probe id, exactly like Collector::process_ready for delay-free
@@ -37,7 +38,7 @@ __device__ __forceinline__ unsigned long long load_counter(const unsigned long l
 }  // namespace
 
 template <typename M>
-__global__ void __launch_bounds__(256) arbiter_round(const ArbArgs a, int i) {
+__global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
   __shared__ int s_pw[kArbMaxProbes], s_pp[kArbMaxProbes], s_ps[kArbMaxProbes];
   __shared__ int batch[kArbMaxProbes];
   __shared__ int got_sh[2 * kArbMaxW];
@@ -215,7 +216,7 @@ __global__ void __launch_bounds__(256) arbiter_round(const ArbArgs a, int i) {
     M out = M(0);
     if (c < a.d) {
       double g = 0.0;
-      constexpr int kB = 8;  // independent loads first, then the fma chain in message order
+      constexpr int kB = 16;  // independent loads first, then the fma chain in message order
       for (int m0 = 0; m0 < s_nmsg; m0 += kB) {
         double v[kB];
 #pragma unroll
@@ -296,9 +297,9 @@ __global__ void __launch_bounds__(256) arbiter_round(const ArbArgs a, int i) {
 hipError_t arbiter_round_launch(const ArbArgs& a, int round, int msg_dtype, hipStream_t st) {
   if (a.W > kArbMaxW || a.nprobe > kArbMaxProbes || a.nsrc > kArbMaxSrc || a.nsrc > 64) return hipErrorInvalidValue;
   if (msg_dtype == 0)
-    hipLaunchKernelGGL(arbiter_round<double>, dim3(1), dim3(256), 0, st, a, round);
+    hipLaunchKernelGGL(arbiter_round<double>, dim3(1), dim3(1024), 0, st, a, round);
   else
-    hipLaunchKernelGGL(arbiter_round<float>, dim3(1), dim3(256), 0, st, a, round);
+    hipLaunchKernelGGL(arbiter_round<float>, dim3(1), dim3(1024), 0, st, a, round);
   return hipGetLastError();
 }
 
