@@ -79,7 +79,7 @@ def test_ipc_worker_wait_and_put_modes(wait, fused, tmp_path):
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
 
 
-@pytest.mark.parametrize("world,case_i,wait", [(2, 2, "device"), (3, 4, "host"), (3, 5, "device"), (3, 0, "device")])
+@pytest.mark.parametrize("world,case_i,wait", [(2, 2, "device"), (3, 4, "host"), (3, 5, "device"), (3, 0, "device"), (8, 5, "device")])
 def test_device_arbiter_rounds(world, case_i, wait, tmp_path):
     """Multi-rank rounds driven by the arbiter kernel (csrc/kernels/arbiter.hip: the master GPU polls the
     workers' counters, applies the stop rule, decodes, updates and releases the next beta): the
