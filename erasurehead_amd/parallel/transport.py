@@ -145,6 +145,7 @@ class RcclTransport(Transport):
         if env.is_master:
             self.beta_ev = torch.cuda.Event()
             self.rem_ev = [[torch.cuda.Event() for _ in range(max(1, self.n_rem))] for _ in range(self.K)]
+            self.ev_of = [list(evs) for evs in self.rem_ev]  # [slot][mailbox row] -> its rank's event
         else:
             self.bbuf = torch.zeros((2, self.ld), dtype=self.dtype, device=env.device)
             self.bev = torch.cuda.Event()
@@ -160,18 +161,21 @@ class RcclTransport(Transport):
                 dist.isend(beta, r)
 
     def post_recvs(self, i, slot, col, rbuf, msgs_by_rank, delays):
+        # one receive per worker rank: its messages are contiguous rows of the mailbox ring and the
+        # rank computes (and sends) them together, so they share one completion event
         for r in sorted(msgs_by_rank):
             s = self.ps[r]
+            j0, n = self.row0[r], len(msgs_by_rank[r])
+            ev = self.rem_ev[slot][j0]
             with torch.cuda.stream(s):
-                for jj, m in enumerate(msgs_by_rank[r]):
-                    j = self.row0[r] + jj
-                    dist.irecv(rbuf[slot, j], r).wait()  # stream-ordered: s waits for the receive
-                    ev = self.rem_ev[slot][j]
-                    ev.record(s)
-                    col.add_event(m.worker, m.part, i, ev, delays[m.worker])
+                dist.irecv(rbuf[slot, j0:j0 + n], r).wait()  # stream-ordered: s waits for the receive
+                ev.record(s)
+            for jj, m in enumerate(msgs_by_rank[r]):
+                self.ev_of[slot][j0 + jj] = ev
+                col.add_event(m.worker, m.part, i, ev, delays[m.worker])
 
     def before_read(self, slot, j):
-        self.cs.wait_event(self.rem_ev[slot][j])
+        self.cs.wait_event(self.ev_of[slot][j])
 
     def recv_beta(self, i):
         b = self.bbuf[i % 2]
@@ -191,8 +195,7 @@ class RcclTransport(Transport):
         s = self.ps[0]
         s.wait_event(self.gev)
         with torch.cuda.stream(s):
-            for j in range(G_slot.shape[0]):
-                dist.isend(G_slot[j], 0).wait()
+            dist.isend(G_slot, 0).wait()  # all of this rank's messages in one send (rows are contiguous)
             ev = self.send_done[slot] or torch.cuda.Event()
             ev.record(s)
             self.send_done[slot] = ev
