@@ -327,6 +327,7 @@ class MasterPump {
   }
 
   void set_state(const Tensor& beta, const Tensor& u, const Tensor& hist, const Tensor& beta_in) {
+    arb_ready_ = false;  // the device arbiter copies this state
     need_gpu(beta, "beta");
     need_gpu(u, "u");
     need_gpu(hist, "hist");
@@ -347,6 +348,7 @@ class MasterPump {
   // local messages: row order of G ([K, n_loc, ld]); each (worker, part).  A (worker, part) may
   // appear several times (partition shards of one message): decode sums all its rows.
   void set_local(std::shared_ptr<GradLauncher> g, const Tensor& G, const std::vector<std::pair<int, int>>& msgs) {
+    arb_ready_ = false;  // the device arbiter copies this state
     need_gpu(G, "G");
     need(G.dim() == 3 && G.size(0) == K_ && G.size(2) == ld_, "G must be [K, n_loc, ld]");
     need(acc_code(G) == acc_, "G dtype must match beta_in");
@@ -368,6 +370,7 @@ class MasterPump {
 
   // remote messages: (worker, part, mailbox row, host address of the sender's round counter)
   void set_remote(const Tensor& rbuf, const std::vector<std::tuple<int, int, int, uintptr_t>>& msgs) {
+    arb_ready_ = false;  // the device arbiter copies this state
     need_gpu(rbuf, "rbuf");
     need(rbuf.dim() == 3 && rbuf.size(0) == K_ && rbuf.size(2) == ld_, "rbuf must be [K, rows, ld]");
     need(acc_code(rbuf) == acc_, "rbuf dtype must match beta_in");
@@ -399,6 +402,7 @@ class MasterPump {
 
   // beta pushes: (inbox base device pointer [R+1, ld], flag device address) per worker rank
   void set_puts(const std::vector<std::pair<uintptr_t, uintptr_t>>& targets, const Tensor& counters) {
+    arb_ready_ = false;  // the device arbiter copies this state
     need(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.numel() >= (int64_t)targets.size(),
          "counters must be int32 GPU [>= n targets]");
     for (const auto& t : targets) need(t.first != 0 && t.second != 0, "null put target");
@@ -409,6 +413,7 @@ class MasterPump {
   void set_schedule(const std::vector<double>& decay, const std::vector<double>& gm, const std::vector<double>& l2,
                     const std::vector<double>& theta, int update_rule, const std::vector<double>& delays, int stop_rule,
                     int k, bool drain) {
+    arb_ready_ = false;  // the device arbiter copies this state
     need((int)decay.size() >= R_ && (int)gm.size() >= R_ && (int)l2.size() >= R_ && (int)theta.size() >= R_,
          "schedule arrays must cover R rounds");
     need((int64_t)delays.size() >= (int64_t)R_ * W_, "delays must be [R*W]");
@@ -424,6 +429,7 @@ class MasterPump {
   }
 
   void set_decode(int kind, const std::vector<int>& group_of, int n_groups) {
+    arb_ready_ = false;  // the device arbiter copies this state
     need((int)group_of.size() == W_, "group_of must have W entries");
     need(!((kind == kTable || kind == kPartialTable) && W_ > 64), "table decode supports at most 64 workers");
     decode_kind_ = kind;
@@ -431,6 +437,7 @@ class MasterPump {
     n_groups_ = n_groups;
   }
   void add_table(uint64_t mask, const std::vector<double>& coefs) {
+    arb_ready_ = false;  // the device arbiter copies this state
     need((int)coefs.size() == W_, "table row must have W coefficients");
     table_[mask] = coefs;
   }
