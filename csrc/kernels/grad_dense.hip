@@ -23,6 +23,9 @@
 // row range); segment -> (partition base pointer, labels, encoding coefficient).
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <type_traits>
 
 #include "common.h"
@@ -235,235 +238,256 @@ template <typename T, typename A, int CPL, int LOSS, bool PAIR>
 __global__ void __launch_bounds__(512)
 grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                   const A* __restrict__ beta, A* __restrict__ slab, int ld, int srows, int pieces, int nstage,
-                  int wpr) {
+                  int wpr, int nbundles, unsigned int* ticket) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  __shared__ int s_next;
   // W waves = R task slots x wpr waves per slot; slot q's waves split each stage's rows
   const int lane = threadIdx.x & 63, W = blockDim.x >> 6, R = W / wpr;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int q = w % R, sub = w / R;
   const unsigned lds_base = static_cast<unsigned>(
       reinterpret_cast<size_t>((__attribute__((address_space(3))) unsigned char*)smem_raw));
-  const Task lead = tasks[blockIdx.x * R];  // slot 0 of a bundle is always a real task
-  const Task task = tasks[blockIdx.x * R + q];
-  const bool active = task.seg >= 0;
-  const Segment ls = segs[lead.seg];
-  const unsigned char* __restrict__ X = static_cast<const unsigned char*>(ls.X);
-  const unsigned char* __restrict__ Y = static_cast<const unsigned char*>(ls.y);
-  const A coef = active ? static_cast<A>(segs[task.seg].coef) : A(0);
   const int rowbytes = ld * static_cast<int>(sizeof(T));
   const int data_bytes = W * pieces * 1024;  // one stage buffer: data, then 256 B of labels
   const int buf_bytes = data_bytes + 256;
-  const int nrows = lead.row_end - lead.row_begin;
-  const int nst = (nrows + srows - 1) / srows;
-
-  // LDS-DMA loads wave w issues for a stage of nbytes: its 1 KiB pieces (+ labels: wave 0).  Every
-  // stage but the last is full, so two counts cover the ring; computing them once keeps integer
-  // divisions (and the loop the vectorizer made of a per-stage sum) out of the stage loop.
-  auto count_bytes = [&](int nbytes) {
-    const int nb = (nbytes + 1023) >> 10;
-    return (nb > w ? (nb - w + W - 1) / W : 0) + (w == 0 ? 1 : 0);
-  };
-  const int cnt_full = count_bytes(srows * rowbytes);
-  const int cnt_last = count_bytes((nrows - (nst - 1) * srows) * rowbytes);
-  auto issue = [&](int t) {
-    const unsigned dst = lds_base + (t % nstage) * buf_bytes;
-    const long long r0 = lead.row_begin + static_cast<long long>(t) * srows;
-    const int ns = min(srows, static_cast<int>(lead.row_end - r0));
-    const int bytes = ns * rowbytes;
-    const unsigned char* src = X + r0 * rowbytes;
-    for (int blk = w; blk * 1024 < bytes; blk += W)
-      glds16(src + min(blk * 1024 + lane * 16, bytes - 16), dst + blk * 1024);
-    if (w == 0) {
-      const int lb = ns * static_cast<int>(sizeof(A));
-      glds4(Y + r0 * sizeof(A) + min(lane * 4, lb - 4), dst + data_bytes);
-    }
-  };
-
-  A b[NV][VN], g[NV][VN];
+  using Rw = typename Vec16<T>::raw;
+  A b[NV][VN];  // beta, loaded once for every bundle this workgroup takes
   bool valid[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int c0 = (j * kWave + lane) * VN;
     valid[j] = c0 < ld;
 #pragma unroll
-    for (int v = 0; v < VN; ++v) {
-      b[j][v] = valid[j] ? beta[c0 + v] : A(0);
-      g[j][v] = A(0);
-    }
+    for (int v = 0; v < VN; ++v) b[j][v] = valid[j] ? beta[c0 + v] : A(0);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // beta in registers before the counted loads
-  using Rw = typename Vec16<T>::raw;
-  for (int t = 0; t < nstage - 1 && t < nst; ++t) issue(t);
-  for (int t = 0; t < nst; ++t) {
-    // loads this wave issued after stage t: stages t+1 .. hi, only stage nst-1 can be partial
-    const int hi = min(t + nstage - 2, nst - 1);
-    const int later = hi > t ? (hi - t) * cnt_full + (hi == nst - 1 ? cnt_last - cnt_full : 0) : 0;
-    wait_vmcnt(later);  // this wave's pieces of stage t landed
-    __syncthreads();    // every wave's pieces of stage t; stage t-1 consumed by every wave
-    if (t + nstage - 1 < nst) issue(t + nstage - 1);  // into the buffer stage t-1 used
-    if (!active) continue;
-    const unsigned char* buf = smem_raw + (t % nstage) * buf_bytes;
-    const A* lab = reinterpret_cast<const A*>(buf + data_bytes);
-    const int ns = min(srows, nrows - t * srows);
-    if constexpr (PAIR) {
-      // Two rows per step with ONE reduction and ONE residual evaluation between them: the two
-      // partial dot products are reduce-scattered (lanes 0-31 finish row i, lanes 32-63 row i+1),
-      // each lane evaluates the loss epilogue of its half's row (one exp for two rows), and the
-      // two residuals are broadcast by readlane.  The rows are re-read from LDS for the update
-      // rather than held in registers across the reduction.  A lone last row is paired with
-      // itself and weighted 0.
-      const bool hi = lane >= 32;
-      for (int i = 2 * sub; i < ns; i += 2 * wpr) {
-        const bool two = i + 1 < ns;
-        const unsigned char* row0 = buf + i * rowbytes;
-        const unsigned char* row1 = two ? row0 + rowbytes : row0;
-        A z0 = A(0), z1 = A(0);
-        if constexpr (std::is_same<T, float>::value) {
-          // fp32: both rows' dot products in one packed accumulator {z0, z1} (v_pk_fma_f32)
-          typedef float f2 __attribute__((ext_vector_type(2)));
-          f2 z01 = f2{0.f, 0.f};
+  // Persistent workgroups (ticket != nullptr): the grid holds as many workgroups as fit at once and
+  // each takes bundles until none is left — its first is blockIdx.x, the next ones come from an
+  // atomic ticket, so no workgroup idles while another still streams a partition (the single-wave
+  // tail of the sharded multi-GPU shapes).  The draw that hands out the launch's last ticket resets
+  // the counter for the next launch.  ticket == nullptr: one bundle per workgroup.
+  for (int bundle = blockIdx.x; bundle < nbundles;) {
+    const Task lead = tasks[bundle * R];  // slot 0 of a bundle is always a real task
+    const Task task = tasks[bundle * R + q];
+    const bool active = task.seg >= 0;
+    const Segment ls = segs[lead.seg];
+    const unsigned char* __restrict__ X = static_cast<const unsigned char*>(ls.X);
+    const unsigned char* __restrict__ Y = static_cast<const unsigned char*>(ls.y);
+    const A coef = active ? static_cast<A>(segs[task.seg].coef) : A(0);
+    const int nrows = lead.row_end - lead.row_begin;
+    const int nst = (nrows + srows - 1) / srows;
+
+    // LDS-DMA loads wave w issues for a stage of nbytes: its 1 KiB pieces (+ labels: wave 0).  Every
+    // stage but the last is full, so two counts cover the ring; computing them once keeps integer
+    // divisions (and the loop the vectorizer made of a per-stage sum) out of the stage loop.
+    auto count_bytes = [&](int nbytes) {
+      const int nb = (nbytes + 1023) >> 10;
+      return (nb > w ? (nb - w + W - 1) / W : 0) + (w == 0 ? 1 : 0);
+    };
+    const int cnt_full = count_bytes(srows * rowbytes);
+    const int cnt_last = count_bytes((nrows - (nst - 1) * srows) * rowbytes);
+    auto issue = [&](int t) {
+      const unsigned dst = lds_base + (t % nstage) * buf_bytes;
+      const long long r0 = lead.row_begin + static_cast<long long>(t) * srows;
+      const int ns = min(srows, static_cast<int>(lead.row_end - r0));
+      const int bytes = ns * rowbytes;
+      const unsigned char* src = X + r0 * rowbytes;
+      for (int blk = w; blk * 1024 < bytes; blk += W)
+        glds16(src + min(blk * 1024 + lane * 16, bytes - 16), dst + blk * 1024);
+      if (w == 0) {
+        const int lb = ns * static_cast<int>(sizeof(A));
+        glds4(Y + r0 * sizeof(A) + min(lane * 4, lb - 4), dst + data_bytes);
+      }
+    };
+
+    A g[NV][VN];
 #pragma unroll
-          for (int j = 0; j < NV; ++j) {
-            const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
-            const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
-            const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
-            z01 = __builtin_elementwise_fma(f2{v0.x, v1.x}, f2{b[j][0], b[j][0]}, z01);
-            z01 = __builtin_elementwise_fma(f2{v0.y, v1.y}, f2{b[j][1], b[j][1]}, z01);
-            z01 = __builtin_elementwise_fma(f2{v0.z, v1.z}, f2{b[j][2], b[j][2]}, z01);
-            z01 = __builtin_elementwise_fma(f2{v0.w, v1.w}, f2{b[j][3], b[j][3]}, z01);
-          }
-          z0 = z01.x;
-          z1 = z01.y;
-        } else {
+    for (int j = 0; j < NV; ++j)
 #pragma unroll
-          for (int j = 0; j < NV; ++j) {
-            const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
-            const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
-            const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
-#pragma unroll
-            for (int v = 0; v < VN; ++v) {
-              z0 = fma(Vec16<T>::template elem<A>(v0, v), b[j][v], z0);  // beta is 0 past the row end
-              z1 = fma(Vec16<T>::template elem<A>(v1, v), b[j][v], z1);
-            }
-          }
-        }
-        const A zs = wave_pair_reduce(z0, z1, hi);
-        const A rr = residual_branchfree<LOSS, A>(zs, lab[two && hi ? i + 1 : i], coef);
-        const A r0 = readlane_a(rr, 0);
-        const A r1 = two ? readlane_a(rr, 32) : A(0);
-        asm volatile("" ::: "memory");  // re-read the rows from LDS below
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
-          const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
-          const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
+      for (int v = 0; v < VN; ++v) g[j][v] = A(0);
+    // beta (first bundle) / the previous bundle's slab stores retired before the counted loads
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int t = 0; t < nstage - 1 && t < nst; ++t) issue(t);
+    for (int t = 0; t < nst; ++t) {
+      // loads this wave issued after stage t: stages t+1 .. hi, only stage nst-1 can be partial
+      const int hi = min(t + nstage - 2, nst - 1);
+      const int later = hi > t ? (hi - t) * cnt_full + (hi == nst - 1 ? cnt_last - cnt_full : 0) : 0;
+      wait_vmcnt(later);  // this wave's pieces of stage t landed
+      __syncthreads();    // every wave's pieces of stage t; stage t-1 consumed by every wave
+      if (t + nstage - 1 < nst) issue(t + nstage - 1);  // into the buffer stage t-1 used
+      if (!active) continue;
+      const unsigned char* buf = smem_raw + (t % nstage) * buf_bytes;
+      const A* lab = reinterpret_cast<const A*>(buf + data_bytes);
+      const int ns = min(srows, nrows - t * srows);
+      if constexpr (PAIR) {
+        // Two rows per step with ONE reduction and ONE residual evaluation between them: the two
+        // partial dot products are reduce-scattered (lanes 0-31 finish row i, lanes 32-63 row i+1),
+        // each lane evaluates the loss epilogue of its half's row (one exp for two rows), and the
+        // two residuals are broadcast by readlane.  The rows are re-read from LDS for the update
+        // rather than held in registers across the reduction.  A lone last row is paired with
+        // itself and weighted 0.
+        const bool hi = lane >= 32;
+        for (int i = 2 * sub; i < ns; i += 2 * wpr) {
+          const bool two = i + 1 < ns;
+          const unsigned char* row0 = buf + i * rowbytes;
+          const unsigned char* row1 = two ? row0 + rowbytes : row0;
+          A z0 = A(0), z1 = A(0);
           if constexpr (std::is_same<T, float>::value) {
+            // fp32: both rows' dot products in one packed accumulator {z0, z1} (v_pk_fma_f32)
             typedef float f2 __attribute__((ext_vector_type(2)));
-            const f2 rr0 = f2{r0, r0}, rr1 = f2{r1, r1};
-            f2 lo = __builtin_elementwise_fma(rr0, f2{v0.x, v0.y}, f2{g[j][0], g[j][1]});
-            f2 hi2 = __builtin_elementwise_fma(rr0, f2{v0.z, v0.w}, f2{g[j][2], g[j][3]});
-            lo = __builtin_elementwise_fma(rr1, f2{v1.x, v1.y}, lo);
-            hi2 = __builtin_elementwise_fma(rr1, f2{v1.z, v1.w}, hi2);
-            g[j][0] = lo.x;
-            g[j][1] = lo.y;
-            g[j][2] = hi2.x;
-            g[j][3] = hi2.y;
+            f2 z01 = f2{0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+              const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
+              const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
+              const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
+              z01 = __builtin_elementwise_fma(f2{v0.x, v1.x}, f2{b[j][0], b[j][0]}, z01);
+              z01 = __builtin_elementwise_fma(f2{v0.y, v1.y}, f2{b[j][1], b[j][1]}, z01);
+              z01 = __builtin_elementwise_fma(f2{v0.z, v1.z}, f2{b[j][2], b[j][2]}, z01);
+              z01 = __builtin_elementwise_fma(f2{v0.w, v1.w}, f2{b[j][3], b[j][3]}, z01);
+            }
+            z0 = z01.x;
+            z1 = z01.y;
           } else {
 #pragma unroll
-            for (int v = 0; v < VN; ++v) {
-              const A e0 = Vec16<T>::template elem<A>(v0, v);  // columns past the row end: never written
-              const A e1 = Vec16<T>::template elem<A>(v1, v);
-              g[j][v] = fma(r1, e1, fma(r0, e0, g[j][v]));
+            for (int j = 0; j < NV; ++j) {
+              const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
+              const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
+              const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
+#pragma unroll
+              for (int v = 0; v < VN; ++v) {
+                z0 = fma(Vec16<T>::template elem<A>(v0, v), b[j][v], z0);  // beta is 0 past the row end
+                z1 = fma(Vec16<T>::template elem<A>(v1, v), b[j][v], z1);
+              }
+            }
+          }
+          const A zs = wave_pair_reduce(z0, z1, hi);
+          const A rr = residual_branchfree<LOSS, A>(zs, lab[two && hi ? i + 1 : i], coef);
+          const A r0 = readlane_a(rr, 0);
+          const A r1 = two ? readlane_a(rr, 32) : A(0);
+          asm volatile("" ::: "memory");  // re-read the rows from LDS below
+#pragma unroll
+          for (int j = 0; j < NV; ++j) {
+            const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
+            const Rw v0 = *reinterpret_cast<const Rw*>(row0 + c0);
+            const Rw v1 = *reinterpret_cast<const Rw*>(row1 + c0);
+            if constexpr (std::is_same<T, float>::value) {
+              typedef float f2 __attribute__((ext_vector_type(2)));
+              const f2 rr0 = f2{r0, r0}, rr1 = f2{r1, r1};
+              f2 lo = __builtin_elementwise_fma(rr0, f2{v0.x, v0.y}, f2{g[j][0], g[j][1]});
+              f2 hi2 = __builtin_elementwise_fma(rr0, f2{v0.z, v0.w}, f2{g[j][2], g[j][3]});
+              lo = __builtin_elementwise_fma(rr1, f2{v1.x, v1.y}, lo);
+              hi2 = __builtin_elementwise_fma(rr1, f2{v1.z, v1.w}, hi2);
+              g[j][0] = lo.x;
+              g[j][1] = lo.y;
+              g[j][2] = hi2.x;
+              g[j][3] = hi2.y;
+            } else {
+#pragma unroll
+              for (int v = 0; v < VN; ++v) {
+                const A e0 = Vec16<T>::template elem<A>(v0, v);  // columns past the row end: never written
+                const A e1 = Vec16<T>::template elem<A>(v1, v);
+                g[j][v] = fma(r1, e1, fma(r0, e0, g[j][v]));
+              }
             }
           }
         }
+      } else if constexpr (std::is_same<T, float>::value) {
+        // fp32: the same row-at-a-time math on packed v_pk_fma_f32 (two columns per instruction).
+        // fp32 rows carry twice the elements per byte of fp64, so the VALU issue rate, not HBM, bound
+        // the scalar form (0.83 ms vs 0.73 ms of bytes at the headline); z keeps two partial sums.
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        for (int i = sub; i < ns; i += wpr) {
+          const unsigned char* row = buf + i * rowbytes;
+          Rw xr[NV];
+#pragma unroll
+          for (int j = 0; j < NV; ++j) {
+            const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
+            xr[j] = *reinterpret_cast<const Rw*>(row + c0);  // clamped read: see the scalar path below
+          }
+          f2 z2 = f2{0.f, 0.f};
+#pragma unroll
+          for (int j = 0; j < NV; ++j) {
+            z2 = __builtin_elementwise_fma(f2{xr[j].x, xr[j].y}, f2{b[j][0], b[j][1]}, z2);
+            z2 = __builtin_elementwise_fma(f2{xr[j].z, xr[j].w}, f2{b[j][2], b[j][3]}, z2);
+          }
+          const A rr = residual<LOSS, A>(wave_allreduce_sum(z2.x + z2.y), lab[i], coef);
+          const f2 r2 = f2{rr, rr};
+#pragma unroll
+          for (int j = 0; j < NV; ++j) {
+            const f2 lo = __builtin_elementwise_fma(r2, f2{xr[j].x, xr[j].y}, f2{g[j][0], g[j][1]});
+            const f2 hi = __builtin_elementwise_fma(r2, f2{xr[j].z, xr[j].w}, f2{g[j][2], g[j][3]});
+            g[j][0] = lo.x;
+            g[j][1] = lo.y;
+            g[j][2] = hi.x;
+            g[j][3] = hi.y;
+          }
+        }
+      } else {
+        // one row at a time
+        for (int i = sub; i < ns; i += wpr) {
+          const unsigned char* row = buf + i * rowbytes;
+          Rw xr[NV];
+#pragma unroll
+          for (int j = 0; j < NV; ++j) {
+            // Clamped read: past the row end a lane re-reads the row's last vector.  It is not
+            // masked: beta is 0 there, so its dot-product terms add exactly 0 (finite data), and the
+            // gradient columns it pollutes are never written.  A per-vector select compiled to exec
+            // branches and 64-bit moves that cost as much as the row's FMAs.
+            const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
+            xr[j] = *reinterpret_cast<const Rw*>(row + c0);
+          }
+          A z = A(0);  // one accumulator: four independent chains measured no faster
+#pragma unroll
+          for (int j = 0; j < NV; ++j)
+#pragma unroll
+            for (int v = 0; v < VN; ++v) z = fma(Vec16<T>::template elem<A>(xr[j], v), b[j][v], z);
+          const A rr = residual<LOSS, A>(wave_allreduce_sum(z), lab[i], coef);
+#pragma unroll
+          for (int j = 0; j < NV; ++j)
+#pragma unroll
+            for (int v = 0; v < VN; ++v) g[j][v] = fma(rr, Vec16<T>::template elem<A>(xr[j], v), g[j][v]);
+        }
       }
-    } else if constexpr (std::is_same<T, float>::value) {
-      // fp32: the same row-at-a-time math on packed v_pk_fma_f32 (two columns per instruction).
-      // fp32 rows carry twice the elements per byte of fp64, so the VALU issue rate, not HBM, bound
-      // the scalar form (0.83 ms vs 0.73 ms of bytes at the headline); z keeps two partial sums.
-      typedef float f2 __attribute__((ext_vector_type(2)));
-      for (int i = sub; i < ns; i += wpr) {
-        const unsigned char* row = buf + i * rowbytes;
-        Rw xr[NV];
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
-          xr[j] = *reinterpret_cast<const Rw*>(row + c0);  // clamped read: see the scalar path below
-        }
-        f2 z2 = f2{0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          z2 = __builtin_elementwise_fma(f2{xr[j].x, xr[j].y}, f2{b[j][0], b[j][1]}, z2);
-          z2 = __builtin_elementwise_fma(f2{xr[j].z, xr[j].w}, f2{b[j][2], b[j][3]}, z2);
-        }
-        const A rr = residual<LOSS, A>(wave_allreduce_sum(z2.x + z2.y), lab[i], coef);
-        const f2 r2 = f2{rr, rr};
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          const f2 lo = __builtin_elementwise_fma(r2, f2{xr[j].x, xr[j].y}, f2{g[j][0], g[j][1]});
-          const f2 hi = __builtin_elementwise_fma(r2, f2{xr[j].z, xr[j].w}, f2{g[j][2], g[j][3]});
-          g[j][0] = lo.x;
-          g[j][1] = lo.y;
-          g[j][2] = hi.x;
-          g[j][3] = hi.y;
-        }
-      }
-    } else {
-      // one row at a time
-      for (int i = sub; i < ns; i += wpr) {
-        const unsigned char* row = buf + i * rowbytes;
-        Rw xr[NV];
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          // Clamped read: past the row end a lane re-reads the row's last vector.  It is not
-          // masked: beta is 0 there, so its dot-product terms add exactly 0 (finite data), and the
-          // gradient columns it pollutes are never written.  A per-vector select compiled to exec
-          // branches and 64-bit moves that cost as much as the row's FMAs.
-          const int c0 = min((j * kWave + lane) * VN, ld - VN) * static_cast<int>(sizeof(T));
-          xr[j] = *reinterpret_cast<const Rw*>(row + c0);
-        }
-        A z = A(0);  // one accumulator: four independent chains measured no faster
+    }
+    if (wpr > 1) {  // fold the slot's waves through LDS (the ring is free after this barrier)
+      A* fold = reinterpret_cast<A*>(smem_raw);
+      __syncthreads();
+      if (active && sub > 0) {
 #pragma unroll
         for (int j = 0; j < NV; ++j)
 #pragma unroll
-          for (int v = 0; v < VN; ++v) z = fma(Vec16<T>::template elem<A>(xr[j], v), b[j][v], z);
-        const A rr = residual<LOSS, A>(wave_allreduce_sum(z), lab[i], coef);
+          for (int v = 0; v < VN; ++v) fold[(((sub - 1) * R + q) * NV * VN + j * VN + v) * kWave + lane] = g[j][v];
+      }
+      __syncthreads();
+      if (active && sub == 0) {
+        for (int k = 0; k < wpr - 1; ++k)
 #pragma unroll
-        for (int j = 0; j < NV; ++j)
+          for (int j = 0; j < NV; ++j)
 #pragma unroll
-          for (int v = 0; v < VN; ++v) g[j][v] = fma(rr, Vec16<T>::template elem<A>(xr[j], v), g[j][v]);
+            for (int v = 0; v < VN; ++v) g[j][v] += fold[((k * R + q) * NV * VN + j * VN + v) * kWave + lane];
       }
     }
-  }
-  if (wpr > 1) {  // fold the slot's waves through LDS (the ring is free after this barrier)
-    A* fold = reinterpret_cast<A*>(smem_raw);
-    __syncthreads();
-    if (active && sub > 0) {
-#pragma unroll
-      for (int j = 0; j < NV; ++j)
-#pragma unroll
-        for (int v = 0; v < VN; ++v) fold[(((sub - 1) * R + q) * NV * VN + j * VN + v) * kWave + lane] = g[j][v];
-    }
-    __syncthreads();
     if (active && sub == 0) {
-      for (int k = 0; k < wpr - 1; ++k)
+      A* out = slab + static_cast<long long>(task.slab) * ld;
 #pragma unroll
-        for (int j = 0; j < NV; ++j)
+      for (int j = 0; j < NV; ++j) {
+        const int c0 = (j * kWave + lane) * VN;
 #pragma unroll
-          for (int v = 0; v < VN; ++v) g[j][v] += fold[((k * R + q) * NV * VN + j * VN + v) * kWave + lane];
+        for (int v = 0; v < VN; ++v)
+          if (c0 + v < ld) out[c0 + v] = g[j][v];
+      }
     }
-  }
-  if (!active || sub > 0) return;
-  A* out = slab + static_cast<long long>(task.slab) * ld;
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const int c0 = (j * kWave + lane) * VN;
-#pragma unroll
-    for (int v = 0; v < VN; ++v)
-      if (c0 + v < ld) out[c0 + v] = g[j][v];
+    if (!ticket) break;
+    if (threadIdx.x == 0) {
+      const unsigned int raw = atomicAdd(ticket, 1u);
+      if (raw == static_cast<unsigned int>(nbundles) - 1u)  // the launch's last draw: reset for the next one
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_next = static_cast<int>(raw) + static_cast<int>(gridDim.x);
+    }
+    __syncthreads();  // s_next, and every wave is done with the ring before the next bundle's loads
+    bundle = s_next;
   }
 }
 
@@ -903,9 +927,25 @@ static int fused_rows(int requested) {
   return std::is_same<T, float>::value ? 4 : 1;
 }
 
+// Workgroups of a staged kernel resident at once on the whole device (persistent grid size).
+static int staged_slots(const void* kern, int block, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, int, size_t>, int> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_tuple(kern, block, lds);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds) != hipSuccess || cus <= 0 || per_cu <= 0)
+    return 1 << 30;  // unknown: no persistence (grid = bundles)
+  return cache[key] = cus * per_cu;
+}
+
 template <typename T, typename A, int LOSS>
 static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
-                                   const A* beta, A* slab, int ld, hipStream_t st, int variant) {
+                                   const A* beta, A* slab, int ld, hipStream_t st, int variant,
+                                   unsigned int* ticket) {
   const int want_wpr = variant / 100;  // staged bundles: waves per replica requested by the plan
   variant %= 100;
   if (variant > 40 && variant <= 56) {  // bf16 replica bundles on MFMA (grad_mfma.hip), R = variant - 40
@@ -940,9 +980,12 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sg.lds));      \
           if (ea != hipSuccess) return ea;                                                \
         }                                                                                 \
-        hipLaunchKernelGGL(kern, dim3(ntasks / staged_r), dim3(64 * staged_r * sg.wpr),   \
+        const int nb_ = ntasks / staged_r;                                                \
+        const int grid_ = ticket ? std::min(nb_, staged_slots(reinterpret_cast<const void*>(kern), \
+                              64 * staged_r * sg.wpr, sg.lds)) : nb_;                      \
+        hipLaunchKernelGGL(kern, dim3(grid_), dim3(64 * staged_r * sg.wpr),                \
                            sg.lds, st, segs, tasks, beta, slab, ld, sg.srows, sg.pieces,  \
-                           sg.nstage, sg.wpr);                                            \
+                           sg.nstage, sg.wpr, nb_, grid_ < nb_ ? ticket : nullptr);       \
         return hipGetLastError();                                                         \
       }                                                                                   \
       if (bundle_r) {                                                                     \
@@ -993,19 +1036,24 @@ hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, con
                              const PutDesc* put) {
   const Segment* S = static_cast<const Segment*>(segs);
   const Task* Tk = static_cast<const Task*>(tasks);
+  // the staged kernels' persistent-grid ticket lives right after the partial sums (slab_part_bytes)
+  static const bool persistent = env_int("ERASUREHEAD_PERSISTENT", 0) != 0;  // opt-in until measured
+  unsigned int* tk = persistent ? reinterpret_cast<unsigned int*>(static_cast<char*>(part) +
+                                                                   slab_part_bytes(nslots, ld, dtype == 0 ? 8 : 4) - 16)
+                                : nullptr;
   hipError_t e = hipSuccess;
   if (dtype == 0) {
     e = loss == kLogistic
-            ? launch_fused_cpl<double, double, kLogistic>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, variant)
-            : launch_fused_cpl<double, double, kLeastSquares>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, variant);
+            ? launch_fused_cpl<double, double, kLogistic>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, variant, tk)
+            : launch_fused_cpl<double, double, kLeastSquares>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, variant, tk);
   } else if (dtype == 1) {
     e = loss == kLogistic
-            ? launch_fused_cpl<float, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant)
-            : launch_fused_cpl<float, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant);
+            ? launch_fused_cpl<float, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant, tk)
+            : launch_fused_cpl<float, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant, tk);
   } else {
     e = loss == kLogistic
-            ? launch_fused_cpl<bf16_t, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant)
-            : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant);
+            ? launch_fused_cpl<bf16_t, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant, tk)
+            : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant, tk);
   }
   if (e != hipSuccess) return e;
   if (dtype == 0) return slab_reduce_launch<double>((const double*)slab, slot_task_begin, (double*)part, (double*)G, nslots, ld, st, put);

@@ -183,6 +183,8 @@ std::shared_ptr<GradLauncher> make_dense(int64_t dtype, int64_t loss, int64_t cp
   g->ld = (int)ld;
   g->ntasks = (int)tasks.size(0);
   g->nslots = (int)stb.numel() - 1;
+  need(part.numel() * part.element_size() >= eh::slab_part_bytes(g->nslots, ld, dtype == 0 ? 8 : 4),
+       "part must hold the partial sums + the persistent-grid ticket (grad.py DenseGradPlan)");
   g->segs = segs.data_ptr();
   g->tasks = tasks.data_ptr();
   g->slab = slab.data_ptr();

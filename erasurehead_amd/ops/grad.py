@@ -207,7 +207,10 @@ class DenseGradPlan:
         self.tasks = torch.from_numpy(t).to(dev)
         self.slot_task_begin = torch.tensor(slot_begin, dtype=torch.int32, device=dev)
         self.slab = torch.empty((max(1, self.ntasks), self.ld), dtype=self.prec.acc, device=dev)
-        self.part = torch.empty(max(1, self.nslots) * SLAB_SPLITS * self.ld, dtype=self.prec.acc, device=dev)
+        # partial sums [nslots, SLAB_SPLITS, ld], then 16 zeroed bytes: the staged kernels' persistent-grid
+        # ticket (csrc/kernels/launchers.h slab_part_bytes)
+        es = torch.tensor([], dtype=self.prec.acc).element_size()
+        self.part = torch.zeros(max(1, self.nslots) * SLAB_SPLITS * self.ld + 16 // es, dtype=self.prec.acc, device=dev)
         if self.cpl is None:
             off = np.zeros(max(1, self.ntasks), dtype=np.int64)
             if self.ntasks:
