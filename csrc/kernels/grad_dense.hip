@@ -494,7 +494,7 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
 // Stage geometry of grad_dense_staged: rows per stage, 1 KiB pieces per wave and ring depth.
 // Defaults measured at the headline (tools/sweep_staged.sh); ERASUREHEAD_STAGE_ROWS and
 // ERASUREHEAD_STAGES override them for sweeps.  Rows shrink until the ring fits kStagedLds.
-constexpr int kStagedLds = 160 * 1024;
+constexpr int kStagedLds = 160 * 1024 - 256;  // 160 KiB per workgroup, less the kernel's static LDS (s_next)
 struct StagedGeom {
   int srows, pieces, nstage, wpr;
   size_t lds;
