@@ -946,6 +946,8 @@ template <typename T, typename A, int LOSS>
 static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
                                    const A* beta, A* slab, int ld, hipStream_t st, int variant,
                                    unsigned int* ticket) {
+  if (variant < 1000) ticket = nullptr;  // staged bundles: persistent workgroups requested by the plan
+  variant %= 1000;
   const int want_wpr = variant / 100;  // staged bundles: waves per replica requested by the plan
   variant %= 100;
   if (variant > 40 && variant <= 56) {  // bf16 replica bundles on MFMA (grad_mfma.hip), R = variant - 40
@@ -1036,11 +1038,10 @@ hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, con
                              const PutDesc* put) {
   const Segment* S = static_cast<const Segment*>(segs);
   const Task* Tk = static_cast<const Task*>(tasks);
-  // the staged kernels' persistent-grid ticket lives right after the partial sums (slab_part_bytes)
-  static const bool persistent = env_int("ERASUREHEAD_PERSISTENT", 0) != 0;  // opt-in until measured
-  unsigned int* tk = persistent ? reinterpret_cast<unsigned int*>(static_cast<char*>(part) +
-                                                                   slab_part_bytes(nslots, ld, dtype == 0 ? 8 : 4) - 16)
-                                : nullptr;
+  // the staged kernels' persistent-grid ticket lives right after the partial sums (slab_part_bytes);
+  // used when the plan's variant asks for persistent workgroups (>= 1000)
+  unsigned int* tk = reinterpret_cast<unsigned int*>(static_cast<char*>(part) +
+                                                     slab_part_bytes(nslots, ld, dtype == 0 ? 8 : 4) - 16);
   hipError_t e = hipSuccess;
   if (dtype == 0) {
     e = loss == kLogistic

@@ -237,7 +237,12 @@ class DenseGradPlan:
             raise ValueError("MFMA bundles hold at most 16 replicas")
         self.variant = (40 if self.mfma else 30 if self.staged_pair else 20 if self.staged else 10) + R
         if self.staged and self.staged_wpr:
-            self.variant += 100 * self.staged_wpr  # csrc: variant / 100 = waves per replica
+            self.variant += 100 * self.staged_wpr  # csrc: variant / 100 % 10 = waves per replica
+        # persistent staged workgroups (csrc: variant >= 1000): as many workgroups as fit, each taking
+        # bundles from an atomic ticket until none is left; ERASUREHEAD_PERSISTENT=1 (read per plan)
+        self.persistent = bool(self.staged and os.environ.get("ERASUREHEAD_PERSISTENT", "0") == "1")
+        if self.persistent:
+            self.variant += 1000
         return table
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:

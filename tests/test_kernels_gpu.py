@@ -278,6 +278,32 @@ def test_dense_grad_staged_is_the_replica_default(prec_name, native, monkeypatch
     torch.testing.assert_close(Ga, Gb, rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("prec_name", ["fp64", "fp32"])
+def test_dense_grad_staged_persistent_grid_is_bitwise_identical(prec_name, native, monkeypatch):
+    """Persistent staged workgroups (ERASUREHEAD_PERSISTENT=1: as many workgroups as fit, bundles handed
+    out by an atomic ticket) compute every bundle exactly as one-bundle-per-workgroup does, launch after
+    launch (the ticket resets itself): bitwise-equal messages, with far more bundles than slots."""
+    monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", "16")
+    monkeypatch.delenv("ERASUREHEAD_STAGED", raising=False)
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(21)
+    parts, _ = _parts(rng, [20000, 20000, 20000], 1000, prec)
+    msgs = [[(0, 1.0)]] * 3 + [[(1, 1.0)]] * 3 + [[(2, -0.5)]] * 2
+    monkeypatch.setenv("ERASUREHEAD_PERSISTENT", "0")
+    a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
+    monkeypatch.setenv("ERASUREHEAD_PERSISTENT", "1")
+    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
+    assert a.staged and b.persistent and not a.persistent and b.variant == a.variant + 1000
+    assert b.ntasks // 3 > 1024  # more bundles than the chip holds at once: the ticket hands them out
+    Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
+    for k in range(3):
+        beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
+        a.native_launcher().launch(beta, Ga)
+        b.native_launcher().launch(beta, Gb)
+        torch.cuda.synchronize()
+        assert torch.equal(Ga, Gb), f"launch {k}"
+
+
 def test_eval_gemm_unaligned_rows_use_scalar_staging(native):
     """Rows whose stride is not a 16-byte multiple take the scalar-staging eval kernel (v1)."""
     rng = np.random.RandomState(9)
