@@ -238,7 +238,7 @@ template <typename T, typename A, int CPL, int LOSS, bool PAIR>
 __global__ void __launch_bounds__(512)
 grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                   const A* __restrict__ beta, A* __restrict__ slab, int ld, int srows, int pieces, int nstage,
-                  int wpr, int nbundles, unsigned int* ticket) {
+                  int wpr, int nbundles, unsigned int* ticket, int rot_mul) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -277,6 +277,11 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
     const A coef = active ? static_cast<A>(segs[task.seg].coef) : A(0);
     const int nrows = lead.row_end - lead.row_begin;
     const int nst = (nrows + srows - 1) / srows;
+    // rot_mul > 0: each bundle walks its stages starting at a bundle-dependent offset (wrapping), so
+    // workgroups that start together do not stream the same relative addresses in lockstep
+    const int rot = rot_mul > 0 ? static_cast<int>((static_cast<long long>(bundle) * rot_mul) % nst) : 0;
+    auto stage_of = [&](int t) { return t + rot < nst ? t + rot : t + rot - nst; };
+    const int p_last = nst - 1 - rot;  // loop position of the (possibly partial) last stage
 
     // LDS-DMA loads wave w issues for a stage of nbytes: its 1 KiB pieces (+ labels: wave 0).  Every
     // stage but the last is full, so two counts cover the ring; computing them once keeps integer
@@ -289,7 +294,7 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
     const int cnt_last = count_bytes((nrows - (nst - 1) * srows) * rowbytes);
     auto issue = [&](int t) {
       const unsigned dst = lds_base + (t % nstage) * buf_bytes;
-      const long long r0 = lead.row_begin + static_cast<long long>(t) * srows;
+      const long long r0 = lead.row_begin + static_cast<long long>(stage_of(t)) * srows;
       const int ns = min(srows, static_cast<int>(lead.row_end - r0));
       const int bytes = ns * rowbytes;
       const unsigned char* src = X + r0 * rowbytes;
@@ -310,16 +315,16 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int t = 0; t < nstage - 1 && t < nst; ++t) issue(t);
     for (int t = 0; t < nst; ++t) {
-      // loads this wave issued after stage t: stages t+1 .. hi, only stage nst-1 can be partial
+      // loads this wave issued after stage t: loop positions t+1 .. hi; only the stage at p_last can be partial
       const int hi = min(t + nstage - 2, nst - 1);
-      const int later = hi > t ? (hi - t) * cnt_full + (hi == nst - 1 ? cnt_last - cnt_full : 0) : 0;
+      const int later = hi > t ? (hi - t) * cnt_full + (p_last > t && p_last <= hi ? cnt_last - cnt_full : 0) : 0;
       wait_vmcnt(later);  // this wave's pieces of stage t landed
       __syncthreads();    // every wave's pieces of stage t; stage t-1 consumed by every wave
       if (t + nstage - 1 < nst) issue(t + nstage - 1);  // into the buffer stage t-1 used
       if (!active) continue;
       const unsigned char* buf = smem_raw + (t % nstage) * buf_bytes;
       const A* lab = reinterpret_cast<const A*>(buf + data_bytes);
-      const int ns = min(srows, nrows - t * srows);
+      const int ns = min(srows, nrows - stage_of(t) * srows);
       if constexpr (PAIR) {
         // Two rows per step with ONE reduction and ONE residual evaluation between them: the two
         // partial dot products are reduce-scattered (lanes 0-31 finish row i, lanes 32-63 row i+1),
@@ -927,6 +932,12 @@ static int fused_rows(int requested) {
   return std::is_same<T, float>::value ? 4 : 1;
 }
 
+// ERASUREHEAD_STAGE_ROTATE=k > 0: bundle b starts its stage walk at (b * k) mod stages (A/B knob).
+static int stage_rotate() {
+  static const int k = env_int("ERASUREHEAD_STAGE_ROTATE", 0);
+  return k;
+}
+
 // Workgroups of a staged kernel resident at once on the whole device (persistent grid size).
 static int staged_slots(const void* kern, int block, size_t lds) {
   static std::mutex mu;
@@ -987,7 +998,8 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
                               64 * staged_r * sg.wpr, sg.lds)) : nb_;                      \
         hipLaunchKernelGGL(kern, dim3(grid_), dim3(64 * staged_r * sg.wpr),                \
                            sg.lds, st, segs, tasks, beta, slab, ld, sg.srows, sg.pieces,  \
-                           sg.nstage, sg.wpr, nb_, grid_ < nb_ ? ticket : nullptr);       \
+                           sg.nstage, sg.wpr, nb_, grid_ < nb_ ? ticket : nullptr,        \
+                           stage_rotate());                                               \
         return hipGetLastError();                                                         \
       }                                                                                   \
       if (bundle_r) {                                                                     \
