@@ -22,6 +22,7 @@
 // (e.g. all 8 FRC/AGC workers at N=1): task -> (output message slot, segment,
 // row range); segment -> (partition base pointer, labels, encoding coefficient).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -946,10 +947,15 @@ static int staged_slots(const void* kern, int block, size_t lds) {
   const auto key = std::make_tuple(kern, block, lds);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
+  static const int env_per_cu = env_int("ERASUREHEAD_PERSISTENT_PER_CU", 0);  // A/B override
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds) != hipSuccess || cus <= 0 || per_cu <= 0)
     return 1 << 30;  // unknown: no persistence (grid = bundles)
+  if (env_per_cu > 0) per_cu = env_per_cu;
+  if (std::getenv("ERASUREHEAD_PERSISTENT_VERBOSE"))
+    std::fprintf(stderr, "[erasurehead] persistent staged grid: %d CUs x %d workgroups (block %d, LDS %zu)\n", cus,
+                 per_cu, block, lds);
   return cache[key] = cus * per_cu;
 }
 
