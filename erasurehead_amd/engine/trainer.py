@@ -688,6 +688,8 @@ class Trainer:
         time-sharing one GPU keep host waits (a queued wait competes with the other ranks' kernels
         there: profiles/r2_worker_wait/).  ERASUREHEAD_WORKER_WAIT=host|device|auto."""
         mode = os.environ.get("ERASUREHEAD_WORKER_WAIT", "auto")
+        if getattr(tx, "name", "") != "ipc" or mode == "host":
+            return False
         buses = [p.get("master_bus") for p in tx.pairs[:1]] + [p.get("bus") for p in tx.pairs]
         shared = len(set(buses)) < len(buses)
         return mode == "device" or (mode == "auto" and not shared)
