@@ -239,7 +239,7 @@ template <typename T, typename A, int CPL, int LOSS, bool PAIR>
 __global__ void __launch_bounds__(512)
 grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                   const A* __restrict__ beta, A* __restrict__ slab, int ld, int srows, int pieces, int nstage,
-                  int wpr, int nbundles, unsigned int* ticket, int rot_mul, int pf) {
+                  int wpr, int nbundles, unsigned int* ticket, int rot_mul) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -293,19 +293,6 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
     };
     const int cnt_full = count_bytes(srows * rowbytes);
     const int cnt_last = count_bytes((nrows - (nst - 1) * srows) * rowbytes);
-    // pf > 0: L2 prefetch pf stages ahead of the ring.  The ring's in-flight bytes are bounded by
-    // LDS (one stage per workgroup with two stages), so each issue(t) also touches every 128-byte
-    // line of stage t + pf with one 4-byte LDS-DMA per lane into a scratch word after the ring
-    // (no VGPR is left waiting on the load); the ring's copy of that stage then hits in L2.
-    auto count_pf = [&](int nbytes) {
-      const int nb = (nbytes + 8191) >> 13;  // one wave-load covers 64 lines = 8 KiB
-      return nb > w ? (nb - w + W - 1) / W : 0;
-    };
-    const int pf_full = pf > 0 ? count_pf(srows * rowbytes) : 0;
-    const int pf_last = pf > 0 ? count_pf((nrows - (nst - 1) * srows) * rowbytes) : 0;
-    auto pf_count = [&](int t) {  // prefetch loads issue(t) makes on this wave
-      return pf > 0 && t + pf < nst ? (t + pf == p_last ? pf_last : pf_full) : 0;
-    };
     auto issue = [&](int t) {
       const unsigned dst = lds_base + (t % nstage) * buf_bytes;
       const long long r0 = lead.row_begin + static_cast<long long>(stage_of(t)) * srows;
@@ -317,13 +304,6 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
       if (w == 0) {
         const int lb = ns * static_cast<int>(sizeof(A));
         glds4(Y + r0 * sizeof(A) + min(lane * 4, lb - 4), dst + data_bytes);
-      }
-      if (pf > 0 && t + pf < nst) {
-        const long long p0 = lead.row_begin + static_cast<long long>(stage_of(t + pf)) * srows;
-        const int pbytes = min(srows, static_cast<int>(lead.row_end - p0)) * rowbytes;
-        const unsigned char* psrc = X + p0 * rowbytes;
-        for (int blk = w; blk * 8192 < pbytes; blk += W)
-          glds4(psrc + min(blk * 8192 + lane * 128, pbytes - 4), lds_base + nstage * buf_bytes);
       }
     };
 
@@ -338,10 +318,7 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
     for (int t = 0; t < nst; ++t) {
       // loads this wave issued after stage t: loop positions t+1 .. hi; only the stage at p_last can be partial
       const int hi = min(t + nstage - 2, nst - 1);
-      int later = hi > t ? (hi - t) * cnt_full + (p_last > t && p_last <= hi ? cnt_last - cnt_full : 0) : 0;
-      if (pf > 0) {  // + the prefetches issued with stage t and with the stages after it
-        for (int x = t; x <= hi; ++x) later += pf_count(x);
-      }
+      const int later = hi > t ? (hi - t) * cnt_full + (p_last > t && p_last <= hi ? cnt_last - cnt_full : 0) : 0;
       wait_vmcnt(later);  // this wave's pieces of stage t landed
       __syncthreads();    // every wave's pieces of stage t; stage t-1 consumed by every wave
       if (t + nstage - 1 < nst) issue(t + nstage - 1);  // into the buffer stage t-1 used
@@ -962,12 +939,6 @@ static int stage_rotate() {
   return k;
 }
 
-// L2 prefetch distance of the staged kernels in stages beyond the ring (0 = off; A/B knob).
-static int stage_prefetch() {
-  static const int k = env_int("ERASUREHEAD_STAGE_PREFETCH", 0);
-  return k < 0 ? 0 : k;
-}
-
 // Workgroups of a staged kernel resident at once on the whole device (persistent grid size).
 static int staged_slots(const void* kern, int block, size_t lds) {
   static std::mutex mu;
@@ -1023,8 +994,6 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
       if (staged_r) {                                                                     \
         auto kern = staged_pair ? grad_dense_staged<T, A, C, LOSS, true>                  \
                                 : grad_dense_staged<T, A, C, LOSS, false>;                \
-        const int pf_ = sg.lds + 256 <= kStagedLds ? stage_prefetch() : 0;                \
-        if (pf_ > 0) sg.lds += 256; /* the prefetch's scratch word per lane */            \
         if (sg.lds > 65536) {                                                             \
           const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),   \
               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sg.lds));      \
@@ -1036,7 +1005,7 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
         hipLaunchKernelGGL(kern, dim3(grid_), dim3(64 * staged_r * sg.wpr),                \
                            sg.lds, st, segs, tasks, beta, slab, ld, sg.srows, sg.pieces,  \
                            sg.nstage, sg.wpr, nb_, grid_ < nb_ ? ticket : nullptr,        \
-                           stage_rotate(), pf_);                                          \
+                           stage_rotate());                                               \
         return hipGetLastError();                                                         \
       }                                                                                   \
       if (bundle_r) {                                                                     \
