@@ -32,3 +32,32 @@ def test_kernel_comment_edit_makes_build_stale(tmp_path):
     out = subprocess.run([sys.executable, "-c", probe], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert out.stdout.startswith("STALE"), out.stdout + out.stderr
     assert "stale native build" in out.stdout
+
+
+def _hold_build_lock(q, hold_s):
+    import time
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import build_ext  # type: ignore
+
+    with build_ext._build_lock():
+        t0 = time.monotonic()
+        time.sleep(hold_s)
+        q.put((t0, time.monotonic()))
+
+
+def test_build_lock_serializes_processes():
+    """torchrun starts every rank at once: ranks that find a stale library must build one at a time
+    (the later ones then find the objects and the library current) instead of racing on build/."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_hold_build_lock, args=(q, 0.4)) for _ in range(3)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    spans = sorted(q.get(timeout=5) for _ in ps)
+    for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+        assert b0 >= a1, f"overlapping build-lock holders: {spans}"

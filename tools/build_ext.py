@@ -19,6 +19,8 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import contextlib
+import fcntl
 import glob
 import hashlib
 import os
@@ -117,7 +119,25 @@ def _run(cmd):
     return r.stdout
 
 
+@contextlib.contextmanager
+def _build_lock():
+    """One build at a time per tree: ranks that all find a stale library (torchrun starts N at once)
+    queue here, and the ones after the first find the objects and library already current."""
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".build.lock"), "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(f, fcntl.LOCK_UN)
+
+
 def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
+    with _build_lock():
+        return _build(force, jobs, verbose)
+
+
+def _build(force: bool, jobs: int, verbose: bool) -> str:
     inc, torchlib, abi = _torch_paths()
     pyinc = sysconfig.get_paths()["include"]
     os.makedirs(BUILD, exist_ok=True)
@@ -159,14 +179,15 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
                 print("compiled", os.path.relpath(futs[f], ROOT), log, flush=True)
     objs = [o for (_, o, _) in jobs_list]
     if force or todo or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
-        link = [os.path.join(ROCM, "bin", "hipcc"), "-shared", "-fPIC", "-o", out + ".tmp", *objs,
+        tmp = f"{out}.{os.getpid()}.tmp"
+        link = [os.path.join(ROCM, "bin", "hipcc"), "-shared", "-fPIC", "-o", tmp, *objs,
                 f"--offload-arch={ARCH}", f"-L{torchlib}", f"-Wl,-rpath,{torchlib}",
                 "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64",
                 f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx"]
         _run(link)
-        if embedded_hash(out + ".tmp") != want:
+        if embedded_hash(tmp) != want:
             raise RuntimeError("build: linked library does not carry the tree's source hash")
-        os.replace(out + ".tmp", out)
+        os.replace(tmp, out)
         if verbose:
             print("linked", os.path.relpath(out, ROOT), flush=True)
     return out
