@@ -235,7 +235,10 @@ grad_dense_bundle(const Segment* __restrict__ segs, const Task* __restrict__ tas
 // its own coefficient, and gradient accumulation — and writes its own slab row.  The rows of a
 // stage are contiguous in HBM, so a stage is one flat copy split into 1 KiB wave pieces (lane-
 // linear LDS image).  Labels ride along as one 4-byte-per-lane LDS-DMA piece.
-template <typename T, typename A, int CPL, int LOSS, bool PAIR>
+// EXT: the opt-in scheduling modes (persistent ticket loop, stage-walk rotation) are compiled in.
+// The default instantiation leaves them out: the bundle loop and the rotation cost the fp32 pair
+// kernel 13 VGPRs (80 -> 93, 6 -> 5 waves per SIMD: 0.77 -> 0.82 ms at the headline).
+template <typename T, typename A, int CPL, int LOSS, bool PAIR, bool EXT>
 __global__ void __launch_bounds__(512)
 grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                   const A* __restrict__ beta, A* __restrict__ slab, int ld, int srows, int pieces, int nstage,
@@ -280,7 +283,7 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
     const int nst = (nrows + srows - 1) / srows;
     // rot_mul > 0: each bundle walks its stages starting at a bundle-dependent offset (wrapping), so
     // workgroups that start together do not stream the same relative addresses in lockstep
-    const int rot = rot_mul > 0 ? static_cast<int>((static_cast<long long>(bundle) * rot_mul) % nst) : 0;
+    const int rot = EXT && rot_mul > 0 ? static_cast<int>((static_cast<long long>(bundle) * rot_mul) % nst) : 0;
     auto stage_of = [&](int t) { return t + rot < nst ? t + rot : t + rot - nst; };
     const int p_last = nst - 1 - rot;  // loop position of the (possibly partial) last stage
 
@@ -485,7 +488,7 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
           if (c0 + v < ld) out[c0 + v] = g[j][v];
       }
     }
-    if (!ticket) break;
+    if (!EXT || !ticket) break;
     if (threadIdx.x == 0) {
       const unsigned int raw = atomicAdd(ticket, 1u);
       if (raw == static_cast<unsigned int>(nbundles) - 1u)  // the launch's last draw: reset for the next one
@@ -992,8 +995,11 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
   case C:                                                                                 \
     if constexpr (C % VN == 0) {                                                          \
       if (staged_r) {                                                                     \
-        auto kern = staged_pair ? grad_dense_staged<T, A, C, LOSS, true>                  \
-                                : grad_dense_staged<T, A, C, LOSS, false>;                \
+        const bool ext_ = ticket != nullptr || stage_rotate() > 0;                        \
+        auto kern = staged_pair ? (ext_ ? grad_dense_staged<T, A, C, LOSS, true, true>    \
+                                        : grad_dense_staged<T, A, C, LOSS, true, false>)  \
+                                : (ext_ ? grad_dense_staged<T, A, C, LOSS, false, true>   \
+                                        : grad_dense_staged<T, A, C, LOSS, false, false>); \
         if (sg.lds > 65536) {                                                             \
           const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),   \
               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sg.lds));      \
