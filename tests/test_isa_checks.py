@@ -61,3 +61,45 @@ def test_staged_kernels_issue_no_compiler_loads_inside_the_stage_pipeline(tmp_pa
                     bad.append(body[i])
             assert not bad, f"{name}: compiler-emitted vector loads inside the counted stage loop: {bad[:4]}"
     assert checked >= 48, f"only {checked} staged kernel instantiations found"
+
+
+READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+
+
+def _kernel_regs(path):
+    """{mangled kernel name: (vgpr_count, vgpr_spill_count)} from the code object's metadata notes."""
+    out = subprocess.run([READELF, "--notes", path], capture_output=True, text=True, check=True).stdout
+    regs, cur = {}, {}
+    for line in out.splitlines():
+        m = re.match(r"\s*-?\s*\.(name|vgpr_count|vgpr_spill_count):\s+(\S+)", line)
+        if not m:
+            continue
+        cur[m.group(1)] = m.group(2)
+        if {"name", "vgpr_count", "vgpr_spill_count"} <= cur.keys():
+            regs[cur["name"]] = (int(cur["vgpr_count"]), int(cur["vgpr_spill_count"]))
+            cur = {}
+    return regs
+
+
+@pytest.mark.skipif(not os.path.exists(READELF), reason="llvm-readelf not installed")
+def test_default_staged_kernels_keep_their_occupancy(tmp_path):
+    """Register budgets of the headline kernels (d <= 1024: 16 columns per lane).  Waves per SIMD =
+    512 // VGPRs rounded up to 8: fp32 pair bundles need <= 80 for 6 waves (93 -> 5 cost 10 % at the
+    fp32 headline, docs/PERF_NOTES.md round 3), fp64 <= 168 for 3.  No default instantiation for
+    d <= 1024 spills."""
+    regs = {}
+    for co in _code_objects(tmp_path):
+        regs.update(_kernel_regs(co))
+    staged = {n: r for n, r in regs.items() if "grad_dense_staged" in n and "Lb0EEEv" in n}  # EXT = false
+    assert staged, "no default staged instantiations found"
+    for n, (v, spill) in staged.items():  # d <= 1024; fp64 at 32 columns per lane (d <= 2048) spills 4
+        if re.search(r"Li(2|4|8|16)ELi", n):
+            assert spill == 0, f"{n} spills {spill} VGPRs"
+    budget = {"IffLi16ELi0ELb1ELb0E": 80, "IddLi16ELi0ELb0ELb0E": 168, "IddLi16ELi0ELb1ELb0E": 168}
+    for key, limit in budget.items():
+        hit = [(n, r) for n, r in staged.items() if key in n]
+        assert hit, f"instantiation {key} not found"
+        for n, (v, _) in hit:
+            assert v <= limit, f"{n}: {v} VGPRs > {limit} (fewer waves per SIMD)"
+    mfma = [(n, r) for n, r in regs.items() if "grad_staged_mfma" in n]
+    assert mfma and all(s == 0 for _, (_, s) in mfma), mfma
