@@ -227,6 +227,102 @@ grad_dense_bundle(const Segment* __restrict__ segs, const Task* __restrict__ tas
   }
 }
 
+// ----- Replica bundles in ONE wave: each row is loaded once, into registers, and every replica
+// computes its own message from there. -----
+// Same bundle table as grad_dense_bundle (R task slots reading the same rows); one wave per bundle.
+// The wave double-buffers whole rows in VGPRs (the next row's loads are in flight while the current
+// one is computed), so there is no LDS staging and no barrier.  Per row and per replica: its own
+// dot product against beta (every replica's chain starts from an opaque zero, so the compiler
+// cannot merge the R identical chains: each logical worker does its own arithmetic, as on its own
+// machine in the reference), its own residual with its own coefficient and its own gradient
+// accumulation; R slab rows are written at the end.
+template <typename T, typename A, int CPL, int LOSS, int R>
+__global__ void __launch_bounds__(256)
+grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ tasks, int nbundles,
+                 const A* __restrict__ beta, A* __restrict__ slab, int ld) {
+  constexpr int VN = Vec16<T>::N;
+  constexpr int NV = CPL / VN;
+  using Rw = typename Vec16<T>::raw;
+  const int lane = threadIdx.x & 63;
+  const int bundle = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (bundle >= nbundles) return;
+  const Task lead = tasks[bundle * R];
+  const Segment ls = segs[lead.seg];
+  const T* __restrict__ X = static_cast<const T*>(ls.X);
+  const A* __restrict__ Y = static_cast<const A*>(ls.y);
+  A coef[R];
+  bool act[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const Task tq = tasks[bundle * R + q];
+    act[q] = tq.seg >= 0;
+    coef[q] = act[q] ? static_cast<A>(segs[tq.seg].coef) : A(0);
+  }
+  A b[NV][VN], g[R][NV][VN];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c0 = (j * kWave + lane) * VN;
+#pragma unroll
+    for (int v = 0; v < VN; ++v) {
+      b[j][v] = c0 < ld ? beta[c0 + v] : A(0);
+#pragma unroll
+      for (int q = 0; q < R; ++q) g[q][j][v] = A(0);
+    }
+  }
+  const int rowbytes = ld * static_cast<int>(sizeof(T));
+  auto load = [&](Rw (&x)[NV], int r) {
+    const auto rs = make_rsrc(X + static_cast<long long>(r) * ld, rowbytes);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) x[j] = buf_load16<Rw>(rs, (j * kWave + lane) * VN * static_cast<int>(sizeof(T)));
+  };
+  auto step = [&](const Rw (&x)[NV], int r) {
+    const A y = Y[r];
+    A z[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      z[q] = A(0);
+      asm volatile("" : "+v"(z[q]));  // opaque start: R separate dot products, not one shared
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v)
+#pragma unroll
+        for (int q = 0; q < R; ++q) z[q] = fma(Vec16<T>::template elem<A>(x[j], v), b[j][v], z[q]);
+    A rr[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) rr[q] = act[q] ? residual<LOSS, A>(wave_allreduce_sum(z[q]), y, coef[q]) : A(0);
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int v = 0; v < VN; ++v)
+#pragma unroll
+        for (int q = 0; q < R; ++q) g[q][j][v] = fma(rr[q], Vec16<T>::template elem<A>(x[j], v), g[q][j][v]);
+  };
+  Rw xa[NV], xb[NV];
+  const int r0 = lead.row_begin, r1 = lead.row_end;
+  if (r0 < r1) load(xa, r0);
+  for (int r = r0; r < r1; r += 2) {  // two rows per trip: the buffers swap roles without copies
+    if (r + 1 < r1) load(xb, r + 1);
+    step(xa, r);
+    if (r + 1 >= r1) break;
+    if (r + 2 < r1) load(xa, r + 2);
+    step(xb, r + 1);
+  }
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    if (!act[q]) continue;
+    A* out = slab + static_cast<long long>(tasks[bundle * R + q].slab) * ld;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c0 = (j * kWave + lane) * VN;
+#pragma unroll
+      for (int v = 0; v < VN; ++v)
+        if (c0 + v < ld) out[c0 + v] = g[q][j][v];
+    }
+  }
+}
+
 // ----- Replica bundles staged through LDS: one HBM read per row, one wave per replica. -----
 // Same task table as grad_dense_bundle (R slots per workgroup, all reading the same rows of one
 // partition).  The workgroup streams its row range through an NS-stage LDS ring with
@@ -986,7 +1082,10 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
   // one row per wave step / two rows sharing one reduction and residual evaluation)
   const bool staged_pair = variant > 30 && variant <= 38;
   const int staged_r = variant > 20 && variant <= 28 ? variant - 20 : staged_pair ? variant - 30 : 0;
-  const int bundle_r = variant > 10 && variant <= 18 ? variant - 10 : staged_r;
+  // variant 60 + R (R = 1..3, fp64/fp32, d <= 1024): one wave per bundle computing all R replicas
+  // (grad_dense_multi)
+  const int multi_r = variant > 60 && variant <= 63 ? variant - 60 : 0;
+  const int bundle_r = variant > 10 && variant <= 18 ? variant - 10 : staged_r ? staged_r : multi_r;
   if (bundle_r && ntasks % bundle_r != 0) return hipErrorInvalidValue;
   StagedGeom sg{};
   if (staged_r && !staged_geometry(staged_r, ld * static_cast<int>(sizeof(T)), 64ull * cpl * sizeof(A), &sg, want_wpr))
@@ -1013,6 +1112,24 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
                            sg.nstage, sg.wpr, nb_, grid_ < nb_ ? ticket : nullptr,        \
                            stage_rotate());                                               \
         return hipGetLastError();                                                         \
+      }                                                                                   \
+      if (multi_r) {                                                                      \
+        if constexpr (C <= 16 && !std::is_same<T, bf16_t>::value) {                       \
+          const int nb_ = ntasks / multi_r;                                               \
+          const dim3 mg((nb_ + 3) / 4), mb(256);                                          \
+          if (multi_r == 1)                                                               \
+            hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, 1>), mg, mb, 0, st, segs, \
+                               tasks, nb_, beta, slab, ld);                               \
+          else if (multi_r == 2)                                                          \
+            hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, 2>), mg, mb, 0, st, segs, \
+                               tasks, nb_, beta, slab, ld);                               \
+          else                                                                            \
+            hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, 3>), mg, mb, 0, st, segs, \
+                               tasks, nb_, beta, slab, ld);                               \
+          return hipGetLastError();                                                       \
+        } else {                                                                          \
+          return hipErrorInvalidValue;                                                    \
+        }                                                                                 \
       }                                                                                   \
       if (bundle_r) {                                                                     \
         hipLaunchKernelGGL((grad_dense_bundle<T, A, C, LOSS>), dim3(ntasks / bundle_r),   \

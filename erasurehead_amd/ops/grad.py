@@ -15,6 +15,7 @@ native kernels are mandatory (:func:`erasurehead_amd._ext.native` raises if abse
 """
 from __future__ import annotations
 
+import collections
 import os
 import struct
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -33,6 +34,15 @@ REPLICA_TASKS = 4096
 MAX_BUNDLE = 8  # replica task slots (waves) per workgroup of grad_dense_bundle / _staged
 STAGED_ROWS = 512  # rows per bundle task of grad_dense_staged (measured: 512 > 256, 1024; 2048 leaves CUs idle)
 SHARD_STAGED_ROWS = 128  # rows per bundle task when a rank holds < SHARD_ROWS distinct rows (multi-GPU shards)
+
+
+def multi_bundle_rows(distinct_rows: int) -> int:
+    """Rows per one-wave bundle of grad_dense_multi (2 waves fit per SIMD at 244 VGPRs): about 2000
+    bundles, 1300 at the one-GPU headline, in multiples of 64 rows (tools/sweep_multi_rows.sh,
+    profiles/r3_multi: N=1 768 rows 1.330 ms vs 512 1.36 / 1024 1.54; N=2 256-384 rows 0.71;
+    N=4 128 rows 0.373 vs 192 0.42; N=8 64 rows 0.206 vs 32-48 0.25)."""
+    waves = 1300 if distinct_rows >= 750_000 else 1953
+    return max(64, 64 * int(round(distinct_rows / waves / 64)))
 SHARD_ROWS = 800_000
 MIN_ROWS_PER_TASK = 32
 SLAB_SPLITS = 16  # csrc/kernels/grad_dense.hip kSplits
@@ -145,7 +155,18 @@ class DenseGradPlan:
         # residual evaluation; the default for fp32 and sharded ranks, see below).
         staged_env = os.environ.get("ERASUREHEAD_STAGED", "")
         staged_ok = shared and self.cpl is not None and self.cpl <= MAX_CPL
-        self.staged = staged_ok and (staged_env in ("1", "pair") or (staged_env == "" and prec.code in (0, 1)))
+        # One-wave bundles (grad_dense_multi, the fp64 default): one wave computes every replica of
+        # its bundle from rows double-buffered in registers, with no LDS staging and no barrier.
+        # R <= 3 replicas, d <= 1024.  Measured against the LDS-staged bundles, fp64
+        # (profiles/r3_multi): one-GPU headline 1.33 vs 1.45 ms, 2/4/8-GPU rank shapes
+        # 0.71 / 0.37 / 0.21 vs 0.78 / 0.41-0.43 / 0.21-0.23 ms.  fp32 stays on the staged pair
+        # bundles (0.749 vs 0.739 ms).  ERASUREHEAD_STAGED=multi selects it for fp32 too.
+        max_rep = max(collections.Counter(p for m in self.messages for p, _ in m).values(), default=0)
+        multi_ok = staged_ok and self.cpl <= 16 and max_rep <= 3
+        self.multi = multi_ok and ((staged_env == "multi" and prec.code in (0, 1))
+                                   or (staged_env == "" and prec.code == 0))
+        self.staged = staged_ok and not self.multi and (
+            staged_env in ("1", "pair") or (staged_env == "" and prec.code in (0, 1)))
         # two rows per step sharing one reduction: the fp32 default (0.790 vs 0.862 ms at the
         # headline, profiles/r2_fp32) and the default on sharded ranks of a multi-GPU run, where it
         # also wins for fp64 with one wave per replica (N=8 rank 0.213 vs 0.238 ms, N=4 0.407 vs
@@ -170,7 +191,9 @@ class DenseGradPlan:
             staged_rows = 256
             while staged_rows < 2048 and staged_rows * 512 < distinct_rows:
                 staged_rows *= 2
-        default_rows = str(staged_rows) if (self.staged or self.mfma) else "0"
+        if self.multi:
+            staged_rows = multi_bundle_rows(distinct_rows)
+        default_rows = str(staged_rows) if (self.staged or self.mfma or self.multi) else "0"
         self.bundle_rows = int(os.environ.get("ERASUREHEAD_BUNDLE_ROWS", default_rows)) if (
             shared and self.cpl is not None and self.cpl <= MAX_CPL) else 0
         if self.bundle_rows:
@@ -235,7 +258,10 @@ class DenseGradPlan:
             table += [tasks[i] for i in g] + [pad] * (R - len(g))
         if self.mfma and R > 16:
             raise ValueError("MFMA bundles hold at most 16 replicas")
-        self.variant = (40 if self.mfma else 30 if self.staged_pair else 20 if self.staged else 10) + R
+        if self.multi and R > 3:
+            raise ValueError("one-wave bundles (ERASUREHEAD_STAGED=multi) hold at most 3 replicas")
+        self.variant = (40 if self.mfma else 60 if self.multi else 30 if self.staged_pair else 20 if self.staged
+                        else 10) + R
         if self.staged and self.staged_wpr:
             self.variant += 100 * self.staged_wpr  # csrc: variant / 100 % 10 = waves per replica
         # persistent staged workgroups (csrc: variant >= 1000): as many workgroups as fit, each taking

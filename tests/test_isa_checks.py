@@ -101,5 +101,11 @@ def test_default_staged_kernels_keep_their_occupancy(tmp_path):
         assert hit, f"instantiation {key} not found"
         for n, (v, _) in hit:
             assert v <= limit, f"{n}: {v} VGPRs > {limit} (fewer waves per SIMD)"
+    # one-wave bundles (the fp64 default): 3 replicas' accumulators + two row buffers must stay
+    # within 256 VGPRs (2 waves per SIMD) without spilling
+    multi = {n: r for n, r in regs.items() if "grad_dense_multi" in n}
+    assert any("IddLi16ELi0ELi3E" in n for n in multi), "fp64 3-replica one-wave bundle not found"
+    for n, (v, spill) in multi.items():
+        assert spill == 0 and v <= 256, f"{n}: {v} VGPRs, {spill} spilled"
     mfma = [(n, r) for n, r in regs.items() if "grad_staged_mfma" in n]
     assert mfma and all(s == 0 for _, (_, s) in mfma), mfma

@@ -253,8 +253,8 @@ def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native,
 
 @pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
 def test_dense_grad_staged_is_the_replica_default(prec_name, native, monkeypatch):
-    """Co-located replicas default to the LDS-staged bundles for fp64/fp32 (interleaved dispatch
-    for bf16), and the staged messages match message-major order to rounding."""
+    """Co-located replicas in bundles of more than 3 default to the LDS-staged bundles for fp64/fp32
+    (MFMA for bf16), and the staged messages match message-major order to rounding."""
     monkeypatch.delenv("ERASUREHEAD_STAGED", raising=False)
     monkeypatch.delenv("ERASUREHEAD_BUNDLE_ROWS", raising=False)
     prec = get_precision(prec_name)
@@ -278,13 +278,40 @@ def test_dense_grad_staged_is_the_replica_default(prec_name, native, monkeypatch
     torch.testing.assert_close(Ga, Gb, rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
+def test_dense_grad_one_wave_bundles_are_the_fp64_default(prec_name, native, monkeypatch):
+    """Bundles of at most 3 replicas default to grad_dense_multi for fp64 (bundle length from
+    multi_bundle_rows), to the staged pair bundles for fp32 and to MFMA for bf16; the fp64 messages
+    match message-major order to rounding."""
+    from erasurehead_amd.ops.grad import multi_bundle_rows
+
+    monkeypatch.delenv("ERASUREHEAD_STAGED", raising=False)
+    monkeypatch.delenv("ERASUREHEAD_BUNDLE_ROWS", raising=False)
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(13)
+    parts, _ = _parts(rng, [3000, 2000, 1000], 1000, prec)
+    msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(2, -1.0)]] * 2
+    a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
+    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, interleave=False)
+    assert a.multi == (prec_name == "fp64") and a.staged == (prec_name == "fp32") and a.mfma == (prec_name == "bf16")
+    if a.multi:
+        assert a.variant == 63 and a.bundle_rows == multi_bundle_rows(6000)
+    beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
+    Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
+    a.native_launcher().launch(beta, Ga)
+    b.run(beta, Gb)
+    torch.cuda.synchronize()
+    tol = 1e-12 if prec_name == "fp64" else 1e-4
+    torch.testing.assert_close(Ga, Gb, rtol=tol, atol=tol)
+
+
 @pytest.mark.parametrize("prec_name", ["fp64", "fp32"])
 def test_dense_grad_staged_persistent_grid_is_bitwise_identical(prec_name, native, monkeypatch):
     """Persistent staged workgroups (ERASUREHEAD_PERSISTENT=1: as many workgroups as fit, bundles handed
     out by an atomic ticket) compute every bundle exactly as one-bundle-per-workgroup does, launch after
     launch (the ticket resets itself): bitwise-equal messages, with far more bundles than slots."""
     monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", "16")
-    monkeypatch.delenv("ERASUREHEAD_STAGED", raising=False)
+    monkeypatch.setenv("ERASUREHEAD_STAGED", "1")  # the LDS-staged bundles (fp64 defaults to one-wave bundles)
     prec = get_precision(prec_name)
     rng = np.random.RandomState(21)
     parts, _ = _parts(rng, [20000, 20000, 20000], 1000, prec)
@@ -352,6 +379,34 @@ def test_dense_grad_replica_bundle_kernel(monkeypatch, native, staged, rows, d, 
     for s, m in enumerate(msgs):
         ref = sum(logistic_grad(host[p][0], host[p][1], bh, c) for p, c in m)
         np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=tol * 1e-2)
+
+
+@pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
+@pytest.mark.parametrize("rows,d,prec_name", [("64", 1000, "fp64"), ("37", 1000, "fp64"), ("256", 250, "fp64"),
+                                              ("64", 1000, "fp32"), ("33", 130, "fp32")])
+def test_dense_grad_one_wave_bundles(monkeypatch, native, rows, d, prec_name, loss):
+    """grad_dense_multi (ERASUREHEAD_STAGED=multi): one wave computes every replica of its bundle
+    from rows double-buffered in registers, each replica with its own dot product, residual and
+    gradient.  Bundles of 3 replicas, of 2 padded to 3, and partial / odd-length bundles (the
+    two-rows-per-trip loop ends on either buffer) against the fp64 oracle."""
+    monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", rows)
+    monkeypatch.setenv("ERASUREHEAD_STAGED", "multi")
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(5)
+    parts, host = _parts(rng, [700, 501, 300], d, prec)
+    msgs = [[(0, 1.0), (1, 1.0)]] * 2 + [[(0, -0.5), (1, 2.0)]] + [[(2, 1.0)], [(2, -3.0)]]
+    plan = DenseGradPlan(msgs, parts, prec, loss, d)
+    assert plan.multi and plan.variant == 63 and plan.bundle_rows == int(rows)
+    beta = torch.randn(plan.ld, dtype=prec.acc, device=DEV) * 0.05
+    G = plan.out_buffer()[0]
+    plan.native_launcher().launch(beta, G)
+    torch.cuda.synchronize()
+    bh = beta[:d].double().cpu().numpy()
+    f = logistic_grad if loss == LOGISTIC else least_squares_grad
+    tol = 1e-10 if prec_name == "fp64" else 2e-4
+    for s, m in enumerate(msgs):
+        ref = sum(f(host[p][0], host[p][1], bh, c) for p, c in m)
+        np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=tol * 1e-2 * max(1.0, np.abs(ref).max()))
 
 
 @pytest.mark.parametrize("shape", [(20000, 15509, 55), (17290, 27654, 19), (6000, 241915, 45)])
