@@ -236,7 +236,12 @@ grad_dense_bundle(const Segment* __restrict__ segs, const Task* __restrict__ tas
 // cannot merge the R identical chains: each logical worker does its own arithmetic, as on its own
 // machine in the reference), its own residual with its own coefficient and its own gradient
 // accumulation; R slab rows are written at the end.
-template <typename T, typename A, int CPL, int LOSS, int R>
+//
+// FOLD: the plan lays the bundle table out in workgroups of 4 bundles of one partition (so the same
+// replica slot q is the same message in all four; pad bundles fill a workgroup at a partition's
+// end).  The four waves fold their accumulators through LDS in a fixed order and wave 0 writes
+// one slab row per replica for the workgroup: a quarter of the slab rows for the reduction to read.
+template <typename T, typename A, int CPL, int LOSS, int R, bool FOLD>
 __global__ void __launch_bounds__(256)
 grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ tasks, int nbundles,
                  const A* __restrict__ beta, A* __restrict__ slab, int ld) {
@@ -244,10 +249,12 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
   constexpr int NV = CPL / VN;
   using Rw = typename Vec16<T>::raw;
   const int lane = threadIdx.x & 63;
-  const int bundle = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  if (bundle >= nbundles) return;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bundle = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + wv);
+  if (!FOLD && bundle >= nbundles) return;  // FOLD: every wave reaches the barrier (nbundles % 4 == 0)
   const Task lead = tasks[bundle * R];
-  const Segment ls = segs[lead.seg];
+  const bool live = lead.seg >= 0;  // FOLD pad bundles: no rows, zero accumulators
+  const Segment ls = segs[live ? lead.seg : 0];
   const T* __restrict__ X = static_cast<const T*>(ls.X);
   const A* __restrict__ Y = static_cast<const A*>(ls.y);
   A coef[R];
@@ -300,7 +307,7 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
         for (int q = 0; q < R; ++q) g[q][j][v] = fma(rr[q], Vec16<T>::template elem<A>(x[j], v), g[q][j][v]);
   };
   Rw xa[NV], xb[NV];
-  const int r0 = lead.row_begin, r1 = lead.row_end;
+  const int r0 = lead.row_begin, r1 = live ? lead.row_end : r0;
   if (r0 < r1) load(xa, r0);
   for (int r = r0; r < r1; r += 2) {  // two rows per trip: the buffers swap roles without copies
     if (r + 1 < r1) load(xb, r + 1);
@@ -308,6 +315,28 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
     if (r + 1 >= r1) break;
     if (r + 2 < r1) load(xa, r + 2);
     step(xb, r + 1);
+  }
+  if constexpr (FOLD) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char fold_raw[];
+    A* fb = reinterpret_cast<A*>(fold_raw);  // [3 waves][R][NV * VN][64 lanes]
+    if (wv > 0) {
+#pragma unroll
+      for (int q = 0; q < R; ++q)
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+#pragma unroll
+          for (int v = 0; v < VN; ++v) fb[((((wv - 1) * R + q) * NV + j) * VN + v) * kWave + lane] = g[q][j][v];
+    }
+    __syncthreads();
+    if (wv > 0) return;
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k)  // one wave's rows at a time: keeps the epilogue's registers low
+#pragma unroll
+      for (int q = 0; q < R; ++q)
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+#pragma unroll
+          for (int v = 0; v < VN; ++v) g[q][j][v] += fb[(((k * R + q) * NV + j) * VN + v) * kWave + lane];
   }
 #pragma unroll
   for (int q = 0; q < R; ++q) {
@@ -1058,6 +1087,25 @@ static int staged_slots(const void* kern, int block, size_t lds) {
   return cache[key] = cus * per_cu;
 }
 
+// grad_dense_multi launch; the folded form takes 3 waves' accumulators in dynamic LDS.
+template <typename T, typename A, int C, int LOSS, int R>
+static hipError_t launch_multi(bool fold, dim3 grid, dim3 block, hipStream_t st, const Segment* segs,
+                               const Task* tasks, int nb, const A* beta, A* slab, int ld) {
+  if (!fold) {
+    hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, R, false>), grid, block, 0, st, segs, tasks, nb, beta, slab, ld);
+    return hipGetLastError();
+  }
+  const size_t lds = 3ull * R * C * kWave * sizeof(A);
+  auto kern = grad_dense_multi<T, A, C, LOSS, R, true>;
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(kern, grid, block, lds, st, segs, tasks, nb, beta, slab, ld);
+  return hipGetLastError();
+}
+
 template <typename T, typename A, int LOSS>
 static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
                                    const A* beta, A* slab, int ld, hipStream_t st, int variant,
@@ -1084,7 +1132,9 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
   const int staged_r = variant > 20 && variant <= 28 ? variant - 20 : staged_pair ? variant - 30 : 0;
   // variant 60 + R (R = 1..3, fp64/fp32, d <= 1024): one wave per bundle computing all R replicas
   // (grad_dense_multi)
-  const int multi_r = variant > 60 && variant <= 63 ? variant - 60 : 0;
+  // variant 70 + R: the same with the workgroup fold (plan-built table in workgroups of 4 bundles)
+  const bool multi_fold = variant > 70 && variant <= 73;
+  const int multi_r = variant > 60 && variant <= 63 ? variant - 60 : multi_fold ? variant - 70 : 0;
   const int bundle_r = variant > 10 && variant <= 18 ? variant - 10 : staged_r ? staged_r : multi_r;
   if (bundle_r && ntasks % bundle_r != 0) return hipErrorInvalidValue;
   StagedGeom sg{};
@@ -1116,17 +1166,14 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
       if (multi_r) {                                                                      \
         if constexpr (C <= 16 && !std::is_same<T, bf16_t>::value) {                       \
           const int nb_ = ntasks / multi_r;                                               \
+          if (multi_fold && nb_ % 4) return hipErrorInvalidValue;                         \
           const dim3 mg((nb_ + 3) / 4), mb(256);                                          \
           if (multi_r == 1)                                                               \
-            hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, 1>), mg, mb, 0, st, segs, \
-                               tasks, nb_, beta, slab, ld);                               \
+            return launch_multi<T, A, C, LOSS, 1>(multi_fold, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
           else if (multi_r == 2)                                                          \
-            hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, 2>), mg, mb, 0, st, segs, \
-                               tasks, nb_, beta, slab, ld);                               \
+            return launch_multi<T, A, C, LOSS, 2>(multi_fold, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
           else                                                                            \
-            hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, 3>), mg, mb, 0, st, segs, \
-                               tasks, nb_, beta, slab, ld);                               \
-          return hipGetLastError();                                                       \
+            return launch_multi<T, A, C, LOSS, 3>(multi_fold, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
         } else {                                                                          \
           return hipErrorInvalidValue;                                                    \
         }                                                                                 \

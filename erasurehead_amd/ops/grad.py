@@ -36,12 +36,14 @@ STAGED_ROWS = 512  # rows per bundle task of grad_dense_staged (measured: 512 > 
 SHARD_STAGED_ROWS = 128  # rows per bundle task when a rank holds < SHARD_ROWS distinct rows (multi-GPU shards)
 
 
-def multi_bundle_rows(distinct_rows: int) -> int:
-    """Rows per one-wave bundle of grad_dense_multi (2 waves fit per SIMD at 244 VGPRs): about 2000
-    bundles, 1300 at the one-GPU headline, in multiples of 64 rows (tools/sweep_multi_rows.sh,
-    profiles/r3_multi: N=1 768 rows 1.330 ms vs 512 1.36 / 1024 1.54; N=2 256-384 rows 0.71;
-    N=4 128 rows 0.373 vs 192 0.42; N=8 64 rows 0.206 vs 32-48 0.25)."""
-    waves = 1300 if distinct_rows >= 750_000 else 1953
+def multi_bundle_rows(distinct_rows: int, fp32: bool = False) -> int:
+    """Rows per one-wave bundle of grad_dense_multi, in multiples of 64 (tools/sweep_multi_rows.sh,
+    profiles/r3_multi).  fp64 (244 VGPRs, 2 waves per SIMD): about 2000 bundles, 1300 at the
+    one-GPU headline (N=1 768 rows 1.330 ms vs 512 1.36 / 640 1.37 / 1024 1.54; N=2 256 rows 0.708;
+    N=4 128 rows 0.370 vs 96 0.45 / 160 0.40; N=8 64 rows 0.206 vs 48 0.25 / 80 0.22).  fp32
+    (155 VGPRs, 3 waves per SIMD): about 2600 bundles, just under the 3072 wave slots (N=1 384
+    rows 0.692 ms; 320 rows = 3125 bundles needs a second pass: 0.95)."""
+    waves = 2600 if fp32 else 1300 if distinct_rows >= 750_000 else 1953
     return max(64, 64 * int(round(distinct_rows / waves / 64)))
 SHARD_ROWS = 800_000
 MIN_ROWS_PER_TASK = 32
@@ -158,20 +160,23 @@ class DenseGradPlan:
         # One-wave bundles (grad_dense_multi, the fp64 default): one wave computes every replica of
         # its bundle from rows double-buffered in registers, with no LDS staging and no barrier.
         # R <= 3 replicas, d <= 1024.  Measured against the LDS-staged bundles, fp64
-        # (profiles/r3_multi): one-GPU headline 1.33 vs 1.45 ms, 2/4/8-GPU rank shapes
-        # 0.71 / 0.37 / 0.21 vs 0.78 / 0.41-0.43 / 0.21-0.23 ms.  fp32 stays on the staged pair
-        # bundles (0.749 vs 0.739 ms).  ERASUREHEAD_STAGED=multi selects it for fp32 too.
+        # (profiles/r3_multi, r3_fold; with the workgroup fold): one-GPU headline 1.33 vs 1.45 ms,
+        # 2/4/8-GPU rank shapes 0.70 / 0.36 / 0.195 vs 0.78 / 0.41-0.43 / 0.21-0.23 ms.  fp32: the one-GPU headline
+        # (0.692 vs 0.740 ms); sharded fp32 ranks stay on the staged pair bundles (N=8 0.115-0.122
+        # vs 0.129 ms).  ERASUREHEAD_STAGED=multi forces it for fp32.
         max_rep = max(collections.Counter(p for m in self.messages for p, _ in m).values(), default=0)
         multi_ok = staged_ok and self.cpl <= 16 and max_rep <= 3
-        self.multi = multi_ok and ((staged_env == "multi" and prec.code in (0, 1))
-                                   or (staged_env == "" and prec.code == 0))
+        distinct_rows = sum(partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
+        # default only for bundles of 3 (AGC / cyclic with s = 2): with 2 replicas (FRC s = 1) the
+        # staged bundles with two waves per replica stay ahead (1.36 vs 1.40 ms, profiles/r3_fold)
+        self.multi = multi_ok and ((staged_env == "multi" and prec.code in (0, 1)) or (
+            staged_env == "" and max_rep == 3 and (prec.code == 0 or (prec.code == 1 and distinct_rows >= 750_000))))
         self.staged = staged_ok and not self.multi and (
             staged_env in ("1", "pair") or (staged_env == "" and prec.code in (0, 1)))
         # two rows per step sharing one reduction: the fp32 default (0.790 vs 0.862 ms at the
         # headline, profiles/r2_fp32) and the default on sharded ranks of a multi-GPU run, where it
         # also wins for fp64 with one wave per replica (N=8 rank 0.213 vs 0.238 ms, N=4 0.407 vs
         # 0.429, profiles/r2_rank_sweep); slower for the one-GPU fp64 headline
-        distinct_rows = sum(partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
         sharded = distinct_rows < SHARD_ROWS
         self.staged_pair = self.staged and (staged_env == "pair" or (staged_env == "" and (prec.code == 1 or sharded)))
         self.staged_wpr = 1 if (self.staged and sharded and staged_env == "") else 0  # 0: kernel default
@@ -192,7 +197,7 @@ class DenseGradPlan:
             while staged_rows < 2048 and staged_rows * 512 < distinct_rows:
                 staged_rows *= 2
         if self.multi:
-            staged_rows = multi_bundle_rows(distinct_rows)
+            staged_rows = multi_bundle_rows(distinct_rows, fp32=prec.code == 1)
         default_rows = str(staged_rows) if (self.staged or self.mfma or self.multi) else "0"
         self.bundle_rows = int(os.environ.get("ERASUREHEAD_BUNDLE_ROWS", default_rows)) if (
             shared and self.cpl is not None and self.cpl <= MAX_CPL) else 0
@@ -220,7 +225,9 @@ class DenseGradPlan:
                 seg_id += 1
             slot_begin.append(len(tasks))
         if self.bundle_rows:
-            tasks = self._bundle_table(tasks, keys)
+            tasks, folded_begin = self._bundle_table(tasks, keys)
+            if folded_begin is not None:  # one slab row per (workgroup, replica): see _fold_table
+                slot_begin = folded_begin
         elif self.interleave and self.cpl is not None:
             tasks = [tasks[i] for i in replica_dispatch_order(keys)]
         dev = self.device
@@ -260,8 +267,9 @@ class DenseGradPlan:
             raise ValueError("MFMA bundles hold at most 16 replicas")
         if self.multi and R > 3:
             raise ValueError("one-wave bundles (ERASUREHEAD_STAGED=multi) hold at most 3 replicas")
-        self.variant = (40 if self.mfma else 60 if self.multi else 30 if self.staged_pair else 20 if self.staged
-                        else 10) + R
+        self.fold = self.multi and os.environ.get("ERASUREHEAD_MULTI_FOLD", "1") != "0"
+        self.variant = (40 if self.mfma else (70 if self.fold else 60) if self.multi else 30 if self.staged_pair
+                        else 20 if self.staged else 10) + R
         if self.staged and self.staged_wpr:
             self.variant += 100 * self.staged_wpr  # csrc: variant / 100 % 10 = waves per replica
         # persistent staged workgroups (csrc: variant >= 1000): as many workgroups as fit, each taking
@@ -269,7 +277,44 @@ class DenseGradPlan:
         self.persistent = bool(self.staged and os.environ.get("ERASUREHEAD_PERSISTENT", "0") == "1")
         if self.persistent:
             self.variant += 1000
-        return table
+        if self.fold:
+            return self._fold_table(groups, tasks, keys, R, pad)
+        return table, None
+
+    def _fold_table(self, groups, tasks, keys, R: int, pad):
+        """Bundle table of the folded one-wave kernel (variant 70 + R): workgroups of 4 bundles of one
+        partition, padded at a partition's end, so replica slot q is the same message in all four.
+        Wave 0 writes one slab row per (workgroup, replica), numbered message by message; returns
+        the table and the per-message slab row ranges that replace the message-major ones."""
+        aligned: List[Optional[List[int]]] = []
+        cur = None
+        for g in groups:
+            p = keys[g[0]][0]
+            if p != cur and len(aligned) % 4:
+                aligned += [None] * (4 - len(aligned) % 4)
+            cur = p
+            aligned.append(g)
+        if len(aligned) % 4:
+            aligned += [None] * (4 - len(aligned) % 4)
+        per_slot: Dict[int, List[Tuple[int, int]]] = collections.defaultdict(list)
+        for w in range(len(aligned) // 4):
+            for q, ti in enumerate(aligned[4 * w]):  # a workgroup starts with a real bundle
+                per_slot[tasks[ti][0]].append((w, q))
+        slab_of: Dict[Tuple[int, int], int] = {}
+        slot_begin = [0]
+        for slot in range(self.nslots):
+            for wq in per_slot[slot]:
+                slab_of[wq] = len(slab_of)
+            slot_begin.append(len(slab_of))
+        table = []
+        for b, g in enumerate(aligned):
+            for q in range(R):
+                if g is None or q >= len(g):
+                    table.append(pad)
+                    continue
+                t = tasks[g[q]]
+                table.append((t[0], t[1], t[2], t[3], slab_of[(b // 4, q)] if b % 4 == 0 else t[4]))
+        return table, slot_begin
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:
         """Message buffer(s) [n, nslots, ld] in the accumulator dtype."""
