@@ -479,12 +479,36 @@ class Trainer:
                                   "messages": len(self.local_msgs),
                                   "partitions": len({p for m in self.local_msgs for p, _ in m.segments})}
         rep.update({k: round(float(v), 2) for k, v in self.rank_stats.items() if v is not None})
+        kern = self._kernel_label()
+        if kern:
+            rep["grad_kernel"] = kern
         if self.tx is not None and self.tx.fallback_reason:
             rep["transport_fallback"] = self.tx.fallback_reason
         if self.tx is not None and env.is_master and self.tx.pairs:
             rep["peer_access"] = [{k: x[k] for k in ("rank", "same_gpu", "master_to_rank", "rank_to_master")}
                                   for x in self.tx.pairs]
         return rep
+
+    def _kernel_label(self) -> Optional[str]:
+        """Which gradient kernel this rank's plan launches (bench.py per-rank breakdown)."""
+        plan = getattr(self, "plan", None)
+        inner = getattr(plan, "inner", plan)  # SharedPlan wraps a dense plan
+        if inner is None or not hasattr(inner, "variant"):
+            return type(plan).__name__ if plan is not None else None
+        if getattr(inner, "device", None) is not None and inner.device.type != "cuda":
+            return "torch reference path (CPU)"
+        if getattr(inner, "multi", False):
+            kind = "one-wave bundles" + (" (folded)" if getattr(inner, "fold", False) else "")
+        elif getattr(inner, "mfma", False):
+            kind = "MFMA bundles"
+        elif getattr(inner, "staged", False):
+            kind = "LDS-staged bundles" + (" (pair)" if getattr(inner, "staged_pair", False) else "")
+        elif getattr(inner, "bundle_rows", 0):
+            kind = "bundle kernel"
+        else:
+            kind = "fused"
+        rows = getattr(inner, "bundle_rows", 0)
+        return f"{kind}, variant {inner.variant}" + (f", {rows}-row bundles" if rows else "")
 
     def _master_loop_native(self, timed_start, log, start: int = 0) -> TrainResult:
         """Master rounds in csrc/runtime/engine.cpp (MasterPump); Python only keeps the books."""
