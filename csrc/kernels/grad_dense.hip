@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <string>
 #include <tuple>
 #include <type_traits>
 
@@ -241,7 +242,11 @@ grad_dense_bundle(const Segment* __restrict__ segs, const Task* __restrict__ tas
 // replica slot q is the same message in all four; pad bundles fill a workgroup at a partition's
 // end).  The four waves fold their accumulators through LDS in a fixed order and wave 0 writes
 // one slab row per replica for the workgroup: a quarter of the slab rows for the reduction to read.
-template <typename T, typename A, int CPL, int LOSS, int R, bool FOLD>
+// LANE_EPI: the reduce-scatter + one-lane-per-replica epilogue below; otherwise every replica's
+// dot product is all-reduced and its residual evaluated wave-uniformly (an inactive replica then
+// skips its share).  Measured: the lane form wins on the sharded multi-GPU rank shapes, the wave
+// form on the one-GPU headline (ops/grad.py picks per plan; docs/PERF_NOTES.md round 3).
+template <typename T, typename A, int CPL, int LOSS, int R, bool FOLD, bool LANE_EPI = false>
 __global__ void __launch_bounds__(256)
 grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ tasks, int nbundles,
                  const A* __restrict__ beta, A* __restrict__ slab, int ld) {
@@ -297,8 +302,29 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
 #pragma unroll
         for (int q = 0; q < R; ++q) z[q] = fma(Vec16<T>::template elem<A>(x[j], v), b[j][v], z[q]);
     A rr[R];
+    if constexpr (R == 1 || !LANE_EPI) {
 #pragma unroll
-    for (int q = 0; q < R; ++q) rr[q] = act[q] ? residual<LOSS, A>(wave_allreduce_sum(z[q]), y, coef[q]) : A(0);
+      for (int q = 0; q < R; ++q) rr[q] = act[q] ? residual<LOSS, A>(wave_allreduce_sum(z[q]), y, coef[q]) : A(0);
+    } else {
+      // Replicas 0 and 1 share one reduce-scatter (lanes 0-31 end with replica 0's dot product,
+      // lanes 32-63 with replica 1's), replica 2 is all-reduced.  Then one lane per replica
+      // evaluates that replica's loss epilogue (lane 0, lane 32, lane 1: one exp / divide for all
+      // of them instead of one wave-uniform evaluation each) and every lane reads the R residuals.
+      static_assert(R <= 3, "one-wave bundles hold at most 3 replicas");
+      const bool hi = lane >= 32;
+      A tq = wave_pair_reduce(z[0], z[1], hi), cq = hi ? coef[1] : coef[0];
+      constexpr int kLane[3] = {0, 32, 1};
+      if constexpr (R == 3) {
+        const A z2 = wave_allreduce_sum(z[2]);
+        if (lane == 1) {
+          tq = z2;
+          cq = coef[2];
+        }
+      }
+      const A rl = residual_branchfree<LOSS, A>(tq, y, cq);
+#pragma unroll
+      for (int q = 0; q < R; ++q) rr[q] = act[q] ? readlane_a(rl, kLane[q]) : A(0);
+    }
 #pragma unroll
     for (int j = 0; j < NV; ++j)
 #pragma unroll
@@ -1089,14 +1115,14 @@ static int staged_slots(const void* kern, int block, size_t lds) {
 
 // grad_dense_multi launch; the folded form takes 3 waves' accumulators in dynamic LDS.
 template <typename T, typename A, int C, int LOSS, int R>
-static hipError_t launch_multi(bool fold, dim3 grid, dim3 block, hipStream_t st, const Segment* segs,
+static hipError_t launch_multi(bool fold, bool lane_epi, dim3 grid, dim3 block, hipStream_t st, const Segment* segs,
                                const Task* tasks, int nb, const A* beta, A* slab, int ld) {
-  if (!fold) {
-    hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, R, false>), grid, block, 0, st, segs, tasks, nb, beta, slab, ld);
+  if (!fold) {  // (the lane epilogue comes with the fold only)
+    hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, R, false, false>), grid, block, 0, st, segs, tasks, nb, beta, slab, ld);
     return hipGetLastError();
   }
   const size_t lds = 3ull * R * C * kWave * sizeof(A);
-  auto kern = grad_dense_multi<T, A, C, LOSS, R, true>;
+  auto kern = lane_epi ? grad_dense_multi<T, A, C, LOSS, R, true, true> : grad_dense_multi<T, A, C, LOSS, R, true, false>;
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
@@ -1133,8 +1159,11 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
   // variant 60 + R (R = 1..3, fp64/fp32, d <= 1024): one wave per bundle computing all R replicas
   // (grad_dense_multi)
   // variant 70 + R: the same with the workgroup fold (plan-built table in workgroups of 4 bundles)
-  const bool multi_fold = variant > 70 && variant <= 73;
-  const int multi_r = variant > 60 && variant <= 63 ? variant - 60 : multi_fold ? variant - 70 : 0;
+  // variant 90 + R: folded, reduce-scatter + one-lane-per-replica epilogue (sharded ranks)
+  const bool multi_lane = variant > 90 && variant <= 93;
+  const bool multi_fold = (variant > 70 && variant <= 73) || multi_lane;
+  const int multi_r = variant > 60 && variant <= 63 ? variant - 60
+                      : multi_lane ? variant - 90 : multi_fold ? variant - 70 : 0;
   const int bundle_r = variant > 10 && variant <= 18 ? variant - 10 : staged_r ? staged_r : multi_r;
   if (bundle_r && ntasks % bundle_r != 0) return hipErrorInvalidValue;
   StagedGeom sg{};
@@ -1169,11 +1198,11 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
           if (multi_fold && nb_ % 4) return hipErrorInvalidValue;                         \
           const dim3 mg((nb_ + 3) / 4), mb(256);                                          \
           if (multi_r == 1)                                                               \
-            return launch_multi<T, A, C, LOSS, 1>(multi_fold, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
+            return launch_multi<T, A, C, LOSS, 1>(multi_fold, multi_lane, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
           else if (multi_r == 2)                                                          \
-            return launch_multi<T, A, C, LOSS, 2>(multi_fold, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
+            return launch_multi<T, A, C, LOSS, 2>(multi_fold, multi_lane, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
           else                                                                            \
-            return launch_multi<T, A, C, LOSS, 3>(multi_fold, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
+            return launch_multi<T, A, C, LOSS, 3>(multi_fold, multi_lane, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
         } else {                                                                          \
           return hipErrorInvalidValue;                                                    \
         }                                                                                 \

@@ -268,8 +268,16 @@ class DenseGradPlan:
         if self.multi and R > 3:
             raise ValueError("one-wave bundles (ERASUREHEAD_STAGED=multi) hold at most 3 replicas")
         self.fold = self.multi and os.environ.get("ERASUREHEAD_MULTI_FOLD", "1") != "0"
-        self.variant = (40 if self.mfma else (70 if self.fold else 60) if self.multi else 30 if self.staged_pair
-                        else 20 if self.staged else 10) + R
+        # epilogue of the folded one-wave kernel: replicas 0/1 reduce-scattered and one lane per
+        # replica evaluating its residual (csrc variant 90 + R) wins on sharded ranks (N=2/4/8
+        # 0.677-0.684 / 0.353-0.354 / 0.188-0.190 vs 0.689-0.699 / 0.365-0.368 / 0.194-0.197 ms);
+        # the wave-uniform one (70 + R) on the one-GPU headline (1.316-1.334 vs 1.40-1.43 ms),
+        # profiles/r3_epi.  ERASUREHEAD_MULTI_EPI=wave|lane overrides.
+        epi = os.environ.get("ERASUREHEAD_MULTI_EPI", "")
+        distinct = sum(self.partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
+        self.lane_epi = self.fold and (epi == "lane" or (epi == "" and distinct < 750_000))
+        self.variant = (40 if self.mfma else (90 if self.lane_epi else 70 if self.fold else 60) if self.multi
+                        else 30 if self.staged_pair else 20 if self.staged else 10) + R
         if self.staged and self.staged_wpr:
             self.variant += 100 * self.staged_wpr  # csrc: variant / 100 % 10 = waves per replica
         # persistent staged workgroups (csrc: variant >= 1000): as many workgroups as fit, each taking

@@ -295,7 +295,7 @@ def test_dense_grad_one_wave_bundles_are_the_fp64_default(prec_name, native, mon
     b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, interleave=False)
     assert a.multi == (prec_name == "fp64") and a.staged == (prec_name == "fp32") and a.mfma == (prec_name == "bf16")
     if a.multi:
-        assert a.variant == 73 and a.bundle_rows == multi_bundle_rows(6000)
+        assert a.variant == 93 and a.bundle_rows == multi_bundle_rows(6000)
     beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
     Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
     a.native_launcher().launch(beta, Ga)
@@ -381,26 +381,30 @@ def test_dense_grad_replica_bundle_kernel(monkeypatch, native, staged, rows, d, 
         np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=tol * 1e-2)
 
 
-@pytest.mark.parametrize("fold", [True, False])
+@pytest.mark.parametrize("form", ["fold-lane", "fold-wave", "unfolded"])
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
 @pytest.mark.parametrize("rows,d,prec_name", [("64", 1000, "fp64"), ("37", 1000, "fp64"), ("256", 250, "fp64"),
                                               ("64", 1000, "fp32"), ("33", 130, "fp32")])
-def test_dense_grad_one_wave_bundles(monkeypatch, native, rows, d, prec_name, loss, fold):
+def test_dense_grad_one_wave_bundles(monkeypatch, native, rows, d, prec_name, loss, form):
     """grad_dense_multi (ERASUREHEAD_STAGED=multi): one wave computes every replica of its bundle
     from rows double-buffered in registers, each replica with its own dot product, residual and
     gradient.  Bundles of 3 replicas, of 2 padded to 3, and partial / odd-length bundles (the
     two-rows-per-trip loop ends on either buffer) against the fp64 oracle; with the workgroup fold
     (4 bundles of one partition per workgroup, pad bundles at partition ends, one slab row per
-    workgroup and replica) and without."""
+    workgroup and replica) and both epilogues (replicas reduce-scattered with one lane per
+    replica's residual, or wave-uniform), and without the fold."""
     monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", rows)
     monkeypatch.setenv("ERASUREHEAD_STAGED", "multi")
+    fold = form != "unfolded"
     monkeypatch.setenv("ERASUREHEAD_MULTI_FOLD", "1" if fold else "0")
+    monkeypatch.setenv("ERASUREHEAD_MULTI_EPI", "wave" if form == "fold-wave" else "lane")
     prec = get_precision(prec_name)
     rng = np.random.RandomState(5)
     parts, host = _parts(rng, [700, 501, 300], d, prec)
     msgs = [[(0, 1.0), (1, 1.0)]] * 2 + [[(0, -0.5), (1, 2.0)]] + [[(2, 1.0)], [(2, -3.0)]]
     plan = DenseGradPlan(msgs, parts, prec, loss, d)
-    assert plan.multi and plan.variant == (73 if fold else 63) and plan.bundle_rows == int(rows)
+    want = {"fold-lane": 93, "fold-wave": 73, "unfolded": 63}[form]
+    assert plan.multi and plan.variant == want and plan.bundle_rows == int(rows)
     if fold:  # slab rows: one per (workgroup, replica), a contiguous range per message
         stb = plan.slot_task_begin.cpu().numpy()
         assert stb[0] == 0 and np.all(np.diff(stb) > 0) and stb[-1] <= plan.ntasks // 4
