@@ -197,12 +197,13 @@ def test_arrival_sets_replay_reference_delays(case, k):
         T = float(np.max(ready)) if tr.drain else float(ready[used[-1]])
         # the used SET is decided at the stop boundary: skip rounds where the last used and the
         # first unused worker are too close for wall-clock scheduling noise (a loaded CPU)
+        noise = 10e-3  # host wake-up jitter of a loaded CPU (pytest -n, a build running alongside)
         nxt = ready[order[len(used)]] if len(used) < W else np.inf
-        if nxt - ready[used[-1]] < 3e-3:
+        if nxt - ready[used[-1]] < noise:
             continue
         arrived = [w for (w, p, _) in res.arrivals[i]]
         assert sorted(arrived) == sorted(used), (i, arrived, used)
-        assert arrived[-1] in {w for w in used if ready[used[-1]] - ready[w] < 3e-3}, (i, arrived, used)
+        assert arrived[-1] in {w for w in used if ready[used[-1]] - ready[w] < noise}, (i, arrived, used)
         if sch.marks_unused:
             assert set(np.where(res.worker_timeset[i] == -1)[0]) == set(range(W)) - set(used)
 
