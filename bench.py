@@ -68,6 +68,8 @@ def parse(argv=None):
     ap.add_argument("--round-timeout", type=float, default=120.0, help="bounds any hang (a round takes ms)")
     ap.add_argument("--device-loop", default="auto", choices=["auto", "graph", "stream", "off"])
     ap.add_argument("--tie-break", default="permute", choices=["permute", "worker"])
+    ap.add_argument("--preflight", type=int, default=1000,
+                    help="N > 1: put -> flag round trips per worker/master pair before the timed rounds (0: off)")
     ap.add_argument("--share-partitions", action="store_true",
                     help="co-located workers stream each distinct partition once (not the headline)")
     return ap.parse_args(argv)
@@ -130,6 +132,8 @@ def main(argv=None) -> int:
     t_setup = time.perf_counter()
     trainer = Trainer(make_cfg(a.warmup + a.steps), env)
     setup_s = time.perf_counter() - t_setup
+    # the first multi-GPU run checks itself: put -> flag latency and payload checks per worker/master pair
+    preflight = trainer.preflight(a.preflight) if env.world > 1 and a.preflight > 0 else None
     res = trainer.run(timed_start=a.warmup)
     mine = res.timed_seconds if env.is_master else trainer.worker_timed_seconds
     timed = env.allreduce_max(mine)
@@ -182,6 +186,8 @@ def main(argv=None) -> int:
                           for r in range(env.world)},
             "shard": trainer.shard_mode,
         }
+        if preflight is not None:
+            out["peer_preflight"] = preflight
         if n_gpu_dev and env.world > n_gpu_dev:
             out["config"]["ranks_per_gpu"] = env.world / n_gpu_dev  # rehearsal: ranks time-share GPUs
         out["config"]["round_loop"] = {"graph": "device-driven, hipGraph", "stream": "device-driven",

@@ -46,7 +46,10 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
   __shared__ long long arr_t[2 * kArbMaxW];
   __shared__ const void* mptr[kMaxMsgs];
   __shared__ double mcoef[kMaxMsgs];
-  __shared__ int s_narr, s_nmsg, s_status;
+  __shared__ int mrow[kMaxMsgs];  // kind << 24 | row of every used buffer row
+  __shared__ unsigned long long vs[kMaxMsgs], scratch[16];
+  __shared__ int s_narr, s_nmsg, s_status, s_bad;
+  __shared__ unsigned long long s_bsum;
   const int tid = threadIdx.x;
   int* lg = a.log + static_cast<long long>(i) * kArbLogInts;
   long long* tl = a.tlog + static_cast<long long>(i) * kArbLogTicks;
@@ -60,10 +63,12 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
     s_ps[q] = a.probe_src[q];
   }
   for (int m = tid; m < 2 * a.W; m += blockDim.x) got_sh[m] = 0;
+  for (int m = tid; m < kMaxMsgs; m += blockDim.x) vs[m] = 0;
   if (tid == 0) {
     s_narr = 0;
     s_nmsg = 0;
     s_status = 0;
+    s_bad = 0;
   }
   __syncthreads();
 
@@ -162,6 +167,7 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
         if (s_nmsg < kMaxMsgs) {
           mptr[s_nmsg] = base;
           mcoef[s_nmsg] = c;
+          mrow[s_nmsg] = e;
         }
         ++s_nmsg;
       }
@@ -210,21 +216,36 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
   }
 
   // ---- 3. combine + update, beta(i+1) into beta_in and every worker inbox -------------------
+  // With tags on, the same loads also sum the checksum terms of every used mailbox row (one wave
+  // reduction per row, LDS adds) and of beta(i+1); the rows are compared with their tags below,
+  // before anything is released.  The column loop has a block-uniform trip count for that.
   const double decay = a.decay[i], gm = a.gm[i], l2 = a.l2[i], theta = a.theta[i];
+  const bool vfy = a.tags != nullptr;
   M* bin_next = static_cast<M*>(a.beta_in) + static_cast<long long>(i + 1) * a.ld;
-  for (int c = tid; c < a.ld; c += blockDim.x) {
+  unsigned long long bterm = 0;
+  for (int c0 = 0; c0 < a.ld; c0 += blockDim.x) {
+    const int c = c0 + tid;
+    const bool in = c < a.ld;
     M out = M(0);
-    if (c < a.d) {
-      double g = 0.0;
-      constexpr int kB = 16;  // independent loads first, then the fma chain in message order
-      for (int m0 = 0; m0 < s_nmsg; m0 += kB) {
-        double v[kB];
+    double g = 0.0;
+    constexpr int kB = 16;  // independent loads first, then the fma chain in message order
+    for (int m0 = 0; m0 < s_nmsg; m0 += kB) {
+      M v[kB];
 #pragma unroll
-        for (int q = 0; q < kB; ++q) v[q] = m0 + q < s_nmsg ? static_cast<double>(static_cast<const M*>(mptr[m0 + q])[c]) : 0.0;
+      for (int q = 0; q < kB; ++q) v[q] = (in && m0 + q < s_nmsg) ? static_cast<const M*>(mptr[m0 + q])[c] : M(0);
 #pragma unroll
-        for (int q = 0; q < kB; ++q)
-          if (m0 + q < s_nmsg) g = fma(mcoef[m0 + q], v[q], g);
+      for (int q = 0; q < kB; ++q)
+        if (m0 + q < s_nmsg) g = fma(mcoef[m0 + q], static_cast<double>(v[q]), g);
+      if (vfy) {
+#pragma unroll
+        for (int q = 0; q < kB; ++q) {
+          if (m0 + q >= s_nmsg || (mrow[m0 + q] >> 24) != 1) continue;  // block-uniform
+          const unsigned long long t = wave_sum_u64(in ? tag_term(elem_bits(v[q]), c) : 0ull);
+          if ((tid & 63) == 0 && t) atomicAdd(&vs[m0 + q], t);
+        }
       }
+    }
+    if (in && c < a.d) {
       const double b = a.beta[c];
       double nb;
       if (a.update_rule == 0) {
@@ -238,12 +259,43 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
       a.hist[static_cast<long long>(i) * a.ld + c] = nb;
       out = static_cast<M>(nb);
     }
-    if (i + 1 <= a.R) bin_next[c] = out;
-    for (int t = 0; t < a.ntarget && i + 1 < a.R; ++t)
-      reinterpret_cast<M*>(a.targets[2 * t])[static_cast<long long>(i + 1) * a.ld + c] = out;
+    if (in) {
+      if (i + 1 <= a.R) bin_next[c] = out;
+      for (int t = 0; t < a.ntarget && i + 1 < a.R; ++t)
+        reinterpret_cast<M*>(a.targets[2 * t])[static_cast<long long>(i + 1) * a.ld + c] = out;
+      bterm += tag_term(elem_bits(out), c);
+    }
+  }
+  if (vfy) {  // ---- 3b. the used mailbox rows against their senders' tags -------------------------
+    const unsigned long long bs = block_sum_u64(bterm, scratch);  // (barrier: every vs add is in)
+    if (tid == 0) s_bsum = bs;
+    for (int m = tid; m < s_nmsg; m += blockDim.x) {
+      if ((mrow[m] >> 24) != 1) continue;
+      const int row = mrow[m] & 0xffffff;
+      const MsgTag tg = a.tags[static_cast<long long>(slot) * a.r_rows + row];
+      const int want = a.row_rank[row];
+      if ((tg.round1 != static_cast<unsigned int>(i + 1) || tg.rank != static_cast<unsigned int>(want) ||
+           tg.sum != vs[m]) && atomicCAS(&s_bad, 0, 1) == 0) {
+        lg[2] = (slot << 16) | row;
+        lg[3] = want;
+        lg[4] = static_cast<int>(tg.round1);
+        lg[5] = static_cast<int>(tg.rank);
+        tl[4] = static_cast<long long>(tg.sum);
+        tl[5] = static_cast<long long>(vs[m]);
+        s_status = kArbIntegrity;
+      }
+    }
   }
   __syncthreads();
   if (tid == 0) tl[1] = wall_clock64();
+  if (s_status != 0) {  // a torn or stale message: beta(i+1) is not released
+    if (tid == 0) {
+      __hip_atomic_store(a.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lg[0] = s_status;
+      lg[1] = s_narr;
+    }
+    return;
+  }
 
   // ---- 4. drain: every worker rank's round-i message has landed ------------------------------
   if (a.drain && tid < 64) {
@@ -271,6 +323,10 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
   }
 
   // ---- 5. release beta(i+1): the inbox rows are visible before every worker's counter -------
+  if (vfy && i + 1 < a.R)
+    for (int t = tid; t < a.ntarget; t += blockDim.x)
+      reinterpret_cast<MsgTag*>(reinterpret_cast<char*>(a.targets[2 * t]) + a.inbox_tag_off)[i + 1] =
+          MsgTag{static_cast<unsigned int>(i + 2), 0u, s_bsum};
   __threadfence_system();
   __syncthreads();
   if (tid == 0) {

@@ -942,30 +942,58 @@ slab_reduce_final(const A* __restrict__ part, A* __restrict__ G, int ld) {
 // [slot][ld] layout as G), fences at system scope and counts itself done; the last block
 // resets the counter and release-stores the flag.  Saves the separate put_signal launch on
 // every worker round's critical path.  No early return: every thread reaches the barrier.
+// Tagged puts (put.tag != nullptr, integrity.h): every block also adds its columns' checksum
+// terms of its slot's row into the sender scratch put.csum[slot]; the last block turns the sums
+// into the receiver's tags before the flag.  put.abort set: the pump gave up, G is still
+// written (the local copy) but nothing is put or announced.
 template <typename A>
 __global__ void __launch_bounds__(256)
 slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, PutDesc put) {
+  __shared__ unsigned long long scratch[4];
+  __shared__ int s_last, s_live;
   const int slot = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (threadIdx.x == 0)  // one read, shared: every wave of the block takes the same branch
+    s_live = !(put.abort && __hip_atomic_load(put.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  __syncthreads();
+  const bool live = s_live;
+  unsigned long long term = 0;
   if (c < ld) {
     A s = A(0);
 #pragma unroll
     for (int k = 0; k < kSplits; ++k) s += part[(static_cast<long long>(slot) * kSplits + k) * ld + c];
     const long long o = static_cast<long long>(slot) * ld + c;
     G[o] = s;
-    static_cast<A*>(put.dst)[o] = s;
+    if (live) static_cast<A*>(put.dst)[o] = s;
+    term = tag_term(elem_bits(s), c);
+  }
+  if (!live) return;  // block-uniform
+  if (put.tag) {
+    const unsigned long long bs = block_sum_u64(term, scratch);
+    if (threadIdx.x == 0 && bs) atomicAdd(put.csum + slot, bs);
   }
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned int total = gridDim.x * gridDim.y;
     const unsigned int prev = __hip_atomic_fetch_add(put.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == total - 1) {
-      __hip_atomic_store(put.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence_system();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // see transport.hip: keep the flag behind the fence
-      __hip_atomic_store(put.flag, put.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    s_last = prev == total - 1;
+    if (s_last) __hip_atomic_store(put.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;  // block-uniform
+  if (put.tag) {
+    for (int r = threadIdx.x; r < static_cast<int>(gridDim.y); r += blockDim.x) {
+      const unsigned long long sum = atomicExch(put.csum + r, 0ull);
+      put.tag[r] = MsgTag{static_cast<unsigned int>(put.value), put.rank, sum};
     }
+    if (put.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(put.dst)[1] ^= 0x10;  // test hook
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // see transport.hip: keep the flag behind the fence
+    __hip_atomic_store(put.flag, put.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -974,6 +1002,7 @@ static hipError_t slab_reduce_launch(const A* slab, const int* stb, A* part, A* 
                                      hipStream_t st, const PutDesc* put = nullptr) {
   hipLaunchKernelGGL(slab_reduce_partial<A>, dim3(ceil_div(ld, kWave), nslots, kSplits), dim3(256), 0, st,
                      slab, stb, part, ld);
+  if (put && put->tag && (nslots > kMaxTagRows || !put->csum)) return hipErrorInvalidValue;
   if (put)
     hipLaunchKernelGGL(slab_reduce_final_put<A>, dim3(ceil_div(ld, 256), nslots), dim3(256), 0, st, part, G, ld, *put);
   else

@@ -1,0 +1,94 @@
+// Message integrity tags of the IPC mailbox transport (SURVEY §5.2 "per-slot generation
+// counters ... a debug mode that checksums beta per round", here always on).
+//
+// The reference relies on MPI's per-source ordering for the reuse of msgBuffers[j] and of the
+// one beta receive buffer (ref src/naive.py:66-79, :97-110).  Here a message is a put over xGMI
+// followed by a release-store of a round counter in host memory; a platform or protocol bug
+// that let the counter overtake the payload would silently decode stale or torn rows.  So every
+// tagged put also writes, per payload row, a 16-byte tag into the receiver's tag slots:
+//     { round + 1 (the counter value), sender rank, checksum of the row }
+// before the counter, and the receiver recomputes the checksum over the row it actually reads
+// (the master's combine / arbiter for worker messages, a verify kernel on the worker for beta).
+//
+// Checksum of a row of n elements of es bytes (4 or 8), element bits zero-extended to 64 bits:
+//     sum_j bits_j * (2 j + 1)  (mod 2^64)
+// Odd multipliers are invertible mod 2^64, so any single corrupted element changes it, an
+// element moved to another column changes it, and a stale row from an earlier round changes it
+// with overwhelming probability.  It is a plain sum of per-element terms: blocks and waves
+// reduce it in any order with integer adds (bitwise deterministic, no float atomics).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace eh {
+
+struct MsgTag {
+  unsigned int round1;      // round + 1: the counter value the put announces
+  unsigned int rank;        // sender rank
+  unsigned long long sum;   // checksum of the row
+};
+static_assert(sizeof(MsgTag) == 16, "MsgTag is 16 bytes");
+
+// First failed check of a pump, in host-mapped memory (written once, by one thread).
+struct IntegrityErr {
+  int flag;                 // 1 once filled in
+  int round;                // round whose message failed
+  int where;                // slot << 16 | mailbox row (worker messages), -1 for beta
+  int rank_want;            // sender the receiver expected
+  unsigned int round1_got;  // tag fields found
+  unsigned int rank_got;
+  unsigned long long sum_got;   // checksum in the tag
+  unsigned long long sum_calc;  // checksum of the payload as read
+};
+
+constexpr int kMaxTagRows = 64;  // rows of one tagged put descriptor (sender scratch / LDS sums)
+
+__host__ __device__ inline unsigned long long tag_term(unsigned long long bits, long long j) {
+  return bits * static_cast<unsigned long long>(2 * j + 1);
+}
+
+#if defined(__HIPCC__)
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+// Sum over the block of one u64 per thread (every thread must call it; result valid in thread 0).
+// scratch: >= blockDim.x / 64 entries of LDS.
+__device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v, unsigned long long* scratch) {
+  v = wave_sum_u64(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  unsigned long long s = 0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < static_cast<int>(blockDim.x >> 6); ++w) s += scratch[w];
+  __syncthreads();
+  return s;
+}
+
+// Element bits of a row (double / float payloads), zero-extended.
+__device__ __forceinline__ unsigned long long elem_bits(double x) {
+  return static_cast<unsigned long long>(__double_as_longlong(x));
+}
+__device__ __forceinline__ unsigned long long elem_bits(float x) { return static_cast<unsigned long long>(__float_as_uint(x)); }
+
+// Record the first failure (caller is a single thread).  Plain vector stores into host-mapped
+// memory, then a system-scope release of the flag so the host sees complete fields.
+__device__ inline void report_integrity(IntegrityErr* err, int round, int where, int rank_want, const MsgTag& got,
+                                        unsigned long long calc) {
+  if (!err || __hip_atomic_load(&err->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
+  err->round = round;
+  err->where = where;
+  err->rank_want = rank_want;
+  err->round1_got = got.round1;
+  err->rank_got = got.rank;
+  err->sum_got = got.sum;
+  err->sum_calc = calc;
+  __threadfence_system();
+  __hip_atomic_store(&err->flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#endif
+
+}  // namespace eh

@@ -7,6 +7,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "integrity.h"
+
 namespace eh {
 
 // ---- worker gradient (grad_dense.hip, grad_sparse.hip) -------------------------------
@@ -70,6 +72,17 @@ struct CombineArgs {
   const void* msg[kMaxMsgs];
   double coef[kMaxMsgs];
   int nmsg;
+  // Integrity check of mailbox rows (integrity.h), off when tags == nullptr: message m is checked
+  // against tags[tag_row[m]] (tag_row < 0: a local row, not checked) for counter value round1 and
+  // sender tag_rank[m].  vsum [kMaxMsgs] / vcount: zeroed device scratch (left zero); err: host-mapped.
+  const MsgTag* tags;
+  int tag_row[kMaxMsgs];
+  unsigned char tag_rank[kMaxMsgs];
+  unsigned int round1;
+  int slot;
+  unsigned long long* vsum;
+  unsigned int* vcount;
+  IntegrityErr* err;
 };
 // msg dtype / worker-beta dtype: 0 fp64, 1 fp32; rule 0 GD, 1 AGD
 hipError_t combine_update_launch(const CombineArgs& args, int msg_dtype, int w_dtype,
@@ -89,6 +102,19 @@ struct PutDesc {
   unsigned long long* flag;   // device-accessible address of the flag (host-registered shm)
   unsigned long long value;   // flag value announced once the payload is visible
   unsigned int* counter;      // per-descriptor block counter (device memory, zero between launches)
+  // Integrity tag (integrity.h), off when tag == nullptr: one MsgTag per payload row is written
+  // into the receiver's tag slots before the flag.  csum: per-row sender scratch [rows] (zero
+  // between launches); rows <= kMaxTagRows; es: element bytes (4 / 8); corrupt: test hook that
+  // flips one payload byte after the checksum (a torn put the receiver must catch).
+  MsgTag* tag;
+  unsigned long long* csum;
+  int rows;
+  int es;
+  unsigned int rank;
+  int corrupt;
+  // Abort word (host-mapped, nullptr = none): once non-zero, the put and its signal are skipped
+  // (a pump that gave up releases its queued stream waits without announcing stale rounds).
+  const int* abort;
 };
 struct PutArgs {
   PutDesc d[kMaxPuts];
@@ -96,5 +122,13 @@ struct PutArgs {
 };
 hipError_t put_signal_launch(const PutArgs& args, int blocks, hipStream_t st);
 hipError_t signal_launch(unsigned long long* flag, unsigned long long value, hipStream_t st);
+
+// Receiver-side check of the tagged rows of one put (integrity.h): rows [nrows][ld] of es-byte
+// elements against tags[nrows] for counter value round1 and sender `rank`; first failure -> err.
+hipError_t verify_rows_launch(const void* rows, const MsgTag* tags, int nrows, int ld, int es,
+                              unsigned int round1, unsigned int rank, IntegrityErr* err, int where,
+                              hipStream_t st);
+// Spin on the device for `ticks` wall_clock64 ticks (a physically late worker, --delay-mode worker).
+hipError_t spin_launch(long long ticks, hipStream_t st);
 
 }  // namespace eh

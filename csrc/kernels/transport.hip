@@ -13,33 +13,100 @@
 // last block of a descriptor resets the counter and release-stores the flag at system
 // scope.  So a receiver that observes flag >= value also observes the payload, without
 // relying on kernel-boundary cache semantics across devices.
+//
+// Integrity (integrity.h): a tagged descriptor also checksums every row it copies (LDS sums per
+// row, one global add per row and block into the sender's scratch) and the last block writes
+// one {round + 1, rank, checksum} tag per row into the receiver's tag slots before the flag.
 #include "common.h"
 #include "launchers.h"
 
 namespace eh {
 
+namespace {
+__device__ __forceinline__ bool aborted(const int* abort) {
+  return abort && __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
+// Terms of one 16-byte vector of a row (es-byte elements starting at element j0).
+__device__ __forceinline__ unsigned long long vec_terms(const uint4& v, int es, long long j0) {
+  if (es == 8) {
+    const unsigned long long a = (static_cast<unsigned long long>(v.y) << 32) | v.x;
+    const unsigned long long b = (static_cast<unsigned long long>(v.w) << 32) | v.z;
+    return tag_term(a, j0) + tag_term(b, j0 + 1);
+  }
+  return tag_term(v.x, j0) + tag_term(v.y, j0 + 1) + tag_term(v.z, j0 + 2) + tag_term(v.w, j0 + 3);
+}
+}  // namespace
+
 __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
+  __shared__ unsigned long long row_sum[kMaxTagRows];
+  __shared__ int s_last, s_abort;
   const int k = blockIdx.y;
   if (k >= args.n) return;
   const PutDesc& p = args.d[k];
+  if (threadIdx.x == 0) s_abort = aborted(p.abort);  // one read, shared by the block
+  __syncthreads();
+  if (s_abort) return;  // the pump gave up: nothing is put or announced
+  const bool tagged = p.tag != nullptr;
   const long long nvec = p.bytes / 16;
+  const long long row_vec = tagged ? nvec / p.rows : 1;  // 16-byte vectors per row
+  const int per_vec = 16 / (tagged ? p.es : 16);
+  if (tagged) {
+    for (int r = threadIdx.x; r < p.rows; r += blockDim.x) row_sum[r] = 0;
+    __syncthreads();
+  }
   const uint4* __restrict__ s = static_cast<const uint4*>(p.src);
   uint4* __restrict__ d = static_cast<uint4*>(p.dst);
-  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec;
-       i += static_cast<long long>(gridDim.x) * blockDim.x)
-    d[i] = s[i];
+  const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
+  // block-uniform trip count, so the wave reductions below run in uniform control flow
+  for (long long base = static_cast<long long>(blockIdx.x) * blockDim.x; base < nvec; base += stride) {
+    const long long i = base + threadIdx.x;
+    const bool act = i < nvec;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (act) {
+      v = s[i];
+      d[i] = v;
+    }
+    if (tagged) {
+      const long long row = act ? i / row_vec : 0;
+      const unsigned long long t = act ? vec_terms(v, p.es, (i - row * row_vec) * per_vec) : 0ull;
+      const int r0 = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
+      if (__ballot(act && row != r0) == 0) {  // the wave's vectors are all in one row
+        const unsigned long long ws = wave_sum_u64(t);
+        if ((threadIdx.x & 63) == 0 && ws) atomicAdd(&row_sum[r0], ws);
+      } else if (act) {
+        atomicAdd(&row_sum[row], t);
+      }
+    }
+  }
+  if (tagged) {
+    __syncthreads();
+    for (int r = threadIdx.x; r < p.rows; r += blockDim.x)
+      if (row_sum[r]) atomicAdd(p.csum + r, row_sum[r]);
+  }
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned int prev = __hip_atomic_fetch_add(p.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      __hip_atomic_store(p.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence_system();
-      // ROCm 7.2 / gfx950: after a returned atomic the compiler may drop the wait that follows
-      // the fence's write-back, letting the flag overtake it; keep the wait explicitly.
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(p.flag, p.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    s_last = prev == gridDim.x - 1;
+    if (s_last) __hip_atomic_store(p.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;  // block-uniform
+  if (tagged) {
+    for (int r = threadIdx.x; r < p.rows; r += blockDim.x) {
+      const unsigned long long sum = atomicExch(p.csum + r, 0ull);  // every block's adds are in
+      p.tag[r] = MsgTag{static_cast<unsigned int>(p.value), p.rank, sum};
     }
+    if (p.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(p.dst)[1] ^= 0x10;  // test hook
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // ROCm 7.2 / gfx950: after a returned atomic the compiler may drop the wait that follows
+    // the fence's write-back, letting the flag overtake it; keep the wait explicitly.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(p.flag, p.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -50,14 +117,63 @@ __global__ void signal_only(unsigned long long* flag, unsigned long long value) 
   __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Receiver check of the tagged rows of one put: one block, rows in turn (beta: one row).
+__global__ void __launch_bounds__(256) verify_rows(const unsigned char* rows, const MsgTag* tags, int nrows, int ld,
+                                                   int es, unsigned int round1, unsigned int rank,
+                                                   IntegrityErr* err, int where) {
+  __shared__ unsigned long long scratch[4];
+  for (int r = 0; r < nrows; ++r) {
+    const unsigned char* row = rows + static_cast<long long>(r) * ld * es;
+    unsigned long long t = 0;
+    for (int c = threadIdx.x; c < ld; c += blockDim.x) {
+      const unsigned long long bits = es == 8 ? *reinterpret_cast<const unsigned long long*>(row + 8ll * c)
+                                              : *reinterpret_cast<const unsigned int*>(row + 4ll * c);
+      t += tag_term(bits, c);
+    }
+    const unsigned long long sum = block_sum_u64(t, scratch);
+    if (threadIdx.x == 0) {
+      const MsgTag g = tags[r];
+      if (g.round1 != round1 || g.rank != rank || g.sum != sum)
+        report_integrity(err, static_cast<int>(round1) - 1, where, static_cast<int>(rank), g, sum);
+    }
+  }
+}
+
+__global__ void spin_ticks(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 hipError_t put_signal_launch(const PutArgs& args, int blocks, hipStream_t st) {
   if (args.n <= 0) return hipSuccess;
+  for (int k = 0; k < args.n; ++k) {
+    const PutDesc& p = args.d[k];
+    if (p.tag && (p.rows < 1 || p.rows > kMaxTagRows || (p.es != 4 && p.es != 8) || !p.csum ||
+                  (p.bytes / 16) % p.rows != 0))
+      return hipErrorInvalidValue;
+  }
   hipLaunchKernelGGL(put_signal, dim3(blocks, args.n), dim3(256), 0, st, args);
   return hipGetLastError();
 }
 
 hipError_t signal_launch(unsigned long long* flag, unsigned long long value, hipStream_t st) {
   hipLaunchKernelGGL(signal_only, dim3(1), dim3(1), 0, st, flag, value);
+  return hipGetLastError();
+}
+
+hipError_t verify_rows_launch(const void* rows, const MsgTag* tags, int nrows, int ld, int es,
+                              unsigned int round1, unsigned int rank, IntegrityErr* err, int where,
+                              hipStream_t st) {
+  if (nrows <= 0) return hipSuccess;
+  if (!rows || !tags || (es != 4 && es != 8)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(verify_rows, dim3(1), dim3(256), 0, st, static_cast<const unsigned char*>(rows), tags, nrows,
+                     ld, es, round1, rank, err, where);
+  return hipGetLastError();
+}
+
+hipError_t spin_launch(long long ticks, hipStream_t st) {
+  if (ticks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(spin_ticks, dim3(1), dim3(64), 0, st, ticks);
   return hipGetLastError();
 }
 

@@ -28,6 +28,8 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstring>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -268,6 +270,58 @@ std::shared_ptr<GradLauncher> make_ell(int64_t loss, const Tensor& idx, std::opt
   return g;
 }
 
+// One buffer row a decode uses: its address, coefficient and, for a mailbox row, its row index
+// (its integrity tag; -1 for a local row).
+struct Used {
+  const void* p;
+  double c;
+  int row;
+};
+using UsedRows = std::vector<Used>;
+
+// Host-mapped integrity record (integrity.h) and abort word of a pump.
+struct HostMapped {
+  void* host = nullptr;
+  void* dev = nullptr;
+  explicit HostMapped(size_t bytes) {
+    hcheck(hipHostMalloc(&host, bytes, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+    std::memset(host, 0, bytes);
+    hcheck(hipHostGetDevicePointer(&dev, host, 0), "hipHostGetDevicePointer");
+  }
+  ~HostMapped() {
+    if (host) hipHostFree(host);
+  }
+  HostMapped(const HostMapped&) = delete;
+  HostMapped& operator=(const HostMapped&) = delete;
+};
+
+// Test hook ERASUREHEAD_SABOTAGE=<what>:<rank>:<round> (what: msg | beta): the named put flips one
+// payload byte after its checksum, so the receiver must report a torn message.
+bool sabotage(const char* what, int rank, int round) {
+  static const std::string spec = [] {
+    const char* e = std::getenv("ERASUREHEAD_SABOTAGE");
+    return std::string(e ? e : "");
+  }();
+  if (spec.empty()) return false;
+  return spec == std::string(what) + ":" + std::to_string(rank) + ":" + std::to_string(round);
+}
+
+std::string integrity_message(const eh::IntegrityErr& e, bool beta) {
+  char buf[512];
+  if (beta)
+    std::snprintf(buf, sizeof(buf),
+                  "message integrity check failed: beta of round %d from rank %d: tag says round %d rank %u "
+                  "checksum %016llx, payload checksum %016llx",
+                  e.round, e.rank_want, static_cast<int>(e.round1_got) - 1, e.rank_got, e.sum_got, e.sum_calc);
+  else
+    std::snprintf(buf, sizeof(buf),
+                  "message integrity check failed: round %d, rank %d's message in mailbox slot %d row %d: tag says "
+                  "round %d rank %u checksum %016llx, payload checksum %016llx",
+                  e.round, e.rank_want, e.where >> 16, e.where & 0xffff, static_cast<int>(e.round1_got) - 1, e.rank_got,
+                  e.sum_got, e.sum_calc);
+  return buf;
+}
+
 // Decode kinds (codes/schemes.py)
 enum DecodeKind : int {
   kSumPart0 = 0,       // naive, avoidstragg: every arrived main message, coefficient 1
@@ -290,6 +344,10 @@ class MasterPump {
     loc_ev_.assign(K, nullptr);
     for (auto& e : loc_ev_) hcheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     index_.assign(2 * W, {});
+    err_ = std::make_unique<HostMapped>(sizeof(eh::IntegrityErr));
+    const auto i64 = at::TensorOptions().dtype(at::kLong).device(at::Device(at::kCUDA, device));
+    vscr_ = at::zeros({eh::kMaxMsgs + 1}, i64);           // combine checksums + block counter
+    csum_ = at::zeros({eh::kMaxPuts * eh::kMaxTagRows}, i64);  // beta put checksums
   }
   ~MasterPump() {
     if (dev_stream_) {
@@ -370,8 +428,8 @@ class MasterPump {
     }
   }
 
-  // remote messages: (worker, part, mailbox row, host address of the sender's round counter)
-  void set_remote(const Tensor& rbuf, const std::vector<std::tuple<int, int, int, uintptr_t>>& msgs) {
+  // remote messages: (worker, part, mailbox row, host address of the sender's round counter, sender rank)
+  void set_remote(const Tensor& rbuf, const std::vector<std::tuple<int, int, int, uintptr_t, int>>& msgs) {
     arb_ready_ = false;  // the device arbiter copies this state
     need_gpu(rbuf, "rbuf");
     need(rbuf.dim() == 3 && rbuf.size(0) == K_ && rbuf.size(2) == ld_, "rbuf must be [K, rows, ld]");
@@ -379,16 +437,37 @@ class MasterPump {
     rbuf_ = rbuf;
     r_rows_ = (int)rbuf.size(1);
     remote_.clear();
+    row_rank_.assign(r_rows_, 0);
     for (auto& ix : index_)
       ix.erase(std::remove_if(ix.begin(), ix.end(), [](const std::pair<int, int>& e) { return e.first == 1; }),
                ix.end());
-    for (const auto& [w, p, row, addr] : msgs) {
+    for (const auto& [w, p, row, addr, rank] : msgs) {
       check_wp(w, p);
       need(row >= 0 && row < r_rows_, "mailbox row out of range");
       need(addr != 0, "null flag address");
+      need(rank > 0 && rank < 256, "sender rank out of range");
       remote_.push_back({w, p, row, addr});
+      row_rank_[row] = rank;
       index_[2 * w + p].push_back({1, row});
     }
+  }
+
+  // Integrity tags (csrc/kernels/integrity.h): mbox_tags = device address of the mailbox's tag
+  // slots [K][rows]; inbox_tag_off = bytes from a worker inbox base to its tag slots [R + 1].
+  // on = false keeps the transport untagged (A/B runs).
+  void set_integrity(uintptr_t mbox_tags, int64_t inbox_tag_off, bool on) {
+    arb_ready_ = false;
+    need(!on || (mbox_tags != 0 && inbox_tag_off > 0), "integrity tags need the tag slots");
+    tags_ = on;
+    mbox_tags_ = mbox_tags;
+    inbox_tag_off_ = inbox_tag_off;
+  }
+  bool integrity() const { return tags_; }
+
+  // Raise the first integrity failure any combine of this pump reported (host-mapped record).
+  void check_integrity() const {
+    const auto* e = static_cast<const eh::IntegrityErr*>(err_->host);
+    if (__atomic_load_n(&e->flag, __ATOMIC_ACQUIRE)) throw std::runtime_error(integrity_message(*e, false));
   }
 
   // Device-side drain (after_combine): (host address, device address) of every worker rank's
@@ -430,6 +509,19 @@ class MasterPump {
     drain_ = drain;
   }
 
+  // --delay-on worker: virtual delays the collector applies to REMOTE messages (the worker ranks
+  // are physically late themselves); default: the same table as the local messages.
+  void set_remote_delays(const std::vector<double>& delays) {
+    arb_ready_ = false;
+    need((int64_t)delays.size() >= (int64_t)R_ * W_, "remote delays must be [R*W]");
+    remote_delays_ = delays;
+  }
+  // --slow-ranks: this rank launches its local gradient `n` times per round (a slower GPU).
+  void set_repeat(int n) {
+    need(n >= 1, "repeat must be >= 1");
+    repeat_ = n;
+  }
+
   void set_decode(int kind, const std::vector<int>& group_of, int n_groups) {
     arb_ready_ = false;  // the device arbiter copies this state
     need((int)group_of.size() == W_, "group_of must have W entries");
@@ -461,17 +553,18 @@ class MasterPump {
     const void* src = bin + static_cast<int64_t>(i) * ld_ * es_;
     if (i != prepub_) put_beta(i);  // else already queued behind the device-side drain of round i-1
     const double* dl = delays_.data() + static_cast<int64_t>(i) * W_;
+    const double* dr = remote_delays_.empty() ? dl : remote_delays_.data() + static_cast<int64_t>(i) * W_;
     if (n_loc_ > 0 && launcher_) {
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
       if (timing_) record_t(i, 2);
-      hcheck(launcher_->launch(src, g, stream_), "local gradient");
+      for (int k = 0; k < repeat_; ++k) hcheck(launcher_->launch(src, g, stream_), "local gradient");
       if (timing_) record_t(i, 3);
       hcheck(hipEventRecord(loc_ev_[slot], stream_), "hipEventRecord");
       for (const auto& m : local_)
         col_->add_event_probe(m.w, m.p, i, reinterpret_cast<uintptr_t>(loc_ev_[slot]), dl[m.w]);
     }
     for (const auto& m : remote_)
-      col_->add_flag_probe(m.w, m.p, i, m.flag, static_cast<uint64_t>(i + 1), dl[m.w]);
+      col_->add_flag_probe(m.w, m.p, i, m.flag, static_cast<uint64_t>(i + 1), dr[m.w]);
   }
 
   // Returns (status, arrivals [(worker, part, t_rel)], t_start, t_decoded, t_end, t_waited):
@@ -489,8 +582,9 @@ class MasterPump {
         ok = col_->wait(timeout_);
       }
       t_waited_ = eh::Collector::now();
+      check_integrity();  // an earlier round's combine found a torn / stale message
       arr = col_->arrivals();
-      std::vector<std::pair<const void*, double>> used;
+      UsedRows used;
       Range tr("eh.master.decode_update");
       const bool decoded = decode(i, arr, used);
       if (!decoded) {
@@ -511,7 +605,7 @@ class MasterPump {
     double t_dec, t_end;
     {
       py::gil_scoped_release nogil;
-      std::vector<std::pair<const void*, double>> used;
+      UsedRows used;
       for (const auto& [w, p, c] : coefs) push_msg(used, i % K_, w, p, c);
       combine(i, used);
       t_dec = eh::Collector::now();
@@ -540,7 +634,7 @@ class MasterPump {
     for (int i = a; i < b; ++i)
       for (int w = 0; w < W_; ++w) need(delays_[static_cast<int64_t>(i) * W_ + w] == 0.0, "injected delay present");
     std::vector<std::vector<eh::Arrival>> arrs;
-    std::vector<std::vector<std::pair<const void*, double>>> useds;
+    std::vector<UsedRows> useds;
     arrs.reserve(b - a);
     useds.reserve(b - a);
     auto decode_round = [&](int i) {
@@ -549,7 +643,7 @@ class MasterPump {
       t_start_[i] = t;
       for (const auto& m : local_) col_->mark_seen(col_->add_host_probe(m.w, m.p, i, 0.0), t);
       need(col_->wait(timeout_), "local arrivals did not satisfy the stop rule");
-      std::vector<std::pair<const void*, double>> used;
+      UsedRows used;
       need(decode(i, col_->arrivals(), used), "completion pattern missing from the decode table");
       arrs.push_back(col_->arrivals());
       useds.push_back(std::move(used));
@@ -640,8 +734,12 @@ class MasterPump {
     if ((int)(local_.size() + remote_.size()) > eh::kArbMaxProbes) return "too many message shards";
     if (!drain_ && stop_rule_ != eh::kRuleAll) return "scheme without a drain (late messages cross rounds)";
     if ((decode_kind_ == kTable || decode_kind_ == kPartialTable) && W_ > 16) return "decode table too large";
-    for (const auto& ix : index_)
+    size_t rows = 0;  // worst case of one decode: every buffer row of every message
+    for (const auto& ix : index_) {
       if ((int)ix.size() > eh::kArbMaxRows) return "message with more than 16 shards";
+      rows += ix.size();
+    }
+    if (rows > static_cast<size_t>(eh::kMaxMsgs)) return "more than 128 message rows in a decode";
     for (const auto& m : remote_) {
       bool found = false;
       for (const auto& f : arb_src_) found |= f.first == m.flag;
@@ -660,6 +758,9 @@ class MasterPump {
     const std::string why = device_blocker(a, b);
     need(why.empty(), "device-driven rounds: " + why);
     if (!arb_ready_) arb_prepare();
+    // a new segment starts clean: no abort from an earlier failed segment (whose failure device_log
+    // reports; the engine does not continue a run past it)
+    hcheck(hipMemsetAsync(arb_abort_.data_ptr(), 0, sizeof(int), stream_), "hipMemsetAsync(abort)");
     eh::ArbArgs args = arb_args_;
     args.deadline_ticks = static_cast<long long>(std::max(0.001, deadline_s) * stamp_hz());
     long long* tlog = reinterpret_cast<long long*>(arb_tlog_.data_ptr<int64_t>());
@@ -671,7 +772,8 @@ class MasterPump {
     for (int i = a; i < b; ++i) {
       if (n_loc_ > 0 && launcher_) {
         char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(i % K_) * g_rows_ * ld_ * es_;
-        hcheck(launcher_->launch(bin + static_cast<int64_t>(i) * ld_ * es_, g, stream_), "local gradient");
+        for (int k = 0; k < repeat_; ++k)
+          hcheck(launcher_->launch(bin + static_cast<int64_t>(i) * ld_ * es_, g, stream_), "local gradient");
       }
       hcheck(eh::arbiter_round_launch(args, i, acc_, stream_), "arbiter_round");
     }
@@ -696,7 +798,22 @@ class MasterPump {
       const int n = std::min(l[1], 2 * eh::kArbMaxW);
       for (int x = 0; x < n && l[0] == 0; ++x)
         arr.append(py::make_tuple(l[4 + 2 * x], l[5 + 2 * x], (t[4 + x] - t[0]) / hz));
-      out.append(py::make_tuple(l[0], arr, (t[1] - t[0]) / hz, (t[2] - t[0]) / hz));
+      std::string why;
+      if (l[0] == eh::kArbIntegrity) {
+        eh::IntegrityErr e{};
+        e.round = i;
+        e.where = l[2];
+        e.rank_want = l[3];
+        e.round1_got = static_cast<unsigned int>(l[4]);
+        e.rank_got = static_cast<unsigned int>(l[5]);
+        e.sum_got = static_cast<unsigned long long>(t[4]);
+        e.sum_calc = static_cast<unsigned long long>(t[5]);
+        why = integrity_message(e, false);
+      }
+      // per-round ticks: poll (release of beta(i) -> stop rule), update (stop rule -> combine and
+      // checks done), release (-> beta(i+1) released, drain included); seconds
+      const double t_stop = l[0] == 0 && n > 0 ? (t[4 + n - 1] - t[0]) / hz : -1.0;
+      out.append(py::make_tuple(l[0], arr, (t[1] - t[0]) / hz, (t[2] - t[0]) / hz, why, t_stop));
     }
     return out;
   }
@@ -743,17 +860,17 @@ class MasterPump {
   }
 
   // every buffer row (one per shard) of message (w, p) in ring slot `slot`, each with coefficient c
-  void push_msg(std::vector<std::pair<const void*, double>>& used, int slot, int w, int p, double c) const {
+  void push_msg(UsedRows& used, int slot, int w, int p, double c) const {
     const auto& ix = index_[2 * w + p];
     if (ix.empty()) throw std::logic_error("message without a buffer");
     for (const auto& [kind, row] : ix) {
       const char* base = kind == 0 ? static_cast<const char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_
                                    : static_cast<const char*>(rbuf_.data_ptr()) + static_cast<int64_t>(slot) * r_rows_ * ld_ * es_;
-      used.push_back({base + static_cast<int64_t>(row) * ld_ * es_, c});
+      used.push_back({base + static_cast<int64_t>(row) * ld_ * es_, c, kind == 0 ? -1 : row});
     }
   }
 
-  bool decode(int i, const std::vector<eh::Arrival>& arr, std::vector<std::pair<const void*, double>>& used) const {
+  bool decode(int i, const std::vector<eh::Arrival>& arr, UsedRows& used) const {
     const int slot = i % K_;
     std::vector<char> gdone(std::max(n_groups_, 1), 0);
     uint64_t mask = 0;
@@ -790,14 +907,27 @@ class MasterPump {
 
   // events: time the update with HIP events (host-driven rounds); stamp: device timestamp
   // written by the update kernel at its start (device-driven rounds, graph capture).
-  void combine(int i, const std::vector<std::pair<const void*, double>>& used, bool events = true,
+  void combine(int i, const UsedRows& used, bool events = true,
                long long* stamp = nullptr) {
     need((int)used.size() <= eh::kMaxMsgs, "too many messages for one combine");
     eh::CombineArgs a{};
     a.nmsg = (int)used.size();
+    bool remote = false;
     for (int m = 0; m < a.nmsg; ++m) {
-      a.msg[m] = used[m].first;
-      a.coef[m] = used[m].second;
+      a.msg[m] = used[m].p;
+      a.coef[m] = used[m].c;
+      a.tag_row[m] = used[m].row;
+      a.tag_rank[m] = static_cast<unsigned char>(used[m].row >= 0 ? row_rank_[used[m].row] : 0);
+      remote |= used[m].row >= 0;
+    }
+    if (tags_ && remote) {  // check the mailbox rows against their senders' tags (update.hip)
+      const int slot = i % K_;
+      a.tags = reinterpret_cast<const eh::MsgTag*>(mbox_tags_) + static_cast<int64_t>(slot) * r_rows_;
+      a.round1 = static_cast<unsigned int>(i + 1);
+      a.slot = slot;
+      a.vsum = reinterpret_cast<unsigned long long*>(vscr_.data_ptr<int64_t>());
+      a.vcount = reinterpret_cast<unsigned int*>(vscr_.data_ptr<int64_t>() + eh::kMaxMsgs);
+      a.err = static_cast<eh::IntegrityErr*>(err_->dev);
     }
     auto& ev = upd_ev_[i];
     if (events) {
@@ -875,7 +1005,8 @@ class MasterPump {
     arb_keep_ = {ints(group_of_), ints(pw), ints(pp), ints(ps), ints(nsh), ints(nrows), ints(rows), ints(tie),
                  dbl(decay_), dbl(gm_), dbl(l2_), dbl(theta_), u64(src.empty() ? std::vector<int64_t>{0} : src),
                  u64(tgt.empty() ? std::vector<int64_t>{0, 0} : tgt),
-                 table.empty() ? at::Tensor() : dbl(table)};
+                 table.empty() ? at::Tensor() : dbl(table),
+                 ints(row_rank_.empty() ? std::vector<int>{0} : row_rank_)};
     arb_log_ = at::zeros({static_cast<int64_t>(R_) * eh::kArbLogInts}, at::TensorOptions().dtype(at::kInt).device(dev));
     arb_tlog_ = at::zeros({static_cast<int64_t>(R_) * eh::kArbLogTicks}, at::TensorOptions().dtype(at::kLong).device(dev));
     arb_abort_ = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(dev));
@@ -920,6 +1051,9 @@ class MasterPump {
     g.log = arb_log_.data_ptr<int>();
     g.tlog = reinterpret_cast<long long*>(arb_tlog_.data_ptr<int64_t>());
     g.abort = arb_abort_.data_ptr<int>();
+    g.tags = tags_ ? reinterpret_cast<const eh::MsgTag*>(mbox_tags_) : nullptr;
+    g.row_rank = arb_keep_[15].data_ptr<int>();
+    g.inbox_tag_off = inbox_tag_off_;
     arb_args_ = g;
     arb_ready_ = true;
   }
@@ -933,11 +1067,20 @@ class MasterPump {
       eh::PutArgs a{};
       a.n = 0;
       for (size_t k = k0; k < targets_.size() && a.n < eh::kMaxPuts; ++k) {
-        a.d[a.n] = eh::PutDesc{src, reinterpret_cast<char*>(targets_[k].first) + static_cast<int64_t>(j) * ld_ * es_,
-                               static_cast<long long>(ld_) * es_,
-                               reinterpret_cast<unsigned long long*>(targets_[k].second),
-                               static_cast<unsigned long long>(j + 1),
-                               reinterpret_cast<unsigned int*>(counters_.data_ptr<int>()) + k};
+        auto& d = a.d[a.n];
+        d = eh::PutDesc{src, reinterpret_cast<char*>(targets_[k].first) + static_cast<int64_t>(j) * ld_ * es_,
+                        static_cast<long long>(ld_) * es_,
+                        reinterpret_cast<unsigned long long*>(targets_[k].second),
+                        static_cast<unsigned long long>(j + 1),
+                        reinterpret_cast<unsigned int*>(counters_.data_ptr<int>()) + k};
+        if (tags_) {
+          d.tag = reinterpret_cast<eh::MsgTag*>(reinterpret_cast<char*>(targets_[k].first) + inbox_tag_off_) + j;
+          d.csum = reinterpret_cast<unsigned long long*>(csum_.data_ptr<int64_t>()) + a.n * eh::kMaxTagRows;
+          d.rows = 1;
+          d.es = es_;
+          d.rank = 0;
+          d.corrupt = sabotage("beta", static_cast<int>(k) + 1, j) ? 1 : 0;
+        }
         ++a.n;
       }
       hcheck(eh::put_signal_launch(a, blocks_for(static_cast<long long>(ld_) * es_), stream_), "put_signal(beta)");
@@ -946,8 +1089,11 @@ class MasterPump {
   }
 
   bool no_delay(int i) const {
+    const auto zero = [](double x) { return x == 0.0; };
     const double* dl = delays_.data() + static_cast<int64_t>(i) * W_;
-    return std::all_of(dl, dl + W_, [](double x) { return x == 0.0; });
+    if (!std::all_of(dl, dl + W_, zero)) return false;
+    const double* dr = remote_delays_.empty() ? dl : remote_delays_.data() + static_cast<int64_t>(i) * W_;
+    return std::all_of(dr, dr + W_, zero);
   }
 
   double after_combine(int i, bool publish_next) {
@@ -1001,12 +1147,19 @@ class MasterPump {
   std::vector<std::pair<uintptr_t, uintptr_t>> targets_;
   std::vector<std::pair<uintptr_t, uintptr_t>> drain_flags_;
   int prepub_ = -1;  // round whose beta is already queued (device-side drain / the arbiter)
+  bool tags_ = false;               // integrity tags on (set_integrity)
+  uintptr_t mbox_tags_ = 0;         // device address of the mailbox tag slots [K][r_rows]
+  int64_t inbox_tag_off_ = 0;       // worker inbox base -> its tag slots
+  std::vector<int> row_rank_;       // [r_rows] sender rank of each mailbox row
+  std::unique_ptr<HostMapped> err_;  // first integrity failure (eh::IntegrityErr)
+  Tensor vscr_, csum_;              // combine checksum scratch, beta put checksum scratch
   std::vector<std::pair<uintptr_t, uintptr_t>> arb_src_;
   bool arb_ready_ = false;
   eh::ArbArgs arb_args_{};
   std::vector<Tensor> arb_keep_;
   Tensor arb_log_, arb_tlog_, arb_abort_;
-  std::vector<double> decay_, gm_, l2_, theta_, delays_;
+  std::vector<double> decay_, gm_, l2_, theta_, delays_, remote_delays_;
+  int repeat_ = 1;
   int update_rule_ = 0, stop_rule_ = 0, k_ = 0;
   bool drain_ = false;
   int decode_kind_ = kSumPart0, n_groups_ = 1;
@@ -1043,6 +1196,7 @@ class WorkerPump {
     need(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.numel() >= 1, "counters");
     ld_ = (int)inbox.size(1);
     R_ = (int)inbox.size(0) - 1;
+    device_ = device;
     es_ = acc_code(G) == 0 ? 8 : 4;
     g_rows_ = (int)G.size(1);
     stream_ = c10::hip::getCurrentHIPStream(device).stream();
@@ -1056,9 +1210,49 @@ class WorkerPump {
     int can = 0;
     if (bflag_dev_ && hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess)
       dwait_ = can != 0;
+    err_ = std::make_unique<HostMapped>(sizeof(eh::IntegrityErr));
+    abort_ = std::make_unique<HostMapped>(sizeof(int));
+    csum_ = at::zeros({eh::kMaxTagRows}, at::TensorOptions().dtype(at::kLong).device(at::Device(at::kCUDA, device)));
   }
   bool fused_put() const { return fuse_put_; }
   bool device_wait() const { return dwait_; }
+
+  // --delay-on worker: seconds this rank is physically late in every round.  A device spin
+  // (wall_clock64 + s_sleep) between the gradient and the put, so the put really leaves late
+  // while the rounds stay queued; the put is then its own kernel (not fused into the reduction).
+  void set_delays(const std::vector<double>& seconds) {
+    need((int)seconds.size() >= R_, "delays must cover R rounds");
+    int khz = 0;
+    hcheck(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_), "hipDeviceGetAttribute");
+    late_ticks_.assign(R_, 0);
+    for (int i = 0; i < R_; ++i)
+      late_ticks_[i] = static_cast<long long>(std::min(seconds[i], 3600.0) * 1e3 * khz);
+    if (std::any_of(late_ticks_.begin(), late_ticks_.end(), [](long long t) { return t > 0; })) fuse_put_ = false;
+  }
+  // --slow-ranks: the gradient runs `n` times per round.
+  void set_repeat(int n) {
+    need(n >= 1, "repeat must be >= 1");
+    repeat_ = n;
+  }
+
+  // Integrity tags (csrc/kernels/integrity.h): mbox_tags = this rank's view of the master
+  // mailbox's tag slots [K][mbox_rows]; inbox_tags = its own inbox's tag slots [R + 1].  Every
+  // message put carries a tag per row; every beta is checked after the round that read it.
+  void set_integrity(uintptr_t mbox_tags, uintptr_t inbox_tags, int rank, bool on) {
+    need(!on || (mbox_tags != 0 && inbox_tags != 0), "integrity tags need the tag slots");
+    need(!on || n_ <= eh::kMaxTagRows, "a tagged put holds at most 64 message rows");
+    tags_ = on;
+    mtags_ = reinterpret_cast<eh::MsgTag*>(mbox_tags);
+    itags_ = reinterpret_cast<const eh::MsgTag*>(inbox_tags);
+    rank_ = rank;
+  }
+  // Raise the first failed beta check (host-mapped record), after releasing this rank's queued work.
+  void check_integrity() {
+    const auto* e = static_cast<const eh::IntegrityErr*>(err_->host);
+    if (!__atomic_load_n(&e->flag, __ATOMIC_ACQUIRE)) return;
+    stop_queued();
+    throw std::runtime_error("rank " + std::to_string(rank_) + ": " + integrity_message(*e, true));
+  }
   ~WorkerPump() {
     for (auto& t : tev_)
       for (auto e : t)
@@ -1091,28 +1285,42 @@ class WorkerPump {
       Range tr("eh.worker.round");
       if (dwait_) {
         // enqueue round i once beta(i-1) is in: one round of lookahead, host timeout kept
-        if (i > a && !host_wait(i, i - 1)) return release(i - 1, b);
+        if (i > a && !host_wait(i, i - 1)) return release(i - 1);
+        check_integrity();
         if (n_ == 0) continue;
         hcheck(hipStreamWaitValue64(stream_, bflag_dev_, static_cast<uint64_t>(i + 1), hipStreamWaitValueGte),
                "hipStreamWaitValue64(beta flag)");
       } else {
         if (!host_wait(i + 1, i)) return i;
+        check_integrity();
         if (n_ == 0) continue;
       }
       const int slot = i % K_;
       const char* beta = static_cast<const char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * ld_ * es_;
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
       const long long bytes = static_cast<long long>(n_) * ld_ * es_;
-      const eh::PutDesc pd{g, reinterpret_cast<char*>(mbox_) + (static_cast<int64_t>(slot) * mbox_rows_ + row0_) * ld_ * es_,
-                           bytes, mflag_, static_cast<unsigned long long>(i + 1),
-                           reinterpret_cast<unsigned int*>(counters_.data_ptr<int>())};
+      eh::PutDesc pd{g, reinterpret_cast<char*>(mbox_) + (static_cast<int64_t>(slot) * mbox_rows_ + row0_) * ld_ * es_,
+                     bytes, mflag_, static_cast<unsigned long long>(i + 1),
+                     reinterpret_cast<unsigned int*>(counters_.data_ptr<int>())};
+      pd.abort = static_cast<const int*>(abort_->dev);
+      if (tags_) {
+        pd.tag = mtags_ + static_cast<int64_t>(slot) * mbox_rows_ + row0_;
+        pd.csum = reinterpret_cast<unsigned long long*>(csum_.data_ptr<int64_t>());
+        pd.rows = n_;
+        pd.es = es_;
+        pd.rank = static_cast<unsigned int>(rank_);
+        pd.corrupt = sabotage("msg", rank_, i) ? 1 : 0;
+      }
       if (timing_) record_t(i, 0);
+      for (int k = 1; k < repeat_; ++k) hcheck(g_->launch(beta, g, stream_), "worker gradient (slow rank)");
       if (fuse_put_) {  // gradient + put + signal in one stream order, no separate put kernel
         hcheck(g_->launch_put(beta, g, pd, stream_), "worker gradient + put");
         if (timing_) record_t(i, 1);
       } else {
         hcheck(g_->launch(beta, g, stream_), "worker gradient");
         if (timing_) record_t(i, 1);
+        if (!late_ticks_.empty() && late_ticks_[i] > 0)  // after compute, before the send (ref src/naive.py:141-148)
+          hcheck(eh::spin_launch(late_ticks_[i], stream_), "late worker spin");
         eh::PutArgs pa{};
         pa.n = 1;
         pa.d[0] = pd;
@@ -1120,8 +1328,16 @@ class WorkerPump {
         hcheck(eh::put_signal_launch(pa, blocks, stream_), "put_signal(messages)");
       }
       if (timing_) record_t(i, 2);
+      if (tags_)  // beta(i) against its tag, behind the round that read it (off the critical path)
+        hcheck(eh::verify_rows_launch(beta, itags_ + i, 1, ld_, es_, static_cast<unsigned int>(i + 1), 0u,
+                                      static_cast<eh::IntegrityErr*>(err_->dev), -1, stream_),
+               "verify_rows(beta)");
     }
-    if (dwait_ && b > a && !host_wait(b, b - 1)) return release(b - 1, b);
+    if (dwait_ && b > a && !host_wait(b, b - 1)) return release(b - 1);
+    if (tags_) {  // the last rounds' checks
+      hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+      check_integrity();
+    }
     return -1;
   }
 
@@ -1143,13 +1359,22 @@ class WorkerPump {
     wait_s_[rec] = std::chrono::duration<double>(clk::now() - t0).count();
     return true;
   }
-  // Timeout with device-side waits queued: the master is gone, so release this rank's own
-  // stream waits (store the flag value they wait for) and let the queued rounds drain on
-  // stale data instead of leaving a wait on the GPU.  Returns the round that timed out.
-  int release(int bad, int b) {
-    __atomic_store_n(bflag_, static_cast<uint64_t>(b), __ATOMIC_RELEASE);
-    hipStreamSynchronize(stream_);
+  // Timeout with device-side waits queued: the master is gone (or late beyond the timeout).  The
+  // queued rounds must not announce messages computed on a beta that never arrived, so the abort
+  // word goes up FIRST (every queued put / put+signal kernel checks it and skips its put and its
+  // signal), then this rank's own stream waits are released (the flag value they wait for) so no
+  // wait is left on the GPU.  Returns the round that timed out.
+  int release(int bad) {
+    stop_queued();
     return bad;
+  }
+  void stop_queued() {
+    __atomic_store_n(static_cast<int*>(abort_->host), 1, __ATOMIC_RELEASE);
+    if (dwait_) {
+      const uint64_t top = static_cast<uint64_t>(R_) + 1;
+      if (__atomic_load_n(bflag_, __ATOMIC_ACQUIRE) < top) __atomic_store_n(bflag_, top, __ATOMIC_RELEASE);
+    }
+    hipStreamSynchronize(stream_);
   }
 
   void record_t(int i, int which) {
@@ -1174,6 +1399,16 @@ class WorkerPump {
   bool timing_ = false;
   bool fuse_put_ = false;
   bool dwait_ = false;
+  bool tags_ = false;
+  eh::MsgTag* mtags_ = nullptr;          // master mailbox tag slots (this rank's mapping)
+  const eh::MsgTag* itags_ = nullptr;    // own inbox tag slots
+  int rank_ = 0;
+  std::unique_ptr<HostMapped> err_;      // first failed beta check (eh::IntegrityErr)
+  std::unique_ptr<HostMapped> abort_;    // int: queued puts skip themselves once set
+  Tensor csum_;                          // tagged put checksum scratch [kMaxTagRows]
+  std::vector<long long> late_ticks_;    // [R] device spin before the put (--delay-on worker)
+  int repeat_ = 1;                       // gradient launches per round (--slow-ranks)
+  int device_ = 0;
   std::vector<std::array<hipEvent_t, 3>> tev_;  // [round] gradient start, gradient end = put start, put end
   std::vector<double> wait_s_;                  // [round] host seconds spent waiting for beta
 };
@@ -1222,6 +1457,11 @@ void bind_engine(py::module& m) {
       .def("set_remote", &MasterPump::set_remote)
       .def("set_puts", &MasterPump::set_puts)
       .def("set_drain_flags", &MasterPump::set_drain_flags)
+      .def("set_remote_delays", &MasterPump::set_remote_delays)
+      .def("set_repeat", &MasterPump::set_repeat)
+      .def("set_integrity", &MasterPump::set_integrity, py::arg("mbox_tags"), py::arg("inbox_tag_off"), py::arg("on"))
+      .def_property_readonly("integrity", &MasterPump::integrity)
+      .def("check_integrity", &MasterPump::check_integrity)
       .def("set_sources", &MasterPump::set_sources)
       .def("device_blocker", &MasterPump::device_blocker)
       .def("run_device", &MasterPump::run_device, py::arg("a"), py::arg("b"), py::arg("deadline_s"))
@@ -1248,6 +1488,11 @@ void bind_engine(py::module& m) {
       .def_property_readonly("fused_put", &WorkerPump::fused_put)
       .def_property_readonly("device_wait", &WorkerPump::device_wait)
       .def("set_timing", &WorkerPump::set_timing)
+      .def("set_delays", &WorkerPump::set_delays)
+      .def("set_repeat", &WorkerPump::set_repeat)
+      .def("set_integrity", &WorkerPump::set_integrity, py::arg("mbox_tags"), py::arg("inbox_tags"), py::arg("rank"),
+           py::arg("on"))
+      .def("check_integrity", &WorkerPump::check_integrity)
       .def("timing", &WorkerPump::timing);
 }
 }  // namespace eh

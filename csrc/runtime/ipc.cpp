@@ -247,6 +247,67 @@ void put_signal(const std::vector<std::tuple<Tensor, Tensor, uintptr_t, uint64_t
          "put_signal");
 }
 
+// One tagged put (csrc/kernels/integrity.h) of src [rows, ld] into dst, with one MsgTag per row into
+// `tags` (uint8 [rows * 16], on any device the GPU can write); csum: int64 zeroed scratch [>= rows].
+// The engine's pumps build the same descriptors natively; this entry point serves the kernel tests.
+void put_signal_tagged(const Tensor& src, const Tensor& dst, const Tensor& tags, uintptr_t flag, uint64_t value,
+                       int64_t rank, const Tensor& counters, const Tensor& csum, bool corrupt) {
+  for (auto* t : {&src, &dst, &tags, &counters, &csum})
+    if (!t->is_cuda() || !t->is_contiguous()) throw std::invalid_argument("put_signal_tagged: GPU contiguous tensors");
+  if (src.dim() != 2 || dst.sizes() != src.sizes() || src.scalar_type() != dst.scalar_type())
+    throw std::invalid_argument("put_signal_tagged: src/dst must be [rows, ld] of one dtype");
+  const int64_t rows = src.size(0), es = src.element_size();
+  if ((es != 4 && es != 8) || (src.size(1) * es) % 16 || rows < 1 || rows > eh::kMaxTagRows)
+    throw std::invalid_argument("put_signal_tagged: rows of fp32/fp64, 16-byte multiples, 1..64 rows");
+  if (tags.numel() * tags.element_size() < rows * 16 || csum.scalar_type() != at::kLong || csum.numel() < rows)
+    throw std::invalid_argument("put_signal_tagged: tags [rows*16 bytes], csum int64 [rows]");
+  if (flag == 0) throw std::invalid_argument("put_signal_tagged: null flag");
+  eh::PutArgs a{};
+  a.n = 1;
+  auto& d = a.d[0];
+  d = eh::PutDesc{src.data_ptr(), dst.data_ptr(), src.numel() * es, reinterpret_cast<unsigned long long*>(flag), value,
+                  reinterpret_cast<unsigned int*>(counters.data_ptr<int>())};
+  d.tag = static_cast<eh::MsgTag*>(tags.data_ptr());
+  d.csum = reinterpret_cast<unsigned long long*>(csum.data_ptr<int64_t>());
+  d.rows = static_cast<int>(rows);
+  d.es = static_cast<int>(es);
+  d.rank = static_cast<unsigned int>(rank);
+  d.corrupt = corrupt ? 1 : 0;
+  const int64_t nb = src.numel() * es;
+  const int blocks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(64, (nb / 16 + 4095) / 4096)));
+  hcheck(eh::put_signal_launch(a, blocks, c10::hip::getCurrentHIPStream(src.device().index()).stream()),
+         "put_signal_tagged");
+}
+
+// Check the rows [n, ld] of one put against tags (uint8 [n * 16]) for counter value round1 and sender
+// `rank`; returns the first failure as a dict (empty when every row matches).  Synchronises.
+py::dict verify_rows(const Tensor& rows, const Tensor& tags, int64_t round1, int64_t rank) {
+  if (!rows.is_cuda() || !tags.is_cuda() || rows.dim() != 2) throw std::invalid_argument("verify_rows: GPU [n, ld]");
+  void* h = nullptr;
+  void* dptr = nullptr;
+  hcheck(hipHostMalloc(&h, sizeof(eh::IntegrityErr), hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+  std::memset(h, 0, sizeof(eh::IntegrityErr));
+  hcheck(hipHostGetDevicePointer(&dptr, h, 0), "hipHostGetDevicePointer");
+  const hipStream_t st = c10::hip::getCurrentHIPStream(rows.device().index()).stream();
+  hipError_t e = eh::verify_rows_launch(rows.data_ptr(), static_cast<const eh::MsgTag*>(tags.data_ptr()),
+                                        static_cast<int>(rows.size(0)), static_cast<int>(rows.size(1)),
+                                        static_cast<int>(rows.element_size()), static_cast<unsigned int>(round1),
+                                        static_cast<unsigned int>(rank), static_cast<eh::IntegrityErr*>(dptr), 0, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  const eh::IntegrityErr r = *static_cast<eh::IntegrityErr*>(h);
+  hipHostFree(h);
+  hcheck(e, "verify_rows");
+  py::dict out;
+  if (r.flag) {
+    out["round"] = r.round;
+    out["round1_got"] = r.round1_got;
+    out["rank_got"] = r.rank_got;
+    out["sum_got"] = r.sum_got;
+    out["sum_calc"] = r.sum_calc;
+  }
+  return out;
+}
+
 void signal(uintptr_t flag, uint64_t value, int64_t device) {
   if (flag == 0) throw std::invalid_argument("signal: null flag");
   hcheck(eh::signal_launch(reinterpret_cast<unsigned long long*>(flag), value,
@@ -298,6 +359,9 @@ void bind_ipc(py::module& m) {
       .def_property_readonly("size", &ShmFlags::size);
   m.def("put_signal", &put_signal, py::arg("puts"), py::arg("counters"), py::arg("blocks") = 0);
   m.def("signal", &signal, py::arg("flag"), py::arg("value"), py::arg("device"));
+  m.def("put_signal_tagged", &put_signal_tagged, py::arg("src"), py::arg("dst"), py::arg("tags"), py::arg("flag"),
+        py::arg("value"), py::arg("rank"), py::arg("counters"), py::arg("csum"), py::arg("corrupt") = false);
+  m.def("verify_rows", &verify_rows, py::arg("rows"), py::arg("tags"), py::arg("round1"), py::arg("rank"));
   m.def("pci_bus_id", &pci_bus_id, py::arg("device"));
   m.def("device_by_pci", &device_by_pci, py::arg("bus_id"));
   m.def("can_access_peer", &can_access_peer, py::arg("device"), py::arg("peer"));

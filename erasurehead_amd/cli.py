@@ -41,7 +41,12 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--data-seed", type=int, default=0)
     g.add_argument("--allow-uneven-groups", action="store_true")
     g.add_argument("--drain", default=None, choices=["all", "lazy"])
-    g.add_argument("--delay-mode", default="exp", choices=["exp", "fixed", "none"])
+    g.add_argument("--delay-mode", default="exp", choices=["exp", "fixed", "none", "worker"],
+                   help="injected delay distribution; worker = exp slept on the worker rank (--delay-on worker)")
+    g.add_argument("--delay-on", default="collector", choices=["collector", "worker"],
+                   help="virtual arrival time on the master (collector) or a physically late worker rank")
+    g.add_argument("--slow-ranks", nargs="*", default=[], metavar="RANK:FACTOR",
+                   help="physically slow GPU ranks: each runs its gradient FACTOR times per round")
     g.add_argument("--fixed-stragglers", type=int, nargs="*", default=[])
     g.add_argument("--fixed-sleep", type=float, default=0.5)
     g.add_argument("--kill-workers", type=int, nargs="*", default=[])
@@ -71,7 +76,18 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--tie-seed", type=int, default=0)
     g.add_argument("--shard", default="auto", choices=["auto", "message", "partition"],
                    help="placement unit on several ranks: whole messages or partition shards (auto: shards)")
+    g.add_argument("--no-integrity", action="store_true",
+                   help="IPC messages without (round, rank, checksum) tags (A/B runs only)")
     return p
+
+
+def parse_slow_ranks(items) -> dict:
+    """['3:4', '5:2'] -> {3: 4, 5: 2}."""
+    out = {}
+    for it in items or []:
+        r, _, f = str(it).partition(":")
+        out[int(r)] = int(f or 2)
+    return out
 
 
 def parse(argv: List[str]):
@@ -91,7 +107,8 @@ def parse(argv: List[str]):
                     full_precision_outputs=a.full_precision_outputs, evaluate=not a.no_eval, verbose=not a.quiet,
                     checkpoint_every=a.checkpoint_every, checkpoint_path=a.checkpoint_path, resume=a.resume, trace=a.trace, verify_beta=a.verify_beta,
                     transport=a.transport, share_partitions=a.share_partitions, device_loop=a.device_loop,
-                    tie_break=a.tie_break, tie_seed=a.tie_seed, shard=a.shard)
+                    tie_break=a.tie_break, tie_seed=a.tie_seed, shard=a.shard,
+                    integrity=not a.no_integrity, delay_on=a.delay_on, slow_ranks=parse_slow_ranks(a.slow_ranks))
     return cfg, a
 
 

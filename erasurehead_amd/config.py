@@ -12,7 +12,7 @@ defaults reproduce the reference, including its quirks, unl
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import numpy as np
 
@@ -51,6 +51,12 @@ class RunConfig:
     allow_uneven_groups: bool = False  # FRC with W % (s+1) != 0
     drain: Optional[str] = None  # None = scheme default; "all" | "lazy"
     delay_mode: str = "exp"  # exp (reference) | fixed | none
+    # where an injected delay happens: "collector" (a virtual arrival time on the master's clock, the
+    # GPUs never idle) or "worker" (the worker rank is physically late: its messages leave after a
+    # device spin / host sleep, after compute and before the send, like the reference's time.sleep)
+    delay_on: str = "collector"
+    # rank -> factor: that rank runs its gradient `factor` times per round (a physically slower GPU)
+    slow_ranks: Dict[int, int] = field(default_factory=dict)
     delay_mean: float = 0.5
     fixed_stragglers: List[int] = field(default_factory=list)  # 1-based worker ids (fixed mode)
     fixed_sleep: float = 0.5
@@ -83,6 +89,8 @@ class RunConfig:
     # or "auto" (partition when there are several ranks)
     shard: str = "auto"
     instrument: bool = False  # per-round HIP-event timing of puts / gradient launches (Trainer.rank_report)
+    # IPC messages carry (round, rank, checksum) tags that the receiver verifies (csrc/kernels/integrity.h)
+    integrity: bool = True
 
     def __post_init__(self):
         self.update_rule = str(self.update_rule)
@@ -91,6 +99,12 @@ class RunConfig:
         self.input_dir = self.input_dir if self.input_dir.endswith("/") else self.input_dir + "/"
         if self.tie_break not in ("permute", "worker"):
             raise ValueError("tie_break must be permute or worker")
+        if self.delay_mode == "worker":  # shorthand: the reference's Exp delays, slept on the worker rank
+            self.delay_mode, self.delay_on = "exp", "worker"
+        if self.delay_on not in ("collector", "worker"):
+            raise ValueError("delay_on must be collector or worker")
+        if any(int(f) < 1 for f in self.slow_ranks.values()):
+            raise ValueError("slow rank factors must be integers >= 1")
 
     @property
     def tie_seed_value(self) -> int:

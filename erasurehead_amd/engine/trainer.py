@@ -46,7 +46,7 @@ from ..ops.precision import get_precision
 from ..ops.update import combine_update
 from ..parallel.collector import ArrivalCollector
 from ..parallel.dist import DistEnv
-from ..parallel.placement import make_shards, place_units, place_workers_shared
+from ..parallel.placement import make_shards, place_spread, place_units
 
 # Cost of a replica's message rows whose HBM reads a co-located replica already streams, relative
 # to a distinct row (dense fp64 on MI355X with the LDS-staged bundles: (1.56 - 1.29) ms for 14 GB
@@ -151,10 +151,10 @@ class Trainer:
             mode = cfg.delay_mode if cfg.delay_mode in ("exp", "fixed") else "none"
         self.delay = DelayModel(W, mode, cfg.delay_mean, [w - 1 for w in cfg.fixed_stragglers], cfg.fixed_sleep,
                                 [w - 1 for w in cfg.kill_workers])
-        # placement: sharing-aware on GPUs (co-located replicas share HBM reads).  The placed units
-        # are whole messages, or with partition sharding (default for multi-rank runs) one shard
-        # per (message, partition): each partition's replicas then live on one rank
-        # (parallel/placement.py).
+        # placement (parallel/placement.py): whole messages dealt round-robin over the ranks (the
+        # default: the reference's one-worker-per-process topology, a slow GPU erases only its own
+        # workers), or with partition shards (benchmark opt-in) one shard per (message, partition)
+        # placed sharing-aware: each partition's replicas live on one rank and stream once.
         rows = scheme.rows_per_partition
         sparse = source.is_sparse if source is not None else bool(cfg.is_real)
         if cfg.share_partitions:
@@ -163,19 +163,25 @@ class Trainer:
             replica_weight = REPLICA_WEIGHT_DENSE
         else:
             replica_weight = 1.0
-        self.shard_mode = cfg.shard if cfg.shard != "auto" else ("partition" if env.world > 1 else "message")
+        self.shard_mode = cfg.shard if cfg.shard != "auto" else "message"
         self.shards = make_shards(scheme.messages, self.shard_mode)
         parts = [[(p, rows) for p, _ in u.segments] for u in self.shards]
         if self.shard_mode == "partition":
             self.owner = place_units(parts, env.world, replica_weight)
         else:
-            self.owner = place_workers_shared(parts, env.world, replica_weight)
+            self.owner = place_spread([u.worker for u in self.shards], env.world)
         self.by_rank = {r: sorted({u.worker for u, o in zip(self.shards, self.owner) if o == r})
                         for r in range(env.world)}
         self.local_msgs = [u for u, o in zip(self.shards, self.owner) if o == env.rank]
         self.remote_msgs = {r: [u for u, o in zip(self.shards, self.owner) if o == r]
                             for r in range(1, env.world)} if env.is_master else {}
         self.n_shards = {(u.worker, u.part): u.n_shards for u in self.shards}
+        # physically late worker ranks (--delay-on worker): a worker rank sleeps / spins after its
+        # compute and before its send; the master's collector then sees real arrival times for
+        # remote messages (virtual delay 0; dead workers stay virtual erasures) and keeps the
+        # virtual per-worker delay only for the logical workers co-located with it on rank 0
+        self.physical = cfg.delay_on == "worker" and env.world > 1 and self.delay.mode != "none"
+        self.repeat = int(cfg.slow_ranks.get(env.rank, 1))  # --slow-ranks: gradient launches per round
 
     def _setup_data(self, source: Optional[DataSource]):
         cfg, sch = self.cfg, self.scheme
@@ -250,6 +256,13 @@ class Trainer:
             self.loc_ev = [torch.cuda.Event() for _ in range(self.K)]
             if env.is_master:
                 self.upd_ev = torch.cuda.Event()
+
+    def preflight(self, iters: int = 1000) -> Optional[List[dict]]:
+        """Collective: per-pair put -> flag round trips over the IPC mailbox (IpcTransport.preflight);
+        None when there is no IPC transport."""
+        if self.tx is None or not hasattr(self.tx, "preflight"):
+            return None
+        return self.tx.preflight(iters)
 
     @property
     def transport(self) -> str:
@@ -359,6 +372,7 @@ class Trainer:
         arrivals_log: List = [[] for _ in range(start)]
         upd_events: List = []
         delay_table = np.stack([self.delay.delays(i) for i in range(R)]) if R else np.zeros((0, W))
+        remote_table = self._remote_delays(delay_table)
         views: Dict[Tuple[int, int, int], torch.Tensor] = {}  # (slot, worker, part) -> message row
         if start:
             timeset[:start] = self._restored["timeset"]
@@ -384,7 +398,8 @@ class Trainer:
                 self._send_beta(i)
             with self.timer.phase("local_grad"):
                 if self.local_msgs:
-                    self.plan.run(self.beta_in[i], self.G[slot])
+                    for _ in range(self.repeat):  # --slow-ranks: a slower GPU
+                        self.plan.run(self.beta_in[i], self.G[slot])
                     if env.gpu:
                         ev = self.loc_ev[slot]
                         ev.record(self.cs)
@@ -395,7 +410,7 @@ class Trainer:
                         for m in self.local_msgs:
                             col.add_work(m.worker, m.part, i, None, delays[m.worker], t_seen=t_done)
             with self.timer.phase("post_recv"):
-                self._post_recvs(i, slot, col, delays)
+                self._post_recvs(i, slot, col, remote_table[i])
             with self.timer.phase("wait_k"):
                 arrivals, ok = col.wait(cfg.round_timeout)
             if not ok:
@@ -524,9 +539,11 @@ class Trainer:
             pump.set_local(self.plan.native_launcher(), self.G, [(m.worker, m.part) for m in self.local_msgs])
         tx = self.tx
         if tx is not None:
-            rem = [(m.worker, m.part, self.rem_slot[(m.worker, m.part, m.shard)], tx.flags.host_addr(env.world + r))
+            rem = [(m.worker, m.part, self.rem_slot[(m.worker, m.part, m.shard)], tx.flags.host_addr(env.world + r), r)
                    for r in sorted(self.remote_msgs) for m in self.remote_msgs[r]]
             pump.set_remote(self.Rbuf, rem)
+            # every message / beta carries a (round, rank, checksum) tag that the receiver checks
+            pump.set_integrity(tx.mbox_tags_addr(), tx.inbox_tag_off, bool(cfg.integrity))
             pump.set_puts([(tx.inbox_remote[r].data_ptr(), tx.flags.dev_addr(r)) for r in range(1, env.world)],
                           tx.counters)
             srcs = [(tx.flags.host_addr(env.world + r), tx.flags.dev_addr(env.world + r))
@@ -540,6 +557,9 @@ class Trainer:
         pump.set_schedule([c[0] for c in co], [c[1] for c in co], [c[2] for c in co], [c[3] for c in co],
                           co[0][4] if co else 0, [float(x) for x in delay_table.ravel()], self.rule_kind,
                           self.rule_k, bool(self.drain))
+        if self.physical:  # remote messages are really late: the collector applies no virtual delay to them
+            pump.set_remote_delays([float(x) for x in self._remote_delays(delay_table).ravel()])
+        pump.set_repeat(self.repeat)
         pump.set_decode(sch.decode_kind, list(sch.group_of), sch.n_groups)
         pump.set_timing(bool(cfg.instrument))
         table_decoded = sch.decode_kind in (3, 4)
@@ -569,12 +589,16 @@ class Trainer:
                 pump.run_device(a, b, deadline)
             if timed_start is not None:
                 t_timed1 = self._timed_fence()
-            for i, (status, arr, tdec, tend) in zip(range(start, R), pump.device_log(start, R)):
+            for i, (status, arr, tdec, tend, detail, tstop) in zip(range(start, R), pump.device_log(start, R)):
                 if status:
                     why = {1: f"a worker rank's message did not arrive within {deadline:.0f} s",
                            2: "the arrivals could not be decoded on the device",
-                           3: "an earlier round failed"}.get(status, f"status {status}")
+                           3: "an earlier round failed"}.get(status, detail or f"status {status}")
                     raise RuntimeError(f"device-driven round {i}: {why}")
+                if tstop >= 0:  # arbiter ticks: poll until the stop rule, combine + checks, drain + release
+                    self.timer.add("arbiter_poll", tstop)
+                    self.timer.add("arbiter_update", tdec - tstop)
+                    self.timer.add("arbiter_release", tend - tdec)
                 arrivals = [Arrival(w, p, t) for (w, p, t) in arr]
                 timeset[i], loop_time[i] = tdec, tend
                 worker_timeset[i] = sch.worker_times(arrivals)
@@ -649,6 +673,7 @@ class Trainer:
             t_timed1 = self._timed_fence()
         col.drain(R - 1, max(cfg.round_timeout, 60.0))
         upd = pump.update_ms()
+        pump.check_integrity()  # the last rounds' combines (update_ms synchronised the stream)
         if not device_mode and not arb_mode:
             timeset[start:] += 1e-3 * np.asarray(upd[start:])
         a0 = timed_start if timed_start is not None else start
@@ -726,11 +751,17 @@ class Trainer:
         dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
         w = env.world
         dwait = self._device_waits(tx)
+        # a worker waits for beta longer than the master's worst round (stop rule + drain, each up to
+        # round_timeout), so only a master that is really gone makes it give up
         pump = C.WorkerPump(self.plan.native_launcher(), tx.inbox, self.G, self.n_loc, tx.rremote.ptr,
                             tx.mbox_rows, tx.my_row0, tx.flags.host_addr(env.rank), tx.flags.dev_addr(w + env.rank),
-                            tx.counters, K, dev, float(cfg.round_timeout),
+                            tx.counters, K, dev, 2.5 * float(cfg.round_timeout) + 5.0,
                             tx.flags.dev_addr(env.rank) if dwait else 0)
         pump.set_timing(bool(cfg.instrument))
+        pump.set_integrity(tx.mbox_tags_addr(), tx.inbox_tags_addr(), env.rank, bool(cfg.integrity))
+        pump.set_repeat(self.repeat)
+        if self.physical:
+            pump.set_delays(self._rank_delays())
         self.rank_stats["fused_put"] = bool(pump.fused_put)
         self.rank_stats["device_wait"] = bool(pump.device_wait)
         cut = timed_start if timed_start is not None and start <= timed_start < R else None
@@ -768,6 +799,20 @@ class Trainer:
                     raise RuntimeError(f"beta race detected: rank {r} round {i}: master {want[i]!r}, worker "
                                        f"before/after gradient {sums[i, 0]!r}/{sums[i, 1]!r}")
 
+    def _remote_delays(self, delay_table: np.ndarray) -> np.ndarray:
+        """Virtual delays the master's collector applies to REMOTE messages: the injected ones, or
+        with physically late worker ranks (--delay-on worker) none but the dead workers'."""
+        if not self.physical:
+            return delay_table
+        return np.where(np.isinf(delay_table), np.inf, 0.0)
+
+    def _rank_delays(self) -> List[float]:
+        """Worker rank: seconds it is physically late in every round (0 unless --delay-on worker)."""
+        R = self.cfg.num_itrs
+        if not self.physical:
+            return [0.0] * R
+        return [self.delay.rank_delay(i, self.by_rank[self.env.rank]) for i in range(R)]
+
     def _send_beta(self, i: int):
         if self.tx is not None:
             self.tx.send_beta(i, self.beta_in[i])
@@ -779,6 +824,7 @@ class Trainer:
     def _worker_loop(self, timed_start, start: int = 0) -> None:
         cfg, env, tx = self.cfg, self.env, self.tx
         R, K, n = cfg.num_itrs, self.K, self.n_loc
+        late = self._rank_delays()
         t0 = None
         bsum = torch.full((R, 2), float("nan"), dtype=torch.float64, device=env.device) if cfg.verify_beta else None
         for i in range(start, R):
@@ -791,7 +837,11 @@ class Trainer:
                 bsum[i, 0] = b.double().sum()
             if n:
                 with self.timer.phase("local_grad"):
-                    self.plan.run(b, self.G[slot])
+                    for _ in range(self.repeat):  # --slow-ranks: a slower GPU
+                        self.plan.run(b, self.G[slot])
+                if late[i] > 0:  # --delay-on worker: after compute, before the send (ref src/naive.py:141-148)
+                    self._sync()
+                    time.sleep(late[i])
                 with self.timer.phase("send_msgs"):
                     tx.send_msgs(i, self.G[slot, :n])
             if bsum is not None:  # beta must be unchanged after the gradient read it

@@ -11,14 +11,23 @@ short last group).  `place_workers_shared` refines it for GPUs, where workers th
 same partitions share HBM reads (LDS-staged bundles / interleaved dispatch), so keeping an FRC group or
 cyclic neighbours together costs less than their message rows suggest.
 
-Partition shards (multi-rank runs): a logical message (worker, part) reads s+1 partitions.
-Placing whole messages caps strong scaling — at W = 8 on 8 GPUs every GPU still streams its
-worker's 3 partitions per round.  ``make_shards(messages, "partition")`` splits every message
-into one shard per partition; ``place_units`` then keeps the shards of one partition (all its
-replicas) together, so each GPU streams its partitions once and computes every replica's
-segment gradient from those rows (no replica's work is skipped).  The master sums a message's
-shards with the decode coefficient, and the collector counts the message as arrived when its
-last shard is ready (csrc/runtime/collector.h).
+Two placements of multi-rank runs, a deliberate trade-off:
+
+* ``message`` (default for training): whole messages dealt round-robin over the ranks
+  (``place_spread``), the reference's one-worker-per-process topology.  A slow or dead GPU
+  erases only its own workers' messages, which the gradient code tolerates.
+* ``partition`` (benchmark opt-in): a logical message (worker, part) reads s+1 partitions.
+  Placing whole messages caps strong scaling — at W = 8 on 8 GPUs every GPU still streams its
+  worker's 3 partitions per round.  ``make_shards(messages, "partition")`` splits every message
+  into one shard per partition; ``place_units`` then keeps the shards of one partition (all its
+  replicas) together, so each GPU streams its partitions once and computes every replica's
+  segment gradient from those rows (no replica's work is skipped).  The master sums a message's
+  shards with the decode coefficient, and the collector counts the message as arrived when its
+  last shard is ready (csrc/runtime/collector.h).  The price: every replica of a partition now
+  lives on ONE rank, so a physically slow GPU delays every message that has a shard there (at
+  N = 8, most of them) and the code's redundancy protects nothing physical.  The injected
+  straggler model is unaffected when it is virtual (--delay-on collector), not when a rank is
+  really late (--delay-on worker, --slow-ranks).
 """
 from __future__ import annotations
 
@@ -48,6 +57,23 @@ def make_shards(messages, mode: str = "message") -> List[Shard]:
         else:
             raise ValueError(f"unknown shard mode {mode!r}")
     return out
+
+
+def place_spread(workers: Sequence[int], world: int) -> List[int]:
+    """owner[u] = worker(u) mod world: the reference topology compressed onto `world` ranks.
+
+    The reference runs every logical worker in its own process (worker w on MPI rank w+1, ref
+    src/approximate_coding.py:47-53, run_approx_coding.sh:47-49), so a slow or dead machine
+    erases exactly one worker's message and the gradient code's redundancy covers it.  Dealing
+    workers round-robin keeps that property on fewer GPUs: the members of an FRC group and cyclic
+    neighbours (consecutive worker ids) land on different ranks whenever world >= s + 1, so one
+    slow GPU delays at most ceil(W / world) workers, never all replicas of a partition.  This is
+    the default placement of multi-rank training runs; partition shards (place_units) trade that
+    tolerance for bandwidth and are a benchmark opt-in.
+    """
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    return [int(w) % world for w in workers]
 
 
 def place_units(parts: Sequence[Sequence[Tuple[int, int]]], world: int, replica_weight: float) -> List[int]:

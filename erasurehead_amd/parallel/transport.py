@@ -28,9 +28,11 @@ import time
 import uuid
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
+TAG_BYTES = 16  # csrc/kernels/integrity.h MsgTag
 TAG_STRIDE = 1024  # gloo tags: beta of round i = 2*i*S, message j of round i = 2*(i*S+j)+1
 
 
@@ -242,10 +244,12 @@ class IpcTransport(Transport):
                 err.append(f"rank {env.rank}: {type(e).__name__}: {e}")
                 return None
 
-        ibytes = (self.R + 1) * self.ld * self.es
+        # every region ends with 16-byte integrity tags, one per payload row (csrc/kernels/integrity.h)
+        self.inbox_tag_off = (self.R + 1) * self.ld * self.es
+        ibytes = self.inbox_tag_off + (self.R + 1) * TAG_BYTES
         if env.is_master:
             name = "/eh_" + uuid.uuid4().hex[:16]
-            rbytes = max(1, self.K * max(1, self.n_rem) * self.ld * self.es)
+            rbytes = self.K * max(1, self.n_rem) * (self.ld * self.es + TAG_BYTES)
 
             def _mk():
                 self.flags = C.ShmFlags(name, 2 * env.world + 1, True)
@@ -275,6 +279,7 @@ class IpcTransport(Transport):
         row0, n_rem = env.broadcast_object((self.row0, self.n_rem), 0)
         self.my_row0 = row0.get(env.rank, 0)
         self.mbox_rows = max(1, n_rem)  # rows per slot of the master's mailbox ring
+        self.mbox_tag_off = self.K * self.mbox_rows * self.ld * self.es  # tags [K][mbox_rows] after the rows
         if env.is_master:
             self.inbox_remote = {}
 
@@ -330,6 +335,15 @@ class IpcTransport(Transport):
                                      f"master->rank {x['master_to_rank']}, rank->master {x['rank_to_master']}"
                                      for x in bad))
         return pairs
+
+    def mbox_tags_addr(self) -> int:
+        """Device address (in this process) of the master mailbox's tag slots [K][mbox_rows]."""
+        reg = self.rreg if self.env.is_master else self.rremote
+        return reg.ptr + self.mbox_tag_off
+
+    def inbox_tags_addr(self) -> int:
+        """Worker: device address of its own inbox's tag slots [R + 1]."""
+        return self.inbox_reg.ptr + self.inbox_tag_off
 
     def make_rbuf(self):
         if not self.env.is_master:
@@ -400,6 +414,76 @@ class IpcTransport(Transport):
             rbuf.zero_()
             torch.cuda.synchronize(env.device)
         env.barrier()
+
+    # ---- per-pair preflight (bench.py --gpus N > 1: the first real multi-GPU run checks itself) --
+    def preflight(self, iters: int = 1000, timeout: float = 30.0) -> Optional[List[dict]]:
+        """Collective.  ``iters`` put -> flag round trips between the master and every worker rank
+        over the real put+signal path: the master pushes pattern k into each worker's spare inbox
+        row (counter k), each worker checks the payload it sees once the counter reads k and
+        echoes it into the master's mailbox (its counter k), and the master checks the echo.
+        Returns (on every rank) one record per worker rank: round-trip percentiles, payload
+        errors in each direction and the peer-access facts of the pair.  Flags are reset to 0."""
+        env, C, w, R = self.env, self.C, self.env.world, self.R
+        pat = torch.arange(self.ld, dtype=self.dtype, device=env.device)
+        mine: Dict[str, object] = {}
+        if env.is_master:
+            rbuf = self.make_rbuf()
+            rtt = {r: [] for r in range(1, w)}
+            bad_echo = {r: 0 for r in range(1, w)}
+            for k in range(1, iters + 1):
+                cur = pat + k
+                puts = [(cur, self.inbox_remote[r][R], self.flags.dev_addr(r), k) for r in range(1, w)]
+                t0 = time.perf_counter()
+                for j in range(0, len(puts), 16):
+                    self.C.put_signal(puts[j:j + 16], self.counters[16 * (j // 16):])
+                for r in range(1, w):
+                    if not self.flags.wait_ge(w + r, k, timeout):
+                        raise TransportError(f"preflight: rank {r} -> rank 0: no echo of put {k} within {timeout:.0f}s")
+                    rtt[r].append(time.perf_counter() - t0)
+                for r in range(1, w):
+                    if self.remote_counts.get(r, 0) and not bool(torch.equal(rbuf[0, self.row0[r]], cur)):
+                        bad_echo[r] += 1
+            mine = {"rtt": rtt, "bad_echo": bad_echo}
+        else:
+            r = env.rank
+            bad = 0
+            for k in range(1, iters + 1):
+                if not self.flags.wait_ge(r, k, timeout):
+                    raise TransportError(f"preflight: rank 0 -> rank {r}: put {k} never signalled within {timeout:.0f}s")
+                got = self.inbox[R]
+                if not bool(torch.equal(got, pat + k)):
+                    bad += 1
+                if self.n_local:
+                    dst = self.rremote.view(self.dname, [self.ld], self.my_row0 * self.ld * self.es)
+                    self.C.put_signal([(got, dst, self.flags.dev_addr(w + r), k)], self.counters)
+                else:
+                    self.C.signal(self.flags.dev_addr(w + r), k, self.dev)
+            torch.cuda.synchronize(env.device)
+            mine = {"bad": bad}
+        got = env.gather_objects(mine)
+        env.barrier()
+        out = None
+        if env.is_master:
+            for r in range(1, w):
+                self.flags.store(r, 0)
+                self.flags.store(w + r, 0)
+            self.make_rbuf().zero_()
+            torch.cuda.synchronize(env.device)
+            out = []
+            for p in self.pairs:
+                r = p["rank"]
+                us = np.sort(1e6 * np.asarray(got[0]["rtt"][r]))
+                out.append({"rank": r, "iters": iters, "same_gpu": p["same_gpu"],
+                            "master_to_rank_peer": p["master_to_rank"], "rank_to_master_peer": p["rank_to_master"],
+                            "mailbox": "fine-grained device memory, host-registered counters" if self.FINE else "coarse",
+                            "rtt_us_p50": round(float(us[len(us) // 2]), 2),
+                            "rtt_us_p99": round(float(us[min(len(us) - 1, int(0.99 * len(us)))]), 2),
+                            "rtt_us_max": round(float(us[-1]), 2),
+                            "payload_errors_master_to_rank": int(got[r]["bad"]),
+                            "payload_errors_rank_to_master": int(got[0]["bad_echo"][r])})
+        out = env.broadcast_object(out, 0)
+        env.barrier()
+        return out
 
     # ---- master ------------------------------------------------------------------------
     def send_beta(self, i, beta):

@@ -45,6 +45,31 @@ class DelayModel:
             d[w] = math.inf
         return d
 
+    # ---- physically late worker ranks (--delay-on worker) -------------------------------------
+    # A worker rank is one process on one GPU: it sends all of its messages together, after
+    # compute, so it is late by the LARGEST delay among the logical workers it hosts (with one
+    # logical worker per rank, --shard message with ranks = workers, this is exactly the
+    # reference's per-worker sleep).  Dead workers (inf) stay virtual erasures on the master.
+    # The master's own co-located workers keep their per-worker delay on the collector's clock.
+    def rank_delay(self, i: int, workers) -> float:
+        """Seconds worker rank hosting `workers` (logical worker ids) sleeps in round i."""
+        d = self.delays(i)
+        vals = [float(d[w]) for w in workers if math.isfinite(d[w])]
+        return max(vals) if vals else 0.0
+
+    def equivalent(self, i: int, hosts) -> np.ndarray:
+        """Per-worker delay of round i that the virtual collector model needs to reproduce the
+        physical schedule: hosts = {rank: logical workers with messages (or shards) on it}.  A
+        worker's message is complete when its last shard lands, i.e. at the max over its ranks."""
+        d = self.delays(i)
+        out = np.zeros_like(d)
+        for r, ws in hosts.items():
+            dr = self.rank_delay(i, ws) if r != 0 else None
+            for w in ws:
+                v = d[w] if (r == 0 or not math.isfinite(d[w])) else dr
+                out[w] = max(out[w], v)
+        return out
+
 
 def delay_floor(n_workers: int, rounds: int, stop_count=None, groups=None, k=None, mean=0.5,
                 carry: bool = False) -> float:

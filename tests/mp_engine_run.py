@@ -6,6 +6,7 @@ with the ranks' transport (ranks sharing one GPU -> IPC mailboxes) and writes, o
 the betaset, beta0 and per-round arrival lists so the test can replay them with the fp64
 NumPy oracle.
 """
+import json
 import os
 import sys
 
@@ -32,12 +33,20 @@ def main():
     if delay:
         cfg.add_delay = 1
         cfg.force_delay = True
+    if os.environ.get("EH_TEST_DRAIN"):
+        cfg.drain = os.environ["EH_TEST_DRAIN"]
+    if os.environ.get("EH_TEST_SHARD"):
+        cfg.shard = os.environ["EH_TEST_SHARD"]
+    if os.environ.get("EH_TEST_NO_INTEGRITY"):
+        cfg.integrity = False
     tr = Trainer(cfg, env, src, scheme=sch)
+    pf = tr.preflight(int(os.environ["EH_TEST_PREFLIGHT"])) if os.environ.get("EH_TEST_PREFLIGHT") else None
     res = tr.run()
     if env.is_master:
         arr = np.array([[(w, p) for (w, p, _) in a] for a in res.arrivals], dtype=object)
         np.savez(out, betaset=res.betaset, beta0=tr.beta0, arrivals=arr, transport=np.array(tr.transport),
-                 timeset=res.timeset, round_loop=np.array(tr.device_loop or "host"))
+                 timeset=res.timeset, round_loop=np.array(tr.device_loop or "host"),
+                 preflight=np.array(json.dumps(pf)), rank_report=np.array(json.dumps(tr.rank_report())))
     env.barrier()
     tr.close()
     env.shutdown()

@@ -24,12 +24,17 @@ def _port():
     return p
 
 
-def _launch(world, case_i, rule, out, delay=0.0, **extra_env):
+def _launch_raw(world, case_i, rule, extra_env, delay=0.0, timeout=600):
+    """torchrun `world` ranks of mp_engine_run.py; returns the CompletedProcess (out path: EH_TEST_OUT)."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", **extra_env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(HERE, "mp_engine_run.py"),
-           out, str(case_i), rule, str(delay)]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+           env.get("EH_TEST_OUT", os.devnull), str(case_i), rule, str(delay)]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def _launch(world, case_i, rule, out, delay=0.0, **extra_env):
+    r = _launch_raw(world, case_i, rule, dict(extra_env, EH_TEST_OUT=out), delay)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return np.load(out, allow_pickle=True)  # our own file (contains the arrival lists)
 
@@ -79,16 +84,21 @@ def test_ipc_worker_wait_and_put_modes(wait, fused, tmp_path):
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
 
 
-@pytest.mark.parametrize("world,case_i,wait", [(2, 2, "device"), (3, 4, "host"), (3, 5, "device"), (3, 0, "device"), (8, 5, "device")])
-def test_device_arbiter_rounds(world, case_i, wait, tmp_path):
+@pytest.mark.parametrize("world,case_i,wait,drain", [(2, 2, "device", ""), (3, 4, "host", ""), (3, 5, "device", ""),
+                                                     (3, 0, "device", ""), (8, 5, "device", ""),
+                                                     (3, 1, "device", "all"), (3, 6, "device", "all"),
+                                                     (3, 7, "host", "all")])
+def test_device_arbiter_rounds(world, case_i, wait, drain, tmp_path):
     """Multi-rank rounds driven by the arbiter kernel (csrc/kernels/arbiter.hip: the master GPU polls the
     workers' counters, applies the stop rule, decodes, updates and releases the next beta): the
-    trajectory replays exactly from the arrivals it logged (FRC, AGC, uneven AGC groups, naive)."""
+    trajectory replays exactly from the arrivals it logged (FRC, AGC, uneven AGC groups, naive; and
+    with a drain, the cyclic-MDS decode table, partial replication and partial coded)."""
     from oracle import replay
     from test_engine_cpu import CASES, make
 
+    extra = {"EH_TEST_DRAIN": drain} if drain else {}
     r = _launch(world, case_i, "AGD", str(tmp_path / "a.npz"), ERASUREHEAD_DEVICE_MASTER="on",
-                ERASUREHEAD_WORKER_WAIT=wait, EH_TEST_ROUND_TIMEOUT="20")
+                ERASUREHEAD_WORKER_WAIT=wait, EH_TEST_ROUND_TIMEOUT="20", **extra)
     assert str(r["transport"]) == "ipc" and str(r["round_loop"]) == "arbiter"
     cfg, src, sch, parts = make(CASES[case_i], "AGD")
     arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
