@@ -59,12 +59,25 @@ def parse(argv=None):
     ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32", "bf16"])
     ap.add_argument("--update-rule", default="AGD")
     ap.add_argument("--add-delay", type=int, default=0)
+    ap.add_argument("--delay-mode", default="exp", choices=["exp", "fixed", "none"])
+    ap.add_argument("--delay-mean", type=float, default=0.5)
+    ap.add_argument("--fixed-stragglers", type=int, nargs="*", default=[])
+    ap.add_argument("--fixed-sleep", type=float, default=0.5)
+    ap.add_argument("--delay-on", default="collector", choices=["collector", "worker"],
+                    help="injected delays as virtual arrival times or physically late worker ranks")
+    ap.add_argument("--slow-ranks", nargs="*", default=[], metavar="RANK:FACTOR",
+                    help="physically slow GPUs: the rank runs its gradient FACTOR times per round")
+    ap.add_argument("--shard", default="partition", choices=["partition", "message"],
+                    help="N > 1 placement: partition shards (default here: fastest, but a physically slow "
+                         "GPU delays every message with a shard on it) or whole messages round-robin "
+                         "(the reference topology and the training default: a slow GPU erases its own workers)")
+    ap.add_argument("--no-integrity", action="store_true", help="untagged IPC messages (A/B of the tag cost)")
     ap.add_argument("--no-floor", action="store_true", help="skip the 100-round convergence runs")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the instrumented host-driven run")
     ap.add_argument("--floor-rounds", type=int, default=100)
     ap.add_argument("--tasks", type=int, default=0)
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl"])
+    ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl", "loopback"])
     ap.add_argument("--round-timeout", type=float, default=120.0, help="bounds any hang (a round takes ms)")
     ap.add_argument("--device-loop", default="auto", choices=["auto", "graph", "stream", "off"])
     ap.add_argument("--tie-break", default="permute", choices=["permute", "worker"])
@@ -88,6 +101,8 @@ def relaunch(gpus: int, argv, script: str = None) -> int:
            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", script or os.path.abspath(__file__), *argv]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if int(env.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:  # erasurehead_amd/__init__.py: per-peer p2p streams
+        env["GPU_MAX_HW_QUEUES"] = "16"
     print(f"[bench] launching {gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
     return subprocess.call(cmd, env=env)
 
@@ -105,6 +120,7 @@ def main(argv=None) -> int:
 
     import torch
 
+    from erasurehead_amd.cli import parse_slow_ranks
     from erasurehead_amd.codes.schemes import Arrival
     from erasurehead_amd.config import RunConfig
     from erasurehead_amd.engine import Trainer, evaluate
@@ -120,7 +136,9 @@ def main(argv=None) -> int:
                          allow_uneven_groups=True, verbose=False, tasks=a.tasks,
                          transport=a.transport, round_timeout=a.round_timeout,
                          share_partitions=a.share_partitions, device_loop=kw.pop("device_loop", a.device_loop),
-                         tie_break=a.tie_break, **kw)
+                         tie_break=a.tie_break, shard=a.shard, delay_mode=a.delay_mode, delay_mean=a.delay_mean,
+                         fixed_stragglers=a.fixed_stragglers, fixed_sleep=a.fixed_sleep, delay_on=a.delay_on,
+                         slow_ranks=parse_slow_ranks(a.slow_ranks), integrity=not a.no_integrity, **kw)
 
     def free(tr):
         tr.close()
@@ -185,7 +203,15 @@ def main(argv=None) -> int:
                                    for u, o in zip(trainer.shards, trainer.owner) if o == r]
                           for r in range(env.world)},
             "shard": trainer.shard_mode,
+            # what a physically slow GPU does to the stop rule under this placement (parallel/placement.py)
+            "straggler_tolerance": ("per worker rank: a slow GPU erases only its own workers' messages"
+                                    if trainer.shard_mode == "message" or env.world == 1 else
+                                    "none across ranks: every replica of a partition is on one rank, a slow GPU "
+                                    "delays every message with a shard there (virtual delays unaffected)"),
         }
+        if a.delay_on == "worker" or a.slow_ranks:
+            out["config"]["delay_on"] = a.delay_on
+            out["config"]["slow_ranks"] = parse_slow_ranks(a.slow_ranks)
         if preflight is not None:
             out["peer_preflight"] = preflight
         if n_gpu_dev and env.world > n_gpu_dev:
@@ -217,10 +243,15 @@ def main(argv=None) -> int:
 
     # ---- 2. the same rounds host-driven, instrumented: real wait-for-k path + per-rank breakdown -----
     if not a.no_breakdown:
+        headline = reports
         tr = Trainer(make_cfg(a.warmup + a.steps, device_loop="off", instrument=True), env)
         r = tr.run(timed_start=a.warmup)
         t = env.allreduce_max(r.timed_seconds if env.is_master else tr.worker_timed_seconds)
         reports = env.gather_objects(tr.rank_report())
+        if env.is_master:  # the headline run's device-side master ticks (arbiter: poll / update / release)
+            for rep, h in zip(reports, headline):
+                rep.update({f"headline_{k}": v for k, v in h.items()
+                            if k.startswith("arbiter_") or k in ("device_round_us", "round_loop")})
         if env.is_master:
             out["host_driven_ms_per_step"] = 1e3 * t / a.steps
             out["host_driven_instrumented"] = True

@@ -48,10 +48,29 @@ __host__ __device__ inline unsigned long long tag_term(unsigned long long bits, 
 }
 
 #if defined(__HIPCC__)
+// Full-wave u64 sum in VALU cross-lane moves only (DPP quad_perm xor 1 / xor 2, row_half_mirror,
+// row_mirror, then gfx950's permlane16 / permlane32 swaps; the same lane pairing as
+// common.h wave_allreduce_sum): no LDS crossbar round trips, every lane ends with the total.
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<unsigned>(v)), CTRL, 0xf, 0xf, true));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<unsigned>(v >> 32)), CTRL, 0xf, 0xf, true));
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+template <bool ROW16>
+__device__ __forceinline__ unsigned long long swap_sum_u64(unsigned long long v) {
+  const unsigned l = static_cast<unsigned>(v), h = static_cast<unsigned>(v >> 32);
+  const auto lo = ROW16 ? __builtin_amdgcn_permlane16_swap(l, l, false, false) : __builtin_amdgcn_permlane32_swap(l, l, false, false);
+  const auto hi = ROW16 ? __builtin_amdgcn_permlane16_swap(h, h, false, false) : __builtin_amdgcn_permlane32_swap(h, h, false, false);
+  return ((static_cast<unsigned long long>(hi[0]) << 32) | lo[0]) + ((static_cast<unsigned long long>(hi[1]) << 32) | lo[1]);
+}
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return v;
+  v += dpp_u64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_u64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_u64<0x141>(v);  // row_half_mirror
+  v += dpp_u64<0x140>(v);  // row_mirror
+  v = swap_sum_u64<true>(v);
+  return swap_sum_u64<false>(v);
 }
 
 // Sum over the block of one u64 per thread (every thread must call it; result valid in thread 0).

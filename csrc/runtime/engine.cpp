@@ -49,6 +49,7 @@
 #include "kernels/arbiter.h"
 #include "kernels/launchers.h"
 #include "runtime/collector.h"
+#include "runtime/comm.h"
 
 namespace {
 
@@ -365,6 +366,13 @@ class MasterPump {
     for (auto& t : tev_)
       for (auto e : t)
         if (e) hipEventDestroy(e);
+    // per-peer comm streams: destroyed without a sync (a receive from a dead peer may never end;
+    // the transport aborts its communicator at close)
+    for (auto e : rev_)
+      if (e) hipEventDestroy(e);
+    if (bev_) hipEventDestroy(bev_);
+    for (auto& [r, st] : send_st_) hipStreamDestroy(st);
+    for (auto& [r, st] : recv_st_) hipStreamDestroy(st);
   }
 
   // Per-round HIP-event timing of the beta puts and the local gradient launch (bench.py's
@@ -444,13 +452,37 @@ class MasterPump {
     for (const auto& [w, p, row, addr, rank] : msgs) {
       check_wp(w, p);
       need(row >= 0 && row < r_rows_, "mailbox row out of range");
-      need(addr != 0, "null flag address");
+      need(addr != 0 || comm_, "null flag address");
       need(rank > 0 && rank < 256, "sender rank out of range");
       remote_.push_back({w, p, row, addr});
       row_rank_[row] = rank;
       index_[2 * w + p].push_back({1, row});
     }
   }
+
+  // Stream-ordered p2p instead of the IPC mailbox (runtime/comm.h: RCCL, or its single-GPU loopback):
+  // ranks = (worker rank, first mailbox row, rows) of every rank that sends messages; `peers` = every
+  // worker rank (each receives beta).  Call before set_remote.  beta(i) goes out with one send per
+  // peer on that peer's own stream; round i's messages of rank r arrive with one receive into its
+  // mailbox rows on r's receive stream, and the HIP event behind it is the collector's probe.
+  void set_comm(std::shared_ptr<eh::P2PComm> comm, const std::vector<std::tuple<int, int, int>>& ranks,
+                const std::vector<int>& peers) {
+    need(comm != nullptr, "null communicator");
+    arb_ready_ = false;
+    comm_ = std::move(comm);
+    comm_ranks_ = ranks;
+    comm_peers_ = peers;
+    auto mk = [](hipStream_t* st) { hcheck(hipStreamCreateWithFlags(st, hipStreamNonBlocking), "hipStreamCreate"); };
+    for (int r : peers) mk(&send_st_[r]);
+    for (const auto& [r, row0, n] : ranks) {
+      need(n > 0 && row0 >= 0, "bad mailbox rows of a rank");
+      mk(&recv_st_[r]);
+    }
+    rev_.assign(static_cast<size_t>(K_) * ranks.size(), nullptr);
+    for (auto& e : rev_) hcheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    if (!bev_) hcheck(hipEventCreateWithFlags(&bev_, hipEventDisableTiming), "hipEventCreate");
+  }
+  std::string comm_kind() const { return comm_ ? comm_->kind() : "ipc"; }
 
   // Integrity tags (csrc/kernels/integrity.h): mbox_tags = device address of the mailbox's tag
   // slots [K][rows]; inbox_tag_off = bytes from a worker inbox base to its tag slots [R + 1].
@@ -562,6 +594,19 @@ class MasterPump {
       hcheck(hipEventRecord(loc_ev_[slot], stream_), "hipEventRecord");
       for (const auto& m : local_)
         col_->add_event_probe(m.w, m.p, i, reinterpret_cast<uintptr_t>(loc_ev_[slot]), dl[m.w]);
+    }
+    if (comm_) {  // one receive per sending rank into its mailbox rows; the event behind it is the probe
+      char* rb = static_cast<char*>(rbuf_.data_ptr()) + static_cast<int64_t>(slot) * r_rows_ * ld_ * es_;
+      for (size_t k = 0; k < comm_ranks_.size(); ++k) {
+        const auto& [r, row0, n] = comm_ranks_[k];
+        hipStream_t rs = recv_st_.at(r);
+        comm_->recv(r, rb + static_cast<int64_t>(row0) * ld_ * es_, static_cast<int64_t>(n) * ld_ * es_, rs);
+        hipEvent_t ev = rev_[static_cast<size_t>(slot) * comm_ranks_.size() + k];
+        hcheck(hipEventRecord(ev, rs), "hipEventRecord(recv)");
+        for (const auto& m : remote_)
+          if (m.row >= row0 && m.row < row0 + n) col_->add_event_probe(m.w, m.p, i, reinterpret_cast<uintptr_t>(ev), dr[m.w]);
+      }
+      return;
     }
     for (const auto& m : remote_)
       col_->add_flag_probe(m.w, m.p, i, m.flag, static_cast<uint64_t>(i + 1), dr[m.w]);
@@ -728,6 +773,7 @@ class MasterPump {
 
   // Why rounds [a, b) cannot run on the device arbiter ("" = they can).
   std::string device_blocker(int a, int b) const {
+    if (comm_) return "messages travel over " + comm_->kind() + " (the arbiter polls IPC counters)";
     if (remote_.empty() || arb_src_.empty()) return "no remote workers";
     if ((int)arb_src_.size() > eh::kArbMaxSrc) return "more than 64 worker ranks";
     if (W_ > eh::kArbMaxW) return "more than 64 workers";
@@ -920,6 +966,16 @@ class MasterPump {
       a.tag_rank[m] = static_cast<unsigned char>(used[m].row >= 0 ? row_rank_[used[m].row] : 0);
       remote |= used[m].row >= 0;
     }
+    if (comm_ && remote) {  // order the combine after the receives it reads (their events are complete)
+      const int slot = i % K_;
+      for (size_t k = 0; k < comm_ranks_.size(); ++k) {
+        const auto& [r, row0, n] = comm_ranks_[k];
+        bool hit = false;
+        for (const auto& u : used) hit |= u.row >= row0 && u.row < row0 + n;
+        if (hit) hcheck(hipStreamWaitEvent(stream_, rev_[static_cast<size_t>(slot) * comm_ranks_.size() + k], 0),
+                        "hipStreamWaitEvent(recv)");
+      }
+    }
     if (tags_ && remote) {  // check the mailbox rows against their senders' tags (update.hip)
       const int slot = i % K_;
       a.tags = reinterpret_cast<const eh::MsgTag*>(mbox_tags_) + static_cast<int64_t>(slot) * r_rows_;
@@ -1060,6 +1116,17 @@ class MasterPump {
 
   // push beta(j) into every worker inbox (put + signal kernels on the pump stream)
   void put_beta(int j) {
+    if (comm_) {  // one send per worker rank, each on its own stream behind the update that wrote beta(j)
+      const void* src = static_cast<const char*>(beta_in_.data_ptr()) + static_cast<int64_t>(j) * ld_ * es_;
+      if (timing_) record_t(j, 0);
+      hcheck(hipEventRecord(bev_, stream_), "hipEventRecord(beta)");
+      for (int r : comm_peers_) {
+        hcheck(hipStreamWaitEvent(send_st_.at(r), bev_, 0), "hipStreamWaitEvent(beta)");
+        comm_->send(r, src, static_cast<int64_t>(ld_) * es_, send_st_.at(r));
+      }
+      if (timing_) record_t(j, 1);
+      return;
+    }
     if (targets_.empty()) return;
     const void* src = static_cast<const char*>(beta_in_.data_ptr()) + static_cast<int64_t>(j) * ld_ * es_;
     if (timing_) record_t(j, 0);
@@ -1147,6 +1214,12 @@ class MasterPump {
   std::vector<std::pair<uintptr_t, uintptr_t>> targets_;
   std::vector<std::pair<uintptr_t, uintptr_t>> drain_flags_;
   int prepub_ = -1;  // round whose beta is already queued (device-side drain / the arbiter)
+  std::shared_ptr<eh::P2PComm> comm_;                 // stream-ordered p2p (set_comm); null: IPC mailbox
+  std::vector<std::tuple<int, int, int>> comm_ranks_;  // (rank, first mailbox row, rows) of every sender
+  std::vector<int> comm_peers_;                        // every worker rank (beta receivers)
+  std::map<int, hipStream_t> send_st_, recv_st_;       // per-peer streams
+  std::vector<hipEvent_t> rev_;                        // [K][sender] receive-done events (collector probes)
+  hipEvent_t bev_ = nullptr;                           // beta(j) written (the sends wait on it)
   bool tags_ = false;               // integrity tags on (set_integrity)
   uintptr_t mbox_tags_ = 0;         // device address of the mailbox tag slots [K][r_rows]
   int64_t inbox_tag_off_ = 0;       // worker inbox base -> its tag slots
@@ -1214,8 +1287,33 @@ class WorkerPump {
     abort_ = std::make_unique<HostMapped>(sizeof(int));
     csum_ = at::zeros({eh::kMaxTagRows}, at::TensorOptions().dtype(at::kLong).device(at::Device(at::kCUDA, device)));
   }
+  // Stream-ordered p2p worker (runtime/comm.h: RCCL, or its single-GPU loopback): every round is
+  // recv(beta) -> gradient -> [late spin] -> send(messages) on this rank's stream, enqueued one round
+  // ahead of the beta that has landed (the host waits on the event behind the previous receive).
+  WorkerPump(std::shared_ptr<GradLauncher> g, const Tensor& inbox, const Tensor& G, int n_loc,
+             std::shared_ptr<eh::P2PComm> comm, int K, int device, double timeout)
+      : g_(std::move(g)), inbox_(inbox), G_(G), n_(n_loc), mbox_(0), mbox_rows_(0), row0_(0), bflag_(nullptr),
+        mflag_(nullptr), K_(K), timeout_(timeout), comm_(std::move(comm)) {
+    need(comm_ != nullptr, "null communicator");
+    need_gpu(inbox, "inbox");
+    need_gpu(G, "G");
+    need(G.dim() == 3 && G.size(0) == K && G.size(2) == inbox.size(1), "G must be [K, n, ld]");
+    need(acc_code(G) == acc_code(inbox), "G/inbox dtype mismatch");
+    need(n_loc >= 0 && n_loc <= G.size(1), "n_loc out of range");
+    ld_ = (int)inbox.size(1);
+    R_ = (int)inbox.size(0) - 1;
+    device_ = device;
+    es_ = acc_code(G) == 0 ? 8 : 4;
+    g_rows_ = (int)G.size(1);
+    stream_ = c10::hip::getCurrentHIPStream(device).stream();
+    wait_s_.assign(R_, -1.0);
+    for (auto& e : rev_) hcheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    err_ = std::make_unique<HostMapped>(sizeof(eh::IntegrityErr));
+    abort_ = std::make_unique<HostMapped>(sizeof(int));
+  }
   bool fused_put() const { return fuse_put_; }
   bool device_wait() const { return dwait_; }
+  std::string comm_kind() const { return comm_ ? comm_->kind() : "ipc"; }
 
   // --delay-on worker: seconds this rank is physically late in every round.  A device spin
   // (wall_clock64 + s_sleep) between the gradient and the put, so the put really leaves late
@@ -1254,6 +1352,8 @@ class WorkerPump {
     throw std::runtime_error("rank " + std::to_string(rank_) + ": " + integrity_message(*e, true));
   }
   ~WorkerPump() {
+    for (auto e : rev_)
+      if (e) hipEventDestroy(e);
     for (auto& t : tev_)
       for (auto e : t)
         if (e) hipEventDestroy(e);
@@ -1279,6 +1379,7 @@ class WorkerPump {
   // Rounds [a, b).  Returns -1 when every round was issued, else the round whose beta
   // did not arrive within the timeout.
   int run(int a, int b) {
+    if (comm_) return run_comm(a, b);
     py::gil_scoped_release nogil;
     for (int i = a; i < b; ++i) {
       need(i >= 0 && i < R_, "round out of range");
@@ -1342,6 +1443,56 @@ class WorkerPump {
   }
 
  private:
+  int run_comm(int a, int b) {
+    py::gil_scoped_release nogil;
+    const int64_t bbytes = static_cast<int64_t>(ld_) * es_;
+    for (int i = a; i < b; ++i) {
+      need(i >= 0 && i < R_, "round out of range");
+      Range tr("eh.worker.round");
+      if (i > a && !event_wait(rev_[(i - 1) % 2], i - 1)) {  // beta(i-1) never came: the master is gone
+        comm_->abort();
+        return i - 1;
+      }
+      char* beta = static_cast<char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * bbytes;
+      comm_->recv(0, beta, bbytes, stream_);
+      hcheck(hipEventRecord(rev_[i % 2], stream_), "hipEventRecord(beta)");
+      if (n_ == 0) continue;
+      char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(i % K_) * g_rows_ * ld_ * es_;
+      if (timing_) record_t(i, 0);
+      for (int k = 0; k < repeat_; ++k) hcheck(g_->launch(beta, g, stream_), "worker gradient");
+      if (timing_) record_t(i, 1);
+      if (!late_ticks_.empty() && late_ticks_[i] > 0)  // after compute, before the send (ref src/naive.py:141-148)
+        hcheck(eh::spin_launch(late_ticks_[i], stream_), "late worker spin");
+      comm_->send(0, g, static_cast<int64_t>(n_) * ld_ * es_, stream_);
+      if (timing_) record_t(i, 2);
+    }
+    if (b > a && !event_wait(rev_[(b - 1) % 2], b - 1)) {
+      comm_->abort();
+      return b - 1;
+    }
+    return -1;
+  }
+  // Host poll of a receive event (comm mode); records the wait under round `rec`.
+  bool event_wait(hipEvent_t ev, int rec) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (int spin = 0;; ++spin) {
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) hcheck(q, "hipEventQuery(beta)");
+      if (spin < 4096) {
+#if defined(__x86_64__)
+        _mm_pause();
+#endif
+        continue;
+      }
+      if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(5));
+    }
+    wait_s_[rec] = std::chrono::duration<double>(clk::now() - t0).count();
+    return true;
+  }
+
   // Host poll until the beta flag reaches `target`; records the wait under round `rec`.
   bool host_wait(uint64_t target, int rec) {
     using clk = std::chrono::steady_clock;
@@ -1369,6 +1520,10 @@ class WorkerPump {
     return bad;
   }
   void stop_queued() {
+    if (comm_) {
+      comm_->abort();
+      return;
+    }
     __atomic_store_n(static_cast<int*>(abort_->host), 1, __ATOMIC_RELEASE);
     if (dwait_) {
       const uint64_t top = static_cast<uint64_t>(R_) + 1;
@@ -1409,6 +1564,8 @@ class WorkerPump {
   std::vector<long long> late_ticks_;    // [R] device spin before the put (--delay-on worker)
   int repeat_ = 1;                       // gradient launches per round (--slow-ranks)
   int device_ = 0;
+  std::shared_ptr<eh::P2PComm> comm_;    // stream-ordered p2p (null: IPC mailbox)
+  std::array<hipEvent_t, 2> rev_{};      // beta receive-done events of the last two rounds (comm mode)
   std::vector<std::array<hipEvent_t, 3>> tev_;  // [round] gradient start, gradient end = put start, put end
   std::vector<double> wait_s_;                  // [round] host seconds spent waiting for beta
 };
@@ -1458,6 +1615,8 @@ void bind_engine(py::module& m) {
       .def("set_puts", &MasterPump::set_puts)
       .def("set_drain_flags", &MasterPump::set_drain_flags)
       .def("set_remote_delays", &MasterPump::set_remote_delays)
+      .def("set_comm", &MasterPump::set_comm, py::arg("comm"), py::arg("ranks"), py::arg("peers"))
+      .def_property_readonly("comm_kind", &MasterPump::comm_kind)
       .def("set_repeat", &MasterPump::set_repeat)
       .def("set_integrity", &MasterPump::set_integrity, py::arg("mbox_tags"), py::arg("inbox_tag_off"), py::arg("on"))
       .def_property_readonly("integrity", &MasterPump::integrity)
@@ -1484,6 +1643,11 @@ void bind_engine(py::module& m) {
            py::arg("g"), py::arg("inbox"), py::arg("G"), py::arg("n_loc"), py::arg("mbox_base"), py::arg("mbox_rows"),
            py::arg("row0"), py::arg("beta_flag_host"), py::arg("msg_flag_dev"), py::arg("counters"), py::arg("K"),
            py::arg("device"), py::arg("timeout"), py::arg("beta_flag_dev") = 0)
+      .def(py::init<std::shared_ptr<GradLauncher>, const Tensor&, const Tensor&, int, std::shared_ptr<eh::P2PComm>, int,
+                    int, double>(),
+           py::arg("g"), py::arg("inbox"), py::arg("G"), py::arg("n_loc"), py::arg("comm"), py::arg("K"),
+           py::arg("device"), py::arg("timeout"))
+      .def_property_readonly("comm_kind", &WorkerPump::comm_kind)
       .def("run", &WorkerPump::run)
       .def_property_readonly("fused_put", &WorkerPump::fused_put)
       .def_property_readonly("device_wait", &WorkerPump::device_wait)

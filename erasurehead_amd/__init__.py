@@ -4,6 +4,23 @@ Capabilities of Distributed-Deep-Learning/ErasureHead (uncoded, cyclic-MDS, frac
 repetition, approximate gradient coding, ignore-stragglers, partial hybrids; logistic and
 least-squares models; GD/AGD) rebuilt on PyTorch-ROCm + gfx950 HIP kernels + RCCL.
 """
+import os as _os
+
 __version__ = "0.1.0"
+
+# Hardware queues per process.  HIP maps streams onto at most GPU_MAX_HW_QUEUES in-order hardware
+# queues (default 4) and streams beyond that share one.  The master's p2p transports (RCCL /
+# loopback, parallel/transport.py CommTransport) keep one receive and one send stream per worker
+# rank; a receive blocked on a straggler would otherwise stall another worker's receive queued
+# behind it on the same hardware queue, and the master could no longer take the fastest k.  Read
+# by the HIP runtime when it initialises, so it is raised here, before anything touches the GPU
+# (to at least 16; a larger setting in the environment is kept).
+MIN_HW_QUEUES = 16
+try:
+    _q = int(_os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+except ValueError:
+    _q = 0
+if _q < MIN_HW_QUEUES:
+    _os.environ["GPU_MAX_HW_QUEUES"] = str(MIN_HW_QUEUES)
 
 from .config import RunConfig  # noqa: E402

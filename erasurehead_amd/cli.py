@@ -65,7 +65,7 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     g.add_argument("--gpus", type=int, default=0,
                    help="N > 1: start N ranks (one per GPU) under torch.distributed.run from this command")
-    g.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl", "gloo"])
+    g.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl", "loopback", "gloo"])
     g.add_argument("--device-loop", default="auto", choices=["auto", "graph", "stream", "off"],
                    help="single-process runs without injected delay: rounds captured in hipGraphs (auto/graph), "
                         "enqueued back to back (stream) or host-driven (off)")
@@ -124,6 +124,8 @@ def relaunch(n: int, argv: List[str]) -> int:
     main_py = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "main.py")
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if int(env.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:  # erasurehead_amd/__init__.py: per-peer p2p streams
+        env["GPU_MAX_HW_QUEUES"] = "16"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", main_py, *argv]
     return subprocess.call(cmd, env=env)

@@ -349,7 +349,7 @@ class Trainer:
         """Run rounds in the C++ executors (GPU; single process or the IPC transport)."""
         if not (self.env.gpu and self.cfg.native_loop) or self.cfg.verify_beta:
             return False
-        if self.tx is not None and self.tx.name != "ipc":
+        if self.tx is not None and self.tx.name not in ("ipc", "rccl", "loopback"):
             return False
         if self.scheme.decode_kind in (3, 4) and self.cfg.n_workers > 64:  # 64-bit completion masks
             return False
@@ -497,6 +497,8 @@ class Trainer:
         kern = self._kernel_label()
         if kern:
             rep["grad_kernel"] = kern
+        if self.tx is not None and self.tx.name in ("rccl", "loopback"):
+            rep["hw_queues"] = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
         if self.tx is not None and self.tx.fallback_reason:
             rep["transport_fallback"] = self.tx.fallback_reason
         if self.tx is not None and env.is_master and self.tx.pairs:
@@ -538,7 +540,12 @@ class Trainer:
         if self.local_msgs:
             pump.set_local(self.plan.native_launcher(), self.G, [(m.worker, m.part) for m in self.local_msgs])
         tx = self.tx
-        if tx is not None:
+        if tx is not None and tx.name != "ipc":  # RCCL / loopback p2p: receives + events, no IPC counters
+            pump.set_comm(tx.comm, tx.sender_rows(), list(range(1, env.world)))
+            rem = [(m.worker, m.part, self.rem_slot[(m.worker, m.part, m.shard)], 0, r)
+                   for r in sorted(self.remote_msgs) for m in self.remote_msgs[r]]
+            pump.set_remote(self.Rbuf, rem)
+        elif tx is not None:
             rem = [(m.worker, m.part, self.rem_slot[(m.worker, m.part, m.shard)], tx.flags.host_addr(env.world + r), r)
                    for r in sorted(self.remote_msgs) for m in self.remote_msgs[r]]
             pump.set_remote(self.Rbuf, rem)
@@ -753,12 +760,15 @@ class Trainer:
         dwait = self._device_waits(tx)
         # a worker waits for beta longer than the master's worst round (stop rule + drain, each up to
         # round_timeout), so only a master that is really gone makes it give up
-        pump = C.WorkerPump(self.plan.native_launcher(), tx.inbox, self.G, self.n_loc, tx.rremote.ptr,
-                            tx.mbox_rows, tx.my_row0, tx.flags.host_addr(env.rank), tx.flags.dev_addr(w + env.rank),
-                            tx.counters, K, dev, 2.5 * float(cfg.round_timeout) + 5.0,
-                            tx.flags.dev_addr(env.rank) if dwait else 0)
+        wait_limit = 2.5 * float(cfg.round_timeout) + 5.0
+        if tx.name != "ipc":  # RCCL / loopback p2p: recv(beta) -> gradient -> send, stream-ordered
+            pump = C.WorkerPump(self.plan.native_launcher(), tx.inbox, self.G, self.n_loc, tx.comm, K, dev, wait_limit)
+        else:
+            pump = C.WorkerPump(self.plan.native_launcher(), tx.inbox, self.G, self.n_loc, tx.rremote.ptr,
+                                tx.mbox_rows, tx.my_row0, tx.flags.host_addr(env.rank), tx.flags.dev_addr(w + env.rank),
+                                tx.counters, K, dev, wait_limit, tx.flags.dev_addr(env.rank) if dwait else 0)
+            pump.set_integrity(tx.mbox_tags_addr(), tx.inbox_tags_addr(), env.rank, bool(cfg.integrity))
         pump.set_timing(bool(cfg.instrument))
-        pump.set_integrity(tx.mbox_tags_addr(), tx.inbox_tags_addr(), env.rank, bool(cfg.integrity))
         pump.set_repeat(self.repeat)
         if self.physical:
             pump.set_delays(self._rank_delays())

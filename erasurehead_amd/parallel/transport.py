@@ -13,8 +13,11 @@ interchangeable transports implement that contract here; the engine never branch
             release-stored into shared host memory.  The master's collector polls those
             counters natively (flag probes); workers poll their beta counter.  No RCCL
             kernel, no host copy, one launch per direction per round.
-  ``rccl``  torch.distributed p2p over RCCL (per-peer isend/irecv on dedicated streams,
-            HIP events behind each receive feed the collector).
+  ``rccl``  native RCCL p2p (csrc/runtime/comm.cpp): a 2-rank communicator per direction per
+            pair, ncclSend/ncclRecv on per-peer streams, HIP events behind each receive feed the
+            collector; driven by the same native pumps as ``ipc``.
+  ``loopback`` the rccl path's exact semantics over IPC staging rings, for ranks sharing a GPU
+            (RCCL refuses that): how the single-GPU box tests the RCCL pump code.
   ``gloo``  CPU tensors over gloo (tests, multi-process plumbing without a GPU).
 
 Buffers are per (round mod K) for messages and per round for beta, so a lagging worker can
@@ -134,33 +137,133 @@ class GlooTransport(Transport):
         self._sends = [[] for _ in range(self.K)]
 
 
-# ===================================================================================== rccl
-class RcclTransport(Transport):
-    name = "rccl"
+# ========================================================================= rccl / loopback
+class CommTransport(Transport):
+    """Stream-ordered point-to-point messaging through a native communicator (csrc/runtime/comm.h).
 
-    def __init__(self, *a, **kw):
+    ``rccl``: one 2-rank RCCL communicator per direction per (master, worker) pair, created from
+    ncclGetUniqueId ids the master broadcasts over the gloo/RCCL control plane.  The
+    native pumps drive it (beta: one send per worker rank on its own stream; messages: one receive
+    per worker rank into its mailbox rows with a HIP event behind it, the collector's probe); the
+    Python round loop uses the same communicator through ``send`` / ``recv`` bindings.
+    ``loopback``: the same semantics through IPC staging rings (RCCL refuses two ranks on one GPU),
+    so the single-GPU test box runs exactly the code path the RCCL transport runs on a node.
+    Buffers are plain device tensors (mailbox ring [K, n_rem, ld], beta inbox [R+1, ld]).
+    """
+
+    DEPTH = 2  # loopback staging slots per channel (messages a sender may run ahead)
+
+    def __init__(self, *a, kind: str = "rccl", **kw):
         super().__init__(*a, **kw)
+        from .._ext import native
+
+        self.name = kind
+        self.C = C = native()
         env = self.env
+        self.dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
+        self.es = torch.tensor([], dtype=self.dtype).element_size()
         self.cs = torch.cuda.current_stream(env.device)
-        peers = range(1, env.world) if env.is_master else [0]
-        self.ps = {r: torch.cuda.Stream(env.device) for r in peers}
+        self._regs = []
+        self.flags = None
+        counts = env.broadcast_object(self.remote_counts, 0)  # every rank: how many rows each rank sends
+        if kind == "rccl":
+            ids = {r: (C.nccl_unique_id(), C.nccl_unique_id()) for r in range(1, env.world)} if env.is_master else None
+            ids = env.broadcast_object(ids, 0)
+            if env.is_master:  # out(r): master -> r (master is rank 0 in it); in(r): r -> master
+                links = [x for r in range(1, env.world) for x in ((r, "out", ids[r][0], 0), (r, "in", ids[r][1], 1))]
+            else:
+                r = env.rank
+                links = [(0, "in", ids[r][0], 1), (0, "out", ids[r][1], 0)]
+            self.comm = C.RcclComm(self.dev, links)
+        elif kind == "loopback":
+            self.comm = self._loopback(counts)
+        else:
+            raise ValueError(f"unknown communicator {kind!r}")
+        env.barrier()
+        self.pairs = []
+        need = 2 * (env.world - 1) + 2  # master: a send and a receive stream per worker rank + compute
+        have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        if env.is_master and have < need:
+            print(f"[erasurehead] WARNING: GPU_MAX_HW_QUEUES={have} < {need}: per-peer receive streams share hardware "
+                  "queues, so a straggler's receive can hold back another worker's (set it before HIP starts)",
+                  file=sys.stderr, flush=True)
+        self._ps: Dict[int, torch.cuda.Stream] = {}  # python round loop's per-peer streams (created on use)
         if env.is_master:
             self.beta_ev = torch.cuda.Event()
             self.rem_ev = [[torch.cuda.Event() for _ in range(max(1, self.n_rem))] for _ in range(self.K)]
-            self.ev_of = [list(evs) for evs in self.rem_ev]  # [slot][mailbox row] -> its rank's event
+            self.ev_of = [list(evs) for evs in self.rem_ev]
         else:
-            self.bbuf = torch.zeros((2, self.ld), dtype=self.dtype, device=env.device)
+            self.inbox = torch.zeros((self.R + 1, self.ld), dtype=self.dtype, device=env.device)
             self.bev = torch.cuda.Event()
             self.gev = torch.cuda.Event()
             self.send_done: List[Optional[torch.cuda.Event]] = [None] * self.K
 
+    def _loopback(self, counts):
+        """Staging rings (receiver-owned IPC regions) + one shared array of 64-bit counters: per worker
+        rank r, [4r] beta ready, [4r+1] beta consumed, [4r+2] messages ready, [4r+3] messages consumed."""
+        env, C, w = self.env, self.C, self.env.world
+        bcap = self.ld * self.es
+        mcap = {r: max(16, counts.get(r, 0) * self.ld * self.es) for r in range(1, w)}
+        if env.is_master:
+            name = "/eh_lb_" + uuid.uuid4().hex[:16]
+            self.flags = C.ShmFlags(name, 4 * w, True)
+            own = {r: C.IpcRegion(self.DEPTH * mcap[r], self.dev, True) for r in range(1, w)}  # message rings
+            info = (name, {r: reg.handle() for r, reg in own.items()})
+        else:
+            info = None
+        info = env.broadcast_object(info, 0)
+        if not env.is_master:
+            self.flags = C.ShmFlags(info[0], 4 * w, False)
+            own = {0: C.IpcRegion(self.DEPTH * bcap, self.dev, True)}  # this rank's beta ring
+        self._regs += list(own.values())
+        handles = env.gather_objects(None if env.is_master else own[0].handle())
+        handles = env.broadcast_object(handles, 0)
+        f = self.flags
+
+        def ch(peer, direction, ring, cap, k):
+            return (peer, direction, ring, cap, self.DEPTH, f.dev_addr(k), f.dev_addr(k + 1), f.host_addr(k),
+                    f.host_addr(k + 1))
+        chans = []
+        if env.is_master:
+            for r in range(1, w):
+                peer_ring = C.IpcRegion(handles[r], self.DEPTH * bcap, self.dev)
+                self._regs.append(peer_ring)
+                chans.append(ch(r, "out", peer_ring.ptr, bcap, 4 * r))
+                if counts.get(r, 0):
+                    chans.append(ch(r, "in", own[r].ptr, mcap[r], 4 * r + 2))
+        else:
+            r = env.rank
+            ring = C.IpcRegion(info[1][r], self.DEPTH * mcap[r], self.dev)
+            self._regs.append(ring)
+            chans.append(ch(0, "in", own[0].ptr, bcap, 4 * r))
+            if counts.get(r, 0):
+                chans.append(ch(0, "out", ring.ptr, mcap[r], 4 * r + 2))
+        env.barrier()
+        if env.is_master:
+            f.unlink()
+        return C.LoopbackComm(self.dev, chans)
+
+    @property
+    def ps(self) -> Dict[int, torch.cuda.Stream]:
+        """Per-peer streams of the Python round loop (the native pumps own theirs)."""
+        if not self._ps:
+            peers = range(1, self.env.world) if self.env.is_master else [0]
+            self._ps = {r: torch.cuda.Stream(self.env.device) for r in peers}
+        return self._ps
+
+    # ---- native pumps --------------------------------------------------------------------
+    def sender_rows(self):
+        """(rank, first mailbox row, rows) of every worker rank that sends messages (master)."""
+        return [(r, self.row0[r], n) for r, n in sorted(self.remote_counts.items()) if n]
+
+    # ---- master (python round loop) ------------------------------------------------------------
     def send_beta(self, i, beta):
         self.beta_ev.record(self.cs)
         for r in range(1, self.env.world):
             s = self.ps[r]
             s.wait_event(self.beta_ev)
             with torch.cuda.stream(s):
-                dist.isend(beta, r)
+                self.comm.send(r, beta)
 
     def post_recvs(self, i, slot, col, rbuf, msgs_by_rank, delays):
         # one receive per worker rank: its messages are contiguous rows of the mailbox ring and the
@@ -170,7 +273,7 @@ class RcclTransport(Transport):
             j0, n = self.row0[r], len(msgs_by_rank[r])
             ev = self.rem_ev[slot][j0]
             with torch.cuda.stream(s):
-                dist.irecv(rbuf[slot, j0:j0 + n], r).wait()  # stream-ordered: s waits for the receive
+                self.comm.recv(r, rbuf[slot, j0:j0 + n])
                 ev.record(s)
             for jj, m in enumerate(msgs_by_rank[r]):
                 self.ev_of[slot][j0 + jj] = ev
@@ -179,11 +282,12 @@ class RcclTransport(Transport):
     def before_read(self, slot, j):
         self.cs.wait_event(self.ev_of[slot][j])
 
+    # ---- worker (python round loop) -----------------------------------------------------------
     def recv_beta(self, i):
-        b = self.bbuf[i % 2]
+        b = self.inbox[i]
         s = self.ps[0]
         with torch.cuda.stream(s):
-            dist.irecv(b, 0).wait()
+            self.comm.recv(0, b)
             self.bev.record(s)
         self.cs.wait_event(self.bev)
         slot = i % self.K
@@ -197,10 +301,25 @@ class RcclTransport(Transport):
         s = self.ps[0]
         s.wait_event(self.gev)
         with torch.cuda.stream(s):
-            dist.isend(G_slot, 0).wait()  # all of this rank's messages in one send (rows are contiguous)
+            self.comm.send(0, G_slot)  # all of this rank's messages in one send (rows are contiguous)
             ev = self.send_done[slot] or torch.cuda.Event()
             ev.record(s)
             self.send_done[slot] = ev
+
+    def finish(self):
+        torch.cuda.synchronize(self.env.device)
+
+    def close(self):
+        self.comm = None
+        for reg in self._regs:
+            reg.close()
+        self._regs = []
+        if self.flags is not None:
+            self.flags.close()
+            self.flags = None
+
+
+RcclTransport = CommTransport  # the RCCL p2p transport (kind="rccl")
 
 
 # ====================================================================================== ipc
@@ -540,18 +659,18 @@ def make_transport(kind: str, env, R: int, K: int, ld: int, dtype, n_local: int,
     if kind == "auto":
         kind = os.environ.get("ERASUREHEAD_TRANSPORT", "auto")
     if env.gpu and env.backend == "gloo" and kind == "rccl":
-        raise ValueError("ranks share a GPU (or run without RCCL): use transport ipc")
+        raise ValueError("ranks share a GPU (RCCL refuses that): use transport ipc, or loopback for the RCCL code path")
     if not env.gpu:
         if kind not in ("auto", "gloo"):
             raise ValueError(f"transport {kind!r} needs GPUs")
         return GlooTransport(*args)
     if kind == "gloo":
         raise ValueError("gloo transport is the CPU path; GPU ranks use ipc or rccl")
-    if kind == "rccl":
-        return RcclTransport(*args)
+    if kind in ("rccl", "loopback"):
+        return CommTransport(*args, kind=kind)
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(env.world)))
     if kind == "auto" and local_world < env.world and env.backend != "gloo":
-        return RcclTransport(*args)  # multi-node (torchrun --nnodes > 1): IPC mailboxes are node-local
+        return CommTransport(*args, kind="rccl")  # multi-node (torchrun --nnodes > 1): IPC mailboxes are node-local
     if kind in ("ipc", "auto"):
         try:
             return IpcTransport(*args, timeout=timeout)
@@ -560,13 +679,12 @@ def make_transport(kind: str, env, R: int, K: int, ld: int, dtype, n_local: int,
                 raise
             if os.environ.get("ERASUREHEAD_NO_FALLBACK"):
                 raise TransportError(f"{e} (ERASUREHEAD_NO_FALLBACK set: not falling back to RCCL)") from e
-            # loud, recorded degradation: the RCCL path runs the Python round loop (parallel/transport.py
-            # RcclTransport), not the native pumps; bench.py reports transport + reason per rank
+            # loud, recorded degradation: RCCL p2p under the same native pumps (per-round host wake-ups
+            # instead of device-side counters); bench.py reports transport + reason per rank
             if env.is_master:
                 print("[erasurehead] WARNING: " + str(e) + "\n[erasurehead] WARNING: falling back to RCCL p2p "
-                      "with the Python round loop (slower; set ERASUREHEAD_NO_FALLBACK=1 or --transport ipc to fail "
-                      "instead)", file=sys.stderr, flush=True)
-            tx = RcclTransport(*args)
+                      "(set ERASUREHEAD_NO_FALLBACK=1 or --transport ipc to fail instead)", file=sys.stderr, flush=True)
+            tx = CommTransport(*args, kind="rccl")
             tx.fallback_reason = str(e)
             return tx
     raise ValueError(f"unknown transport {kind!r}")

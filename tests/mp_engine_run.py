@@ -26,8 +26,11 @@ def main():
 
     env = init_distributed(os.environ.get("EH_TEST_DEVICE", "cuda"))
     extra = {"delay_mean": delay} if delay else {}
-    cfg, src, sch, parts = make(CASES[case_i], rule, **extra)
+    case = tuple(json.loads(os.environ["EH_TEST_CASE"])) if os.environ.get("EH_TEST_CASE") else CASES[case_i]
+    cfg, src, sch, parts = make(case, rule, **extra)
     cfg.num_itrs = 12
+    for k, v in json.loads(os.environ.get("EH_TEST_CFG", "{}")).items():  # RunConfig overrides
+        setattr(cfg, k, v)
     if os.environ.get("EH_TEST_ROUND_TIMEOUT"):
         cfg.round_timeout = float(os.environ["EH_TEST_ROUND_TIMEOUT"])
     if delay:

@@ -30,7 +30,10 @@ def _worker(rank, world, port, case, rule, out_path, extra):
     extra = dict(extra)
     corrupt = extra.pop("corrupt", False)
     timed_start = extra.pop("timed_start", None)
+    rounds = extra.pop("rounds", None)
     cfg, src, sch, parts = make(case, rule, **extra)
+    if rounds:
+        cfg.num_itrs = rounds
     if extra.get("delay_mode"):
         cfg.add_delay = 1
     tr = Trainer(cfg, env, src, scheme=sch)

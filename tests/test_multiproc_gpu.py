@@ -187,3 +187,99 @@ def test_ipc_handshake_failure_names_pair_and_step(tmp_path, monkeypatch):
     assert r.returncode != 0
     err = r.stdout + r.stderr
     assert "IPC mailbox handshake failed" in err and "rank 1 -> rank 0: message flag never signalled" in err, err[-3000:]
+
+
+def test_physically_late_worker_ranks_match_virtual_model(tmp_path):
+    """--delay-on worker on the native pumps: each worker rank spins on the device between its
+    gradient and its put (Exp delays, one logical worker per rank), the master's collector sees
+    the real flags.  Cyclic W=3 s=1 with a drain: the arrival sets equal the virtual model's (the
+    2 fastest) on every well-separated round, and the trajectory replays through the oracle."""
+    import json
+
+    from oracle import replay
+    from test_engine_cpu import make
+    from test_physical_delay import MARGIN, _predict
+
+    case, mean = (1, 0, 0, 4, 1, 0), 0.08
+    over = dict(add_delay=1, delay_mode="exp", delay_mean=mean, delay_on="worker", shard="message", drain="all")
+    r = _launch(3, 0, "GD", str(tmp_path / "p.npz"), EH_TEST_CASE=json.dumps(case), EH_TEST_CFG=json.dumps(over),
+                EH_TEST_ROUND_TIMEOUT="30")
+    cfg, src, sch, parts = make(case, "GD")
+    checked = 0
+    for i, a in enumerate(r["arrivals"]):
+        d = np.random.RandomState(i).exponential(mean, 3)
+        if np.all(np.diff(np.sort(d)) > MARGIN):
+            assert [w for (w, p) in a] == _predict(d, "count", 2, [0, 1, 2]), (i, d, a)
+            checked += 1
+    assert checked >= 2
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "GD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+    rep = json.loads(str(r["rank_report"]))
+    assert rep["round_loop"] == "native pump"
+
+
+def test_dead_worker_with_drain_never_feeds_stale_messages(tmp_path):
+    """a dead logical worker in a draining scheme makes every master round last a stop-rule
+    wait plus a drain timeout.  Healthy worker ranks with device-side beta waits must keep waiting
+    (their timeout exceeds the master's worst round) instead of releasing their queued rounds on a
+    beta that never arrived; the run completes and replays exactly through the oracle."""
+    import json
+
+    from oracle import replay
+    from test_engine_cpu import CASES, make
+
+    over = dict(kill_workers=[2], round_timeout=1.5, num_itrs=4)
+    r = _launch(3, 2, "AGD", str(tmp_path / "k.npz"), EH_TEST_CFG=json.dumps(over), ERASUREHEAD_WORKER_WAIT="device")
+    cfg, src, sch, parts = make(CASES[2], "AGD")
+    assert all(1 not in {w for (w, p) in a} for a in r["arrivals"])
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.parametrize("world,case_i,native", [(2, 4, True), (3, 1, True), (4, 7, True), (8, 5, True), (3, 4, False)])
+def test_loopback_comm_matches_replay(world, case_i, native, tmp_path):
+    """The RCCL transport's code path (csrc/runtime/comm.h: per-peer stream-ordered send/recv, a HIP
+    event behind every receive feeding the collector, the native pumps' comm mode) on one GPU,
+    where RCCL itself refuses two ranks: the loopback communicator has the same semantics over IPC
+    staging rings.  2-8 ranks, every trajectory replayed through the fp64 oracle; also the Python
+    round loop over the same communicator."""
+    import json
+
+    from oracle import replay
+    from test_engine_cpu import CASES, make
+
+    extra = {} if native else {"EH_TEST_CFG": json.dumps({"native_loop": False})}
+    r = _launch(world, case_i, "AGD", str(tmp_path / "l.npz"), ERASUREHEAD_TRANSPORT="loopback", **extra)
+    assert str(r["transport"]) == "loopback"
+    assert json.loads(str(r["rank_report"]))["round_loop"] == ("native pump" if native else "python")
+    cfg, src, sch, parts = make(CASES[case_i], "AGD")
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+
+
+def test_loopback_physically_late_ranks(tmp_path):
+    """--delay-on worker over the comm path: the late rank's spin sits between its gradient and its send."""
+    import json
+
+    from oracle import replay
+    from test_engine_cpu import make
+    from test_physical_delay import MARGIN, _predict
+
+    case, mean = (1, 0, 0, 4, 1, 0), 0.08
+    over = dict(add_delay=1, delay_mode="exp", delay_mean=mean, delay_on="worker", shard="message", drain="all")
+    r = _launch(3, 0, "GD", str(tmp_path / "q.npz"), EH_TEST_CASE=json.dumps(case), EH_TEST_CFG=json.dumps(over),
+                ERASUREHEAD_TRANSPORT="loopback", EH_TEST_ROUND_TIMEOUT="30")
+    cfg, src, sch, parts = make(case, "GD")
+    checked = 0
+    for i, a in enumerate(r["arrivals"]):
+        d = np.random.RandomState(i).exponential(mean, 3)
+        if np.all(np.diff(np.sort(d)) > MARGIN):
+            assert [w for (w, p) in a] == _predict(d, "count", 2, [0, 1, 2]), (i, d, a)
+            checked += 1
+    assert checked >= 2
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "GD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)

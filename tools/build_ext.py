@@ -183,6 +183,7 @@ def _build(force: bool, jobs: int, verbose: bool) -> str:
         link = [os.path.join(ROCM, "bin", "hipcc"), "-shared", "-fPIC", "-o", tmp, *objs,
                 f"--offload-arch={ARCH}", f"-L{torchlib}", f"-Wl,-rpath,{torchlib}",
                 "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64",
+                "-lrccl",  # torch's librccl (first -L): one RCCL per process (csrc/runtime/comm.cpp)
                 f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx"]
         _run(link)
         if embedded_hash(tmp) != want:
