@@ -53,19 +53,24 @@ struct ArbArgs {
   int* log;                              // [R][kArbLogInts]
   long long* tlog;                       // [R][kArbLogTicks]
   int* abort;                            // set by a failed round: every later arbiter returns at once
-  // Integrity (integrity.h; tags == nullptr: off): the mailbox rows a round decodes are checked
-  // against their senders' tags before beta(i+1) is released (status 4 on a mismatch), and
-  // beta(i+1) carries a tag into every worker inbox (inbox base + inbox_tag_off, one per round).
+  // Integrity (integrity.h; tags == nullptr: off): the mailbox rows round i decodes are checked
+  // against their senders' tags by round i+1's idle waves while its wave 0 polls (a segment's last
+  // round by a tail check), and beta(i+1) carries a tag into every worker inbox (inbox base +
+  // inbox_tag_off, one per round).
   const MsgTag* tags;                    // [K][r_rows] mailbox tags
   const int* row_rank;                   // [r_rows] sender rank of each mailbox row
   long long inbox_tag_off;               // bytes from a worker inbox base to its tag slots
+  CheckList* checks;                     // [2] device memory: the mailbox rows rounds i-1 / i decoded
+  IntegrityErr* err;                     // host-mapped: the first failed check
 };
-// Round statuses in the log: 0 ok, 1 timeout, 2 not decodable, 3 skipped, 4 integrity failure
-// (log ints 2..5: slot << 16 | row, expected rank, tag round + 1, tag rank; ticks 4..5: tag
-// checksum, payload checksum).
+// Round statuses in the log: 0 ok, 1 timeout, 2 not decodable, 3 skipped, 4 integrity failure of the
+// PREVIOUS round's messages (found by this round's idle waves; details in ArbArgs::err).
 constexpr int kArbIntegrity = 4;
 
 // msg_dtype 0 fp64 / 1 fp32 (messages, beta_in, inboxes)
-hipError_t arbiter_round_launch(const ArbArgs& a, int round, int msg_dtype, hipStream_t st);
+// check_prev: this round's idle waves check round-1's mailbox rows (false for a segment's first round)
+hipError_t arbiter_round_launch(const ArbArgs& a, int round, int msg_dtype, hipStream_t st, bool check_prev);
+// after a segment's last round: check that round's rows (no later arbiter does)
+hipError_t arbiter_tail_check_launch(const ArbArgs& a, int round, hipStream_t st);
 
 }  // namespace eh

@@ -38,7 +38,7 @@ __device__ __forceinline__ unsigned long long load_counter(const unsigned long l
 }  // namespace
 
 template <typename M>
-__global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
+__global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, int check_prev) {
   __shared__ int s_pw[kArbMaxProbes], s_pp[kArbMaxProbes], s_ps[kArbMaxProbes];
   __shared__ int batch[kArbMaxProbes];
   __shared__ int got_sh[2 * kArbMaxW];
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
   __shared__ const void* mptr[kMaxMsgs];
   __shared__ double mcoef[kMaxMsgs];
   __shared__ int mrow[kMaxMsgs];  // kind << 24 | row of every used buffer row
-  __shared__ unsigned long long vs[kMaxMsgs], scratch[16];
+  __shared__ unsigned long long scratch[16];
   __shared__ int s_narr, s_nmsg, s_status, s_bad;
   __shared__ unsigned long long s_bsum;
   const int tid = threadIdx.x;
@@ -63,7 +63,6 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
     s_ps[q] = a.probe_src[q];
   }
   for (int m = tid; m < 2 * a.W; m += blockDim.x) got_sh[m] = 0;
-  for (int m = tid; m < kMaxMsgs; m += blockDim.x) vs[m] = 0;
   if (tid == 0) {
     s_narr = 0;
     s_nmsg = 0;
@@ -141,8 +140,13 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
       }
       __builtin_amdgcn_s_sleep(2);
     }
+  } else if (a.tags && check_prev) {
+    // waves 1..15 meanwhile check the mailbox rows the PREVIOUS round decoded against their senders'
+    // tags (integrity.h): off the critical path, those rows stay intact until their slot comes back
+    check_rows_waves(a.checks[(i - 1) & 1], 1, static_cast<int>(blockDim.x >> 6) - 1, a.err, &s_bad);
   }
   __syncthreads();
+  if (s_status == 0 && s_bad) s_status = kArbIntegrity;  // a torn / stale message of round i-1
   if (s_status != 0) {
     if (tid == 0) {
       __hip_atomic_store(a.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -216,9 +220,8 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
   }
 
   // ---- 3. combine + update, beta(i+1) into beta_in and every worker inbox -------------------
-  // With tags on, the same loads also sum the checksum terms of every used mailbox row (one wave
-  // reduction per row, LDS adds) and of beta(i+1); the rows are compared with their tags below,
-  // before anything is released.  The column loop has a block-uniform trip count for that.
+  // With tags on, the loop also sums the checksum terms of beta(i+1) for its inbox tags (the
+  // column loop has a block-uniform trip count for the block reduction after it).
   const double decay = a.decay[i], gm = a.gm[i], l2 = a.l2[i], theta = a.theta[i];
   const bool vfy = a.tags != nullptr;
   M* bin_next = static_cast<M*>(a.beta_in) + static_cast<long long>(i + 1) * a.ld;
@@ -236,14 +239,6 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
 #pragma unroll
       for (int q = 0; q < kB; ++q)
         if (m0 + q < s_nmsg) g = fma(mcoef[m0 + q], static_cast<double>(v[q]), g);
-      if (vfy) {
-#pragma unroll
-        for (int q = 0; q < kB; ++q) {
-          if (m0 + q >= s_nmsg || (mrow[m0 + q] >> 24) != 1) continue;  // block-uniform
-          const unsigned long long t = wave_sum_u64(in ? tag_term(elem_bits(v[q]), c) : 0ull);
-          if ((tid & 63) == 0 && t) atomicAdd(&vs[m0 + q], t);
-        }
-      }
     }
     if (in && c < a.d) {
       const double b = a.beta[c];
@@ -266,36 +261,12 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
       bterm += tag_term(elem_bits(out), c);
     }
   }
-  if (vfy) {  // ---- 3b. the used mailbox rows against their senders' tags -------------------------
-    const unsigned long long bs = block_sum_u64(bterm, scratch);  // (barrier: every vs add is in)
+  if (vfy) {
+    const unsigned long long bs = block_sum_u64(bterm, scratch);
     if (tid == 0) s_bsum = bs;
-    for (int m = tid; m < s_nmsg; m += blockDim.x) {
-      if ((mrow[m] >> 24) != 1) continue;
-      const int row = mrow[m] & 0xffffff;
-      const MsgTag tg = a.tags[static_cast<long long>(slot) * a.r_rows + row];
-      const int want = a.row_rank[row];
-      if ((tg.round1 != static_cast<unsigned int>(i + 1) || tg.rank != static_cast<unsigned int>(want) ||
-           tg.sum != vs[m]) && atomicCAS(&s_bad, 0, 1) == 0) {
-        lg[2] = (slot << 16) | row;
-        lg[3] = want;
-        lg[4] = static_cast<int>(tg.round1);
-        lg[5] = static_cast<int>(tg.rank);
-        tl[4] = static_cast<long long>(tg.sum);
-        tl[5] = static_cast<long long>(vs[m]);
-        s_status = kArbIntegrity;
-      }
-    }
   }
   __syncthreads();
   if (tid == 0) tl[1] = wall_clock64();
-  if (s_status != 0) {  // a torn or stale message: beta(i+1) is not released
-    if (tid == 0) {
-      __hip_atomic_store(a.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lg[0] = s_status;
-      lg[1] = s_narr;
-    }
-    return;
-  }
 
   // ---- 4. drain: every worker rank's round-i message has landed ------------------------------
   if (a.drain && tid < 64) {
@@ -348,14 +319,48 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i) {
       tl[4 + x] = arr_t[x];
     }
   }
+  if (vfy) {  // this round's decoded rows for the next arbiter's idle waves (or the segment's tail check):
+              // one thread per row, local rows marked -1 (not checked)
+    CheckList& cl = a.checks[i & 1];
+    for (int m = tid; m < s_nmsg && m < kMaxMsgs; m += blockDim.x) {
+      const bool mb = (mrow[m] >> 24) == 1;
+      const int row = mrow[m] & 0xffffff;
+      cl.row[m] = mptr[m];
+      cl.mrow[m] = mb ? row : -1;
+      cl.rank[m] = mb ? a.row_rank[row] : 0;
+    }
+    if (tid == 0) {
+      cl.n = min(s_nmsg, kMaxMsgs);
+      cl.round = i;
+      cl.slot = slot;
+      cl.es = static_cast<int>(sizeof(M));
+      cl.ld = a.ld;
+      cl.tags = a.tags + static_cast<long long>(slot) * a.r_rows;
+    }
+  }
 }
 
-hipError_t arbiter_round_launch(const ArbArgs& a, int round, int msg_dtype, hipStream_t st) {
+// The segment's last round has no successor to check its rows: one workgroup does it.
+__global__ void __launch_bounds__(1024) arbiter_tail_check(const ArbArgs a, int i) {
+  __shared__ int claim;
+  if (threadIdx.x == 0) claim = 0;
+  __syncthreads();
+  if (__hip_atomic_load(a.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  check_rows_waves(a.checks[i & 1], 0, static_cast<int>(blockDim.x >> 6), a.err, &claim);
+}
+
+hipError_t arbiter_round_launch(const ArbArgs& a, int round, int msg_dtype, hipStream_t st, bool check_prev) {
   if (a.W > kArbMaxW || a.nprobe > kArbMaxProbes || a.nsrc > kArbMaxSrc || a.nsrc > 64) return hipErrorInvalidValue;
   if (msg_dtype == 0)
-    hipLaunchKernelGGL(arbiter_round<double>, dim3(1), dim3(1024), 0, st, a, round);
+    hipLaunchKernelGGL(arbiter_round<double>, dim3(1), dim3(1024), 0, st, a, round, check_prev ? 1 : 0);
   else
-    hipLaunchKernelGGL(arbiter_round<float>, dim3(1), dim3(1024), 0, st, a, round);
+    hipLaunchKernelGGL(arbiter_round<float>, dim3(1), dim3(1024), 0, st, a, round, check_prev ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t arbiter_tail_check_launch(const ArbArgs& a, int round, hipStream_t st) {
+  if (!a.tags) return hipSuccess;
+  hipLaunchKernelGGL(arbiter_tail_check, dim3(1), dim3(1024), 0, st, a, round);
   return hipGetLastError();
 }
 

@@ -42,6 +42,22 @@ struct IntegrityErr {
 };
 
 constexpr int kMaxTagRows = 64;  // rows of one tagged put descriptor (sender scratch / LDS sums)
+constexpr int kMaxCheckRows = 128;  // mailbox rows one deferred check covers (= kMaxMsgs of a decode)
+
+// The mailbox rows a round's decode read, checked AFTER the round (off the critical path: the rows
+// stay intact until their ring slot is reused K >= 2 rounds later).  Passed by value to the host
+// pump's check kernel; written to device memory by the arbiter for the next round's idle waves.
+struct CheckList {
+  int n;                          // rows
+  int round;                      // the round whose messages they are
+  int slot;                       // ring slot
+  int es;                         // element bytes
+  int ld;
+  const void* row[kMaxCheckRows];
+  int mrow[kMaxCheckRows];        // mailbox row (tag index within the slot); < 0: skip (a local row)
+  int rank[kMaxCheckRows];        // expected sender
+  const MsgTag* tags;             // this slot's tags [rows]
+};
 
 __host__ __device__ inline unsigned long long tag_term(unsigned long long bits, long long j) {
   return bits * static_cast<unsigned long long>(2 * j + 1);
@@ -85,6 +101,46 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v
     for (int w = 0; w < static_cast<int>(blockDim.x >> 6); ++w) s += scratch[w];
   __syncthreads();
   return s;
+}
+
+// Checksum of one row of ld es-byte elements, by one wave (lanes stride the columns, four loads in
+// flight per lane); every lane returns the total.
+__device__ __forceinline__ unsigned long long wave_row_checksum(const void* row, int ld, int es) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long t = 0;
+  if (es == 8) {
+    const unsigned long long* p = static_cast<const unsigned long long*>(row);
+#pragma unroll 4
+    for (int c = lane; c < ld; c += 64) t += tag_term(p[c], c);
+  } else {
+    const unsigned int* p = static_cast<const unsigned int*>(row);
+#pragma unroll 4
+    for (int c = lane; c < ld; c += 64) t += tag_term(p[c], c);
+  }
+  return wave_sum_u64(t);
+}
+
+// Waves [w0, w0 + nw) of the block check the rows of `cl`, one wave per row in turn; the first
+// mismatch (claimed with atomicCAS on *claim, an LDS int) is reported to err.  Returns (wave-uniform)
+// whether this wave found one.
+__device__ inline void report_integrity(IntegrityErr* err, int round, int where, int rank_want, const MsgTag& got,
+                                        unsigned long long calc);
+__device__ inline bool check_rows_waves(const CheckList& cl, int w0, int nw, IntegrityErr* err, int* claim) {
+  const int w = static_cast<int>(threadIdx.x >> 6) - w0;
+  if (w < 0 || w >= nw) return false;
+  bool bad = false;
+  for (int m = w; m < cl.n; m += nw) {
+    if (cl.mrow[m] < 0) continue;  // a local row (no transport, no tag)
+    const unsigned long long sum = wave_row_checksum(cl.row[m], cl.ld, cl.es);
+    const MsgTag tg = cl.tags[cl.mrow[m]];
+    if (tg.round1 != static_cast<unsigned int>(cl.round + 1) || tg.rank != static_cast<unsigned int>(cl.rank[m]) ||
+        tg.sum != sum) {
+      bad = true;
+      if ((threadIdx.x & 63) == 0 && atomicCAS(claim, 0, 1) == 0)
+        report_integrity(err, cl.round, (cl.slot << 16) | cl.mrow[m], cl.rank[m], tg, sum);
+    }
+  }
+  return bad;
 }
 
 // Element bits of a row (double / float payloads), zero-extended.

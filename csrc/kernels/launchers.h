@@ -72,17 +72,6 @@ struct CombineArgs {
   const void* msg[kMaxMsgs];
   double coef[kMaxMsgs];
   int nmsg;
-  // Integrity check of mailbox rows (integrity.h), off when tags == nullptr: message m is checked
-  // against tags[tag_row[m]] (tag_row < 0: a local row, not checked) for counter value round1 and
-  // sender tag_rank[m].  vsum [kMaxMsgs] / vcount: zeroed device scratch (left zero); err: host-mapped.
-  const MsgTag* tags;
-  int tag_row[kMaxMsgs];
-  unsigned char tag_rank[kMaxMsgs];
-  unsigned int round1;
-  int slot;
-  unsigned long long* vsum;
-  unsigned int* vcount;
-  IntegrityErr* err;
 };
 // msg dtype / worker-beta dtype: 0 fp64, 1 fp32; rule 0 GD, 1 AGD
 hipError_t combine_update_launch(const CombineArgs& args, int msg_dtype, int w_dtype,
@@ -128,6 +117,9 @@ hipError_t signal_launch(unsigned long long* flag, unsigned long long value, hip
 hipError_t verify_rows_launch(const void* rows, const MsgTag* tags, int nrows, int ld, int es,
                               unsigned int round1, unsigned int rank, IntegrityErr* err, int where,
                               hipStream_t st);
+// Deferred check of the mailbox rows one round decoded (integrity.h CheckList): one workgroup,
+// one wave per row; the first mismatch goes to err (host-mapped).
+hipError_t check_list_launch(const CheckList& cl, IntegrityErr* err, hipStream_t st);
 // Spin on the device for `ticks` wall_clock64 ticks (a physically late worker, --delay-mode worker).
 hipError_t spin_launch(long long ticks, hipStream_t st);
 

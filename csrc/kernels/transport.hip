@@ -139,6 +139,13 @@ __global__ void __launch_bounds__(256) verify_rows(const unsigned char* rows, co
   }
 }
 
+__global__ void __launch_bounds__(1024) check_list(const CheckList cl, IntegrityErr* err) {
+  __shared__ int claim;
+  if (threadIdx.x == 0) claim = 0;
+  __syncthreads();
+  check_rows_waves(cl, 0, static_cast<int>(blockDim.x >> 6), err, &claim);
+}
+
 __global__ void spin_ticks(long long ticks) {
   const long long t0 = wall_clock64();
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
@@ -168,6 +175,13 @@ hipError_t verify_rows_launch(const void* rows, const MsgTag* tags, int nrows, i
   if (!rows || !tags || (es != 4 && es != 8)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(verify_rows, dim3(1), dim3(256), 0, st, static_cast<const unsigned char*>(rows), tags, nrows,
                      ld, es, round1, rank, err, where);
+  return hipGetLastError();
+}
+
+hipError_t check_list_launch(const CheckList& cl, IntegrityErr* err, hipStream_t st) {
+  if (cl.n <= 0) return hipSuccess;
+  if (cl.n > kMaxCheckRows || !cl.tags || (cl.es != 4 && cl.es != 8)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(check_list, dim3(1), dim3(1024), 0, st, cl, err);
   return hipGetLastError();
 }
 

@@ -20,78 +20,32 @@
 
 namespace eh {
 
-// Integrity (args.tags != nullptr, integrity.h): while it streams the message rows, every block
-// also sums the checksum terms of its columns of each tagged (mailbox) row — one wave reduction
-// per tagged row, LDS, one global add per row and block — and the last block compares the sums
-// with the senders' tags.  A mismatch is reported to the host-mapped record (the pump raises a
-// named error); the update itself cannot be held back without a grid-wide barrier.
 template <typename M, typename W>
 __global__ void __launch_bounds__(256)
 combine_update(const CombineArgs args, double* __restrict__ beta, double* __restrict__ u,
                double* __restrict__ hist, W* __restrict__ beta_w, double* __restrict__ g_out,
                int d, int ld, double decay, double gm, double l2, double theta, int rule,
                long long* __restrict__ stamp) {
-  __shared__ unsigned long long vs[kMaxMsgs];
-  __shared__ int s_last;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool verify = args.tags != nullptr;  // kernel-uniform
   if (stamp && c == 0) *stamp = wall_clock64();  // device time the round's messages were all ready
-  if (verify) {
-    for (int m = threadIdx.x; m < args.nmsg; m += blockDim.x) vs[m] = 0;
-    __syncthreads();
-  } else if (c >= ld) {
+  if (c >= ld) return;
+  if (c >= d) {  // padded columns stay exactly zero
+    if (beta_w) beta_w[c] = W(0);
     return;
   }
-  const bool col = c < d;  // padded columns (d <= c < ld) stay exactly zero
   // The message rows are independent loads (remote ones in fine-grained memory, ~µs each): issue
   // them eight at a time, then accumulate in message order (the same fma chain, bitwise, as a
   // one-at-a-time loop).
   double g = 0.0;
   constexpr int kBatch = 8;
   for (int m0 = 0; m0 < args.nmsg; m0 += kBatch) {
-    M raw[kBatch];
-#pragma unroll
-    for (int k = 0; k < kBatch; ++k)  // padded columns too: the checksum covers the whole row
-      raw[k] = (c < ld && m0 + k < args.nmsg) ? static_cast<const M*>(args.msg[m0 + k])[c] : M(0);
+    double v[kBatch];
 #pragma unroll
     for (int k = 0; k < kBatch; ++k)
-      if (m0 + k < args.nmsg) g = fma(args.coef[m0 + k], static_cast<double>(raw[k]), g);
-    if (verify) {
+      v[k] = m0 + k < args.nmsg ? static_cast<double>(static_cast<const M*>(args.msg[m0 + k])[c]) : 0.0;
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k) {
-        if (m0 + k >= args.nmsg || args.tag_row[m0 + k] < 0) continue;  // uniform
-        const unsigned long long t = wave_sum_u64(c < ld ? tag_term(elem_bits(raw[k]), c) : 0ull);
-        if ((threadIdx.x & 63) == 0 && t) atomicAdd(&vs[m0 + k], t);
-      }
-    }
-  }
-  if (verify) {
-    __syncthreads();
-    for (int m = threadIdx.x; m < args.nmsg; m += blockDim.x)
-      if (args.tag_row[m] >= 0 && vs[m]) atomicAdd(args.vsum + m, vs[m]);
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned int prev = __hip_atomic_fetch_add(args.vcount, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = prev == gridDim.x - 1;
-      if (s_last) __hip_atomic_store(args.vcount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (s_last) {
-      for (int m = threadIdx.x; m < args.nmsg; m += blockDim.x) {
-        if (args.tag_row[m] < 0) continue;
-        const unsigned long long sum = atomicExch(args.vsum + m, 0ull);
-        const MsgTag tg = args.tags[args.tag_row[m]];
-        if (tg.round1 != args.round1 || tg.rank != args.tag_rank[m] || tg.sum != sum)
-          report_integrity(args.err, static_cast<int>(args.round1) - 1, (args.slot << 16) | args.tag_row[m],
-                           args.tag_rank[m], tg, sum);
-      }
-    }
-    if (c >= ld) return;
-  }
-  if (!col) {
-    if (beta_w) beta_w[c] = W(0);
-    return;
+    for (int k = 0; k < kBatch; ++k)
+      if (m0 + k < args.nmsg) g = fma(args.coef[m0 + k], v[k], g);
   }
   const double b = beta[c];
   double nb;

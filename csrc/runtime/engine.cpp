@@ -347,7 +347,6 @@ class MasterPump {
     index_.assign(2 * W, {});
     err_ = std::make_unique<HostMapped>(sizeof(eh::IntegrityErr));
     const auto i64 = at::TensorOptions().dtype(at::kLong).device(at::Device(at::kCUDA, device));
-    vscr_ = at::zeros({eh::kMaxMsgs + 1}, i64);           // combine checksums + block counter
     csum_ = at::zeros({eh::kMaxPuts * eh::kMaxTagRows}, i64);  // beta put checksums
   }
   ~MasterPump() {
@@ -496,10 +495,16 @@ class MasterPump {
   }
   bool integrity() const { return tags_; }
 
-  // Raise the first integrity failure any combine of this pump reported (host-mapped record).
+  // Raise the first integrity failure any deferred check of this pump reported (host-mapped record).
   void check_integrity() const {
     const auto* e = static_cast<const eh::IntegrityErr*>(err_->host);
     if (__atomic_load_n(&e->flag, __ATOMIC_ACQUIRE)) throw std::runtime_error(integrity_message(*e, false));
+  }
+  // End of a run: check the last round's rows too, then raise any failure.  Syncs the stream.
+  void final_check() {
+    flush_check();
+    hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    check_integrity();
   }
 
   // Device-side drain (after_combine): (host address, device address) of every worker rank's
@@ -595,6 +600,7 @@ class MasterPump {
       for (const auto& m : local_)
         col_->add_event_probe(m.w, m.p, i, reinterpret_cast<uintptr_t>(loc_ev_[slot]), dl[m.w]);
     }
+    flush_check();  // round i-1's mailbox rows, behind this round's beta and local gradient
     if (comm_) {  // one receive per sending rank into its mailbox rows; the event behind it is the probe
       char* rb = static_cast<char*>(rbuf_.data_ptr()) + static_cast<int64_t>(slot) * r_rows_ * ld_ * es_;
       for (size_t k = 0; k < comm_ranks_.size(); ++k) {
@@ -821,9 +827,12 @@ class MasterPump {
         for (int k = 0; k < repeat_; ++k)
           hcheck(launcher_->launch(bin + static_cast<int64_t>(i) * ld_ * es_, g, stream_), "local gradient");
       }
-      hcheck(eh::arbiter_round_launch(args, i, acc_, stream_), "arbiter_round");
+      hcheck(eh::arbiter_round_launch(args, i, acc_, stream_, i > a), "arbiter_round");
     }
-    if (b > a) prepub_ = b;
+    if (b > a) {
+      hcheck(eh::arbiter_tail_check_launch(args, b - 1, stream_), "arbiter_tail_check");
+      prepub_ = b;
+    }
   }
 
   // Rounds [a, b) of run_device: (status, arrivals [(worker, part, t_rel)], t_decoded, t_end), times
@@ -845,17 +854,9 @@ class MasterPump {
       for (int x = 0; x < n && l[0] == 0; ++x)
         arr.append(py::make_tuple(l[4 + 2 * x], l[5 + 2 * x], (t[4 + x] - t[0]) / hz));
       std::string why;
-      if (l[0] == eh::kArbIntegrity) {
-        eh::IntegrityErr e{};
-        e.round = i;
-        e.where = l[2];
-        e.rank_want = l[3];
-        e.round1_got = static_cast<unsigned int>(l[4]);
-        e.rank_got = static_cast<unsigned int>(l[5]);
-        e.sum_got = static_cast<unsigned long long>(t[4]);
-        e.sum_calc = static_cast<unsigned long long>(t[5]);
-        why = integrity_message(e, false);
-      }
+      const auto* e = static_cast<const eh::IntegrityErr*>(err_->host);
+      if (l[0] == eh::kArbIntegrity || (l[0] == 3 && __atomic_load_n(&e->flag, __ATOMIC_ACQUIRE)))
+        why = integrity_message(*e, false);
       // per-round ticks: poll (release of beta(i) -> stop rule), update (stop rule -> combine and
       // checks done), release (-> beta(i+1) released, drain included); seconds
       const double t_stop = l[0] == 0 && n > 0 ? (t[4 + n - 1] - t[0]) / hz : -1.0;
@@ -962,8 +963,6 @@ class MasterPump {
     for (int m = 0; m < a.nmsg; ++m) {
       a.msg[m] = used[m].p;
       a.coef[m] = used[m].c;
-      a.tag_row[m] = used[m].row;
-      a.tag_rank[m] = static_cast<unsigned char>(used[m].row >= 0 ? row_rank_[used[m].row] : 0);
       remote |= used[m].row >= 0;
     }
     if (comm_ && remote) {  // order the combine after the receives it reads (their events are complete)
@@ -976,14 +975,23 @@ class MasterPump {
                         "hipStreamWaitEvent(recv)");
       }
     }
-    if (tags_ && remote) {  // check the mailbox rows against their senders' tags (update.hip)
+    if (tags_ && remote) {  // the mailbox rows it reads are checked after the next round starts
+      eh::CheckList& cl = check_;
       const int slot = i % K_;
-      a.tags = reinterpret_cast<const eh::MsgTag*>(mbox_tags_) + static_cast<int64_t>(slot) * r_rows_;
-      a.round1 = static_cast<unsigned int>(i + 1);
-      a.slot = slot;
-      a.vsum = reinterpret_cast<unsigned long long*>(vscr_.data_ptr<int64_t>());
-      a.vcount = reinterpret_cast<unsigned int*>(vscr_.data_ptr<int64_t>() + eh::kMaxMsgs);
-      a.err = static_cast<eh::IntegrityErr*>(err_->dev);
+      cl = eh::CheckList{};
+      cl.round = i;
+      cl.slot = slot;
+      cl.es = es_;
+      cl.ld = ld_;
+      cl.tags = reinterpret_cast<const eh::MsgTag*>(mbox_tags_) + static_cast<int64_t>(slot) * r_rows_;
+      for (const auto& u : used)
+        if (u.row >= 0 && cl.n < eh::kMaxCheckRows) {
+          cl.row[cl.n] = u.p;
+          cl.mrow[cl.n] = u.row;
+          cl.rank[cl.n] = row_rank_[u.row];
+          ++cl.n;
+        }
+      check_pending_ = cl.n > 0;
     }
     auto& ev = upd_ev_[i];
     if (events) {
@@ -1110,6 +1118,9 @@ class MasterPump {
     g.tags = tags_ ? reinterpret_cast<const eh::MsgTag*>(mbox_tags_) : nullptr;
     g.row_rank = arb_keep_[15].data_ptr<int>();
     g.inbox_tag_off = inbox_tag_off_;
+    arb_checks_ = at::zeros({static_cast<int64_t>(2 * sizeof(eh::CheckList))}, at::TensorOptions().dtype(at::kByte).device(dev));
+    g.checks = reinterpret_cast<eh::CheckList*>(arb_checks_.data_ptr());
+    g.err = static_cast<eh::IntegrityErr*>(err_->dev);
     arb_args_ = g;
     arb_ready_ = true;
   }
@@ -1153,6 +1164,14 @@ class MasterPump {
       hcheck(eh::put_signal_launch(a, blocks_for(static_cast<long long>(ld_) * es_), stream_), "put_signal(beta)");
     }
     if (timing_) record_t(j, 1);
+  }
+
+  // Enqueue the pending check of the last combined round (integrity.h CheckList): off the round's
+  // critical path, the rows stay intact until slot reuse K >= 2 rounds later.
+  void flush_check() {
+    if (!check_pending_) return;
+    check_pending_ = false;
+    hcheck(eh::check_list_launch(check_, static_cast<eh::IntegrityErr*>(err_->dev), stream_), "check_list");
   }
 
   bool no_delay(int i) const {
@@ -1225,12 +1244,14 @@ class MasterPump {
   int64_t inbox_tag_off_ = 0;       // worker inbox base -> its tag slots
   std::vector<int> row_rank_;       // [r_rows] sender rank of each mailbox row
   std::unique_ptr<HostMapped> err_;  // first integrity failure (eh::IntegrityErr)
-  Tensor vscr_, csum_;              // combine checksum scratch, beta put checksum scratch
+  Tensor csum_;                     // beta put checksum scratch
+  eh::CheckList check_{};           // mailbox rows of the last combined round, checked after the next begins
+  bool check_pending_ = false;
   std::vector<std::pair<uintptr_t, uintptr_t>> arb_src_;
   bool arb_ready_ = false;
   eh::ArbArgs arb_args_{};
   std::vector<Tensor> arb_keep_;
-  Tensor arb_log_, arb_tlog_, arb_abort_;
+  Tensor arb_log_, arb_tlog_, arb_abort_, arb_checks_;
   std::vector<double> decay_, gm_, l2_, theta_, delays_, remote_delays_;
   int repeat_ = 1;
   int update_rule_ = 0, stop_rule_ = 0, k_ = 0;
@@ -1621,6 +1642,7 @@ void bind_engine(py::module& m) {
       .def("set_integrity", &MasterPump::set_integrity, py::arg("mbox_tags"), py::arg("inbox_tag_off"), py::arg("on"))
       .def_property_readonly("integrity", &MasterPump::integrity)
       .def("check_integrity", &MasterPump::check_integrity)
+      .def("final_check", &MasterPump::final_check)
       .def("set_sources", &MasterPump::set_sources)
       .def("device_blocker", &MasterPump::device_blocker)
       .def("run_device", &MasterPump::run_device, py::arg("a"), py::arg("b"), py::arg("deadline_s"))

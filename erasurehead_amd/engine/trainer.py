@@ -598,9 +598,9 @@ class Trainer:
                 t_timed1 = self._timed_fence()
             for i, (status, arr, tdec, tend, detail, tstop) in zip(range(start, R), pump.device_log(start, R)):
                 if status:
-                    why = {1: f"a worker rank's message did not arrive within {deadline:.0f} s",
-                           2: "the arrivals could not be decoded on the device",
-                           3: "an earlier round failed"}.get(status, detail or f"status {status}")
+                    why = detail or {1: f"a worker rank's message did not arrive within {deadline:.0f} s",
+                                 2: "the arrivals could not be decoded on the device",
+                                 3: "an earlier round failed"}.get(status, f"status {status}")
                     raise RuntimeError(f"device-driven round {i}: {why}")
                 if tstop >= 0:  # arbiter ticks: poll until the stop rule, combine + checks, drain + release
                     self.timer.add("arbiter_poll", tstop)
@@ -611,6 +611,7 @@ class Trainer:
                 worker_timeset[i] = sch.worker_times(arrivals)
                 arrivals_log.append([(a.worker, a.part, a.t_rel) for a in arrivals])
                 self.timer.add("device_round", tend)
+            pump.check_integrity()  # the segments' tail checks (device_log synchronised the stream)
             self.device_loop = "arbiter"
         if device_mode:
             stamps = torch.zeros(R + 1, dtype=torch.int64, device=env.device)
@@ -680,7 +681,7 @@ class Trainer:
             t_timed1 = self._timed_fence()
         col.drain(R - 1, max(cfg.round_timeout, 60.0))
         upd = pump.update_ms()
-        pump.check_integrity()  # the last rounds' combines (update_ms synchronised the stream)
+        pump.final_check()  # the last round's mailbox rows (earlier rounds were checked as the run went)
         if not device_mode and not arb_mode:
             timeset[start:] += 1e-3 * np.asarray(upd[start:])
         a0 = timed_start if timed_start is not None else start

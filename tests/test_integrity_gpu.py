@@ -7,8 +7,10 @@ the receiver-side check accepts clean rows and reports a flipped byte or a stale
 Engine level (ranks sharing the GPU over the IPC mailbox, like tests/test_multiproc_gpu.py): the
 sabotage hook flips one payload byte of one put AFTER its checksum (a torn put), and the run must
 fail with an error naming the round, the rank and the mailbox slot: on the host-driven master
-pump (the combine kernel checks), on the device arbiter (checked before beta is released) and
-for beta on a worker (checked behind the round that read it).  Also the per-pair preflight.
+pump (a check kernel queued behind the next round's beta and local gradient), on the device
+arbiter (the next round's idle waves check while wave 0 polls) and for beta on a worker (checked
+behind the round that read it).  All checks sit off the round's critical path.  Also the
+per-pair preflight.
 """
 import json
 import os
@@ -88,7 +90,8 @@ def test_sabotaged_message_fails_host_pump(tmp_path):
 
 
 def test_sabotaged_message_fails_arbiter(tmp_path):
-    _fails(3, 0, "device-driven round 4: message integrity check failed: round 4, rank 2's message",
+    # round 5's idle waves check round 4's rows while wave 0 polls: round 5 fails, naming round 4
+    _fails(3, 0, "device-driven round 5: message integrity check failed: round 4, rank 2's message",
            ERASUREHEAD_SABOTAGE="msg:2:4", ERASUREHEAD_DEVICE_MASTER="on", ERASUREHEAD_WORKER_WAIT="device",
            EH_TEST_ROUND_TIMEOUT="20", EH_TEST_OUT=str(tmp_path / "x.npz"))
 
