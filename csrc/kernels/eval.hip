@@ -273,8 +273,7 @@ hipError_t eval_gemm_loss_launch(int x_dtype, int loss_kind, const void* X, long
   const int xv = x_dtype == 0 ? 2 : (x_dtype == 1 ? 4 : 8), bv = x_dtype == 0 ? 2 : 4;
   const bool aligned = ldx % xv == 0 && ldb % bv == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0 &&
                        reinterpret_cast<uintptr_t>(B) % 16 == 0;
-  static const bool force_v1 = std::getenv("ERASUREHEAD_EVAL_V1") != nullptr;  // A/B benchmarking only
-  if (aligned && !force_v1) {
+  if (aligned) {
     const dim3 grid2(static_cast<unsigned>((n + kBM2 - 1) / kBM2), ceil_div(R, 16 * kNT2));
 #define EH_EVAL2(T, A, L) \
   hipLaunchKernelGGL((eval_gemm_loss_v2<T, A, L>), grid2, block, 0, st, (const T*)X, ldx, n, d, (const A*)y, (const A*)B, ldb, R, loss, (A*)P)

@@ -169,65 +169,6 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
   }
 }
 
-// ----- Replica bundles: one wave per co-located replica, all in one workgroup. -----
-// A workgroup holds R = blockDim/64 task slots (tasks[blockIdx.x * R + q] for wave q); the
-// tasks of a bundle read the SAME rows of the same partition for different messages (FRC group
-// members, cyclic neighbours).  Each wave walks every row of the range for its own message —
-// its own loads, dot product, residual with its own coefficient, gradient accumulation — and
-// writes its own slab row.  Because the replicas of a row are requested by waves of one CU at
-// nearly the same time, the repeated requests hit in that CU's L1 / merge in flight instead of
-// crossing to L2.  Unused slots have seg < 0 (the wave exits; no barrier is used).
-template <typename T, typename A, int CPL, int LOSS>
-__global__ void __launch_bounds__(512)
-grad_dense_bundle(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
-                  const A* __restrict__ beta, A* __restrict__ slab, int ld) {
-  constexpr int VN = Vec16<T>::N;
-  constexpr int NV = CPL / VN;
-  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6, R = blockDim.x >> 6;
-  const Task task = tasks[blockIdx.x * R + q];
-  if (task.seg < 0) return;
-  const Segment seg = segs[task.seg];
-  const T* __restrict__ X = static_cast<const T*>(seg.X);
-  const A* __restrict__ Y = static_cast<const A*>(seg.y);
-  const A coef = static_cast<A>(seg.coef);
-  A b[NV][VN], g[NV][VN];
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const int c0 = (j * kWave + lane) * VN;
-#pragma unroll
-    for (int v = 0; v < VN; ++v) {
-      b[j][v] = c0 < ld ? beta[c0 + v] : A(0);
-      g[j][v] = A(0);
-    }
-  }
-  for (int r = task.row_begin; r < task.row_end; ++r) {
-    using Rw = typename Vec16<T>::raw;
-    Rw xr[NV];
-    const auto rs = make_rsrc(X + static_cast<long long>(r) * ld, ld * static_cast<int>(sizeof(T)));
-#pragma unroll
-    for (int j = 0; j < NV; ++j) xr[j] = buf_load16<Rw>(rs, (j * kWave + lane) * VN * static_cast<int>(sizeof(T)));
-    A z = A(0);
-#pragma unroll
-    for (int j = 0; j < NV; ++j)
-#pragma unroll
-      for (int v = 0; v < VN; ++v) z = fma(Vec16<T>::template elem<A>(xr[j], v), b[j][v], z);
-    z = wave_allreduce_sum(z);
-    const A rr = residual<LOSS, A>(z, Y[r], coef);
-#pragma unroll
-    for (int j = 0; j < NV; ++j)
-#pragma unroll
-      for (int v = 0; v < VN; ++v) g[j][v] = fma(rr, Vec16<T>::template elem<A>(xr[j], v), g[j][v]);
-  }
-  A* out = slab + static_cast<long long>(task.slab) * ld;
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const int c0 = (j * kWave + lane) * VN;
-#pragma unroll
-    for (int v = 0; v < VN; ++v)
-      if (c0 + v < ld) out[c0 + v] = g[j][v];
-  }
-}
-
 // ----- Replica bundles in ONE wave: each row is loaded once, into registers, and every replica
 // computes its own message from there. -----
 // Same bundle table as grad_dense_bundle (R task slots reading the same rows); one wave per bundle.
@@ -386,18 +327,16 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
 // its own coefficient, and gradient accumulation — and writes its own slab row.  The rows of a
 // stage are contiguous in HBM, so a stage is one flat copy split into 1 KiB wave pieces (lane-
 // linear LDS image).  Labels ride along as one 4-byte-per-lane LDS-DMA piece.
-// EXT: the opt-in scheduling modes (persistent ticket loop, stage-walk rotation) are compiled in.
-// The default instantiation leaves them out: the bundle loop and the rotation cost the fp32 pair
-// kernel 13 VGPRs (80 -> 93, 6 -> 5 waves per SIMD: 0.77 -> 0.82 ms at the headline).
-template <typename T, typename A, int CPL, int LOSS, bool PAIR, bool EXT>
+// (A persistent-grid variant with an atomic bundle ticket and a stage-walk rotation were measured
+// slower and removed in round 3: docs/PERF_NOTES.md.)
+template <typename T, typename A, int CPL, int LOSS, bool PAIR>
 __global__ void __launch_bounds__(512)
 grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                   const A* __restrict__ beta, A* __restrict__ slab, int ld, int srows, int pieces, int nstage,
-                  int wpr, int nbundles, unsigned int* ticket, int rot_mul) {
+                  int wpr) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  __shared__ int s_next;
   // W waves = R task slots x wpr waves per slot; slot q's waves split each stage's rows
   const int lane = threadIdx.x & 63, W = blockDim.x >> 6, R = W / wpr;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -408,7 +347,7 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
   const int data_bytes = W * pieces * 1024;  // one stage buffer: data, then 256 B of labels
   const int buf_bytes = data_bytes + 256;
   using Rw = typename Vec16<T>::raw;
-  A b[NV][VN];  // beta, loaded once for every bundle this workgroup takes
+  A b[NV][VN];  // beta
   bool valid[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
@@ -417,12 +356,8 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
 #pragma unroll
     for (int v = 0; v < VN; ++v) b[j][v] = valid[j] ? beta[c0 + v] : A(0);
   }
-  // Persistent workgroups (ticket != nullptr): the grid holds as many workgroups as fit at once and
-  // each takes bundles until none is left — its first is blockIdx.x, the next ones come from an
-  // atomic ticket, so no workgroup idles while another still streams a partition (the single-wave
-  // tail of the sharded multi-GPU shapes).  The draw that hands out the launch's last ticket resets
-  // the counter for the next launch.  ticket == nullptr: one bundle per workgroup.
-  for (int bundle = blockIdx.x; bundle < nbundles;) {
+  {  // one bundle per workgroup
+    const int bundle = blockIdx.x;
     const Task lead = tasks[bundle * R];  // slot 0 of a bundle is always a real task
     const Task task = tasks[bundle * R + q];
     const bool active = task.seg >= 0;
@@ -432,11 +367,8 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
     const A coef = active ? static_cast<A>(segs[task.seg].coef) : A(0);
     const int nrows = lead.row_end - lead.row_begin;
     const int nst = (nrows + srows - 1) / srows;
-    // rot_mul > 0: each bundle walks its stages starting at a bundle-dependent offset (wrapping), so
-    // workgroups that start together do not stream the same relative addresses in lockstep
-    const int rot = EXT && rot_mul > 0 ? static_cast<int>((static_cast<long long>(bundle) * rot_mul) % nst) : 0;
-    auto stage_of = [&](int t) { return t + rot < nst ? t + rot : t + rot - nst; };
-    const int p_last = nst - 1 - rot;  // loop position of the (possibly partial) last stage
+    auto stage_of = [](int t) { return t; };
+    const int p_last = nst - 1;  // loop position of the (possibly partial) last stage
 
     // LDS-DMA loads wave w issues for a stage of nbytes: its 1 KiB pieces (+ labels: wave 0).  Every
     // stage but the last is full, so two counts cover the ring; computing them once keeps integer
@@ -466,7 +398,7 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
     for (int j = 0; j < NV; ++j)
 #pragma unroll
       for (int v = 0; v < VN; ++v) g[j][v] = A(0);
-    // beta (first bundle) / the previous bundle's slab stores retired before the counted loads
+    // beta retired before the counted loads
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int t = 0; t < nstage - 1 && t < nst; ++t) issue(t);
     for (int t = 0; t < nst; ++t) {
@@ -639,45 +571,26 @@ grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tas
           if (c0 + v < ld) out[c0 + v] = g[j][v];
       }
     }
-    if (!EXT || !ticket) break;
-    if (threadIdx.x == 0) {
-      const unsigned int raw = atomicAdd(ticket, 1u);
-      if (raw == static_cast<unsigned int>(nbundles) - 1u)  // the launch's last draw: reset for the next one
-        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_next = static_cast<int>(raw) + static_cast<int>(gridDim.x);
-    }
-    __syncthreads();  // s_next, and every wave is done with the ring before the next bundle's loads
-    bundle = s_next;
   }
 }
 
-// Stage geometry of grad_dense_staged: rows per stage, 1 KiB pieces per wave and ring depth.
-// Defaults measured at the headline (tools/sweep_staged.sh); ERASUREHEAD_STAGE_ROWS and
-// ERASUREHEAD_STAGES override them for sweeps.  Rows shrink until the ring fits kStagedLds.
-constexpr int kStagedLds = 160 * 1024 - 256;  // 160 KiB per workgroup, less the kernel's static LDS (s_next)
+// Stage geometry of grad_dense_staged: rows per stage, 1 KiB pieces per wave and ring depth, measured
+// at the headline (docs/PERF_NOTES.md): a 2-stage ring, about 4 waves per workgroup and 2 rows per
+// wave per stage (R = 3: 1 wave per replica, 2 rows; R = 2: 2 waves per replica, 4 rows).  Rows
+// shrink until the ring fits kStagedLds.
+constexpr int kStagedLds = 160 * 1024 - 256;  // 160 KiB per workgroup
 struct StagedGeom {
   int srows, pieces, nstage, wpr;
   size_t lds;
 };
-static inline int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
 // R task slots; fold_bytes_per_wave: one wave's gradient slice (64 * CPL accumulators);
-// want_wpr > 0: waves per replica requested by the plan (variant / 100), else the default below
+// want_wpr > 0: waves per replica chosen by the plan (KernelChoice::wpr), else the default above
 static inline bool staged_geometry(int R, int rowbytes, size_t fold_bytes_per_wave, StagedGeom* g, int want_wpr = 0) {
-  static const int env_rows = env_int("ERASUREHEAD_STAGE_ROWS", 0);
-  static const int env_stages = env_int("ERASUREHEAD_STAGES", 0);
-  static const int env_wpr = env_int("ERASUREHEAD_STAGED_WPR", 0);  // waves per replica slot
-  // defaults (tools/ab_staged_loss.sh): about 4 waves per workgroup and 2 rows per wave per
-  // stage — R = 3: 1 wave per replica, 2 rows; R = 2: 2 waves per replica, 4 rows
-  const int ns = env_stages >= 2 && env_stages <= 8 ? env_stages : 2;
-  const int wpr = env_wpr >= 1 && env_wpr <= 4 && R * env_wpr <= 8 ? env_wpr
-                  : want_wpr >= 1 && want_wpr <= 4 && R * want_wpr <= 8 ? want_wpr
-                                                                       : std::max(1, 4 / R);
+  const int ns = 2;
+  const int wpr = want_wpr >= 1 && want_wpr <= 4 && R * want_wpr <= 8 ? want_wpr : std::max(1, 4 / R);
   const int W = R * wpr;
   const size_t fold = static_cast<size_t>(wpr - 1) * R * fold_bytes_per_wave;
-  int s = env_rows > 0 ? std::min(env_rows, 32) : 2 * wpr;
+  int s = 2 * wpr;
   for (; s >= 1; --s) {
     const int p = (s * rowbytes + W * 1024 - 1) / (W * 1024);
     const size_t bytes = std::max(fold, static_cast<size_t>(ns) * (static_cast<size_t>(W) * p * 1024 + 256));
@@ -1096,52 +1009,6 @@ static hipError_t launch_wide(int bs, const Segment* segs, const Task* tasks, in
   return hipGetLastError();
 }
 
-// Kernel variant of grad_dense_fused per storage type (tools/sweep_grad_rows.sh,
-// docs/PERF_NOTES.md), measured at full headline scale:
-//   1 / 2 / 4  beta in registers, 1 row / the interleaved pair kernel / 4 rows in flight
-//   5 / 6 / 7  beta in LDS, 1 / 2 / 4 rows in flight
-// fp64 -> 6 (frees 32 VGPRs: 2 rows at 3 waves/SIMD), fp32 -> 4, bf16 -> 1.
-// ERASUREHEAD_GRAD_ROWS overrides (sweeps only).
-// The plan may request a variant (DenseGradPlan.variant: replica-shared vs distinct rows).
-template <typename T>
-static int fused_rows(int requested) {
-  static const int env = [] {
-    const char* e = std::getenv("ERASUREHEAD_GRAD_ROWS");
-    return e ? std::atoi(e) : 0;
-  }();
-  auto ok = [](int v) { return v >= 1 && v <= 7 && v != 3; };
-  if (ok(env)) return env;
-  if (ok(requested)) return requested;
-  if (std::is_same<T, double>::value) return 6;
-  return std::is_same<T, float>::value ? 4 : 1;
-}
-
-// ERASUREHEAD_STAGE_ROTATE=k > 0: bundle b starts its stage walk at (b * k) mod stages (A/B knob).
-static int stage_rotate() {
-  static const int k = env_int("ERASUREHEAD_STAGE_ROTATE", 0);
-  return k;
-}
-
-// Workgroups of a staged kernel resident at once on the whole device (persistent grid size).
-static int staged_slots(const void* kern, int block, size_t lds) {
-  static std::mutex mu;
-  static std::map<std::tuple<const void*, int, size_t>, int> cache;
-  std::lock_guard<std::mutex> lock(mu);
-  const auto key = std::make_tuple(kern, block, lds);
-  auto it = cache.find(key);
-  if (it != cache.end()) return it->second;
-  static const int env_per_cu = env_int("ERASUREHEAD_PERSISTENT_PER_CU", 0);  // A/B override
-  int dev = 0, cus = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds) != hipSuccess || cus <= 0 || per_cu <= 0)
-    return 1 << 30;  // unknown: no persistence (grid = bundles)
-  if (env_per_cu > 0) per_cu = env_per_cu;
-  if (std::getenv("ERASUREHEAD_PERSISTENT_VERBOSE"))
-    std::fprintf(stderr, "[erasurehead] persistent staged grid: %d CUs x %d workgroups (block %d, LDS %zu)\n", cus,
-                 per_cu, block, lds);
-  return cache[key] = cus * per_cu;
-}
-
 // grad_dense_multi launch; the folded form takes 3 waves' accumulators in dynamic LDS.
 template <typename T, typename A, int C, int LOSS, int R>
 static hipError_t launch_multi(bool fold, bool lane_epi, dim3 grid, dim3 block, hipStream_t st, const Segment* segs,
@@ -1163,107 +1030,71 @@ static hipError_t launch_multi(bool fold, bool lane_epi, dim3 grid, dim3 block, 
 
 template <typename T, typename A, int LOSS>
 static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
-                                   const A* beta, A* slab, int ld, hipStream_t st, int variant,
-                                   unsigned int* ticket) {
-  if (variant < 1000) ticket = nullptr;  // staged bundles: persistent workgroups requested by the plan
-  variant %= 1000;
-  const int want_wpr = variant / 100;  // staged bundles: waves per replica requested by the plan
-  variant %= 100;
-  if (variant > 40 && variant <= 56) {  // bf16 replica bundles on MFMA (grad_mfma.hip), R = variant - 40
+                                   const A* beta, A* slab, int ld, hipStream_t st, const KernelChoice& k) {
+  if (k.kind == kGradMfma) {  // bf16 replica bundles on the matrix cores (grad_mfma.hip)
     if constexpr (std::is_same<T, bf16_t>::value)
-      return grad_mfma_launch(LOSS, segs, tasks, ntasks, variant - 40, beta, slab, ld, st);
+      return grad_mfma_launch(LOSS, segs, tasks, ntasks, k.replicas, beta, slab, ld, st);
     return hipErrorInvalidValue;
   }
-  if (cpl >= 256) return launch_wide<T, A, LOSS>(cpl, segs, tasks, ntasks, beta, slab, ld, st);
+  if (k.kind == kGradWide || cpl >= 256) return launch_wide<T, A, LOSS>(cpl, segs, tasks, ntasks, beta, slab, ld, st);
+  const int R = k.replicas;
+  const bool bundled = k.kind == kGradStaged || k.kind == kGradMulti;
+  if (bundled && (R < 1 || ntasks % R != 0)) return hipErrorInvalidValue;
+  StagedGeom sg{};
+  if (k.kind == kGradStaged &&
+      (R > 8 || !staged_geometry(R, ld * static_cast<int>(sizeof(T)), 64ull * cpl * sizeof(A), &sg, k.wpr)))
+    return hipErrorInvalidValue;
+  constexpr int VN = Vec16<T>::N;
   const dim3 block(256);
   const dim3 grid(ntasks);
-  constexpr int VN = Vec16<T>::N;
   // CPL (columns per lane) must be a multiple of the 16-byte vector width VN.
-  const int rows = fused_rows<T>(variant);
-  // variant 10 + R (R = 1..8): replica-bundle kernel, R task slots (waves) per workgroup
-  // variant 20 + R / 30 + R: the same bundle table, rows staged through LDS (grad_dense_staged,
-  // one row per wave step / two rows sharing one reduction and residual evaluation)
-  const bool staged_pair = variant > 30 && variant <= 38;
-  const int staged_r = variant > 20 && variant <= 28 ? variant - 20 : staged_pair ? variant - 30 : 0;
-  // variant 60 + R (R = 1..3, fp64/fp32, d <= 1024): one wave per bundle computing all R replicas
-  // (grad_dense_multi)
-  // variant 70 + R: the same with the workgroup fold (plan-built table in workgroups of 4 bundles)
-  // variant 90 + R: folded, reduce-scatter + one-lane-per-replica epilogue (sharded ranks)
-  const bool multi_lane = variant > 90 && variant <= 93;
-  const bool multi_fold = (variant > 70 && variant <= 73) || multi_lane;
-  const int multi_r = variant > 60 && variant <= 63 ? variant - 60
-                      : multi_lane ? variant - 90 : multi_fold ? variant - 70 : 0;
-  const int bundle_r = variant > 10 && variant <= 18 ? variant - 10 : staged_r ? staged_r : multi_r;
-  if (bundle_r && ntasks % bundle_r != 0) return hipErrorInvalidValue;
-  StagedGeom sg{};
-  if (staged_r && !staged_geometry(staged_r, ld * static_cast<int>(sizeof(T)), 64ull * cpl * sizeof(A), &sg, want_wpr))
-    return hipErrorInvalidValue;
-#define EH_IF(C)                                                                          \
-  case C:                                                                                 \
-    if constexpr (C % VN == 0) {                                                          \
-      if (staged_r) {                                                                     \
-        const bool ext_ = ticket != nullptr || stage_rotate() > 0;                        \
-        auto kern = staged_pair ? (ext_ ? grad_dense_staged<T, A, C, LOSS, true, true>    \
-                                        : grad_dense_staged<T, A, C, LOSS, true, false>)  \
-                                : (ext_ ? grad_dense_staged<T, A, C, LOSS, false, true>   \
-                                        : grad_dense_staged<T, A, C, LOSS, false, false>); \
-        if (sg.lds > 65536) {                                                             \
-          const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),   \
-              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sg.lds));      \
-          if (ea != hipSuccess) return ea;                                                \
-        }                                                                                 \
-        const int nb_ = ntasks / staged_r;                                                \
-        const int grid_ = ticket ? std::min(nb_, staged_slots(reinterpret_cast<const void*>(kern), \
-                              64 * staged_r * sg.wpr, sg.lds)) : nb_;                      \
-        hipLaunchKernelGGL(kern, dim3(grid_), dim3(64 * staged_r * sg.wpr),                \
-                           sg.lds, st, segs, tasks, beta, slab, ld, sg.srows, sg.pieces,  \
-                           sg.nstage, sg.wpr, nb_, grid_ < nb_ ? ticket : nullptr,        \
-                           stage_rotate());                                               \
-        return hipGetLastError();                                                         \
-      }                                                                                   \
-      if (multi_r) {                                                                      \
-        if constexpr (C <= 16 && !std::is_same<T, bf16_t>::value) {                       \
-          const int nb_ = ntasks / multi_r;                                               \
-          if (multi_fold && nb_ % 4) return hipErrorInvalidValue;                         \
-          const dim3 mg((nb_ + 3) / 4), mb(256);                                          \
-          if (multi_r == 1)                                                               \
-            return launch_multi<T, A, C, LOSS, 1>(multi_fold, multi_lane, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
-          else if (multi_r == 2)                                                          \
-            return launch_multi<T, A, C, LOSS, 2>(multi_fold, multi_lane, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
-          else                                                                            \
-            return launch_multi<T, A, C, LOSS, 3>(multi_fold, multi_lane, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
-        } else {                                                                          \
-          return hipErrorInvalidValue;                                                    \
-        }                                                                                 \
-      }                                                                                   \
-      if (bundle_r) {                                                                     \
-        hipLaunchKernelGGL((grad_dense_bundle<T, A, C, LOSS>), dim3(ntasks / bundle_r),   \
-                           dim3(64 * bundle_r), 0, st, segs, tasks, beta, slab, ld);       \
-        return hipGetLastError();                                                         \
-      }                                                                                   \
-      const size_t sh = 4ull * kWave * C * sizeof(A);                                     \
-      const size_t shb = sh + kWave * C * sizeof(A);                                      \
-      if (rows == 5)                                                                      \
-        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1, true>), grid, block, shb,  \
-                           st, segs, tasks, beta, slab, ld);                              \
-      else if (rows == 6)                                                                 \
-        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 2, true>), grid, block, shb,  \
-                           st, segs, tasks, beta, slab, ld);                              \
-      else if (rows == 7)                                                                 \
-        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 4, true>), grid, block, shb,  \
-                           st, segs, tasks, beta, slab, ld);                              \
-      else if (rows == 1)                                                                 \
-        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1>), grid, block, sh, st,     \
-                           segs, tasks, beta, slab, ld);                                  \
-      else if (rows == 4)                                                                 \
-        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 4>), grid, block, sh, st,     \
-                           segs, tasks, beta, slab, ld);                                  \
-      else                                                                                \
-        hipLaunchKernelGGL((grad_dense_fused_pair<T, A, C, LOSS>), grid, block, sh, st,   \
-                           segs, tasks, beta, slab, ld);                                  \
-      return hipGetLastError();                                                           \
-    } else {                                                                              \
-      return hipErrorInvalidValue;                                                        \
+#define EH_IF(C)                                                                                       \
+  case C:                                                                                              \
+    if constexpr (C % VN == 0) {                                                                       \
+      if (k.kind == kGradStaged) { /* rows streamed once through an LDS ring, one wave per replica */  \
+        auto kern = k.pair ? grad_dense_staged<T, A, C, LOSS, true> : grad_dense_staged<T, A, C, LOSS, false>; \
+        if (sg.lds > 65536) {                                                                          \
+          const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),                \
+              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sg.lds));                   \
+          if (ea != hipSuccess) return ea;                                                             \
+        }                                                                                              \
+        hipLaunchKernelGGL(kern, dim3(ntasks / R), dim3(64 * R * sg.wpr), sg.lds, st, segs, tasks, beta, \
+                           slab, ld, sg.srows, sg.pieces, sg.nstage, sg.wpr);                          \
+        return hipGetLastError();                                                                      \
+      }                                                                                                \
+      if (k.kind == kGradMulti) { /* every replica of a bundle in one wave, rows in registers */       \
+        if constexpr (C <= 16 && !std::is_same<T, bf16_t>::value) {                                    \
+          const int nb_ = ntasks / R;                                                                  \
+          if (k.fold && nb_ % 4) return hipErrorInvalidValue;                                          \
+          const dim3 mg((nb_ + 3) / 4), mb(256);                                                       \
+          const bool f = k.fold != 0, le = k.lane_epi != 0;                                            \
+          if (R == 1) return launch_multi<T, A, C, LOSS, 1>(f, le, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
+          if (R == 2) return launch_multi<T, A, C, LOSS, 2>(f, le, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
+          if (R == 3) return launch_multi<T, A, C, LOSS, 3>(f, le, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
+        }                                                                                              \
+        return hipErrorInvalidValue;                                                                   \
+      }                                                                                                \
+      /* fused: a wave per row, k.rows rows in flight (2: the interleaved pair kernel), beta in      \
+         registers or LDS */                                                                           \
+      const size_t sh = 4ull * kWave * C * sizeof(A);                                                  \
+      const size_t shb = sh + kWave * C * sizeof(A);                                                   \
+      if (k.beta_lds) {                                                                                \
+        if (k.rows == 1)                                                                               \
+          hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1, true>), grid, block, shb, st, segs, tasks, beta, slab, ld); \
+        else if (k.rows == 2)                                                                          \
+          hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 2, true>), grid, block, shb, st, segs, tasks, beta, slab, ld); \
+        else                                                                                           \
+          hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 4, true>), grid, block, shb, st, segs, tasks, beta, slab, ld); \
+      } else if (k.rows == 1) {                                                                        \
+        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1>), grid, block, sh, st, segs, tasks, beta, slab, ld); \
+      } else if (k.rows == 4) {                                                                        \
+        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 4>), grid, block, sh, st, segs, tasks, beta, slab, ld); \
+      } else {                                                                                         \
+        hipLaunchKernelGGL((grad_dense_fused_pair<T, A, C, LOSS>), grid, block, sh, st, segs, tasks, beta, slab, ld); \
+      }                                                                                                \
+      return hipGetLastError();                                                                        \
+    } else {                                                                                           \
+      return hipErrorInvalidValue;                                                                     \
     }
   switch (cpl) {
     EH_IF(2)
@@ -1280,27 +1111,23 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
 // dtype codes: 0 = fp64 storage/fp64 acc, 1 = fp32/fp32, 2 = bf16 storage/fp32 acc
 hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
                              int ntasks, const void* beta, void* slab, const int* slot_task_begin,
-                             int nslots, void* part, void* G, int ld, hipStream_t st, int variant,
+                             int nslots, void* part, void* G, int ld, hipStream_t st, const KernelChoice& k,
                              const PutDesc* put) {
   const Segment* S = static_cast<const Segment*>(segs);
   const Task* Tk = static_cast<const Task*>(tasks);
-  // the staged kernels' persistent-grid ticket lives right after the partial sums (slab_part_bytes);
-  // used when the plan's variant asks for persistent workgroups (>= 1000)
-  unsigned int* tk = reinterpret_cast<unsigned int*>(static_cast<char*>(part) +
-                                                     slab_part_bytes(nslots, ld, dtype == 0 ? 8 : 4) - 16);
   hipError_t e = hipSuccess;
   if (dtype == 0) {
     e = loss == kLogistic
-            ? launch_fused_cpl<double, double, kLogistic>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, variant, tk)
-            : launch_fused_cpl<double, double, kLeastSquares>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, variant, tk);
+            ? launch_fused_cpl<double, double, kLogistic>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, k)
+            : launch_fused_cpl<double, double, kLeastSquares>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, k);
   } else if (dtype == 1) {
     e = loss == kLogistic
-            ? launch_fused_cpl<float, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant, tk)
-            : launch_fused_cpl<float, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant, tk);
+            ? launch_fused_cpl<float, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k)
+            : launch_fused_cpl<float, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k);
   } else {
     e = loss == kLogistic
-            ? launch_fused_cpl<bf16_t, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant, tk)
-            : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, variant, tk);
+            ? launch_fused_cpl<bf16_t, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k)
+            : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k);
   }
   if (e != hipSuccess) return e;
   if (dtype == 0) return slab_reduce_launch<double>((const double*)slab, slot_task_begin, (double*)part, (double*)G, nslots, ld, st, put);

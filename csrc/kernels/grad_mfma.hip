@@ -282,17 +282,12 @@ hipError_t tr_probe_launch(const float* tile, int rowlen, float* out, hipStream_
   return hipGetLastError();
 }
 
-// Geometry of grad_staged_mfma: rows per stage S (32, 2-stage ring, the default: 0.48 vs 0.59 ms
-// for 16-row stages in a 4-deep ring at the bf16 headline, profiles/r2_mfma), LDS-DMA pieces per
-// wave per stage, ring depth and LDS bytes; false when ld does not fit.
-// ERASUREHEAD_MFMA_ROWS=16 selects the 16-row form (A/B runs).
+// Geometry of grad_staged_mfma: rows per stage S (32, 2-stage ring: 0.48 vs 0.59 ms for 16-row
+// stages in a 4-deep ring at the bf16 headline, profiles/r2_mfma), LDS-DMA pieces per wave per
+// stage, ring depth and LDS bytes; false when ld does not fit.
 bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds) {
   if (ld < 8 || ld > kMfNW * kMfKPW * 32 || ld % 8) return false;
-  static const int env_rows = [] {
-    const char* e = std::getenv("ERASUREHEAD_MFMA_ROWS");
-    return e ? std::atoi(e) : 0;
-  }();
-  const int S = env_rows == 16 ? 16 : 32;  // measured: 32-row stages (fewer barriers per byte) win
+  const int S = 32;  // measured: 32-row stages (fewer barriers per byte) win
   const int rowbytes = ld * 2;
   *rows = S;
   *pieces = (S * rowbytes + kMfNW * 1024 - 1) / (kMfNW * 1024);

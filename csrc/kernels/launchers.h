@@ -13,21 +13,21 @@ namespace eh {
 
 // ---- worker gradient (grad_dense.hip, grad_sparse.hip) -------------------------------
 // dtype: 0 fp64 storage/acc, 1 fp32/fp32, 2 bf16 storage/fp32 acc; loss: 0 logistic, 1 least squares
-// variant: 0 = per-dtype default, else the grad_dense_fused variant (grad_dense.hip fused_rows)
+// k: the kernel the plan chose (grad_dense.h KernelChoice)
 // Slab-reduction scratch of the dense launchers ("part"): [nslots][kSlabSplits][ld] partial sums in
-// the accumulator type, then 16 bytes holding the staged kernels' persistent-grid ticket (zero when
-// allocated; every launch leaves it zero).
+// the accumulator type.
 constexpr long long kSlabSplits = 16;  // grad_dense.hip kSplits
 inline long long slab_part_bytes(long long nslots, long long ld, long long acc_bytes) {
-  return nslots * kSlabSplits * ld * acc_bytes + 16;
+  return nslots * kSlabSplits * ld * acc_bytes;
 }
 
 struct PutDesc;
+struct KernelChoice;
 // put (optional): fuse the message put + signal into the final slab reduction; put->dst
 // receives the nslots x ld result rows, put->bytes is ignored.
 hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
                              int ntasks, const void* beta, void* slab, const int* slot_task_begin,
-                             int nslots, void* part, void* G, int ld, hipStream_t st, int variant = 0,
+                             int nslots, void* part, void* G, int ld, hipStream_t st, const KernelChoice& k,
                              const PutDesc* put = nullptr);
 hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, const void* tasks,
                                      int ntasks, const void* beta, const int* task_row_off,

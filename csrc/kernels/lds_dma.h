@@ -9,8 +9,8 @@ namespace eh {
 // the builtin, hipcc cannot tell the stage being filled from the one being read and waits vmcnt(0)
 // before every ds_read, which drains the prefetch (checked in the .s).  The kernels count and wait
 // for their own loads instead: "stage t landed" is vmcnt <= the loads this wave issued for the
-// stages after t.  ERASUREHEAD_FULL_VMCNT=1 (a build-time define, see wait_vmcnt) turns every such
-// wait into vmcnt(0) for A/B checks of a suspected LDS race.
+// stages after t (tests/test_isa_checks.py checks the compiler adds no loads of its own inside the
+// counted stage loop; -DEH_FULL_VMCNT turns every such wait into vmcnt(0) for a suspected LDS race).
 __device__ __forceinline__ void glds16(const void* g, unsigned lds) {
   int keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -25,7 +25,7 @@ __device__ __forceinline__ void glds4(const void* g, unsigned lds) {
 // for 63, which is stricter and therefore safe).
 __device__ __forceinline__ void wait_vmcnt(int n) {
 #ifdef EH_FULL_VMCNT
-  n = 0;  // debug build: every stage wait drains all loads (tools/build_ext.py ERASUREHEAD_FULL_VMCNT=1)
+  n = 0;  // debug build: every stage wait drains all loads
 #endif
   // The two-stage ring (the default) always waits for everything: test that first.  Testing a
   // readfirstlane copy keeps the compiler from folding it into the switch's compare tree.

@@ -47,6 +47,7 @@
 #include <cstdlib>
 
 #include "kernels/arbiter.h"
+#include "kernels/grad_dense.h"
 #include "kernels/launchers.h"
 #include "runtime/collector.h"
 #include "runtime/comm.h"
@@ -99,7 +100,8 @@ void need_gpu(const Tensor& t, const char* name) {
 // launcher also holds references.
 struct GradLauncher {
   int kind = 0;  // 0 dense fused, 1 dense two-pass, 2 sparse
-  int dtype = 0, loss = 0, cpl = 0, ntasks = 0, nslots = 0, ld = 0, variant = 0;
+  int dtype = 0, loss = 0, cpl = 0, ntasks = 0, nslots = 0, ld = 0;
+  eh::KernelChoice choice{};
   const void* segs = nullptr;
   const void* tasks = nullptr;
   void* slab = nullptr;
@@ -146,14 +148,14 @@ struct GradLauncher {
   bool can_fuse_put(int rows) const { return kind == 0 && !Gb && ntasks > 0 && nslots == rows; }
   hipError_t launch_put(const void* beta, void* G, const eh::PutDesc& put, hipStream_t st) const {
     return eh::grad_dense_launch(dtype, loss, cpl, segs, tasks, ntasks, beta, slab, stb, nslots, part, G, ld, st,
-                                 variant, &put);
+                                 choice, &put);
   }
 
   hipError_t launch_raw(const void* beta, void* G, hipStream_t st) const {
     switch (kind) {
       case 0:
         return ntasks ? eh::grad_dense_launch(dtype, loss, cpl, segs, tasks, ntasks, beta, slab, stb, nslots, part, G,
-                                              ld, st, variant)
+                                              ld, st, choice)
                       : hipSuccess;
       case 1:
         return ntasks ? eh::grad_dense_twopass_launch(dtype, loss, segs, tasks, ntasks, beta, task_row_off, rbuf, slab,
@@ -174,7 +176,7 @@ struct GradLauncher {
 std::shared_ptr<GradLauncher> make_dense(int64_t dtype, int64_t loss, int64_t cpl, const Tensor& segs,
                                          const Tensor& tasks, const Tensor& slab, const Tensor& stb,
                                          const Tensor& part, int64_t ld, std::optional<Tensor> task_row_off,
-                                         std::optional<Tensor> rbuf, int64_t variant) {
+                                         std::optional<Tensor> rbuf, const eh::KernelChoice& choice) {
   for (auto* t : {&segs, &tasks, &slab, &stb, &part}) need_gpu(*t, "dense plan operand");
   need(tasks.dim() == 2 && tasks.size(1) == 5 && tasks.scalar_type() == at::kInt, "tasks must be int32 [n,5]");
   need(stb.scalar_type() == at::kInt, "slot_task_begin must be int32");
@@ -182,12 +184,12 @@ std::shared_ptr<GradLauncher> make_dense(int64_t dtype, int64_t loss, int64_t cp
   g->dtype = (int)dtype;
   g->loss = (int)loss;
   g->cpl = (int)cpl;
-  g->variant = (int)variant;
+  g->choice = choice;
   g->ld = (int)ld;
   g->ntasks = (int)tasks.size(0);
   g->nslots = (int)stb.numel() - 1;
   need(part.numel() * part.element_size() >= eh::slab_part_bytes(g->nslots, ld, dtype == 0 ? 8 : 4),
-       "part must hold the partial sums + the persistent-grid ticket (grad.py DenseGradPlan)");
+       "part must hold the slab partial sums (grad.py DenseGradPlan)");
   g->segs = segs.data_ptr();
   g->tasks = tasks.data_ptr();
   g->slab = slab.data_ptr();
@@ -297,7 +299,8 @@ struct HostMapped {
 };
 
 // Test hook ERASUREHEAD_SABOTAGE=<what>:<rank>:<round> (what: msg | beta): the named put flips one
-// payload byte after its checksum, so the receiver must report a torn message.
+// payload byte after its checksum, so the receiver must report a torn message.  ("handshake:<rank>":
+// that rank never answers the IPC handshake, parallel/transport.py.)
 bool sabotage(const char* what, int rank, int round) {
   static const std::string spec = [] {
     const char* e = std::getenv("ERASUREHEAD_SABOTAGE");
@@ -1295,8 +1298,7 @@ class WorkerPump {
     g_rows_ = (int)G.size(1);
     stream_ = c10::hip::getCurrentHIPStream(device).stream();
     wait_s_.assign(R_, -1.0);
-    const char* e = std::getenv("ERASUREHEAD_FUSED_PUT");
-    fuse_put_ = g_->can_fuse_put(n_loc) && !(e && e[0] == '0');
+    fuse_put_ = g_->can_fuse_put(n_loc);
     // Device-side beta wait: the stream itself waits for the flag (hipStreamWaitValue64 on the
     // host-registered shared flag), so round i's kernels are already queued when beta(i) lands
     // instead of after a host wake-up + launch.  The host stays one round ahead and keeps the
@@ -1598,7 +1600,8 @@ void bind_engine(py::module& m) {
   py::class_<GradLauncher, std::shared_ptr<GradLauncher>>(m, "GradLauncher")
       .def_static("dense", &make_dense, py::arg("dtype"), py::arg("loss"), py::arg("cpl"), py::arg("segs"),
                   py::arg("tasks"), py::arg("slab"), py::arg("slot_task_begin"), py::arg("part"), py::arg("ld"),
-                  py::arg("task_row_off") = py::none(), py::arg("rbuf") = py::none(), py::arg("variant") = 0)
+                  py::arg("task_row_off") = py::none(), py::arg("rbuf") = py::none(),
+                  py::arg("choice") = eh::KernelChoice{})
       .def_static("sparse", &make_sparse, py::arg("loss"), py::arg("row_ptr"), py::arg("col_idx"), py::arg("vals"),
                   py::arg("y"), py::arg("coef"), py::arg("rbuf"), py::arg("keys"), py::arg("rows"), py::arg("cvals"),
                   py::arg("nslots"), py::arg("ld"))

@@ -88,6 +88,10 @@ def native(build_if_missing: bool = True):
             build()
             importlib.invalidate_caches()
             check_fresh()
+        # torch first: _C links torch's libraries (and its RCCL); initialised in the other order, the
+        # process aborts at exit with a corrupted heap ("corrupted size vs. prev_size")
+        import torch  # noqa: F401
+
         try:
             mod = importlib.import_module("erasurehead_amd._C")
         except ImportError as e:

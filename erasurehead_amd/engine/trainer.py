@@ -510,22 +510,11 @@ class Trainer:
         """Which gradient kernel this rank's plan launches (bench.py per-rank breakdown)."""
         plan = getattr(self, "plan", None)
         inner = getattr(plan, "inner", plan)  # SharedPlan wraps a dense plan
-        if inner is None or not hasattr(inner, "variant"):
+        if inner is None or not hasattr(inner, "choice"):
             return type(plan).__name__ if plan is not None else None
         if getattr(inner, "device", None) is not None and inner.device.type != "cuda":
             return "torch reference path (CPU)"
-        if getattr(inner, "multi", False):
-            kind = "one-wave bundles" + (" (folded)" if getattr(inner, "fold", False) else "")
-        elif getattr(inner, "mfma", False):
-            kind = "MFMA bundles"
-        elif getattr(inner, "staged", False):
-            kind = "LDS-staged bundles" + (" (pair)" if getattr(inner, "staged_pair", False) else "")
-        elif getattr(inner, "bundle_rows", 0):
-            kind = "bundle kernel"
-        else:
-            kind = "fused"
-        rows = getattr(inner, "bundle_rows", 0)
-        return f"{kind}, variant {inner.variant}" + (f", {rows}-row bundles" if rows else "")
+        return inner.choice.label()
 
     def _master_loop_native(self, timed_start, log, start: int = 0) -> TrainResult:
         """Master rounds in csrc/runtime/engine.cpp (MasterPump); Python only keeps the books."""

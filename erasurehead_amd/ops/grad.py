@@ -16,8 +16,8 @@ native kernels are mandatory (:func:`erasurehead_amd._ext.native` raises if abse
 from __future__ import annotations
 
 import collections
-import os
 import struct
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -31,23 +31,137 @@ _SEG = struct.Struct("<QQdq")  # csrc Segment {const void* X; const void* y; dou
 MAX_CPL = 32
 DEFAULT_TASKS = 2048
 REPLICA_TASKS = 4096
-MAX_BUNDLE = 8  # replica task slots (waves) per workgroup of grad_dense_bundle / _staged
-STAGED_ROWS = 512  # rows per bundle task of grad_dense_staged (measured: 512 > 256, 1024; 2048 leaves CUs idle)
-SHARD_STAGED_ROWS = 128  # rows per bundle task when a rank holds < SHARD_ROWS distinct rows (multi-GPU shards)
-
-
-def multi_bundle_rows(distinct_rows: int, fp32: bool = False) -> int:
-    """Rows per one-wave bundle of grad_dense_multi, in multiples of 64 (tools/sweep_multi_rows.sh,
-    profiles/r3_multi).  fp64 (244 VGPRs, 2 waves per SIMD): about 2000 bundles, 1300 at the
-    one-GPU headline (N=1 768 rows 1.330 ms vs 512 1.36 / 640 1.37 / 1024 1.54; N=2 256 rows 0.708;
-    N=4 128 rows 0.370 vs 96 0.45 / 160 0.40; N=8 64 rows 0.206 vs 48 0.25 / 80 0.22).  fp32
-    (155 VGPRs, 3 waves per SIMD): about 2600 bundles, just under the 3072 wave slots (N=1 384
-    rows 0.692 ms; 320 rows = 3125 bundles needs a second pass: 0.95)."""
-    waves = 2600 if fp32 else 1300 if distinct_rows >= 750_000 else 1953
-    return max(64, 64 * int(round(distinct_rows / waves / 64)))
-SHARD_ROWS = 800_000
+MAX_BUNDLE = 8  # replica task slots (waves) per workgroup of grad_dense_staged
 MIN_ROWS_PER_TASK = 32
 SLAB_SPLITS = 16  # csrc/kernels/grad_dense.hip kSplits
+N_CUS = 256  # MI355X compute units (8 XCDs x 32)
+# A rank streams in the "long-stream" regime when each CU reads at least this many distinct rows per
+# round: there the gradient is HBM-bound with fewer, longer bundles (their per-bundle beta load,
+# fold and slab write amortise over more rows), below it the grid must fill every wave slot.  The
+# measured crossover lies between 500k and 1e6 rows of 1000 columns on 256 CUs (N = 2 vs N = 1 of
+# the headline, profiles/r3_multi, r3_epi); 2900 rows per CU (~742k rows) sits in between.
+LONG_STREAM_ROWS_PER_CU = 2900
+
+KIND_IDS = {"fused": 0, "multi": 1, "staged": 2, "mfma": 3, "wide": 4, "twopass": -1}
+
+
+@dataclass(frozen=True)
+class KernelChoice:
+    """The dense-gradient kernel a plan launches (csrc/kernels/grad_dense.h KernelChoice).
+
+    kind     fused    a wave per row, ``rows`` rows in flight (2: the interleaved pair kernel),
+                      beta in registers or LDS (``beta_lds``); distinct rows, or replicas with the
+                      replica-interleaved dispatch (``interleave``)
+             multi    one-wave replica bundles: each row loaded once into registers, every one of the
+                      ``replicas`` co-located messages computed from it (``fold``: 4 bundles of one
+                      partition per workgroup folded through LDS; ``lane_epi``: reduce-scatter
+                      epilogue with one lane per replica)
+             staged   replica bundles streamed through an LDS ring, a wave per replica (``pair``: two
+                      rows per step share one reduction; ``wpr`` waves per replica)
+             mfma     bf16 replica bundles on the matrix cores
+             wide     a workgroup per row (2048 < d <= 8192 fp64 / 16384 fp32)
+             twopass  wider rows / bf16 beyond the one-pass kernels: two passes over X
+    bundle_rows  rows per bundle task (bundle kinds)
+    """
+    kind: str
+    replicas: int = 1
+    bundle_rows: int = 0
+    fold: bool = False
+    lane_epi: bool = False
+    pair: bool = False
+    wpr: int = 0
+    rows: int = 2
+    beta_lds: bool = False
+    interleave: bool = False
+
+    @property
+    def bundled(self) -> bool:
+        return self.kind in ("multi", "staged", "mfma")
+
+    def native(self):
+        """The C++ struct (csrc/kernels/grad_dense.h) passed to the launchers."""
+        return native().KernelChoice(kind=KIND_IDS[self.kind], replicas=self.replicas, fold=int(self.fold),
+                                     lane_epi=int(self.lane_epi), pair=int(self.pair), wpr=self.wpr,
+                                     rows=self.rows, beta_lds=int(self.beta_lds))
+
+    def label(self) -> str:
+        name = {"fused": "fused", "multi": "one-wave bundles", "staged": "LDS-staged bundles", "mfma": "MFMA bundles",
+                "wide": "wide rows", "twopass": "two-pass"}[self.kind]
+        opts = [o for o, on in (("folded", self.fold), ("lane epilogue", self.lane_epi), ("pair", self.pair),
+                                ("interleaved", self.interleave)) if on]
+        out = name + (f" ({', '.join(opts)})" if opts else "")
+        if self.bundled:
+            out += f", R={self.replicas}, {self.bundle_rows}-row bundles"
+        elif self.kind == "fused":
+            out += f", {self.rows} rows in flight" + (", beta in LDS" if self.beta_lds else "")
+        return out
+
+
+def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS) -> int:
+    """Rows per one-wave bundle of grad_dense_multi, in multiples of 64, from the rows per CU.
+
+    Resident one-wave bundles per CU: 8 fp64 (244 VGPRs, 2 waves per SIMD), 12 fp32 (155 VGPRs,
+    3 per SIMD).  Below the long-stream regime a rank fills every slot (one bundle per wave slot);
+    in it, fewer, longer bundles win (HBM-bound: ~10 MB of rows in flight already saturate it, and
+    each bundle's beta load / fold / slab write amortises over more rows): 5 bundles per CU fp64,
+    10 fp32.  Measured (tools/sweep_multi_rows.sh, profiles/r3_multi): N=1 fp64 768 rows 1.330 ms vs
+    512 1.36 / 640 1.37 / 1024 1.54; N=2 256 rows 0.708; N=4 128 rows 0.370 vs 96 0.45 / 160 0.40;
+    N=8 64 rows 0.206 vs 48 0.25 / 80 0.22; fp32 N=1 384 rows 0.692 (320: 0.95, a second pass)."""
+    long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
+    per_cu = (10 if long_stream else 12) if fp32 else (5 if long_stream else 8)
+    return max(64, 64 * int(round(distinct_rows / (per_cu * n_cus) / 64)))
+
+
+def mfma_bundle_rows(distinct_rows: int) -> int:
+    """Rows per bf16 MFMA bundle: one 8-wave workgroup per CU (150 KB of LDS); long bundles amortise
+    its prologue (profiles/r2_mfma_ab2: 512 / 1024 / 2048 rows -> 0.458 / 0.440 / 0.430 ms at the bf16
+    headline): about two bundles per CU, 256..2048 rows."""
+    rows = 256
+    while rows < 2048 and rows * 2 * N_CUS < distinct_rows:
+        rows *= 2
+    return rows
+
+
+def staged_bundle_rows(distinct_rows: int, n_cus: int = N_CUS) -> int:
+    """Rows per LDS-staged bundle: 512 in the long-stream regime (measured 512 > 256, 1024; 2048 leaves
+    CUs idle), 128 below it (profiles/r2_shapes: N=8 0.238 vs 0.415 ms, N=2 0.80 vs 0.99 ms at 512)."""
+    return 512 if distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus else 128
+
+
+def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, distinct_rows: int,
+                  n_cus: int = N_CUS) -> KernelChoice:
+    """The measured default kernel of a plan (a pure function; tests/test_plan_tables.py pins the table).
+
+    prec_code: 0 fp64, 1 fp32, 2 bf16 storage.  max_rep: most co-located messages reading one
+    partition (1 = distinct rows only).  distinct_rows: rows of the distinct partitions per round.
+    Measured choices (docs/PERF_NOTES.md):
+      * distinct rows: the fused kernel, fp64 the interleaved pair kernel, fp32 4 rows, bf16 1 row;
+      * replicas, fp64, 3 per bundle (AGC / cyclic s = 2): one-wave bundles, folded; the lane
+        epilogue below the long-stream regime (sharded ranks: 0.188 vs 0.195 ms at N = 8), the
+        wave-uniform one in it (the one-GPU headline: 1.316 vs 1.40 ms);
+      * replicas otherwise (fp64 R = 2, fp32): LDS-staged bundles; fp32 in the long-stream regime
+        with R = 3 one-wave bundles (0.692 vs 0.740 ms); the pair form for fp32 and for every
+        short-stream rank (one wave per replica there);
+      * bf16 replicas: MFMA bundles (d <= 1024, d % 8 == 0), else the fused kernel interleaved;
+      * 2048 < d (fp64, 4096 fp32): the wide kernel; beyond 8192 / 16384 or cpl unknown: two passes.
+    """
+    if cpl is None:
+        return KernelChoice("twopass")
+    shared = max_rep > 1
+    if cpl >= 256:
+        return KernelChoice("wide", interleave=shared)
+    if not shared:
+        return KernelChoice("fused", rows={0: 2, 1: 4, 2: 1}[prec_code])
+    long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
+    if prec_code == 2:
+        if ld <= 1024 and ld % 8 == 0 and max_rep <= 16:
+            return KernelChoice("mfma", replicas=max_rep, bundle_rows=mfma_bundle_rows(distinct_rows))
+        return KernelChoice("fused", rows=1, interleave=True)
+    if cpl <= 16 and max_rep == 3 and (prec_code == 0 or long_stream):
+        return KernelChoice("multi", replicas=3, bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus),
+                            fold=True, lane_epi=not long_stream)
+    return KernelChoice("staged", replicas=max_rep, bundle_rows=staged_bundle_rows(distinct_rows, n_cus),
+                        pair=prec_code == 1 or not long_stream, wpr=0 if long_stream else 1)
 
 
 WIDE_EPT = {2: 16, 4: 32, 8: 32}  # elements per thread per row of grad_dense_wide (by vector width)
@@ -85,10 +199,9 @@ def replica_dispatch_order(keys: Sequence[Tuple[int, int]], stride: int = 0) -> 
     order changes, and slab rows stay message-major, so results are bitwise unchanged.
 
     keys[i] = (partition, first row) of task i (message-major order).  Returns a permutation.
-    stride: dispatch distance between bundle members (default XCDS: same XCD; 1: adjacent
-    slots, i.e. different XCDs sharing through the Infinity Cache — A/B runs only).
+    stride: dispatch distance between bundle members (default XCDS: same XCD).
     """
-    stride = stride or int(os.environ.get("ERASUREHEAD_REPLICA_STRIDE", XCDS))
+    stride = stride or XCDS
     bundles: Dict[Tuple[int, int], List[int]] = {}
     for i, k in enumerate(keys):
         bundles.setdefault(k, []).append(i)
@@ -120,9 +233,8 @@ class DenseGradPlan:
 
     def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]],
                  partitions: Dict[int, Tuple[torch.Tensor, torch.Tensor]], prec: Precision, loss: int, d: int,
-                 target_tasks: Optional[int] = None, interleave: Optional[bool] = None):
-        # replica-interleaved dispatch (see replica_dispatch_order); ERASUREHEAD_NO_INTERLEAVE=1 for A/B runs
-        self.interleave = (not os.environ.get("ERASUREHEAD_NO_INTERLEAVE")) if interleave is None else interleave
+                 target_tasks: Optional[int] = None, choice: Optional[KernelChoice] = None):
+        """choice: the kernel to launch (tests / sweeps); default: :func:`choose_kernel`'s measured pick."""
         self.prec = prec
         self.loss = loss
         self.d = d
@@ -139,71 +251,26 @@ class DenseGradPlan:
                 raise ValueError(f"partition {p}: y must be [{X.shape[0]}] {prec.acc}")
         self.total_rows = sum(partitions[p][0].shape[0] for m in self.messages for p, _ in m)
         self.cpl = choose_cpl(self.ld, prec.vec)
-        # co-located replicas (a partition in several local messages) read shared rows
-        self.replicated = len({p for m in self.messages for p, _ in m}) < sum(len(m) for m in self.messages)
-        shared = self.replicated and self.interleave
-        if target_tasks is None:  # measured: smaller tasks keep interleaved replicas in step
-            target_tasks = REPLICA_TASKS if shared else DEFAULT_TASKS
-        # grad_dense_fused variant (csrc/kernels/grad_dense.hip fused_rows), measured per case:
-        # one row in flight for interleaved replicas (L2-fed) in every precision; for distinct
-        # rows the interleaved pair kernel (fp64), 4 rows (fp32), 1 row (bf16)
-        self.variant = 1 if shared else {0: 2, 1: 4, 2: 1}[prec.code]
-        # Replica bundles: the tasks that read the same rows run in one workgroup, one wave per
-        # replica.  Default for fp64/fp32 replicas: grad_dense_staged streams each bundle's rows
-        # from HBM once through LDS and every replica wave computes its own message from there
-        # (measured 1.58 vs 1.80 ms fp64, 0.89 vs 0.99 ms fp32 at the headline; bf16 rows are
-        # too short to pay for the staging: 0.70 vs 0.66 ms, docs/PERF_NOTES.md).
-        # ERASUREHEAD_STAGED=0 / 1 / pair overrides (pair: two rows share one reduction and one
-        # residual evaluation; the default for fp32 and sharded ranks, see below).
-        staged_env = os.environ.get("ERASUREHEAD_STAGED", "")
-        staged_ok = shared and self.cpl is not None and self.cpl <= MAX_CPL
-        # One-wave bundles (grad_dense_multi, the fp64 default): one wave computes every replica of
-        # its bundle from rows double-buffered in registers, with no LDS staging and no barrier.
-        # R <= 3 replicas, d <= 1024.  Measured against the LDS-staged bundles, fp64
-        # (profiles/r3_multi, r3_fold; with the workgroup fold): one-GPU headline 1.33 vs 1.45 ms,
-        # 2/4/8-GPU rank shapes 0.70 / 0.36 / 0.195 vs 0.78 / 0.41-0.43 / 0.21-0.23 ms.  fp32: the one-GPU headline
-        # (0.692 vs 0.740 ms); sharded fp32 ranks stay on the staged pair bundles (N=8 0.115-0.122
-        # vs 0.129 ms).  ERASUREHEAD_STAGED=multi forces it for fp32.
-        max_rep = max(collections.Counter(p for m in self.messages for p, _ in m).values(), default=0)
-        multi_ok = staged_ok and self.cpl <= 16 and max_rep <= 3
+        # co-located replicas: a partition read by several local messages
+        self.max_rep = max(collections.Counter(p for m in self.messages for p, _ in m).values(), default=0)
         distinct_rows = sum(partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
-        # default only for bundles of 3 (AGC / cyclic with s = 2): with 2 replicas (FRC s = 1) the
-        # staged bundles with two waves per replica stay ahead (1.36 vs 1.40 ms, profiles/r3_fold)
-        self.multi = multi_ok and ((staged_env == "multi" and prec.code in (0, 1)) or (
-            staged_env == "" and max_rep == 3 and (prec.code == 0 or (prec.code == 1 and distinct_rows >= 750_000))))
-        self.staged = staged_ok and not self.multi and (
-            staged_env in ("1", "pair") or (staged_env == "" and prec.code in (0, 1)))
-        # two rows per step sharing one reduction: the fp32 default (0.790 vs 0.862 ms at the
-        # headline, profiles/r2_fp32) and the default on sharded ranks of a multi-GPU run, where it
-        # also wins for fp64 with one wave per replica (N=8 rank 0.213 vs 0.238 ms, N=4 0.407 vs
-        # 0.429, profiles/r2_rank_sweep); slower for the one-GPU fp64 headline
-        sharded = distinct_rows < SHARD_ROWS
-        self.staged_pair = self.staged and (staged_env == "pair" or (staged_env == "" and (prec.code == 1 or sharded)))
-        self.staged_wpr = 1 if (self.staged and sharded and staged_env == "") else 0  # 0: kernel default
-        # bf16 replica bundles on the matrix cores (csrc/kernels/grad_mfma.hip): the R replicas of a
-        # bundle are the M dimension of X·beta and Xᵀ·r per 32-row LDS stage.  ERASUREHEAD_MFMA=0
-        # keeps the VALU kernels (A/B runs).
-        self.mfma = (prec.code == 2 and staged_ok and self.ld <= 1024 and self.ld % 8 == 0
-                     and os.environ.get("ERASUREHEAD_MFMA", "1") != "0")
-        # rows per bundle task: 512 at the one-GPU headline (1e6 distinct rows); a rank holding the
-        # partition shards of an N-GPU run (500k / 250k / 125k rows at N = 2 / 4 / 8) is fastest with
-        # 128-row bundles (profiles/r2_shapes: N=8 0.238 vs 0.415 ms, N=2 0.80 vs 0.99 ms at 512)
-        staged_rows = STAGED_ROWS if distinct_rows >= SHARD_ROWS else SHARD_STAGED_ROWS
-        if self.mfma:
-            # MFMA bundles run one 8-wave workgroup per CU (150 KB of LDS): long bundles amortise its
-            # prologue (profiles/r2_mfma_ab2: 512 / 1024 / 2048 rows -> 0.458 / 0.440 / 0.430 ms at
-            # the bf16 headline); about two bundles per CU, 256..2048 rows
-            staged_rows = 256
-            while staged_rows < 2048 and staged_rows * 512 < distinct_rows:
-                staged_rows *= 2
-        if self.multi:
-            staged_rows = multi_bundle_rows(distinct_rows, fp32=prec.code == 1)
-        default_rows = str(staged_rows) if (self.staged or self.mfma or self.multi) else "0"
-        self.bundle_rows = int(os.environ.get("ERASUREHEAD_BUNDLE_ROWS", default_rows)) if (
-            shared and self.cpl is not None and self.cpl <= MAX_CPL) else 0
+        self.choice = choice or choose_kernel(prec.code, self.ld, self.cpl, self.max_rep, distinct_rows)
+        c = self.choice
+        if c.kind == "twopass" and self.cpl is not None:
+            raise ValueError("the two-pass kernel is for rows wider than the one-pass kernels")
+        if c.kind in ("multi", "staged", "mfma") and (self.cpl is None or self.cpl > MAX_CPL):
+            raise ValueError(f"{c.kind} bundles need d <= {64 * MAX_CPL} columns per vector width")
+        if c.kind == "multi" and (self.cpl > 16 or prec.code == 2 or self.max_rep > 3):
+            raise ValueError("one-wave bundles hold at most 3 fp64/fp32 replicas of d <= 1024")
+        if c.kind == "mfma" and (prec.code != 2 or self.ld > 1024 or self.ld % 8 or self.max_rep > 16):
+            raise ValueError("MFMA bundles are bf16, d <= 1024, d % 8 == 0, at most 16 replicas")
+        self.bundle_rows = c.bundle_rows if c.bundled else 0
+        if target_tasks is None:  # measured: smaller tasks keep interleaved replicas in step
+            target_tasks = REPLICA_TASKS if c.interleave else DEFAULT_TASKS
         if self.bundle_rows:
             target_tasks = max(1, -(-self.total_rows // self.bundle_rows))
         if self.device.type == "cuda":
+            self._native_choice = c.native()
             self._build_tables(target_tasks)
 
     # ---- device tables ----------------------------------------------------------------
@@ -228,7 +295,7 @@ class DenseGradPlan:
             tasks, folded_begin = self._bundle_table(tasks, keys)
             if folded_begin is not None:  # one slab row per (workgroup, replica): see _fold_table
                 slot_begin = folded_begin
-        elif self.interleave and self.cpl is not None:
+        elif self.choice.interleave:
             tasks = [tasks[i] for i in replica_dispatch_order(keys)]
         dev = self.device
         self.segs = torch.tensor(list(bytes(segs) or b"\0" * 32), dtype=torch.uint8).to(dev)
@@ -237,10 +304,8 @@ class DenseGradPlan:
         self.tasks = torch.from_numpy(t).to(dev)
         self.slot_task_begin = torch.tensor(slot_begin, dtype=torch.int32, device=dev)
         self.slab = torch.empty((max(1, self.ntasks), self.ld), dtype=self.prec.acc, device=dev)
-        # partial sums [nslots, SLAB_SPLITS, ld], then 16 zeroed bytes: the staged kernels' persistent-grid
-        # ticket (csrc/kernels/launchers.h slab_part_bytes)
-        es = torch.tensor([], dtype=self.prec.acc).element_size()
-        self.part = torch.zeros(max(1, self.nslots) * SLAB_SPLITS * self.ld + 16 // es, dtype=self.prec.acc, device=dev)
+        # slab partial sums [nslots, SLAB_SPLITS, ld] (csrc/kernels/launchers.h slab_part_bytes)
+        self.part = torch.zeros(max(1, self.nslots) * SLAB_SPLITS * self.ld, dtype=self.prec.acc, device=dev)
         if self.cpl is None:
             off = np.zeros(max(1, self.ntasks), dtype=np.int64)
             if self.ntasks:
@@ -251,7 +316,7 @@ class DenseGradPlan:
             self.rbuf = torch.empty(max(1, int(self.total_rows)), dtype=self.prec.acc, device=dev)
 
     def _bundle_table(self, tasks, keys):
-        """Replica-bundle layout for grad_dense_bundle: R task slots per workgroup, one wave each."""
+        """Replica-bundle layout: R task slots per bundle (one wave each, or all in one wave for multi)."""
         bundles: Dict[Tuple[int, int], List[int]] = {}
         for i, k in enumerate(keys):
             bundles.setdefault(k, []).append(i)
@@ -259,33 +324,13 @@ class DenseGradPlan:
         for b in bundles.values():
             groups += [b[i:i + MAX_BUNDLE] for i in range(0, len(b), MAX_BUNDLE)]
         R = max(len(g) for g in groups)
+        if R != self.choice.replicas:
+            raise ValueError(f"the plan's bundles hold {R} replicas, the kernel choice {self.choice.replicas}")
         pad = (0, -1, 0, 0, 0)
         table = []
         for g in groups:
             table += [tasks[i] for i in g] + [pad] * (R - len(g))
-        if self.mfma and R > 16:
-            raise ValueError("MFMA bundles hold at most 16 replicas")
-        if self.multi and R > 3:
-            raise ValueError("one-wave bundles (ERASUREHEAD_STAGED=multi) hold at most 3 replicas")
-        self.fold = self.multi and os.environ.get("ERASUREHEAD_MULTI_FOLD", "1") != "0"
-        # epilogue of the folded one-wave kernel: replicas 0/1 reduce-scattered and one lane per
-        # replica evaluating its residual (csrc variant 90 + R) wins on sharded ranks (N=2/4/8
-        # 0.677-0.684 / 0.353-0.354 / 0.188-0.190 vs 0.689-0.699 / 0.365-0.368 / 0.194-0.197 ms);
-        # the wave-uniform one (70 + R) on the one-GPU headline (1.316-1.334 vs 1.40-1.43 ms),
-        # profiles/r3_epi.  ERASUREHEAD_MULTI_EPI=wave|lane overrides.
-        epi = os.environ.get("ERASUREHEAD_MULTI_EPI", "")
-        distinct = sum(self.partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
-        self.lane_epi = self.fold and (epi == "lane" or (epi == "" and distinct < 750_000))
-        self.variant = (40 if self.mfma else (90 if self.lane_epi else 70 if self.fold else 60) if self.multi
-                        else 30 if self.staged_pair else 20 if self.staged else 10) + R
-        if self.staged and self.staged_wpr:
-            self.variant += 100 * self.staged_wpr  # csrc: variant / 100 % 10 = waves per replica
-        # persistent staged workgroups (csrc: variant >= 1000): as many workgroups as fit, each taking
-        # bundles from an atomic ticket until none is left; ERASUREHEAD_PERSISTENT=1 (read per plan)
-        self.persistent = bool(self.staged and os.environ.get("ERASUREHEAD_PERSISTENT", "0") == "1")
-        if self.persistent:
-            self.variant += 1000
-        if self.fold:
+        if self.choice.kind == "multi" and self.choice.fold:
             return self._fold_table(groups, tasks, keys, R, pad)
         return table, None
 
@@ -337,7 +382,7 @@ class DenseGradPlan:
             C = native()
             if self.cpl is not None:
                 C.grad_dense(self.prec.code, self.loss, self.cpl, self.segs, self.tasks, beta, self.slab,
-                             self.slot_task_begin, self.part, G, self.ld, self.variant)
+                             self.slot_task_begin, self.part, G, self.ld, self._native_choice)
             else:
                 C.grad_dense_twopass(self.prec.code, self.loss, self.segs, self.tasks, beta, self.task_row_off,
                                      self.rbuf, self.slab, self.slot_task_begin, self.part, G, self.ld)
@@ -351,7 +396,7 @@ class DenseGradPlan:
         C = native()
         if self.cpl is not None:
             return C.GradLauncher.dense(self.prec.code, self.loss, self.cpl, self.segs, self.tasks, self.slab,
-                                        self.slot_task_begin, self.part, self.ld, variant=self.variant)
+                                        self.slot_task_begin, self.part, self.ld, choice=self._native_choice)
         return C.GradLauncher.dense(self.prec.code, self.loss, 0, self.segs, self.tasks, self.slab,
                                     self.slot_task_begin, self.part, self.ld, self.task_row_off, self.rbuf)
 

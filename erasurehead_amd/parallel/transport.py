@@ -510,7 +510,7 @@ class IpcTransport(Transport):
                     errs.append(f"rank 0 -> rank {r}: beta payload in the inbox differs from the pattern sent "
                                 f"(step: master put over xGMI)")
                 n = self.n_local
-                if os.environ.get("ERASUREHEAD_IPC_SABOTAGE") == str(r):  # test hook: this rank never answers
+                if os.environ.get("ERASUREHEAD_SABOTAGE") == f"handshake:{r}":  # test hook: this rank never answers
                     pass
                 elif n:
                     src = (pat * (r + 1)).unsqueeze(0).repeat(n, 1).contiguous()

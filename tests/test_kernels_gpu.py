@@ -1,4 +1,6 @@
 """Numerics of the gfx950 HIP kernels against fp64 NumPy/PyTorch references (GPU only)."""
+import collections
+
 import numpy as np
 import pytest
 import scipy.sparse as sps
@@ -7,6 +9,7 @@ import torch
 from erasurehead_amd.models.losses import LEAST_SQUARES, LOGISTIC, least_squares_grad, logistic_grad, logistic_loss, mse
 from erasurehead_amd.ops import DenseGradPlan, SparseGradPlan, auc_columns, combine_update, get_precision, loss_sums, predictions
 from erasurehead_amd.models.losses import roc_auc, UpdateRule
+from erasurehead_amd.ops.grad import KernelChoice
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -231,18 +234,20 @@ def test_encode_messages(dtype, native):
     np.testing.assert_allclose(G.double().cpu().numpy(), ref, rtol=tol, atol=tol)
 
 
+MESSAGE_MAJOR = KernelChoice("fused", rows=1)  # one row per wave, message-major tasks: the plain reference
+
+
 @pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
-def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native, monkeypatch):
-    """Replica-interleaved task order + per-case kernel variant: same bits as message-major order."""
-    monkeypatch.setenv("ERASUREHEAD_STAGED", "0")  # the interleaved dispatch, not the LDS-staged bundles
-    monkeypatch.setenv("ERASUREHEAD_MFMA", "0")  # nor the bf16 MFMA bundles
+def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native):
+    """Replica-interleaved task order: same bits as message-major order."""
     prec = get_precision(prec_name)
     rng = np.random.RandomState(11)
     parts, _ = _parts(rng, [3000, 2000, 1000], 1000, prec)
     msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
-    a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, target_tasks=256, interleave=True)
-    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, target_tasks=256, interleave=False)
-    assert a.replicated and not torch.equal(a.tasks, b.tasks)
+    a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, target_tasks=256,
+                      choice=KernelChoice("fused", rows=1, interleave=True))
+    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, target_tasks=256, choice=MESSAGE_MAJOR)
+    assert a.max_rep > 1 and not torch.equal(a.tasks, b.tasks)
     beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
     Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
     a.native_launcher().launch(beta, Ga)
@@ -252,23 +257,20 @@ def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native,
 
 
 @pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
-def test_dense_grad_staged_is_the_replica_default(prec_name, native, monkeypatch):
+def test_dense_grad_staged_is_the_replica_default(prec_name, native):
     """Co-located replicas in bundles of more than 3 default to the LDS-staged bundles for fp64/fp32
     (MFMA for bf16), and the staged messages match message-major order to rounding."""
-    monkeypatch.delenv("ERASUREHEAD_STAGED", raising=False)
-    monkeypatch.delenv("ERASUREHEAD_BUNDLE_ROWS", raising=False)
+    from erasurehead_amd.ops.grad import staged_bundle_rows
+
     prec = get_precision(prec_name)
     rng = np.random.RandomState(12)
     parts, _ = _parts(rng, [3000, 2000, 1000], 1000, prec)
     msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
     a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
-    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, interleave=False)
-    from erasurehead_amd.ops.grad import SHARD_STAGED_ROWS
-
-    assert a.staged == (prec_name != "bf16") and not b.staged
-    assert a.mfma == (prec_name == "bf16")
-    if a.staged:  # 6000 distinct rows: the small-rank bundle size
-        assert 20 < a.variant % 100 <= 38 and a.bundle_rows == SHARD_STAGED_ROWS  # small rank: pair form
+    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, choice=MESSAGE_MAJOR)
+    assert a.choice.kind == ("mfma" if prec_name == "bf16" else "staged")
+    if a.choice.kind == "staged":  # 6000 distinct rows: a short-stream rank, pair form, 128-row bundles
+        assert a.choice.pair and a.bundle_rows == staged_bundle_rows(6000) == 128
     beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
     Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
     a.native_launcher().launch(beta, Ga)
@@ -279,23 +281,21 @@ def test_dense_grad_staged_is_the_replica_default(prec_name, native, monkeypatch
 
 
 @pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
-def test_dense_grad_one_wave_bundles_are_the_fp64_default(prec_name, native, monkeypatch):
+def test_dense_grad_one_wave_bundles_are_the_fp64_default(prec_name, native):
     """Bundles of at most 3 replicas default to grad_dense_multi for fp64 (bundle length from
-    multi_bundle_rows), to the staged pair bundles for fp32 and to MFMA for bf16; the fp64 messages
+    multi_bundle_rows), to the staged pair bundles for fp32 and to MFMA for bf16; the messages
     match message-major order to rounding."""
     from erasurehead_amd.ops.grad import multi_bundle_rows
 
-    monkeypatch.delenv("ERASUREHEAD_STAGED", raising=False)
-    monkeypatch.delenv("ERASUREHEAD_BUNDLE_ROWS", raising=False)
     prec = get_precision(prec_name)
     rng = np.random.RandomState(13)
     parts, _ = _parts(rng, [3000, 2000, 1000], 1000, prec)
     msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(2, -1.0)]] * 2
     a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
-    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, interleave=False)
-    assert a.multi == (prec_name == "fp64") and a.staged == (prec_name == "fp32") and a.mfma == (prec_name == "bf16")
-    if a.multi:
-        assert a.variant == 93 and a.bundle_rows == multi_bundle_rows(6000)
+    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, choice=MESSAGE_MAJOR)
+    assert a.choice.kind == {"fp64": "multi", "fp32": "staged", "bf16": "mfma"}[prec_name]
+    if a.choice.kind == "multi":
+        assert a.choice.fold and a.choice.lane_epi and a.bundle_rows == multi_bundle_rows(6000)
     beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
     Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
     a.native_launcher().launch(beta, Ga)
@@ -303,32 +303,6 @@ def test_dense_grad_one_wave_bundles_are_the_fp64_default(prec_name, native, mon
     torch.cuda.synchronize()
     tol = 1e-12 if prec_name == "fp64" else 1e-4
     torch.testing.assert_close(Ga, Gb, rtol=tol, atol=tol)
-
-
-@pytest.mark.parametrize("prec_name", ["fp64", "fp32"])
-def test_dense_grad_staged_persistent_grid_is_bitwise_identical(prec_name, native, monkeypatch):
-    """Persistent staged workgroups (ERASUREHEAD_PERSISTENT=1: as many workgroups as fit, bundles handed
-    out by an atomic ticket) compute every bundle exactly as one-bundle-per-workgroup does, launch after
-    launch (the ticket resets itself): bitwise-equal messages, with far more bundles than slots."""
-    monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", "16")
-    monkeypatch.setenv("ERASUREHEAD_STAGED", "1")  # the LDS-staged bundles (fp64 defaults to one-wave bundles)
-    prec = get_precision(prec_name)
-    rng = np.random.RandomState(21)
-    parts, _ = _parts(rng, [20000, 20000, 20000], 1000, prec)
-    msgs = [[(0, 1.0)]] * 3 + [[(1, 1.0)]] * 3 + [[(2, -0.5)]] * 2
-    monkeypatch.setenv("ERASUREHEAD_PERSISTENT", "0")
-    a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
-    monkeypatch.setenv("ERASUREHEAD_PERSISTENT", "1")
-    b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
-    assert a.staged and b.persistent and not a.persistent and b.variant == a.variant + 1000
-    assert b.ntasks // 3 > 1024  # more bundles than the chip holds at once: the ticket hands them out
-    Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
-    for k in range(3):
-        beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
-        a.native_launcher().launch(beta, Ga)
-        b.native_launcher().launch(beta, Gb)
-        torch.cuda.synchronize()
-        assert torch.equal(Ga, Gb), f"launch {k}"
 
 
 def test_eval_gemm_unaligned_rows_use_scalar_staging(native):
@@ -349,18 +323,13 @@ def test_eval_gemm_unaligned_rows_use_scalar_staging(native):
 
 @pytest.mark.parametrize("layout", ["mixed", "pairs"])
 @pytest.mark.parametrize("pair", [False, True])
-@pytest.mark.parametrize("staged,rows,d,prec_name", [(False, "64", 1000, "fp64"), (True, "64", 1000, "fp64"),
-                                                     (True, "37", 1000, "fp64"), (True, "100", 250, "fp64"),
-                                                     (True, "64", 1000, "fp32"), (True, "64", 1000, "bf16")])
-def test_dense_grad_replica_bundle_kernel(monkeypatch, native, staged, rows, d, prec_name, pair, layout):
-    """Bundle kernels (one wave per replica per workgroup; rows loaded per wave, or staged once
-    through LDS by LDS-DMA) against the fp64 oracle.  Row counts that leave partial stages and
-    partial bundles are included.  "mixed": bundles of 5 and 3 replicas (one wave per replica);
-    "pairs": bundles of 2 (the staged kernel then runs two waves per replica and folds them)."""
-    monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", rows)
-    if pair and not staged:
-        pytest.skip("pair applies to the staged kernel")
-    monkeypatch.setenv("ERASUREHEAD_STAGED", ("pair" if pair else "1") if staged else "0")
+@pytest.mark.parametrize("rows,d,prec_name", [(64, 1000, "fp64"), (37, 1000, "fp64"), (100, 250, "fp64"),
+                                              (64, 1000, "fp32"), (64, 1000, "bf16")])
+def test_dense_grad_staged_bundles(native, rows, d, prec_name, pair, layout):
+    """LDS-staged replica bundles (rows streamed once through an LDS ring by LDS-DMA, a wave per
+    replica) against the fp64 oracle.  Row counts that leave partial stages and partial bundles are
+    included.  "mixed": bundles of 5 and 3 replicas (one wave per replica); "pairs": bundles of 2
+    (two waves per replica, folded); pair: two rows per step sharing one reduction."""
     prec = get_precision(prec_name)
     rng = np.random.RandomState(21)
     parts, host = _parts(rng, [700, 500, 301], d, prec)
@@ -368,8 +337,10 @@ def test_dense_grad_replica_bundle_kernel(monkeypatch, native, staged, rows, d, 
         msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
     else:
         msgs = [[(0, 1.0)]] * 2 + [[(1, 1.0), (2, 0.5)], [(1, -1.0), (2, 2.0)]]
-    plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, d)
-    assert plan.bundle_rows == int(rows) and plan.variant > (30 if pair else 20 if staged else 10)
+    R = max(collections.Counter(p for m in msgs for p, _ in m).values())
+    plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, d,
+                         choice=KernelChoice("staged", replicas=R, bundle_rows=rows, pair=pair))
+    assert plan.bundle_rows == rows
     beta = torch.randn(plan.ld, dtype=prec.acc, device=DEV) * 0.05
     G = plan.out_buffer()[0]
     plan.native_launcher().launch(beta, G)
@@ -383,28 +354,25 @@ def test_dense_grad_replica_bundle_kernel(monkeypatch, native, staged, rows, d, 
 
 @pytest.mark.parametrize("form", ["fold-lane", "fold-wave", "unfolded"])
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
-@pytest.mark.parametrize("rows,d,prec_name", [("64", 1000, "fp64"), ("37", 1000, "fp64"), ("256", 250, "fp64"),
-                                              ("64", 1000, "fp32"), ("33", 130, "fp32")])
-def test_dense_grad_one_wave_bundles(monkeypatch, native, rows, d, prec_name, loss, form):
-    """grad_dense_multi (ERASUREHEAD_STAGED=multi): one wave computes every replica of its bundle
-    from rows double-buffered in registers, each replica with its own dot product, residual and
-    gradient.  Bundles of 3 replicas, of 2 padded to 3, and partial / odd-length bundles (the
-    two-rows-per-trip loop ends on either buffer) against the fp64 oracle; with the workgroup fold
-    (4 bundles of one partition per workgroup, pad bundles at partition ends, one slab row per
-    workgroup and replica) and both epilogues (replicas reduce-scattered with one lane per
-    replica's residual, or wave-uniform), and without the fold."""
-    monkeypatch.setenv("ERASUREHEAD_BUNDLE_ROWS", rows)
-    monkeypatch.setenv("ERASUREHEAD_STAGED", "multi")
+@pytest.mark.parametrize("rows,d,prec_name", [(64, 1000, "fp64"), (37, 1000, "fp64"), (256, 250, "fp64"),
+                                              (64, 1000, "fp32"), (33, 130, "fp32")])
+def test_dense_grad_one_wave_bundles(native, rows, d, prec_name, loss, form):
+    """grad_dense_multi: one wave computes every replica of its bundle from rows double-buffered in
+    registers, each replica with its own dot product, residual and gradient.  Bundles of 3 replicas,
+    of 2 padded to 3, and partial / odd-length bundles (the two-rows-per-trip loop ends on either
+    buffer) against the fp64 oracle; with the workgroup fold (4 bundles of one partition per
+    workgroup, pad bundles at partition ends, one slab row per workgroup and replica) and both
+    epilogues (replicas reduce-scattered with one lane per replica's residual, or wave-uniform),
+    and without the fold."""
     fold = form != "unfolded"
-    monkeypatch.setenv("ERASUREHEAD_MULTI_FOLD", "1" if fold else "0")
-    monkeypatch.setenv("ERASUREHEAD_MULTI_EPI", "wave" if form == "fold-wave" else "lane")
     prec = get_precision(prec_name)
     rng = np.random.RandomState(5)
     parts, host = _parts(rng, [700, 501, 300], d, prec)
     msgs = [[(0, 1.0), (1, 1.0)]] * 2 + [[(0, -0.5), (1, 2.0)]] + [[(2, 1.0)], [(2, -3.0)]]
-    plan = DenseGradPlan(msgs, parts, prec, loss, d)
-    want = {"fold-lane": 93, "fold-wave": 73, "unfolded": 63}[form]
-    assert plan.multi and plan.variant == want and plan.bundle_rows == int(rows)
+    plan = DenseGradPlan(msgs, parts, prec, loss, d,
+                         choice=KernelChoice("multi", replicas=3, bundle_rows=rows, fold=fold,
+                                             lane_epi=form == "fold-lane"))
+    assert plan.bundle_rows == rows
     if fold:  # slab rows: one per (workgroup, replica), a contiguous range per message
         stb = plan.slot_task_begin.cpu().numpy()
         assert stb[0] == 0 and np.all(np.diff(stb) > 0) and stb[-1] <= plan.ntasks // 4
@@ -483,7 +451,7 @@ def test_lds_transpose_read_map(rowlen, native):
 
 @pytest.mark.parametrize("d", [1000, 1024, 333, 8])
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
-def test_mfma_bf16_replica_bundles(d, loss, native, monkeypatch):
+def test_mfma_bf16_replica_bundles(d, loss, native):
     """bf16 replica bundles on MFMA (grad_mfma.hip) at the staged geometry: the headline's uneven FRC
     layout (bundles of 3 and 2 replicas) plus cyclic-style distinct coefficients, every message
     against the fp64 oracle on the stored bf16 values; and close to the VALU kernels."""
@@ -494,7 +462,7 @@ def test_mfma_bf16_replica_bundles(d, loss, native, monkeypatch):
             [(2, 1.0)], [(2, 1.0)],  # group of 2
             [(0, 0.5), (2, -1.25)], [(1, 2.0)]]  # distinct coefficients
     plan = DenseGradPlan(msgs, parts, prec, loss, d)
-    assert plan.mfma and plan.variant > 40
+    assert plan.choice.kind == "mfma" and plan.choice.replicas == 3
     beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
     b = rng.randn(d) * 0.3
     beta[:d] = torch.from_numpy(b).to(prec.acc)
@@ -507,9 +475,7 @@ def test_mfma_bf16_replica_bundles(d, loss, native, monkeypatch):
         got = G[slot, :d].double().cpu().numpy()
         err = np.max(np.abs(got - ref)) / max(1e-30, np.max(np.abs(ref)))
         assert err < 2e-4, (slot, err)
-    monkeypatch.setenv("ERASUREHEAD_MFMA", "0")
-    valu = DenseGradPlan(msgs, parts, prec, loss, d)
-    assert not valu.mfma
+    valu = DenseGradPlan(msgs, parts, prec, loss, d, choice=KernelChoice("fused", rows=1, interleave=True))
     G2 = valu.out_buffer()[0]
     valu.run(beta, G2)
     np.testing.assert_allclose(G[:, :d].cpu().numpy(), G2[:, :d].cpu().numpy(), rtol=2e-4,

@@ -68,15 +68,16 @@ def test_ipc_many_ranks(world, case_i, tmp_path):
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
 
 
-@pytest.mark.parametrize("wait,fused", [("device", "1"), ("host", "0"), ("device", "0")])
-def test_ipc_worker_wait_and_put_modes(wait, fused, tmp_path):
+@pytest.mark.parametrize("wait", ["device", "host"])
+def test_ipc_worker_wait_modes(wait, tmp_path):
     """Worker rounds with the beta wait on the device stream (hipStreamWaitValue64; the default
-    when a rank has its GPU to itself) or on the host, and with the message put fused into the
-    final reduction or as its own kernel: every combination matches the oracle replay."""
+    when a rank has its GPU to itself) or on the host, the message put fused into the final
+    reduction (the put as its own kernel runs in the physically-late-rank tests): both match the
+    oracle replay."""
     from oracle import replay
     from test_engine_cpu import CASES, make
 
-    r = _launch(3, 1, "AGD", str(tmp_path / "w.npz"), ERASUREHEAD_WORKER_WAIT=wait, ERASUREHEAD_FUSED_PUT=fused)
+    r = _launch(3, 1, "AGD", str(tmp_path / "w.npz"), ERASUREHEAD_WORKER_WAIT=wait)
     assert str(r["transport"]) == "ipc"
     cfg, src, sch, parts = make(CASES[1], "AGD")
     arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
@@ -177,7 +178,7 @@ def test_ipc_handshake_failure_names_pair_and_step(tmp_path, monkeypatch):
     """A worker rank that never answers the setup handshake: --transport ipc fails with an error
     naming the pair and the step instead of training on garbage or hanging."""
     monkeypatch.setenv("ERASUREHEAD_TRANSPORT", "ipc")
-    monkeypatch.setenv("ERASUREHEAD_IPC_SABOTAGE", "1")
+    monkeypatch.setenv("ERASUREHEAD_SABOTAGE", "handshake:1")
     monkeypatch.setenv("ERASUREHEAD_HANDSHAKE_TIMEOUT", "3")
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",

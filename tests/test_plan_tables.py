@@ -53,3 +53,55 @@ def test_fold_table_groups_one_partition_per_workgroup():
 def test_multi_bundle_rows_table():
     assert [multi_bundle_rows(n) for n in (1_000_000, 500_000, 250_000, 125_000)] == [768, 256, 128, 64]
     assert multi_bundle_rows(1_000_000, fp32=True) == 384 and multi_bundle_rows(1000) == 64
+
+
+def test_kernel_selection_table():
+    """choose_kernel (ops/grad.py): every default reachable without environment variables, one row
+    per regime (precision x replication x rows per CU x row width)."""
+    from erasurehead_amd.ops.grad import KernelChoice, choose_cpl, choose_kernel
+
+    def pick(prec, d, rep, rows):
+        vec = {0: 2, 1: 4, 2: 8}[prec]
+        ld = -(-d // vec) * vec
+        return choose_kernel(prec, ld, choose_cpl(ld, vec), rep, rows)
+
+    # the headline (AGC W=8 s=2: bundles of 3 replicas), one GPU (1e6 distinct rows): long stream
+    assert pick(0, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=768, fold=True)
+    assert pick(1, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=384, fold=True)
+    assert pick(2, 1000, 3, 1_000_000) == KernelChoice("mfma", replicas=3, bundle_rows=2048)
+    # the 8-GPU partition-shard rank (125k rows): fill every wave slot, lane epilogue
+    assert pick(0, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)
+    assert pick(1, 1000, 3, 125_000) == KernelChoice("staged", replicas=3, bundle_rows=128, pair=True, wpr=1)
+    # FRC s=1 (bundles of 2): staged, one GPU / a sharded rank
+    assert pick(0, 1000, 2, 1_000_000) == KernelChoice("staged", replicas=2, bundle_rows=512)
+    assert pick(0, 1000, 2, 250_000) == KernelChoice("staged", replicas=2, bundle_rows=128, pair=True, wpr=1)
+    # distinct rows (naive): the fused kernel per precision
+    assert [pick(p, 1000, 1, 1_000_000) for p in (0, 1, 2)] == [KernelChoice("fused", rows=2), KernelChoice("fused", rows=4),
+                                                                   KernelChoice("fused", rows=1)]
+    # wide rows: d = 2048 fp64 (32 columns per lane) stays on staged bundles; 4096 takes the wide kernel
+    assert pick(0, 2048, 3, 1_000_000).kind == "staged"
+    assert pick(0, 4096, 3, 1_000_000) == KernelChoice("wide", interleave=True)
+    assert pick(0, 4096, 1, 1_000_000) == KernelChoice("wide")
+    assert pick(0, 10000, 3, 100_000) == KernelChoice("twopass")
+    # bf16 beyond the MFMA tile: the fused kernel, replica-interleaved
+    assert pick(2, 2000, 3, 1_000_000) == KernelChoice("fused", rows=1, interleave=True)
+    # the regime boundary is a rows-per-CU rule, not a row count: 4x the CUs -> 4x the rows
+    assert pick(0, 1000, 3, 700_000).lane_epi and not pick(0, 1000, 3, 800_000).lane_epi
+    assert choose_kernel(0, 1000, 16, 3, 2_800_000, n_cus=1024).lane_epi
+
+
+def test_no_tuning_env_knobs_left():
+    """The kernel selection reads no environment variable (round-2 verdict: 28 knobs -> <= 10, all of
+    them runtime policy, test hooks or build plumbing)."""
+    import glob
+    import os
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    knobs = set()
+    for pat in ("erasurehead_amd/**/*.py", "csrc/**/*.cpp", "csrc/**/*.hip", "csrc/**/*.h", "bench.py"):
+        for f in glob.glob(os.path.join(root, pat), recursive=True):
+            knobs |= set(re.findall(r"ERASUREHEAD_[A-Z0-9_]+", open(f).read()))
+    assert len(knobs) <= 10, sorted(knobs)
+    assert not any(k.startswith(("ERASUREHEAD_STAGE", "ERASUREHEAD_MULTI", "ERASUREHEAD_BUNDLE", "ERASUREHEAD_MFMA",
+                                 "ERASUREHEAD_PERSISTENT", "ERASUREHEAD_GRAD")) for k in knobs), sorted(knobs)

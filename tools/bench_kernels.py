@@ -4,6 +4,8 @@
 
 * dense ``grad_dense`` (fused single pass; two-pass above d = 2048 fp64) at several widths,
   reported as effective HBM bandwidth over the bytes of X it must stream;
+* ``--only sweep``: d in {256, 1000, 2048, 4096} x n in {1e5, 1e6, 4e6} x fp64/fp32 against the
+  device-copy ceiling, distinct-row and replica-bundle layouts;
 * sparse one-hot gradients on covtype / kc_house / amazon-shaped data (the reference's real
   datasets, synthetic stand-ins of the same shape): the ELL path against the generic
   sorted-COO path.
@@ -113,6 +115,53 @@ def scale_cases(out):
             del plan
 
 
+def sweep_cases(out, ds=(256, 1000, 2048, 4096), ns=(100_000, 1_000_000, 4_000_000), precs=("fp64", "fp32")):
+    """Shape sweep of the dense gradient against the device-copy ceiling (round-2 verdict item 6).
+
+    For every (precision, d, n): n rows in 8 partitions, two message layouts -- ``naive`` (one
+    partition per message, distinct rows) and ``agc`` (the headline's replica bundles: groups
+    {0,1,2}x3, {3,4,5}x3, {6,7}x2) -- with the kernel ``choose_kernel`` picks for that shape.  The
+    ceiling is a device-to-device copy of one partition (read + write bytes / time); ``frac`` is the
+    kernel's distinct-X read rate over it.
+    """
+    import torch
+
+    from erasurehead_amd.models.losses import LOGISTIC
+    from erasurehead_amd.ops import DenseGradPlan, get_precision
+
+    layouts = {"naive": [[p] for p in range(8)], "agc": [[0, 1, 2]] * 3 + [[3, 4, 5]] * 3 + [[6, 7]] * 2}
+    for prec_name in precs:
+        prec = get_precision(prec_name)
+        for d in ds:
+            for n in ns:
+                rpp = n // 8
+                parts = {}
+                for p in range(8):
+                    X = torch.empty(rpp, prec.ld(d), device="cuda", dtype=prec.storage).uniform_(-1, 1)
+                    y = torch.where(torch.rand(rpp, device="cuda") > 0.5, 1.0, -1.0).to(prec.acc)
+                    parts[p] = (X, y)
+                nbytes = parts[0][0].numel() * parts[0][0].element_size()
+                dst = torch.empty_like(parts[0][0])
+                copy_ms = _time(lambda: dst.copy_(parts[0][0]), reps=20)
+                ceiling = 2 * nbytes / copy_ms / 1e9  # TB/s
+                del dst
+                beta = torch.randn(prec.ld(d), device="cuda", dtype=prec.acc) * 0.01
+                for lay, msgs in layouts.items():
+                    plan = DenseGradPlan([[(p, 1.0) for p in m] for m in msgs], parts, prec, LOGISTIC, d)
+                    G = plan.out_buffer()[0]
+                    ms = _time(lambda: plan.run(beta, G), reps=20)
+                    distinct = 8 * nbytes / 1e12  # TB
+                    r = {"kernel": "grad_dense_sweep", "precision": prec_name, "d": d, "n": n, "layout": lay,
+                         "choice": plan.choice.label() if plan.choice else "twopass", "ms": ms,
+                         "distinct_TBps": distinct / ms * 1e3, "copy_TBps": ceiling,
+                         "frac": distinct / ms * 1e3 / ceiling}
+                    out.append(r)
+                    print(json.dumps(r), flush=True)
+                    del plan, G
+                del parts
+                torch.cuda.empty_cache()
+
+
 def eval_cases(out):
     """Post-hoc evaluation GEMM (MFMA, loss fused): X [n, 1000] . B[100, 1000]^T, fp64 / fp32."""
     import torch
@@ -129,8 +178,7 @@ def eval_cases(out):
         ms = _time(lambda: native().eval_gemm_loss(LOGISTIC, X, n, d, y, B, s, None), reps=10, warm=2)
         flops = 2.0 * n * d * R
         r = {"kernel": "eval_gemm_loss", "dtype": str(dt), "n": n, "d": d, "R": R, "ms": ms,
-             "TFLOPs": flops / ms / 1e9, "x_TBps": n * d * X.element_size() / ms / 1e9,
-             "v1": bool(os.environ.get("ERASUREHEAD_EVAL_V1"))}
+             "TFLOPs": flops / ms / 1e9, "x_TBps": n * d * X.element_size() / ms / 1e9}
         out.append(r)
         print(json.dumps(r), flush=True)
         del X
@@ -166,7 +214,7 @@ def sparse_cases(out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "kernels.jsonl"))
-    ap.add_argument("--only", choices=["dense", "sparse", "scale", "eval"], default=None)
+    ap.add_argument("--only", choices=["dense", "sparse", "scale", "eval", "sweep"], default=None)
     a = ap.parse_args()
     out = []
     if a.only in (None, "dense"):
@@ -175,6 +223,8 @@ def main():
         scale_cases(out)
     if a.only == "eval":
         eval_cases(out)
+    if a.only == "sweep":
+        sweep_cases(out)
     if a.only in (None, "sparse"):
         sparse_cases(out)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)

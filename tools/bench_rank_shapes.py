@@ -1,12 +1,13 @@
 """Per-rank gradient work of the headline at N = 1/2/4/8 GPUs, timed on one MI355X.
 
-    python tools/bench_rank_shapes.py [--rows-sweep] [--out FILE]
+    python tools/bench_rank_shapes.py [--shard partition|message] [--rows-sweep] [--out FILE]
 
 With partition shards (parallel/placement.py) the rank of an N-GPU headline run (AGC W=8, s=2,
-k=6, 1e6 x 1e3 fp64) holds 8/N partitions of 125k rows, each with its 2-3 replica messages.
-This builds exactly that local plan (DenseGradPlan over the rank's shards) and times one
+k=6, 1e6 x 1e3 fp64) holds 8/N partitions of 125k rows, each with its 2-3 replica messages; with
+whole messages (the reference topology) it holds its logical workers' 3 partitions each.  This
+builds exactly the heaviest rank's local plan (DenseGradPlan over its units) and times one
 gradient launch with HIP events: the compute floor of one round at that N.  --rows-sweep also
-times the staged bundle task sizes (ERASUREHEAD_BUNDLE_ROWS) at each shape.
+times other bundle lengths of the chosen kernel at each shape.
 """
 from __future__ import annotations
 
@@ -20,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def one(n_gpus: int, precision: str) -> dict:
+def one(n_gpus: int, precision: str, shard: str = "partition", rows: int = 0) -> dict:
     import numpy as np
     import torch
 
@@ -28,13 +29,18 @@ def one(n_gpus: int, precision: str) -> dict:
     from erasurehead_amd.data.source import SyntheticSource
     from erasurehead_amd.models.losses import LOGISTIC
     from erasurehead_amd.ops import DenseGradPlan, get_precision
-    from erasurehead_amd.parallel.placement import make_shards, place_units
+    from dataclasses import replace
+
+    from erasurehead_amd.ops.grad import choose_cpl, choose_kernel
+    from erasurehead_amd.parallel.placement import make_shards, place_spread, place_units
 
     prec = get_precision(precision)
     sch = make_scheme("approx", 8, 2, 1_000_000, 6, 0, allow_uneven=True)
     rows = sch.rows_per_partition
-    shards = make_shards(sch.messages, "partition" if n_gpus > 1 else "message")
-    owner = place_units([[(p, rows) for p, _ in u.segments] for u in shards], n_gpus, 0.12)
+    mode = shard if n_gpus > 1 else "message"
+    shards = make_shards(sch.messages, mode)
+    owner = (place_units([[(p, rows) for p, _ in u.segments] for u in shards], n_gpus, 0.12) if mode == "partition"
+             else place_spread([u.worker for u in shards], n_gpus))
     costs = []
     for r in range(n_gpus):  # time the heaviest rank
         mine = [u for u, o in zip(shards, owner) if o == r]
@@ -42,9 +48,19 @@ def one(n_gpus: int, precision: str) -> dict:
     _, _, r = max(costs)
     mine = [u for u, o in zip(shards, owner) if o == r]
     src = SyntheticSource(1_000_000, 1000, sch.n_partition_files, 1234)
+    bundle_rows = rows
     need = sorted({p for u in mine for p, _ in u.segments})
     parts = {p: src.partition(p, prec, torch.device("cuda")) for p in need}
-    plan = DenseGradPlan([list(u.segments) for u in mine], parts, prec, LOGISTIC, 1000)
+    msgs = [list(u.segments) for u in mine]
+    choice = None
+    if bundle_rows:  # the default kernel with another bundle length
+        import collections
+
+        max_rep = max(collections.Counter(p for m in msgs for p, _ in m).values())
+        distinct = sum(parts[p][0].shape[0] for p in need)
+        choice = replace(choose_kernel(prec.code, prec.ld(1000), choose_cpl(prec.ld(1000), prec.vec), max_rep, distinct),
+                         bundle_rows=bundle_rows)
+    plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, choice=choice)
     beta = torch.randn(prec.ld(1000), device="cuda", dtype=prec.acc) * 0.01
     G = plan.out_buffer()[0]
     for _ in range(5):
@@ -56,8 +72,8 @@ def one(n_gpus: int, precision: str) -> dict:
         b.record()
     torch.cuda.synchronize()
     ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
-    return {"n_gpus": n_gpus, "precision": precision, "rank": r, "partitions": len(need), "shards": len(mine),
-            "bundle_rows": plan.bundle_rows, "variant": plan.variant, "ntasks": plan.ntasks,
+    return {"n_gpus": n_gpus, "precision": precision, "shard": mode, "rank": r, "partitions": len(need),
+            "shards": len(mine), "bundle_rows": plan.bundle_rows, "kernel": plan.choice.label(), "ntasks": plan.ntasks,
             "kernel_ms": ms, "distinct_TBps": plan.distinct_bytes / ms / 1e9}
 
 
@@ -66,25 +82,25 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--rows-sweep", action="store_true")
     ap.add_argument("--precision", default="fp64")
+    ap.add_argument("--shard", default="partition", choices=["partition", "message"])
     ap.add_argument("--one", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--rows", type=int, default=0, help=argparse.SUPPRESS)
     a = ap.parse_args()
     if a.one:
-        print(json.dumps(one(a.one, a.precision)), flush=True)
+        print(json.dumps(one(a.one, a.precision, a.shard, a.rows)), flush=True)
         return 0
     lines = []
     sweeps = [None] + ([64, 128, 256, 512] if a.rows_sweep else [])
     for n in (1, 2, 4, 8):
         for rows in sweeps:
-            env = dict(os.environ)
-            if rows:
-                env["ERASUREHEAD_BUNDLE_ROWS"] = str(rows)
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", str(n), "--precision",
-                                  a.precision], env=env, capture_output=True, text=True, timeout=300)
+                                  a.precision, "--shard", a.shard, "--rows", str(rows or 0)],
+                                 capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print(out.stdout[-2000:], out.stderr[-2000:], file=sys.stderr)
                 return 1
             rec = json.loads(out.stdout.strip().splitlines()[-1])
-            rec["rows_env"] = rows
+            rec["rows_override"] = rows
             print(json.dumps(rec), flush=True)
             lines.append(rec)
     if a.out:

@@ -47,11 +47,8 @@ def _hash_inputs(csrc: str = CSRC):
 
 
 def _defines():
-    """Build-time debug / A-B switches (part of the provenance hash)."""
-    d = []
-    if os.environ.get("ERASUREHEAD_FULL_VMCNT") == "1":
-        d.append("-DEH_FULL_VMCNT")
-    return d
+    """Build-time defines (part of the provenance hash); none by default."""
+    return []
 
 
 def source_hash(csrc: str = CSRC) -> str:

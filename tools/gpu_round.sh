@@ -1,0 +1,85 @@
+#!/bin/bash
+# One GPU round on a fresh MI355X box, in stages (each under its own time limit; the first failure
+# ends the script, nothing more touches the GPU after it):
+#
+#   gpurun --timeout 1200 -- 'bash tools/gpu_round.sh OUT=gpurun_out/r5 tests smoke bench prec'
+#
+#   tests    python -m pytest tests -m gpu (thread timeouts, so a hang names its test)
+#   smoke    __graft_entry__.smoke()
+#   bench    bench.py at N=1 (20 steps as the driver runs it, then 100 settled steps)
+#   prec     the headline in fp32 and bf16 (20 steps)
+#   shapes   the heaviest rank's gradient at every N-GPU placement (tools/bench_rank_shapes.py)
+#   sweep    dense gradient shape sweep vs the copy ceiling (tools/bench_kernels.py --only sweep)
+#   rehearse 2/4/8 ranks time-sharing this GPU through bench.py --gpus N (host pump and arbiter)
+#   prof     rocprofv3 --kernel-trace --stats of the fp64 / fp32 / bf16 headline
+#   pmc      counter passes (one rocprofv3 --pmc run each) of the fp64 / fp32 headline
+#   eval     evaluation phase profile (tools/profile_eval.py)
+set -o pipefail
+OUT=gpurun_out/round
+STAGES=()
+for a in "$@"; do
+  case "$a" in
+    OUT=*) OUT="${a#OUT=}" ;;
+    *) STAGES+=("$a") ;;
+  esac
+done
+mkdir -p "$OUT"
+OUT=$(cd "$OUT" && pwd)
+export TMPDIR=/tmp
+log() { echo "[$(date +%T)] $*"; }
+run() {  # run <seconds> <log> <cmd...>
+  local t=$1 f=$2; shift 2
+  log "start $f"
+  timeout -k 10 "$t" "$@" > "$OUT/$f" 2>&1
+  local rc=$?
+  log "end $f rc=$rc"
+  if [ $rc -ne 0 ]; then tail -30 "$OUT/$f"; exit $rc; fi
+}
+BENCH="python -u bench.py --no-floor"
+for s in "${STAGES[@]}"; do
+  case "$s" in
+    tests)
+      run 1500 pytest.log python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+      tail -3 "$OUT/pytest.log" ;;
+    smoke)
+      run 300 smoke.log python -c 'import __graft_entry__ as g; g.build(); g.smoke(); print("smoke ok")' ;;
+    bench)
+      run 600 bench.log python -u bench.py && tail -1 "$OUT/bench.log" > "$OUT/bench.json"
+      run 600 bench100.log $BENCH --steps 100 --warmup 10 && tail -1 "$OUT/bench100.log" > "$OUT/bench100.json"
+      cat "$OUT/bench.json" ;;
+    prec)
+      for p in fp32 bf16; do
+        run 600 "bench_$p.log" $BENCH --precision $p && tail -1 "$OUT/bench_$p.log" > "$OUT/bench_$p.json"
+      done ;;
+    shapes)
+      run 900 shapes.log python -u tools/bench_rank_shapes.py --out "$OUT/shapes.jsonl" ;;
+    sweep)
+      run 1100 sweep.log python -u tools/bench_kernels.py --only sweep --out "$OUT/sweep.jsonl" ;;
+    rehearse)
+      for n in 2 4 8; do
+        run 600 "rehearse_$n.log" python -u bench.py --gpus $n --steps 20 --warmup 5 --no-floor \
+          --json-out "$OUT/rehearse_$n.json"
+      done ;;
+    prof)
+      for p in fp64 fp32 bf16; do
+        run 600 "prof_$p.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$p" -o run -- \
+          python bench.py --no-floor --no-breakdown --precision $p --steps 50
+      done ;;
+    pmc)
+      G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY"
+      G2="SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM"
+      for p in fp64 fp32; do
+        i=0
+        for grp in "$G1" "$G2" "FETCH_SIZE"; do
+          i=$((i+1))
+          run 120 "pmc_${p}_$i.log" rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc" -o "${p}_$i" -- \
+            python bench.py --no-floor --no-breakdown --precision $p --steps 4 --warmup 1
+        done
+      done
+      python tools/pmc_summary.py "$OUT/pmc" > "$OUT/pmc_summary.json" ;;
+    eval)
+      run 600 eval.log python -u tools/profile_eval.py --out "$OUT/eval.json" ;;
+    *) echo "unknown stage $s"; exit 2 ;;
+  esac
+done
+log "all stages done"
