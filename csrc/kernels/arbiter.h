@@ -54,9 +54,9 @@ struct ArbArgs {
   long long* tlog;                       // [R][kArbLogTicks]
   int* abort;                            // set by a failed round: every later arbiter returns at once
   // Integrity (integrity.h; tags == nullptr: off): the mailbox rows round i decodes are checked
-  // against their senders' tags by round i+1's idle waves while its wave 0 polls (a segment's last
-  // round by a tail check), and beta(i+1) carries a tag into every worker inbox (inbox base +
-  // inbox_tag_off, one per round).
+  // against their senders' tags by arbiter_check on a side stream during round i+1's local
+  // gradient (arbiter i+1 fails if it found one), and beta(i+1) carries a tag into every worker
+  // inbox (inbox base + inbox_tag_off, one per round).
   const MsgTag* tags;                    // [K][r_rows] mailbox tags
   const int* row_rank;                   // [r_rows] sender rank of each mailbox row
   long long inbox_tag_off;               // bytes from a worker inbox base to its tag slots
@@ -64,13 +64,13 @@ struct ArbArgs {
   IntegrityErr* err;                     // host-mapped: the first failed check
 };
 // Round statuses in the log: 0 ok, 1 timeout, 2 not decodable, 3 skipped, 4 integrity failure of the
-// PREVIOUS round's messages (found by this round's idle waves; details in ArbArgs::err).
+// PREVIOUS round's messages (found by its arbiter_check; details in ArbArgs::err).
 constexpr int kArbIntegrity = 4;
 
 // msg_dtype 0 fp64 / 1 fp32 (messages, beta_in, inboxes)
-// check_prev: this round's idle waves check round-1's mailbox rows (false for a segment's first round)
+// check_prev: round-1's rows were checked (arbiter_check) before this launch: fail on a reported error
 hipError_t arbiter_round_launch(const ArbArgs& a, int round, int msg_dtype, hipStream_t st, bool check_prev);
-// after a segment's last round: check that round's rows (no later arbiter does)
-hipError_t arbiter_tail_check_launch(const ArbArgs& a, int round, hipStream_t st);
+// round's decoded mailbox rows against their tags (a no-op with tags off)
+hipError_t arbiter_check_launch(const ArbArgs& a, int round, hipStream_t st);
 
 }  // namespace eh

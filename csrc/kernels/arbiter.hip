@@ -42,6 +42,12 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
   __shared__ int s_pw[kArbMaxProbes], s_pp[kArbMaxProbes], s_ps[kArbMaxProbes];
   __shared__ int batch[kArbMaxProbes];
   __shared__ int got_sh[2 * kArbMaxW];
+  // the round's tables in LDS: thread 0's books and decode walk them serially (a dependent global load
+  // per step cost ~15 us per round)
+  __shared__ int s_key[kArbMaxProbes];  // tie rank of each probe's worker
+  __shared__ int s_group[kArbMaxW], s_nsh[2 * kArbMaxW], s_nrows[2 * kArbMaxW];
+  __shared__ int s_rows[2 * kArbMaxW * kArbMaxRows];
+  __shared__ double s_trow[kArbMaxW];   // decode-table row of the round's completion pattern
   __shared__ int arr_w[2 * kArbMaxW], arr_p[2 * kArbMaxW];
   __shared__ long long arr_t[2 * kArbMaxW];
   __shared__ const void* mptr[kMaxMsgs];
@@ -49,6 +55,7 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
   __shared__ int mrow[kMaxMsgs];  // kind << 24 | row of every used buffer row
   __shared__ unsigned long long scratch[16];
   __shared__ int s_narr, s_nmsg, s_status, s_bad;
+  __shared__ unsigned long long s_mask;
   __shared__ unsigned long long s_bsum;
   const int tid = threadIdx.x;
   int* lg = a.log + static_cast<long long>(i) * kArbLogInts;
@@ -57,12 +64,21 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
     if (tid == 0) lg[0] = 3;
     return;
   }
+  const int* tie = a.tie + static_cast<long long>(i) * a.W;
   for (int q = tid; q < a.nprobe; q += blockDim.x) {
-    s_pw[q] = a.probe_w[q];
+    const int w = a.probe_w[q];
+    s_pw[q] = w;
     s_pp[q] = a.probe_p[q];
     s_ps[q] = a.probe_src[q];
+    s_key[q] = tie[w];
   }
-  for (int m = tid; m < 2 * a.W; m += blockDim.x) got_sh[m] = 0;
+  for (int m = tid; m < 2 * a.W; m += blockDim.x) {
+    got_sh[m] = 0;
+    s_nsh[m] = a.nsh[m];
+    s_nrows[m] = a.msg_nrows[m];
+  }
+  for (int e = tid; e < 2 * a.W * kArbMaxRows; e += blockDim.x) s_rows[e] = a.msg_rows[e];
+  for (int w = tid; w < a.W; w += blockDim.x) s_group[w] = a.group_of[w];
   if (tid == 0) {
     s_narr = 0;
     s_nmsg = 0;
@@ -72,7 +88,6 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
   __syncthreads();
 
   // ---- 1. poll until the stop rule holds (wave 0) -------------------------------------------
-  const int* tie = a.tie + static_cast<long long>(i) * a.W;
   unsigned long long seen = 0;  // sources seen so far (wave-uniform)
   if (tid < 64) {
     const long long t0 = wall_clock64();
@@ -92,9 +107,9 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
           }
           for (int x = 1; x < nb; ++x) {  // (tie rank, probe id) order
             const int q = batch[x];
-            const int kq = tie[s_pw[q]];
+            const int kq = s_key[q];
             int y = x - 1;
-            while (y >= 0 && (tie[s_pw[batch[y]]] > kq || (tie[s_pw[batch[y]]] == kq && batch[y] > q))) {
+            while (y >= 0 && (s_key[batch[y]] > kq || (s_key[batch[y]] == kq && batch[y] > q))) {
               batch[y + 1] = batch[y];
               --y;
             }
@@ -104,7 +119,7 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
             const int q = batch[x];
             const int w = s_pw[q], p = s_pp[q];
             const int mi = 2 * w + p;
-            if (++got_sh[mi] < a.nsh[mi] || stopped) continue;  // more shards to come / late
+            if (++got_sh[mi] < s_nsh[mi] || stopped) continue;  // more shards to come / late
             arr_w[s_narr] = w;
             arr_p[s_narr] = p;
             arr_t[s_narr] = t;
@@ -113,7 +128,7 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
               if (!(got0 >> w & 1)) {
                 got0 |= 1ull << w;
                 ++cnt0;
-                const int g = a.group_of[w];
+                const int g = s_group[w];
                 if (!(gdone >> g & 1)) {
                   gdone |= 1ull << g;
                   ++cntg;
@@ -140,10 +155,19 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
       }
       __builtin_amdgcn_s_sleep(2);
     }
-  } else if (a.tags && check_prev) {
-    // waves 1..15 meanwhile check the mailbox rows the PREVIOUS round decoded against their senders'
-    // tags (integrity.h): off the critical path, those rows stay intact until their slot comes back
-    check_rows_waves(a.checks[(i - 1) & 1], 1, static_cast<int>(blockDim.x >> 6) - 1, a.err, &s_bad);
+    // the completion pattern (every p = 0 arrival) and its decode-table row, one lane per worker
+    const unsigned long long mask = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(got0)) |
+                                    static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(
+                                        static_cast<unsigned>(got0 >> 32))) << 32;
+    if (tid == 0) s_mask = mask;
+    if ((a.decode == 3 || a.decode == 4) && a.table)
+      for (int w = tid; w < a.W; w += 64)
+        s_trow[w] = (mask >> w & 1) ? a.table[static_cast<long long>(mask) * a.W + w] : 0.0;
+  } else if (a.tags && check_prev && tid == 64) {
+    // the previous round's mailbox rows were checked against their senders' tags by a side-stream
+    // kernel during this round's local gradient (arbiter_check, queued ahead of this kernel): a
+    // failure there fails this round
+    if (__hip_atomic_load(&a.err->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) s_bad = 1;
   }
   __syncthreads();
   if (s_status == 0 && s_bad) s_status = kArbIntegrity;  // a torn / stale message of round i-1
@@ -162,8 +186,8 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
   if (tid == 0) {
     auto push = [&](int w, int p, double c) {
       const int mi = 2 * w + p;
-      for (int r = 0; r < a.msg_nrows[mi]; ++r) {
-        const int e = a.msg_rows[mi * kArbMaxRows + r];
+      for (int r = 0; r < s_nrows[mi]; ++r) {
+        const int e = s_rows[mi * kArbMaxRows + r];
         const int row = e & 0xffffff;
         const M* base = (e >> 24) == 0
                             ? static_cast<const M*>(a.G) + (static_cast<long long>(slot) * a.g_rows + row) * a.ld
@@ -176,7 +200,7 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
         ++s_nmsg;
       }
     };
-    unsigned long long gd = 0, mask = 0;
+    unsigned long long gd = 0;
     for (int x = 0; x < s_narr; ++x) {
       const int w = arr_w[x], p = arr_p[x];
       if (p == 1) {
@@ -186,26 +210,25 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
       if (a.decode == 0) {
         push(w, 0, 1.0);
       } else if (a.decode == 1 || a.decode == 2) {
-        const int g = a.group_of[w];
+        const int g = s_group[w];
         if (!(gd >> g & 1)) {
           gd |= 1ull << g;
           push(w, 0, 1.0);
         }
-      } else {
-        mask |= 1ull << w;
       }
     }
     if (a.decode == 3 || a.decode == 4) {
-      const double* row = a.table ? a.table + static_cast<long long>(mask) * a.W : nullptr;
-      for (int w = 0; w < a.W && row; ++w) {
+      const unsigned long long mask = s_mask;
+      for (int w = 0; w < a.W && a.table; ++w) {
         if (!(mask >> w & 1)) continue;
-        if (row[w] != row[w]) {  // NaN: completion pattern without a table row
+        const double c = s_trow[w];
+        if (c != c) {  // NaN: completion pattern without a table row
           s_status = 2;
           break;
         }
-        push(w, 0, row[w]);
+        push(w, 0, c);
       }
-      if (!row) s_status = 2;
+      if (!a.table) s_status = 2;
     }
     if (s_nmsg > kMaxMsgs) s_status = 2;
   }
@@ -340,8 +363,10 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
   }
 }
 
-// The segment's last round has no successor to check its rows: one workgroup does it.
-__global__ void __launch_bounds__(1024) arbiter_tail_check(const ArbArgs a, int i) {
+// Round i's decoded mailbox rows against their senders' tags: one workgroup on a side stream, queued
+// behind arbiter i and ahead of arbiter i+1 (MasterPump::run_device), so it runs during round i+1's
+// local gradient; the rows stay intact until their slot comes back (K >= 2 rounds later).
+__global__ void __launch_bounds__(1024) arbiter_check(const ArbArgs a, int i) {
   __shared__ int claim;
   if (threadIdx.x == 0) claim = 0;
   __syncthreads();
@@ -358,9 +383,9 @@ hipError_t arbiter_round_launch(const ArbArgs& a, int round, int msg_dtype, hipS
   return hipGetLastError();
 }
 
-hipError_t arbiter_tail_check_launch(const ArbArgs& a, int round, hipStream_t st) {
+hipError_t arbiter_check_launch(const ArbArgs& a, int round, hipStream_t st) {
   if (!a.tags) return hipSuccess;
-  hipLaunchKernelGGL(arbiter_tail_check, dim3(1), dim3(1024), 0, st, a, round);
+  hipLaunchKernelGGL(arbiter_check, dim3(1), dim3(1024), 0, st, a, round);
   return hipGetLastError();
 }
 

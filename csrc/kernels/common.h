@@ -204,7 +204,7 @@ __device__ __forceinline__ A sigmoid_neg(A t) {
 // exp(-|t|) is in (0, 1], so 1 + e is in [1, 2] and neither can overflow.  Used where a wave's
 // lanes hold different rows (the MFMA bundles: 0.382 -> 0.371 ms at the bf16 headline).  The
 // fp32 staged pair kernel measured SLOWER with it (0.737 -> 0.81 ms, same box,
-// profiles/r2_ab_fastsig), so the library form stays the default elsewhere.
+// profiles/round2/s1_ab_fastsig), so the library form stays the default elsewhere.
 __device__ __forceinline__ float sigmoid_neg_hw(float t) {
   const float e = __builtin_amdgcn_exp2f(-__builtin_fabsf(t) * 1.4426950408889634f);
   const float q = __builtin_amdgcn_rcpf(1.0f + e);

@@ -283,7 +283,7 @@ hipError_t tr_probe_launch(const float* tile, int rowlen, float* out, hipStream_
 }
 
 // Geometry of grad_staged_mfma: rows per stage S (32, 2-stage ring: 0.48 vs 0.59 ms for 16-row
-// stages in a 4-deep ring at the bf16 headline, profiles/r2_mfma), LDS-DMA pieces per wave per
+// stages in a 4-deep ring at the bf16 headline, profiles/round2/s1_mfma), LDS-DMA pieces per wave per
 // stage, ring depth and LDS bytes; false when ld does not fit.
 bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds) {
   if (ld < 8 || ld > kMfNW * kMfKPW * 32 || ld % 8) return false;

@@ -353,6 +353,12 @@ class MasterPump {
     csum_ = at::zeros({eh::kMaxPuts * eh::kMaxTagRows}, i64);  // beta put checksums
   }
   ~MasterPump() {
+    if (chk_stream_) {
+      hipStreamSynchronize(chk_stream_);
+      hipStreamDestroy(chk_stream_);
+      hipEventDestroy(arb_ev_);
+      hipEventDestroy(chk_ev_);
+    }
     if (dev_stream_) {
       hipStreamSynchronize(dev_stream_);
       for (auto g : graphs_) hipGraphExecDestroy(g);
@@ -824,16 +830,31 @@ class MasterPump {
       put_beta(a);
       hcheck(eh::stamp_launch(tlog + static_cast<int64_t>(a) * eh::kArbLogTicks, stream_), "stamp");
     }
+    // Integrity checks ride a side stream: check(i) waits for arbiter i, runs during round i+1's local
+    // gradient, and arbiter i+1 waits for it (it fails the round if check(i) found a torn row).
+    const bool chk = args.tags != nullptr;
+    if (chk && !chk_stream_) {
+      hcheck(hipStreamCreateWithFlags(&chk_stream_, hipStreamNonBlocking), "hipStreamCreate");
+      hcheck(hipEventCreateWithFlags(&arb_ev_, hipEventDisableTiming), "hipEventCreate");
+      hcheck(hipEventCreateWithFlags(&chk_ev_, hipEventDisableTiming), "hipEventCreate");
+    }
     for (int i = a; i < b; ++i) {
       if (n_loc_ > 0 && launcher_) {
         char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(i % K_) * g_rows_ * ld_ * es_;
         for (int k = 0; k < repeat_; ++k)
           hcheck(launcher_->launch(bin + static_cast<int64_t>(i) * ld_ * es_, g, stream_), "local gradient");
       }
-      hcheck(eh::arbiter_round_launch(args, i, acc_, stream_, i > a), "arbiter_round");
+      if (chk && i > a) hcheck(hipStreamWaitEvent(stream_, chk_ev_, 0), "hipStreamWaitEvent");
+      hcheck(eh::arbiter_round_launch(args, i, acc_, stream_, chk && i > a), "arbiter_round");
+      if (chk) {
+        hcheck(hipEventRecord(arb_ev_, stream_), "hipEventRecord");
+        hcheck(hipStreamWaitEvent(chk_stream_, arb_ev_, 0), "hipStreamWaitEvent");
+        hcheck(eh::arbiter_check_launch(args, i, chk_stream_), "arbiter_check");
+        hcheck(hipEventRecord(chk_ev_, chk_stream_), "hipEventRecord");
+      }
     }
     if (b > a) {
-      hcheck(eh::arbiter_tail_check_launch(args, b - 1, stream_), "arbiter_tail_check");
+      if (chk) hcheck(hipStreamWaitEvent(stream_, chk_ev_, 0), "hipStreamWaitEvent");  // device_log sees it
       prepub_ = b;
     }
   }
@@ -1268,6 +1289,8 @@ class MasterPump {
   std::vector<hipEvent_t> loc_ev_;
   std::vector<hipGraphExec_t> graphs_;  // device-driven segments (destroyed after a sync)
   hipStream_t dev_stream_ = nullptr;     // stream of the device-driven rounds (capturable)
+  hipStream_t chk_stream_ = nullptr;     // run_device: arbiter_check kernels beside the local gradient
+  hipEvent_t arb_ev_ = nullptr, chk_ev_ = nullptr;
   hipEvent_t join_ev_ = nullptr;
   int graph_segments_ = 0;
   bool timing_ = false;

@@ -732,7 +732,7 @@ class Trainer:
         """Stream-side waits on the shared flags (hipStreamWaitValue64): a worker's wait for beta and
         the master's drain before the next beta.  On when every rank has its GPU to itself; ranks
         time-sharing one GPU keep host waits (a queued wait competes with the other ranks' kernels
-        there: profiles/r2_worker_wait/).  ERASUREHEAD_WORKER_WAIT=host|device|auto."""
+        there: profiles/round2/s1_worker_wait/).  ERASUREHEAD_WORKER_WAIT=host|device|auto."""
         mode = os.environ.get("ERASUREHEAD_WORKER_WAIT", "auto")
         if getattr(tx, "name", "") != "ipc" or mode == "host":
             return False

@@ -166,7 +166,7 @@ def loss_sums(chunks: Iterable[Tuple[object, torch.Tensor]], B: torch.Tensor, d:
 def warm_auc(device) -> None:
     """Load the code objects of the AUC path (torch's segmented sort, scans, index_add) once.
 
-    Measured (profiles/r2_eval): the first auc_columns call of a process costs 0.6 s, all of it
+    Measured (profiles/round2/s1_eval): the first auc_columns call of a process costs 0.6 s, all of it
     first-use code-object loading (the same call warm: 4.5 ms for 100 x 2e5).  The trainer runs
     this on the master while it generates / loads the training data, so the post-hoc evaluation
     does not pay it."""

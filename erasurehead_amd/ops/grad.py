@@ -39,7 +39,7 @@ N_CUS = 256  # MI355X compute units (8 XCDs x 32)
 # round: there the gradient is HBM-bound with fewer, longer bundles (their per-bundle beta load,
 # fold and slab write amortise over more rows), below it the grid must fill every wave slot.  The
 # measured crossover lies between 500k and 1e6 rows of 1000 columns on 256 CUs (N = 2 vs N = 1 of
-# the headline, profiles/r3_multi, r3_epi); 2900 rows per CU (~742k rows) sits in between.
+# the headline, profiles/round2/s2_multi, round2/s2_epi); 2900 rows per CU (~742k rows) sits in between.
 LONG_STREAM_ROWS_PER_CU = 2900
 
 KIND_IDS = {"fused": 0, "multi": 1, "staged": 2, "mfma": 3, "wide": 4, "twopass": -1}
@@ -104,7 +104,7 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
     3 per SIMD).  Below the long-stream regime a rank fills every slot (one bundle per wave slot);
     in it, fewer, longer bundles win (HBM-bound: ~10 MB of rows in flight already saturate it, and
     each bundle's beta load / fold / slab write amortises over more rows): 5 bundles per CU fp64,
-    10 fp32.  Measured (tools/sweep_multi_rows.sh, profiles/r3_multi): N=1 fp64 768 rows 1.330 ms vs
+    10 fp32.  Measured (tools/sweep_multi_rows.sh, profiles/round2/s2_multi): N=1 fp64 768 rows 1.330 ms vs
     512 1.36 / 640 1.37 / 1024 1.54; N=2 256 rows 0.708; N=4 128 rows 0.370 vs 96 0.45 / 160 0.40;
     N=8 64 rows 0.206 vs 48 0.25 / 80 0.22; fp32 N=1 384 rows 0.692 (320: 0.95, a second pass)."""
     long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
@@ -124,7 +124,7 @@ def mfma_bundle_rows(distinct_rows: int) -> int:
 
 def staged_bundle_rows(distinct_rows: int, n_cus: int = N_CUS) -> int:
     """Rows per LDS-staged bundle: 512 in the long-stream regime (measured 512 > 256, 1024; 2048 leaves
-    CUs idle), 128 below it (profiles/r2_shapes: N=8 0.238 vs 0.415 ms, N=2 0.80 vs 0.99 ms at 512)."""
+    CUs idle), 128 below it (profiles/round2/s1_shapes: N=8 0.238 vs 0.415 ms, N=2 0.80 vs 0.99 ms at 512)."""
     return 512 if distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus else 128
 
 
@@ -155,12 +155,13 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
     if prec_code == 2:
         if ld <= 1024 and ld % 8 == 0 and max_rep <= 16:
-            return KernelChoice("mfma", replicas=max_rep, bundle_rows=mfma_bundle_rows(distinct_rows))
+            return KernelChoice("mfma", replicas=min(max_rep, MAX_BUNDLE), bundle_rows=mfma_bundle_rows(distinct_rows))
         return KernelChoice("fused", rows=1, interleave=True)
     if cpl <= 16 and max_rep == 3 and (prec_code == 0 or long_stream):
         return KernelChoice("multi", replicas=3, bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus),
                             fold=True, lane_epi=not long_stream)
-    return KernelChoice("staged", replicas=max_rep, bundle_rows=staged_bundle_rows(distinct_rows, n_cus),
+    # more replicas than a workgroup's task slots: bundles of MAX_BUNDLE (and the remainder, padded)
+    return KernelChoice("staged", replicas=min(max_rep, MAX_BUNDLE), bundle_rows=staged_bundle_rows(distinct_rows, n_cus),
                         pair=prec_code == 1 or not long_stream, wpr=0 if long_stream else 1)
 
 

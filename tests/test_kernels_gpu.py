@@ -462,7 +462,7 @@ def test_mfma_bf16_replica_bundles(d, loss, native):
             [(2, 1.0)], [(2, 1.0)],  # group of 2
             [(0, 0.5), (2, -1.25)], [(1, 2.0)]]  # distinct coefficients
     plan = DenseGradPlan(msgs, parts, prec, loss, d)
-    assert plan.choice.kind == "mfma" and plan.choice.replicas == 3
+    assert plan.choice.kind == "mfma" and plan.choice.replicas == 4  # partition 0 is read by messages 0, 1, 2 and 5
     beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
     b = rng.randn(d) * 0.3
     beta[:d] = torch.from_numpy(b).to(prec.acc)

@@ -75,6 +75,8 @@ def test_kernel_selection_table():
     # FRC s=1 (bundles of 2): staged, one GPU / a sharded rank
     assert pick(0, 1000, 2, 1_000_000) == KernelChoice("staged", replicas=2, bundle_rows=512)
     assert pick(0, 1000, 2, 250_000) == KernelChoice("staged", replicas=2, bundle_rows=128, pair=True, wpr=1)
+    # more co-located replicas than task slots per workgroup (a cyclic W = 9 table on one rank): bundles of 8
+    assert pick(0, 1000, 9, 1_000_000).replicas == 8 and pick(2, 1000, 9, 1_000_000).replicas == 8
     # distinct rows (naive): the fused kernel per precision
     assert [pick(p, 1000, 1, 1_000_000) for p in (0, 1, 2)] == [KernelChoice("fused", rows=2), KernelChoice("fused", rows=4),
                                                                    KernelChoice("fused", rows=1)]

@@ -1,4 +1,4 @@
-"""Is the slow stretch after an idle period (profiles/r3_prof/per_call_grad_us.txt) the platform's
+"""Is the slow stretch after an idle period (profiles/round2/s2_prof/per_call_grad_us.txt) the platform's
 power management or the gradient kernel?  Times back-to-back reads of 8 GB with torch (a plain
 sum, no LDS, no replicas) after an idle second, per call, with HIP events.  Prints one JSON line."""
 import json
