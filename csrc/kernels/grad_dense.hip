@@ -726,22 +726,33 @@ grad_dense_fused_pair(const Segment* __restrict__ segs, const Task* __restrict__
 // one barrier per pair); the loss residual is then applied from registers, so X is read
 // from HBM exactly once.  Columns are disjoint per thread: the slab row is written
 // directly, no LDS fold.
-template <typename T, typename A, int NV, int BS, int LOSS>
+// R > 1: a replica bundle (R task slots per workgroup, all reading the same rows, ops/grad.py): each
+// row is loaded once and every replica computes its own dot product, residual (own coefficient) and
+// gradient from the registers, so the replicated messages cost one HBM stream (the interleaved
+// dispatch re-read them through L2 at ~4 TB/s, profiles/round3/choices).
+template <typename T, typename A, int NV, int BS, int LOSS, int R>
 __global__ void __launch_bounds__(BS)
 grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                 const A* __restrict__ beta, A* __restrict__ slab, int ld) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NW = BS / kWave;
-  __shared__ A part[2][2][NW];  // [buffer][row of the pair][wave]
+  __shared__ A part[2][2][R][NW];  // [buffer][row of the pair][replica][wave]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const Task task = tasks[blockIdx.x];
-  const Segment seg = segs[task.seg];
+  const Task lead = tasks[blockIdx.x * R];  // slot 0 of a bundle is always a real task
+  const Segment seg = segs[lead.seg];
   const T* __restrict__ X = static_cast<const T*>(seg.X);
   const A* __restrict__ Y = static_cast<const A*>(seg.y);
-  const A coef = static_cast<A>(seg.coef);
+  A coef[R];
+  bool act[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const Task tq = tasks[blockIdx.x * R + q];
+    act[q] = tq.seg >= 0;
+    coef[q] = act[q] ? static_cast<A>(segs[tq.seg].coef) : A(0);
+  }
 
   bool valid[NV];
-  A b[NV][VN], g[NV][VN];
+  A b[NV][VN], g[R][NV][VN];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int c0 = (j * BS + tid) * VN;
@@ -749,12 +760,13 @@ grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks
 #pragma unroll
     for (int v = 0; v < VN; ++v) {
       b[j][v] = valid[j] ? beta[c0 + v] : A(0);
-      g[j][v] = A(0);
+#pragma unroll
+      for (int q = 0; q < R; ++q) g[q][j][v] = A(0);
     }
   }
   int buf = 0;
-  for (int r = task.row_begin; r < task.row_end; r += 2) {
-    const bool two = r + 1 < task.row_end;
+  for (int r = lead.row_begin; r < lead.row_end; r += 2) {
+    const bool two = r + 1 < lead.row_end;
     const T* x0 = X + static_cast<long long>(r) * ld;
     const T* x1 = X + static_cast<long long>(two ? r + 1 : r) * ld;
     A a0[NV][VN], a1[NV][VN];
@@ -769,42 +781,83 @@ grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks
         for (int v = 0; v < VN; ++v) { a0[j][v] = A(0); a1[j][v] = A(0); }
       }
     }
-    A z0 = A(0), z1 = A(0);
+    A z0[R], z1[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      z0[q] = A(0);
+      z1[q] = A(0);
+      asm volatile("" : "+v"(z0[q]), "+v"(z1[q]));  // opaque start: R separate dot products
+    }
 #pragma unroll
     for (int j = 0; j < NV; ++j)
 #pragma unroll
-      for (int v = 0; v < VN; ++v) {
-        z0 = fma(a0[j][v], b[j][v], z0);
-        z1 = fma(a1[j][v], b[j][v], z1);
+      for (int v = 0; v < VN; ++v)
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+          z0[q] = fma(a0[j][v], b[j][v], z0[q]);
+          z1[q] = fma(a1[j][v], b[j][v], z1[q]);
+        }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      z0[q] = wave_allreduce_sum(z0[q]);
+      z1[q] = wave_allreduce_sum(z1[q]);
+      if (lane == 0) {
+        part[buf][0][q][wid] = z0[q];
+        part[buf][1][q][wid] = z1[q];
       }
-    z0 = wave_allreduce_sum(z0);
-    z1 = wave_allreduce_sum(z1);
-    if (lane == 0) {
-      part[buf][0][wid] = z0;
-      part[buf][1][wid] = z1;
     }
     __syncthreads();
-    A s0 = A(0), s1 = A(0);
+    const A y0 = Y[r], y1 = two ? Y[r + 1] : A(0);
+    A r0[R], r1[R];
+    if constexpr (R == 1) {
+      A s0 = A(0), s1 = A(0);
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {  // fixed order: every thread gets the bitwise-same sums
-      s0 += part[buf][0][w];
-      s1 += part[buf][1][w];
+      for (int w = 0; w < NW; ++w) {  // fixed order: every thread gets the bitwise-same sums
+        s0 += part[buf][0][0][w];
+        s1 += part[buf][1][0][w];
+      }
+      r0[0] = residual<LOSS, A>(s0, y0, coef[0]);
+      r1[0] = two ? residual<LOSS, A>(s1, y1, coef[0]) : A(0);
+    } else {
+      // one loss epilogue per lane instead of 2R wave-uniform ones: lane (row k, replica q) = k R + q
+      // sums its dot product (same fixed order) and evaluates its residual, then every lane reads
+      // the 2R results
+      const int k = lane >= R ? 1 : 0, q = lane - k * R;
+      A sl = A(0);
+      if (lane < 2 * R) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) sl += part[buf][k][q][w];
+      }
+      A cq = A(0);  // this lane's replica coefficient (coef[] stays in registers: no dynamic index)
+#pragma unroll
+      for (int qq = 0; qq < R; ++qq)
+        if (q == qq) cq = coef[qq];
+      const A rl = residual_branchfree<LOSS, A>(sl, k ? y1 : y0, cq);
+#pragma unroll
+      for (int qq = 0; qq < R; ++qq) {
+        r0[qq] = act[qq] ? readlane_a(rl, qq) : A(0);
+        r1[qq] = act[qq] && two ? readlane_a(rl, R + qq) : A(0);
+      }
     }
     buf ^= 1;  // the next pair writes the other buffer: no second barrier needed
-    const A r0 = residual<LOSS, A>(s0, Y[r], coef);
-    const A r1 = two ? residual<LOSS, A>(s1, Y[r + 1], coef) : A(0);
 #pragma unroll
     for (int j = 0; j < NV; ++j)
 #pragma unroll
-      for (int v = 0; v < VN; ++v) g[j][v] = fma(r1, a1[j][v], fma(r0, a0[j][v], g[j][v]));
+      for (int v = 0; v < VN; ++v)
+#pragma unroll
+        for (int q = 0; q < R; ++q) g[q][j][v] = fma(r1[q], a1[j][v], fma(r0[q], a0[j][v], g[q][j][v]));
   }
-  A* out = slab + static_cast<long long>(task.slab) * ld;
 #pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const int c0 = (j * BS + tid) * VN;
-    if (valid[j]) {
+  for (int q = 0; q < R; ++q) {
+    if (!act[q]) continue;
+    A* out = slab + static_cast<long long>(tasks[blockIdx.x * R + q].slab) * ld;
 #pragma unroll
-      for (int v = 0; v < VN; ++v) out[c0 + v] = g[j][v];
+    for (int j = 0; j < NV; ++j) {
+      const int c0 = (j * BS + tid) * VN;
+      if (valid[j]) {
+#pragma unroll
+        for (int v = 0; v < VN; ++v) out[c0 + v] = g[q][j][v];
+      }
     }
   }
 }
@@ -992,20 +1045,21 @@ namespace eh {
 // bf16 (NV = 4); the block size BS (256 / 512) covers ld.  (1024-thread blocks would cap a
 // wave at 128 VGPRs and spill the two-row register tiles, so wider rows take the two-pass path.)
 template <typename T, typename A, int LOSS>
-static hipError_t launch_wide(int bs, const Segment* segs, const Task* tasks, int ntasks, const A* beta,
+static hipError_t launch_wide(int bs, int R, const Segment* segs, const Task* tasks, int ntasks, const A* beta,
                               A* slab, int ld, hipStream_t st) {
   constexpr int NV = Vec16<T>::N == 8 ? 4 : 8;
-  const dim3 grid(ntasks);
-  switch (bs) {
-    case 256:
-      hipLaunchKernelGGL((grad_dense_wide<T, A, NV, 256, LOSS>), grid, dim3(256), 0, st, segs, tasks, beta, slab, ld);
-      break;
-    case 512:
-      hipLaunchKernelGGL((grad_dense_wide<T, A, NV, 512, LOSS>), grid, dim3(512), 0, st, segs, tasks, beta, slab, ld);
-      break;
-    default:
-      return hipErrorInvalidValue;
+  if (R < 1 || R > 3 || ntasks % R) return hipErrorInvalidValue;
+  const dim3 grid(ntasks / R);
+#define EH_WIDE(BS_, R_) \
+  hipLaunchKernelGGL((grad_dense_wide<T, A, NV, BS_, LOSS, R_>), grid, dim3(BS_), 0, st, segs, tasks, beta, slab, ld)
+  if (bs == 256) {
+    if (R == 1) EH_WIDE(256, 1); else if (R == 2) EH_WIDE(256, 2); else EH_WIDE(256, 3);
+  } else if (bs == 512 && R == 1) {  // (replica bundles of 512-thread rows would spill: R * 16+ accumulators)
+    EH_WIDE(512, 1);
+  } else {
+    return hipErrorInvalidValue;
   }
+#undef EH_WIDE
   return hipGetLastError();
 }
 
@@ -1036,7 +1090,8 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
       return grad_mfma_launch(LOSS, segs, tasks, ntasks, k.replicas, beta, slab, ld, st);
     return hipErrorInvalidValue;
   }
-  if (k.kind == kGradWide || cpl >= 256) return launch_wide<T, A, LOSS>(cpl, segs, tasks, ntasks, beta, slab, ld, st);
+  if (k.kind == kGradWide || cpl >= 256)
+    return launch_wide<T, A, LOSS>(cpl, k.kind == kGradWide ? k.replicas : 1, segs, tasks, ntasks, beta, slab, ld, st);
   const int R = k.replicas;
   const bool bundled = k.kind == kGradStaged || k.kind == kGradMulti;
   if (bundled && (R < 1 || ntasks % R != 0)) return hipErrorInvalidValue;

@@ -59,7 +59,8 @@ class KernelChoice:
              staged   replica bundles streamed through an LDS ring, a wave per replica (``pair``: two
                       rows per step share one reduction; ``wpr`` waves per replica)
              mfma     bf16 replica bundles on the matrix cores
-             wide     a workgroup per row (2048 < d <= 8192 fp64 / 16384 fp32)
+             wide     a workgroup per row (2048 < d <= 8192 fp64 / 16384 fp32); ``replicas`` > 1: replica
+                      bundles of 256-thread rows (one row load, every replica's dot product and gradient)
              twopass  wider rows / bf16 beyond the one-pass kernels: two passes over X
     bundle_rows  rows per bundle task (bundle kinds)
     """
@@ -76,7 +77,7 @@ class KernelChoice:
 
     @property
     def bundled(self) -> bool:
-        return self.kind in ("multi", "staged", "mfma")
+        return self.kind in ("multi", "staged", "mfma") or (self.kind == "wide" and self.replicas > 1)
 
     def native(self):
         """The C++ struct (csrc/kernels/grad_dense.h) passed to the launchers."""
@@ -97,7 +98,7 @@ class KernelChoice:
         return out
 
 
-def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS) -> int:
+def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS, cpl: int = 16) -> int:
     """Rows per one-wave bundle of grad_dense_multi, in multiples of 64, from the rows per CU.
 
     Resident one-wave bundles per CU: 8 fp64 (244 VGPRs, 2 waves per SIMD), 12 fp32 (155 VGPRs,
@@ -106,9 +107,14 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
     each bundle's beta load / fold / slab write amortises over more rows): 5 bundles per CU fp64,
     10 fp32.  Measured (tools/sweep_multi_rows.sh, profiles/round2/s2_multi): N=1 fp64 768 rows 1.330 ms vs
     512 1.36 / 640 1.37 / 1024 1.54; N=2 256 rows 0.708; N=4 128 rows 0.370 vs 96 0.45 / 160 0.40;
-    N=8 64 rows 0.206 vs 48 0.25 / 80 0.22; fp32 N=1 384 rows 0.692 (320: 0.95, a second pass)."""
+    N=8 64 rows 0.206 vs 48 0.25 / 80 0.22; fp32 N=1 384 rows 0.692 (320: 0.95, a second pass).
+    Narrower rows (cpl < 16 columns per lane) hold proportionally fewer registers, so proportionally
+    more bundles fit per CU, and each carries fewer bytes in flight: the count scales by 16 / cpl
+    (d = 256 at 1e6 rows: 256-row fp64 bundles 4.8 TB/s vs 2.3 at 768, 128-row fp32 4.1 vs 2.4;
+    profiles/round3/choices)."""
     long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
     per_cu = (10 if long_stream else 12) if fp32 else (5 if long_stream else 8)
+    per_cu *= max(1, 16 // cpl)
     return max(64, 64 * int(round(distinct_rows / (per_cu * n_cus) / 64)))
 
 
@@ -149,6 +155,8 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
         return KernelChoice("twopass")
     shared = max_rep > 1
     if cpl >= 256:
+        if shared and cpl == 256 and max_rep <= 3:
+            return KernelChoice("wide", replicas=max_rep, bundle_rows=wide_bundle_rows(distinct_rows, n_cus))
         return KernelChoice("wide", interleave=shared)
     if not shared:
         return KernelChoice("fused", rows={0: 2, 1: 4, 2: 1}[prec_code])
@@ -157,12 +165,19 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
         if ld <= 1024 and ld % 8 == 0 and max_rep <= 16:
             return KernelChoice("mfma", replicas=min(max_rep, MAX_BUNDLE), bundle_rows=mfma_bundle_rows(distinct_rows))
         return KernelChoice("fused", rows=1, interleave=True)
-    if cpl <= 16 and max_rep == 3 and (prec_code == 0 or long_stream):
-        return KernelChoice("multi", replicas=3, bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus),
-                            fold=True, lane_epi=not long_stream)
+    if cpl <= 16 and max_rep == 3 and (prec_code == 0 or long_stream or cpl < 16):
+        return KernelChoice("multi", replicas=3,
+                            bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl),
+                            fold=True, lane_epi=not long_stream or cpl < 16)
     # more replicas than a workgroup's task slots: bundles of MAX_BUNDLE (and the remainder, padded)
     return KernelChoice("staged", replicas=min(max_rep, MAX_BUNDLE), bundle_rows=staged_bundle_rows(distinct_rows, n_cus),
                         pair=prec_code == 1 or not long_stream, wpr=0 if long_stream else 1)
+
+
+def wide_bundle_rows(distinct_rows: int, n_cus: int = N_CUS) -> int:
+    """Rows per wide-row replica bundle (one 256-thread workgroup, 2 resident per CU): about 4
+    bundles per CU, multiples of 16 rows."""
+    return max(16, 16 * int(round(distinct_rows / (4 * n_cus) / 16)))
 
 
 WIDE_EPT = {2: 16, 4: 32, 8: 32}  # elements per thread per row of grad_dense_wide (by vector width)
@@ -263,6 +278,8 @@ class DenseGradPlan:
             raise ValueError(f"{c.kind} bundles need d <= {64 * MAX_CPL} columns per vector width")
         if c.kind == "multi" and (self.cpl > 16 or prec.code == 2 or self.max_rep > 3):
             raise ValueError("one-wave bundles hold at most 3 fp64/fp32 replicas of d <= 1024")
+        if c.kind == "wide" and c.replicas > 1 and (self.cpl != 256 or c.replicas > 3):
+            raise ValueError("wide-row bundles are 256-thread rows of at most 3 replicas")
         if c.kind == "mfma" and (prec.code != 2 or self.ld > 1024 or self.ld % 8 or self.max_rep > 16):
             raise ValueError("MFMA bundles are bf16, d <= 1024, d % 8 == 0, at most 16 replicas")
         self.bundle_rows = c.bundle_rows if c.bundled else 0

@@ -108,3 +108,16 @@ def test_default_staged_kernels_keep_their_occupancy(tmp_path):
         assert spill == 0 and v <= 256, f"{n}: {v} VGPRs, {spill} spilled"
     mfma = [(n, r) for n, r in regs.items() if "grad_staged_mfma" in n]
     assert mfma and all(s == 0 for _, (_, s) in mfma), mfma
+
+
+@pytest.mark.skipif(not os.path.exists(READELF), reason="llvm-readelf not installed")
+def test_wide_row_bundles_do_not_spill(tmp_path):
+    """grad_dense_wide with R replicas (one row load feeds R dot products and R gradients) keeps
+    its accumulators in registers at every width and precision."""
+    regs = {}
+    for co in _code_objects(tmp_path):
+        regs.update(_kernel_regs(co))
+    wide = {n: r for n, r in regs.items() if "grad_dense_wide" in n}
+    assert len(wide) >= 24, sorted(wide)  # 3 storage types x 2 losses x (256 threads x R in 1..3, 512 x R = 1)
+    bad = {n: r for n, r in wide.items() if r[1] > 0}
+    assert not bad, bad

@@ -388,6 +388,39 @@ def test_dense_grad_one_wave_bundles(native, rows, d, prec_name, loss, form):
         np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=tol * 1e-2 * max(1.0, np.abs(ref).max()))
 
 
+@pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
+@pytest.mark.parametrize("rows,d,prec_name", [(16, 4096, "fp64"), (33, 3000, "fp64"), (64, 8000, "fp32"),
+                                              (17, 5000, "bf16")])
+def test_dense_grad_wide_row_bundles(native, rows, d, prec_name, loss):
+    """grad_dense_wide with replica bundles: a 256-thread workgroup loads each wide row once and
+    computes every replica's dot product, residual (own coefficient) and gradient from registers.
+    Bundles of 3, of 2 padded to 3 and odd-length bundles against the fp64 oracle, and equal to the
+    one-replica wide kernel message by message (to rounding: the row split into tasks differs)."""
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(9)
+    parts, host = _parts(rng, [301, 200, 77], d, prec)
+    msgs = [[(0, 1.0), (1, 1.0)]] * 2 + [[(0, -0.5), (1, 2.0)]] + [[(2, 1.0)], [(2, -3.0)]]
+    plan = DenseGradPlan(msgs, parts, prec, loss, d, choice=KernelChoice("wide", replicas=3, bundle_rows=rows))
+    assert plan.cpl == 256 and plan.bundle_rows == rows and plan.choice.bundled
+    beta = torch.randn(plan.ld, dtype=prec.acc, device=DEV) * 0.05
+    G = plan.out_buffer()[0]
+    plan.native_launcher().launch(beta, G)
+    torch.cuda.synchronize()
+    bh = beta[:d].double().cpu().numpy()
+    f = logistic_grad if loss == LOGISTIC else least_squares_grad
+    tol = 1e-10 if prec_name == "fp64" else 2e-4
+    for s, m in enumerate(msgs):
+        ref = sum(f(host[p][0], host[p][1], bh, c) for p, c in m)
+        np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol,
+                                   atol=tol * 1e-2 * max(1.0, np.abs(ref).max()))
+    single = DenseGradPlan(msgs, parts, prec, loss, d, choice=KernelChoice("wide"))
+    G1 = single.out_buffer()[0]
+    single.run(beta, G1)
+    torch.cuda.synchronize()
+    g1 = G1.double().cpu().numpy()
+    np.testing.assert_allclose(G.double().cpu().numpy(), g1, rtol=tol, atol=tol * 1e-2 * max(1.0, np.abs(g1).max()))
+
+
 @pytest.mark.parametrize("shape", [(20000, 15509, 55), (17290, 27654, 19), (6000, 241915, 45)])
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
 @pytest.mark.parametrize("R,valued", [(100, False), (300, True), (7, True)])

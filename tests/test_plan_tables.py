@@ -82,7 +82,12 @@ def test_kernel_selection_table():
                                                                    KernelChoice("fused", rows=1)]
     # wide rows: d = 2048 fp64 (32 columns per lane) stays on staged bundles; 4096 takes the wide kernel
     assert pick(0, 2048, 3, 1_000_000).kind == "staged"
-    assert pick(0, 4096, 3, 1_000_000) == KernelChoice("wide", interleave=True)
+    assert pick(0, 4096, 3, 1_000_000) == KernelChoice("wide", replicas=3, bundle_rows=976)
+    assert pick(1, 4096, 2, 100_000) == KernelChoice("wide", replicas=2, bundle_rows=96)
+    assert pick(0, 8192, 3, 1_000_000) == KernelChoice("wide", interleave=True)  # 512-thread rows: no bundles
+    # narrow rows: more, shorter one-wave bundles with the lane epilogue
+    assert pick(0, 256, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=192, fold=True, lane_epi=True)
+    assert pick(1, 256, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=128, fold=True, lane_epi=True)
     assert pick(0, 4096, 1, 1_000_000) == KernelChoice("wide")
     assert pick(0, 10000, 3, 100_000) == KernelChoice("twopass")
     # bf16 beyond the MFMA tile: the fused kernel, replica-interleaved

@@ -162,6 +162,57 @@ def sweep_cases(out, ds=(256, 1000, 2048, 4096), ns=(100_000, 1_000_000, 4_000_0
                 torch.cuda.empty_cache()
 
 
+def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000), ("fp64", 256, 100_000),
+                                ("fp64", 4096, 1_000_000), ("fp32", 4096, 1_000_000), ("fp32", 2048, 1_000_000),
+                                ("fp64", 1000, 100_000))):
+    """Every valid KernelChoice on the replica-bundle (agc) layout of a few shapes: the candidates
+    behind choose_kernel's table (tests/test_plan_tables.py pins the picks)."""
+    import dataclasses
+
+    import torch
+
+    from erasurehead_amd.models.losses import LOGISTIC
+    from erasurehead_amd.ops import DenseGradPlan, get_precision
+    from erasurehead_amd.ops.grad import KernelChoice
+
+    msgs = [[0, 1, 2]] * 3 + [[3, 4, 5]] * 3 + [[6, 7]] * 2
+    for prec_name, d, n in shapes:
+        prec = get_precision(prec_name)
+        rpp = n // 8
+        parts = {p: (torch.empty(rpp, prec.ld(d), device="cuda", dtype=prec.storage).uniform_(-1, 1),
+                     torch.where(torch.rand(rpp, device="cuda") > 0.5, 1.0, -1.0).to(prec.acc)) for p in range(8)}
+        beta = torch.randn(prec.ld(d), device="cuda", dtype=prec.acc) * 0.01
+        distinct = 8 * parts[0][0].numel() * parts[0][0].element_size() / 1e12
+        cands = [KernelChoice("fused", rows=r, interleave=i) for r in (1, 2, 4) for i in (False, True)]
+        cands += [KernelChoice("multi", replicas=3, bundle_rows=b, fold=True, lane_epi=e)
+                  for b in (64, 128, 192, 256, 512, 768) for e in (False, True)]
+        cands += [KernelChoice("staged", replicas=3, bundle_rows=b, pair=p, wpr=w)
+                  for b in (128, 512) for p in (False, True) for w in (0, 1)]
+        cands += [KernelChoice("wide", interleave=i) for i in (False, True)]
+        cands += [KernelChoice("wide", replicas=3, bundle_rows=b) for b in (16, 64, 256, 976)]
+        default = None
+        for c in [None] + cands:
+            try:
+                plan = DenseGradPlan([[(p, 1.0) for p in m] for m in msgs], parts, prec, LOGISTIC, d, choice=c)
+            except (ValueError, RuntimeError):
+                continue
+            G = plan.out_buffer()[0]
+            try:
+                ms = _time(lambda: plan.run(beta, G), reps=20)
+            except RuntimeError:
+                continue
+            if c is None:
+                default = plan.choice
+            r = {"kernel": "grad_dense_choice", "precision": prec_name, "d": d, "n": n,
+                 "choice": dataclasses.asdict(plan.choice), "label": plan.choice.label(), "default": c is None,
+                 "ms": ms, "distinct_TBps": distinct / ms * 1e3}
+            out.append(r)
+            print(json.dumps(r), flush=True)
+            del plan, G
+        del parts
+        torch.cuda.empty_cache()
+
+
 def eval_cases(out):
     """Post-hoc evaluation GEMM (MFMA, loss fused): X [n, 1000] . B[100, 1000]^T, fp64 / fp32."""
     import torch
@@ -214,7 +265,8 @@ def sparse_cases(out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "kernels.jsonl"))
-    ap.add_argument("--only", choices=["dense", "sparse", "scale", "eval", "sweep"], default=None)
+    ap.add_argument("--shapes", default=None, help="--only choices: prec:d:n,... (default: the built-in list)")
+    ap.add_argument("--only", choices=["dense", "sparse", "scale", "eval", "sweep", "choices"], default=None)
     a = ap.parse_args()
     out = []
     if a.only in (None, "dense"):
@@ -225,6 +277,11 @@ def main():
         eval_cases(out)
     if a.only == "sweep":
         sweep_cases(out)
+    if a.only == "choices":
+        if a.shapes:
+            choice_cases(out, [(p, int(d), int(float(n))) for p, d, n in (x.split(":") for x in a.shapes.split(","))])
+        else:
+            choice_cases(out)
     if a.only in (None, "sparse"):
         sparse_cases(out)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
