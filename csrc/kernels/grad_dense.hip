@@ -963,6 +963,54 @@ slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, Put
   }
 }
 
+// Stage 2 + the master's combine and update of a device-driven local round in one launch
+// (MasterPump::run_local; update.hip combine_update's arithmetic).  One block per 64-column chunk:
+// its waves sum the chunk's splits for every slot (slab_reduce_final's order; G rows written, sums
+// kept in LDS), then wave 0 combines the decoded messages in message order and updates beta / u /
+// history / the next worker beta for those columns.  Replaces slab_reduce_final + combine_update
+// (one launch less per round), results bitwise unchanged.  (A variant that also folded stage 1 in,
+// with the last block of each chunk finishing it, paid a device-scope release fence per block --
+// an L2 writeback on every XCD -- and took 427 us: profiles/round3/fused_update.)
+template <typename A>
+__global__ void __launch_bounds__(256)
+slab_final_update(const A* __restrict__ part, A* __restrict__ G, int ld, int nslots, const LocalUpdate up) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lu_raw[];
+  A* gs = reinterpret_cast<A*>(lu_raw);  // [nslots][64] the chunk's message sums
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = blockIdx.x * kWave + lane;
+  if (up.stamp && blockIdx.x == 0 && threadIdx.x == 0) *up.stamp = wall_clock64();
+  for (int q = wid; q < nslots; q += 4) {
+    A v = A(0);
+    if (c < ld) {
+#pragma unroll
+      for (int k = 0; k < kSplits; ++k) v += part[(static_cast<long long>(q) * kSplits + k) * ld + c];
+      G[static_cast<long long>(q) * ld + c] = v;
+    }
+    gs[q * kWave + lane] = v;
+  }
+  __syncthreads();
+  if (wid != 0 || c >= ld) return;
+  A* bw = static_cast<A*>(up.beta_w);
+  if (c >= up.d) {  // padded columns stay exactly zero
+    if (bw) bw[c] = A(0);
+    return;
+  }
+  double g = 0.0;  // combine_update: the fma chain in message order
+  for (int m = 0; m < up.nmsg; ++m) g = fma(up.coef[m], static_cast<double>(gs[up.slot[m] * kWave + lane]), g);
+  const double b = up.beta[c];
+  double nb;
+  if (up.rule == 0) {  // GD
+    nb = up.decay * b - up.gm * g;
+  } else {  // AGD
+    const double yt = (1.0 - up.theta) * b + up.theta * up.u[c];
+    nb = yt - up.gm * g - up.l2 * b;
+    up.u[c] = b + (nb - b) * (1.0 / up.theta);
+  }
+  up.beta[c] = nb;
+  if (up.hist) up.hist[c] = nb;
+  if (bw) bw[c] = static_cast<A>(nb);
+}
+
 template <typename A>
 static hipError_t slab_reduce_launch(const A* slab, const int* stb, A* part, A* G, int nslots, int ld,
                                      hipStream_t st, const PutDesc* put = nullptr) {
@@ -1189,6 +1237,45 @@ hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, con
   return slab_reduce_launch<float>((const float*)slab, slot_task_begin, (float*)part, (float*)G, nslots, ld, st, put);
 }
 
+
+hipError_t grad_dense_update_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks, int ntasks,
+                                    const void* beta, void* slab, const int* stb, int nslots, void* part, void* G,
+                                    int ld, hipStream_t st, const KernelChoice& k, const LocalUpdate& up) {
+  if (nslots < 1 || nslots > kMaxMsgs || up.nmsg < 0 || up.nmsg > kMaxMsgs || !up.beta) return hipErrorInvalidValue;
+  for (int m = 0; m < up.nmsg; ++m)
+    if (up.slot[m] < 0 || up.slot[m] >= nslots) return hipErrorInvalidValue;
+  const Segment* S = static_cast<const Segment*>(segs);
+  const Task* Tk = static_cast<const Task*>(tasks);
+  hipError_t e;
+  if (dtype == 0)
+    e = loss == kLogistic ? launch_fused_cpl<double, double, kLogistic>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, k)
+                          : launch_fused_cpl<double, double, kLeastSquares>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, k);
+  else if (dtype == 1)
+    e = loss == kLogistic ? launch_fused_cpl<float, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k)
+                          : launch_fused_cpl<float, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k);
+  else
+    e = loss == kLogistic ? launch_fused_cpl<bf16_t, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k)
+                          : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k);
+  if (e != hipSuccess) return e;
+  const dim3 pgrid(ceil_div(ld, kWave), nslots, kSplits);
+  const size_t lds = static_cast<size_t>(nslots) * kWave * (dtype == 0 ? 8 : 4);
+  auto go = [&](const void* kern) -> hipError_t {
+    if (lds <= 60 * 1024) return hipSuccess;
+    return hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  };
+  if (dtype == 0) {
+    hipLaunchKernelGGL(slab_reduce_partial<double>, pgrid, dim3(256), 0, st, (const double*)slab, stb, (double*)part, ld);
+    if ((e = go(reinterpret_cast<const void*>(slab_final_update<double>))) != hipSuccess) return e;
+    hipLaunchKernelGGL(slab_final_update<double>, dim3(ceil_div(ld, kWave)), dim3(256), lds, st, (const double*)part,
+                       (double*)G, ld, nslots, up);
+  } else {
+    hipLaunchKernelGGL(slab_reduce_partial<float>, pgrid, dim3(256), 0, st, (const float*)slab, stb, (float*)part, ld);
+    if ((e = go(reinterpret_cast<const void*>(slab_final_update<float>))) != hipSuccess) return e;
+    hipLaunchKernelGGL(slab_final_update<float>, dim3(ceil_div(ld, kWave)), dim3(256), lds, st, (const float*)part,
+                       (float*)G, ld, nslots, up);
+  }
+  return hipGetLastError();
+}
 
 hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, const void* tasks,
                                      int ntasks, const void* beta, const int* task_row_off,

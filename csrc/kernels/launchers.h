@@ -73,6 +73,26 @@ struct CombineArgs {
   double coef[kMaxMsgs];
   int nmsg;
 };
+// One device-driven local round's decode-combine + update fused into the gradient's slab reduction
+// (grad_dense_update_launch): the decoded messages are rows of this launch's G.
+struct LocalUpdate {
+  int nmsg;
+  int slot[kMaxMsgs];        // G row of every decoded message, in combine order
+  double coef[kMaxMsgs];
+  double* beta;              // [ld] fp64 master state
+  double* u;                 // [ld] AGD state
+  double* hist;              // [ld] this round's history row
+  void* beta_w;              // [ld] next round's worker beta (message dtype)
+  long long* stamp;          // device time the round's messages were all reduced (or nullptr)
+  int d, rule;
+  double decay, gm, l2, theta;
+};
+// Gradient + slab reduction + combine + GD/AGD update in three launches (grad_dense.hip
+// slab_final_update); bitwise equal to grad_dense_launch followed by combine_update_launch.
+hipError_t grad_dense_update_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks, int ntasks,
+                                    const void* beta, void* slab, const int* slot_task_begin, int nslots, void* part,
+                                    void* G, int ld, hipStream_t st, const KernelChoice& k, const LocalUpdate& up);
+
 // msg dtype / worker-beta dtype: 0 fp64, 1 fp32; rule 0 GD, 1 AGD
 hipError_t combine_update_launch(const CombineArgs& args, int msg_dtype, int w_dtype,
                                  double* beta, double* u, double* hist, void* beta_w,

@@ -146,6 +146,12 @@ struct GradLauncher {
   // Dense fused plans without device encoding can hand their result rows straight to the
   // receiver's mailbox from the final reduction kernel (grad_dense.hip slab_reduce_final_put).
   bool can_fuse_put(int rows) const { return kind == 0 && !Gb && ntasks > 0 && nslots == rows; }
+  // Device-driven local rounds: the combine + update ride the slab reduction (grad_dense_update_launch).
+  bool can_fuse_update() const { return kind == 0 && !Gb && ntasks > 0; }
+  hipError_t launch_update(const void* beta, void* G, const eh::LocalUpdate& up, hipStream_t st) const {
+    return eh::grad_dense_update_launch(dtype, loss, cpl, segs, tasks, ntasks, beta, slab, stb, nslots, part, G, ld,
+                                        st, choice, up);
+  }
   hipError_t launch_put(const void* beta, void* G, const eh::PutDesc& put, hipStream_t st) const {
     return eh::grad_dense_launch(dtype, loss, cpl, segs, tasks, ntasks, beta, slab, stb, nslots, part, G, ld, st,
                                  choice, &put);
@@ -737,6 +743,12 @@ class MasterPump {
         if (!graph) decode_round(i);
         const int slot = i % K_;
         char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
+        eh::LocalUpdate up;
+        if (fused_update_ && launcher_->can_fuse_update() && local_update(i, useds[i - a], g, st + i + 1, &up)) {
+          hcheck(launcher_->launch_update(bin + static_cast<int64_t>(i) * ld_ * es_, g, up, stream_),
+                 "local gradient + update");
+          continue;
+        }
         hcheck(launcher_->launch(bin + static_cast<int64_t>(i) * ld_ * es_, g, stream_), "local gradient");
         combine(i, useds[i - a], false, st + i + 1);
       }
@@ -896,6 +908,8 @@ class MasterPump {
     return 1e3 * khz;
   }
   int graphs_launched() const { return (int)graphs_.size(); }
+  // run_local: combine + update inside the slab reduction (default) or as their own launches (A/B, tests)
+  void set_fused_update(bool on) { fused_update_ = on; }
 
   // Update-kernel durations (ms) of every round run so far (host sync).
   std::vector<double> update_ms() {
@@ -978,6 +992,31 @@ class MasterPump {
 
   // events: time the update with HIP events (host-driven rounds); stamp: device timestamp
   // written by the update kernel at its start (device-driven rounds, graph capture).
+  // Round i's combine + update as a LocalUpdate over the G rows of this launch (run_local); false
+  // when a decoded row is not one of them.
+  bool local_update(int i, const UsedRows& used, const char* g, long long* stamp, eh::LocalUpdate* up) const {
+    if ((int)used.size() > eh::kMaxMsgs) return false;
+    const int64_t rb = static_cast<int64_t>(ld_) * es_;
+    up->nmsg = (int)used.size();
+    for (int m = 0; m < up->nmsg; ++m) {
+      const int64_t off = static_cast<const char*>(used[m].p) - g;
+      if (used[m].row >= 0 || off < 0 || off % rb || off / rb >= launcher_->nslots) return false;
+      up->slot[m] = static_cast<int>(off / rb);
+      up->coef[m] = used[m].c;
+    }
+    up->beta = beta_.data_ptr<double>();
+    up->u = u_.data_ptr<double>();
+    up->hist = hist_.data_ptr<double>() + static_cast<int64_t>(i) * ld_;
+    up->beta_w = static_cast<char*>(beta_in_.data_ptr()) + static_cast<int64_t>(i + 1) * ld_ * es_;
+    up->stamp = stamp;
+    up->d = d_;
+    up->rule = update_rule_;
+    up->decay = decay_[i];
+    up->gm = gm_[i];
+    up->l2 = l2_[i];
+    up->theta = theta_[i];
+    return true;
+  }
   void combine(int i, const UsedRows& used, bool events = true,
                long long* stamp = nullptr) {
     need((int)used.size() <= eh::kMaxMsgs, "too many messages for one combine");
@@ -1289,6 +1328,7 @@ class MasterPump {
   std::vector<hipEvent_t> loc_ev_;
   std::vector<hipGraphExec_t> graphs_;  // device-driven segments (destroyed after a sync)
   hipStream_t dev_stream_ = nullptr;     // stream of the device-driven rounds (capturable)
+  bool fused_update_ = true;              // run_local: combine + update inside the slab reduction
   hipStream_t chk_stream_ = nullptr;     // run_device: arbiter_check kernels beside the local gradient
   hipEvent_t arb_ev_ = nullptr, chk_ev_ = nullptr;
   hipEvent_t join_ev_ = nullptr;
@@ -1684,7 +1724,8 @@ void bind_engine(py::module& m) {
       .def("stamp_hz", &MasterPump::stamp_hz)
       .def("set_timing", &MasterPump::set_timing)
       .def("timing_ms", &MasterPump::timing_ms)
-      .def("graphs_launched", &MasterPump::graphs_launched);
+      .def("graphs_launched", &MasterPump::graphs_launched)
+      .def("set_fused_update", &MasterPump::set_fused_update, py::arg("on"));
   py::class_<WorkerPump>(m, "WorkerPump")
       .def(py::init<std::shared_ptr<GradLauncher>, const Tensor&, const Tensor&, int, uintptr_t, int, int, uintptr_t,
                     uintptr_t, const Tensor&, int, int, double, uintptr_t>(),

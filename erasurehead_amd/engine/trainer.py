@@ -556,6 +556,8 @@ class Trainer:
         if self.physical:  # remote messages are really late: the collector applies no virtual delay to them
             pump.set_remote_delays([float(x) for x in self._remote_delays(delay_table).ravel()])
         pump.set_repeat(self.repeat)
+        # device-driven local rounds: combine + update inside the slab reduction (off: separate launches)
+        pump.set_fused_update(bool(getattr(self, "fused_update", True)))
         pump.set_decode(sch.decode_kind, list(sch.group_of), sch.n_groups)
         pump.set_timing(bool(cfg.instrument))
         table_decoded = sch.decode_kind in (3, 4)

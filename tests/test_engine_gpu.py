@@ -84,6 +84,37 @@ def test_gpu_device_loop_timed_segments(native):
     np.testing.assert_allclose(out["graph"], out["off"], rtol=1e-12, atol=1e-14)
 
 
+@pytest.mark.parametrize("mode", ["graph", "stream"])
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+@pytest.mark.parametrize("case", [(1, 0, 3, 7, 2, 4), (1, 0, 0, 7, 2, 0), (0, 0, 0, 5, 0, 0)])
+def test_gpu_fused_update_is_bitwise_identical(case, precision, mode, native):
+    """Device-driven local rounds with the combine + update inside the slab reduction
+    (grad_dense.hip slab_reduce_update) give bitwise the betas of the separate slab_reduce_final +
+    combine_update launches, AGD and GD, fp64 and fp32 messages, d not a multiple of the 64-column
+    chunk."""
+    is_coded, P, ver, n_procs, s, k = case
+    from erasurehead_amd.codes import make_scheme, scheme_key
+
+    W = n_procs - 1
+    key = scheme_key(is_coded, P, ver)
+    d, rows = 150, 64
+    n_parts = make_scheme(key, W, s, rows * W, k, P, rng=np.random.RandomState(0)).n_partition_files
+    src = _source(n_parts, rows, d, seed=3)
+    out = {}
+    for fused in (True, False):
+        for rule in ("AGD", "GD"):
+            cfg = RunConfig(n_procs, rows * n_parts, d, "/tmp/eh_gpu_eng/", 0, "x", is_coded, s, P, ver, k, 0, rule,
+                            num_itrs=9, seed=0, verbose=False, device_loop=mode, precision=precision)
+            sch = make_scheme(key, W, s, rows * n_parts, k, P, rng=np.random.RandomState(0))
+            tr = Trainer(cfg, DistEnv(device=torch.device("cuda")), src, scheme=sch)
+            tr.fused_update = fused
+            res = tr.run()
+            assert tr.device_loop == mode
+            out[(fused, rule)] = res.betaset
+    for rule in ("AGD", "GD"):
+        assert np.array_equal(out[(True, rule)], out[(False, rule)]), rule
+
+
 def test_gpu_delay_semantics(native):
     """AGC with the reference Exp(0.5)*0.02 delays: time-to-decode tracks the deterministic floor."""
     from erasurehead_amd.utils.delay import delay_floor
