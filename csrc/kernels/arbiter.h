@@ -23,7 +23,10 @@ constexpr int kArbMaxProbes = 512;    // expected shards per round
 constexpr int kArbMaxSrc = 64;        // worker ranks (one shared counter each)
 constexpr int kArbMaxRows = 16;       // buffer rows (shards) of one message
 constexpr int kArbLogInts = 4 + 4 * kArbMaxW;   // per round: status, n_arrivals, n_used, -, then (w, p) pairs
-constexpr int kArbLogTicks = 4 + 2 * kArbMaxW;  // per round: t_begin, t_dec, t_end, -, then one tick per arrival
+// per round: t_begin, t_dec (combine done), t_end (released), t_join (poll joined), t_decoded (decode
+// done), -, -, -, then one tick per arrival
+constexpr int kArbTickArr = 8;
+constexpr int kArbLogTicks = kArbTickArr + 2 * kArbMaxW;
 
 struct ArbArgs {
   int W, n_groups, rule, k, decode, drain;

@@ -87,6 +87,12 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
   }
   __syncthreads();
 
+  // this round's update constants and the first 1024 columns of beta / u, loaded while the workers
+  // compute (off the stop-rule -> release path)
+  const double decay = a.decay[i], gm = a.gm[i], l2 = a.l2[i], theta = a.theta[i];
+  const double b_pre = tid < a.d ? a.beta[tid] : 0.0;
+  const double u_pre = tid < a.d && a.update_rule != 0 ? a.u[tid] : 0.0;
+
   // ---- 1. poll until the stop rule holds (wave 0) -------------------------------------------
   unsigned long long seen = 0;  // sources seen so far (wave-uniform)
   if (tid < 64) {
@@ -179,58 +185,80 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
     }
     return;
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the workers' message rows behind their counters
+  // (no further fence: wave 0's system-scope acquire loads of the counters invalidated this CU's
+  // caches after seeing them, and the barrier orders every wave's loads after those)
+  if (tid == 0) tl[3] = wall_clock64();
 
-  // ---- 2. decode (thread 0; MasterPump::decode) -----------------------------------------------
+  // ---- 2. decode (wave 0, one lane per arrival; MasterPump::decode's message order) ------------
+  // Arrival x contributes its message rows iff: p = 1 and a partial decode (2, 4); p = 0 and decode 0;
+  // p = 0, decode 1 / 2 and the first p = 0 arrival of its FRC group.  Then, for the table decodes
+  // (3, 4), every worker of the completion pattern in worker order with its table coefficient.  Each
+  // lane's rows land at its exclusive prefix sum (wave scan), so the combine order is the serial one.
   const int slot = i % a.K;
-  if (tid == 0) {
-    auto push = [&](int w, int p, double c) {
+  if (tid < 64) {
+    auto scan = [&](int v) {  // inclusive prefix sum over the wave
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const int u = __shfl_up(v, dd, 64);
+        if (tid >= dd) v += u;
+      }
+      return v;
+    };
+    auto put_rows = [&](int w, int p, double c, int pos) {
       const int mi = 2 * w + p;
-      for (int r = 0; r < s_nrows[mi]; ++r) {
+      for (int r = 0; r < s_nrows[mi] && pos + r < kMaxMsgs; ++r) {
         const int e = s_rows[mi * kArbMaxRows + r];
         const int row = e & 0xffffff;
-        const M* base = (e >> 24) == 0
-                            ? static_cast<const M*>(a.G) + (static_cast<long long>(slot) * a.g_rows + row) * a.ld
-                            : static_cast<const M*>(a.rbuf) + (static_cast<long long>(slot) * a.r_rows + row) * a.ld;
-        if (s_nmsg < kMaxMsgs) {
-          mptr[s_nmsg] = base;
-          mcoef[s_nmsg] = c;
-          mrow[s_nmsg] = e;
-        }
-        ++s_nmsg;
+        mptr[pos + r] = (e >> 24) == 0
+                            ? static_cast<const void*>(static_cast<const M*>(a.G) + (static_cast<long long>(slot) * a.g_rows + row) * a.ld)
+                            : static_cast<const void*>(static_cast<const M*>(a.rbuf) + (static_cast<long long>(slot) * a.r_rows + row) * a.ld);
+        mcoef[pos + r] = c;
+        mrow[pos + r] = e;
       }
     };
-    unsigned long long gd = 0;
-    for (int x = 0; x < s_narr; ++x) {
-      const int w = arr_w[x], p = arr_p[x];
-      if (p == 1) {
-        if (a.decode == 2 || a.decode == 4) push(w, 1, 1.0);
-        continue;
+    const bool frc = a.decode == 1 || a.decode == 2;
+    if (frc) {  // first p = 0 arrival of every group
+      for (int g = tid; g < kArbMaxW; g += 64) batch[g] = 1 << 30;  // (batch is free after the poll)
+      __builtin_amdgcn_wave_barrier();
+      for (int x = tid; x < s_narr; x += 64)
+        if (arr_p[x] == 0) atomicMin(&batch[s_group[arr_w[x]]], x);
+      __builtin_amdgcn_wave_barrier();
+    }
+    int base = 0;
+    for (int x0 = 0; x0 < s_narr; x0 += 64) {  // arrival order
+      const int x = x0 + tid;
+      int nr = 0;
+      if (x < s_narr) {
+        const int w = arr_w[x], p = arr_p[x];
+        const bool use = p == 1 ? (a.decode == 2 || a.decode == 4)
+                                : (a.decode == 0 || (frc && batch[s_group[w]] == x));
+        if (use) nr = s_nrows[2 * w + p];
       }
-      if (a.decode == 0) {
-        push(w, 0, 1.0);
-      } else if (a.decode == 1 || a.decode == 2) {
-        const int g = s_group[w];
-        if (!(gd >> g & 1)) {
-          gd |= 1ull << g;
-          push(w, 0, 1.0);
+      const int incl = scan(nr);
+      if (nr) put_rows(arr_w[x], arr_p[x], 1.0, base + incl - nr);
+      base += __shfl(incl, 63, 64);
+    }
+    if (a.decode == 3 || a.decode == 4) {  // the table's coefficients, worker order
+      if (!a.table) {
+        if (tid == 0) s_status = 2;
+      } else {
+        const unsigned long long mask = s_mask;
+        for (int w0 = 0; w0 < a.W; w0 += 64) {
+          const int w = w0 + tid;
+          const bool on = w < a.W && (mask >> w & 1);
+          const double c = on ? s_trow[w] : 0.0;
+          if (__ballot(on && c != c) && tid == 0) s_status = 2;  // NaN: completion pattern without a table row
+          const int nr = on ? s_nrows[2 * w] : 0;
+          const int incl = scan(nr);
+          if (nr) put_rows(w, 0, c, base + incl - nr);
+          base += __shfl(incl, 63, 64);
         }
       }
     }
-    if (a.decode == 3 || a.decode == 4) {
-      const unsigned long long mask = s_mask;
-      for (int w = 0; w < a.W && a.table; ++w) {
-        if (!(mask >> w & 1)) continue;
-        const double c = s_trow[w];
-        if (c != c) {  // NaN: completion pattern without a table row
-          s_status = 2;
-          break;
-        }
-        push(w, 0, c);
-      }
-      if (!a.table) s_status = 2;
+    if (tid == 0) {
+      s_nmsg = min(base, kMaxMsgs + 1);
+      if (base > kMaxMsgs) s_status = 2;
     }
-    if (s_nmsg > kMaxMsgs) s_status = 2;
   }
   __syncthreads();
   if (s_status != 0) {
@@ -242,10 +270,11 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
     return;
   }
 
+  if (tid == 0) tl[4] = wall_clock64();
+
   // ---- 3. combine + update, beta(i+1) into beta_in and every worker inbox -------------------
   // With tags on, the loop also sums the checksum terms of beta(i+1) for its inbox tags (the
   // column loop has a block-uniform trip count for the block reduction after it).
-  const double decay = a.decay[i], gm = a.gm[i], l2 = a.l2[i], theta = a.theta[i];
   const bool vfy = a.tags != nullptr;
   M* bin_next = static_cast<M*>(a.beta_in) + static_cast<long long>(i + 1) * a.ld;
   unsigned long long bterm = 0;
@@ -264,12 +293,12 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
         if (m0 + q < s_nmsg) g = fma(mcoef[m0 + q], static_cast<double>(v[q]), g);
     }
     if (in && c < a.d) {
-      const double b = a.beta[c];
+      const double b = c0 == 0 ? b_pre : a.beta[c];
       double nb;
       if (a.update_rule == 0) {
         nb = decay * b - gm * g;
       } else {
-        const double yt = (1.0 - theta) * b + theta * a.u[c];
+        const double yt = (1.0 - theta) * b + theta * (c0 == 0 ? u_pre : a.u[c]);
         nb = yt - gm * g - l2 * b;
         a.u[c] = b + (nb - b) * (1.0 / theta);
       }
@@ -339,7 +368,7 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
     for (int x = 0; x < s_narr; ++x) {
       lg[4 + 2 * x] = arr_w[x];
       lg[5 + 2 * x] = arr_p[x];
-      tl[4 + x] = arr_t[x];
+      tl[kArbTickArr + x] = arr_t[x];
     }
   }
   if (vfy) {  // this round's decoded rows for the next arbiter's idle waves (or the segment's tail check):

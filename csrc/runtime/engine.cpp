@@ -888,15 +888,17 @@ class MasterPump {
       py::list arr;
       const int n = std::min(l[1], 2 * eh::kArbMaxW);
       for (int x = 0; x < n && l[0] == 0; ++x)
-        arr.append(py::make_tuple(l[4 + 2 * x], l[5 + 2 * x], (t[4 + x] - t[0]) / hz));
+        arr.append(py::make_tuple(l[4 + 2 * x], l[5 + 2 * x], (t[eh::kArbTickArr + x] - t[0]) / hz));
       std::string why;
       const auto* e = static_cast<const eh::IntegrityErr*>(err_->host);
       if (l[0] == eh::kArbIntegrity || (l[0] == 3 && __atomic_load_n(&e->flag, __ATOMIC_ACQUIRE)))
         why = integrity_message(*e, false);
       // per-round ticks: poll (release of beta(i) -> stop rule), update (stop rule -> combine and
       // checks done), release (-> beta(i+1) released, drain included); seconds
-      const double t_stop = l[0] == 0 && n > 0 ? (t[4 + n - 1] - t[0]) / hz : -1.0;
-      out.append(py::make_tuple(l[0], arr, (t[1] - t[0]) / hz, (t[2] - t[0]) / hz, why, t_stop));
+      const double t_stop = l[0] == 0 && n > 0 ? (t[eh::kArbTickArr + n - 1] - t[0]) / hz : -1.0;
+      // inside the update: poll joined (all waves past the barrier + acquire), decode done
+      const py::tuple sub = py::make_tuple((t[3] - t[0]) / hz, (t[4] - t[0]) / hz);
+      out.append(py::make_tuple(l[0], arr, (t[1] - t[0]) / hz, (t[2] - t[0]) / hz, why, t_stop, sub));
     }
     return out;
   }

@@ -587,7 +587,8 @@ class Trainer:
                 pump.run_device(a, b, deadline)
             if timed_start is not None:
                 t_timed1 = self._timed_fence()
-            for i, (status, arr, tdec, tend, detail, tstop) in zip(range(start, R), pump.device_log(start, R)):
+            for i, (status, arr, tdec, tend, detail, tstop, (tjoin, tdecoded)) in zip(range(start, R),
+                                                                                     pump.device_log(start, R)):
                 if status:
                     why = detail or {1: f"a worker rank's message did not arrive within {deadline:.0f} s",
                                  2: "the arrivals could not be decoded on the device",
@@ -596,6 +597,9 @@ class Trainer:
                 if tstop >= 0:  # arbiter ticks: poll until the stop rule, combine + checks, drain + release
                     self.timer.add("arbiter_poll", tstop)
                     self.timer.add("arbiter_update", tdec - tstop)
+                    self.timer.add("arbiter_join", tjoin - tstop)  # the update's parts: barrier + acquire,
+                    self.timer.add("arbiter_decode", tdecoded - tjoin)  # decode (thread 0),
+                    self.timer.add("arbiter_combine", tdec - tdecoded)  # combine + update + beta puts
                     self.timer.add("arbiter_release", tend - tdec)
                 arrivals = [Arrival(w, p, t) for (w, p, t) in arr]
                 timeset[i], loop_time[i] = tdec, tend
