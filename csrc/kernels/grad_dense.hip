@@ -183,11 +183,16 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
 // replica slot q is the same message in all four; pad bundles fill a workgroup at a partition's
 // end).  The four waves fold their accumulators through LDS in a fixed order and wave 0 writes
 // one slab row per replica for the workgroup: a quarter of the slab rows for the reduction to read.
-// LANE_EPI: the reduce-scatter + one-lane-per-replica epilogue below; otherwise every replica's
+// EPI 1: the reduce-scatter + one-lane-per-replica epilogue below; EPI 0: every replica's
 // dot product is all-reduced and its residual evaluated wave-uniformly (an inactive replica then
 // skips its share).  Measured: the lane form wins on the sharded multi-GPU rank shapes, the wave
 // form on the one-GPU headline (ops/grad.py picks per plan; docs/PERF_NOTES.md round 3).
-template <typename T, typename A, int CPL, int LOSS, int R, bool FOLD, bool LANE_EPI = false>
+// EPI 2 (pair rows, cpl <= 8): two rows per reduction -- the 2R dot products of a row pair are
+// reduce-scattered in one 8-value exchange (wave_reduce_scatter8), lane 8v evaluates value v's
+// residual, and both rows' gradients accumulate from four row buffers (the next pair in flight).
+// Narrow rows spend most of their time in the per-row cross-lane reductions (d = 256:
+// profiles/round3/choices), which this halves.
+template <typename T, typename A, int CPL, int LOSS, int R, bool FOLD, int EPI = 0>
 __global__ void __launch_bounds__(256)
 grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ tasks, int nbundles,
                  const A* __restrict__ beta, A* __restrict__ slab, int ld) {
@@ -243,7 +248,7 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
 #pragma unroll
         for (int q = 0; q < R; ++q) z[q] = fma(Vec16<T>::template elem<A>(x[j], v), b[j][v], z[q]);
     A rr[R];
-    if constexpr (R == 1 || !LANE_EPI) {
+    if constexpr (R == 1 || EPI == 0) {
 #pragma unroll
       for (int q = 0; q < R; ++q) rr[q] = act[q] ? residual<LOSS, A>(wave_allreduce_sum(z[q]), y, coef[q]) : A(0);
     } else {
@@ -273,15 +278,73 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
 #pragma unroll
         for (int q = 0; q < R; ++q) g[q][j][v] = fma(rr[q], Vec16<T>::template elem<A>(x[j], v), g[q][j][v]);
   };
-  Rw xa[NV], xb[NV];
+  // two rows at once (EPI 2): 2R dot products, one reduce-scatter, one residual per lane
+  auto step2 = [&](const Rw (&x0)[NV], const Rw (&x1)[NV], int r, bool two) {
+    static_assert(2 * R <= 8, "pair rows hold at most 4 replicas");
+    const A y0 = Y[r], y1 = two ? Y[r + 1] : A(0);
+    A v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      v[q] = A(0);
+      if (q < 2 * R) asm volatile("" : "+v"(v[q]));  // opaque start: separate dot products
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int e = 0; e < VN; ++e)
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+          v[q] = fma(Vec16<T>::template elem<A>(x0[j], e), b[j][e], v[q]);
+          v[R + q] = fma(Vec16<T>::template elem<A>(x1[j], e), b[j][e], v[R + q]);
+        }
+    const A tot = wave_reduce_scatter8(v, lane);  // lanes 8m..8m+7: value m = k R + q
+    const int m = lane >> 3, k = m >= R ? 1 : 0, qm = m - k * R;
+    A cq = A(0);
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+      if (qm == q) cq = coef[q];
+    const A rl = m < 2 * R ? residual_branchfree<LOSS, A>(tot, k ? y1 : y0, cq) : A(0);
+    A r0v[R], r1v[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      r0v[q] = act[q] ? readlane_a(rl, 8 * q) : A(0);
+      r1v[q] = act[q] && two ? readlane_a(rl, 8 * (R + q)) : A(0);
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int e = 0; e < VN; ++e)
+#pragma unroll
+        for (int q = 0; q < R; ++q)
+          g[q][j][e] = fma(r1v[q], Vec16<T>::template elem<A>(x1[j], e),
+                           fma(r0v[q], Vec16<T>::template elem<A>(x0[j], e), g[q][j][e]));
+  };
   const int r0 = lead.row_begin, r1 = live ? lead.row_end : r0;
-  if (r0 < r1) load(xa, r0);
-  for (int r = r0; r < r1; r += 2) {  // two rows per trip: the buffers swap roles without copies
-    if (r + 1 < r1) load(xb, r + 1);
-    step(xa, r);
-    if (r + 1 >= r1) break;
-    if (r + 2 < r1) load(xa, r + 2);
-    step(xb, r + 1);
+  if constexpr (EPI == 2) {
+    Rw xa[NV], xb[NV], xc[NV], xd[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) xa[j] = xb[j] = xc[j] = xd[j] = Rw{};  // a missing pair row reads zeros
+    if (r0 < r1) load(xa, r0);
+    if (r0 + 1 < r1) load(xb, r0 + 1);
+    for (int r = r0; r < r1; r += 4) {  // four rows per trip: the buffer pairs swap roles
+      if (r + 2 < r1) load(xc, r + 2);
+      if (r + 3 < r1) load(xd, r + 3);
+      step2(xa, xb, r, r + 1 < r1);
+      if (r + 2 >= r1) break;
+      if (r + 4 < r1) load(xa, r + 4);
+      if (r + 5 < r1) load(xb, r + 5);
+      step2(xc, xd, r + 2, r + 3 < r1);
+    }
+  } else {
+    Rw xa[NV], xb[NV];
+    if (r0 < r1) load(xa, r0);
+    for (int r = r0; r < r1; r += 2) {  // two rows per trip: the buffers swap roles without copies
+      if (r + 1 < r1) load(xb, r + 1);
+      step(xa, r);
+      if (r + 1 >= r1) break;
+      if (r + 2 < r1) load(xa, r + 2);
+      step(xb, r + 1);
+    }
   }
   if constexpr (FOLD) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fold_raw[];
@@ -1113,14 +1176,20 @@ static hipError_t launch_wide(int bs, int R, const Segment* segs, const Task* ta
 
 // grad_dense_multi launch; the folded form takes 3 waves' accumulators in dynamic LDS.
 template <typename T, typename A, int C, int LOSS, int R>
-static hipError_t launch_multi(bool fold, bool lane_epi, dim3 grid, dim3 block, hipStream_t st, const Segment* segs,
-                               const Task* tasks, int nb, const A* beta, A* slab, int ld) {
-  if (!fold) {  // (the lane epilogue comes with the fold only)
-    hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, R, false, false>), grid, block, 0, st, segs, tasks, nb, beta, slab, ld);
+static hipError_t launch_multi(bool fold, bool lane_epi, bool pair, dim3 grid, dim3 block, hipStream_t st,
+                               const Segment* segs, const Task* tasks, int nb, const A* beta, A* slab, int ld) {
+  if (!fold) {  // (the lane / pair-row epilogues come with the fold only)
+    hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, R, false, 0>), grid, block, 0, st, segs, tasks, nb, beta, slab, ld);
     return hipGetLastError();
   }
   const size_t lds = 3ull * R * C * kWave * sizeof(A);
-  auto kern = lane_epi ? grad_dense_multi<T, A, C, LOSS, R, true, true> : grad_dense_multi<T, A, C, LOSS, R, true, false>;
+  auto kern = grad_dense_multi<T, A, C, LOSS, R, true, 0>;
+  if (pair) {  // four row buffers: narrow rows only
+    if constexpr (C <= 8) kern = grad_dense_multi<T, A, C, LOSS, R, true, 2>;
+    else return hipErrorInvalidValue;
+  } else if (lane_epi) {
+    kern = grad_dense_multi<T, A, C, LOSS, R, true, 1>;
+  }
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
@@ -1170,10 +1239,10 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
           const int nb_ = ntasks / R;                                                                  \
           if (k.fold && nb_ % 4) return hipErrorInvalidValue;                                          \
           const dim3 mg((nb_ + 3) / 4), mb(256);                                                       \
-          const bool f = k.fold != 0, le = k.lane_epi != 0;                                            \
-          if (R == 1) return launch_multi<T, A, C, LOSS, 1>(f, le, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
-          if (R == 2) return launch_multi<T, A, C, LOSS, 2>(f, le, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
-          if (R == 3) return launch_multi<T, A, C, LOSS, 3>(f, le, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
+          const bool f = k.fold != 0, le = k.lane_epi != 0, pr = k.pair != 0;                          \
+          if (R == 1) return launch_multi<T, A, C, LOSS, 1>(f, le, pr, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
+          if (R == 2) return launch_multi<T, A, C, LOSS, 2>(f, le, pr, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
+          if (R == 3) return launch_multi<T, A, C, LOSS, 3>(f, le, pr, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
         }                                                                                              \
         return hipErrorInvalidValue;                                                                   \
       }                                                                                                \

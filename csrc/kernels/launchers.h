@@ -141,6 +141,19 @@ hipError_t verify_rows_launch(const void* rows, const MsgTag* tags, int nrows, i
 // one wave per row; the first mismatch goes to err (host-mapped).
 hipError_t check_list_launch(const CheckList& cl, IntegrityErr* err, hipStream_t st);
 // Spin on the device for `ticks` wall_clock64 ticks (a physically late worker, --delay-mode worker).
+// Transport preflight ping-pong (transport.hip ping_pong), one block per side.
+struct PingArgs {
+  unsigned long long* out_row;       // the row this side writes (the peer's memory)
+  const unsigned long long* in_row;  // the row this side reads (its own memory)
+  int nwords_out, nwords_in;         // 64-bit words per row (0: counters only)
+  unsigned long long* out_flag;      // counter this side release-stores
+  const unsigned long long* in_flag; // counter this side polls
+  int iters;
+  long long deadline_ticks;          // per wait (wall_clock64 ticks)
+  long long* rtt;                    // [iters] master: ticks from its store to the echo (nullptr: worker)
+  int* status;                       // [2]: payload words that differed, 1 on a timeout
+};
+hipError_t ping_pong_launch(const PingArgs& a, bool master, hipStream_t st);
 hipError_t spin_launch(long long ticks, hipStream_t st);
 
 }  // namespace eh

@@ -151,6 +151,71 @@ __global__ void spin_ticks(long long ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
+// Device ping-pong of the transport preflight (parallel/transport.py IpcTransport.preflight), one
+// worker rank at a time: the master block writes pattern k into the worker's spare inbox row and
+// release-stores the worker's counter; the worker block, spinning on that counter, checks the row,
+// echoes it into the master's mailbox row and release-stores its own counter; the master times
+// counter store -> echo seen (wall_clock64) and checks the echo.  Every wait has a deadline, so a
+// missing peer ends both kernels (status[1] = 1) instead of hanging the GPU.
+__device__ __forceinline__ unsigned long long ping_word(int k, int j) {
+  return (static_cast<unsigned long long>(k) << 32) | static_cast<unsigned int>(j * 2654435761u);
+}
+__global__ void __launch_bounds__(256) ping_pong(const PingArgs a, int master) {
+  __shared__ int s_ok;
+  const int tid = threadIdx.x;
+  int errs = 0;
+  for (int k = 1; k <= a.iters; ++k) {
+    if (master) {
+      for (int j = tid; j < a.nwords_out; j += blockDim.x) a.out_row[j] = ping_word(k, j);
+      __threadfence_system();
+      __syncthreads();
+      if (tid == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // see put_signal: the counter stays behind the row
+        __hip_atomic_store(a.out_flag, static_cast<unsigned long long>(k), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    if (tid == 0) {
+      const long long t0 = wall_clock64();
+      int ok = 1;
+      while (__hip_atomic_load(const_cast<unsigned long long*>(a.in_flag), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) <
+             static_cast<unsigned long long>(k)) {
+        if (wall_clock64() - t0 > a.deadline_ticks) {
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (master && a.rtt) a.rtt[k - 1] = wall_clock64() - t0;
+      s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) {  // block-uniform
+      if (tid == 0) __hip_atomic_store(a.status + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    for (int j = tid; j < a.nwords_in; j += blockDim.x) errs += a.in_row[j] != ping_word(k, j);
+    if (!master) {
+      for (int j = tid; j < a.nwords_out; j += blockDim.x) a.out_row[j] = a.in_row[j];
+      __threadfence_system();
+      __syncthreads();
+      if (tid == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.out_flag, static_cast<unsigned long long>(k), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    __syncthreads();  // this round's reads done before the next round's writes
+  }
+  if (errs) atomicAdd(a.status, errs);
+}
+
+hipError_t ping_pong_launch(const PingArgs& a, bool master, hipStream_t st) {
+  if (a.iters < 1 || !a.out_flag || !a.in_flag || !a.status || a.nwords_in < 0 || a.nwords_out < 0 ||
+      (a.nwords_in && !a.in_row) || (a.nwords_out && !a.out_row))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ping_pong, dim3(1), dim3(256), 0, st, a, master ? 1 : 0);
+  return hipGetLastError();
+}
+
 hipError_t put_signal_launch(const PutArgs& args, int blocks, hipStream_t st) {
   if (args.n <= 0) return hipSuccess;
   for (int k = 0; k < args.n; ++k) {

@@ -358,6 +358,43 @@ void bind_ipc(py::module& m) {
       .def("unlink", &ShmFlags::unlink)
       .def_property_readonly("size", &ShmFlags::size);
   m.def("put_signal", &put_signal, py::arg("puts"), py::arg("counters"), py::arg("blocks") = 0);
+  // Preflight ping-pong (transport.hip ping_pong): blocks until this side's kernel ends.
+  m.def(
+      "ping_pong",
+      [](uintptr_t out_row, uintptr_t in_row, int64_t nwords_out, int64_t nwords_in, uintptr_t out_flag,
+         uintptr_t in_flag, int64_t iters, double deadline_s, bool master, int64_t device) {
+        hcheck(hipSetDevice(static_cast<int>(device)), "hipSetDevice");
+        const auto dev = at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device));
+        Tensor rtt = at::zeros({std::max<int64_t>(1, iters)}, at::TensorOptions().dtype(at::kLong).device(dev));
+        Tensor status = at::zeros({2}, at::TensorOptions().dtype(at::kInt).device(dev));
+        int khz = 0;
+        hcheck(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, static_cast<int>(device)), "wall clock rate");
+        eh::PingArgs a{};
+        a.out_row = reinterpret_cast<unsigned long long*>(out_row);
+        a.in_row = reinterpret_cast<const unsigned long long*>(in_row);
+        a.nwords_out = static_cast<int>(nwords_out);
+        a.nwords_in = static_cast<int>(nwords_in);
+        a.out_flag = reinterpret_cast<unsigned long long*>(out_flag);
+        a.in_flag = reinterpret_cast<const unsigned long long*>(in_flag);
+        a.iters = static_cast<int>(iters);
+        a.deadline_ticks = static_cast<long long>(deadline_s * 1e3 * khz);
+        a.rtt = master ? reinterpret_cast<long long*>(rtt.data_ptr<int64_t>()) : nullptr;
+        a.status = status.data_ptr<int>();
+        const hipStream_t st = c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(device)).stream();
+        {
+          py::gil_scoped_release nogil;
+          hcheck(eh::ping_pong_launch(a, master, st), "ping_pong");
+          hcheck(hipStreamSynchronize(st), "ping_pong sync");
+        }
+        const Tensor st_h = status.cpu();
+        py::dict out;
+        out["payload_errors"] = st_h[0].item<int>();
+        out["timeout"] = st_h[1].item<int>() != 0;
+        if (master) out["rtt_us"] = (rtt.to(at::kDouble) * (1e3 / khz)).cpu();
+        return out;
+      },
+      py::arg("out_row"), py::arg("in_row"), py::arg("nwords_out"), py::arg("nwords_in"), py::arg("out_flag"),
+      py::arg("in_flag"), py::arg("iters"), py::arg("deadline_s"), py::arg("master"), py::arg("device"));
   m.def("signal", &signal, py::arg("flag"), py::arg("value"), py::arg("device"));
   m.def("put_signal_tagged", &put_signal_tagged, py::arg("src"), py::arg("dst"), py::arg("tags"), py::arg("flag"),
         py::arg("value"), py::arg("rank"), py::arg("counters"), py::arg("csum"), py::arg("corrupt") = false);

@@ -55,7 +55,8 @@ class KernelChoice:
              multi    one-wave replica bundles: each row loaded once into registers, every one of the
                       ``replicas`` co-located messages computed from it (``fold``: 4 bundles of one
                       partition per workgroup folded through LDS; ``lane_epi``: reduce-scatter
-                      epilogue with one lane per replica)
+                      epilogue with one lane per replica; ``pair``: two rows per reduce-scatter,
+                      narrow rows)
              staged   replica bundles streamed through an LDS ring, a wave per replica (``pair``: two
                       rows per step share one reduction; ``wpr`` waves per replica)
              mfma     bf16 replica bundles on the matrix cores
@@ -118,6 +119,15 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
     return max(64, 64 * int(round(distinct_rows / (per_cu * n_cus) / 64)))
 
 
+def pair_bundle_rows(distinct_rows: int, n_cus: int = N_CUS) -> int:
+    """Rows per narrow-row (cpl <= 8) one-wave bundle with the pair-row epilogue: about 16 bundles
+    (4 folded workgroups) per CU, the power of two nearest to that, 32..512 rows.  Measured
+    (profiles/round3/choices/choices_pair_rows.jsonl): d = 256 fp64 1e6 rows 256-row bundles 5.2
+    TB/s (128: 5.1, 512: 4.7), 1e5 rows 32-row 4.4; d = 512 fp64 / fp32 1e6 rows 256-row 5.8 / 5.6."""
+    per = max(1.0, distinct_rows / (16 * n_cus))
+    return int(min(512, max(32, 2 ** round(np.log2(per)))))
+
+
 def mfma_bundle_rows(distinct_rows: int) -> int:
     """Rows per bf16 MFMA bundle: one 8-wave workgroup per CU (150 KB of LDS); long bundles amortise
     its prologue (profiles/r2_mfma_ab2: 512 / 1024 / 2048 rows -> 0.458 / 0.440 / 0.430 ms at the bf16
@@ -142,6 +152,8 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     partition (1 = distinct rows only).  distinct_rows: rows of the distinct partitions per round.
     Measured choices (docs/PERF_NOTES.md):
       * distinct rows: the fused kernel, fp64 the interleaved pair kernel, fp32 4 rows, bf16 1 row;
+      * replicas, 3 per bundle, narrow rows (<= 8 columns per lane, d <= 512 fp64 / 1024 fp32):
+        one-wave bundles with two rows per reduce-scatter (d = 256: 5.2 vs 2.3 TB/s before);
       * replicas, fp64, 3 per bundle (AGC / cyclic s = 2): one-wave bundles, folded; the lane
         epilogue below the long-stream regime (sharded ranks: 0.188 vs 0.195 ms at N = 8), the
         wave-uniform one in it (the one-GPU headline: 1.316 vs 1.40 ms);
@@ -165,10 +177,13 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
         if ld <= 1024 and ld % 8 == 0 and max_rep <= 16:
             return KernelChoice("mfma", replicas=min(max_rep, MAX_BUNDLE), bundle_rows=mfma_bundle_rows(distinct_rows))
         return KernelChoice("fused", rows=1, interleave=True)
-    if cpl <= 16 and max_rep == 3 and (prec_code == 0 or long_stream or cpl < 16):
+    if cpl <= 8 and max_rep == 3:  # narrow rows: two rows per reduce-scatter
+        return KernelChoice("multi", replicas=3, bundle_rows=pair_bundle_rows(distinct_rows, n_cus), fold=True,
+                            pair=True)
+    if cpl <= 16 and max_rep == 3 and (prec_code == 0 or long_stream):
         return KernelChoice("multi", replicas=3,
                             bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl),
-                            fold=True, lane_epi=not long_stream or cpl < 16)
+                            fold=True, lane_epi=not long_stream)
     # more replicas than a workgroup's task slots: bundles of MAX_BUNDLE (and the remainder, padded)
     return KernelChoice("staged", replicas=min(max_rep, MAX_BUNDLE), bundle_rows=staged_bundle_rows(distinct_rows, n_cus),
                         pair=prec_code == 1 or not long_stream, wpr=0 if long_stream else 1)
@@ -278,6 +293,8 @@ class DenseGradPlan:
             raise ValueError(f"{c.kind} bundles need d <= {64 * MAX_CPL} columns per vector width")
         if c.kind == "multi" and (self.cpl > 16 or prec.code == 2 or self.max_rep > 3):
             raise ValueError("one-wave bundles hold at most 3 fp64/fp32 replicas of d <= 1024")
+        if c.kind == "multi" and c.pair and (self.cpl > 8 or not c.fold):
+            raise ValueError("pair-row one-wave bundles need <= 8 columns per lane and the fold")
         if c.kind == "wide" and c.replicas > 1 and (self.cpl != 256 or c.replicas > 3):
             raise ValueError("wide-row bundles are 256-thread rows of at most 3 replicas")
         if c.kind == "mfma" and (prec.code != 2 or self.ld > 1024 or self.ld % 8 or self.max_rep > 16):

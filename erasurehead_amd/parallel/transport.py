@@ -536,49 +536,39 @@ class IpcTransport(Transport):
 
     # ---- per-pair preflight (bench.py --gpus N > 1: the first real multi-GPU run checks itself) --
     def preflight(self, iters: int = 1000, timeout: float = 30.0) -> Optional[List[dict]]:
-        """Collective.  ``iters`` put -> flag round trips between the master and every worker rank
-        over the real put+signal path: the master pushes pattern k into each worker's spare inbox
-        row (counter k), each worker checks the payload it sees once the counter reads k and
-        echoes it into the master's mailbox (its counter k), and the master checks the echo.
-        Returns (on every rank) one record per worker rank: round-trip percentiles, payload
-        errors in each direction and the peer-access facts of the pair.  Flags are reset to 0."""
+        """Collective.  ``iters`` put -> flag round trips between the master and each worker rank in
+        turn, on the device over the real put+signal path (csrc/kernels/transport.hip ping_pong): the
+        master block writes pattern k into the worker's spare inbox row and release-stores its counter;
+        the worker block checks the row, echoes it into the master's mailbox row and release-stores
+        its own counter; the master times counter store -> echo seen and checks the echo.  Returns
+        (on every rank) one record per worker rank: round-trip percentiles (device clock), payload
+        words that differed in each direction, and the peer-access facts of the pair.  Counters are
+        reset to 0 before and after each pair; every wait has a deadline (``timeout``)."""
         env, C, w, R = self.env, self.C, self.env.world, self.R
-        pat = torch.arange(self.ld, dtype=self.dtype, device=env.device)
-        mine: Dict[str, object] = {}
-        if env.is_master:
-            rbuf = self.make_rbuf()
-            rtt = {r: [] for r in range(1, w)}
-            bad_echo = {r: 0 for r in range(1, w)}
-            for k in range(1, iters + 1):
-                cur = pat + k
-                puts = [(cur, self.inbox_remote[r][R], self.flags.dev_addr(r), k) for r in range(1, w)]
-                t0 = time.perf_counter()
-                for j in range(0, len(puts), 16):
-                    self.C.put_signal(puts[j:j + 16], self.counters[16 * (j // 16):])
-                for r in range(1, w):
-                    if not self.flags.wait_ge(w + r, k, timeout):
-                        raise TransportError(f"preflight: rank {r} -> rank 0: no echo of put {k} within {timeout:.0f}s")
-                    rtt[r].append(time.perf_counter() - t0)
-                for r in range(1, w):
-                    if self.remote_counts.get(r, 0) and not bool(torch.equal(rbuf[0, self.row0[r]], cur)):
-                        bad_echo[r] += 1
-            mine = {"rtt": rtt, "bad_echo": bad_echo}
-        else:
-            r = env.rank
-            bad = 0
-            for k in range(1, iters + 1):
-                if not self.flags.wait_ge(r, k, timeout):
-                    raise TransportError(f"preflight: rank 0 -> rank {r}: put {k} never signalled within {timeout:.0f}s")
-                got = self.inbox[R]
-                if not bool(torch.equal(got, pat + k)):
-                    bad += 1
-                if self.n_local:
-                    dst = self.rremote.view(self.dname, [self.ld], self.my_row0 * self.ld * self.es)
-                    self.C.put_signal([(got, dst, self.flags.dev_addr(w + r), k)], self.counters)
-                else:
-                    self.C.signal(self.flags.dev_addr(w + r), k, self.dev)
-            torch.cuda.synchronize(env.device)
-            mine = {"bad": bad}
+        words = self.ld * self.es // 8
+        dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
+        results: Dict[int, dict] = {}
+        rbuf = self.make_rbuf() if env.is_master else None
+        for r in range(1, w):
+            if env.is_master:
+                self.flags.store(r, 0)
+                self.flags.store(w + r, 0)
+            env.barrier()
+            if env.is_master:
+                echo = self.remote_counts.get(r, 0) > 0
+                res = C.ping_pong(self.inbox_remote[r][R].data_ptr(), rbuf[0, self.row0[r]].data_ptr() if echo else 0,
+                                  words, words if echo else 0, self.flags.dev_addr(r), self.flags.dev_addr(w + r),
+                                  iters, float(timeout), True, dev)
+                results[r] = res
+            elif env.rank == r:
+                out = (self.rremote.view(self.dname, [self.ld], self.my_row0 * self.ld * self.es).data_ptr()
+                       if self.n_local else 0)
+                res = C.ping_pong(out, self.inbox[R].data_ptr(), words if self.n_local else 0, words,
+                                  self.flags.dev_addr(w + r), self.flags.dev_addr(r), iters, float(timeout), False, dev)
+                results[r] = res
+            env.barrier()
+        mine = {r: {"errors": int(v["payload_errors"]), "timeout": bool(v["timeout"]),
+                    "rtt": (v["rtt_us"].numpy().tolist() if "rtt_us" in v else None)} for r, v in results.items()}
         got = env.gather_objects(mine)
         env.barrier()
         out = None
@@ -586,20 +576,25 @@ class IpcTransport(Transport):
             for r in range(1, w):
                 self.flags.store(r, 0)
                 self.flags.store(w + r, 0)
-            self.make_rbuf().zero_()
+            rbuf.zero_()
             torch.cuda.synchronize(env.device)
             out = []
             for p in self.pairs:
                 r = p["rank"]
-                us = np.sort(1e6 * np.asarray(got[0]["rtt"][r]))
+                m, wk = got[0][r], got[r][r]
+                if m["timeout"] or wk["timeout"]:
+                    raise TransportError(f"preflight: rank 0 <-> rank {r}: a put or its echo never signalled "
+                                         f"within {timeout:.0f}s (device ping-pong)")
+                us = np.sort(np.asarray(m["rtt"]))
                 out.append({"rank": r, "iters": iters, "same_gpu": p["same_gpu"],
                             "master_to_rank_peer": p["master_to_rank"], "rank_to_master_peer": p["rank_to_master"],
                             "mailbox": "fine-grained device memory, host-registered counters" if self.FINE else "coarse",
+                            "rtt_clock": "device wall clock, counter store -> echo counter seen",
                             "rtt_us_p50": round(float(us[len(us) // 2]), 2),
                             "rtt_us_p99": round(float(us[min(len(us) - 1, int(0.99 * len(us)))]), 2),
                             "rtt_us_max": round(float(us[-1]), 2),
-                            "payload_errors_master_to_rank": int(got[r]["bad"]),
-                            "payload_errors_rank_to_master": int(got[0]["bad_echo"][r])})
+                            "payload_errors_master_to_rank": int(wk["errors"]),
+                            "payload_errors_rank_to_master": int(m["errors"])})
         out = env.broadcast_object(out, 0)
         env.barrier()
         return out

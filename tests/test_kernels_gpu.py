@@ -352,26 +352,30 @@ def test_dense_grad_staged_bundles(native, rows, d, prec_name, pair, layout):
         np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=tol * 1e-2)
 
 
-@pytest.mark.parametrize("form", ["fold-lane", "fold-wave", "unfolded"])
+@pytest.mark.parametrize("form", ["fold-lane", "fold-wave", "fold-pair", "unfolded"])
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
 @pytest.mark.parametrize("rows,d,prec_name", [(64, 1000, "fp64"), (37, 1000, "fp64"), (256, 250, "fp64"),
-                                              (64, 1000, "fp32"), (33, 130, "fp32")])
+                                              (33, 500, "fp64"), (64, 1000, "fp32"), (33, 130, "fp32"),
+                                              (35, 512, "fp32")])
 def test_dense_grad_one_wave_bundles(native, rows, d, prec_name, loss, form):
     """grad_dense_multi: one wave computes every replica of its bundle from rows double-buffered in
     registers, each replica with its own dot product, residual and gradient.  Bundles of 3 replicas,
     of 2 padded to 3, and partial / odd-length bundles (the two-rows-per-trip loop ends on either
     buffer) against the fp64 oracle; with the workgroup fold (4 bundles of one partition per
-    workgroup, pad bundles at partition ends, one slab row per workgroup and replica) and both
-    epilogues (replicas reduce-scattered with one lane per replica's residual, or wave-uniform),
-    and without the fold."""
+    workgroup, pad bundles at partition ends, one slab row per workgroup and replica) and all three
+    epilogues (replicas reduce-scattered with one lane per replica's residual, wave-uniform, or two
+    rows per 8-value reduce-scatter on narrow rows: odd bundles end on a half pair), and without
+    the fold."""
     fold = form != "unfolded"
     prec = get_precision(prec_name)
+    if form == "fold-pair" and -(-prec.ld(d) // (64 * prec.vec)) * prec.vec > 8:
+        pytest.skip("pair rows: narrow rows only (<= 8 columns per lane)")
     rng = np.random.RandomState(5)
     parts, host = _parts(rng, [700, 501, 300], d, prec)
     msgs = [[(0, 1.0), (1, 1.0)]] * 2 + [[(0, -0.5), (1, 2.0)]] + [[(2, 1.0)], [(2, -3.0)]]
     plan = DenseGradPlan(msgs, parts, prec, loss, d,
                          choice=KernelChoice("multi", replicas=3, bundle_rows=rows, fold=fold,
-                                             lane_epi=form == "fold-lane"))
+                                             lane_epi=form == "fold-lane", pair=form == "fold-pair"))
     assert plan.bundle_rows == rows
     if fold:  # slab rows: one per (workgroup, replica), a contiguous range per message
         stb = plan.slot_task_begin.cpu().numpy()

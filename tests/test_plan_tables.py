@@ -85,9 +85,12 @@ def test_kernel_selection_table():
     assert pick(0, 4096, 3, 1_000_000) == KernelChoice("wide", replicas=3, bundle_rows=976)
     assert pick(1, 4096, 2, 100_000) == KernelChoice("wide", replicas=2, bundle_rows=96)
     assert pick(0, 8192, 3, 1_000_000) == KernelChoice("wide", interleave=True)  # 512-thread rows: no bundles
-    # narrow rows: more, shorter one-wave bundles with the lane epilogue
-    assert pick(0, 256, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=192, fold=True, lane_epi=True)
-    assert pick(1, 256, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=128, fold=True, lane_epi=True)
+    # narrow rows: one-wave bundles with two rows per reduce-scatter, ~16 bundles per CU
+    assert pick(0, 256, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=256, fold=True, pair=True)
+    assert pick(1, 256, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=256, fold=True, pair=True)
+    assert pick(0, 512, 3, 1_000_000).pair and pick(1, 512, 3, 1_000_000).pair  # cpl 8
+    assert pick(0, 256, 3, 100_000).bundle_rows == 32 and pick(0, 256, 3, 4_000_000).bundle_rows == 512
+    assert not pick(1, 1000, 3, 1_000_000).pair  # cpl 16: four row buffers would not fit
     assert pick(0, 4096, 1, 1_000_000) == KernelChoice("wide")
     assert pick(0, 10000, 3, 100_000) == KernelChoice("twopass")
     # bf16 beyond the MFMA tile: the fused kernel, replica-interleaved

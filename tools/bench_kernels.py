@@ -185,11 +185,13 @@ def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000)
         distinct = 8 * parts[0][0].numel() * parts[0][0].element_size() / 1e12
         cands = [KernelChoice("fused", rows=r, interleave=i) for r in (1, 2, 4) for i in (False, True)]
         cands += [KernelChoice("multi", replicas=3, bundle_rows=b, fold=True, lane_epi=e)
-                  for b in (64, 128, 192, 256, 512, 768) for e in (False, True)]
+                  for b in (32, 64, 128, 192, 256, 512, 768) for e in (False, True)]
+        cands += [KernelChoice("multi", replicas=3, bundle_rows=b, fold=True, pair=True)
+                  for b in (32, 64, 128, 192, 256, 512, 768)]
         cands += [KernelChoice("staged", replicas=3, bundle_rows=b, pair=p, wpr=w)
                   for b in (128, 512) for p in (False, True) for w in (0, 1)]
         cands += [KernelChoice("wide", interleave=i) for i in (False, True)]
-        cands += [KernelChoice("wide", replicas=3, bundle_rows=b) for b in (16, 64, 256, 976)]
+        cands += [KernelChoice("wide", replicas=3, bundle_rows=b) for b in (16, 32, 64, 128, 256, 976)]
         default = None
         for c in [None] + cands:
             try:
