@@ -262,7 +262,19 @@ class Trainer:
         None when there is no IPC transport."""
         if self.tx is None or not hasattr(self.tx, "preflight"):
             return None
-        return self.tx.preflight(iters)
+        recs = self.tx.preflight(iters)
+        # ranks with their own GPUs: the RCCL point-to-point path (the IPC fallback) measured per pair too
+        if recs is not None and self.env.backend == "nccl" and self.env.device.type == "cuda":
+            from ..parallel.transport import rccl_p2p_preflight
+
+            try:  # informational: a failure is recorded, the run goes on over IPC
+                rc = rccl_p2p_preflight(self.env, self.ld, self.prec.acc, iters=min(200, iters))
+            except Exception as e:  # noqa: BLE001
+                rc = {r: {"rccl_error": f"{type(e).__name__}: {e}"[:300]} for r in range(1, self.env.world)}
+            rc = self.env.broadcast_object(rc, 0)
+            for rec in recs:
+                rec.update(rc.get(rec["rank"], {}))
+        return recs
 
     @property
     def transport(self) -> str:

@@ -646,6 +646,46 @@ class TransportError(RuntimeError):
     pass
 
 
+def rccl_p2p_preflight(env, ld: int, dtype, iters: int = 200, warm: int = 10) -> Dict[int, dict]:
+    """Collective (ranks with their own GPUs, world process group on RCCL): ``iters`` send -> echo
+    round trips of one row between the master and each worker rank in turn through
+    torch.distributed send/recv, i.e. RCCL point-to-point over xGMI -- the fallback transport's wire
+    path, measured beside the IPC mailbox's.  Host-timed (launch + completion), first ``warm`` trips
+    (lazy channel setup) dropped.  Returns {rank: {rtt_us_p50, rtt_us_p99, payload_errors}} on the
+    master, {} elsewhere."""
+    import datetime
+
+    out: Dict[int, dict] = {}
+    x = torch.zeros(ld, dtype=dtype, device=env.device)
+    y = torch.empty_like(x)
+    limit = datetime.timedelta(seconds=30)  # every transfer waits with a deadline: no silent hang
+    for r in range(1, env.world):
+        env.barrier()
+        if env.is_master:
+            ts, bad = [], 0
+            for k in range(warm + iters):
+                x.fill_(float(k % 1000) + 0.5)
+                torch.cuda.synchronize(env.device)
+                t0 = time.perf_counter()
+                dist.isend(x, dst=r).wait(limit)
+                dist.irecv(y, src=r).wait(limit)
+                torch.cuda.synchronize(env.device)
+                if k >= warm:
+                    ts.append(1e6 * (time.perf_counter() - t0))
+                    bad += int(not bool(torch.equal(x, y)))
+            us = np.sort(np.asarray(ts))
+            out[r] = {"rccl_rtt_us_p50": round(float(us[len(us) // 2]), 2),
+                      "rccl_rtt_us_p99": round(float(us[min(len(us) - 1, int(0.99 * len(us)))]), 2),
+                      "rccl_payload_errors": bad}
+        elif env.rank == r:
+            for _ in range(warm + iters):
+                dist.irecv(y, src=0).wait(limit)
+                dist.isend(y, dst=0).wait(limit)
+            torch.cuda.synchronize(env.device)
+        env.barrier()
+    return out
+
+
 def make_transport(kind: str, env, R: int, K: int, ld: int, dtype, n_local: int, remote_counts,
                    timeout: float = 600.0) -> Transport:
     """kind: auto | ipc | rccl | gloo.  auto = gloo on CPU; on GPUs the IPC mailbox after a
