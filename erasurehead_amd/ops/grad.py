@@ -108,13 +108,15 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
     each bundle's beta load / fold / slab write amortises over more rows): 5 bundles per CU fp64,
     10 fp32.  Measured (tools/sweep_multi_rows.sh, profiles/round2/s2_multi): N=1 fp64 768 rows 1.330 ms vs
     512 1.36 / 640 1.37 / 1024 1.54; N=2 256 rows 0.708; N=4 128 rows 0.370 vs 96 0.45 / 160 0.40;
-    N=8 64 rows 0.206 vs 48 0.25 / 80 0.22; fp32 N=1 384 rows 0.692 (320: 0.95, a second pass).
+    N=8 64 rows 0.206 vs 48 0.25 / 80 0.22; fp32 N=1 384 rows 0.692 (320: 0.95, a second pass);
+    fp32 short streams 8 per CU (500k / 250k / 125k rows: 256 / 128 / 64-row bundles, 0.346 / 0.182 /
+    0.100 ms, 12-19 % under the LDS-staged pair bundles; profiles/round3/choices/choices_fp32_short.jsonl).
     Narrower rows (cpl < 16 columns per lane) hold proportionally fewer registers, so proportionally
     more bundles fit per CU, and each carries fewer bytes in flight: the count scales by 16 / cpl
     (d = 256 at 1e6 rows: 256-row fp64 bundles 4.8 TB/s vs 2.3 at 768, 128-row fp32 4.1 vs 2.4;
     profiles/round3/choices)."""
     long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
-    per_cu = (10 if long_stream else 12) if fp32 else (5 if long_stream else 8)
+    per_cu = (10 if long_stream else 8) if fp32 else (5 if long_stream else 8)
     per_cu *= max(1, 16 // cpl)
     return max(64, 64 * int(round(distinct_rows / (per_cu * n_cus) / 64)))
 
@@ -157,8 +159,9 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
       * replicas, fp64, 3 per bundle (AGC / cyclic s = 2): one-wave bundles, folded; the lane
         epilogue below the long-stream regime (sharded ranks: 0.188 vs 0.195 ms at N = 8), the
         wave-uniform one in it (the one-GPU headline: 1.316 vs 1.40 ms);
-      * replicas otherwise (fp64 R = 2, fp32): LDS-staged bundles; fp32 in the long-stream regime
-        with R = 3 one-wave bundles (0.692 vs 0.740 ms); the pair form for fp32 and for every
+      * fp32 with 3 replicas: one-wave bundles too (long stream 0.692 vs 0.740 ms staged; short
+        streams, the sharded ranks, 12-19 % under the staged pair bundles);
+      * replicas otherwise (R = 2, R > 3): LDS-staged bundles, the pair form for fp32 and for every
         short-stream rank (one wave per replica there);
       * bf16 replicas: MFMA bundles (d <= 1024, d % 8 == 0), else the fused kernel interleaved;
       * 2048 < d (fp64, 4096 fp32): the wide kernel; beyond 8192 / 16384 or cpl unknown: two passes.
@@ -180,7 +183,7 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     if cpl <= 8 and max_rep == 3:  # narrow rows: two rows per reduce-scatter
         return KernelChoice("multi", replicas=3, bundle_rows=pair_bundle_rows(distinct_rows, n_cus), fold=True,
                             pair=True)
-    if cpl <= 16 and max_rep == 3 and (prec_code == 0 or long_stream):
+    if cpl <= 16 and max_rep == 3:
         return KernelChoice("multi", replicas=3,
                             bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl),
                             fold=True, lane_epi=not long_stream)

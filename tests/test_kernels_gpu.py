@@ -282,9 +282,8 @@ def test_dense_grad_staged_is_the_replica_default(prec_name, native):
 
 @pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
 def test_dense_grad_one_wave_bundles_are_the_fp64_default(prec_name, native):
-    """Bundles of at most 3 replicas default to grad_dense_multi for fp64 (bundle length from
-    multi_bundle_rows), to the staged pair bundles for fp32 and to MFMA for bf16; the messages
-    match message-major order to rounding."""
+    """Bundles of 3 replicas default to grad_dense_multi for fp64 and fp32 (bundle length from
+    multi_bundle_rows) and to MFMA for bf16; the messages match message-major order to rounding."""
     from erasurehead_amd.ops.grad import multi_bundle_rows
 
     prec = get_precision(prec_name)
@@ -293,9 +292,9 @@ def test_dense_grad_one_wave_bundles_are_the_fp64_default(prec_name, native):
     msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(2, -1.0)]] * 2
     a = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000)
     b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, choice=MESSAGE_MAJOR)
-    assert a.choice.kind == {"fp64": "multi", "fp32": "staged", "bf16": "mfma"}[prec_name]
+    assert a.choice.kind == {"fp64": "multi", "fp32": "multi", "bf16": "mfma"}[prec_name]
     if a.choice.kind == "multi":
-        assert a.choice.fold and a.choice.lane_epi and a.bundle_rows == multi_bundle_rows(6000)
+        assert a.choice.fold and a.choice.lane_epi and a.bundle_rows == multi_bundle_rows(6000, prec_name == "fp32")
     beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
     Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
     a.native_launcher().launch(beta, Ga)

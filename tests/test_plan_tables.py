@@ -71,7 +71,8 @@ def test_kernel_selection_table():
     assert pick(2, 1000, 3, 1_000_000) == KernelChoice("mfma", replicas=3, bundle_rows=2048)
     # the 8-GPU partition-shard rank (125k rows): fill every wave slot, lane epilogue
     assert pick(0, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)
-    assert pick(1, 1000, 3, 125_000) == KernelChoice("staged", replicas=3, bundle_rows=128, pair=True, wpr=1)
+    assert pick(1, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)
+    assert pick(1, 1000, 3, 500_000).bundle_rows == 256 and pick(1, 1000, 3, 250_000).bundle_rows == 128
     # FRC s=1 (bundles of 2): staged, one GPU / a sharded rank
     assert pick(0, 1000, 2, 1_000_000) == KernelChoice("staged", replicas=2, bundle_rows=512)
     assert pick(0, 1000, 2, 250_000) == KernelChoice("staged", replicas=2, bundle_rows=128, pair=True, wpr=1)

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def one(n_gpus: int, precision: str, shard: str = "partition", rows: int = 0) -> dict:
+def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0) -> dict:
     import numpy as np
     import torch
 
@@ -48,7 +48,7 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows: int = 0) ->
     _, _, r = max(costs)
     mine = [u for u, o in zip(shards, owner) if o == r]
     src = SyntheticSource(1_000_000, 1000, sch.n_partition_files, 1234)
-    bundle_rows = rows
+    bundle_rows = rows_override
     need = sorted({p for u in mine for p, _ in u.segments})
     parts = {p: src.partition(p, prec, torch.device("cuda")) for p in need}
     msgs = [list(u.segments) for u in mine]
