@@ -128,6 +128,7 @@ def main(argv=None) -> int:
     from erasurehead_amd.config import RunConfig
     from erasurehead_amd.engine import Trainer, evaluate
     from erasurehead_amd.parallel.dist import init_distributed
+    from erasurehead_amd.parallel.transport import TransportError
 
     env = init_distributed("auto")
 
@@ -162,7 +163,22 @@ def main(argv=None) -> int:
     trainer = Trainer(make_cfg(w0 + a.steps), env)
     setup_s = time.perf_counter() - t_setup
     # the first multi-GPU run checks itself: put -> flag latency and payload checks per worker/master pair
-    preflight = trainer.preflight(a.preflight) if env.world > 1 and a.preflight > 0 else None
+    preflight_failure = None
+    try:
+        preflight = trainer.preflight(a.preflight) if env.world > 1 and a.preflight > 0 else None
+    except TransportError as e:
+        # every rank raised the same verdict (IpcTransport.preflight): the IPC mailbox lost a payload or a
+        # signal.  Unless the IPC path was asked for by name, rebuild on RCCL p2p under the same pumps
+        # (the loud fallback make_transport takes when the handshake fails) and record why.  Ranks that
+        # share a GPU (rehearsals; RCCL refuses them) take the loopback communicator, RCCL's code path.
+        if a.transport == "ipc" or os.environ.get("ERASUREHEAD_NO_FALLBACK"):
+            raise
+        preflight_failure, preflight = str(e), None
+        a.transport = "rccl" if env.backend == "nccl" else "loopback"
+        if env.is_master:
+            print(f"[bench] WARNING: {e}; rebuilding on {a.transport}", file=sys.stderr, flush=True)
+        free(trainer)
+        trainer = Trainer(make_cfg(w0 + a.steps), env)
     res = trainer.run(timed_start=w0)
     mine = res.timed_seconds if env.is_master else trainer.worker_timed_seconds
     timed = env.allreduce_max(mine)
@@ -226,6 +242,8 @@ def main(argv=None) -> int:
             out["config"]["slow_ranks"] = parse_slow_ranks(a.slow_ranks)
         if preflight is not None:
             out["peer_preflight"] = preflight
+        if preflight_failure is not None:
+            out["peer_preflight_failure"] = preflight_failure
         if n_gpu_dev and env.world > n_gpu_dev:
             out["config"]["ranks_per_gpu"] = env.world / n_gpu_dev  # rehearsal: ranks time-share GPUs
         out["config"]["round_loop"] = {"graph": "device-driven, hipGraph", "stream": "device-driven",

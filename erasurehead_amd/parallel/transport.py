@@ -569,9 +569,11 @@ class IpcTransport(Transport):
             env.barrier()
         mine = {r: {"errors": int(v["payload_errors"]), "timeout": bool(v["timeout"]),
                     "rtt": (v["rtt_us"].numpy().tolist() if "rtt_us" in v else None)} for r, v in results.items()}
+        if os.environ.get("ERASUREHEAD_SABOTAGE") == f"preflight:{env.rank}" and env.rank in mine:
+            mine[env.rank]["errors"] += 1  # test hook: this worker reports one bad payload word (the verdict path)
         got = env.gather_objects(mine)
         env.barrier()
-        out = None
+        out, err = None, None
         if env.is_master:
             for r in range(1, w):
                 self.flags.store(r, 0)
@@ -583,8 +585,13 @@ class IpcTransport(Transport):
                 r = p["rank"]
                 m, wk = got[0][r], got[r][r]
                 if m["timeout"] or wk["timeout"]:
-                    raise TransportError(f"preflight: rank 0 <-> rank {r}: a put or its echo never signalled "
-                                         f"within {timeout:.0f}s (device ping-pong)")
+                    err = (f"preflight: rank 0 <-> rank {r}: a put or its echo never signalled "
+                           f"within {timeout:.0f}s (device ping-pong)")
+                    break
+                if wk["errors"] or m["errors"]:
+                    err = (f"preflight: rank 0 <-> rank {r}: {wk['errors']} payload words wrong master -> rank, "
+                           f"{m['errors']} rank -> master after the counter was seen (device ping-pong)")
+                    break
                 us = np.sort(np.asarray(m["rtt"]))
                 out.append({"rank": r, "iters": iters, "same_gpu": p["same_gpu"],
                             "master_to_rank_peer": p["master_to_rank"], "rank_to_master_peer": p["rank_to_master"],
@@ -595,8 +602,11 @@ class IpcTransport(Transport):
                             "rtt_us_max": round(float(us[-1]), 2),
                             "payload_errors_master_to_rank": int(wk["errors"]),
                             "payload_errors_rank_to_master": int(m["errors"])})
-        out = env.broadcast_object(out, 0)
+        # the verdict is collective: every rank raises the same error (bench.py then rebuilds on RCCL)
+        out, err = env.broadcast_object((out, err), 0)
         env.barrier()
+        if err is not None:
+            raise TransportError(err)
         return out
 
     # ---- master ------------------------------------------------------------------------
