@@ -30,10 +30,15 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
 }
+// Cache policy of the design-matrix stream: nt (aux bit 1).  Every X row is read exactly once per
+// round from HBM (8 GB per headline round, 32x the Infinity Cache), so default-policy loads only
+// churn L2 / MALL.  Measured on a plain 8 KB-row read stream (tools/probes/nt_stream.hip,
+// profiles/round3/nt_stream): 5.92 -> 6.62 TB/s at 8 GB, 5.82 -> 6.57 TB/s at 1 GB; sc0 = default.
+constexpr int kStreamAux = 2;
 template <typename V>
 __device__ __forceinline__ V buf_load16(__amdgpu_buffer_rsrc_t rs, int byte_off) {
   static_assert(sizeof(V) == 16, "16-byte vector");
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, kStreamAux);
   V out;
   __builtin_memcpy(&out, &v, 16);
   return out;
@@ -53,6 +58,18 @@ __device__ __forceinline__ A buf_load_scalar(__amdgpu_buffer_rsrc_t rs, int byte
   }
 }
 
+// 16 bytes through a non-temporal global load (global_load_dwordx4 ... nt): the X stream's policy
+// for the kernels that address rows through plain pointers (see kStreamAux).
+typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+template <typename V>
+__device__ __forceinline__ V load16_nt(const void* p) {
+  static_assert(sizeof(V) == 16, "16-byte vector");
+  const u32x4_nt v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
+  V out;
+  __builtin_memcpy(&out, &v, 16);
+  return out;
+}
+
 // Storage-type traits: how many elements fit a 16-byte vector load and how to widen.
 template <typename T> struct Vec16;
 template <> struct Vec16<double> {
@@ -61,9 +78,9 @@ template <> struct Vec16<double> {
   __device__ __forceinline__ static raw load_raw(const double* p) { return *reinterpret_cast<const raw*>(p); }
   template <typename A>
   __device__ __forceinline__ static A elem(const raw& v, int i) { return static_cast<A>(i == 0 ? v.x : v.y); }
-  template <typename A>
+  template <typename A, bool NT = false>
   __device__ __forceinline__ static void load(const double* p, A (&out)[N]) {
-    const double2 v = *reinterpret_cast<const double2*>(p);
+    const double2 v = NT ? load16_nt<double2>(p) : *reinterpret_cast<const double2*>(p);
     out[0] = static_cast<A>(v.x);
     out[1] = static_cast<A>(v.y);
   }
@@ -76,9 +93,9 @@ template <> struct Vec16<float> {
   __device__ __forceinline__ static A elem(const raw& v, int i) {
     return static_cast<A>(i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
   }
-  template <typename A>
+  template <typename A, bool NT = false>
   __device__ __forceinline__ static void load(const float* p, A (&out)[N]) {
-    const float4 v = *reinterpret_cast<const float4*>(p);
+    const float4 v = NT ? load16_nt<float4>(p) : *reinterpret_cast<const float4*>(p);
     out[0] = static_cast<A>(v.x);
     out[1] = static_cast<A>(v.y);
     out[2] = static_cast<A>(v.z);
@@ -94,9 +111,9 @@ template <> struct Vec16<bf16_t> {
     const uint32_t w = (i >> 1) == 0 ? v.x : (i >> 1) == 1 ? v.y : (i >> 1) == 2 ? v.z : v.w;
     return static_cast<A>(__uint_as_float((i & 1) ? (w & 0xffff0000u) : (w << 16)));
   }
-  template <typename A>
+  template <typename A, bool NT = false>
   __device__ __forceinline__ static void load(const bf16_t* p, A (&out)[N]) {
-    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint4 v = NT ? load16_nt<uint4>(p) : *reinterpret_cast<const uint4*>(p);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

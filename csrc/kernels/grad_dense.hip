@@ -133,7 +133,7 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
     for (int j = 0; j < NV; ++j) {
       const int c0 = (j * kWave + lane) * VN;
       if (valid[j]) {
-        Vec16<T>::load(x0 + c0, a0[j]);
+        Vec16<T>::template load<A, true>(x0 + c0, a0[j]);
       } else {
 #pragma unroll
         for (int v = 0; v < VN; ++v) a0[j][v] = A(0);
@@ -713,8 +713,8 @@ grad_dense_fused_pair(const Segment* __restrict__ segs, const Task* __restrict__
     for (int j = 0; j < NV; ++j) {
       const int c0 = (j * kWave + lane) * VN;
       if (valid[j]) {
-        Vec16<T>::load(x0 + c0, a0[j]);
-        Vec16<T>::load(x1 + c0, a1[j]);
+        Vec16<T>::template load<A, true>(x0 + c0, a0[j]);
+        Vec16<T>::template load<A, true>(x1 + c0, a1[j]);
       } else {
 #pragma unroll
         for (int v = 0; v < VN; ++v) { a0[j][v] = A(0); a1[j][v] = A(0); }
@@ -745,7 +745,7 @@ grad_dense_fused_pair(const Segment* __restrict__ segs, const Task* __restrict__
     for (int j = 0; j < NV; ++j) {
       const int c0 = (j * kWave + lane) * VN;
       if (valid[j]) {
-        Vec16<T>::load(x0 + c0, a0[j]);
+        Vec16<T>::template load<A, true>(x0 + c0, a0[j]);
       } else {
 #pragma unroll
         for (int v = 0; v < VN; ++v) a0[j][v] = A(0);
@@ -837,8 +837,8 @@ grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks
     for (int j = 0; j < NV; ++j) {
       const int c0 = (j * BS + tid) * VN;
       if (valid[j]) {
-        Vec16<T>::load(x0 + c0, a0[j]);
-        Vec16<T>::load(x1 + c0, a1[j]);
+        Vec16<T>::template load<A, true>(x0 + c0, a0[j]);
+        Vec16<T>::template load<A, true>(x1 + c0, a1[j]);
       } else {
 #pragma unroll
         for (int v = 0; v < VN; ++v) { a0[j][v] = A(0); a1[j][v] = A(0); }
@@ -1109,7 +1109,7 @@ rowdot_residual(const Segment* __restrict__ segs, const Task* __restrict__ tasks
     A z = A(0);
     for (int c0 = lane * VN; c0 < ld; c0 += kWave * VN) {
       A a[VN];
-      Vec16<T>::load(x + c0, a);
+      Vec16<T>::template load<A, true>(x + c0, a);
 #pragma unroll
       for (int v = 0; v < VN; ++v) z = fma(a[v], beta[c0 + v], z);
     }
@@ -1136,7 +1136,7 @@ xt_r_tiles(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
   for (int v = 0; v < VN; ++v) g[v] = A(0);
   for (int r = task.row_begin; r < task.row_end; ++r) {
     A a[VN];
-    Vec16<T>::load(X + static_cast<long long>(r) * ld + c0, a);
+    Vec16<T>::template load<A, true>(X + static_cast<long long>(r) * ld + c0, a);
     const A rr = rbuf[off + (r - task.row_begin)];
 #pragma unroll
     for (int v = 0; v < VN; ++v) g[v] = fma(rr, a[v], g[v]);

@@ -11,9 +11,10 @@ namespace eh {
 // for their own loads instead: "stage t landed" is vmcnt <= the loads this wave issued for the
 // stages after t (tests/test_isa_checks.py checks the compiler adds no loads of its own inside the
 // counted stage loop; -DEH_FULL_VMCNT turns every such wait into vmcnt(0) for a suspected LDS race).
+// glds16 carries the X stream: nt, like kStreamAux (common.h); glds4 (labels) keeps the default policy.
 __device__ __forceinline__ void glds16(const void* g, unsigned lds) {
   int keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
 }
 __device__ __forceinline__ void glds4(const void* g, unsigned lds) {
