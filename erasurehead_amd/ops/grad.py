@@ -99,26 +99,33 @@ class KernelChoice:
         return out
 
 
-def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS, cpl: int = 16) -> int:
-    """Rows per one-wave bundle of grad_dense_multi, in multiples of 64, from the rows per CU.
+def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS, cpl: int = 16,
+                      part_rows: Optional[Sequence[int]] = None) -> int:
+    """Rows per one-wave bundle of grad_dense_multi: the shortest multiple of 32 rows whose folded
+    workgroups (4 bundles of one partition each, the last one per partition padded) all fit the
+    chip's resident slots at once, so every bundle starts in the first dispatch round and no CU is
+    left with a second, partial round of equal-length bundles (the tail that costs a whole bundle).
 
     Resident one-wave bundles per CU: 8 fp64 (244 VGPRs, 2 waves per SIMD), 12 fp32 (155 VGPRs,
-    3 per SIMD).  Below the long-stream regime a rank fills every slot (one bundle per wave slot);
-    in it, fewer, longer bundles win (HBM-bound: ~10 MB of rows in flight already saturate it, and
-    each bundle's beta load / fold / slab write amortises over more rows): 5 bundles per CU fp64,
-    10 fp32.  Measured (tools/sweep_multi_rows.sh, profiles/round2/s2_multi): N=1 fp64 768 rows 1.330 ms vs
-    512 1.36 / 640 1.37 / 1024 1.54; N=2 256 rows 0.708; N=4 128 rows 0.370 vs 96 0.45 / 160 0.40;
-    N=8 64 rows 0.206 vs 48 0.25 / 80 0.22; fp32 N=1 384 rows 0.692 (320: 0.95, a second pass);
-    fp32 short streams 8 per CU (500k / 250k / 125k rows: 256 / 128 / 64-row bundles, 0.346 / 0.182 /
-    0.100 ms, 12-19 % under the LDS-staged pair bundles; profiles/round3/choices/choices_fp32_short.jsonl).
-    Narrower rows (cpl < 16 columns per lane) hold proportionally fewer registers, so proportionally
-    more bundles fit per CU, and each carries fewer bytes in flight: the count scales by 16 / cpl
-    (d = 256 at 1e6 rows: 256-row fp64 bundles 4.8 TB/s vs 2.3 at 768, 128-row fp32 4.1 vs 2.4;
-    profiles/round3/choices)."""
-    long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
-    per_cu = (10 if long_stream else 8) if fp32 else (5 if long_stream else 8)
-    per_cu *= max(1, 16 // cpl)
-    return max(64, 64 * int(round(distinct_rows / (per_cu * n_cus) / 64)))
+    3 per SIMD); narrower rows (cpl < 16 columns per lane) hold proportionally fewer registers, so
+    16 / cpl times as many fit.  part_rows: row counts of the distinct partitions (default: the
+    rows split evenly over 8).  With the non-temporal X stream (common.h kStreamAux) every slot
+    filled once wins at every rank shape (profiles/round3/nt_rows): fp64 1e6 / 500k / 250k / 125k
+    distinct rows -> 512 / 256 / 128 / 64-row bundles, 1.195 / 0.600 / 0.312 / 0.169 ms (768 rows,
+    the default before nt: 1.26 ms; 384: 1.42 = a second partial round); fp32 -> 352 / 192 / 96 /
+    64 rows (192: 0.333 vs 256: 0.341-0.350 ms at 500k; 96: 0.177 vs 128: 0.186 at 250k)."""
+    per_cu = (12 if fp32 else 8) * max(1, 16 // cpl)
+    slots = per_cu * n_cus
+    parts = [int(r) for r in part_rows if r > 0] if part_rows else [distinct_rows / 8.0] * 8
+    base = max(32, 32 * int(np.ceil(distinct_rows / slots / 32)))
+
+    def fits(rows: int) -> bool:
+        return sum(4 * int(np.ceil(np.ceil(p / rows) / 4)) for p in parts) <= slots
+
+    rows = base
+    while not fits(rows) and rows < max(parts):
+        rows += 32
+    return rows if fits(rows) else base  # more partitions than slots: short bundles keep the tail short
 
 
 def pair_bundle_rows(distinct_rows: int, n_cus: int = N_CUS) -> int:
@@ -147,7 +154,7 @@ def staged_bundle_rows(distinct_rows: int, n_cus: int = N_CUS) -> int:
 
 
 def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, distinct_rows: int,
-                  n_cus: int = N_CUS) -> KernelChoice:
+                  n_cus: int = N_CUS, part_rows: Optional[Sequence[int]] = None) -> KernelChoice:
     """The measured default kernel of a plan (a pure function; tests/test_plan_tables.py pins the table).
 
     prec_code: 0 fp64, 1 fp32, 2 bf16 storage.  max_rep: most co-located messages reading one
@@ -185,7 +192,7 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
                             pair=True)
     if cpl <= 16 and max_rep == 3:
         return KernelChoice("multi", replicas=3,
-                            bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl),
+                            bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl, part_rows),
                             fold=True, lane_epi=not long_stream)
     # more replicas than a workgroup's task slots: bundles of MAX_BUNDLE (and the remainder, padded)
     return KernelChoice("staged", replicas=min(max_rep, MAX_BUNDLE), bundle_rows=staged_bundle_rows(distinct_rows, n_cus),
@@ -287,8 +294,10 @@ class DenseGradPlan:
         self.cpl = choose_cpl(self.ld, prec.vec)
         # co-located replicas: a partition read by several local messages
         self.max_rep = max(collections.Counter(p for m in self.messages for p, _ in m).values(), default=0)
-        distinct_rows = sum(partitions[p][0].shape[0] for p in {p for m in self.messages for p, _ in m})
-        self.choice = choice or choose_kernel(prec.code, self.ld, self.cpl, self.max_rep, distinct_rows)
+        part_rows = [partitions[p][0].shape[0] for p in sorted({p for m in self.messages for p, _ in m})]
+        distinct_rows = sum(part_rows)
+        self.choice = choice or choose_kernel(prec.code, self.ld, self.cpl, self.max_rep, distinct_rows,
+                                              part_rows=part_rows)
         c = self.choice
         if c.kind == "twopass" and self.cpl is not None:
             raise ValueError("the two-pass kernel is for rows wider than the one-pass kernels")

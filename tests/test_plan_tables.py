@@ -51,8 +51,13 @@ def test_fold_table_groups_one_partition_per_workgroup():
 
 
 def test_multi_bundle_rows_table():
-    assert [multi_bundle_rows(n) for n in (1_000_000, 500_000, 250_000, 125_000)] == [768, 256, 128, 64]
-    assert multi_bundle_rows(1_000_000, fp32=True) == 384 and multi_bundle_rows(1000) == 64
+    # every folded workgroup resident at once (profiles/round3/nt_rows)
+    assert [multi_bundle_rows(n) for n in (1_000_000, 500_000, 250_000, 125_000)] == [512, 256, 128, 64]
+    assert [multi_bundle_rows(n, fp32=True) for n in (1_000_000, 500_000, 250_000, 125_000)] == [352, 192, 96, 64]
+    assert multi_bundle_rows(1000) == 32 and multi_bundle_rows(4_000_000) == 1984
+    # per-partition fold padding pushes a bundle length up until the workgroups fit the slots
+    assert multi_bundle_rows(300_000) == 160 and multi_bundle_rows(300_000, part_rows=[1000] * 300) == 256
+    assert multi_bundle_rows(300_000, part_rows=[100] * 3000) == 160  # can never fit: the plain length
 
 
 def test_kernel_selection_table():
@@ -66,13 +71,13 @@ def test_kernel_selection_table():
         return choose_kernel(prec, ld, choose_cpl(ld, vec), rep, rows)
 
     # the headline (AGC W=8 s=2: bundles of 3 replicas), one GPU (1e6 distinct rows): long stream
-    assert pick(0, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=768, fold=True)
-    assert pick(1, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=384, fold=True)
+    assert pick(0, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=512, fold=True)
+    assert pick(1, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=352, fold=True)
     assert pick(2, 1000, 3, 1_000_000) == KernelChoice("mfma", replicas=3, bundle_rows=2048)
     # the 8-GPU partition-shard rank (125k rows): fill every wave slot, lane epilogue
     assert pick(0, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)
     assert pick(1, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)
-    assert pick(1, 1000, 3, 500_000).bundle_rows == 256 and pick(1, 1000, 3, 250_000).bundle_rows == 128
+    assert pick(1, 1000, 3, 500_000).bundle_rows == 192 and pick(1, 1000, 3, 250_000).bundle_rows == 96
     # FRC s=1 (bundles of 2): staged, one GPU / a sharded rank
     assert pick(0, 1000, 2, 1_000_000) == KernelChoice("staged", replicas=2, bundle_rows=512)
     assert pick(0, 1000, 2, 250_000) == KernelChoice("staged", replicas=2, bundle_rows=128, pair=True, wpr=1)

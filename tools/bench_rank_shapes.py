@@ -1,6 +1,6 @@
 """Per-rank gradient work of the headline at N = 1/2/4/8 GPUs, timed on one MI355X.
 
-    python tools/bench_rank_shapes.py [--shard partition|message] [--rows-sweep] [--out FILE]
+    python tools/bench_rank_shapes.py [--shard partition|message] [--rows-sweep [--rows-list 64,128,...]] [--out FILE]
 
 With partition shards (parallel/placement.py) the rank of an N-GPU headline run (AGC W=8, s=2,
 k=6, 1e6 x 1e3 fp64) holds 8/N partitions of 125k rows, each with its 2-3 replica messages; with
@@ -81,6 +81,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--rows-sweep", action="store_true")
+    ap.add_argument("--rows-list", default="64,128,256,512", help="bundle lengths of --rows-sweep")
+    ap.add_argument("--gpus-list", default="1,2,4,8")
     ap.add_argument("--precision", default="fp64")
     ap.add_argument("--shard", default="partition", choices=["partition", "message"])
     ap.add_argument("--one", type=int, default=0, help=argparse.SUPPRESS)
@@ -90,8 +92,8 @@ def main():
         print(json.dumps(one(a.one, a.precision, a.shard, a.rows)), flush=True)
         return 0
     lines = []
-    sweeps = [None] + ([64, 128, 256, 512] if a.rows_sweep else [])
-    for n in (1, 2, 4, 8):
+    sweeps = [None] + ([int(x) for x in a.rows_list.split(",")] if a.rows_sweep else [])
+    for n in [int(x) for x in a.gpus_list.split(",")]:
         for rows in sweeps:
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", str(n), "--precision",
                                   a.precision, "--shard", a.shard, "--rows", str(rows or 0)],
