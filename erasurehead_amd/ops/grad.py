@@ -137,12 +137,16 @@ def pair_bundle_rows(distinct_rows: int, n_cus: int = N_CUS) -> int:
     return int(min(512, max(32, 2 ** round(np.log2(per)))))
 
 
-def mfma_bundle_rows(distinct_rows: int) -> int:
-    """Rows per bf16 MFMA bundle: one 8-wave workgroup per CU (150 KB of LDS); long bundles amortise
-    its prologue (profiles/r2_mfma_ab2: 512 / 1024 / 2048 rows -> 0.458 / 0.440 / 0.430 ms at the bf16
-    headline): about two bundles per CU, 256..2048 rows."""
+def mfma_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional[Sequence[int]] = None) -> int:
+    """Rows per bf16 MFMA bundle: one 8-wave workgroup per CU (150 KB of LDS); the shortest power of two
+    from 256 rows whose bundles (one per workgroup, per partition) all start in the first dispatch
+    round.  Measured with the nt stream (profiles/round3/nt_rows/bf16.jsonl), rank gradient ms by
+    bundle rows: 500k distinct rows 2048: 0.200 (1024: 0.208, 4096: 0.302 = a second round);
+    250k 1024: 0.097 (512: 0.112, 2048: 0.159); 125k 512: 0.054 (256: 0.062, 1024: 0.086); 1e6 rows
+    4096: 0.375 = 2048: 0.378."""
+    parts = [int(r) for r in part_rows if r > 0] if part_rows else [distinct_rows / 8.0] * 8
     rows = 256
-    while rows < 2048 and rows * 2 * N_CUS < distinct_rows:
+    while rows < 8192 and sum(int(np.ceil(p / rows)) for p in parts) > n_cus:
         rows *= 2
     return rows
 
@@ -185,7 +189,8 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
     if prec_code == 2:
         if ld <= 1024 and ld % 8 == 0 and max_rep <= 16:
-            return KernelChoice("mfma", replicas=min(max_rep, MAX_BUNDLE), bundle_rows=mfma_bundle_rows(distinct_rows))
+            return KernelChoice("mfma", replicas=min(max_rep, MAX_BUNDLE),
+                                bundle_rows=mfma_bundle_rows(distinct_rows, n_cus, part_rows))
         return KernelChoice("fused", rows=1, interleave=True)
     if cpl <= 8 and max_rep == 3:  # narrow rows: two rows per reduce-scatter
         return KernelChoice("multi", replicas=3, bundle_rows=pair_bundle_rows(distinct_rows, n_cus), fold=True,

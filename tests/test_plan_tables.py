@@ -73,7 +73,9 @@ def test_kernel_selection_table():
     # the headline (AGC W=8 s=2: bundles of 3 replicas), one GPU (1e6 distinct rows): long stream
     assert pick(0, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=512, fold=True)
     assert pick(1, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=352, fold=True)
-    assert pick(2, 1000, 3, 1_000_000) == KernelChoice("mfma", replicas=3, bundle_rows=2048)
+    assert pick(2, 1000, 3, 1_000_000) == KernelChoice("mfma", replicas=3, bundle_rows=4096)
+    # bf16 MFMA bundles: every workgroup (one per CU) in the first dispatch round
+    assert [pick(2, 1000, 3, n).bundle_rows for n in (500_000, 250_000, 125_000, 10_000)] == [2048, 1024, 512, 256]
     # the 8-GPU partition-shard rank (125k rows): fill every wave slot, lane epilogue
     assert pick(0, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)
     assert pick(1, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)

@@ -1,0 +1,14 @@
+# Per-round overhead chain on one GPU: a tiny AGC problem (16k x 1000 rows, kernels of a few us)
+# so the round time is mostly messaging + arbiter / host pump; 2 and 8 ranks, arbiter off / on.
+#   gpurun -- bash tools/probes/overhead_tiny.sh   (writes gpurun_out/overhead/)
+set -o pipefail
+O=gpurun_out/overhead
+mkdir -p $O
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 300 python -u bench.py --precision bf16 --no-floor --json-out $O/bf16.json > $O/bf16.log 2>&1 || exit 1
+for n in 2 8; do
+  for m in off on; do
+    ERASUREHEAD_DEVICE_MASTER=$m timeout -k 10 300 python -u bench.py --gpus $n --steps 200 --warmup 20 --no-floor --n-rows 16000 --n-cols 1000 --json-out $O/tiny_${n}_$m.json > $O/tiny_${n}_$m.log 2>&1 || exit 1
+  done
+done
+echo done
