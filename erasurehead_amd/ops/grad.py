@@ -108,13 +108,16 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
 
     Resident one-wave bundles per CU: 8 fp64 (244 VGPRs, 2 waves per SIMD), 12 fp32 (155 VGPRs,
     3 per SIMD); narrower rows (cpl < 16 columns per lane) hold proportionally fewer registers, so
-    16 / cpl times as many fit.  part_rows: row counts of the distinct partitions (default: the
+    16 / cpl times as many fit.  In the long-stream regime fp32 fills 8 per CU too (1e6 rows, lane
+    epilogue: 512-row bundles 0.631 ms vs 352 rows 0.693 / 256 rows 0.644 with the wave epilogue;
+    profiles/round3/choices_nt/agc.jsonl).  part_rows: row counts of the distinct partitions (default: the
     rows split evenly over 8).  With the non-temporal X stream (common.h kStreamAux) every slot
     filled once wins at every rank shape (profiles/round3/nt_rows): fp64 1e6 / 500k / 250k / 125k
     distinct rows -> 512 / 256 / 128 / 64-row bundles, 1.195 / 0.600 / 0.312 / 0.169 ms (768 rows,
     the default before nt: 1.26 ms; 384: 1.42 = a second partial round); fp32 -> 352 / 192 / 96 /
     64 rows (192: 0.333 vs 256: 0.341-0.350 ms at 500k; 96: 0.177 vs 128: 0.186 at 250k)."""
-    per_cu = (12 if fp32 else 8) * max(1, 16 // cpl)
+    long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
+    per_cu = (12 if fp32 and not long_stream else 8) * max(1, 16 // cpl)
     slots = per_cu * n_cus
     parts = [int(r) for r in part_rows if r > 0] if part_rows else [distinct_rows / 8.0] * 8
     base = max(32, 32 * int(np.ceil(distinct_rows / slots / 32)))
@@ -167,12 +170,11 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
       * distinct rows: the fused kernel, fp64 the interleaved pair kernel, fp32 4 rows, bf16 1 row;
       * replicas, 3 per bundle, narrow rows (<= 8 columns per lane, d <= 512 fp64 / 1024 fp32):
         one-wave bundles with two rows per reduce-scatter (d = 256: 5.2 vs 2.3 TB/s before);
-      * replicas, fp64, 3 per bundle (AGC / cyclic s = 2): one-wave bundles, folded; the lane
-        epilogue below the long-stream regime (sharded ranks: 0.188 vs 0.195 ms at N = 8), the
-        wave-uniform one in it (the one-GPU headline: 1.316 vs 1.40 ms);
-      * fp32 with 3 replicas: one-wave bundles too (long stream 0.692 vs 0.740 ms staged; short
-        streams, the sharded ranks, 12-19 % under the staged pair bundles);
-      * replicas otherwise (R = 2, R > 3): LDS-staged bundles, the pair form for fp32 and for every
+      * replicas, fp64 / fp32, 2 or 3 per bundle (AGC / cyclic s = 2, FRC s = 1): one-wave bundles,
+        folded, lane epilogue (with the nt stream, profiles/round3/choices_nt: AGC fp64 1e6 rows
+        1.165 vs 1.199-1.217 ms wave-uniform; FRC s = 1 fp64 1.157 vs 1.315 ms LDS-staged, fp32
+        0.615 vs 0.666, 250k rows 0.303 vs 0.370);
+      * replicas otherwise (R > 3): LDS-staged bundles, the pair form for fp32 and for every
         short-stream rank (one wave per replica there);
       * bf16 replicas: MFMA bundles (d <= 1024, d % 8 == 0), else the fused kernel interleaved;
       * 2048 < d (fp64, 4096 fp32): the wide kernel; beyond 8192 / 16384 or cpl unknown: two passes.
@@ -195,10 +197,10 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     if cpl <= 8 and max_rep == 3:  # narrow rows: two rows per reduce-scatter
         return KernelChoice("multi", replicas=3, bundle_rows=pair_bundle_rows(distinct_rows, n_cus), fold=True,
                             pair=True)
-    if cpl <= 16 and max_rep == 3:
-        return KernelChoice("multi", replicas=3,
+    if cpl <= 16 and max_rep in (2, 3):
+        return KernelChoice("multi", replicas=max_rep,
                             bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl, part_rows),
-                            fold=True, lane_epi=not long_stream)
+                            fold=True, lane_epi=True)
     # more replicas than a workgroup's task slots: bundles of MAX_BUNDLE (and the remainder, padded)
     return KernelChoice("staged", replicas=min(max_rep, MAX_BUNDLE), bundle_rows=staged_bundle_rows(distinct_rows, n_cus),
                         pair=prec_code == 1 or not long_stream, wpr=0 if long_stream else 1)

@@ -351,6 +351,45 @@ def test_dense_grad_staged_bundles(native, rows, d, prec_name, pair, layout):
         np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=tol * 1e-2)
 
 
+@pytest.mark.parametrize("form", ["fold-lane", "fold-wave", "unfolded"])
+@pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
+@pytest.mark.parametrize("rows,d,prec_name", [(64, 1000, "fp64"), (37, 1000, "fp64"), (64, 1000, "fp32"),
+                                              (33, 500, "fp32")])
+def test_dense_grad_one_wave_bundles_of_two(native, rows, d, prec_name, loss, form):
+    """grad_dense_multi with bundles of 2 replicas (FRC s = 1: groups of two workers sharing two
+    partitions, the default for 2 co-located replicas): each replica's dot product, residual and
+    gradient from the shared row registers, distinct coefficients per replica, against the fp64 oracle."""
+    fold = form != "unfolded"
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(8)
+    parts, host = _parts(rng, [700, 501, 300, 64], d, prec)
+    msgs = [[(0, 1.0), (1, 1.0)], [(0, 0.5), (1, -2.0)], [(2, 1.0), (3, 1.0)], [(2, -1.0), (3, 3.0)]]
+    plan = DenseGradPlan(msgs, parts, prec, loss, d,
+                         choice=KernelChoice("multi", replicas=2, bundle_rows=rows, fold=fold,
+                                             lane_epi=form == "fold-lane"))
+    assert plan.bundle_rows == rows and plan.max_rep == 2
+    beta = torch.randn(plan.ld, dtype=prec.acc, device=DEV) * 0.05
+    G = plan.out_buffer()[0]
+    plan.native_launcher().launch(beta, G)
+    torch.cuda.synchronize()
+    bh = beta[:d].double().cpu().numpy()
+    f = logistic_grad if loss == LOGISTIC else least_squares_grad
+    tol = 1e-10 if prec_name == "fp64" else 2e-4
+    atol = tol * 1e-2 if prec_name == "fp64" else 2e-5  # fp32: coefficients up to 3 over 1.2k rows
+    for s, m in enumerate(msgs):
+        ref = sum(f(host[p][0], host[p][1], bh, c) for p, c in m)
+        np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=atol)
+
+
+def test_frc_pairs_default_to_one_wave_bundles(native):
+    """Two co-located replicas per partition (FRC s = 1) pick grad_dense_multi with R = 2."""
+    prec = get_precision("fp64")
+    rng = np.random.RandomState(3)
+    parts, _ = _parts(rng, [900, 800], 1000, prec)
+    plan = DenseGradPlan([[(0, 1.0), (1, 1.0)]] * 2, parts, prec, LOGISTIC, 1000)
+    assert plan.choice.kind == "multi" and plan.choice.replicas == 2 and plan.choice.lane_epi
+
+
 @pytest.mark.parametrize("form", ["fold-lane", "fold-wave", "fold-pair", "unfolded"])
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
 @pytest.mark.parametrize("rows,d,prec_name", [(64, 1000, "fp64"), (37, 1000, "fp64"), (256, 250, "fp64"),

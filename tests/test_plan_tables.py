@@ -53,7 +53,7 @@ def test_fold_table_groups_one_partition_per_workgroup():
 def test_multi_bundle_rows_table():
     # every folded workgroup resident at once (profiles/round3/nt_rows)
     assert [multi_bundle_rows(n) for n in (1_000_000, 500_000, 250_000, 125_000)] == [512, 256, 128, 64]
-    assert [multi_bundle_rows(n, fp32=True) for n in (1_000_000, 500_000, 250_000, 125_000)] == [352, 192, 96, 64]
+    assert [multi_bundle_rows(n, fp32=True) for n in (1_000_000, 500_000, 250_000, 125_000)] == [512, 192, 96, 64]
     assert multi_bundle_rows(1000) == 32 and multi_bundle_rows(4_000_000) == 1984
     # per-partition fold padding pushes a bundle length up until the workgroups fit the slots
     assert multi_bundle_rows(300_000) == 160 and multi_bundle_rows(300_000, part_rows=[1000] * 300) == 256
@@ -71,8 +71,8 @@ def test_kernel_selection_table():
         return choose_kernel(prec, ld, choose_cpl(ld, vec), rep, rows)
 
     # the headline (AGC W=8 s=2: bundles of 3 replicas), one GPU (1e6 distinct rows): long stream
-    assert pick(0, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=512, fold=True)
-    assert pick(1, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=352, fold=True)
+    assert pick(0, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=512, fold=True, lane_epi=True)
+    assert pick(1, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=512, fold=True, lane_epi=True)
     assert pick(2, 1000, 3, 1_000_000) == KernelChoice("mfma", replicas=3, bundle_rows=4096)
     # bf16 MFMA bundles: every workgroup (one per CU) in the first dispatch round
     assert [pick(2, 1000, 3, n).bundle_rows for n in (500_000, 250_000, 125_000, 10_000)] == [2048, 1024, 512, 256]
@@ -80,9 +80,12 @@ def test_kernel_selection_table():
     assert pick(0, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)
     assert pick(1, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)
     assert pick(1, 1000, 3, 500_000).bundle_rows == 192 and pick(1, 1000, 3, 250_000).bundle_rows == 96
-    # FRC s=1 (bundles of 2): staged, one GPU / a sharded rank
-    assert pick(0, 1000, 2, 1_000_000) == KernelChoice("staged", replicas=2, bundle_rows=512)
-    assert pick(0, 1000, 2, 250_000) == KernelChoice("staged", replicas=2, bundle_rows=128, pair=True, wpr=1)
+    # FRC s=1 (bundles of 2): one-wave bundles too, one GPU / a sharded rank
+    assert pick(0, 1000, 2, 1_000_000) == KernelChoice("multi", replicas=2, bundle_rows=512, fold=True, lane_epi=True)
+    assert pick(0, 1000, 2, 250_000) == KernelChoice("multi", replicas=2, bundle_rows=128, fold=True, lane_epi=True)
+    # more than 3 co-located replicas: LDS-staged bundles
+    assert pick(0, 1000, 4, 1_000_000) == KernelChoice("staged", replicas=4, bundle_rows=512)
+    assert pick(0, 1000, 4, 250_000) == KernelChoice("staged", replicas=4, bundle_rows=128, pair=True, wpr=1)
     # more co-located replicas than task slots per workgroup (a cyclic W = 9 table on one rank): bundles of 8
     assert pick(0, 1000, 9, 1_000_000).replicas == 8 and pick(2, 1000, 9, 1_000_000).replicas == 8
     # distinct rows (naive): the fused kernel per precision
@@ -104,8 +107,10 @@ def test_kernel_selection_table():
     # bf16 beyond the MFMA tile: the fused kernel, replica-interleaved
     assert pick(2, 2000, 3, 1_000_000) == KernelChoice("fused", rows=1, interleave=True)
     # the regime boundary is a rows-per-CU rule, not a row count: 4x the CUs -> 4x the rows
-    assert pick(0, 1000, 3, 700_000).lane_epi and not pick(0, 1000, 3, 800_000).lane_epi
-    assert choose_kernel(0, 1000, 16, 3, 2_800_000, n_cus=1024).lane_epi
+    assert pick(0, 1000, 4, 700_000).pair and not pick(0, 1000, 4, 800_000).pair
+    assert choose_kernel(0, 1000, 16, 4, 2_800_000, n_cus=1024).pair
+    # fp32 one-wave bundles: 12 per CU below the long-stream regime, 8 in it
+    assert pick(1, 1000, 3, 700_000).bundle_rows == 256 and pick(1, 1000, 3, 800_000).bundle_rows == 416
 
 
 def test_no_tuning_env_knobs_left():

@@ -164,9 +164,10 @@ def sweep_cases(out, ds=(256, 1000, 2048, 4096), ns=(100_000, 1_000_000, 4_000_0
 
 def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000), ("fp64", 256, 100_000),
                                 ("fp64", 4096, 1_000_000), ("fp32", 4096, 1_000_000), ("fp32", 2048, 1_000_000),
-                                ("fp64", 1000, 100_000))):
-    """Every valid KernelChoice on the replica-bundle (agc) layout of a few shapes: the candidates
-    behind choose_kernel's table (tests/test_plan_tables.py pins the picks)."""
+                                ("fp64", 1000, 100_000)), layout: str = "agc"):
+    """Every valid KernelChoice on the replica-bundle layout of a few shapes: the candidates
+    behind choose_kernel's table (tests/test_plan_tables.py pins the picks).  layout agc: the
+    headline's uneven AGC groups (3 replicas); frc2: FRC s = 1 (4 groups of 2 workers x 2 partitions)."""
     import dataclasses
 
     import torch
@@ -175,7 +176,9 @@ def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000)
     from erasurehead_amd.ops import DenseGradPlan, get_precision
     from erasurehead_amd.ops.grad import KernelChoice
 
-    msgs = [[0, 1, 2]] * 3 + [[3, 4, 5]] * 3 + [[6, 7]] * 2
+    msgs = ([[0, 1, 2]] * 3 + [[3, 4, 5]] * 3 + [[6, 7]] * 2 if layout == "agc" else
+            [[2 * g, 2 * g + 1] for g in range(4) for _ in range(2)])
+    R = 3 if layout == "agc" else 2
     for prec_name, d, n in shapes:
         prec = get_precision(prec_name)
         rpp = n // 8
@@ -184,12 +187,12 @@ def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000)
         beta = torch.randn(prec.ld(d), device="cuda", dtype=prec.acc) * 0.01
         distinct = 8 * parts[0][0].numel() * parts[0][0].element_size() / 1e12
         cands = [KernelChoice("fused", rows=r, interleave=i) for r in (1, 2, 4) for i in (False, True)]
-        cands += [KernelChoice("multi", replicas=3, bundle_rows=b, fold=True, lane_epi=e)
+        cands += [KernelChoice("multi", replicas=R, bundle_rows=b, fold=True, lane_epi=e)
                   for b in (32, 64, 128, 192, 256, 512, 768) for e in (False, True)]
-        cands += [KernelChoice("multi", replicas=3, bundle_rows=b, fold=True, pair=True)
+        cands += [KernelChoice("multi", replicas=R, bundle_rows=b, fold=True, pair=True)
                   for b in (32, 64, 128, 192, 256, 512, 768)]
-        cands += [KernelChoice("staged", replicas=3, bundle_rows=b, pair=p, wpr=w)
-                  for b in (128, 512) for p in (False, True) for w in (0, 1)]
+        cands += [KernelChoice("staged", replicas=R, bundle_rows=b, pair=p, wpr=w)
+                  for b in (128, 256, 512) for p in (False, True) for w in (0, 1)]
         cands += [KernelChoice("wide", interleave=i) for i in (False, True)]
         cands += [KernelChoice("wide", replicas=3, bundle_rows=b) for b in (16, 32, 64, 128, 256, 976)]
         default = None
@@ -205,7 +208,7 @@ def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000)
                 continue
             if c is None:
                 default = plan.choice
-            r = {"kernel": "grad_dense_choice", "precision": prec_name, "d": d, "n": n,
+            r = {"kernel": "grad_dense_choice", "layout": layout, "precision": prec_name, "d": d, "n": n,
                  "choice": dataclasses.asdict(plan.choice), "label": plan.choice.label(), "default": c is None,
                  "ms": ms, "distinct_TBps": distinct / ms * 1e3}
             out.append(r)
@@ -268,6 +271,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "kernels.jsonl"))
     ap.add_argument("--shapes", default=None, help="--only choices: prec:d:n,... (default: the built-in list)")
+    ap.add_argument("--layout", default="agc", choices=["agc", "frc2"], help="--only choices: replica layout")
     ap.add_argument("--only", choices=["dense", "sparse", "scale", "eval", "sweep", "choices"], default=None)
     a = ap.parse_args()
     out = []
@@ -281,9 +285,10 @@ def main():
         sweep_cases(out)
     if a.only == "choices":
         if a.shapes:
-            choice_cases(out, [(p, int(d), int(float(n))) for p, d, n in (x.split(":") for x in a.shapes.split(","))])
+            choice_cases(out, [(p, int(d), int(float(n))) for p, d, n in (x.split(":") for x in a.shapes.split(","))],
+                         layout=a.layout)
         else:
-            choice_cases(out)
+            choice_cases(out, layout=a.layout)
     if a.only in (None, "sparse"):
         sparse_cases(out)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
