@@ -6,10 +6,11 @@
 //
 // One workgroup of 1024 threads (one column each at d <= 1024, so the combine is a couple of
 // batches of independent message loads).  Wave 0 polls the workers' shared 64-bit round counters (one
-// lane per worker rank, system-scope acquire loads of host memory); thread 0 keeps the
-// collector's books in LDS.  Probes that complete in the same poll are ordered by the round's
-// tie permutation, then by probe id, exactly like Collector::process_ready for delay-free
-// rounds (csrc/runtime/collector.cpp), so a replay of the logged arrivals reproduces the update.
+// lane per worker rank, system-scope acquire loads of host memory) and keeps the collector's books
+// wave-parallel (one lane per probe of a poll: rank sort, prefix-summed stop-rule counts).  Probes
+// that complete in the same poll are ordered by the round's tie permutation, then by probe id,
+// exactly like Collector::process_ready for delay-free rounds (csrc/runtime/collector.cpp), so a
+// replay of the logged arrivals reproduces the update.
 // Every spin has a deadline (a.deadline_ticks): a round that times out sets a.abort, skips its
 // update and its broadcast, and every later arbiter returns at once, so the grid always drains.
 #include "arbiter.h"
@@ -35,12 +36,35 @@ __device__ __forceinline__ unsigned long long load_counter(const unsigned long l
   return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Inclusive prefix sum over the wave (every lane active).
+__device__ __forceinline__ int wave_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const int u = __shfl_up(v, dd, 64);
+    if (lane >= dd) v += u;
+  }
+  return v;
+}
+// Bitwise OR over the wave (every lane active); every lane ends with the result.
+__device__ __forceinline__ unsigned long long wave_or(unsigned long long v) {
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const unsigned lo = __shfl_xor(static_cast<unsigned>(v), dd, 64);
+    const unsigned hi = __shfl_xor(static_cast<unsigned>(v >> 32), dd, 64);
+    v |= static_cast<unsigned long long>(hi) << 32 | lo;
+  }
+  return v;
+}
+
 }  // namespace
 
 template <typename M>
 __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, int check_prev) {
   __shared__ int s_pw[kArbMaxProbes], s_pp[kArbMaxProbes], s_ps[kArbMaxProbes];
   __shared__ int batch[kArbMaxProbes];
+  __shared__ int s_bkey[kArbMaxProbes], s_sorted[kArbMaxProbes];  // a poll's batch: tie ranks, sorted messages
+  __shared__ int s_gfirst[kArbMaxW];
   __shared__ int got_sh[2 * kArbMaxW];
   // the round's tables in LDS: thread 0's books and decode walk them serially (a dependent global load
   // per step cost ~15 us per round)
@@ -98,54 +122,89 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
   if (tid < 64) {
     const long long t0 = wall_clock64();
     const unsigned long long all_src = a.nsrc >= 64 ? ~0ull : ((1ull << a.nsrc) - 1);
-    unsigned long long got0 = 0, got1 = 0, gdone = 0;
-    int cnt0 = 0, cnt1 = 0, cntg = 0, stopped = 0;
+    const unsigned long long below = tid == 0 ? 0ull : (~0ull >> (64 - tid));  // lanes under this one
+    // the collector's books, wave-uniform (every lane holds the same values)
+    unsigned long long got0 = 0, gdone = 0;
+    int cnt0 = 0, cnt1 = 0, cntg = 0, stopped = 0, narr = 0;
     for (int it = 0;; ++it) {
       const long long t = wall_clock64();
       const bool mine = tid < a.nsrc && !(seen >> tid & 1) && load_counter(reinterpret_cast<const unsigned long long*>(a.src_flag[tid])) >= static_cast<unsigned long long>(i + 1);
       const unsigned long long nm = __ballot(mine);
       if (it == 0 || nm) {
-        if (tid == 0) {
-          int nb = 0;
-          for (int q = 0; q < a.nprobe; ++q) {
+        // (a) this poll's batch: its probes in probe-id order (the local ones on the first poll)
+        int nb = 0;
+        for (int q0 = 0; q0 < a.nprobe; q0 += 64) {
+          const int q = q0 + tid;
+          bool in = false;
+          if (q < a.nprobe) {
             const int s = s_ps[q];
-            if ((s < 0 && it == 0) || (s >= 0 && (nm >> s & 1))) batch[nb++] = q;
+            in = (s < 0 && it == 0) || (s >= 0 && (nm >> s & 1));
           }
-          for (int x = 1; x < nb; ++x) {  // (tie rank, probe id) order
-            const int q = batch[x];
-            const int kq = s_key[q];
-            int y = x - 1;
-            while (y >= 0 && (s_key[batch[y]] > kq || (s_key[batch[y]] == kq && batch[y] > q))) {
-              batch[y + 1] = batch[y];
-              --y;
+          const unsigned long long m = __ballot(in);
+          if (in) {
+            const int x = nb + __popcll(m & below);
+            batch[x] = q;
+            s_bkey[x] = s_key[q];
+          }
+          nb += __popcll(m);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // (b) (tie rank, probe id) order: the batch is in probe-id order, so an element's place is the
+        // number of elements with a smaller tie rank plus the earlier ones with its own
+        for (int x0 = 0; x0 < nb; x0 += 64) {
+          const int x = x0 + tid;
+          if (x < nb) {
+            const int kx = s_bkey[x];
+            int pos = 0;
+            for (int y = 0; y < nb; ++y) {
+              const int ky = s_bkey[y];
+              pos += (ky < kx || (ky == kx && y < x)) ? 1 : 0;
             }
-            batch[y + 1] = q;
-          }
-          for (int x = 0; x < nb; ++x) {
             const int q = batch[x];
-            const int w = s_pw[q], p = s_pp[q];
-            const int mi = 2 * w + p;
-            if (++got_sh[mi] < s_nsh[mi] || stopped) continue;  // more shards to come / late
-            arr_w[s_narr] = w;
-            arr_p[s_narr] = p;
-            arr_t[s_narr] = t;
-            ++s_narr;
-            if (p == 0) {
-              if (!(got0 >> w & 1)) {
-                got0 |= 1ull << w;
-                ++cnt0;
-                const int g = s_group[w];
-                if (!(gdone >> g & 1)) {
-                  gdone |= 1ull << g;
-                  ++cntg;
-                }
-              }
-            } else if (!(got1 >> w & 1)) {
-              got1 |= 1ull << w;
-              ++cnt1;
-            }
-            if (rule_holds(a.rule, a.k, a.W, a.n_groups, cnt0, cnt1, cntg)) stopped = 1;
+            s_sorted[pos] = 2 * s_pw[q] + s_pp[q];
           }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // (c) the books in that order, 64 elements at a time.  An element completes its message when
+        // the shards counted before plus the earlier elements of the same message reach nsh; the
+        // completions are the arrivals, the stop rule's counts are prefix sums over them, and the
+        // first arrival at which the rule holds is the last one recorded (later ones are late).
+        for (int j0 = 0; j0 < nb && !stopped; j0 += 64) {
+          const int j = j0 + tid;
+          const bool valid = j < nb;
+          const int mi = valid ? s_sorted[j] : 0;
+          int before = 0;
+          const int jend = min(j0 + 64, nb);
+          for (int y = j0; y < jend; ++y) before += (y < j && s_sorted[y] == mi) ? 1 : 0;
+          const int prev = valid ? got_sh[mi] : 0;
+          for (int gg = tid; gg < kArbMaxW; gg += 64) s_gfirst[gg] = 64;
+          __builtin_amdgcn_wave_barrier();
+          if (valid) atomicAdd(&got_sh[mi], 1);
+          const bool comp = valid && prev + before + 1 == s_nsh[mi];
+          const int w = mi >> 1, p = mi & 1;
+          const int g = s_group[w];
+          const bool a0 = comp && p == 0, a1 = comp && p == 1;
+          if (a0) atomicMin(&s_gfirst[g], tid);
+          __builtin_amdgcn_wave_barrier();
+          const bool gf = a0 && !(gdone >> g & 1) && s_gfirst[g] == tid;  // its group's first p = 0 arrival
+          const int c0 = cnt0 + wave_scan(a0 ? 1 : 0), c1 = cnt1 + wave_scan(a1 ? 1 : 0), cg = cntg + wave_scan(gf ? 1 : 0);
+          const unsigned long long hm = __ballot(comp && rule_holds(a.rule, a.k, a.W, a.n_groups, c0, c1, cg));
+          const int last = hm ? __ffsll(hm) - 1 : 63;
+          const bool rec = comp && tid <= last;
+          const unsigned long long rm = __ballot(rec);
+          if (rec) {
+            const int x = narr + __popcll(rm & below);
+            arr_w[x] = w;
+            arr_p[x] = p;
+            arr_t[x] = t;
+          }
+          narr += __popcll(rm);
+          cnt0 += __popcll(__ballot(rec && p == 0));
+          cnt1 += __popcll(__ballot(rec && p == 1));
+          cntg += __popcll(__ballot(rec && gf));
+          got0 |= wave_or((rec && p == 0) ? 1ull << w : 0ull);
+          gdone |= wave_or((rec && gf) ? 1ull << g : 0ull);
+          if (hm) stopped = 1;
         }
         seen |= nm;
       }
@@ -165,7 +224,10 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
     const unsigned long long mask = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(got0)) |
                                     static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(
                                         static_cast<unsigned>(got0 >> 32))) << 32;
-    if (tid == 0) s_mask = mask;
+    if (tid == 0) {
+      s_mask = mask;
+      s_narr = narr;
+    }
     if ((a.decode == 3 || a.decode == 4) && a.table)
       for (int w = tid; w < a.W; w += 64)
         s_trow[w] = (mask >> w & 1) ? a.table[static_cast<long long>(mask) * a.W + w] : 0.0;

@@ -120,14 +120,17 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
     per_cu = (12 if fp32 and not long_stream else 8) * max(1, 16 // cpl)
     slots = per_cu * n_cus
     parts = [int(r) for r in part_rows if r > 0] if part_rows else [distinct_rows / 8.0] * 8
-    base = max(32, 32 * int(np.ceil(distinct_rows / slots / 32)))
+    per = distinct_rows / slots
+    # small problems: bundles down to 8 rows (a wave with one row ahead streams ~1.4 us per row, so a
+    # 32-row bundle alone is ~45 us: 4000 x 1000 fp64 rows over 2 ranks took 46 us per gradient)
+    base = 32 * int(np.ceil(per / 32)) if per > 16 else max(8, 8 * int(np.ceil(per / 8)))
 
     def fits(rows: int) -> bool:
         return sum(4 * int(np.ceil(np.ceil(p / rows) / 4)) for p in parts) <= slots
 
     rows = base
     while not fits(rows) and rows < max(parts):
-        rows += 32
+        rows += 32 if rows >= 32 else 8
     return rows if fits(rows) else base  # more partitions than slots: short bundles keep the tail short
 
 

@@ -11,7 +11,7 @@ from erasurehead_amd.data.source import ArraySource
 from erasurehead_amd.engine import Trainer, evaluate
 from erasurehead_amd.models.losses import LEAST_SQUARES, LOGISTIC, logistic_loss, roc_auc
 from erasurehead_amd.parallel.dist import DistEnv
-from oracle import replay
+from oracle import replay, stops_exactly_at_last
 
 CASES = [  # key args: (is_coded, partitions, coded_ver, n_procs, s, num_collect)
     (0, 0, 0, 5, 0, 0),
@@ -51,6 +51,7 @@ def test_engine_matches_numpy_replay(case, rule):
     res = tr.run()
     ref = replay(sch, parts, tr.beta0, res.arrivals, rule, cfg.alpha_value, cfg.n_rows, cfg.eta())
     np.testing.assert_allclose(res.betaset, ref, rtol=1e-10, atol=1e-12)
+    assert stops_exactly_at_last(sch, res.arrivals)  # the collector's stop rule, independently re-derived
     assert res.timeset.shape == (6,) and np.all(res.timeset > 0)
     assert res.worker_timeset.shape == (6, cfg.n_workers)
 

@@ -94,7 +94,7 @@ def test_device_arbiter_rounds(world, case_i, wait, drain, tmp_path):
     workers' counters, applies the stop rule, decodes, updates and releases the next beta): the
     trajectory replays exactly from the arrivals it logged (FRC, AGC, uneven AGC groups, naive; and
     with a drain, the cyclic-MDS decode table, partial replication and partial coded)."""
-    from oracle import replay
+    from oracle import replay, stops_exactly_at_last
     from test_engine_cpu import CASES, make
 
     extra = {"EH_TEST_DRAIN": drain} if drain else {}
@@ -104,6 +104,7 @@ def test_device_arbiter_rounds(world, case_i, wait, drain, tmp_path):
     cfg, src, sch, parts = make(CASES[case_i], "AGD")
     arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
     assert all(len(a) for a in arrivals)
+    assert stops_exactly_at_last(sch, arrivals)  # the wave-parallel books: no late arrival logged, no early stop
     ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
     assert np.all(r["timeset"] > 0)

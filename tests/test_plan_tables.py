@@ -54,7 +54,7 @@ def test_multi_bundle_rows_table():
     # every folded workgroup resident at once (profiles/round3/nt_rows)
     assert [multi_bundle_rows(n) for n in (1_000_000, 500_000, 250_000, 125_000)] == [512, 256, 128, 64]
     assert [multi_bundle_rows(n, fp32=True) for n in (1_000_000, 500_000, 250_000, 125_000)] == [512, 192, 96, 64]
-    assert multi_bundle_rows(1000) == 32 and multi_bundle_rows(4_000_000) == 1984
+    assert multi_bundle_rows(1000) == 8 and multi_bundle_rows(30_000) == 16 and multi_bundle_rows(4_000_000) == 1984
     # per-partition fold padding pushes a bundle length up until the workgroups fit the slots
     assert multi_bundle_rows(300_000) == 160 and multi_bundle_rows(300_000, part_rows=[1000] * 300) == 256
     assert multi_bundle_rows(300_000, part_rows=[100] * 3000) == 160  # can never fit: the plain length

@@ -2,13 +2,13 @@
 # so the round time is mostly messaging + arbiter / host pump; 2 and 8 ranks, arbiter off / on.
 #   gpurun -- bash tools/probes/overhead_tiny.sh   (writes gpurun_out/overhead/)
 set -o pipefail
-O=gpurun_out/overhead
+O=gpurun_out/overhead${TAG:-}
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 300 python -u bench.py --precision bf16 --no-floor --json-out $O/bf16.json > $O/bf16.log 2>&1 || exit 1
-for n in 2 8; do
+for n in ${RANKS:-2 8}; do
   for m in off on; do
-    ERASUREHEAD_DEVICE_MASTER=$m timeout -k 10 300 python -u bench.py --gpus $n --steps 200 --warmup 20 --no-floor --n-rows 16000 --n-cols 1000 --json-out $O/tiny_${n}_$m.json > $O/tiny_${n}_$m.log 2>&1 || exit 1
+    ERASUREHEAD_DEVICE_MASTER=$m timeout -k 10 300 python -u bench.py --gpus $n --steps 200 --warmup 20 --no-floor --n-rows ${NROWS:-16000} --n-cols 1000 --json-out $O/tiny_${n}_$m.json > $O/tiny_${n}_$m.log 2>&1 || exit 1
   done
 done
 echo done
