@@ -11,7 +11,8 @@ each run ends, so a long matrix keeps the remote runner's liveness check fed.
 
 A run spec is 'label | environment assignments | bench.py arguments'.  Each output line holds the
 label, the environment, the arguments, the repetition, the wall time and the bench JSON (or the
-error tail).  `--summary` prints label -> ms_per_step (median over repetitions) at the end.
+error tail).  `--summary` prints label -> ms_per_step (median over repetitions) at the end;
+`python tools/ab.py --table FILE` prints the per-label medians of a finished jsonl.
 """
 from __future__ import annotations
 
@@ -58,7 +59,34 @@ def run_one(label, env, args, rep, timeout):
     return rec
 
 
+def table(path: str) -> None:
+    """Per label of an ab.py jsonl: medians of ms/step, of the per-round phase ticks and of rank 0's
+    arbiter / pump microseconds (was tools/ab_table.py)."""
+    from collections import defaultdict
+
+    rows = defaultdict(lambda: defaultdict(list))
+    for line in open(path):
+        r = json.loads(line)
+        b = r.get("bench")
+        if not b:
+            continue
+        d = rows[r["label"]]
+        d["ms"].append(b["ms_per_step"])
+        for k, v in (b.get("phases_us") or {}).items():
+            d[k].append(v)
+        r0 = (b.get("ranks") or [{}])[0]
+        for k in ("arbiter_poll_us", "arbiter_update_us", "release_us", "decode_update_us", "put_beta_us"):
+            if k in r0:
+                d["r0." + k].append(r0[k])
+    for label, d in rows.items():
+        print(label.ljust(22), "  ".join(f"{k}={statistics.median(v):.4g}" for k, v in d.items()))
+
+
 def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
+    if argv[:1] == ["--table"]:  # python tools/ab.py --table FILE
+        table(argv[1])
+        return 0
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--out", required=True)
     ap.add_argument("--run", action="append", default=[], help="'label | ENV=v ... | bench args'")
