@@ -187,7 +187,7 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     shared = max_rep > 1
     if cpl >= 256:
         if shared and cpl == 256 and max_rep <= 3:
-            return KernelChoice("wide", replicas=max_rep, bundle_rows=wide_bundle_rows(distinct_rows, n_cus))
+            return KernelChoice("wide", replicas=max_rep, bundle_rows=wide_bundle_rows(distinct_rows, n_cus, part_rows))
         return KernelChoice("wide", interleave=shared)
     if not shared:
         return KernelChoice("fused", rows={0: 2, 1: 4, 2: 1}[prec_code])
@@ -209,10 +209,22 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
                         pair=prec_code == 1 or not long_stream, wpr=0 if long_stream else 1)
 
 
-def wide_bundle_rows(distinct_rows: int, n_cus: int = N_CUS) -> int:
-    """Rows per wide-row replica bundle (one 256-thread workgroup, 2 resident per CU): about 4
-    bundles per CU, multiples of 16 rows."""
-    return max(16, 16 * int(round(distinct_rows / (4 * n_cus) / 16)))
+def wide_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional[Sequence[int]] = None) -> int:
+    """Rows per wide-row replica bundle (one 256-thread workgroup per bundle, 2 resident per CU): the
+    shortest multiple of 16 rows whose bundles (per partition) all start in the first dispatch round,
+    the rule of multi_bundle_rows.  The earlier "about 4 bundles per CU" sizing put 1032 bundles of
+    976 rows on 1024 slot-rounds at 1e6 rows (a third, near-empty round) and 1042 of 96 rows at 1e5."""
+    slots = 2 * n_cus
+    parts = [int(r) for r in part_rows if r > 0] if part_rows else [distinct_rows / 8.0] * 8
+    base = max(16, 16 * int(np.ceil(distinct_rows / slots / 16)))
+
+    def fits(rows: int) -> bool:
+        return sum(int(np.ceil(p / rows)) for p in parts) <= slots
+
+    rows = base
+    while not fits(rows) and rows < max(parts):
+        rows += 16
+    return rows if fits(rows) else base
 
 
 WIDE_EPT = {2: 16, 4: 32, 8: 32}  # elements per thread per row of grad_dense_wide (by vector width)

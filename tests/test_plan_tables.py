@@ -93,8 +93,8 @@ def test_kernel_selection_table():
                                                                    KernelChoice("fused", rows=1)]
     # wide rows: d = 2048 fp64 (32 columns per lane) stays on staged bundles; 4096 takes the wide kernel
     assert pick(0, 2048, 3, 1_000_000).kind == "staged"
-    assert pick(0, 4096, 3, 1_000_000) == KernelChoice("wide", replicas=3, bundle_rows=976)
-    assert pick(1, 4096, 2, 100_000) == KernelChoice("wide", replicas=2, bundle_rows=96)
+    assert pick(0, 4096, 3, 1_000_000) == KernelChoice("wide", replicas=3, bundle_rows=1968)
+    assert pick(1, 4096, 2, 100_000) == KernelChoice("wide", replicas=2, bundle_rows=208)
     assert pick(0, 8192, 3, 1_000_000) == KernelChoice("wide", interleave=True)  # 512-thread rows: no bundles
     # narrow rows: one-wave bundles with two rows per reduce-scatter, ~16 bundles per CU
     assert pick(0, 256, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=256, fold=True, pair=True)
