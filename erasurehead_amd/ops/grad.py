@@ -157,10 +157,16 @@ def mfma_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional
     return rows
 
 
-def staged_bundle_rows(distinct_rows: int, n_cus: int = N_CUS) -> int:
-    """Rows per LDS-staged bundle: 512 in the long-stream regime (measured 512 > 256, 1024; 2048 leaves
-    CUs idle), 128 below it (profiles/round2/s1_shapes: N=8 0.238 vs 0.415 ms, N=2 0.80 vs 0.99 ms at 512)."""
-    return 512 if distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus else 128
+def staged_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, fp32: bool = False, cpl: int = 16) -> int:
+    """Rows per LDS-staged bundle.  Long streams: 512 fp64, 384 fp32; short streams: 256 for rows of
+    32 columns per lane (d = 1025..2048), else 128.  Measured with the nt stream, pair form
+    (profiles/round3/choices_nt/staged.jsonl, d = 2048, 3 replicas): fp64 1e6 rows 512: 2.676 ms
+    (496: 2.624, 1024: 2.629; the old non-pair default 2.751), fp32 1e6 384: 1.377 (512: 1.485),
+    fp64 1e5 256: 0.326 (128: 0.334-0.376); d = 1000 ranks (round 2, profiles/round2/s1_shapes):
+    128 at N = 8 (0.238 vs 0.415 ms at 512)."""
+    if distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus:
+        return 384 if fp32 else 512
+    return 256 if cpl >= 32 else 128
 
 
 def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, distinct_rows: int,
@@ -177,8 +183,9 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
         folded, lane epilogue (with the nt stream, profiles/round3/choices_nt: AGC fp64 1e6 rows
         1.165 vs 1.199-1.217 ms wave-uniform; FRC s = 1 fp64 1.157 vs 1.315 ms LDS-staged, fp32
         0.615 vs 0.666, 250k rows 0.303 vs 0.370);
-      * replicas otherwise (R > 3): LDS-staged bundles, the pair form for fp32 and for every
-        short-stream rank (one wave per replica there);
+      * replicas otherwise (R > 3, or rows of 32 columns per lane): LDS-staged bundles, the pair form
+        (two rows per reduction) for fp32, short streams and 32-column rows (d = 2048 fp64 long
+        stream with the nt stream: 2.676 vs 2.751 ms);
       * bf16 replicas: MFMA bundles (d <= 1024, d % 8 == 0), else the fused kernel interleaved;
       * 2048 < d (fp64, 4096 fp32): the wide kernel; beyond 8192 / 16384 or cpl unknown: two passes.
     """
@@ -205,8 +212,9 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
                             bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl, part_rows),
                             fold=True, lane_epi=True)
     # more replicas than a workgroup's task slots: bundles of MAX_BUNDLE (and the remainder, padded)
-    return KernelChoice("staged", replicas=min(max_rep, MAX_BUNDLE), bundle_rows=staged_bundle_rows(distinct_rows, n_cus),
-                        pair=prec_code == 1 or not long_stream, wpr=0 if long_stream else 1)
+    return KernelChoice("staged", replicas=min(max_rep, MAX_BUNDLE),
+                        bundle_rows=staged_bundle_rows(distinct_rows, n_cus, prec_code == 1, cpl),
+                        pair=prec_code == 1 or not long_stream or cpl >= 32, wpr=0 if long_stream else 1)
 
 
 def wide_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional[Sequence[int]] = None) -> int:

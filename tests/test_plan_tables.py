@@ -91,8 +91,10 @@ def test_kernel_selection_table():
     # distinct rows (naive): the fused kernel per precision
     assert [pick(p, 1000, 1, 1_000_000) for p in (0, 1, 2)] == [KernelChoice("fused", rows=2), KernelChoice("fused", rows=4),
                                                                    KernelChoice("fused", rows=1)]
-    # wide rows: d = 2048 fp64 (32 columns per lane) stays on staged bundles; 4096 takes the wide kernel
-    assert pick(0, 2048, 3, 1_000_000).kind == "staged"
+    # wide rows: d = 2048 fp64 (32 columns per lane) stays on staged bundles (pair form); 4096 takes the wide kernel
+    assert pick(0, 2048, 3, 1_000_000) == KernelChoice("staged", replicas=3, bundle_rows=512, pair=True)
+    assert pick(1, 2048, 3, 1_000_000) == KernelChoice("staged", replicas=3, bundle_rows=384, pair=True)
+    assert pick(0, 2048, 3, 100_000) == KernelChoice("staged", replicas=3, bundle_rows=256, pair=True, wpr=1)
     assert pick(0, 4096, 3, 1_000_000) == KernelChoice("wide", replicas=3, bundle_rows=1968)
     assert pick(1, 4096, 2, 100_000) == KernelChoice("wide", replicas=2, bundle_rows=208)
     assert pick(0, 8192, 3, 1_000_000) == KernelChoice("wide", interleave=True)  # 512-thread rows: no bundles

@@ -192,7 +192,7 @@ def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000)
         cands += [KernelChoice("multi", replicas=R, bundle_rows=b, fold=True, pair=True)
                   for b in (32, 64, 128, 192, 256, 512, 768)]
         cands += [KernelChoice("staged", replicas=R, bundle_rows=b, pair=p, wpr=w)
-                  for b in (128, 256, 512) for p in (False, True) for w in (0, 1)]
+                  for b in (64, 128, 192, 256, 384, 496, 512, 768, 1024) for p in (False, True) for w in (0, 1)]
         cands += [KernelChoice("wide", interleave=i) for i in (False, True)]
         cands += [KernelChoice("wide", replicas=R, bundle_rows=b) for b in (64, 128, 192, 208, 256, 512, 976, 1968)]
         default = None
