@@ -158,15 +158,15 @@ def mfma_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional
 
 
 def staged_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, fp32: bool = False, cpl: int = 16) -> int:
-    """Rows per LDS-staged bundle.  Long streams: 512 fp64, 384 fp32; short streams: 256 for rows of
-    32 columns per lane (d = 1025..2048), else 128.  Measured with the nt stream, pair form
+    """Rows per LDS-staged bundle.  Long streams: 512 fp64, 384 fp32; short streams: 256 for fp64 rows
+    of 32 columns per lane (d = 1025..2048, 16 KB rows), else 128.  Measured with the nt stream, pair form
     (profiles/round3/choices_nt/staged.jsonl, d = 2048, 3 replicas): fp64 1e6 rows 512: 2.676 ms
     (496: 2.624, 1024: 2.629; the old non-pair default 2.751), fp32 1e6 384: 1.377 (512: 1.485),
     fp64 1e5 256: 0.326 (128: 0.334-0.376); d = 1000 ranks (round 2, profiles/round2/s1_shapes):
     128 at N = 8 (0.238 vs 0.415 ms at 512)."""
     if distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus:
         return 384 if fp32 else 512
-    return 256 if cpl >= 32 else 128
+    return 256 if cpl >= 32 and not fp32 else 128  # 16 KB rows (fp64 d > 1024); fp32 2048 at 1e5: 128 rows 0.169 vs 256 0.194 ms
 
 
 def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, distinct_rows: int,
