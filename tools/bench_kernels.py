@@ -190,7 +190,7 @@ def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000)
         cands += [KernelChoice("multi", replicas=R, bundle_rows=b, fold=True, lane_epi=e)
                   for b in (32, 64, 128, 192, 256, 512, 768) for e in (False, True)]
         cands += [KernelChoice("multi", replicas=R, bundle_rows=b, fold=True, pair=True)
-                  for b in (32, 64, 128, 192, 256, 512, 768)]
+                  for b in (8, 16, 32, 64, 128, 192, 256, 512, 768)]
         cands += [KernelChoice("staged", replicas=R, bundle_rows=b, pair=p, wpr=w)
                   for b in (64, 128, 192, 256, 384, 496, 512, 768, 1024) for p in (False, True) for w in (0, 1)]
         cands += [KernelChoice("wide", interleave=i) for i in (False, True)]
