@@ -134,15 +134,16 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
     return rows if fits(rows) else base  # more partitions than slots: short bundles keep the tail short
 
 
-def pair_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, fp32: bool = False) -> int:
+def pair_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, fp32: bool = False, cpl: int = 8) -> int:
     """Rows per narrow-row (cpl <= 8) one-wave bundle with the pair-row epilogue: about 16 bundles
-    (4 folded workgroups) per CU for fp64, 64 for fp32 (half the registers per row, so twice the
-    waves per SIMD, and each wave's rows are half the bytes), the power of two nearest to that,
-    8..512 rows.  Measured (profiles/round3/choices/choices_pair_rows.jsonl, round3/choices_nt/
-    narrow.jsonl): d = 256 fp64 1e6 rows 256-row bundles 5.3 TB/s (128: 5.3, 512: 4.7), 1e5 rows
-    32-row 4.1; fp32 1e6 rows 64-row 5.05 TB/s (256: 4.5); d = 512 fp64 / fp32 1e6 rows 5.8 / 5.6."""
-    per = max(1.0, distinct_rows / ((64 if fp32 else 16) * n_cus))
-    return int(min(512, max(8 if fp32 else 32, 2 ** round(np.log2(per)))))
+    (4 folded workgroups) per CU, 64 for fp32 rows of <= 4 columns per lane (1 KB rows: far fewer
+    registers, so more waves per SIMD), the power of two nearest to that, 8..512 rows.  Measured
+    (profiles/round3/choices/choices_pair_rows.jsonl, round3/choices_nt/narrow*.jsonl): d = 256
+    fp64 1e6 rows 256-row bundles 5.3 TB/s (128: 5.3, 512: 4.7), 1e5 rows 32-row 4.1; fp32 d = 256
+    1e6 rows 64-row 5.05 (128: 5.1, 256: 4.5), 1e5 8 / 16 / 32 rows equal; fp32 d = 512 1e6 rows
+    256-row 5.9 (64: 5.2)."""
+    per = max(1.0, distinct_rows / ((64 if fp32 and cpl <= 4 else 16) * n_cus))
+    return int(min(512, max(8 if fp32 and cpl <= 4 else 32, 2 ** round(np.log2(per)))))
 
 
 def mfma_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional[Sequence[int]] = None) -> int:
@@ -207,7 +208,7 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
                                 bundle_rows=mfma_bundle_rows(distinct_rows, n_cus, part_rows))
         return KernelChoice("fused", rows=1, interleave=True)
     if cpl <= 8 and max_rep == 3:  # narrow rows: two rows per reduce-scatter
-        return KernelChoice("multi", replicas=3, bundle_rows=pair_bundle_rows(distinct_rows, n_cus, prec_code == 1),
+        return KernelChoice("multi", replicas=3, bundle_rows=pair_bundle_rows(distinct_rows, n_cus, prec_code == 1, cpl),
                             fold=True,
                             pair=True)
     if cpl <= 16 and max_rep in (2, 3):

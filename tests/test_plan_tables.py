@@ -103,6 +103,7 @@ def test_kernel_selection_table():
     assert pick(1, 256, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, pair=True)
     assert pick(1, 256, 3, 100_000).bundle_rows == 8
     assert pick(0, 512, 3, 1_000_000).pair and pick(1, 512, 3, 1_000_000).pair  # cpl 8
+    assert pick(1, 512, 3, 1_000_000).bundle_rows == 256
     assert pick(0, 256, 3, 100_000).bundle_rows == 32 and pick(0, 256, 3, 4_000_000).bundle_rows == 512
     assert not pick(1, 1000, 3, 1_000_000).pair  # cpl 16: four row buffers would not fit
     assert pick(0, 4096, 1, 1_000_000) == KernelChoice("wide")
