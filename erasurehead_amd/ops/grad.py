@@ -161,14 +161,15 @@ def mfma_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional
 
 
 def staged_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, fp32: bool = False, cpl: int = 16) -> int:
-    """Rows per LDS-staged bundle.  Long streams: 512 fp64, 384 fp32; short streams: 256 for fp64 rows
-    of 32 columns per lane (d = 1025..2048, 16 KB rows), else 128.  Measured with the nt stream, pair form
+    """Rows per LDS-staged bundle.  Long streams: 512, 384 for fp32 rows of 32 columns per lane (4
+    replicas at d = 1000 fp32: 496-512 rows 0.78-0.80 ms vs 384 0.80-0.84); short streams: 256 for
+    fp64 rows of 32 columns per lane (d = 1025..2048, 16 KB rows), else 128.  Measured with the nt stream, pair form
     (profiles/round3/choices_nt/staged.jsonl, d = 2048, 3 replicas): fp64 1e6 rows 512: 2.676 ms
     (496: 2.624, 1024: 2.629; the old non-pair default 2.751), fp32 1e6 384: 1.377 (512: 1.485),
     fp64 1e5 256: 0.326 (128: 0.334-0.376); d = 1000 ranks (round 2, profiles/round2/s1_shapes):
     128 at N = 8 (0.238 vs 0.415 ms at 512)."""
     if distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus:
-        return 384 if fp32 else 512
+        return 384 if fp32 and cpl >= 32 else 512
     return 256 if cpl >= 32 and not fp32 else 128  # 16 KB rows (fp64 d > 1024); fp32 2048 at 1e5: 128 rows 0.169 vs 256 0.194 ms
 
 
@@ -186,9 +187,10 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
         folded, lane epilogue (with the nt stream, profiles/round3/choices_nt: AGC fp64 1e6 rows
         1.165 vs 1.199-1.217 ms wave-uniform; FRC s = 1 fp64 1.157 vs 1.315 ms LDS-staged, fp32
         0.615 vs 0.666, 250k rows 0.303 vs 0.370);
-      * replicas otherwise (R > 3, or rows of 32 columns per lane): LDS-staged bundles, the pair form
-        (two rows per reduction) for fp32, short streams and 32-column rows (d = 2048 fp64 long
-        stream with the nt stream: 2.676 vs 2.751 ms);
+      * replicas otherwise (R > 3, or rows of 32 columns per lane): LDS-staged bundles, pair form
+        (two rows per reduction; with the nt stream it wins everywhere: d = 2048 fp64 2.676 vs 2.751
+        ms, 4 replicas at d = 1000 fp64 1.532-1.542 vs 1.668; one-wave bundles of 4 replicas need
+        276 registers, 1 wave per SIMD, and measured 1.76 ms: profiles/round3/choices_nt/frc4.jsonl);
       * bf16 replicas: MFMA bundles (d <= 1024, d % 8 == 0), else the fused kernel interleaved;
       * 2048 < d (fp64, 4096 fp32): the wide kernel; beyond 8192 / 16384 or cpl unknown: two passes.
     """
@@ -218,7 +220,7 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     # more replicas than a workgroup's task slots: bundles of MAX_BUNDLE (and the remainder, padded)
     return KernelChoice("staged", replicas=min(max_rep, MAX_BUNDLE),
                         bundle_rows=staged_bundle_rows(distinct_rows, n_cus, prec_code == 1, cpl),
-                        pair=prec_code == 1 or not long_stream or cpl >= 32, wpr=0 if long_stream else 1)
+                        pair=True, wpr=0 if long_stream else 1)
 
 
 def wide_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional[Sequence[int]] = None) -> int:

@@ -84,7 +84,8 @@ def test_kernel_selection_table():
     assert pick(0, 1000, 2, 1_000_000) == KernelChoice("multi", replicas=2, bundle_rows=512, fold=True, lane_epi=True)
     assert pick(0, 1000, 2, 250_000) == KernelChoice("multi", replicas=2, bundle_rows=128, fold=True, lane_epi=True)
     # more than 3 co-located replicas: LDS-staged bundles
-    assert pick(0, 1000, 4, 1_000_000) == KernelChoice("staged", replicas=4, bundle_rows=512)
+    assert pick(0, 1000, 4, 1_000_000) == KernelChoice("staged", replicas=4, bundle_rows=512, pair=True)
+    assert pick(1, 1000, 4, 1_000_000) == KernelChoice("staged", replicas=4, bundle_rows=512, pair=True)
     assert pick(0, 1000, 4, 250_000) == KernelChoice("staged", replicas=4, bundle_rows=128, pair=True, wpr=1)
     # more co-located replicas than task slots per workgroup (a cyclic W = 9 table on one rank): bundles of 8
     assert pick(0, 1000, 9, 1_000_000).replicas == 8 and pick(2, 1000, 9, 1_000_000).replicas == 8
@@ -111,8 +112,8 @@ def test_kernel_selection_table():
     # bf16 beyond the MFMA tile: the fused kernel, replica-interleaved
     assert pick(2, 2000, 3, 1_000_000) == KernelChoice("fused", rows=1, interleave=True)
     # the regime boundary is a rows-per-CU rule, not a row count: 4x the CUs -> 4x the rows
-    assert pick(0, 1000, 4, 700_000).pair and not pick(0, 1000, 4, 800_000).pair
-    assert choose_kernel(0, 1000, 16, 4, 2_800_000, n_cus=1024).pair
+    assert pick(0, 1000, 4, 700_000).wpr == 1 and pick(0, 1000, 4, 800_000).wpr == 0
+    assert choose_kernel(0, 1000, 16, 4, 2_800_000, n_cus=1024).wpr == 1
     # fp32 one-wave bundles: 12 per CU below the long-stream regime, 8 in it
     assert pick(1, 1000, 3, 700_000).bundle_rows == 256 and pick(1, 1000, 3, 800_000).bundle_rows == 416
 
