@@ -228,13 +228,24 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
     }
   }
   const int rowbytes = ld * static_cast<int>(sizeof(T));
-  auto load = [&](Rw (&x)[NV], int r) {
-    const auto rs = make_rsrc(X + static_cast<long long>(r) * ld, rowbytes);
+  const int r0 = lead.row_begin, r1 = live ? lead.row_end : r0;
+  // A row's label is loaded right behind the row itself, through a buffer descriptor: it is then
+  // older than the next row's prefetch, so a step waits for its own row and label only
+  // (vmcnt(loads of one row)) and the prefetched row stays in flight.  (Read at use through the
+  // segment pointer, it was a flat load issued AFTER the prefetch: every step waited vmcnt(0),
+  // which drained the prefetch -- one row in flight per wave, not two.)
+  const auto yrs = make_rsrc(Y + r0, (r1 - r0) * static_cast<int>(sizeof(A)));
+  // Loads are issued unconditionally (the compiler can then count them: a step waits with
+  // vmcnt(one row's loads), not a conservative merge of "prefetched / not prefetched"); a row past
+  // the bundle gets a zero-size descriptor, which returns zeros without touching memory.
+  auto load = [&](Rw (&x)[NV], A& yv, int r) {
+    const bool in = r < r1;
+    const auto rs = make_rsrc(X + static_cast<long long>(in ? r : r0) * ld, in ? rowbytes : 0);
 #pragma unroll
     for (int j = 0; j < NV; ++j) x[j] = buf_load16<Rw>(rs, (j * kWave + lane) * VN * static_cast<int>(sizeof(T)));
+    yv = buf_load_scalar<A>(yrs, (r - r0) * static_cast<int>(sizeof(A)));
   };
-  auto step = [&](const Rw (&x)[NV], int r) {
-    const A y = Y[r];
+  auto step = [&](const Rw (&x)[NV], const A y) {
     A z[R];
 #pragma unroll
     for (int q = 0; q < R; ++q) {
@@ -258,7 +269,11 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
       // of them instead of one wave-uniform evaluation each) and every lane reads the R residuals.
       static_assert(R <= 3, "one-wave bundles hold at most 3 replicas");
       const bool hi = lane >= 32;
-      A tq = wave_pair_reduce(z[0], z[1], hi), cq = hi ? coef[1] : coef[0];
+      // opaque copies: a select between two elements of coef[] would otherwise become one
+      // lane-indexed load of the array, i.e. coef[] in scratch memory (seen in the fp32 kernel)
+      A c0 = coef[0], c1 = coef[1];
+      asm volatile("" : "+v"(c0), "+v"(c1));
+      A tq = wave_pair_reduce(z[0], z[1], hi), cq = hi ? c1 : c0;
       constexpr int kLane[3] = {0, 32, 1};
       if constexpr (R == 3) {
         const A z2 = wave_allreduce_sum(z[2]);
@@ -279,9 +294,8 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
         for (int q = 0; q < R; ++q) g[q][j][v] = fma(rr[q], Vec16<T>::template elem<A>(x[j], v), g[q][j][v]);
   };
   // two rows at once (EPI 2): 2R dot products, one reduce-scatter, one residual per lane
-  auto step2 = [&](const Rw (&x0)[NV], const Rw (&x1)[NV], int r, bool two) {
+  auto step2 = [&](const Rw (&x0)[NV], const Rw (&x1)[NV], const A y0, const A y1, bool two) {
     static_assert(2 * R <= 8, "pair rows hold at most 4 replicas");
-    const A y0 = Y[r], y1 = two ? Y[r + 1] : A(0);
     A v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -319,31 +333,32 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
           g[q][j][e] = fma(r1v[q], Vec16<T>::template elem<A>(x1[j], e),
                            fma(r0v[q], Vec16<T>::template elem<A>(x0[j], e), g[q][j][e]));
   };
-  const int r0 = lead.row_begin, r1 = live ? lead.row_end : r0;
   if constexpr (EPI == 2) {
     Rw xa[NV], xb[NV], xc[NV], xd[NV];
+    A ya = A(0), yb = A(0), yc = A(0), yd = A(0);
 #pragma unroll
     for (int j = 0; j < NV; ++j) xa[j] = xb[j] = xc[j] = xd[j] = Rw{};  // a missing pair row reads zeros
-    if (r0 < r1) load(xa, r0);
-    if (r0 + 1 < r1) load(xb, r0 + 1);
+    load(xa, ya, r0);
+    load(xb, yb, r0 + 1);
     for (int r = r0; r < r1; r += 4) {  // four rows per trip: the buffer pairs swap roles
-      if (r + 2 < r1) load(xc, r + 2);
-      if (r + 3 < r1) load(xd, r + 3);
-      step2(xa, xb, r, r + 1 < r1);
+      load(xc, yc, r + 2);
+      load(xd, yd, r + 3);
+      step2(xa, xb, ya, yb, r + 1 < r1);
       if (r + 2 >= r1) break;
-      if (r + 4 < r1) load(xa, r + 4);
-      if (r + 5 < r1) load(xb, r + 5);
-      step2(xc, xd, r + 2, r + 3 < r1);
+      load(xa, ya, r + 4);
+      load(xb, yb, r + 5);
+      step2(xc, xd, yc, yd, r + 3 < r1);
     }
   } else {
     Rw xa[NV], xb[NV];
-    if (r0 < r1) load(xa, r0);
+    A ya = A(0), yb = A(0);
+    load(xa, ya, r0);
     for (int r = r0; r < r1; r += 2) {  // two rows per trip: the buffers swap roles without copies
-      if (r + 1 < r1) load(xb, r + 1);
-      step(xa, r);
+      load(xb, yb, r + 1);
+      step(xa, ya);
       if (r + 1 >= r1) break;
-      if (r + 2 < r1) load(xa, r + 2);
-      step(xb, r + 1);
+      load(xa, ya, r + 2);
+      step(xb, yb);
     }
   }
   if constexpr (FOLD) {
