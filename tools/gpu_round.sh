@@ -14,6 +14,9 @@
 #   prof     rocprofv3 --kernel-trace --stats of the fp64 / fp32 / bf16 headline
 #   pmc      counter passes (one rocprofv3 --pmc run each) of the fp64 / fp32 headline
 #   eval     evaluation phase profile (tools/profile_eval.py)
+#   abtree   same-box A/B against an older tree exported and built under build/ab_old
+#            (git archive <rev> | tar -x -C build/ab_old, then __graft_entry__.build() there):
+#            fp64 / fp32 headline, 100 steps, old / new interleaved twice
 set -o pipefail
 OUT=gpurun_out/round
 STAGES=()
@@ -77,6 +80,16 @@ for s in "${STAGES[@]}"; do
         done
       done
       python tools/pmc_summary.py "$OUT/pmc" > "$OUT/pmc_summary.json" ;;
+    abtree)
+      for rep in 1 2; do
+        for v in old new; do
+          D=.; [ $v = old ] && D=build/ab_old
+          for p in fp64 fp32; do
+            (cd $D && run 300 "ab_${v}_${p}_$rep.log" python -u bench.py --no-floor --no-breakdown --precision $p \
+              --steps 100 --warmup 10) || exit 1
+          done
+        done
+      done ;;
     eval)
       run 600 eval.log python -u tools/profile_eval.py --out "$OUT/eval.json" ;;
     *) echo "unknown stage $s"; exit 2 ;;
