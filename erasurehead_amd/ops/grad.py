@@ -180,7 +180,10 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     prec_code: 0 fp64, 1 fp32, 2 bf16 storage.  max_rep: most co-located messages reading one
     partition (1 = distinct rows only).  distinct_rows: rows of the distinct partitions per round.
     Measured choices (docs/PERF_NOTES.md):
-      * distinct rows: the fused kernel, fp64 the interleaved pair kernel, fp32 4 rows, bf16 1 row;
+      * distinct rows (naive, message-placed ranks): one-wave bundles of one replica at 16 columns per
+        lane (profiles/round3/choices_nt/naive.jsonl: fp64 1e6 rows 1.160 vs 1.197-1.213 ms fused,
+        fp32 0.581 vs 0.639, fp64 375k rows 0.447-0.456 vs 0.491); otherwise the fused kernel, fp64
+        the interleaved pair kernel, fp32 4 rows, bf16 1 row;
       * replicas, 3 per bundle, narrow rows (<= 8 columns per lane, d <= 512 fp64 / 1024 fp32):
         one-wave bundles with two rows per reduce-scatter (d = 256: 5.2 vs 2.3 TB/s before);
       * replicas, fp64 / fp32, 2 or 3 per bundle (AGC / cyclic s = 2, FRC s = 1): one-wave bundles,
@@ -202,6 +205,10 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
             return KernelChoice("wide", replicas=max_rep, bundle_rows=wide_bundle_rows(distinct_rows, n_cus, part_rows))
         return KernelChoice("wide", interleave=shared)
     if not shared:
+        if prec_code != 2 and 8 < cpl <= 16:  # distinct rows of 16 columns per lane: bundles of one
+            return KernelChoice("multi", replicas=1,
+                                bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl, part_rows),
+                                fold=True)
         return KernelChoice("fused", rows={0: 2, 1: 4, 2: 1}[prec_code])
     long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
     if prec_code == 2:

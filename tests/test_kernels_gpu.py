@@ -381,6 +381,30 @@ def test_dense_grad_one_wave_bundles_of_two(native, rows, d, prec_name, loss, fo
         np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=atol)
 
 
+@pytest.mark.parametrize("prec_name", ["fp64", "fp32"])
+@pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
+def test_distinct_rows_default_to_one_wave_bundles_of_one(native, prec_name, loss):
+    """Distinct rows (naive, message-placed ranks) at 16 columns per lane pick grad_dense_multi with
+    one replica per bundle; messages with two partitions and label coefficients against the oracle."""
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(17)
+    parts, host = _parts(rng, [900, 700, 333, 64], 1000, prec)
+    msgs = [[(0, 1.0), (1, 0.5)], [(2, -1.0)], [(3, 2.0)]]
+    plan = DenseGradPlan(msgs, parts, prec, loss, 1000)
+    assert plan.choice.kind == "multi" and plan.choice.replicas == 1 and plan.max_rep == 1
+    beta = torch.randn(plan.ld, dtype=prec.acc, device=DEV) * 0.05
+    G = plan.out_buffer()[0]
+    plan.native_launcher().launch(beta, G)
+    torch.cuda.synchronize()
+    bh = beta[:1000].double().cpu().numpy()
+    f = logistic_grad if loss == LOGISTIC else least_squares_grad
+    tol = 1e-10 if prec_name == "fp64" else 2e-4
+    atol = tol * 1e-2 if prec_name == "fp64" else 2e-5
+    for s_, m in enumerate(msgs):
+        ref = sum(f(host[p][0], host[p][1], bh, c) for p, c in m)
+        np.testing.assert_allclose(G[s_, :1000].double().cpu().numpy(), ref, rtol=tol, atol=atol)
+
+
 def test_frc_pairs_default_to_one_wave_bundles(native):
     """Two co-located replicas per partition (FRC s = 1) pick grad_dense_multi with R = 2."""
     prec = get_precision("fp64")

@@ -90,8 +90,10 @@ def test_kernel_selection_table():
     # more co-located replicas than task slots per workgroup (a cyclic W = 9 table on one rank): bundles of 8
     assert pick(0, 1000, 9, 1_000_000).replicas == 8 and pick(2, 1000, 9, 1_000_000).replicas == 8
     # distinct rows (naive): the fused kernel per precision
-    assert [pick(p, 1000, 1, 1_000_000) for p in (0, 1, 2)] == [KernelChoice("fused", rows=2), KernelChoice("fused", rows=4),
-                                                                   KernelChoice("fused", rows=1)]
+    assert [pick(p, 1000, 1, 1_000_000) for p in (0, 1, 2)] == [
+        KernelChoice("multi", replicas=1, bundle_rows=512, fold=True),
+        KernelChoice("multi", replicas=1, bundle_rows=512, fold=True), KernelChoice("fused", rows=1)]
+    assert pick(0, 256, 1, 1_000_000) == KernelChoice("fused", rows=2)  # narrow distinct rows: fused
     # wide rows: d = 2048 fp64 (32 columns per lane) stays on staged bundles (pair form); 4096 takes the wide kernel
     assert pick(0, 2048, 3, 1_000_000) == KernelChoice("staged", replicas=3, bundle_rows=512, pair=True)
     assert pick(1, 2048, 3, 1_000_000) == KernelChoice("staged", replicas=3, bundle_rows=384, pair=True)

@@ -168,7 +168,7 @@ def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000)
     """Every valid KernelChoice on the replica-bundle layout of a few shapes: the candidates
     behind choose_kernel's table (tests/test_plan_tables.py pins the picks).  layout agc: the
     headline's uneven AGC groups (3 replicas); frc2: FRC s = 1 (4 groups of 2 workers x 2 partitions);
-    frc4: FRC / AGC s = 3 (2 groups of 4 workers x 4 partitions)."""
+    frc4: FRC / AGC s = 3 (2 groups of 4 workers x 4 partitions); naive: one partition per message."""
     import dataclasses
 
     import torch
@@ -179,8 +179,9 @@ def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000)
 
     msgs = {"agc": [[0, 1, 2]] * 3 + [[3, 4, 5]] * 3 + [[6, 7]] * 2,
             "frc2": [[2 * g, 2 * g + 1] for g in range(4) for _ in range(2)],
-            "frc4": [[0, 1, 2, 3]] * 4 + [[4, 5, 6, 7]] * 4}[layout]
-    R = {"agc": 3, "frc2": 2, "frc4": 4}[layout]
+            "frc4": [[0, 1, 2, 3]] * 4 + [[4, 5, 6, 7]] * 4,
+            "naive": [[p] for p in range(8)]}[layout]
+    R = {"agc": 3, "frc2": 2, "frc4": 4, "naive": 1}[layout]
     for prec_name, d, n in shapes:
         prec = get_precision(prec_name)
         rpp = n // 8
@@ -273,7 +274,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "kernels.jsonl"))
     ap.add_argument("--shapes", default=None, help="--only choices: prec:d:n,... (default: the built-in list)")
-    ap.add_argument("--layout", default="agc", choices=["agc", "frc2", "frc4"], help="--only choices: replica layout")
+    ap.add_argument("--layout", default="agc", choices=["agc", "frc2", "frc4", "naive"],
+                    help="--only choices: replica layout")
     ap.add_argument("--only", choices=["dense", "sparse", "scale", "eval", "sweep", "choices"], default=None)
     a = ap.parse_args()
     out = []
