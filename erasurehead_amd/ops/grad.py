@@ -117,7 +117,13 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
     the default before nt: 1.26 ms; 384: 1.42 = a second partial round); fp32 -> 352 / 192 / 96 /
     64 rows (192: 0.333 vs 256: 0.341-0.350 ms at 500k; 96: 0.177 vs 128: 0.186 at 250k)."""
     long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
-    per_cu = (12 if fp32 and not long_stream else 8) * max(1, 16 // cpl)
+    # fp64: one workgroup (4 bundles) per CU.  Since a step waits for its own row only (the label
+    # load behind the row), 4 waves with the next row in flight keep a CU's share of HBM busy, and
+    # half as many slab rows, betas and folds are paid (profiles/round3/rows_prefetch: 1024 / 512 /
+    # 256 / 128-row bundles at 1e6 / 500k / 250k / 125k rows: 1.142 / 0.587 / 0.304 / 0.160 ms vs
+    # 1.185-1.218 / 0.611 / 0.320 / 0.171 at two workgroups per CU)
+    per_cu = (12 if not long_stream else 8) if fp32 else 4
+    per_cu *= max(1, 16 // cpl)
     slots = per_cu * n_cus
     parts = [int(r) for r in part_rows if r > 0] if part_rows else [distinct_rows / 8.0] * 8
     per = distinct_rows / slots

@@ -191,7 +191,7 @@ def choice_cases(out, shapes=(("fp64", 256, 1_000_000), ("fp32", 256, 1_000_000)
         distinct = 8 * parts[0][0].numel() * parts[0][0].element_size() / 1e12
         cands = [KernelChoice("fused", rows=r, interleave=i) for r in (1, 2, 4) for i in (False, True)]
         cands += [KernelChoice("multi", replicas=R, bundle_rows=b, fold=True, lane_epi=e)
-                  for b in (32, 64, 128, 192, 256, 512, 768) for e in (False, True)]
+                  for b in (32, 64, 128, 192, 256, 512, 768, 1024) for e in (False, True)]
         cands += [KernelChoice("multi", replicas=R, bundle_rows=b, fold=True, pair=True)
                   for b in (8, 16, 32, 64, 128, 192, 256, 512, 768)]
         cands += [KernelChoice("staged", replicas=R, bundle_rows=b, pair=p, wpr=w)
