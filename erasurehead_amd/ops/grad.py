@@ -129,14 +129,18 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
     per = distinct_rows / slots
     # small problems: bundles down to 8 rows (a wave with one row ahead streams ~1.4 us per row, so a
     # 32-row bundle alone is ~45 us: 4000 x 1000 fp64 rows over 2 ranks took 46 us per gradient)
-    base = 32 * int(np.ceil(per / 32)) if per > 16 else max(8, 8 * int(np.ceil(per / 8)))
+    # granularity: 128 rows for long bundles (fp64 1e6 rows: 1024-row bundles 1.198 ms vs 992-row 1.214,
+    # the same box, profiles/round3/rows_prefetch/rows5_fp64.jsonl: one padded workgroup less per
+    # partition), 32 for mid-size ones, 8 for small problems
+    gran = 128 if per > 128 else 32 if per > 16 else 8
+    base = max(8, gran * int(np.ceil(per / gran)))
 
     def fits(rows: int) -> bool:
         return sum(4 * int(np.ceil(np.ceil(p / rows) / 4)) for p in parts) <= slots
 
     rows = base
     while not fits(rows) and rows < max(parts):
-        rows += 32 if rows >= 32 else 8
+        rows += gran
     return rows if fits(rows) else base  # more partitions than slots: short bundles keep the tail short
 
 

@@ -52,12 +52,12 @@ def test_fold_table_groups_one_partition_per_workgroup():
 
 def test_multi_bundle_rows_table():
     # every folded workgroup resident at once (profiles/round3/nt_rows)
-    assert [multi_bundle_rows(n) for n in (1_000_000, 500_000, 250_000, 125_000)] == [992, 512, 256, 128]
-    assert [multi_bundle_rows(n, fp32=True) for n in (1_000_000, 500_000, 250_000, 125_000)] == [512, 192, 96, 64]
-    assert multi_bundle_rows(1000) == 8 and multi_bundle_rows(12_000) == 16 and multi_bundle_rows(4_000_000) == 3936
+    assert [multi_bundle_rows(n) for n in (1_000_000, 500_000, 250_000, 125_000)] == [1024, 512, 256, 128]
+    assert [multi_bundle_rows(n, fp32=True) for n in (1_000_000, 500_000, 250_000, 125_000)] == [512, 256, 96, 64]
+    assert multi_bundle_rows(1000) == 8 and multi_bundle_rows(12_000) == 16 and multi_bundle_rows(4_000_000) == 3968
     # per-partition fold padding pushes a bundle length up until the workgroups fit the slots
-    assert multi_bundle_rows(300_000) == 320 and multi_bundle_rows(300_000, part_rows=[3000] * 100) == 384
-    assert multi_bundle_rows(300_000, part_rows=[100] * 3000) == 320  # can never fit: the plain length
+    assert multi_bundle_rows(260_000) == 256 and multi_bundle_rows(260_000, part_rows=[2600] * 100) == 384
+    assert multi_bundle_rows(260_000, part_rows=[100] * 2600) == 256  # can never fit: the plain length
 
 
 def test_kernel_selection_table():
@@ -71,7 +71,7 @@ def test_kernel_selection_table():
         return choose_kernel(prec, ld, choose_cpl(ld, vec), rep, rows)
 
     # the headline (AGC W=8 s=2: bundles of 3 replicas), one GPU (1e6 distinct rows): long stream
-    assert pick(0, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=992, fold=True, lane_epi=True)
+    assert pick(0, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=1024, fold=True, lane_epi=True)
     assert pick(1, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=512, fold=True, lane_epi=True)
     assert pick(2, 1000, 3, 1_000_000) == KernelChoice("mfma", replicas=3, bundle_rows=4096)
     # bf16 MFMA bundles: every workgroup (one per CU) in the first dispatch round
@@ -79,9 +79,9 @@ def test_kernel_selection_table():
     # the 8-GPU partition-shard rank (125k rows): fill every wave slot, lane epilogue
     assert pick(0, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=128, fold=True, lane_epi=True)
     assert pick(1, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)
-    assert pick(1, 1000, 3, 500_000).bundle_rows == 192 and pick(1, 1000, 3, 250_000).bundle_rows == 96
+    assert pick(1, 1000, 3, 500_000).bundle_rows == 256 and pick(1, 1000, 3, 250_000).bundle_rows == 96
     # FRC s=1 (bundles of 2): one-wave bundles too, one GPU / a sharded rank
-    assert pick(0, 1000, 2, 1_000_000) == KernelChoice("multi", replicas=2, bundle_rows=992, fold=True, lane_epi=True)
+    assert pick(0, 1000, 2, 1_000_000) == KernelChoice("multi", replicas=2, bundle_rows=1024, fold=True, lane_epi=True)
     assert pick(0, 1000, 2, 250_000) == KernelChoice("multi", replicas=2, bundle_rows=256, fold=True, lane_epi=True)
     # more than 3 co-located replicas: LDS-staged bundles
     assert pick(0, 1000, 4, 1_000_000) == KernelChoice("staged", replicas=4, bundle_rows=512, pair=True)
@@ -91,7 +91,7 @@ def test_kernel_selection_table():
     assert pick(0, 1000, 9, 1_000_000).replicas == 8 and pick(2, 1000, 9, 1_000_000).replicas == 8
     # distinct rows (naive): the fused kernel per precision
     assert [pick(p, 1000, 1, 1_000_000) for p in (0, 1, 2)] == [
-        KernelChoice("multi", replicas=1, bundle_rows=992, fold=True),
+        KernelChoice("multi", replicas=1, bundle_rows=1024, fold=True),
         KernelChoice("multi", replicas=1, bundle_rows=512, fold=True), KernelChoice("fused", rows=1)]
     assert pick(0, 256, 1, 1_000_000) == KernelChoice("fused", rows=2)  # narrow distinct rows: fused
     # wide rows: d = 2048 fp64 (32 columns per lane) stays on staged bundles (pair form); 4096 takes the wide kernel
@@ -117,7 +117,7 @@ def test_kernel_selection_table():
     assert pick(0, 1000, 4, 700_000).wpr == 1 and pick(0, 1000, 4, 800_000).wpr == 0
     assert choose_kernel(0, 1000, 16, 4, 2_800_000, n_cus=1024).wpr == 1
     # fp32 one-wave bundles: 12 per CU below the long-stream regime, 8 in it
-    assert pick(1, 1000, 3, 700_000).bundle_rows == 256 and pick(1, 1000, 3, 800_000).bundle_rows == 416
+    assert pick(1, 1000, 3, 700_000).bundle_rows == 256 and pick(1, 1000, 3, 800_000).bundle_rows == 512
 
 
 def test_no_tuning_env_knobs_left():
