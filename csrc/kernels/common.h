@@ -292,4 +292,14 @@ __device__ __forceinline__ A residual(A z, A y, A coef) {
 
 __host__ __device__ constexpr int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
+// Stale-round gate of a lazy-drain worker round (launchers.h PutDesc::gate, engine.cpp WorkerPump):
+// nonzero = the master had published the next beta before this round could start, so every kernel
+// of the round returns at once.  The value is launch-uniform (written by the previous round's put
+// kernel, stream-ordered before this launch), so whole grids return together and no barrier is left
+// half-reached.  nullptr = not gated (every other launch).
+__device__ __forceinline__ bool gate_closed(const int* gate) {
+  if (!gate) return false;
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
+}
+
 }  // namespace eh

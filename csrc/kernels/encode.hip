@@ -21,10 +21,10 @@ namespace eh {
 template <typename A>
 __global__ void __launch_bounds__(256)
 encode_messages(const A* __restrict__ Gb, const int* __restrict__ ptr, const int* __restrict__ idx,
-                const double* __restrict__ coef, A* __restrict__ G, int ld) {
+                const double* __restrict__ coef, A* __restrict__ G, int ld, const int* __restrict__ gate) {
   const int slot = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ld) return;
+  if (c >= ld || gate_closed(gate)) return;
   const int b = ptr[slot], e = ptr[slot + 1];
   A s = A(0);
   for (int k = b; k < e; ++k) s = fma(static_cast<A>(coef[k]), Gb[static_cast<long long>(idx[k]) * ld + c], s);
@@ -32,13 +32,13 @@ encode_messages(const A* __restrict__ Gb, const int* __restrict__ ptr, const int
 }
 
 hipError_t encode_messages_launch(int dtype, const void* Gb, const int* ptr, const int* idx, const double* coef,
-                                  void* G, int nslots, int ld, hipStream_t st) {
+                                  void* G, int nslots, int ld, hipStream_t st, const int* gate) {
   if (nslots == 0) return hipSuccess;
   const dim3 block(256), grid(ceil_div(ld, 256), nslots);
   if (dtype == 0)
-    hipLaunchKernelGGL(encode_messages<double>, grid, block, 0, st, (const double*)Gb, ptr, idx, coef, (double*)G, ld);
+    hipLaunchKernelGGL(encode_messages<double>, grid, block, 0, st, (const double*)Gb, ptr, idx, coef, (double*)G, ld, gate);
   else
-    hipLaunchKernelGGL(encode_messages<float>, grid, block, 0, st, (const float*)Gb, ptr, idx, coef, (float*)G, ld);
+    hipLaunchKernelGGL(encode_messages<float>, grid, block, 0, st, (const float*)Gb, ptr, idx, coef, (float*)G, ld, gate);
   return hipGetLastError();
 }
 

@@ -47,7 +47,7 @@ struct KernelChoice {
 
 // grad_mfma.hip: bf16 replica bundles on the matrix cores (R task slots per workgroup, ld <= 1024)
 hipError_t grad_mfma_launch(int loss, const Segment* segs, const Task* tasks, int ntasks, int R, const float* beta,
-                            float* slab, int ld, hipStream_t st);
+                            float* slab, int ld, hipStream_t st, const int* gate = nullptr);
 bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds);
 
 }  // namespace eh

@@ -40,10 +40,11 @@ namespace eh {
 template <typename T, typename A, int CPL, int LOSS, int ROWS, bool BL = false>
 __global__ void __launch_bounds__(256)
 grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
-                 const A* __restrict__ beta, A* __restrict__ slab, int ld) {
+                 const A* __restrict__ beta, A* __restrict__ slab, int ld, const int* __restrict__ gate) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;  // vector loads per row per lane
   static_assert(CPL % VN == 0, "CPL must be a multiple of the vector width");
+  if (gate_closed(gate)) return;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   A* red = reinterpret_cast<A*>(smem_raw);
@@ -195,10 +196,11 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
 template <typename T, typename A, int CPL, int LOSS, int R, bool FOLD, int EPI = 0>
 __global__ void __launch_bounds__(256)
 grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ tasks, int nbundles,
-                 const A* __restrict__ beta, A* __restrict__ slab, int ld) {
+                 const A* __restrict__ beta, A* __restrict__ slab, int ld, const int* __restrict__ gate) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;
   using Rw = typename Vec16<T>::raw;
+  if (gate_closed(gate)) return;  // launch-uniform: the FOLD barrier is never half-reached
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int bundle = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + wv);
@@ -411,10 +413,11 @@ template <typename T, typename A, int CPL, int LOSS, bool PAIR>
 __global__ void __launch_bounds__(512)
 grad_dense_staged(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                   const A* __restrict__ beta, A* __restrict__ slab, int ld, int srows, int pieces, int nstage,
-                  int wpr) {
+                  int wpr, const int* __restrict__ gate) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  if (gate_closed(gate)) return;
   // W waves = R task slots x wpr waves per slot; slot q's waves split each stage's rows
   const int lane = threadIdx.x & 63, W = blockDim.x >> 6, R = W / wpr;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -685,10 +688,11 @@ static inline bool staged_geometry(int R, int rowbytes, size_t fold_bytes_per_wa
 template <typename T, typename A, int CPL, int LOSS>
 __global__ void __launch_bounds__(256)
 grad_dense_fused_pair(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
-                 const A* __restrict__ beta, A* __restrict__ slab, int ld) {
+                 const A* __restrict__ beta, A* __restrict__ slab, int ld, const int* __restrict__ gate) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;  // vector loads per row per lane
   static_assert(CPL % VN == 0, "CPL must be a multiple of the vector width");
+  if (gate_closed(gate)) return;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   A* red = reinterpret_cast<A*>(smem_raw);
@@ -811,10 +815,11 @@ grad_dense_fused_pair(const Segment* __restrict__ segs, const Task* __restrict__
 template <typename T, typename A, int NV, int BS, int LOSS, int R>
 __global__ void __launch_bounds__(BS)
 grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
-                const A* __restrict__ beta, A* __restrict__ slab, int ld) {
+                const A* __restrict__ beta, A* __restrict__ slab, int ld, const int* __restrict__ gate) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NW = BS / kWave;
   __shared__ A part[2][2][R][NW];  // [buffer][row of the pair][replica][wave]
+  if (gate_closed(gate)) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const Task lead = tasks[blockIdx.x * R];  // slot 0 of a bundle is always a real task
   const Segment seg = segs[lead.seg];
@@ -951,8 +956,9 @@ constexpr int kSplits = 16;
 template <typename A>
 __global__ void __launch_bounds__(256)
 slab_reduce_partial(const A* __restrict__ slab, const int* __restrict__ slot_task_begin,
-                    A* __restrict__ part, int ld) {
+                    A* __restrict__ part, int ld, const int* __restrict__ gate) {
   __shared__ A red[4][kWave];
+  if (gate_closed(gate)) return;
   const int slot = blockIdx.y, split = blockIdx.z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = blockIdx.x * kWave + lane;
@@ -971,10 +977,10 @@ slab_reduce_partial(const A* __restrict__ slab, const int* __restrict__ slot_tas
 
 template <typename A>
 __global__ void __launch_bounds__(256)
-slab_reduce_final(const A* __restrict__ part, A* __restrict__ G, int ld) {
+slab_reduce_final(const A* __restrict__ part, A* __restrict__ G, int ld, const int* __restrict__ gate) {
   const int slot = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ld) return;
+  if (c >= ld || gate_closed(gate)) return;
   A s = A(0);
 #pragma unroll
   for (int k = 0; k < kSplits; ++k) s += part[(static_cast<long long>(slot) * kSplits + k) * ld + c];
@@ -997,6 +1003,10 @@ slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, Put
   __shared__ int s_last, s_live;
   const int slot = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gate_closed(put.gate)) {  // a skipped stale round (launch-uniform): decide the next one's gate
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) put_decide_next_gate(put);
+    return;
+  }
   if (threadIdx.x == 0)  // one read, shared: every wave of the block takes the same branch
     s_live = !(put.abort && __hip_atomic_load(put.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
   __syncthreads();
@@ -1038,6 +1048,7 @@ slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, Put
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // see transport.hip: keep the flag behind the fence
     __hip_atomic_store(put.flag, put.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    put_decide_next_gate(put);
   }
 }
 
@@ -1091,14 +1102,15 @@ slab_final_update(const A* __restrict__ part, A* __restrict__ G, int ld, int nsl
 
 template <typename A>
 static hipError_t slab_reduce_launch(const A* slab, const int* stb, A* part, A* G, int nslots, int ld,
-                                     hipStream_t st, const PutDesc* put = nullptr) {
+                                     hipStream_t st, const PutDesc* put = nullptr, const int* gate = nullptr) {
   hipLaunchKernelGGL(slab_reduce_partial<A>, dim3(ceil_div(ld, kWave), nslots, kSplits), dim3(256), 0, st,
-                     slab, stb, part, ld);
+                     slab, stb, part, ld, gate);
   if (put && put->tag && (nslots > kMaxTagRows || !put->csum)) return hipErrorInvalidValue;
+  if (put && put->gate != gate) return hipErrorInvalidValue;  // one round, one gate
   if (put)
     hipLaunchKernelGGL(slab_reduce_final_put<A>, dim3(ceil_div(ld, 256), nslots), dim3(256), 0, st, part, G, ld, *put);
   else
-    hipLaunchKernelGGL(slab_reduce_final<A>, dim3(ceil_div(ld, 256), nslots), dim3(256), 0, st, part, G, ld);
+    hipLaunchKernelGGL(slab_reduce_final<A>, dim3(ceil_div(ld, 256), nslots), dim3(256), 0, st, part, G, ld, gate);
   return hipGetLastError();
 }
 
@@ -1108,8 +1120,9 @@ template <typename T, typename A, int LOSS>
 __global__ void __launch_bounds__(256)
 rowdot_residual(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                 const A* __restrict__ beta, const int* __restrict__ task_row_off,
-                A* __restrict__ rbuf, int ld) {
+                A* __restrict__ rbuf, int ld, const int* __restrict__ gate) {
   constexpr int VN = Vec16<T>::N;
+  if (gate_closed(gate)) return;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nw = blockDim.x >> 6;
@@ -1138,8 +1151,9 @@ template <typename T, typename A>
 __global__ void __launch_bounds__(256)
 xt_r_tiles(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
            const int* __restrict__ task_row_off, const A* __restrict__ rbuf,
-           A* __restrict__ slab, int ld) {
+           A* __restrict__ slab, int ld, const int* __restrict__ gate) {
   constexpr int VN = Vec16<T>::N;
+  if (gate_closed(gate)) return;
   const Task task = tasks[blockIdx.x];
   const Segment seg = segs[task.seg];
   const T* __restrict__ X = static_cast<const T*>(seg.X);
@@ -1172,12 +1186,12 @@ namespace eh {
 // wave at 128 VGPRs and spill the two-row register tiles, so wider rows take the two-pass path.)
 template <typename T, typename A, int LOSS>
 static hipError_t launch_wide(int bs, int R, const Segment* segs, const Task* tasks, int ntasks, const A* beta,
-                              A* slab, int ld, hipStream_t st) {
+                              A* slab, int ld, hipStream_t st, const int* gate) {
   constexpr int NV = Vec16<T>::N == 8 ? 4 : 8;
   if (R < 1 || R > 3 || ntasks % R) return hipErrorInvalidValue;
   const dim3 grid(ntasks / R);
 #define EH_WIDE(BS_, R_) \
-  hipLaunchKernelGGL((grad_dense_wide<T, A, NV, BS_, LOSS, R_>), grid, dim3(BS_), 0, st, segs, tasks, beta, slab, ld)
+  hipLaunchKernelGGL((grad_dense_wide<T, A, NV, BS_, LOSS, R_>), grid, dim3(BS_), 0, st, segs, tasks, beta, slab, ld, gate)
   if (bs == 256) {
     if (R == 1) EH_WIDE(256, 1); else if (R == 2) EH_WIDE(256, 2); else EH_WIDE(256, 3);
   } else if (bs == 512 && R == 1) {  // (replica bundles of 512-thread rows would spill: R * 16+ accumulators)
@@ -1192,9 +1206,11 @@ static hipError_t launch_wide(int bs, int R, const Segment* segs, const Task* ta
 // grad_dense_multi launch; the folded form takes 3 waves' accumulators in dynamic LDS.
 template <typename T, typename A, int C, int LOSS, int R>
 static hipError_t launch_multi(bool fold, bool lane_epi, bool pair, dim3 grid, dim3 block, hipStream_t st,
-                               const Segment* segs, const Task* tasks, int nb, const A* beta, A* slab, int ld) {
+                               const Segment* segs, const Task* tasks, int nb, const A* beta, A* slab, int ld,
+                               const int* gate) {
   if (!fold) {  // (the lane / pair-row epilogues come with the fold only)
-    hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, R, false, 0>), grid, block, 0, st, segs, tasks, nb, beta, slab, ld);
+    hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, R, false, 0>), grid, block, 0, st, segs, tasks, nb, beta, slab, ld,
+                       gate);
     return hipGetLastError();
   }
   const size_t lds = 3ull * R * C * kWave * sizeof(A);
@@ -1210,20 +1226,22 @@ static hipError_t launch_multi(bool fold, bool lane_epi, bool pair, dim3 grid, d
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, grid, block, lds, st, segs, tasks, nb, beta, slab, ld);
+  hipLaunchKernelGGL(kern, grid, block, lds, st, segs, tasks, nb, beta, slab, ld, gate);
   return hipGetLastError();
 }
 
 template <typename T, typename A, int LOSS>
 static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tasks, int ntasks,
-                                   const A* beta, A* slab, int ld, hipStream_t st, const KernelChoice& k) {
+                                   const A* beta, A* slab, int ld, hipStream_t st, const KernelChoice& k,
+                                   const int* gate = nullptr) {
   if (k.kind == kGradMfma) {  // bf16 replica bundles on the matrix cores (grad_mfma.hip)
     if constexpr (std::is_same<T, bf16_t>::value)
-      return grad_mfma_launch(LOSS, segs, tasks, ntasks, k.replicas, beta, slab, ld, st);
+      return grad_mfma_launch(LOSS, segs, tasks, ntasks, k.replicas, beta, slab, ld, st, gate);
     return hipErrorInvalidValue;
   }
   if (k.kind == kGradWide || cpl >= 256)
-    return launch_wide<T, A, LOSS>(cpl, k.kind == kGradWide ? k.replicas : 1, segs, tasks, ntasks, beta, slab, ld, st);
+    return launch_wide<T, A, LOSS>(cpl, k.kind == kGradWide ? k.replicas : 1, segs, tasks, ntasks, beta, slab, ld, st,
+                                   gate);
   const int R = k.replicas;
   const bool bundled = k.kind == kGradStaged || k.kind == kGradMulti;
   if (bundled && (R < 1 || ntasks % R != 0)) return hipErrorInvalidValue;
@@ -1246,7 +1264,7 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
           if (ea != hipSuccess) return ea;                                                             \
         }                                                                                              \
         hipLaunchKernelGGL(kern, dim3(ntasks / R), dim3(64 * R * sg.wpr), sg.lds, st, segs, tasks, beta, \
-                           slab, ld, sg.srows, sg.pieces, sg.nstage, sg.wpr);                          \
+                           slab, ld, sg.srows, sg.pieces, sg.nstage, sg.wpr, gate);                    \
         return hipGetLastError();                                                                      \
       }                                                                                                \
       if (k.kind == kGradMulti) { /* every replica of a bundle in one wave, rows in registers */       \
@@ -1255,9 +1273,9 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
           if (k.fold && nb_ % 4) return hipErrorInvalidValue;                                          \
           const dim3 mg((nb_ + 3) / 4), mb(256);                                                       \
           const bool f = k.fold != 0, le = k.lane_epi != 0, pr = k.pair != 0;                          \
-          if (R == 1) return launch_multi<T, A, C, LOSS, 1>(f, le, pr, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
-          if (R == 2) return launch_multi<T, A, C, LOSS, 2>(f, le, pr, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
-          if (R == 3) return launch_multi<T, A, C, LOSS, 3>(f, le, pr, mg, mb, st, segs, tasks, nb_, beta, slab, ld); \
+          if (R == 1) return launch_multi<T, A, C, LOSS, 1>(f, le, pr, mg, mb, st, segs, tasks, nb_, beta, slab, ld, gate); \
+          if (R == 2) return launch_multi<T, A, C, LOSS, 2>(f, le, pr, mg, mb, st, segs, tasks, nb_, beta, slab, ld, gate); \
+          if (R == 3) return launch_multi<T, A, C, LOSS, 3>(f, le, pr, mg, mb, st, segs, tasks, nb_, beta, slab, ld, gate); \
         }                                                                                              \
         return hipErrorInvalidValue;                                                                   \
       }                                                                                                \
@@ -1267,17 +1285,17 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
       const size_t shb = sh + kWave * C * sizeof(A);                                                   \
       if (k.beta_lds) {                                                                                \
         if (k.rows == 1)                                                                               \
-          hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1, true>), grid, block, shb, st, segs, tasks, beta, slab, ld); \
+          hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1, true>), grid, block, shb, st, segs, tasks, beta, slab, ld, gate); \
         else if (k.rows == 2)                                                                          \
-          hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 2, true>), grid, block, shb, st, segs, tasks, beta, slab, ld); \
+          hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 2, true>), grid, block, shb, st, segs, tasks, beta, slab, ld, gate); \
         else                                                                                           \
-          hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 4, true>), grid, block, shb, st, segs, tasks, beta, slab, ld); \
+          hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 4, true>), grid, block, shb, st, segs, tasks, beta, slab, ld, gate); \
       } else if (k.rows == 1) {                                                                        \
-        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1>), grid, block, sh, st, segs, tasks, beta, slab, ld); \
+        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 1>), grid, block, sh, st, segs, tasks, beta, slab, ld, gate); \
       } else if (k.rows == 4) {                                                                        \
-        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 4>), grid, block, sh, st, segs, tasks, beta, slab, ld); \
+        hipLaunchKernelGGL((grad_dense_fused<T, A, C, LOSS, 4>), grid, block, sh, st, segs, tasks, beta, slab, ld, gate); \
       } else {                                                                                         \
-        hipLaunchKernelGGL((grad_dense_fused_pair<T, A, C, LOSS>), grid, block, sh, st, segs, tasks, beta, slab, ld); \
+        hipLaunchKernelGGL((grad_dense_fused_pair<T, A, C, LOSS>), grid, block, sh, st, segs, tasks, beta, slab, ld, gate); \
       }                                                                                                \
       return hipGetLastError();                                                                        \
     } else {                                                                                           \
@@ -1299,26 +1317,26 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
 hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
                              int ntasks, const void* beta, void* slab, const int* slot_task_begin,
                              int nslots, void* part, void* G, int ld, hipStream_t st, const KernelChoice& k,
-                             const PutDesc* put) {
+                             const PutDesc* put, const int* gate) {
   const Segment* S = static_cast<const Segment*>(segs);
   const Task* Tk = static_cast<const Task*>(tasks);
   hipError_t e = hipSuccess;
   if (dtype == 0) {
     e = loss == kLogistic
-            ? launch_fused_cpl<double, double, kLogistic>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, k)
-            : launch_fused_cpl<double, double, kLeastSquares>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, k);
+            ? launch_fused_cpl<double, double, kLogistic>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, k, gate)
+            : launch_fused_cpl<double, double, kLeastSquares>(cpl, S, Tk, ntasks, (const double*)beta, (double*)slab, ld, st, k, gate);
   } else if (dtype == 1) {
     e = loss == kLogistic
-            ? launch_fused_cpl<float, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k)
-            : launch_fused_cpl<float, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k);
+            ? launch_fused_cpl<float, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k, gate)
+            : launch_fused_cpl<float, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k, gate);
   } else {
     e = loss == kLogistic
-            ? launch_fused_cpl<bf16_t, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k)
-            : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k);
+            ? launch_fused_cpl<bf16_t, float, kLogistic>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k, gate)
+            : launch_fused_cpl<bf16_t, float, kLeastSquares>(cpl, S, Tk, ntasks, (const float*)beta, (float*)slab, ld, st, k, gate);
   }
   if (e != hipSuccess) return e;
-  if (dtype == 0) return slab_reduce_launch<double>((const double*)slab, slot_task_begin, (double*)part, (double*)G, nslots, ld, st, put);
-  return slab_reduce_launch<float>((const float*)slab, slot_task_begin, (float*)part, (float*)G, nslots, ld, st, put);
+  if (dtype == 0) return slab_reduce_launch<double>((const double*)slab, slot_task_begin, (double*)part, (double*)G, nslots, ld, st, put, gate);
+  return slab_reduce_launch<float>((const float*)slab, slot_task_begin, (float*)part, (float*)G, nslots, ld, st, put, gate);
 }
 
 
@@ -1348,12 +1366,12 @@ hipError_t grad_dense_update_launch(int dtype, int loss, int cpl, const void* se
     return hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
   };
   if (dtype == 0) {
-    hipLaunchKernelGGL(slab_reduce_partial<double>, pgrid, dim3(256), 0, st, (const double*)slab, stb, (double*)part, ld);
+    hipLaunchKernelGGL(slab_reduce_partial<double>, pgrid, dim3(256), 0, st, (const double*)slab, stb, (double*)part, ld, nullptr);
     if ((e = go(reinterpret_cast<const void*>(slab_final_update<double>))) != hipSuccess) return e;
     hipLaunchKernelGGL(slab_final_update<double>, dim3(ceil_div(ld, kWave)), dim3(256), lds, st, (const double*)part,
                        (double*)G, ld, nslots, up);
   } else {
-    hipLaunchKernelGGL(slab_reduce_partial<float>, pgrid, dim3(256), 0, st, (const float*)slab, stb, (float*)part, ld);
+    hipLaunchKernelGGL(slab_reduce_partial<float>, pgrid, dim3(256), 0, st, (const float*)slab, stb, (float*)part, ld, nullptr);
     if ((e = go(reinterpret_cast<const void*>(slab_final_update<float>))) != hipSuccess) return e;
     hipLaunchKernelGGL(slab_final_update<float>, dim3(ceil_div(ld, kWave)), dim3(256), lds, st, (const float*)part,
                        (float*)G, ld, nslots, up);
@@ -1364,33 +1382,33 @@ hipError_t grad_dense_update_launch(int dtype, int loss, int cpl, const void* se
 hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, const void* tasks,
                                      int ntasks, const void* beta, const int* task_row_off,
                                      void* rbuf, void* slab, const int* slot_task_begin,
-                                     int nslots, void* part, void* G, int ld, hipStream_t st) {
+                                     int nslots, void* part, void* G, int ld, hipStream_t st, const int* gate) {
   const Segment* S = static_cast<const Segment*>(segs);
   const Task* Tk = static_cast<const Task*>(tasks);
   const dim3 block(256);
   if (dtype == 0) {
     if (loss == kLogistic)
-      hipLaunchKernelGGL((rowdot_residual<double, double, kLogistic>), dim3(ntasks), block, 0, st, S, Tk, (const double*)beta, task_row_off, (double*)rbuf, ld);
+      hipLaunchKernelGGL((rowdot_residual<double, double, kLogistic>), dim3(ntasks), block, 0, st, S, Tk, (const double*)beta, task_row_off, (double*)rbuf, ld, gate);
     else
-      hipLaunchKernelGGL((rowdot_residual<double, double, kLeastSquares>), dim3(ntasks), block, 0, st, S, Tk, (const double*)beta, task_row_off, (double*)rbuf, ld);
-    hipLaunchKernelGGL((xt_r_tiles<double, double>), dim3(ntasks, ceil_div(ld, 256 * 2)), block, 0, st, S, Tk, task_row_off, (const double*)rbuf, (double*)slab, ld);
+      hipLaunchKernelGGL((rowdot_residual<double, double, kLeastSquares>), dim3(ntasks), block, 0, st, S, Tk, (const double*)beta, task_row_off, (double*)rbuf, ld, gate);
+    hipLaunchKernelGGL((xt_r_tiles<double, double>), dim3(ntasks, ceil_div(ld, 256 * 2)), block, 0, st, S, Tk, task_row_off, (const double*)rbuf, (double*)slab, ld, gate);
   } else if (dtype == 1) {
     if (loss == kLogistic)
-      hipLaunchKernelGGL((rowdot_residual<float, float, kLogistic>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld);
+      hipLaunchKernelGGL((rowdot_residual<float, float, kLogistic>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld, gate);
     else
-      hipLaunchKernelGGL((rowdot_residual<float, float, kLeastSquares>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld);
-    hipLaunchKernelGGL((xt_r_tiles<float, float>), dim3(ntasks, ceil_div(ld, 256 * 4)), block, 0, st, S, Tk, task_row_off, (const float*)rbuf, (float*)slab, ld);
+      hipLaunchKernelGGL((rowdot_residual<float, float, kLeastSquares>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld, gate);
+    hipLaunchKernelGGL((xt_r_tiles<float, float>), dim3(ntasks, ceil_div(ld, 256 * 4)), block, 0, st, S, Tk, task_row_off, (const float*)rbuf, (float*)slab, ld, gate);
   } else {
     if (loss == kLogistic)
-      hipLaunchKernelGGL((rowdot_residual<bf16_t, float, kLogistic>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld);
+      hipLaunchKernelGGL((rowdot_residual<bf16_t, float, kLogistic>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld, gate);
     else
-      hipLaunchKernelGGL((rowdot_residual<bf16_t, float, kLeastSquares>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld);
-    hipLaunchKernelGGL((xt_r_tiles<bf16_t, float>), dim3(ntasks, ceil_div(ld, 256 * 8)), block, 0, st, S, Tk, task_row_off, (const float*)rbuf, (float*)slab, ld);
+      hipLaunchKernelGGL((rowdot_residual<bf16_t, float, kLeastSquares>), dim3(ntasks), block, 0, st, S, Tk, (const float*)beta, task_row_off, (float*)rbuf, ld, gate);
+    hipLaunchKernelGGL((xt_r_tiles<bf16_t, float>), dim3(ntasks, ceil_div(ld, 256 * 8)), block, 0, st, S, Tk, task_row_off, (const float*)rbuf, (float*)slab, ld, gate);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (dtype == 0) return slab_reduce_launch<double>((const double*)slab, slot_task_begin, (double*)part, (double*)G, nslots, ld, st);
-  return slab_reduce_launch<float>((const float*)slab, slot_task_begin, (float*)part, (float*)G, nslots, ld, st);
+  if (dtype == 0) return slab_reduce_launch<double>((const double*)slab, slot_task_begin, (double*)part, (double*)G, nslots, ld, st, nullptr, gate);
+  return slab_reduce_launch<float>((const float*)slab, slot_task_begin, (float*)part, (float*)G, nslots, ld, st, nullptr, gate);
 }
 
 }  // namespace eh

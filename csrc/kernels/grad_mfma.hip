@@ -72,8 +72,9 @@ __device__ __forceinline__ bf16x4 tr_read(const unsigned char* p) {
 template <int LOSS, int kMfS>
 __global__ void __launch_bounds__(512)
 grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ tasks, const float* __restrict__ beta,
-                 float* __restrict__ slab, int ld, int R, int pieces, int nstage) {
+                 float* __restrict__ slab, int ld, int R, int pieces, int nstage, const int* __restrict__ gate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  if (gate_closed(gate)) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned lds_base = static_cast<unsigned>(
@@ -305,7 +306,7 @@ bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds) {
 }
 
 hipError_t grad_mfma_launch(int loss, const Segment* segs, const Task* tasks, int ntasks, int R, const float* beta,
-                            float* slab, int ld, hipStream_t st) {
+                            float* slab, int ld, hipStream_t st, const int* gate) {
   if (R < 1 || R > 16 || ntasks % R) return hipErrorInvalidValue;
   int rows = 0, pieces = 0, nstage = 0;
   size_t lds = 0;
@@ -316,7 +317,7 @@ hipError_t grad_mfma_launch(int loss, const Segment* segs, const Task* tasks, in
                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
   if (ea != hipSuccess) return ea;
   hipLaunchKernelGGL(kern, dim3(ntasks / R), dim3(64 * kMfNW), lds, st, segs, tasks, beta, slab, ld, R, pieces,
-                     nstage);
+                     nstage, gate);
   return hipGetLastError();
 }
 

@@ -26,7 +26,8 @@ __global__ void __launch_bounds__(256)
 csr_rowpass(const long long* __restrict__ row_ptr, const int* __restrict__ col_idx,
             const A* __restrict__ vals,
             const A* __restrict__ y, const A* __restrict__ coef, const A* __restrict__ beta,
-            A* __restrict__ rbuf, long long nrows, int ld) {
+            A* __restrict__ rbuf, long long nrows, int ld, const int* __restrict__ gate) {
+  if (gate_closed(gate)) return;
   const long long gid = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x);
   const long long row = gid / G;
   const int sub = threadIdx.x % G;
@@ -46,7 +47,8 @@ template <typename A>
 __global__ void __launch_bounds__(256)
 coo_colpass(const long long* __restrict__ keys, const int* __restrict__ rows,
             const A* __restrict__ vals, const A* __restrict__ rbuf, A* __restrict__ G,
-            long long nnz) {
+            long long nnz, const int* __restrict__ gate) {
+  if (gate_closed(gate)) return;
   const long long e = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const bool live = e < nnz;
@@ -77,7 +79,8 @@ template <typename A, int LOSS, bool VALS>
 __global__ void __launch_bounds__(256)
 ell_rowpass(const int* __restrict__ idx, const A* __restrict__ vals, const A* __restrict__ y,
             const A* __restrict__ coef, const A* __restrict__ beta, A* __restrict__ rbuf,
-            long long nrows, int m, A* __restrict__ G, long long gsize) {
+            long long nrows, int m, A* __restrict__ G, long long gsize, const int* __restrict__ gate) {
+  if (gate_closed(gate)) return;
   const long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   // the column pass accumulates into G: zero it here (stream order) instead of a memset launch
   const long long nthreads = static_cast<long long>(gridDim.x) * blockDim.x;
@@ -122,8 +125,9 @@ template <typename A, bool VALS>
 __global__ void __launch_bounds__(256)
 ell_colpass(const int* __restrict__ idx, const A* __restrict__ vals, const A* __restrict__ rbuf,
             const EllChunk* __restrict__ chunks, const int* __restrict__ lo, const int* __restrict__ width,
-            A* __restrict__ G, long long nrows, int ld, int lds_cap) {
+            A* __restrict__ G, long long nrows, int ld, int lds_cap, const int* __restrict__ gate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  if (gate_closed(gate)) return;
   A* hist = reinterpret_cast<A*>(smem_raw);
   const EllChunk ch = chunks[blockIdx.x];
   const int k = blockIdx.y;
@@ -181,7 +185,7 @@ ell_colpass(const int* __restrict__ idx, const A* __restrict__ vals, const A* __
 hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals, const void* y,
                            const void* coef, const void* beta, void* rbuf, long long nrows, int m,
                            const void* chunks, int nchunks, const int* lo, const int* width,
-                           int max_width, void* G, long long gsize, int ld, hipStream_t st) {
+                           int max_width, void* G, long long gsize, int ld, hipStream_t st, const int* gate) {
   const size_t esz = dtype == 0 ? sizeof(double) : sizeof(float);
   if (nrows == 0 || m == 0) return hipMemsetAsync(G, 0, gsize * esz, st);
   constexpr int kLdsBytes = 64 * 1024;
@@ -192,12 +196,12 @@ hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals
 #define EH_ELL(A, VALS)                                                                                  \
   if (loss == kLogistic)                                                                                 \
     hipLaunchKernelGGL((ell_rowpass<A, kLogistic, VALS>), grid1, block, 0, st, idx, (const A*)vals,      \
-                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m, (A*)G, gsize);   \
+                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m, (A*)G, gsize, gate);   \
   else                                                                                                   \
     hipLaunchKernelGGL((ell_rowpass<A, kLeastSquares, VALS>), grid1, block, 0, st, idx, (const A*)vals,  \
-                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m, (A*)G, gsize);   \
+                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m, (A*)G, gsize, gate);   \
   hipLaunchKernelGGL((ell_colpass<A, VALS>), grid2, block, sh, st, idx, (const A*)vals, (const A*)rbuf, C, \
-                     lo, width, (A*)G, nrows, ld, cap);
+                     lo, width, (A*)G, nrows, ld, cap, gate);
   if (dtype == 0) {
     if (vals) { EH_ELL(double, true) } else { EH_ELL(double, false) }
   } else {
@@ -211,7 +215,7 @@ hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, con
                               const void* vals, const void* y, const void* coef,
                               const void* beta, void* rbuf, long long nrows,
                               const long long* keys, const int* rows, const void* cvals,
-                              long long nnz, void* G, long long gsize, int ld, hipStream_t st) {
+                              long long nnz, void* G, long long gsize, int ld, hipStream_t st, const int* gate) {
   constexpr int Gs = 16;
   const dim3 block(256);
   const dim3 grid1(static_cast<unsigned>((nrows * Gs + 255) / 256));
@@ -222,18 +226,18 @@ hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, con
   if (nrows == 0) return hipSuccess;
   if (dtype == 0) {
     if (loss == kLogistic)
-      hipLaunchKernelGGL((csr_rowpass<double, kLogistic, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const double*)vals, (const double*)y, (const double*)coef, (const double*)beta, (double*)rbuf, nrows, ld);
+      hipLaunchKernelGGL((csr_rowpass<double, kLogistic, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const double*)vals, (const double*)y, (const double*)coef, (const double*)beta, (double*)rbuf, nrows, ld, gate);
     else
-      hipLaunchKernelGGL((csr_rowpass<double, kLeastSquares, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const double*)vals, (const double*)y, (const double*)coef, (const double*)beta, (double*)rbuf, nrows, ld);
+      hipLaunchKernelGGL((csr_rowpass<double, kLeastSquares, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const double*)vals, (const double*)y, (const double*)coef, (const double*)beta, (double*)rbuf, nrows, ld, gate);
     if (nnz > 0)
-      hipLaunchKernelGGL((coo_colpass<double>), grid2, block, 0, st, keys, rows, (const double*)cvals, (const double*)rbuf, (double*)G, nnz);
+      hipLaunchKernelGGL((coo_colpass<double>), grid2, block, 0, st, keys, rows, (const double*)cvals, (const double*)rbuf, (double*)G, nnz, gate);
   } else {
     if (loss == kLogistic)
-      hipLaunchKernelGGL((csr_rowpass<float, kLogistic, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const float*)vals, (const float*)y, (const float*)coef, (const float*)beta, (float*)rbuf, nrows, ld);
+      hipLaunchKernelGGL((csr_rowpass<float, kLogistic, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const float*)vals, (const float*)y, (const float*)coef, (const float*)beta, (float*)rbuf, nrows, ld, gate);
     else
-      hipLaunchKernelGGL((csr_rowpass<float, kLeastSquares, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const float*)vals, (const float*)y, (const float*)coef, (const float*)beta, (float*)rbuf, nrows, ld);
+      hipLaunchKernelGGL((csr_rowpass<float, kLeastSquares, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const float*)vals, (const float*)y, (const float*)coef, (const float*)beta, (float*)rbuf, nrows, ld, gate);
     if (nnz > 0)
-      hipLaunchKernelGGL((coo_colpass<float>), grid2, block, 0, st, keys, rows, (const float*)cvals, (const float*)rbuf, (float*)G, nnz);
+      hipLaunchKernelGGL((coo_colpass<float>), grid2, block, 0, st, keys, rows, (const float*)cvals, (const float*)rbuf, (float*)G, nnz, gate);
   }
   return hipGetLastError();
 }

@@ -28,23 +28,26 @@ struct KernelChoice;
 hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,
                              int ntasks, const void* beta, void* slab, const int* slot_task_begin,
                              int nslots, void* part, void* G, int ld, hipStream_t st, const KernelChoice& k,
-                             const PutDesc* put = nullptr);
+                             const PutDesc* put = nullptr, const int* gate = nullptr);
 hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, const void* tasks,
                                      int ntasks, const void* beta, const int* task_row_off,
                                      void* rbuf, void* slab, const int* slot_task_begin,
-                                     int nslots, void* part, void* G, int ld, hipStream_t st);
+                                     int nslots, void* part, void* G, int ld, hipStream_t st,
+                                     const int* gate = nullptr);
 hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, const int* col_idx,
                               const void* vals, const void* y, const void* coef,
                               const void* beta, void* rbuf, long long nrows,
                               const long long* keys, const int* rows, const void* cvals,
-                              long long nnz, void* G, long long gsize, int ld, hipStream_t st);
+                              long long nnz, void* G, long long gsize, int ld, hipStream_t st,
+                              const int* gate = nullptr);
 
 // ELL (constant nnz per row) variant: idx/vals column-major [m][nrows]; chunks = EllChunk
 // {row_begin, row_end, slot, pad} of rows of one message; lo/width = column window of feature k.
 hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals, const void* y,
                            const void* coef, const void* beta, void* rbuf, long long nrows, int m,
                            const void* chunks, int nchunks, const int* lo, const int* width,
-                           int max_width, void* G, long long gsize, int ld, hipStream_t st);
+                           int max_width, void* G, long long gsize, int ld, hipStream_t st,
+                           const int* gate = nullptr);
 
 // layout probes of the bf16 MFMA gradient (grad_mfma.hip): one 16x16x32 product; one transposing read
 hipError_t mfma_probe_launch(const float* A, const float* B, float* C, hipStream_t st);
@@ -53,7 +56,7 @@ hipError_t tr_probe_launch(const float* tile, int rowlen, float* out, hipStream_
 // ---- device encoding of shared-partition gradients (encode.hip) ---------------------------
 // G[slot] = sum_{k in [ptr[slot], ptr[slot+1])} coef[k] * Gb[idx[k]]; dtype 0 fp64, 1 fp32
 hipError_t encode_messages_launch(int dtype, const void* Gb, const int* ptr, const int* idx, const double* coef,
-                                  void* G, int nslots, int ld, hipStream_t st);
+                                  void* G, int nslots, int ld, hipStream_t st, const int* gate = nullptr);
 
 // ---- post-hoc evaluation GEMM (eval.hip) -----------------------------------------------
 hipError_t eval_gemm_loss_launch(int x_dtype, int loss_kind, const void* X, long long ldx,
@@ -124,7 +127,27 @@ struct PutDesc {
   // Abort word (host-mapped, nullptr = none): once non-zero, the put and its signal are skipped
   // (a pump that gave up releases its queued stream waits without announcing stale rounds).
   const int* abort;
+  // Stale-round gate of a lazy-drain worker round (engine.cpp WorkerPump::set_skip_stale; nullptr =
+  // off).  gate: this round's word (common.h gate_closed): nonzero = the round was skipped, nothing
+  // is put or announced.  next_gate: the next round's word, decided by this launch once (after the
+  // signal, or at once when skipped): 1 iff the worker's beta counter (beta_flag, its device address)
+  // has reached stale_next, i.e. the master published the beta AFTER the next round's, so the next
+  // round is stale before it starts (the replacement of the reference's send Cancel, ref
+  // src/coded.py:178-180: a late worker jumps to the newest beta instead of computing stale rounds).
+  const int* gate;
+  int* next_gate;
+  const unsigned long long* beta_flag;
+  unsigned long long stale_next;
 };
+#if defined(__HIPCC__)
+// The next round's gate word (one thread of the launch calls it).
+__device__ __forceinline__ void put_decide_next_gate(const PutDesc& p) {
+  if (!p.next_gate) return;
+  const unsigned long long b =
+      __hip_atomic_load(const_cast<unsigned long long*>(p.beta_flag), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(p.next_gate, b >= p.stale_next ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
 struct PutArgs {
   PutDesc d[kMaxPuts];
   int n;
@@ -140,7 +163,6 @@ hipError_t verify_rows_launch(const void* rows, const MsgTag* tags, int nrows, i
 // Deferred check of the mailbox rows one round decoded (integrity.h CheckList): one workgroup,
 // one wave per row; the first mismatch goes to err (host-mapped).
 hipError_t check_list_launch(const CheckList& cl, IntegrityErr* err, hipStream_t st);
-// Spin on the device for `ticks` wall_clock64 ticks (a physically late worker, --delay-mode worker).
 // Transport preflight ping-pong (transport.hip ping_pong), one block per side.
 struct PingArgs {
   unsigned long long* out_row;       // the row this side writes (the peer's memory)
@@ -154,6 +176,8 @@ struct PingArgs {
   int* status;                       // [2]: payload words that differed, 1 on a timeout
 };
 hipError_t ping_pong_launch(const PingArgs& a, bool master, hipStream_t st);
-hipError_t spin_launch(long long ticks, hipStream_t st);
+// Spin on the device for `ticks` wall_clock64 ticks (a physically late worker, --delay-on worker), after
+// the round's gradient and before its put; a skipped round (gate_closed) does not spin.
+hipError_t spin_launch(long long ticks, hipStream_t st, const int* gate = nullptr);
 
 }  // namespace eh

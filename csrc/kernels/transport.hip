@@ -44,6 +44,10 @@ __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
   const int k = blockIdx.y;
   if (k >= args.n) return;
   const PutDesc& p = args.d[k];
+  if (gate_closed(p.gate)) {  // a skipped stale round (launch-uniform): decide the next one's gate
+    if (blockIdx.x == 0 && threadIdx.x == 0) put_decide_next_gate(p);
+    return;
+  }
   if (threadIdx.x == 0) s_abort = aborted(p.abort);  // one read, shared by the block
   __syncthreads();
   if (s_abort) return;  // the pump gave up: nothing is put or announced
@@ -107,6 +111,7 @@ __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
     // the fence's write-back, letting the flag overtake it; keep the wait explicitly.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(p.flag, p.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    put_decide_next_gate(p);
   }
 }
 
@@ -146,7 +151,8 @@ __global__ void __launch_bounds__(1024) check_list(const CheckList cl, Integrity
   check_rows_waves(cl, 0, static_cast<int>(blockDim.x >> 6), err, &claim);
 }
 
-__global__ void spin_ticks(long long ticks) {
+__global__ void spin_ticks(long long ticks, const int* gate) {
+  if (gate_closed(gate)) return;
   const long long t0 = wall_clock64();
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
@@ -250,9 +256,9 @@ hipError_t check_list_launch(const CheckList& cl, IntegrityErr* err, hipStream_t
   return hipGetLastError();
 }
 
-hipError_t spin_launch(long long ticks, hipStream_t st) {
+hipError_t spin_launch(long long ticks, hipStream_t st, const int* gate) {
   if (ticks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(spin_ticks, dim3(1), dim3(64), 0, st, ticks);
+  hipLaunchKernelGGL(spin_ticks, dim3(1), dim3(64), 0, st, ticks, gate);
   return hipGetLastError();
 }
 

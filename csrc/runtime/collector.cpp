@@ -29,6 +29,7 @@ Collector::Collector(int n_workers, std::vector<int> group_of, int n_groups)
   group_done_.assign(std::max(n_groups_, 1), 0);
   nsh_.assign(2 * W_, 1);
   got_sh_.assign(2 * W_, 0);
+  last_seen_.assign(2 * W_, -kInf);
 }
 
 void Collector::set_shards(int worker, int part, int n) {
@@ -72,32 +73,43 @@ void Collector::begin_round(int round, double t_start, int rule, int k) {
   tie_.assign(W_, 0);
   if (tie_seed_ >= 0)
     for (int w = 0; w < W_; ++w) tie_[w] = tie_key(tie_seed_, round, w);
+  // the start of this round decides whether a worker still busy with the previous one skips it
+  if (skip_stale_)
+    for (int id : live_) maybe_skip(probes_[id]);
 }
 
-int Collector::add_event_probe(int worker, int part, int round, uintptr_t event, double delay) {
-  if (worker < 0 || worker >= W_) throw std::invalid_argument("Collector: bad worker");
-  Probe p{worker, part, round, reinterpret_cast<hipEvent_t>(event), nullptr, 0, false, false, false, 0.0, delay, kInf};
+int Collector::add_probe(const Probe& p) {
+  if (p.worker < 0 || p.worker >= W_) throw std::invalid_argument("Collector: bad worker");
+  if (p.part < 0 || p.part > 1) throw std::invalid_argument("Collector: bad part");
   probes_.push_back(p);
   live_.push_back(static_cast<int>(probes_.size()) - 1);
   return static_cast<int>(probes_.size()) - 1;
 }
 
-int Collector::add_host_probe(int worker, int part, int round, double delay) {
-  if (worker < 0 || worker >= W_) throw std::invalid_argument("Collector: bad worker");
-  Probe p{worker, part, round, nullptr, nullptr, 0, true, false, false, 0.0, delay, kInf};
-  probes_.push_back(p);
-  live_.push_back(static_cast<int>(probes_.size()) - 1);
-  return static_cast<int>(probes_.size()) - 1;
+int Collector::add_event_probe(int worker, int part, int round, uintptr_t event, double delay, bool physical) {
+  return add_probe(Probe{worker, part, round, reinterpret_cast<hipEvent_t>(event), nullptr, 0, false, false, false, 0.0,
+                         delay, kInf, physical, false, 0.0});
 }
 
-int Collector::add_flag_probe(int worker, int part, int round, uintptr_t flag_addr, uint64_t value, double delay) {
-  if (worker < 0 || worker >= W_) throw std::invalid_argument("Collector: bad worker");
+int Collector::add_host_probe(int worker, int part, int round, double delay, bool physical) {
+  return add_probe(Probe{worker, part, round, nullptr, nullptr, 0, true, false, false, 0.0, delay, kInf, physical,
+                         false, 0.0});
+}
+
+int Collector::add_flag_probe(int worker, int part, int round, uintptr_t flag_addr, uint64_t value, double delay,
+                              bool physical) {
   if (flag_addr == 0) throw std::invalid_argument("Collector: null flag");
-  Probe p{worker, part, round, nullptr, reinterpret_cast<const uint64_t*>(flag_addr), value, false, false, false,
-          0.0, delay, kInf};
-  probes_.push_back(p);
-  live_.push_back(static_cast<int>(probes_.size()) - 1);
-  return static_cast<int>(probes_.size()) - 1;
+  return add_probe(Probe{worker, part, round, nullptr, reinterpret_cast<const uint64_t*>(flag_addr), value, false,
+                         false, false, 0.0, delay, kInf, physical, false, 0.0});
+}
+
+bool Collector::maybe_skip(Probe& p) {
+  if (!skip_stale_ || p.physical || !p.seen || p.arrived || p.round >= round_) return false;
+  if (p.start < round_start_[p.round + 1]) return false;  // the worker began it before the next beta
+  p.skipped = p.arrived = true;
+  ++n_skipped_;
+  finish_[p.worker][p.round] = finish_of(p.worker, p.round - 1);  // never ran: the finish carries over
+  return true;
 }
 
 double Collector::finish_of(int worker, int round) const {
@@ -109,15 +121,23 @@ double Collector::finish_of(int worker, int round) const {
 
 void Collector::mark_seen(int id, double t) {
   Probe& p = probes_.at(id);
-  if (p.seen) return;
+  if (p.seen || p.arrived) return;
   p.seen = true;
   p.t_seen = t;
   const double ts = p.round < static_cast<int>(round_start_.size()) ? round_start_[p.round] : t;
-  const double start = std::max(ts, finish_of(p.worker, p.round - 1));
-  const double compute = std::max(0.0, t - ts);
-  p.ready = start + compute + p.delay;
+  double& last = last_seen_[2 * p.worker + (p.part ? 1 : 0)];
+  const double busy_from = std::max(ts, last);  // this round's work began after the previous round's
+  last = std::max(last, t);
   auto& f = finish_[p.worker];
   if (static_cast<int>(f.size()) <= p.round) f.resize(p.round + 1, -kInf);
+  if (p.physical) {  // a really late rank: seen = arrived
+    p.start = ts;
+    p.ready = t + p.delay;
+  } else {
+    p.start = std::max(ts, finish_of(p.worker, p.round - 1));
+    p.ready = p.start + std::max(0.0, t - busy_from) + p.delay;
+    if (maybe_skip(p)) return;
+  }
   f[p.round] = std::max(f[p.round], p.ready);
 }
 
@@ -128,7 +148,7 @@ void Collector::poll_events(double t) {
   std::vector<std::pair<hipEvent_t, bool>> done;
   for (int id : live_) {
     Probe& p = probes_[id];
-    if (p.seen || p.host) continue;
+    if (p.seen || p.host || p.arrived) continue;
     if (p.flag) {
       if (__atomic_load_n(p.flag, __ATOMIC_ACQUIRE) >= p.fval) mark_seen(id, t);
       continue;
@@ -159,13 +179,19 @@ bool Collector::rule_holds() const {
 }
 
 bool Collector::process_ready(double t, bool /*stop_at_rule*/) {
-  // Ready probes, in virtual arrival order.
+  // Ready probes, in virtual arrival order (skipped ones leave the live list here too).
   std::vector<int> ready;
+  bool gone = false;
   for (int id : live_) {
     const Probe& p = probes_[id];
-    if (p.seen && p.ready <= t) ready.push_back(id);
+    gone |= p.arrived;
+    if (!p.arrived && p.seen && p.ready <= t) ready.push_back(id);
   }
-  if (ready.empty()) return stopped_;
+  if (ready.empty()) {
+    if (gone)
+      live_.erase(std::remove_if(live_.begin(), live_.end(), [&](int id) { return probes_[id].arrived; }), live_.end());
+    return stopped_;
+  }
   std::sort(ready.begin(), ready.end(), [&](int a, int b) {
     const Probe& pa = probes_[a];
     const Probe& pb = probes_[b];
@@ -178,7 +204,10 @@ bool Collector::process_ready(double t, bool /*stop_at_rule*/) {
     Probe& p = probes_[id];
     p.arrived = true;
     const Arrival a{p.worker, p.part, p.round, p.ready - round_start_[p.round], id};
-    if (p.round != round_) continue;  // stale message of an earlier round: drained, ignored
+    if (p.round != round_) {  // stale message of an earlier round: drained, ignored
+      ++n_stale_;
+      continue;
+    }
     const int mi = 2 * p.worker + (p.part ? 1 : 0);
     if (++got_sh_[mi] < nsh_[mi]) continue;  // more shards of this message still to come
     if (stopped_) {
@@ -234,11 +263,11 @@ bool Collector::wait(double timeout) {
     double next = kInf;
     for (int id : live_) {
       const Probe& p = probes_[id];
-      if (p.seen) next = std::min(next, p.ready);
+      if (p.seen && !p.arrived) next = std::min(next, p.ready);
     }
     bool unseen_event = false;
     for (int id : live_)
-      if (!probes_[id].seen && !probes_[id].host) { unseen_event = true; break; }
+      if (!probes_[id].seen && !probes_[id].host && !probes_[id].arrived) { unseen_event = true; break; }
     double dt = next - t;
     if (unseen_event) dt = std::min(dt, 2e-5);  // keep polling hardware events tightly
     dt = std::min(dt, t_start_ + timeout - t);
@@ -257,7 +286,7 @@ bool Collector::drain(int round, double timeout) {
     bool unseen_event = false;
     for (int id : live_) {
       const Probe& p = probes_[id];
-      if (p.round > round) continue;
+      if (p.round > round || p.arrived) continue;
       if (p.seen && std::isinf(p.delay)) continue;  // dead worker: its message was received
       left = true;
       if (p.seen) next = std::min(next, p.ready);
@@ -280,7 +309,7 @@ bool Collector::wait_seen(int round, double timeout) {
     bool left = false;
     for (int id : live_) {
       const Probe& p = probes_[id];
-      if (p.round <= round && !p.seen) {
+      if (p.round <= round && !p.seen && !p.arrived) {
         left = true;
         break;
       }
@@ -296,13 +325,17 @@ std::vector<Arrival> Collector::late_arrivals(int round) const {
   return late_;
 }
 
-int Collector::pending() const { return static_cast<int>(live_.size()); }
+int Collector::pending() const {
+  int n = 0;
+  for (int id : live_) n += probes_[id].arrived ? 0 : 1;
+  return n;
+}
 
 int Collector::pending_upto(int round) const {
   int n = 0;
   for (int id : live_) {
     const Probe& p = probes_[id];
-    if (p.round > round) continue;
+    if (p.round > round || p.arrived) continue;
     if (p.seen && std::isinf(p.delay)) continue;
     ++n;
   }

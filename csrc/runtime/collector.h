@@ -35,6 +35,19 @@
 // round to round.  Ordering such ties by worker id instead would let AGC stop on the same
 // k workers every round and never cover the last FRC groups' partitions.  tie_seed < 0
 // restores the plain probe (worker) order.
+//
+// Physical probes: with physically late worker ranks (--delay-on worker) a remote message's seen
+// time IS its arrival (ready = t_seen, or +inf for a dead worker): no virtual carry-over, the rank
+// really was late.  Compute time of a virtual probe is the physical busy time of THIS round:
+// t_seen - max(t_start, the previous round's seen time of that message), so work queued behind an
+// earlier round on one stream is not counted twice when lag carries over.
+//
+// Stale-round skipping (drain "lazy", engine/trainer.py): a worker that is still busy with an
+// earlier round when the round AFTER a probe's round begins skips that round, exactly like a
+// physical worker whose gate finds the next beta already published (csrc/kernels/common.h
+// gate_closed): the probe never arrives, the worker's finish time carries over to its next round.
+// The decision for a probe of round j is taken when round j+1 begins (or when the probe is seen, if
+// later): skipped iff its virtual start max(t_start(j), finish(w, j-1)) >= t_start(j+1).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -74,12 +87,22 @@ class Collector {
   static uint64_t tie_key(int64_t seed, int round, int worker);
   // Message (worker, part) is delivered as n >= 1 shards (probes); default 1.
   void set_shards(int worker, int part, int n);
-  int add_event_probe(int worker, int part, int round, uintptr_t event, double delay);
-  int add_host_probe(int worker, int part, int round, double delay);
+  // physical: the probe's seen time is its arrival (see "Physical probes" above).
+  int add_event_probe(int worker, int part, int round, uintptr_t event, double delay, bool physical = false);
+  int add_host_probe(int worker, int part, int round, double delay, bool physical = false);
   // IPC mailbox probe: arrived once the 64-bit flag at `flag_addr` (shared host memory,
   // release-stored by the sending GPU) reaches `value` (csrc/runtime/ipc.cpp).
-  int add_flag_probe(int worker, int part, int round, uintptr_t flag_addr, uint64_t value, double delay);
+  int add_flag_probe(int worker, int part, int round, uintptr_t flag_addr, uint64_t value, double delay,
+                     bool physical = false);
   void mark_seen(int probe, double t);
+  // Stale-round skipping of virtual probes (drain "lazy"; see above).  Off: lag carries over and
+  // every round's message is delivered in order (the reference's no-Waitall schemes).
+  void set_skip_stale(bool on) { skip_stale_ = on; }
+  bool skip_stale() const { return skip_stale_; }
+  // Virtual probes skipped as stale so far, and stale arrivals (a round's message after the round
+  // ended: drained, never decoded).
+  int skipped() const { return n_skipped_; }
+  int stale_arrivals() const { return n_stale_; }
 
   // Process everything that is ready; returns true once the current round's stop rule holds.
   bool step();
@@ -111,7 +134,13 @@ class Collector {
     double t_seen;
     double delay;
     double ready;
+    bool physical;
+    bool skipped;
+    double start;  // virtual start (seen virtual probes)
   };
+  int add_probe(const Probe& p);
+  // Skip a seen virtual probe whose next round began before its start (skip_stale_).
+  bool maybe_skip(Probe& p);
   void poll_events(double t);
   bool process_ready(double t, bool stop_at_rule);
   bool rule_holds() const;
@@ -131,6 +160,9 @@ class Collector {
   std::vector<int> got_sh_;    // [2 * worker + part] shards of the current round ready so far
   std::vector<double> round_start_;
   std::vector<std::vector<double>> finish_;  // [worker][round] virtual finish
+  std::vector<double> last_seen_;            // [2 * worker + part] seen time of the latest probe
+  bool skip_stale_ = false;
+  int n_skipped_ = 0, n_stale_ = 0;
   std::vector<Probe> probes_;
   std::vector<int> live_;  // probe ids not yet arrived
   std::vector<Arrival> cur_;

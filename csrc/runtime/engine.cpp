@@ -136,11 +136,12 @@ struct GradLauncher {
   int enc_slots = 0;
   std::vector<Tensor> keep;
 
-  hipError_t launch(const void* beta, void* G, hipStream_t st) const {
-    if (!Gb) return launch_raw(beta, G, st);
-    const hipError_t e = launch_raw(beta, Gb, st);
+  // gate: a lazy-drain worker round's stale-round gate (common.h gate_closed); nullptr = always run
+  hipError_t launch(const void* beta, void* G, hipStream_t st, const int* gate = nullptr) const {
+    if (!Gb) return launch_raw(beta, G, st, gate);
+    const hipError_t e = launch_raw(beta, Gb, st, gate);
     if (e != hipSuccess) return e;
-    return eh::encode_messages_launch(acc, Gb, enc_ptr, enc_idx, enc_coef, G, enc_slots, ld, st);
+    return eh::encode_messages_launch(acc, Gb, enc_ptr, enc_idx, enc_coef, G, enc_slots, ld, st, gate);
   }
 
   // Dense fused plans without device encoding can hand their result rows straight to the
@@ -154,25 +155,25 @@ struct GradLauncher {
   }
   hipError_t launch_put(const void* beta, void* G, const eh::PutDesc& put, hipStream_t st) const {
     return eh::grad_dense_launch(dtype, loss, cpl, segs, tasks, ntasks, beta, slab, stb, nslots, part, G, ld, st,
-                                 choice, &put);
+                                 choice, &put, put.gate);
   }
 
-  hipError_t launch_raw(const void* beta, void* G, hipStream_t st) const {
+  hipError_t launch_raw(const void* beta, void* G, hipStream_t st, const int* gate = nullptr) const {
     switch (kind) {
       case 0:
         return ntasks ? eh::grad_dense_launch(dtype, loss, cpl, segs, tasks, ntasks, beta, slab, stb, nslots, part, G,
-                                              ld, st, choice)
+                                              ld, st, choice, nullptr, gate)
                       : hipSuccess;
       case 1:
         return ntasks ? eh::grad_dense_twopass_launch(dtype, loss, segs, tasks, ntasks, beta, task_row_off, rbuf, slab,
-                                                      stb, nslots, part, G, ld, st)
+                                                      stb, nslots, part, G, ld, st, gate)
                       : hipSuccess;
       case 2:
         return eh::grad_sparse_launch(acc, loss, row_ptr, col_idx, vals, y, coef, beta, rbuf, nrows, keys, rows,
-                                      cvals, nnz, G, static_cast<long long>(nslots) * ld, ld, st);
+                                      cvals, nnz, G, static_cast<long long>(nslots) * ld, ld, st, gate);
       case 3:
         return eh::grad_ell_launch(acc, loss, ell_idx, ell_vals, y, coef, beta, rbuf, nrows, m, chunks, nchunks, lo,
-                                   width, max_width, G, static_cast<long long>(nslots) * ld, ld, st);
+                                   width, max_width, G, static_cast<long long>(nslots) * ld, ld, st, gate);
       default:
         return hipErrorInvalidValue;
     }
@@ -568,6 +569,24 @@ class MasterPump {
     need((int64_t)delays.size() >= (int64_t)R_ * W_, "remote delays must be [R*W]");
     remote_delays_ = delays;
   }
+  // Drain "lazy" (engine/trainer.py): the collector skips stale virtual rounds (collector.h) and, with
+  // IPC targets, finish_run() tells every worker rank the run is over so its queued rounds are stale.
+  void set_skip_stale(bool on) {
+    skip_ = on;
+    col_->set_skip_stale(on);
+  }
+  // End of the master's rounds (stream-ordered after its last beta put): with skip_stale on, every
+  // worker's beta counter goes to R + 1 (as if beta(R) were out), so whatever a late worker rank still
+  // has queued is stale and skipped (its gate), and its final signal lets the collector drain.
+  void finish_run() {
+    if (!skip_ || comm_) return;
+    for (const auto& t : targets_)
+      hcheck(eh::signal_launch(reinterpret_cast<unsigned long long*>(t.second), static_cast<unsigned long long>(R_) + 1,
+                               stream_),
+             "signal(end of run)");
+  }
+  int skipped() const { return col_->skipped(); }
+  int stale_arrivals() const { return col_->stale_arrivals(); }
   // --slow-ranks: this rank launches its local gradient `n` times per round (a slower GPU).
   void set_repeat(int n) {
     need(n >= 1, "repeat must be >= 1");
@@ -625,12 +644,13 @@ class MasterPump {
         hipEvent_t ev = rev_[static_cast<size_t>(slot) * comm_ranks_.size() + k];
         hcheck(hipEventRecord(ev, rs), "hipEventRecord(recv)");
         for (const auto& m : remote_)
-          if (m.row >= row0 && m.row < row0 + n) col_->add_event_probe(m.w, m.p, i, reinterpret_cast<uintptr_t>(ev), dr[m.w]);
+          if (m.row >= row0 && m.row < row0 + n)
+            col_->add_event_probe(m.w, m.p, i, reinterpret_cast<uintptr_t>(ev), dr[m.w], !remote_delays_.empty());
       }
       return;
     }
-    for (const auto& m : remote_)
-      col_->add_flag_probe(m.w, m.p, i, m.flag, static_cast<uint64_t>(i + 1), dr[m.w]);
+    for (const auto& m : remote_)  // physically late ranks (remote delays set): seen = arrived
+      col_->add_flag_probe(m.w, m.p, i, m.flag, static_cast<uint64_t>(i + 1), dr[m.w], !remote_delays_.empty());
   }
 
   // Returns (status, arrivals [(worker, part, t_rel)], t_start, t_decoded, t_end, t_waited):
@@ -805,7 +825,6 @@ class MasterPump {
     if ((int)arb_src_.size() > eh::kArbMaxSrc) return "more than 64 worker ranks";
     if (W_ > eh::kArbMaxW) return "more than 64 workers";
     if ((int)(local_.size() + remote_.size()) > eh::kArbMaxProbes) return "too many message shards";
-    if (!drain_ && stop_rule_ != eh::kRuleAll) return "scheme without a drain (late messages cross rounds)";
     if ((decode_kind_ == kTable || decode_kind_ == kPartialTable) && W_ > 16) return "decode table too large";
     size_t rows = 0;  // worst case of one decode: every buffer row of every message
     for (const auto& ix : index_) {
@@ -1239,12 +1258,16 @@ class MasterPump {
     hcheck(eh::check_list_launch(check_, static_cast<eh::IntegrityErr*>(err_->dev), stream_), "check_list");
   }
 
+  // No virtual delay applies in round i: the local messages' entries of the delay table and the remote
+  // ones of the remote table (a physically late rank's own lateness is no virtual delay).
   bool no_delay(int i) const {
-    const auto zero = [](double x) { return x == 0.0; };
     const double* dl = delays_.data() + static_cast<int64_t>(i) * W_;
-    if (!std::all_of(dl, dl + W_, zero)) return false;
     const double* dr = remote_delays_.empty() ? dl : remote_delays_.data() + static_cast<int64_t>(i) * W_;
-    return std::all_of(dr, dr + W_, zero);
+    for (const auto& m : local_)
+      if (dl[m.w] != 0.0) return false;
+    for (const auto& m : remote_)
+      if (dr[m.w] != 0.0) return false;
+    return true;
   }
 
   double after_combine(int i, bool publish_next) {
@@ -1321,6 +1344,7 @@ class MasterPump {
   int repeat_ = 1;
   int update_rule_ = 0, stop_rule_ = 0, k_ = 0;
   bool drain_ = false;
+  bool skip_ = false;  // drain "lazy": stale-round skipping (set_skip_stale)
   int decode_kind_ = kSumPart0, n_groups_ = 1;
   std::vector<int> group_of_;
   std::map<uint64_t, std::vector<double>> table_;
@@ -1421,6 +1445,32 @@ class WorkerPump {
     repeat_ = n;
   }
 
+  // Drain "lazy": stale-round skipping (the replacement of the reference's send Cancel, ref
+  // src/coded.py:178-180).  Every round's kernels carry a gate word (common.h gate_closed); round i's
+  // put decides round i+1's: skip it iff this rank's beta counter (beta_flag_dev, its device address)
+  // already says beta(i+2) is out, i.e. the master finished round i+1 before this rank could start it.
+  // Decided on the device when the previous round ends, so a rank that fell behind (a late spin, a
+  // slow GPU) jumps to the newest beta instead of computing stale rounds.  IPC mailbox only (RCCL has
+  // no cancel: a skipped send would desynchronise the FIFO pairing).
+  void set_skip_stale(uintptr_t beta_flag_dev) {
+    need(!comm_, "stale-round skipping needs the IPC mailbox (p2p sends cannot be skipped)");
+    need(beta_flag_dev != 0, "null beta flag");
+    skip_flag_ = reinterpret_cast<const unsigned long long*>(beta_flag_dev);
+    gate_ = at::zeros({R_ + 1}, at::TensorOptions().dtype(at::kInt).device(at::Device(at::kCUDA, device_)));
+  }
+  bool skip_stale() const { return skip_flag_ != nullptr; }
+  // Rounds this rank skipped as stale (syncs the stream).
+  std::vector<int> skipped_rounds() {
+    std::vector<int> out;
+    if (!gate_.defined()) return out;
+    hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    const Tensor g = gate_.cpu();
+    const int* v = g.data_ptr<int>();
+    for (int i = 0; i < R_; ++i)
+      if (v[i]) out.push_back(i);
+    return out;
+  }
+
   // Integrity tags (csrc/kernels/integrity.h): mbox_tags = this rank's view of the master
   // mailbox's tag slots [K][mbox_rows]; inbox_tags = its own inbox's tag slots [R + 1].  Every
   // message put carries a tag per row; every beta is checked after the round that read it.
@@ -1492,6 +1542,15 @@ class WorkerPump {
                      bytes, mflag_, static_cast<unsigned long long>(i + 1),
                      reinterpret_cast<unsigned int*>(counters_.data_ptr<int>())};
       pd.abort = static_cast<const int*>(abort_->dev);
+      const int* gate = nullptr;  // stale-round gate of this round (set_skip_stale)
+      if (skip_flag_) {
+        int* gw = gate_.data_ptr<int>();
+        gate = gw + i;
+        pd.gate = gate;
+        pd.next_gate = gw + i + 1;
+        pd.beta_flag = skip_flag_;
+        pd.stale_next = static_cast<unsigned long long>(i) + 3;  // round i+1 is stale once beta(i+2) is out
+      }
       if (tags_) {
         pd.tag = mtags_ + static_cast<int64_t>(slot) * mbox_rows_ + row0_;
         pd.csum = reinterpret_cast<unsigned long long*>(csum_.data_ptr<int64_t>());
@@ -1501,15 +1560,15 @@ class WorkerPump {
         pd.corrupt = sabotage("msg", rank_, i) ? 1 : 0;
       }
       if (timing_) record_t(i, 0);
-      for (int k = 1; k < repeat_; ++k) hcheck(g_->launch(beta, g, stream_), "worker gradient (slow rank)");
+      for (int k = 1; k < repeat_; ++k) hcheck(g_->launch(beta, g, stream_, gate), "worker gradient (slow rank)");
       if (fuse_put_) {  // gradient + put + signal in one stream order, no separate put kernel
         hcheck(g_->launch_put(beta, g, pd, stream_), "worker gradient + put");
         if (timing_) record_t(i, 1);
       } else {
-        hcheck(g_->launch(beta, g, stream_), "worker gradient");
+        hcheck(g_->launch(beta, g, stream_, gate), "worker gradient");
         if (timing_) record_t(i, 1);
         if (!late_ticks_.empty() && late_ticks_[i] > 0)  // after compute, before the send (ref src/naive.py:141-148)
-          hcheck(eh::spin_launch(late_ticks_[i], stream_), "late worker spin");
+          hcheck(eh::spin_launch(late_ticks_[i], stream_, gate), "late worker spin");
         eh::PutArgs pa{};
         pa.n = 1;
         pa.d[0] = pd;
@@ -1523,6 +1582,8 @@ class WorkerPump {
                "verify_rows(beta)");
     }
     if (dwait_ && b > a && !host_wait(b, b - 1)) return release(b - 1);
+    if (skip_flag_ && b == R_ && n_ > 0)  // every round is put or skipped: the master's collector can drain
+      hcheck(eh::signal_launch(mflag_, static_cast<unsigned long long>(R_), stream_), "signal(rounds done)");
     if (tags_) {  // the last rounds' checks
       hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
       check_integrity();
@@ -1650,6 +1711,8 @@ class WorkerPump {
   std::unique_ptr<HostMapped> abort_;    // int: queued puts skip themselves once set
   Tensor csum_;                          // tagged put checksum scratch [kMaxTagRows]
   std::vector<long long> late_ticks_;    // [R] device spin before the put (--delay-on worker)
+  const unsigned long long* skip_flag_ = nullptr;  // beta counter read by the stale-round gates (lazy drain)
+  Tensor gate_;                          // int32 [R + 1] stale-round gates (1 = round skipped)
   int repeat_ = 1;                       // gradient launches per round (--slow-ranks)
   int device_ = 0;
   std::shared_ptr<eh::P2PComm> comm_;    // stream-ordered p2p (null: IPC mailbox)
@@ -1707,6 +1770,10 @@ void bind_engine(py::module& m) {
       .def("set_comm", &MasterPump::set_comm, py::arg("comm"), py::arg("ranks"), py::arg("peers"))
       .def_property_readonly("comm_kind", &MasterPump::comm_kind)
       .def("set_repeat", &MasterPump::set_repeat)
+      .def("set_skip_stale", &MasterPump::set_skip_stale, py::arg("on"))
+      .def("finish_run", &MasterPump::finish_run)
+      .def_property_readonly("skipped", &MasterPump::skipped)
+      .def_property_readonly("stale_arrivals", &MasterPump::stale_arrivals)
       .def("set_integrity", &MasterPump::set_integrity, py::arg("mbox_tags"), py::arg("inbox_tag_off"), py::arg("on"))
       .def_property_readonly("integrity", &MasterPump::integrity)
       .def("check_integrity", &MasterPump::check_integrity)
@@ -1745,6 +1812,9 @@ void bind_engine(py::module& m) {
       .def("set_timing", &WorkerPump::set_timing)
       .def("set_delays", &WorkerPump::set_delays)
       .def("set_repeat", &WorkerPump::set_repeat)
+      .def("set_skip_stale", &WorkerPump::set_skip_stale, py::arg("beta_flag_dev"))
+      .def_property_readonly("skip_stale", &WorkerPump::skip_stale)
+      .def("skipped_rounds", &WorkerPump::skipped_rounds)
       .def("set_integrity", &WorkerPump::set_integrity, py::arg("mbox_tags"), py::arg("inbox_tags"), py::arg("rank"),
            py::arg("on"))
       .def("check_integrity", &WorkerPump::check_integrity)

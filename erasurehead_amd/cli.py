@@ -40,7 +40,11 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--data", default="files", choices=["files", "synthetic"])
     g.add_argument("--data-seed", type=int, default=0)
     g.add_argument("--allow-uneven-groups", action="store_true")
-    g.add_argument("--drain", default=None, choices=["all", "lazy"])
+    g.add_argument("--drain", default=None, choices=["all", "carry", "lazy"],
+                   help="straggler tail after the stop rule: all = the master waits for every message before the "
+                        "next beta (ref Waitall, FRC/AGC default); carry = no wait, late workers deliver every round "
+                        "in order (the reference's other schemes); lazy = no wait, and a worker still busy when the "
+                        "next beta is out skips the stale round (default: the scheme's reference behaviour)")
     g.add_argument("--delay-mode", default="exp", choices=["exp", "fixed", "none", "worker"],
                    help="injected delay distribution; worker = exp slept on the worker rank (--delay-on worker)")
     g.add_argument("--delay-on", default="collector", choices=["collector", "worker"],
@@ -75,7 +79,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="order of simultaneous arrivals: seeded per-round worker permutation (default) or worker id")
     g.add_argument("--tie-seed", type=int, default=0)
     g.add_argument("--shard", default="auto", choices=["auto", "message", "partition"],
-                   help="placement unit on several ranks: whole messages or partition shards (auto: shards)")
+                   help="placement unit on several ranks: whole messages, the reference topology (auto) or "
+                        "partition shards (bandwidth, no physical straggler tolerance)")
     g.add_argument("--no-integrity", action="store_true",
                    help="IPC messages without (round, rank, checksum) tags (A/B runs only)")
     return p

@@ -49,7 +49,10 @@ class RunConfig:
     data: str = "files"  # files | synthetic (on-device generator, no files)
     data_seed: int = 0
     allow_uneven_groups: bool = False  # FRC with W % (s+1) != 0
-    drain: Optional[str] = None  # None = scheme default; "all" | "lazy"
+    # straggler tail after the stop rule (engine/trainer.py): None = the scheme's reference behaviour
+    # ("all" for FRC/AGC, ref src/approximate_coding.py:182-183; "carry" for the rest, which never
+    # Waitall); "all" | "carry" | "lazy" (no wait + stale-round skipping on the workers)
+    drain: Optional[str] = None
     delay_mode: str = "exp"  # exp (reference) | fixed | none
     # where an injected delay happens: "collector" (a virtual arrival time on the master's clock, the
     # GPUs never idle) or "worker" (the worker rank is physically late: its messages leave after a
@@ -103,6 +106,8 @@ class RunConfig:
             self.delay_mode, self.delay_on = "exp", "worker"
         if self.delay_on not in ("collector", "worker"):
             raise ValueError("delay_on must be collector or worker")
+        if self.drain not in (None, "all", "carry", "lazy"):
+            raise ValueError("drain must be all, carry or lazy")
         if any(int(f) < 1 for f in self.slow_ranks.values()):
             raise ValueError("slow rank factors must be integers >= 1")
 

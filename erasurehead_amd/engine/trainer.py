@@ -20,8 +20,16 @@ MI355X design:
     ring buffers are protected by device-side event waits;
   * every buffer is per (round mod K) — no aliasing of beta or message buffers across
     rounds (the reference's latent races, SURVEY §5.2, cannot happen);
-  * the injected straggler delay is a virtual arrival time (utils/delay.py), so the
-    same wall-clock semantics as the reference hold while the GPUs never sleep.
+  * the injected straggler delay is, by default, a virtual arrival time on the master's
+    clock (utils/delay.py, --delay-on collector: the GPUs never sleep); with --delay-on worker
+    a worker rank is physically late instead (a device spin between its gradient and its
+    put, like the reference's time.sleep) and --slow-ranks makes a GPU really slower;
+  * the straggler tail after the stop rule (``drain``): "all" waits for every message before
+    the next beta (the reference's Waitall, FRC/AGC), "carry" does not wait and late workers
+    deliver every round in order (the reference's other schemes), "lazy" does not wait and a
+    worker still busy when the next beta is out skips the stale round (csrc/kernels/common.h
+    gate_closed; the collector models the same skip for virtual delays) — the replacement of
+    the reference's send Cancel (ref src/coded.py:178-180).
 """
 from __future__ import annotations
 
@@ -36,6 +44,7 @@ import torch
 import torch.distributed as dist
 
 from .._ext import native as native_ext
+from .loops import LoopInputs, select_round_loop
 from ..codes.schemes import Arrival, Scheme, SchemeError, make_scheme, scheme_key
 from ..config import RunConfig
 from ..data import io as dio
@@ -144,7 +153,9 @@ class Trainer:
         self.rule_kind, self.rule_k = scheme.rule()
         self.update = UpdateRule("AGD" if scheme.fixed_agd else cfg.update_rule, cfg.alpha_value, cfg.n_rows,
                                  scheme.grad_scale())
-        self.drain = scheme.drain if cfg.drain is None else cfg.drain == "all"
+        self.drain_mode = cfg.drain or ("all" if scheme.drain else "carry")
+        self.drain = self.drain_mode == "all"
+        self.skip_stale = self.drain_mode == "lazy"
         inject = cfg.add_delay == 1 and (scheme.has_delay or cfg.force_delay)
         mode = "none"
         if inject:
@@ -349,6 +360,7 @@ class Trainer:
                     log(line)
         start = env.broadcast_object(start, 0)
         env.barrier()
+        self.loop, self.loop_reason = select_round_loop(self.loop_inputs(start))
         native_loop = self.native_loop
         if env.is_master:
             res = (self._master_loop_native if native_loop else self._master_loop)(timed_start, log, start)
@@ -356,14 +368,43 @@ class Trainer:
             res = (self._worker_loop_native if native_loop else self._worker_loop)(timed_start, start)
         return res
 
+    def loop_inputs(self, start: int = 0, blocker: str = "") -> LoopInputs:
+        """This run's facts for engine/loops.py select_round_loop (the same on every rank)."""
+        cfg, sch, R = self.cfg, self.scheme, self.cfg.num_itrs
+        W, s = cfg.n_workers, sch.n_stragglers
+        table = sch.decode_kind in (3, 4)
+        tx = self.tx
+        if self.env.world > 1:
+            d = self.delay_table()[start:]
+            r = self._remote_delays(d) if d.size else d
+            local = sorted({u.worker for u, o in zip(self.shards, self.owner) if o == 0})
+            remote = sorted({u.worker for u, o in zip(self.shards, self.owner) if o != 0})
+            virtual = bool(d.size) and (bool(np.any(d[:, local] != 0)) or bool(np.any(r[:, remote] != 0)))
+        else:
+            d = self.delay_table()[start:]
+            virtual = bool(d.size) and bool(np.any(d != 0))
+        return LoopInputs(
+            gpu=bool(self.env.gpu), world=self.env.world,
+            transport="local" if tx is None else ("gloo" if not self.env.gpu else tx.name),
+            virtual_delay=virtual, physical_delay=bool(self.physical or self.cfg.slow_ranks),
+            drain=self.drain_mode, instrument=bool(cfg.instrument), checkpoint=bool(cfg.checkpoint_every),
+            resume=bool(start), verify_beta=bool(cfg.verify_beta), native_loop=bool(cfg.native_loop),
+            device_loop=cfg.device_loop, device_master=os.environ.get("ERASUREHEAD_DEVICE_MASTER", "auto"),
+            shared_gpu=bool(tx is not None and self._shared_gpu(tx)), has_local=bool(self.local_msgs),
+            table_w64=table and W > 64, table_ondemand=table and math.comb(W, s) > 20000, blocker=blocker)
+
+    def delay_table(self) -> np.ndarray:
+        """[R, W] injected delay of every logical worker in every round (utils/delay.py)."""
+        R, W = self.cfg.num_itrs, self.cfg.n_workers
+        return np.stack([self.delay.delays(i) for i in range(R)]) if R else np.zeros((0, W))
+
     @property
     def native_loop(self) -> bool:
-        """Run rounds in the C++ executors (GPU; single process or the IPC transport)."""
-        if not (self.env.gpu and self.cfg.native_loop) or self.cfg.verify_beta:
-            return False
-        if self.tx is not None and self.tx.name not in ("ipc", "rccl", "loopback"):
-            return False
-        if self.scheme.decode_kind in (3, 4) and self.cfg.n_workers > 64:  # 64-bit completion masks
+        """Run rounds in the C++ executors (engine/loops.py: every master loop but "python"; a worker
+        rank without messages only waits for beta, which the Python loop does as well)."""
+        if not hasattr(self, "loop"):
+            self.loop, self.loop_reason = select_round_loop(self.loop_inputs())
+        if self.loop == "python":
             return False
         return self.n_loc > 0 or self.env.is_master
 
@@ -378,12 +419,13 @@ class Trainer:
         eta = cfg.eta()
         col = ArrivalCollector(W, sch.group_of, sch.n_groups, env.gpu, cfg.tie_seed_value)
         col.set_shards(self.n_shards)
+        col.set_skip_stale(self.skip_stale)
         timeset = np.zeros(R)
         loop_time = np.zeros(R)
         worker_timeset = np.zeros((R, W))
         arrivals_log: List = [[] for _ in range(start)]
         upd_events: List = []
-        delay_table = np.stack([self.delay.delays(i) for i in range(R)]) if R else np.zeros((0, W))
+        delay_table = self.delay_table()
         remote_table = self._remote_delays(delay_table)
         views: Dict[Tuple[int, int, int], torch.Tensor] = {}  # (slot, worker, part) -> message row
         if start:
@@ -464,9 +506,12 @@ class Trainer:
             loop_time[i] = col.now() - t_start
             if cfg.checkpoint_every and (i + 1) % cfg.checkpoint_every == 0:
                 self._checkpoint(i + 1, timeset, worker_timeset)
+        if self.skip_stale and self.tx is not None:  # whatever a late worker still has queued is stale now
+            self.tx.release_workers(R + 1)
         if timed_start is not None:  # rounds complete on every rank at the fence (see the native loop)
             t_timed1 = self._timed_fence()
         col.drain(R - 1, max(cfg.round_timeout, 60.0))
+        self.rank_stats.update(stale_skipped_virtual=col.skipped, stale_arrivals=col.stale_arrivals)
         col.close()
         if cfg.verify_beta and env.world > 1:
             self._verify_beta_checksums(start)
@@ -502,6 +547,8 @@ class Trainer:
         rep: Dict[str, object] = {"rank": env.rank, "role": role, "device": str(env.device),
                                   "transport": self.transport,
                                   "round_loop": self.device_loop or ("native pump" if self.native_loop else "python"),
+                                  "loop_reason": getattr(self, "loop_reason", None),
+                                  "drain": self.drain_mode,
                                   "workers": sorted({int(m.worker) for m in self.local_msgs}),
                                   "messages": len(self.local_msgs),
                                   "partitions": len({p for m in self.local_msgs for p, _ in m.segments})}
@@ -537,6 +584,7 @@ class Trainer:
         col.set_shards(self.n_shards)
         dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
         pump = C.MasterPump(col.c, W, R, K, self.d, self.ld, dev, float(cfg.round_timeout))
+        pump.set_skip_stale(self.skip_stale)
         pump.set_state(self.beta, self.u, self.hist, self.beta_in)
         if self.local_msgs:
             pump.set_local(self.plan.native_launcher(), self.G, [(m.worker, m.part) for m in self.local_msgs])
@@ -561,7 +609,7 @@ class Trainer:
                 self.rank_stats["device_drain"] = bool(pump.set_drain_flags(srcs))
         eta = cfg.eta()
         co = [self.update.coeffs(i, float(eta[i])) for i in range(R)]
-        delay_table = np.stack([self.delay.delays(i) for i in range(R)])
+        delay_table = self.delay_table()
         pump.set_schedule([c[0] for c in co], [c[1] for c in co], [c[2] for c in co], [c[3] for c in co],
                           co[0][4] if co else 0, [float(x) for x in delay_table.ravel()], self.rule_kind,
                           self.rule_k, bool(self.drain))
@@ -586,8 +634,14 @@ class Trainer:
         if cfg.verbose:
             log(sch.banner(cfg.add_delay))
         orig_start = time.perf_counter()
-        device_mode = self._device_loop_mode(start, delay_table, table_decoded)
-        arb_mode = not device_mode and self._arbiter_mode(pump, start)
+        if self.loop == "arbiter":  # the pump's structural limits (engine/loops.py: blocker)
+            why = pump.device_blocker(start, R)
+            if why:
+                if os.environ.get("ERASUREHEAD_DEVICE_MASTER", "auto") == "on":
+                    raise RuntimeError(f"ERASUREHEAD_DEVICE_MASTER=on, but the rounds cannot run on the device: {why}")
+                self.loop, self.loop_reason = select_round_loop(self.loop_inputs(start, blocker=why))
+        device_mode = self.loop if self.loop in ("graph", "stream") else None
+        arb_mode = self.loop == "arbiter"
         if arb_mode:
             # every round on the device: the master's gradient, then csrc/kernels/arbiter.hip polls the
             # workers' counters, decodes, updates and releases the next beta; the host only reads back
@@ -597,6 +651,7 @@ class Trainer:
                 if timed_start is not None and a == timed_start:
                     t_timed0 = self._timed_fence()
                 pump.run_device(a, b, deadline)
+            pump.finish_run()  # lazy drain: a late worker's queued rounds are stale now
             if timed_start is not None:
                 t_timed1 = self._timed_fence()
             for i, (status, arr, tdec, tend, detail, tstop, (tjoin, tdecoded)) in zip(range(start, R),
@@ -682,6 +737,8 @@ class Trainer:
             arrivals_log.append([(a.worker, a.part, a.t_rel) for a in arrivals])
             if cfg.checkpoint_every and (i + 1) % cfg.checkpoint_every == 0:
                 self._checkpoint(i + 1, timeset, worker_timeset)
+        if not device_mode and not arb_mode:
+            pump.finish_run()  # lazy drain: a late worker's queued rounds are stale now
         if timed_start is not None and not device_mode and not arb_mode:
             # every rank's rounds are complete once all ranks pass the fence (workers' puts have landed
             # before their barrier); the straggler drain and bookkeeping below are not round time
@@ -695,6 +752,8 @@ class Trainer:
         if cfg.instrument:
             put_ms, ker_ms = pump.timing_ms()
             self.rank_stats.update(beta_put_us=_mean_us(put_ms, a0), kernel_us=_mean_us(ker_ms, a0))
+        if self.drain_mode != "all":
+            self.rank_stats.update(stale_skipped_virtual=col.skipped, stale_arrivals=col.stale_arrivals)
         self.rank_stats.update(update_kernel_us=_mean_us(upd, a0),
                                **{f"{k}_us": float(1e6 * np.mean(v[a0 - start:]))
                                   for k, v in self.timer.t.items() if len(v) > a0 - start})
@@ -710,43 +769,18 @@ class Trainer:
         del pump
         return res
 
-    def _arbiter_mode(self, pump, start: int) -> bool:
-        """Multi-rank rounds on the device arbiter (MasterPump.run_device)?  ERASUREHEAD_DEVICE_MASTER =
-        auto | on | off.  auto: when the ranks own their GPUs (a spinning arbiter would compete with
-        the other ranks' kernels on a shared one), the rounds are delay-free and drain, and nothing
-        needs the host between rounds (checkpoints, the beta race check, HIP-event instrumentation,
-        --device-loop off)."""
-        mode = os.environ.get("ERASUREHEAD_DEVICE_MASTER", "auto")
-        cfg, tx = self.cfg, self.tx
-        if mode == "off" or tx is None or cfg.device_loop == "off" or cfg.instrument or cfg.verify_beta \
-                or cfg.checkpoint_every or start:
-            return False
-        why = pump.device_blocker(start, cfg.num_itrs)
-        if why:
-            if mode == "on":
-                raise RuntimeError(f"ERASUREHEAD_DEVICE_MASTER=on, but the rounds cannot run on the device: {why}")
-            return False
-        return mode == "on" or self._device_waits(tx)
-
-    def _device_loop_mode(self, start: int, delay_table: np.ndarray, table_decoded: bool) -> Optional[str]:
-        """'graph' | 'stream' when the rounds can run device-driven (MasterPump.run_local), else None.
-
-        Eligible: one process (every message local), no injected delay in any remaining round
-        (the arrival order is then fixed before the GPU runs), every decode pattern already
-        in the table, no per-round checkpoints.
-        """
-        mode = self.cfg.device_loop
-        if mode == "off" or self.tx is not None or not self.local_msgs or self.cfg.checkpoint_every:
-            return None
-        if delay_table.size and np.any(delay_table[start:] != 0.0):
-            return None
-        W, s = self.cfg.n_workers, self.scheme.n_stragglers
-        if table_decoded and math.comb(W, s) > 20000:
-            return None
-        return "graph" if mode == "graph" else "stream"
-
     @staticmethod
-    def _device_waits(tx) -> bool:
+    def _shared_gpu(tx) -> bool:
+        """Some ranks time-share one GPU (the IPC topology check compares PCI bus ids; other
+        transports: never known to share, RCCL refuses it)."""
+        pairs = getattr(tx, "pairs", None) or []
+        if getattr(tx, "name", "") != "ipc" or not pairs:
+            return False
+        buses = [p.get("master_bus") for p in pairs[:1]] + [p.get("bus") for p in pairs]
+        return len(set(buses)) < len(buses)
+
+    @classmethod
+    def _device_waits(cls, tx) -> bool:
         """Stream-side waits on the shared flags (hipStreamWaitValue64): a worker's wait for beta and
         the master's drain before the next beta.  On when every rank has its GPU to itself; ranks
         time-sharing one GPU keep host waits (a queued wait competes with the other ranks' kernels
@@ -754,9 +788,7 @@ class Trainer:
         mode = os.environ.get("ERASUREHEAD_WORKER_WAIT", "auto")
         if getattr(tx, "name", "") != "ipc" or mode == "host":
             return False
-        buses = [p.get("master_bus") for p in tx.pairs[:1]] + [p.get("bus") for p in tx.pairs]
-        shared = len(set(buses)) < len(buses)
-        return mode == "device" or (mode == "auto" and not shared)
+        return mode == "device" or (mode == "auto" and not cls._shared_gpu(tx))
 
     def _worker_loop_native(self, timed_start, start: int = 0) -> None:
         """Worker rounds in csrc/runtime/engine.cpp (WorkerPump) over the IPC mailbox."""
@@ -780,6 +812,8 @@ class Trainer:
         pump.set_repeat(self.repeat)
         if self.physical:
             pump.set_delays(self._rank_delays())
+        if self.skip_stale and tx.name == "ipc" and self.n_loc:  # stale-round gates (p2p sends cannot be skipped)
+            pump.set_skip_stale(tx.flags.dev_addr(env.rank))
         self.rank_stats["fused_put"] = bool(pump.fused_put)
         self.rank_stats["device_wait"] = bool(pump.device_wait)
         cut = timed_start if timed_start is not None and start <= timed_start < R else None
@@ -798,6 +832,9 @@ class Trainer:
         a0 = cut if cut is not None else start
         wait_s, ker_ms, put_ms = pump.timing()
         self.rank_stats.update(beta_wait_us=_mean_us([1e3 * x if x >= 0 else -1.0 for x in wait_s], a0))
+        if pump.skip_stale:
+            self.skipped_rounds = list(pump.skipped_rounds())
+            self.rank_stats["stale_rounds_skipped"] = len(self.skipped_rounds)
         if cfg.instrument:
             self.rank_stats.update(kernel_us=_mean_us(ker_ms, a0), msg_put_us=_mean_us(put_ms, a0))
         env.barrier()
@@ -837,7 +874,7 @@ class Trainer:
 
     def _post_recvs(self, i: int, slot: int, col: ArrivalCollector, delays):
         if self.tx is not None:
-            self.tx.post_recvs(i, slot, col, self.Rbuf, self.remote_msgs, delays)
+            self.tx.post_recvs(i, slot, col, self.Rbuf, self.remote_msgs, delays, self.physical)
 
     def _worker_loop(self, timed_start, start: int = 0) -> None:
         cfg, env, tx = self.cfg, self.env, self.tx
@@ -845,6 +882,7 @@ class Trainer:
         late = self._rank_delays()
         t0 = None
         bsum = torch.full((R, 2), float("nan"), dtype=torch.float64, device=env.device) if cfg.verify_beta else None
+        self.skipped_rounds = []
         for i in range(start, R):
             if timed_start is not None and i == timed_start:
                 t0 = self._timed_fence()
@@ -853,7 +891,10 @@ class Trainer:
                 b = tx.recv_beta(i)
             if bsum is not None:
                 bsum[i, 0] = b.double().sum()
-            if n:
+            stale = bool(n) and self.skip_stale and tx.stale(i)  # beta(i+1) is already out
+            if stale:
+                self.skipped_rounds.append(i)
+            if n and not stale:
                 with self.timer.phase("local_grad"):
                     for _ in range(self.repeat):  # --slow-ranks: a slower GPU
                         self.plan.run(b, self.G[slot])
@@ -864,6 +905,9 @@ class Trainer:
                     tx.send_msgs(i, self.G[slot, :n])
             if bsum is not None:  # beta must be unchanged after the gradient read it
                 bsum[i, 1] = b.double().sum()
+        if self.skip_stale and n:
+            tx.rounds_done(R)  # every round put or skipped: the master's collector can drain
+            self.rank_stats["stale_rounds_skipped"] = len(self.skipped_rounds)
         tx.finish()
         if timed_start is not None:  # same collective order as the master: fence, then the race check
             self.worker_timed_seconds = self._timed_fence() - t0

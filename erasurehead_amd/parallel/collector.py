@@ -60,23 +60,40 @@ class ArrivalCollector:
             if n != 1:
                 self.c.set_shards(int(w), int(p), int(n))
 
+    def set_skip_stale(self, on: bool) -> None:
+        """Drain "lazy": a worker still busy with an earlier round when the next one begins skips it
+        (csrc/runtime/collector.h, stale-round skipping); off = lag carries, every round is delivered."""
+        self.c.set_skip_stale(bool(on))
+
+    @property
+    def skipped(self) -> int:
+        """Virtual probes skipped as stale so far."""
+        return int(self.c.skipped)
+
+    @property
+    def stale_arrivals(self) -> int:
+        """Messages that arrived after their round ended (never decoded)."""
+        return int(self.c.stale_arrivals)
+
     def begin_round(self, i: int, t_start: float, rule: int, k: int) -> None:
         self.round = i
         self.c.begin_round(int(i), float(t_start), int(rule), int(k))
 
-    def add_event(self, worker: int, part: int, i: int, event, delay: float) -> int:
-        pid = self.c.add_event_probe(int(worker), int(part), int(i), int(event.cuda_event), float(delay))
+    def add_event(self, worker: int, part: int, i: int, event, delay: float, physical: bool = False) -> int:
+        """physical: a really late rank's message; its completion time is its arrival (no carry-over)."""
+        pid = self.c.add_event_probe(int(worker), int(part), int(i), int(event.cuda_event), float(delay), bool(physical))
         self._keep[pid] = event
         return pid
 
-    def add_flag(self, worker: int, part: int, i: int, addr: int, value: int, delay: float) -> int:
+    def add_flag(self, worker: int, part: int, i: int, addr: int, value: int, delay: float,
+                 physical: bool = False) -> int:
         """IPC mailbox probe: arrived when the shared-host counter at ``addr`` reaches ``value``."""
-        return self.c.add_flag_probe(int(worker), int(part), int(i), int(addr), int(value), float(delay))
+        return self.c.add_flag_probe(int(worker), int(part), int(i), int(addr), int(value), float(delay), bool(physical))
 
     def add_work(self, worker: int, part: int, i: int, work, delay: float, src: int = 0,
-                 t_seen: float = None) -> int:
+                 t_seen: float = None, physical: bool = False) -> int:
         """Host probe completed when ``work`` finishes (None = already complete at ``t_seen``, default now)."""
-        pid = self.c.add_host_probe(int(worker), int(part), int(i), float(delay))
+        pid = self.c.add_host_probe(int(worker), int(part), int(i), float(delay), bool(physical))
         if work is None:
             self.c.mark_seen(pid, self.now() if t_seen is None else float(t_seen))
         else:

@@ -77,15 +77,29 @@ class Transport:
     def send_beta(self, i: int, beta: torch.Tensor) -> None:
         raise NotImplementedError
 
-    def post_recvs(self, i: int, slot: int, col, rbuf: torch.Tensor, msgs_by_rank, delays) -> None:
+    def post_recvs(self, i: int, slot: int, col, rbuf: torch.Tensor, msgs_by_rank, delays,
+                   physical: bool = False) -> None:
+        """physical: the worker ranks are really late (--delay-on worker): arrival = completion."""
         raise NotImplementedError
 
     def before_read(self, slot: int, j: int) -> None:
         """Order the current stream after message (slot, j) landed (no-op when the host already knows)."""
 
+    def release_workers(self, value: int) -> None:
+        """Master, drain "lazy", after its last round: every worker's beta counter to ``value`` (R + 1),
+        so rounds a late worker still has queued are stale and skipped (no-op without counters)."""
+
     # ---- worker side -------------------------------------------------------------------
     def recv_beta(self, i: int) -> torch.Tensor:
         raise NotImplementedError
+
+    def stale(self, i: int) -> bool:
+        """Worker, drain "lazy": beta(i+1) is already out, so round i is stale (only where the transport
+        can tell without receiving it: the IPC counters)."""
+        return False
+
+    def rounds_done(self, R: int) -> None:
+        """Worker, drain "lazy": announce every round < R as put or skipped (the master's final drain)."""
 
     def send_msgs(self, i: int, G_slot: torch.Tensor) -> None:
         raise NotImplementedError
@@ -110,12 +124,12 @@ class GlooTransport(Transport):
         for r in range(1, self.env.world):
             self._sends[i % self.K].append(dist.isend(beta, r, tag=_tag_beta(i)))
 
-    def post_recvs(self, i, slot, col, rbuf, msgs_by_rank, delays):
+    def post_recvs(self, i, slot, col, rbuf, msgs_by_rank, delays, physical=False):
         for r in sorted(msgs_by_rank):
             for jj, m in enumerate(msgs_by_rank[r]):
                 j = self.row0[r] + jj
                 w = dist.irecv(rbuf[slot, j], r, tag=_tag_msg(i, jj))
-                col.add_work(m.worker, m.part, i, w, delays[m.worker], src=r)
+                col.add_work(m.worker, m.part, i, w, delays[m.worker], src=r, physical=physical)
 
     def recv_beta(self, i):
         slot = i % self.K
@@ -265,7 +279,7 @@ class CommTransport(Transport):
             with torch.cuda.stream(s):
                 self.comm.send(r, beta)
 
-    def post_recvs(self, i, slot, col, rbuf, msgs_by_rank, delays):
+    def post_recvs(self, i, slot, col, rbuf, msgs_by_rank, delays, physical=False):
         # one receive per worker rank: its messages are contiguous rows of the mailbox ring and the
         # rank computes (and sends) them together, so they share one completion event
         for r in sorted(msgs_by_rank):
@@ -277,7 +291,7 @@ class CommTransport(Transport):
                 ev.record(s)
             for jj, m in enumerate(msgs_by_rank[r]):
                 self.ev_of[slot][j0 + jj] = ev
-                col.add_event(m.worker, m.part, i, ev, delays[m.worker])
+                col.add_event(m.worker, m.part, i, ev, delays[m.worker], physical)
 
     def before_read(self, slot, j):
         self.cs.wait_event(self.ev_of[slot][j])
@@ -615,18 +629,28 @@ class IpcTransport(Transport):
         for k in range(0, len(puts), 16):
             self.C.put_signal(puts[k:k + 16], self.counters[16 * (k // 16):])
 
-    def post_recvs(self, i, slot, col, rbuf, msgs_by_rank, delays):
+    def post_recvs(self, i, slot, col, rbuf, msgs_by_rank, delays, physical=False):
         w = self.env.world
         for r in sorted(msgs_by_rank):
             addr = self.flags.host_addr(w + r)
             for m in msgs_by_rank[r]:
-                col.add_flag(m.worker, m.part, i, addr, i + 1, delays[m.worker])
+                col.add_flag(m.worker, m.part, i, addr, i + 1, delays[m.worker], physical)
+
+    def release_workers(self, value):
+        for r in range(1, self.env.world):  # stream-ordered behind the last beta put
+            self.C.signal(self.flags.dev_addr(r), int(value), self.dev)
 
     # ---- worker ------------------------------------------------------------------------
     def recv_beta(self, i):
         if not self.flags.wait_ge(self.env.rank, i + 1, self.timeout):
             raise TimeoutError(f"rank {self.env.rank}: no beta for round {i} within {self.timeout}s")
         return self.inbox[i]
+
+    def stale(self, i):
+        return self.flags.load(self.env.rank) >= i + 2
+
+    def rounds_done(self, R):
+        self.C.signal(self.flags.dev_addr(self.env.world + self.env.rank), int(R), self.dev)
 
     def send_msgs(self, i, G_slot):
         slot = i % self.K
