@@ -169,12 +169,13 @@ def main(argv=None) -> int:
     except TransportError as e:
         # every rank raised the same verdict (IpcTransport.preflight): the IPC mailbox lost a payload or a
         # signal.  Unless the IPC path was asked for by name, rebuild on RCCL p2p under the same pumps
-        # (the loud fallback make_transport takes when the handshake fails) and record why.  Ranks that
-        # share a GPU (rehearsals; RCCL refuses them) take the loopback communicator, RCCL's code path.
-        if a.transport == "ipc" or os.environ.get("ERASUREHEAD_NO_FALLBACK"):
+        # (the loud fallback make_transport takes when the handshake fails) and record why.
+        if a.transport == "ipc" or os.environ.get("ERASUREHEAD_NO_FALLBACK") or env.backend == "gloo":
+            # ranks sharing a GPU (gloo control plane): the loopback communicator runs over the same IPC
+            # mappings and shared counters whose failure this is, so it is no independent fallback
             raise
         preflight_failure, preflight = str(e), None
-        a.transport = "rccl" if env.backend == "nccl" else "loopback"
+        a.transport = "rccl"
         if env.is_master:
             print(f"[bench] WARNING: {e}; rebuilding on {a.transport}", file=sys.stderr, flush=True)
         free(trainer)

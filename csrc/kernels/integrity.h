@@ -41,7 +41,7 @@ struct IntegrityErr {
   unsigned long long sum_calc;  // checksum of the payload as read
 };
 
-constexpr int kMaxTagRows = 64;  // rows of one tagged put descriptor (sender scratch / LDS sums)
+constexpr int kMaxTagRows = 1024;  // rows of one tagged put descriptor (sender scratch / LDS sums: 8 KB)
 constexpr int kMaxCheckRows = 128;  // mailbox rows one deferred check covers (= kMaxMsgs of a decode)
 
 // The mailbox rows a round's decode read, checked AFTER the round (off the critical path: the rows

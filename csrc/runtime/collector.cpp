@@ -78,6 +78,16 @@ void Collector::begin_round(int round, double t_start, int rule, int k) {
     for (int id : live_) maybe_skip(probes_[id]);
 }
 
+void Collector::end_run(double t) {
+  if (!skip_stale_ || round_ < 0) return;
+  const int r = round_ + 1;
+  if (static_cast<int>(round_start_.size()) <= r) round_start_.resize(r + 1, 0.0);
+  round_start_[r] = t;
+  round_ = r;  // later arrivals of the last round count as stale
+  stopped_ = true;
+  for (int id : live_) maybe_skip(probes_[id]);
+}
+
 int Collector::add_probe(const Probe& p) {
   if (p.worker < 0 || p.worker >= W_) throw std::invalid_argument("Collector: bad worker");
   if (p.part < 0 || p.part > 1) throw std::invalid_argument("Collector: bad part");

@@ -98,6 +98,10 @@ class Collector {
   // Stale-round skipping of virtual probes (drain "lazy"; see above).  Off: lag carries over and
   // every round's message is delivered in order (the reference's no-Waitall schemes).
   void set_skip_stale(bool on) { skip_stale_ = on; }
+  // End of the master's rounds at time t (skip_stale only): like the start of one more round, every
+  // virtual probe whose worker could not start its round before t is skipped (the physical workers
+  // get the same release: MasterPump::finish_run).  No round may begin after it.
+  void end_run(double t);
   bool skip_stale() const { return skip_stale_; }
   // Virtual probes skipped as stale so far, and stale arrivals (a round's message after the round
   // ended: drained, never decoded).

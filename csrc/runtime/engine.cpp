@@ -579,7 +579,9 @@ class MasterPump {
   // worker's beta counter goes to R + 1 (as if beta(R) were out), so whatever a late worker rank still
   // has queued is stale and skipped (its gate), and its final signal lets the collector drain.
   void finish_run() {
-    if (!skip_ || comm_) return;
+    if (!skip_) return;
+    col_->end_run(eh::Collector::now());
+    if (comm_) return;
     for (const auto& t : targets_)
       hcheck(eh::signal_launch(reinterpret_cast<unsigned long long*>(t.second), static_cast<unsigned long long>(R_) + 1,
                                stream_),
@@ -1069,7 +1071,8 @@ class MasterPump {
       cl.ld = ld_;
       cl.tags = reinterpret_cast<const eh::MsgTag*>(mbox_tags_) + static_cast<int64_t>(slot) * r_rows_;
       for (const auto& u : used)
-        if (u.row >= 0 && cl.n < eh::kMaxCheckRows) {
+        if (u.row >= 0) {
+          need(cl.n < eh::kMaxCheckRows, "integrity check list: more mailbox rows than one decode holds");
           cl.row[cl.n] = u.p;
           cl.mrow[cl.n] = u.row;
           cl.rank[cl.n] = row_rank_[u.row];
@@ -1474,13 +1477,16 @@ class WorkerPump {
   // Integrity tags (csrc/kernels/integrity.h): mbox_tags = this rank's view of the master
   // mailbox's tag slots [K][mbox_rows]; inbox_tags = its own inbox's tag slots [R + 1].  Every
   // message put carries a tag per row; every beta is checked after the round that read it.
-  void set_integrity(uintptr_t mbox_tags, uintptr_t inbox_tags, int rank, bool on) {
+  // Returns whether tags are on: a rank hosting more than kMaxTagRows message rows puts them untagged
+  // (the caller records why) rather than failing its setup.
+  bool set_integrity(uintptr_t mbox_tags, uintptr_t inbox_tags, int rank, bool on) {
     need(!on || (mbox_tags != 0 && inbox_tags != 0), "integrity tags need the tag slots");
-    need(!on || n_ <= eh::kMaxTagRows, "a tagged put holds at most 64 message rows");
+    if (n_ > eh::kMaxTagRows) on = false;
     tags_ = on;
     mtags_ = reinterpret_cast<eh::MsgTag*>(mbox_tags);
     itags_ = reinterpret_cast<const eh::MsgTag*>(inbox_tags);
     rank_ = rank;
+    return tags_;
   }
   // Raise the first failed beta check (host-mapped record), after releasing this rank's queued work.
   void check_integrity() {
@@ -1751,12 +1757,17 @@ void bind_engine(py::module& m) {
              g.enc_coef = coef.data_ptr<double>();
              for (auto* t : {&ptr, &idx, &coef, &Gb}) g.keep.push_back(*t);
            })
-      .def("launch", [](const GradLauncher& g, const Tensor& beta, const Tensor& G) {
-        need_gpu(beta, "beta");
-        need_gpu(G, "G");
-        hcheck(g.launch(beta.data_ptr(), G.data_ptr(), c10::hip::getCurrentHIPStream(G.device().index()).stream()),
-               "GradLauncher.launch");
-      });
+      .def(
+          "launch",
+          [](const GradLauncher& g, const Tensor& beta, const Tensor& G, std::optional<Tensor> gate) {
+            need_gpu(beta, "beta");
+            need_gpu(G, "G");
+            if (gate) need(gate->is_cuda() && gate->scalar_type() == at::kInt && gate->numel() >= 1, "gate: int32 GPU");
+            hcheck(g.launch(beta.data_ptr(), G.data_ptr(), c10::hip::getCurrentHIPStream(G.device().index()).stream(),
+                            gate ? gate->data_ptr<int>() : nullptr),
+                   "GradLauncher.launch");
+          },
+          py::arg("beta"), py::arg("G"), py::arg("gate") = py::none());
   py::class_<MasterPump>(m, "MasterPump")
       .def(py::init<eh::Collector*, int, int, int, int, int, int, double>(), py::arg("collector"), py::arg("W"),
            py::arg("R"), py::arg("K"), py::arg("d"), py::arg("ld"), py::arg("device"), py::arg("timeout"),

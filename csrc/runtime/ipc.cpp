@@ -20,6 +20,7 @@
 #include <torch/extension.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <memory>
@@ -247,6 +248,31 @@ void put_signal(const std::vector<std::tuple<Tensor, Tensor, uintptr_t, uint64_t
          "put_signal");
 }
 
+// One gated put (launchers.h PutDesc::gate, the lazy-drain stale-round gate) of src into dst with its
+// signal, and the next round's gate decided from the beta counter at beta_flag (device address):
+// the engine's WorkerPump builds the same descriptor; this entry point serves the kernel tests.
+void put_signal_gated(const Tensor& src, const Tensor& dst, uintptr_t flag, uint64_t value, const Tensor& counters,
+                      const Tensor& gate, uintptr_t beta_flag, uint64_t stale_next) {
+  for (auto* t : {&src, &dst, &counters, &gate})
+    if (!t->is_cuda() || !t->is_contiguous()) throw std::invalid_argument("put_signal_gated: GPU contiguous tensors");
+  if (gate.scalar_type() != at::kInt || gate.numel() < 2) throw std::invalid_argument("put_signal_gated: gate int32 [2]");
+  const int64_t nb = src.numel() * src.element_size();
+  if (nb != dst.numel() * dst.element_size() || nb % 16 || flag == 0 || beta_flag == 0)
+    throw std::invalid_argument("put_signal_gated: sizes / addresses");
+  eh::PutArgs a{};
+  a.n = 1;
+  auto& d = a.d[0];
+  d = eh::PutDesc{src.data_ptr(), dst.data_ptr(), nb, reinterpret_cast<unsigned long long*>(flag), value,
+                  reinterpret_cast<unsigned int*>(counters.data_ptr<int>())};
+  d.gate = gate.data_ptr<int>();
+  d.next_gate = gate.data_ptr<int>() + 1;
+  d.beta_flag = reinterpret_cast<const unsigned long long*>(beta_flag);
+  d.stale_next = stale_next;
+  const int blocks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(64, (nb / 16 + 4095) / 4096)));
+  hcheck(eh::put_signal_launch(a, blocks, c10::hip::getCurrentHIPStream(src.device().index()).stream()),
+         "put_signal_gated");
+}
+
 // One tagged put (csrc/kernels/integrity.h) of src [rows, ld] into dst, with one MsgTag per row into
 // `tags` (uint8 [rows * 16], on any device the GPU can write); csum: int64 zeroed scratch [>= rows].
 // The engine's pumps build the same descriptors natively; this entry point serves the kernel tests.
@@ -396,6 +422,8 @@ void bind_ipc(py::module& m) {
       py::arg("out_row"), py::arg("in_row"), py::arg("nwords_out"), py::arg("nwords_in"), py::arg("out_flag"),
       py::arg("in_flag"), py::arg("iters"), py::arg("deadline_s"), py::arg("master"), py::arg("device"));
   m.def("signal", &signal, py::arg("flag"), py::arg("value"), py::arg("device"));
+  m.def("put_signal_gated", &put_signal_gated, py::arg("src"), py::arg("dst"), py::arg("flag"), py::arg("value"),
+        py::arg("counters"), py::arg("gate"), py::arg("beta_flag"), py::arg("stale_next"));
   m.def("put_signal_tagged", &put_signal_tagged, py::arg("src"), py::arg("dst"), py::arg("tags"), py::arg("flag"),
         py::arg("value"), py::arg("rank"), py::arg("counters"), py::arg("csum"), py::arg("corrupt") = false);
   m.def("verify_rows", &verify_rows, py::arg("rows"), py::arg("tags"), py::arg("round1"), py::arg("rank"));

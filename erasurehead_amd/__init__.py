@@ -20,7 +20,19 @@ try:
     _q = int(_os.environ.get("GPU_MAX_HW_QUEUES", "0"))
 except ValueError:
     _q = 0
-if _q < MIN_HW_QUEUES:
+# What the HIP runtime of this process actually uses: the value from before the override when HIP
+# was already initialised (torch touched the GPU before this package was imported), else ours.
+# parallel/transport.py warns on it and Trainer.rank_report records it.
+_HIP_WAS_UP = False
+try:
+    import sys as _sys
+
+    _t = _sys.modules.get("torch")
+    _HIP_WAS_UP = bool(_t is not None and _t.cuda.is_initialized())
+except Exception:  # noqa: BLE001 - torch half-imported: treat as not initialised
+    _HIP_WAS_UP = False
+if _q < MIN_HW_QUEUES and not _HIP_WAS_UP:
     _os.environ["GPU_MAX_HW_QUEUES"] = str(MIN_HW_QUEUES)
+HW_QUEUES = (_q or 4) if _HIP_WAS_UP else max(_q, MIN_HW_QUEUES)
 
 from .config import RunConfig  # noqa: E402

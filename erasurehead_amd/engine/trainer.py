@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import math
 import os
+import sys
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
@@ -80,6 +81,15 @@ class TrainResult:
     timeouts: int = 0
     phases: Dict[str, Dict[str, float]] = field(default_factory=dict)
     arrivals: List[List[Tuple[int, int, float]]] = field(default_factory=list)
+
+
+def _sabotage_exit(rank: int) -> Optional[int]:
+    """Test hook ERASUREHEAD_SABOTAGE=exit:<rank>:<round>: that worker rank exits before that round."""
+    spec = os.environ.get("ERASUREHEAD_SABOTAGE", "")
+    parts = spec.split(":")
+    if len(parts) == 3 and parts[0] == "exit" and int(parts[1]) == rank:
+        return int(parts[2])
+    return None
 
 
 def _mean_us(ms, a0: int = 0) -> Optional[float]:
@@ -362,10 +372,15 @@ class Trainer:
         env.barrier()
         self.loop, self.loop_reason = select_round_loop(self.loop_inputs(start))
         native_loop = self.native_loop
-        if env.is_master:
-            res = (self._master_loop_native if native_loop else self._master_loop)(timed_start, log, start)
-        else:
-            res = (self._worker_loop_native if native_loop else self._worker_loop)(timed_start, start)
+        try:
+            if env.is_master:
+                res = (self._master_loop_native if native_loop else self._master_loop)(timed_start, log, start)
+            else:
+                res = (self._worker_loop_native if native_loop else self._worker_loop)(timed_start, start)
+        except BaseException:
+            if self.tx is not None:  # release queued p2p work on peers that will not answer
+                self.tx.abort()
+            raise
         return res
 
     def loop_inputs(self, start: int = 0, blocker: str = "") -> LoopInputs:
@@ -407,6 +422,22 @@ class Trainer:
         if self.loop == "python":
             return False
         return self.n_loc > 0 or self.env.is_master
+
+    def _final_drain(self, col) -> bool:
+        """After the last round: wait until every message of every round has arrived (dead workers
+        excepted), bounded by the round timeout or the longest virtual lag the delays can carry.  A
+        message that never lands means a worker rank is gone: the transport is aborted (its queued
+        receives released) before anything synchronises the device, and the run says so."""
+        d = self.delay_table()
+        fin = np.where(np.isfinite(d), d, 0.0) if d.size else d
+        lag = float(np.sum(np.max(fin, axis=1))) if fin.size else 0.0
+        ok = col.drain(self.cfg.num_itrs - 1, max(float(self.cfg.round_timeout), min(600.0, lag + 10.0)))
+        if not ok and self.tx is not None:
+            why = f"rank 0: {col.c.pending_upto(self.cfg.num_itrs - 1)} messages never arrived; aborting the transport"
+            print(f"[erasurehead] WARNING: {why}", file=sys.stderr, flush=True)
+            self.rank_stats["aborted"] = why
+            self.tx.abort()
+        return ok
 
     def _timed_fence(self):
         self._sync()
@@ -506,11 +537,13 @@ class Trainer:
             loop_time[i] = col.now() - t_start
             if cfg.checkpoint_every and (i + 1) % cfg.checkpoint_every == 0:
                 self._checkpoint(i + 1, timeset, worker_timeset)
-        if self.skip_stale and self.tx is not None:  # whatever a late worker still has queued is stale now
-            self.tx.release_workers(R + 1)
+        if self.skip_stale:  # whatever a late worker still has queued is stale now
+            col.c.end_run(col.now())
+            if self.tx is not None:
+                self.tx.release_workers(R + 1)
         if timed_start is not None:  # rounds complete on every rank at the fence (see the native loop)
             t_timed1 = self._timed_fence()
-        col.drain(R - 1, max(cfg.round_timeout, 60.0))
+        self._final_drain(col)
         self.rank_stats.update(stale_skipped_virtual=col.skipped, stale_arrivals=col.stale_arrivals)
         col.close()
         if cfg.verify_beta and env.world > 1:
@@ -552,12 +585,15 @@ class Trainer:
                                   "workers": sorted({int(m.worker) for m in self.local_msgs}),
                                   "messages": len(self.local_msgs),
                                   "partitions": len({p for m in self.local_msgs for p, _ in m.segments})}
-        rep.update({k: round(float(v), 2) for k, v in self.rank_stats.items() if v is not None})
+        rep.update({k: (round(float(v), 2) if isinstance(v, (int, float)) and not isinstance(v, bool) else v)
+                    for k, v in self.rank_stats.items() if v is not None})
         kern = self._kernel_label()
         if kern:
             rep["grad_kernel"] = kern
         if self.tx is not None and self.tx.name in ("rccl", "loopback"):
-            rep["hw_queues"] = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+            from .. import HW_QUEUES
+
+            rep["hw_queues"] = int(HW_QUEUES)  # what HIP started with, not the (possibly later) environment
         if self.tx is not None and self.tx.fallback_reason:
             rep["transport_fallback"] = self.tx.fallback_reason
         if self.tx is not None and env.is_master and self.tx.pairs:
@@ -743,7 +779,7 @@ class Trainer:
             # every rank's rounds are complete once all ranks pass the fence (workers' puts have landed
             # before their barrier); the straggler drain and bookkeeping below are not round time
             t_timed1 = self._timed_fence()
-        col.drain(R - 1, max(cfg.round_timeout, 60.0))
+        self._final_drain(col)
         upd = pump.update_ms()
         pump.final_check()  # the last round's mailbox rows (earlier rounds were checked as the run went)
         if not device_mode and not arb_mode:
@@ -807,7 +843,11 @@ class Trainer:
             pump = C.WorkerPump(self.plan.native_launcher(), tx.inbox, self.G, self.n_loc, tx.rremote.ptr,
                                 tx.mbox_rows, tx.my_row0, tx.flags.host_addr(env.rank), tx.flags.dev_addr(w + env.rank),
                                 tx.counters, K, dev, wait_limit, tx.flags.dev_addr(env.rank) if dwait else 0)
-            pump.set_integrity(tx.mbox_tags_addr(), tx.inbox_tags_addr(), env.rank, bool(cfg.integrity))
+            tagged = pump.set_integrity(tx.mbox_tags_addr(), tx.inbox_tags_addr(), env.rank, bool(cfg.integrity))
+            if cfg.integrity and not tagged:  # more message rows than one tagged put holds: loud, recorded
+                why = f"rank {env.rank} hosts {self.n_loc} message rows (> 1024 per tagged put): its puts are untagged"
+                print(f"[erasurehead] WARNING: {why}", file=sys.stderr, flush=True)
+                self.rank_stats["integrity_off"] = why
         pump.set_timing(bool(cfg.instrument))
         pump.set_repeat(self.repeat)
         if self.physical:
@@ -818,6 +858,11 @@ class Trainer:
         self.rank_stats["device_wait"] = bool(pump.device_wait)
         cut = timed_start if timed_start is not None and start <= timed_start < R else None
         segments = [(start, cut), (cut, R)] if cut is not None else [(start, R)]
+        gone = _sabotage_exit(env.rank)  # test hook: this worker rank dies after that round
+        if gone is not None:
+            pump.run(start, min(R, gone))
+            torch.cuda.synchronize(env.device)
+            os._exit(0)
         t0 = None
         for k, (a, b) in enumerate(segments):
             if k == 1:

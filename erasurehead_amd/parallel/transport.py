@@ -107,6 +107,10 @@ class Transport:
     def finish(self) -> None:
         """Worker: every send issued so far has completed."""
 
+    def abort(self) -> None:
+        """Release every operation still queued on a peer that will never answer (stream-ordered p2p):
+        after it, a device synchronisation returns; the transport is unusable."""
+
     def close(self) -> None:
         pass
 
@@ -196,7 +200,9 @@ class CommTransport(Transport):
         env.barrier()
         self.pairs = []
         need = 2 * (env.world - 1) + 2  # master: a send and a receive stream per worker rank + compute
-        have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        from .. import HW_QUEUES
+
+        have = HW_QUEUES  # the value the HIP runtime of this process started with (erasurehead_amd/__init__.py)
         if env.is_master and have < need:
             print(f"[erasurehead] WARNING: GPU_MAX_HW_QUEUES={have} < {need}: per-peer receive streams share hardware "
                   "queues, so a straggler's receive can hold back another worker's (set it before HIP starts)",
@@ -323,7 +329,16 @@ class CommTransport(Transport):
     def finish(self):
         torch.cuda.synchronize(self.env.device)
 
+    def abort(self):
+        if self.comm is not None:
+            self.comm.abort()
+
     def close(self):
+        # abort first (a no-op for finished work; a receive or send queued on a dead peer is released),
+        # then wait for the device, and only then unmap the staging rings copy kernels may still target
+        if self.comm is not None:
+            self.comm.abort()
+        torch.cuda.synchronize(self.env.device)
         self.comm = None
         for reg in self._regs:
             reg.close()

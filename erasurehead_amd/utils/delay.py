@@ -105,6 +105,64 @@ def delay_floor(n_workers: int, rounds: int, stop_count=None, groups=None, k=Non
     return tot
 
 
+def schedule(delays: np.ndarray, rule: str, k: int, groups, drain: str = "lazy", compute: float = 0.0,
+             margin: float = 0.0):
+    """Event model of the master's rounds under ``drain`` with per-round worker delays [R, W].
+
+    The master publishes beta(i) at t_i (t_0 = 0) and decides round i when the stop rule holds over
+    the arrivals sorted by time (rule: "all" | "count" (k arrivals) | "frc" (k arrivals or every
+    group covered)); decode and update take no time, so t_{i+1} = that stop time, or, with drain
+    "all", the last arrival.  Worker w, free from F_w on (its previous put), starts round i at
+    s = max(t_i, F_w) and its message lands at s + compute + d[i, w]:
+      * "all" / "carry": every round runs (carry: lag crosses rounds, the reference's no-Waitall
+        schemes, the collector's carried finish);
+      * "lazy": a worker not free before t_{i+1} skips round i (its gate finds beta(i+1) out:
+        csrc/kernels/common.h gate_closed, the collector's stale-round skipping).
+    Returns (arrivals, separated): arrivals[i] = worker ids in arrival order up to the stop (the
+    decode's inputs), separated[i] = every event the round's outcome depends on (arrival order near
+    the stop, a busy worker's start against t_{i+1}) is more than ``margin`` apart -- the rounds a
+    physical run with timing noise below the margin must reproduce exactly.
+    """
+    delays = np.asarray(delays, dtype=np.float64)
+    R, W = delays.shape
+    n_groups = len(set(groups))
+    F = np.full(W, -np.inf)
+    t = 0.0
+    out, sep = [], []
+    for i in range(R):
+        s = np.maximum(t, F)
+        a = s + compute + delays[i]
+        order = sorted(range(W), key=lambda w: (a[w], w))
+        got, cov = [], set()
+        t_stop = np.inf
+        for w in order:
+            if not np.isfinite(a[w]):
+                break
+            got.append(w)
+            cov.add(groups[w])
+            if (rule == "all" and len(got) == W) or (rule == "count" and len(got) >= k) or \
+                    (rule == "frc" and (len(got) >= k or len(cov) == n_groups)):
+                t_stop = a[w]
+                break
+        t_next = t_stop if drain != "all" else float(np.max(a[np.isfinite(a)]))
+        ok = True
+        fin = np.sort(a[np.isfinite(a)])
+        if margin > 0 and fin.size > 1:
+            # the order up to (and one past) the stop must be unambiguous
+            near = fin[: min(len(fin), len(got) + 1)]
+            ok = bool(np.all(np.diff(near) > margin))
+        for w in range(W):
+            runs = drain != "lazy" or F[w] <= t or s[w] < t_next  # free at t_i: it starts at once
+            if drain == "lazy" and margin > 0 and F[w] > t and abs(s[w] - t_next) <= margin:
+                ok = False  # a busy worker's skip decision is within the noise
+            if runs:
+                F[w] = a[w]
+        out.append(got)
+        sep.append(ok)
+        t = t_next
+    return out, sep
+
+
 def _carried_floor(n_workers, rounds, stop_count, groups, k, mean) -> float:
     finish = np.zeros(n_workers)  # virtual finish of every worker's latest message
     t = 0.0  # start of the current round (= decode of the previous one, zero compute)

@@ -45,11 +45,16 @@ def main():
     tr = Trainer(cfg, env, src, scheme=sch)
     pf = tr.preflight(int(os.environ["EH_TEST_PREFLIGHT"])) if os.environ.get("EH_TEST_PREFLIGHT") else None
     res = tr.run()
+    reports = env.gather_objects(tr.rank_report())  # every rank's (stale rounds skipped, ...)
+    skipped = env.gather_objects([int(i) for i in getattr(tr, "skipped_rounds", [])])
     if env.is_master:
         arr = np.array([[(w, p) for (w, p, _) in a] for a in res.arrivals], dtype=object)
-        np.savez(out, betaset=res.betaset, beta0=tr.beta0, arrivals=arr, transport=np.array(tr.transport),
-                 timeset=res.timeset, round_loop=np.array(tr.device_loop or "host"),
-                 preflight=np.array(json.dumps(pf)), rank_report=np.array(json.dumps(tr.rank_report())))
+        t_rel = np.array([[t for (_, _, t) in a] for a in res.arrivals], dtype=object)
+        np.savez(out, betaset=res.betaset, beta0=tr.beta0, arrivals=arr, t_rel=t_rel, transport=np.array(tr.transport),
+                 timeset=res.timeset, loop_time=res.loop_time, round_loop=np.array(tr.device_loop or "host"),
+                 preflight=np.array(json.dumps(pf)), rank_report=np.array(json.dumps(tr.rank_report())),
+                 reports=np.array(json.dumps(reports)), skipped=np.array(json.dumps(skipped)),
+                 owner=np.array(json.dumps({int(u.worker): int(o) for u, o in zip(tr.shards, tr.owner)})))
     env.barrier()
     tr.close()
     env.shutdown()

@@ -209,3 +209,99 @@ def test_sharded_message_arrives_with_its_last_shard(C):
     arr = c.arrivals()
     assert [a.worker for a in arr] == [1, 0]  # worker 0 counts once, at its slowest shard
     assert arr[1].t_rel == pytest.approx(0.02, abs=1e-6)
+
+
+def _lazy_two_rounds(C, skip):
+    """Worker 1 is still busy with round 0 (virtual delay 0.2 s) when rounds 1 and 2 begin."""
+    c = C.Collector(2, [0, 1], 2)
+    c.set_skip_stale(skip)
+    t0 = C.Collector.now()
+    c.begin_round(0, t0, RULE_COUNT, 1)
+    c.mark_seen(c.add_host_probe(0, 0, 0, 0.0), t0)
+    c.mark_seen(c.add_host_probe(1, 0, 0, 0.2), t0)
+    assert c.wait(1.0) and [x.worker for x in c.arrivals()] == [0]
+    t1 = C.Collector.now()
+    c.begin_round(1, t1, RULE_COUNT, 1)
+    c.mark_seen(c.add_host_probe(0, 0, 1, 0.0), t1)
+    c.mark_seen(c.add_host_probe(1, 0, 1, 0.1), t1)  # would finish at t0 + 0.3 if it ran
+    assert c.wait(1.0) and [x.worker for x in c.arrivals()] == [0]
+    t2 = C.Collector.now()
+    c.begin_round(2, t2, RULE_COUNT, 1)
+    c.mark_seen(c.add_host_probe(0, 0, 2, 0.5), t2)
+    c.mark_seen(c.add_host_probe(1, 0, 2, 0.0), t2)
+    assert c.wait(2.0)
+    arr = c.arrivals()
+    assert arr[0].worker == 1
+    return c, arr[0].t_rel + (t2 - t0)  # worker 1's round-2 arrival, from t0
+
+
+def test_lazy_drain_skips_the_stale_round(C):
+    """Drain "lazy": worker 1, busy until t0 + 0.2 when round 2 began, skips round 1 (beta(2) was
+    out before it could start it) and delivers round 2 at t0 + 0.2; with the lag carried (the
+    reference's no-Waitall schemes) it runs round 1 first and round 2 lands at t0 + 0.3."""
+    c, t_lazy = _lazy_two_rounds(C, True)
+    assert t_lazy == pytest.approx(0.2, abs=3e-3)
+    assert c.skipped == 1
+    assert c.drain(2, 2.0)
+    assert c.stale_arrivals >= 1  # its round-0 message landed during round 2: drained, never decoded
+    c2, t_carry = _lazy_two_rounds(C, False)
+    assert t_carry == pytest.approx(0.3, abs=3e-3)
+    assert c2.skipped == 0
+
+
+def test_end_run_skips_what_a_late_worker_has_not_started(C):
+    c = C.Collector(2, [0, 1], 2)
+    c.set_skip_stale(True)
+    t0 = C.Collector.now()
+    for r in range(3):
+        t = C.Collector.now()
+        c.begin_round(r, t, RULE_COUNT, 1)
+        c.mark_seen(c.add_host_probe(0, 0, r, 0.0), t)
+        c.mark_seen(c.add_host_probe(1, 0, r, 5.0), t)  # worker 1: 5 s late every round
+        assert c.wait(1.0)
+    c.end_run(C.Collector.now())
+    # rounds 1 and 2 of worker 1 never start (it is busy with round 0 until t0 + 5 s): skipped, so the
+    # final drain only waits for its round-0 message
+    assert c.skipped == 2
+    assert c.pending_upto(2) == 1
+    assert C.Collector.now() - t0 < 1.0
+
+
+def test_physical_probes_arrive_when_seen(C):
+    """--delay-on worker: a remote message's completion time is its arrival; a rank that was late in
+    round 0 carries no virtual lag into round 1 (it really was late, and really is on time now)."""
+    c = C.Collector(2, [0, 1], 2)
+    t0 = C.Collector.now()
+    c.begin_round(0, t0, RULE_ALL, 2)
+    a = c.add_host_probe(0, 0, 0, 0.0, True)
+    b = c.add_host_probe(1, 0, 0, 0.0, True)
+    c.mark_seen(a, t0)
+    c.mark_seen(b, t0 + 0.05)  # really late by 50 ms
+    assert c.wait(1.0)
+    assert [round(x.t_rel, 3) for x in c.arrivals()] == [0.0, 0.05]
+    t1 = t0 + 0.06
+    c.begin_round(1, t1, RULE_ALL, 2)
+    p = [c.add_host_probe(w, 0, 1, 0.0, True) for w in range(2)]
+    for q in p:
+        c.mark_seen(q, t1 + 0.001)
+    assert c.wait(1.0)
+    assert max(x.t_rel for x in c.arrivals()) == pytest.approx(0.001, abs=1e-9)
+
+
+def test_schedule_model_matches_the_collector_rules():
+    """utils/delay.schedule: drain all / carry / lazy on a hand-checked 3-round, 2-worker case."""
+    import numpy as np
+
+    from erasurehead_amd.utils.delay import schedule
+
+    d = np.array([[0.0, 0.2], [0.0, 0.1], [0.5, 0.0]])
+    lazy, _ = schedule(d, "count", 1, [0, 1], "lazy")
+    carry, _ = schedule(d, "count", 1, [0, 1], "carry")
+    drained, _ = schedule(d, "count", 1, [0, 1], "all")
+    assert lazy == [[0], [0], [1]]  # round 2: worker 1 (free at 0.2, skipped round 1) beats 0.5
+    assert carry == [[0], [0], [1]]  # worker 1 at 0.3 still beats worker 0 at 0.5
+    assert drained == [[0], [0], [1]]
+    d2 = d.copy()
+    d2[2, 0] = 0.25  # worker 0 lands at 0.25: before carry's 0.3, after lazy's 0.2
+    assert schedule(d2, "count", 1, [0, 1], "lazy")[0][2] == [1]
+    assert schedule(d2, "count", 1, [0, 1], "carry")[0][2] == [0]

@@ -1,0 +1,208 @@
+"""Drain "lazy" on the GPU: stale-round gates in the kernels and physically late worker ranks.
+
+Reference: cyclic / naive / avoidstragg never Waitall, and a worker cancels its previous send once
+the next beta arrives (ref src/coded.py:137-196, :178-180); AGC's stop rule ends a round at k
+arrivals (ref src/approximate_coding.py:144-158).  Here a worker rank still busy when beta(i+1)
+is published skips round i on the device (csrc/kernels/common.h gate_closed, decided by its
+previous round's put kernel from the beta counter), and the master never waits for the tail.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from erasurehead_amd.models.losses import LOGISTIC
+from erasurehead_amd.ops import DenseGradPlan, SparseGradPlan, get_precision
+from erasurehead_amd.ops.grad import KernelChoice
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+MARGIN = 0.012
+
+
+def _dense_parts(rng, sizes, d, prec):
+    parts = {}
+    for p, n in enumerate(sizes):
+        X = torch.zeros((n, prec.ld(d)), dtype=torch.float64)
+        X[:, :d] = torch.from_numpy(rng.randn(n, d) * 0.3)
+        y = torch.from_numpy(rng.choice([-1.0, 1.0], n))
+        parts[p] = (X.to(prec.storage).to(DEV).contiguous(), y.to(prec.acc).to(DEV))
+    return parts
+
+
+@pytest.mark.parametrize("prec_name,d,msgs,choice", [
+    ("fp64", 1000, [[(0, 1.0)], [(1, 1.0)]], None),                                   # one-wave bundles of one
+    ("fp64", 1000, [[(0, 1.0), (1, 1.0)], [(0, 0.5), (1, 1.0)]], None),               # replica bundles
+    ("fp32", 1000, [[(0, 1.0), (1, 1.0)], [(0, 0.5), (1, 1.0)], [(1, 2.0)]], None),   # staged / pair
+    ("bf16", 1000, [[(0, 1.0), (1, 1.0)], [(0, 0.5), (1, 1.0)]], None),               # MFMA bundles
+    ("fp64", 3000, [[(0, 1.0)], [(1, -1.0)]], None),                                  # wide rows
+    ("fp64", 17000, [[(0, 1.0)]], None),                                              # two-pass
+    ("fp64", 256, [[(0, 1.0)], [(1, 1.0)]], KernelChoice(kind="fused", rows=4)),       # fused, 4 rows in flight
+])
+def test_closed_gate_skips_every_gradient_kernel(prec_name, d, msgs, choice, native):
+    """gate = 1: the whole launch chain (gradient, slab reduction, encode) returns at once and the
+    message rows keep their previous contents; gate = 0: bitwise the ungated result."""
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(d)
+    parts = _dense_parts(rng, [300, 257], d, prec)
+    kw = {"choice": choice} if choice is not None else {}
+    plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, d, **kw)
+    beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
+    beta[:d] = torch.from_numpy(rng.randn(d) * 0.2).to(prec.acc)
+    launcher = plan.native_launcher()
+    ref = plan.out_buffer()[0]
+    launcher.launch(beta, ref)
+    gate = torch.ones(1, dtype=torch.int32, device=DEV)
+    G = torch.full_like(ref, 7.0)
+    launcher.launch(beta, G, gate)
+    torch.cuda.synchronize()
+    assert torch.all(G == 7.0)
+    gate.zero_()
+    launcher.launch(beta, G, gate)
+    torch.cuda.synchronize()
+    assert torch.equal(G, ref)
+
+
+def test_closed_gate_skips_the_sparse_ell_kernels(native):
+    import scipy.sparse as sps
+
+    prec = get_precision("fp64")
+    rng = np.random.RandomState(1)
+    d, parts = 500, {}
+    for p in range(2):
+        n = 300
+        cols = np.stack([rng.choice(d, 4, replace=False) for _ in range(n)])
+        parts[p] = (sps.csr_matrix((np.ones(cols.size), cols.ravel(), np.arange(0, cols.size + 1, 4)), shape=(n, d)),
+                    rng.choice([-1.0, 1.0], n))
+    plan = SparseGradPlan([[(0, 1.0), (1, 1.0)], [(1, 1.0)]], parts, prec, LOGISTIC, d, device=DEV, use_ell=True)
+    beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
+    beta[:d] = torch.from_numpy(rng.randn(d) * 0.2)
+    launcher = plan.native_launcher()
+    ref = plan.out_buffer()[0]
+    launcher.launch(beta, ref)
+    G = torch.full_like(ref, 7.0)
+    launcher.launch(beta, G, torch.ones(1, dtype=torch.int32, device=DEV))
+    torch.cuda.synchronize()
+    assert torch.all(G == 7.0)
+    launcher.launch(beta, G, torch.zeros(1, dtype=torch.int32, device=DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(G, ref)
+
+
+def test_gated_put_and_next_gate(native):
+    """The put kernel of round i: open gate -> payload + signal, then next gate = (beta counter >=
+    stale_next); closed gate -> nothing put or signalled, next gate still decided."""
+    import uuid
+
+    C = native
+    flags = C.ShmFlags("/eh_gate_" + uuid.uuid4().hex[:12], 4, True)
+    try:
+        src = torch.arange(64, dtype=torch.float64, device=DEV) + 1.0
+        dst = torch.zeros_like(src)
+        counters = torch.zeros(4, dtype=torch.int32, device=DEV)
+        gate = torch.zeros(2, dtype=torch.int32, device=DEV)
+        flags.store(0, 5)  # beta counter: beta(4) is out
+        C.put_signal_gated(src, dst, flags.dev_addr(1), 5, counters, gate, flags.dev_addr(0), 6)
+        torch.cuda.synchronize()
+        assert torch.equal(dst, src) and flags.load(1) == 5 and gate.tolist() == [0, 0]
+        flags.store(0, 6)  # beta(5) out: the next round (5) is stale before it starts
+        C.put_signal_gated(src * 2, dst, flags.dev_addr(1), 6, counters, gate, flags.dev_addr(0), 6)
+        torch.cuda.synchronize()
+        assert torch.equal(dst, src * 2) and flags.load(1) == 6 and gate.tolist() == [0, 1]
+        gate[0] = 1  # a closed gate: the round was skipped
+        C.put_signal_gated(src * 3, dst, flags.dev_addr(1), 7, counters, gate, flags.dev_addr(0), 9)
+        torch.cuda.synchronize()
+        assert torch.equal(dst, src * 2) and flags.load(1) == 6 and gate.tolist() == [1, 0]
+        assert counters.tolist() == [0, 0, 0, 0]  # the block counter protocol is untouched by a skip
+    finally:
+        flags.close()
+
+
+# ---- multi-rank runs, ranks sharing the test box's GPU ---------------------------------------------
+from test_multiproc_gpu import _launch  # noqa: E402
+
+
+def _lazy_run(world, case, over, tmp_path, **env):
+    r = _launch(world, 0, "GD", str(tmp_path / "z.npz"), EH_TEST_CASE=json.dumps(case), EH_TEST_CFG=json.dumps(over),
+                EH_TEST_ROUND_TIMEOUT="30", **env)
+    owner = {int(w): int(o) for w, o in json.loads(str(r["owner"])).items()}
+    skipped = json.loads(str(r["skipped"]))
+    return r, owner, skipped
+
+
+@pytest.mark.parametrize("world,case,rule,k,groups,mean,R", [
+    (3, (1, 0, 0, 4, 1, 0), "count", 2, [0, 1, 2], 0.12, 14),                  # cyclic W=3 s=1
+    (4, (1, 0, 3, 5, 1, 3), "frc", 3, [0, 0, 1, 1], 0.12, 14),                 # AGC W=4 s=1 k=3
+    (8, (1, 0, 3, 9, 2, 6), "frc", 6, [0, 0, 0, 1, 1, 1, 2, 2], 0.3, 18),      # AGC W=8 s=2 k=6, 8 ranks
+])
+def test_lazy_drain_physically_late_ranks(world, case, rule, k, groups, mean, R, tmp_path):
+    """--delay-on worker --drain lazy, one logical worker per rank: every worker rank spins Exp(mean)
+    after its gradient; the master never waits for the tail and a rank still busy when the next beta
+    is out skips that round on the device.  Checked against the event model replayed along the run's
+    own round starts: the decode inputs on every round it can call with a margin, and every rank's
+    skip decision.  Late rows never reach a decode (every decoded mailbox row's integrity tag names
+    its round), and the trajectory replays exactly through the fp64 oracle."""
+    from lazy_check import check_lazy
+    from oracle import replay, stops_exactly_at_last
+    from test_engine_cpu import make
+
+    over = dict(add_delay=1, delay_mode="exp", delay_mean=mean, delay_on="worker", shard="message", drain="lazy",
+                num_itrs=R)
+    r, owner, skipped = _lazy_run(world, case, over, tmp_path)
+    cfg, src, sch, parts = make(case, "GD")
+    W = cfg.n_workers
+    d = np.stack([np.random.RandomState(i).exponential(mean, W) for i in range(R)])
+    arrivals = [[int(w) for (w, p) in a] for a in r["arrivals"]]
+    by_worker = {w: skipped[o] for w, o in owner.items() if o != 0}
+    n_rounds, n_skips = check_lazy(arrivals, r["loop_time"], d, rule, k, groups, MARGIN, by_worker,
+                                   local={w for w, o in owner.items() if o == 0})
+    assert n_rounds >= 3 and n_skips >= W
+    assert sum(len(v) for v in skipped) >= 1  # some rank fell behind and skipped a stale round
+    full = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    assert stops_exactly_at_last(sch, full)
+    ref = replay(sch, parts, r["beta0"], full, "GD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(R))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+    rep = json.loads(str(r["rank_report"]))
+    assert rep["drain"] == "lazy" and rep["round_loop"] == "native pump"
+    assert rep["stale_arrivals"] >= 1  # late messages landed during later rounds and were not decoded
+    reports = json.loads(str(r["reports"]))
+    assert sum(x.get("stale_rounds_skipped", 0) for x in reports) == sum(len(v) for v in skipped)
+
+
+@pytest.mark.parametrize("arbiter", [False, True])
+def test_lazy_fixed_straggler_is_skipped_and_costs_nothing(arbiter, tmp_path):
+    """AGC W=4 s=1 k=3 on 4 ranks, worker 3's rank 40 ms late every round (fixed straggler, physically
+    spun): with drain lazy the master's rounds never wait for it, the rank computes one round, then
+    finds every later round stale and skips it; on the host pump and on the device arbiter."""
+    from oracle import replay
+    from test_engine_cpu import make
+
+    case, R = (1, 0, 3, 5, 1, 3), 16
+    over = dict(add_delay=1, delay_mode="fixed", fixed_stragglers=[4], fixed_sleep=0.04, delay_on="worker",
+                shard="message", drain="lazy", num_itrs=R)
+    env = {"ERASUREHEAD_DEVICE_MASTER": "on"} if arbiter else {}
+    r, owner, skipped = _lazy_run(4, case, over, tmp_path, **env)
+    assert json.loads(str(r["rank_report"]))["round_loop"] == ("arbiter" if arbiter else "native pump")
+    for a in r["arrivals"]:
+        assert 3 not in {int(w) for (w, p) in a}
+    assert float(np.sum(r["loop_time"])) < 0.04 * R / 4  # the straggler's 40 ms never enter the rounds
+    late_rank = owner[3]
+    assert len(skipped[late_rank]) >= R - 4  # it ran a handful of rounds (one per 40 ms), skipped the rest
+    cfg, src, sch, parts = make(case, "GD")
+    full = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], full, "GD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(R))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+
+
+def test_carry_keeps_every_round_of_a_late_rank(tmp_path):
+    """The reference's no-Waitall semantics (drain carry): the late rank computes and sends every
+    round in order (no skipping), so it is still busy after the master's last round."""
+    case, R = (1, 0, 3, 5, 1, 3), 8
+    over = dict(add_delay=1, delay_mode="fixed", fixed_stragglers=[4], fixed_sleep=0.03, delay_on="worker",
+                shard="message", drain="carry", num_itrs=R)
+    r, owner, skipped = _lazy_run(4, case, over, tmp_path)
+    assert all(len(v) == 0 for v in skipped)
+    for a in r["arrivals"]:
+        assert 3 not in {int(w) for (w, p) in a}

@@ -73,3 +73,52 @@ def test_slow_rank_is_skipped_with_message_placement(tmp_path):
     for a in r["arrivals"]:
         assert 3 not in {w for (w, p) in a}
         assert len(a) in (2, 3)  # k = 3 arrivals or both groups covered
+
+
+@pytest.mark.parametrize("case,rule,k,groups", [
+    ((1, 0, 0, 4, 1, 0), "count", 2, [0, 1, 2]),           # cyclic W=3 s=1: the 2 fastest
+    ((1, 0, 3, 5, 1, 3), "frc", 3, [0, 0, 1, 1]),          # AGC W=4 s=1 k=3
+])
+def test_lazy_drain_virtual_model(case, rule, k, groups):
+    """Drain "lazy" on the collector's clock (one process, virtual Exp delays): the master never
+    waits for the straggler tail and a worker still busy when the next beta is out skips the stale
+    round (csrc/runtime/collector.h).  The decode inputs match the event model replayed along the
+    run's own round starts on every round it can call with a margin, late messages are never decoded
+    (the stop rule re-derived from the logged arrivals), and the trajectory replays exactly."""
+    from lazy_check import check_lazy
+    from oracle import replay, stops_exactly_at_last
+
+    from erasurehead_amd.engine import Trainer
+    from erasurehead_amd.parallel.dist import DistEnv
+
+    R, mean = 12, 0.2
+    cfg, src, sch, parts = make(case, "GD", delay_mode="exp", delay_mean=mean, drain="lazy")
+    cfg.num_itrs, cfg.add_delay, cfg.force_delay = R, 1, True
+    tr = Trainer(cfg, DistEnv(), src, scheme=sch)
+    res = tr.run()
+    d = np.stack([np.random.RandomState(i).exponential(mean, cfg.n_workers) for i in range(R)])
+    arrivals = [[w for (w, p, _) in a] for a in res.arrivals]
+    n_rounds, _ = check_lazy(arrivals, res.loop_time, d, rule, k, groups, MARGIN)
+    assert n_rounds >= 6
+    assert stops_exactly_at_last(sch, res.arrivals)
+    ref = replay(sch, parts, tr.beta0, res.arrivals, "GD", cfg.alpha_value, cfg.n_rows, cfg.eta())
+    np.testing.assert_allclose(res.betaset, ref, rtol=1e-10, atol=1e-12)
+    # nothing waits for the tail: every round ends at its stop (no drain phase)
+    np.testing.assert_allclose(res.loop_time, res.timeset, atol=0.02)
+    rep = tr.rank_report()
+    assert rep["drain"] == "lazy" and rep["stale_skipped_virtual"] >= 1
+
+
+def test_lazy_beats_drain_and_carry_in_wall_clock():
+    """Same delays, three drains (cyclic W=3 s=1): lazy's summed round time is the smallest and a
+    drained run pays the full straggler tail every round."""
+    from erasurehead_amd.engine import Trainer
+    from erasurehead_amd.parallel.dist import DistEnv
+
+    tot = {}
+    for drain in ("all", "carry", "lazy"):
+        cfg, src, sch, parts = make((1, 0, 0, 4, 1, 0), "GD", delay_mode="exp", delay_mean=0.05, drain=drain)
+        cfg.num_itrs, cfg.add_delay, cfg.force_delay = 12, 1, True
+        res = Trainer(cfg, DistEnv(), src, scheme=sch).run()
+        tot[drain] = float(np.sum(res.loop_time))
+    assert tot["lazy"] <= tot["carry"] + 0.02 and tot["lazy"] < tot["all"], tot
