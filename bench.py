@@ -88,6 +88,13 @@ def parse(argv=None):
                     help="N > 1: put -> flag round trips per worker/master pair before the timed rounds (0: off)")
     ap.add_argument("--share-partitions", action="store_true",
                     help="co-located workers stream each distinct partition once (not the headline)")
+    ap.add_argument("--drain", default=None, choices=["all", "carry", "lazy"],
+                    help="straggler tail (default: the scheme's reference behaviour; AGC drains)")
+    ap.add_argument("--late-ms", type=float, default=5.0,
+                    help="N > 1 straggler sub-run: the last rank is physically late by this much every round")
+    ap.add_argument("--straggler-steps", type=int, default=40, help="timed rounds of each straggler sub-run")
+    ap.add_argument("--no-straggler", action="store_true",
+                    help="N > 1: skip the reference-topology and straggler sub-runs")
     return ap.parse_args(argv)
 
 
@@ -133,16 +140,17 @@ def main(argv=None) -> int:
     env = init_distributed("auto")
 
     def make_cfg(rounds: int, naive: bool = a.naive, **kw) -> RunConfig:
+        opts = dict(add_delay=a.add_delay, num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234,
+                    seed=0, allow_uneven_groups=True, verbose=False, tasks=a.tasks, transport=a.transport,
+                    round_timeout=a.round_timeout, share_partitions=a.share_partitions, device_loop=a.device_loop,
+                    tie_break=a.tie_break, shard=a.shard, delay_mode=a.delay_mode, delay_mean=a.delay_mean,
+                    fixed_stragglers=a.fixed_stragglers, fixed_sleep=a.fixed_sleep, delay_on=a.delay_on,
+                    slow_ranks=parse_slow_ranks(a.slow_ranks), integrity=not a.no_integrity, drain=a.drain)
+        opts.update(kw)
+        add_delay = opts.pop("add_delay")
         return RunConfig(a.workers + 1, a.n_rows, a.n_cols, "/tmp/erasurehead_bench/", 0, "synthetic",
-                         0 if naive else 1,
-                         a.stragglers, 0, a.coded_ver, a.num_collect, a.add_delay, a.update_rule,
-                         num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234, seed=0,
-                         allow_uneven_groups=True, verbose=False, tasks=a.tasks,
-                         transport=a.transport, round_timeout=a.round_timeout,
-                         share_partitions=a.share_partitions, device_loop=kw.pop("device_loop", a.device_loop),
-                         tie_break=a.tie_break, shard=a.shard, delay_mode=a.delay_mode, delay_mean=a.delay_mean,
-                         fixed_stragglers=a.fixed_stragglers, fixed_sleep=a.fixed_sleep, delay_on=a.delay_on,
-                         slow_ranks=parse_slow_ranks(a.slow_ranks), integrity=not a.no_integrity, **kw)
+                         0 if naive else 1, a.stragglers, 0, a.coded_ver, a.num_collect, add_delay, a.update_rule,
+                         **opts)
 
     def free(tr):
         tr.close()
@@ -163,23 +171,25 @@ def main(argv=None) -> int:
     trainer = Trainer(make_cfg(w0 + a.steps), env)
     setup_s = time.perf_counter() - t_setup
     # the first multi-GPU run checks itself: put -> flag latency and payload checks per worker/master pair
-    preflight_failure = None
+    preflight_failure = fallback_preflight = None
     try:
         preflight = trainer.preflight(a.preflight) if env.world > 1 and a.preflight > 0 else None
     except TransportError as e:
         # every rank raised the same verdict (IpcTransport.preflight): the IPC mailbox lost a payload or a
         # signal.  Unless the IPC path was asked for by name, rebuild on RCCL p2p under the same pumps
         # (the loud fallback make_transport takes when the handshake fails) and record why.
-        if a.transport == "ipc" or os.environ.get("ERASUREHEAD_NO_FALLBACK") or env.backend == "gloo":
-            # ranks sharing a GPU (gloo control plane): the loopback communicator runs over the same IPC
-            # mappings and shared counters whose failure this is, so it is no independent fallback
+        if a.transport == "ipc" or os.environ.get("ERASUREHEAD_NO_FALLBACK"):
             raise
         preflight_failure, preflight = str(e), None
-        a.transport = "rccl"
+        a.transport = "rccl" if env.backend == "nccl" else "loopback"
         if env.is_master:
             print(f"[bench] WARNING: {e}; rebuilding on {a.transport}", file=sys.stderr, flush=True)
         free(trainer)
         trainer = Trainer(make_cfg(w0 + a.steps), env)
+        # the fallback checks itself before anything is timed: round trips over its own send/recv
+        # path (loopback runs over the same IPC mappings and shared counters as the mailbox whose
+        # check failed, so it is no independent path until it has passed this)
+        fallback_preflight = trainer.tx.preflight(min(200, a.preflight))
     res = trainer.run(timed_start=w0)
     mine = res.timed_seconds if env.is_master else trainer.worker_timed_seconds
     timed = env.allreduce_max(mine)
@@ -245,6 +255,10 @@ def main(argv=None) -> int:
             out["peer_preflight"] = preflight
         if preflight_failure is not None:
             out["peer_preflight_failure"] = preflight_failure
+            out["fallback_preflight"] = fallback_preflight
+            out["fallback_mechanism"] = ("loopback: device copies through IPC staging rings + shared counters (the "
+                                         "mailbox's mechanism), checked by fallback_preflight before timing"
+                                         if trainer.transport == "loopback" else "RCCL p2p (ncclSend / ncclRecv)")
         if n_gpu_dev and env.world > n_gpu_dev:
             out["config"]["ranks_per_gpu"] = env.world / n_gpu_dev  # rehearsal: ranks time-share GPUs
         out["config"]["round_loop"] = {"graph": "device-driven, hipGraph", "stream": "device-driven",
@@ -293,6 +307,58 @@ def main(argv=None) -> int:
             if k is not None:
                 rep["kernel_us_isolated"] = round(k, 1)
         out["ranks"] = reports
+
+    # ---- 2b. N > 1: the reference topology and a physically late rank -------------------------------
+    # The headline places partition shards (bandwidth: each GPU streams its partitions once), whose
+    # replicas of a partition share one rank, so a slow GPU stalls every message with a shard there.
+    # The reference runs one worker per process (ref run_approx_coding.sh:47-49,
+    # src/approximate_coding.py:47-53): message placement.  On it, one rank is made late by --late-ms
+    # every round (a device spin after its gradient, before its put: ref src/naive.py:141-148), and
+    # AGC with a lazy drain (no wait for the tail, stale rounds skipped on the late rank) is timed
+    # against naive (which must wait for every worker), each with and without the straggler.
+    if env.world > 1 and not a.no_straggler:
+        S, W = a.straggler_steps, a.workers
+        late_rank = env.world - 1
+        late_workers = [w for w in range(W) if w % env.world == late_rank]  # parallel/placement.py place_spread
+        keys = ("rank", "workers", "round_loop", "kernel_us", "wait_k_us", "beta_wait_us", "stale_rounds_skipped",
+                "stale_arrivals", "stale_skipped_virtual", "arbiter_poll_us")
+
+        def sub_run(naive: bool, late: bool, **kw):
+            extra = dict(shard="message", drain=kw.pop("drain", None), **kw)
+            if late:
+                extra.update(add_delay=1, delay_mode="fixed", delay_on="worker", fixed_sleep=a.late_ms / 1e3,
+                             fixed_stragglers=[w + 1 for w in late_workers], force_delay=True)
+            else:
+                extra.update(add_delay=0)
+            tr_s = Trainer(make_cfg(a.warmup + S, naive=naive, **extra), env)
+            r_s = tr_s.run(timed_start=a.warmup)
+            t_s = env.allreduce_max(r_s.timed_seconds if env.is_master else tr_s.worker_timed_seconds)
+            reps = env.gather_objects(tr_s.rank_report())
+            rec = None
+            if env.is_master:
+                lt = np.asarray(r_s.loop_time[a.warmup:])
+                rec = {"ms_per_step": 1e3 * t_s / S, "round_ms_mean": float(1e3 * np.mean(lt)),
+                       "round_ms_median": float(1e3 * np.median(lt)), "drain": tr_s.drain_mode,
+                       "ranks": [{k: x[k] for k in keys if k in x} for x in reps]}
+            free(tr_s)
+            return rec
+
+        topo = sub_run(a.naive, False)
+        straggler = {
+            "late_rank": late_rank, "late_workers": late_workers, "late_ms": a.late_ms, "placement": "message",
+            "steps": S, "agc_lazy": sub_run(False, True, drain="lazy"),
+            "agc_lazy_no_straggler": sub_run(False, False, drain="lazy"),
+            "naive": sub_run(True, True), "naive_no_straggler": sub_run(True, False)}
+        if env.is_master:
+            out["message_placement_ms_per_step"] = topo["ms_per_step"]
+            out["message_placement"] = topo
+            for name in ("agc_lazy", "naive"):  # the master's round period: late vs on time
+                straggler[f"{name}_round_slowdown"] = (straggler[name]["round_ms_mean"]
+                                                      / straggler[f"{name}_no_straggler"]["round_ms_mean"])
+            straggler["definition"] = ("round_ms_*: mean master round (beta(i) out -> beta(i+1) out) over the timed "
+                                       "rounds; ms_per_step: fenced wall-clock / steps (includes the late rank's "
+                                       "last in-flight round)")
+            out["straggler"] = straggler
 
     # ---- 3. convergence: naive (exact GD) sets the common loss target, then the scheme -------------
     if not a.no_floor:

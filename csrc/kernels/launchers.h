@@ -177,7 +177,9 @@ struct PingArgs {
 };
 hipError_t ping_pong_launch(const PingArgs& a, bool master, hipStream_t st);
 // Spin on the device for `ticks` wall_clock64 ticks (a physically late worker, --delay-on worker), after
-// the round's gradient and before its put; a skipped round (gate_closed) does not spin.
-hipError_t spin_launch(long long ticks, hipStream_t st, const int* gate = nullptr);
+// the round's gradient and before its put; a skipped round (gate_closed) does not spin, and a spin
+// ends early once *stop >= stop_at (the master's end-of-run release of a lazy-drain run).
+hipError_t spin_launch(long long ticks, hipStream_t st, const int* gate = nullptr,
+                       const unsigned long long* stop = nullptr, unsigned long long stop_at = 0);
 
 }  // namespace eh

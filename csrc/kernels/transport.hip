@@ -151,10 +151,15 @@ __global__ void __launch_bounds__(1024) check_list(const CheckList cl, Integrity
   check_rows_waves(cl, 0, static_cast<int>(blockDim.x >> 6), err, &claim);
 }
 
-__global__ void spin_ticks(long long ticks, const int* gate) {
+__global__ void spin_ticks(long long ticks, const int* gate, const unsigned long long* stop, unsigned long long stop_at) {
   if (gate_closed(gate)) return;
   const long long t0 = wall_clock64();
-  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+  while (wall_clock64() - t0 < ticks) {
+    // the master's run is over (its end-of-run release): nothing this rank still does can matter
+    if (stop && __hip_atomic_load(const_cast<unsigned long long*>(stop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= stop_at)
+      return;
+    __builtin_amdgcn_s_sleep(127);
+  }
 }
 
 // Device ping-pong of the transport preflight (parallel/transport.py IpcTransport.preflight), one
@@ -256,9 +261,10 @@ hipError_t check_list_launch(const CheckList& cl, IntegrityErr* err, hipStream_t
   return hipGetLastError();
 }
 
-hipError_t spin_launch(long long ticks, hipStream_t st, const int* gate) {
+hipError_t spin_launch(long long ticks, hipStream_t st, const int* gate, const unsigned long long* stop,
+                       unsigned long long stop_at) {
   if (ticks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(spin_ticks, dim3(1), dim3(64), 0, st, ticks, gate);
+  hipLaunchKernelGGL(spin_ticks, dim3(1), dim3(64), 0, st, ticks, gate, stop, stop_at);
   return hipGetLastError();
 }
 

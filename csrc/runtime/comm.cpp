@@ -16,6 +16,7 @@
 #include <torch/extension.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -182,6 +183,131 @@ class LoopbackComm : public eh::P2PComm {
   std::map<int, Chan> out_, in_;
 };
 
+// RcclSelfLoop: RCCL on ONE GPU, for the one-GPU test box (RCCL refuses two ranks on one device).
+// The master and its worker ranks are threads of one process (parallel/dist.py ThreadEnv), each
+// with its own stream; every (sender, receiver) channel owns a 1-rank RCCL communicator and a
+// staging ring of `depth` slots.  send #s waits until the receiver consumed #s-depth, moves the
+// payload into slot s % depth with a GROUPED ncclSend + ncclRecv to self (RCCL's own p2p kernel does
+// the copy) and release-stores ready = s; recv #s waits for ready >= s, copies the slot out and
+// stores consumed = s.  So the pumps' comm mode runs RCCL calls (ncclCommInitRank, ncclSend,
+// ncclRecv, ncclGroupStart/End) on the test box with the exact FIFO semantics of RcclComm.
+class RcclSelfLoop {
+ public:
+  RcclSelfLoop(int device, int world, int depth, int64_t cap) : device_(device), world_(world), depth_(depth), cap_(cap) {
+    need(world >= 2 && depth >= 1 && cap > 0 && cap % 16 == 0, "RcclSelfLoop: bad shape");
+    hcheck(hipSetDevice(device), "hipSetDevice");
+    int can = 0;
+    hcheck(hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device), "hipDeviceGetAttribute");
+    need(can != 0, "RcclSelfLoop needs hipStreamWaitValue64");
+    const int nch = 2 * (world - 1);
+    hcheck(hipHostMalloc(reinterpret_cast<void**>(&flags_h_), sizeof(uint64_t) * 2 * nch,
+                         hipHostMallocMapped | hipHostMallocCoherent),
+           "hipHostMalloc(flags)");
+    std::memset(flags_h_, 0, sizeof(uint64_t) * 2 * nch);
+    hcheck(hipHostGetDevicePointer(reinterpret_cast<void**>(&flags_d_), flags_h_, 0), "hipHostGetDevicePointer");
+    counters_ = at::zeros({nch}, at::TensorOptions().dtype(at::kInt).device(at::Device(at::kCUDA, device)));
+    rings_ = at::zeros({static_cast<int64_t>(nch) * depth * cap}, at::TensorOptions().dtype(at::kByte).device(
+                                                                     at::Device(at::kCUDA, device)));
+    chans_.resize(nch);
+    for (int k = 0; k < nch; ++k) {
+      ncclUniqueId id;
+      ncheck(ncclGetUniqueId(&id), "ncclGetUniqueId");
+      Chan& c = chans_[k];
+      ncheck(ncclCommInitRank(&c.comm, 1, id, 0), "ncclCommInitRank(1 rank)");
+      c.ring = static_cast<char*>(rings_.data_ptr()) + static_cast<int64_t>(k) * depth * cap;
+      c.ready_h = flags_h_ + 2 * k;
+      c.consumed_h = flags_h_ + 2 * k + 1;
+      c.ready_d = reinterpret_cast<unsigned long long*>(flags_d_ + 2 * k);
+      c.consumed_d = reinterpret_cast<unsigned long long*>(flags_d_ + 2 * k + 1);
+      c.counter = reinterpret_cast<unsigned int*>(counters_.data_ptr<int>()) + k;
+    }
+  }
+  ~RcclSelfLoop() {
+    hipDeviceSynchronize();
+    for (auto& c : chans_)
+      if (c.comm) aborted_ ? ncclCommAbort(c.comm) : ncclCommDestroy(c.comm);
+    if (flags_h_) hipHostFree(flags_h_);
+  }
+  // from -> to, called by the sending thread on its stream
+  void send(int from, int to, const void* buf, int64_t bytes, hipStream_t st) {
+    Chan& c = chan(from, to, bytes);
+    const uint64_t s = ++c.send_seq;
+    if (s > static_cast<uint64_t>(depth_))
+      hcheck(hipStreamWaitValue64(st, c.consumed_d, s - depth_, hipStreamWaitValueGte), "hipStreamWaitValue64(consumed)");
+    void* slot = c.ring + static_cast<int64_t>(s % depth_) * cap_;
+    ncheck(ncclGroupStart(), "ncclGroupStart");
+    ncheck(ncclSend(buf, static_cast<size_t>(bytes), ncclUint8, 0, c.comm, st), "ncclSend(self)");
+    ncheck(ncclRecv(slot, static_cast<size_t>(bytes), ncclUint8, 0, c.comm, st), "ncclRecv(self)");
+    ncheck(ncclGroupEnd(), "ncclGroupEnd");
+    hcheck(eh::signal_launch(c.ready_d, s, st), "signal(ready)");
+    ++sends_;
+  }
+  // from -> to, called by the receiving thread on its stream
+  void recv(int from, int to, void* buf, int64_t bytes, hipStream_t st) {
+    Chan& c = chan(from, to, bytes);
+    const uint64_t s = ++c.recv_seq;
+    hcheck(hipStreamWaitValue64(st, c.ready_d, s, hipStreamWaitValueGte), "hipStreamWaitValue64(ready)");
+    eh::PutArgs a{};
+    a.n = 1;
+    a.d[0] = eh::PutDesc{c.ring + static_cast<int64_t>(s % depth_) * cap_, buf, bytes, c.consumed_d, s, c.counter};
+    const int blocks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(64, (bytes / 16 + 4095) / 4096)));
+    hcheck(eh::put_signal_launch(a, blocks, st), "put_signal(self-loop recv)");
+  }
+  void abort() {  // release every queued wait (data after it is garbage)
+    aborted_ = true;
+    const uint64_t top = uint64_t{1} << 62;
+    for (auto& c : chans_) {
+      __atomic_store_n(c.ready_h, top, __ATOMIC_RELEASE);
+      __atomic_store_n(c.consumed_h, top, __ATOMIC_RELEASE);
+    }
+  }
+  int64_t rccl_sends() const { return sends_; }
+  int world() const { return world_; }
+
+ private:
+  struct Chan {
+    ncclComm_t comm = nullptr;
+    char* ring = nullptr;
+    uint64_t* ready_h = nullptr;
+    uint64_t* consumed_h = nullptr;
+    unsigned long long* ready_d = nullptr;
+    unsigned long long* consumed_d = nullptr;
+    unsigned int* counter = nullptr;
+    uint64_t send_seq = 0, recv_seq = 0;
+  };
+  // channels: k = r - 1 for master -> worker rank r, world - 1 + r - 1 for r -> master
+  Chan& chan(int from, int to, int64_t bytes) {
+    need(bytes > 0 && bytes <= cap_ && bytes % 16 == 0, "RcclSelfLoop: message larger than its slot");
+    need((from == 0) != (to == 0) && from >= 0 && to >= 0 && from < world_ && to < world_,
+         "RcclSelfLoop: channels run between the master (0) and a worker rank");
+    return from == 0 ? chans_[to - 1] : chans_[world_ - 1 + from - 1];
+  }
+  int device_, world_, depth_;
+  int64_t cap_;
+  uint64_t* flags_h_ = nullptr;
+  uint64_t* flags_d_ = nullptr;
+  Tensor counters_, rings_;
+  std::vector<Chan> chans_;
+  bool aborted_ = false;
+  std::atomic<int64_t> sends_{0};
+};
+
+// One thread-rank's view of an RcclSelfLoop: send(peer) = channel (me -> peer), recv(peer) = (peer -> me).
+class RcclSelfView : public eh::P2PComm {
+ public:
+  RcclSelfView(std::shared_ptr<RcclSelfLoop> loop, int me) : loop_(std::move(loop)), me_(me) {
+    need(me >= 0 && me < loop_->world(), "RcclSelfView: rank out of range");
+  }
+  void send(int peer, const void* buf, int64_t bytes, hipStream_t st) override { loop_->send(me_, peer, buf, bytes, st); }
+  void recv(int peer, void* buf, int64_t bytes, hipStream_t st) override { loop_->recv(peer, me_, buf, bytes, st); }
+  void abort() override { loop_->abort(); }
+  std::string kind() const override { return "rccl-self"; }
+
+ private:
+  std::shared_ptr<RcclSelfLoop> loop_;
+  int me_;
+};
+
 hipStream_t cur_stream(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
 }  // namespace
@@ -203,6 +329,13 @@ void bind_comm(py::module& m) {
   py::class_<RcclComm, P2PComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def(py::init<int, const std::vector<std::tuple<int, std::string, std::string, int>>&>(), py::arg("device"),
            py::arg("links"));
+  py::class_<RcclSelfLoop, std::shared_ptr<RcclSelfLoop>>(m, "RcclSelfLoop")
+      .def(py::init<int, int, int, int64_t>(), py::arg("device"), py::arg("world"), py::arg("depth"), py::arg("cap"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("view", [](std::shared_ptr<RcclSelfLoop> l, int me) { return std::make_shared<RcclSelfView>(l, me); })
+      .def("abort", &RcclSelfLoop::abort)
+      .def_property_readonly("rccl_sends", &RcclSelfLoop::rccl_sends);
+  py::class_<RcclSelfView, P2PComm, std::shared_ptr<RcclSelfView>>(m, "RcclSelfView");
   py::class_<LoopbackComm, P2PComm, std::shared_ptr<LoopbackComm>>(m, "LoopbackComm")
       .def(py::init<int, const std::vector<std::tuple<int, std::string, uintptr_t, int64_t, int, uintptr_t, uintptr_t,
                                                       uintptr_t, uintptr_t>>&>(),

@@ -1574,7 +1574,8 @@ class WorkerPump {
         hcheck(g_->launch(beta, g, stream_, gate), "worker gradient");
         if (timing_) record_t(i, 1);
         if (!late_ticks_.empty() && late_ticks_[i] > 0)  // after compute, before the send (ref src/naive.py:141-148)
-          hcheck(eh::spin_launch(late_ticks_[i], stream_, gate), "late worker spin");
+          hcheck(eh::spin_launch(late_ticks_[i], stream_, gate, skip_flag_, static_cast<unsigned long long>(R_) + 1),
+                 "late worker spin");
         eh::PutArgs pa{};
         pa.n = 1;
         pa.d[0] = pd;

@@ -590,7 +590,7 @@ class Trainer:
         kern = self._kernel_label()
         if kern:
             rep["grad_kernel"] = kern
-        if self.tx is not None and self.tx.name in ("rccl", "loopback"):
+        if self.tx is not None and self.tx.name in ("rccl", "loopback", "rccl-self"):
             from .. import HW_QUEUES
 
             rep["hw_queues"] = int(HW_QUEUES)  # what HIP started with, not the (possibly later) environment

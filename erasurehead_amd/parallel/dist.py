@@ -73,6 +73,102 @@ class DistEnv:
                 pass
 
 
+class ThreadGroup:
+    """In-process rendezvous of ThreadEnv ranks (barriers with a deadline: a rank that fails breaks
+    the group, so the others raise instead of waiting forever)."""
+
+    def __init__(self, world: int, timeout: float = 300.0):
+        import threading
+
+        self.world = world
+        self.timeout = timeout
+        self._bar = threading.Barrier(world)
+        self.slots: List[Any] = [None] * world
+
+    def wait(self) -> None:
+        self._bar.wait(self.timeout)
+
+    def abort(self) -> None:
+        self._bar.abort()
+
+
+@dataclass
+class ThreadEnv(DistEnv):
+    """Ranks as THREADS of one process sharing one GPU (backend "threads").
+
+    RCCL refuses two processes on one device, so the one-GPU test box cannot run the RCCL transport
+    across processes; with every rank a thread of one process, each on its own HIP stream, the
+    native pumps run their comm mode over a real RCCL path (parallel/transport.py "rccl-self",
+    csrc/runtime/comm.cpp RcclSelfLoop).  Collectives are in-process: broadcast hands every rank the
+    SAME object (so the self-loop communicator is shared), the others copy nothing either.
+    """
+    group: Any = None
+
+    def barrier(self) -> None:
+        self.group.wait()
+
+    def broadcast_object(self, obj, src: int = 0):
+        g = self.group
+        if self.rank == src:
+            g.slots[src] = obj
+        g.wait()
+        out = g.slots[src]
+        g.wait()
+        return out
+
+    def allreduce_max(self, x: float) -> float:
+        g = self.group
+        g.slots[self.rank] = float(x)
+        g.wait()
+        m = max(g.slots)
+        g.wait()
+        return m
+
+    def gather_objects(self, obj) -> Optional[List[Any]]:
+        g = self.group
+        g.slots[self.rank] = obj
+        g.wait()
+        out = list(g.slots) if self.rank == 0 else None
+        g.wait()
+        return out
+
+    def shutdown(self) -> None:
+        pass
+
+
+def run_thread_ranks(world: int, fn, timeout: float = 300.0) -> List[Any]:
+    """Run ``fn(env)`` on ``world`` thread-ranks of this process (cuda:0, one stream per rank);
+    returns their results in rank order, or raises the first failure (the group is broken so no
+    rank waits forever)."""
+    import threading
+
+    group = ThreadGroup(world, timeout)
+    out: List[Any] = [None] * world
+    errs: List[BaseException] = []
+
+    def body(rank: int) -> None:
+        try:
+            torch.cuda.set_device(0)
+            env = ThreadEnv(rank=rank, world=world, local_rank=rank, device=torch.device("cuda", 0),
+                            backend="threads", group=group)
+            with torch.cuda.stream(torch.cuda.Stream()):
+                out[rank] = fn(env)
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            errs.append(e)
+            group.abort()
+
+    ths = [threading.Thread(target=body, args=(r,), name=f"eh-rank{r}") for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout + 60.0)
+    if any(t.is_alive() for t in ths):
+        raise TimeoutError("thread ranks did not finish")
+    if errs:
+        raise errs[0]
+    return out
+
+
 def init_distributed(device: str = "auto", timeout_min: float = 60.0) -> DistEnv:
     """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))

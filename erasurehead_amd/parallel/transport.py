@@ -18,6 +18,10 @@ interchangeable transports implement that contract here; the engine never branch
             collector; driven by the same native pumps as ``ipc``.
   ``loopback`` the rccl path's exact semantics over IPC staging rings, for ranks sharing a GPU
             (RCCL refuses that): how the single-GPU box tests the RCCL pump code.
+  ``rccl-self`` ranks as threads of ONE process on one GPU (parallel/dist.py ThreadEnv): every
+            channel is a 1-rank RCCL communicator whose grouped ncclSend + ncclRecv to self moves
+            the payload through a staging ring, so the pumps' comm mode executes real RCCL calls
+            on the one-GPU box (csrc/runtime/comm.cpp RcclSelfLoop).
   ``gloo``  CPU tensors over gloo (tests, multi-process plumbing without a GPU).
 
 Buffers are per (round mod K) for messages and per round for beta, so a lagging worker can
@@ -195,6 +199,13 @@ class CommTransport(Transport):
             self.comm = C.RcclComm(self.dev, links)
         elif kind == "loopback":
             self.comm = self._loopback(counts)
+        elif kind == "rccl-self":  # thread ranks of one process (parallel/dist.py ThreadEnv): RCCL on one GPU
+            if env.backend != "threads":
+                raise ValueError("the rccl-self transport runs ranks as threads of one process (ThreadEnv)")
+            cap = max([self.ld * self.es] + [n * self.ld * self.es for n in counts.values()])
+            loop = C.RcclSelfLoop(self.dev, env.world, self.DEPTH, cap) if env.is_master else None
+            self.selfloop = env.broadcast_object(loop, 0)
+            self.comm = self.selfloop.view(env.rank)
         else:
             raise ValueError(f"unknown communicator {kind!r}")
         env.barrier()
@@ -270,6 +281,70 @@ class CommTransport(Transport):
             peers = range(1, self.env.world) if self.env.is_master else [0]
             self._ps = {r: torch.cuda.Stream(self.env.device) for r in peers}
         return self._ps
+
+    # ---- preflight -------------------------------------------------------------------------
+    def preflight(self, iters: int = 200, timeout: float = 30.0) -> List[dict]:
+        """Collective.  ``iters`` send -> echo round trips of one row between the master and each worker
+        rank in turn over THIS communicator (the pumps' own send/recv path), host-timed, every echo
+        checked; a wait past ``timeout`` aborts the communicator and raises (never a hang).  Both sides
+        issue the same number of operations per channel, so the FIFO pairing of the training rounds
+        is unchanged.  Returns one record per worker rank on every rank."""
+        env = self.env
+        x = torch.zeros(self.ld, dtype=self.dtype, device=env.device)
+        y = torch.empty_like(x)
+        ev = torch.cuda.Event()
+
+        def wait(what):
+            t0 = time.perf_counter()
+            while not ev.query():
+                if time.perf_counter() - t0 > timeout:
+                    self.comm.abort()
+                    raise TransportError(f"{self.name} preflight: {what} did not complete within {timeout:.0f}s")
+                time.sleep(2e-5)
+
+        recs: Dict[int, dict] = {}
+        err = None
+        for r in range(1, env.world):
+            env.barrier()
+            if env.is_master:
+                ts, bad = [], 0
+                try:
+                    for k in range(iters):
+                        x.fill_(float(k % 1000) + 0.5)
+                        t0 = time.perf_counter()
+                        self.comm.send(r, x)
+                        self.comm.recv(r, y)
+                        ev.record()
+                        wait(f"rank 0 <-> rank {r} round trip {k}")
+                        ts.append(1e6 * (time.perf_counter() - t0))
+                        bad += int(not bool(torch.equal(x, y)))
+                except TransportError as e:
+                    err = str(e)
+                us = np.sort(np.asarray(ts)) if ts else np.zeros(1)
+                recs[r] = {"rank": r, "iters": len(ts), "path": self.name,
+                           "rtt_clock": "host, send + echo receive complete",
+                           "rtt_us_p50": round(float(us[len(us) // 2]), 2),
+                           "rtt_us_p99": round(float(us[min(len(us) - 1, int(0.99 * len(us)))]), 2),
+                           "payload_errors": bad}
+                if bad and err is None:
+                    err = f"{self.name} preflight: rank 0 <-> rank {r}: {bad} echoed rows differ"
+            elif env.rank == r:
+                try:
+                    for k in range(iters):
+                        self.comm.recv(0, y)
+                        self.comm.send(0, y)
+                    ev.record()
+                    wait(f"rank {r} echo")
+                except TransportError as e:
+                    err = str(e)
+            err = env.broadcast_object(err, 0) if env.is_master else env.broadcast_object(None, 0)
+            if err:
+                break
+        out = env.broadcast_object([recs[r] for r in sorted(recs)] if env.is_master else None, 0)
+        env.barrier()
+        if err:
+            raise TransportError(err)
+        return out
 
     # ---- native pumps --------------------------------------------------------------------
     def sender_rows(self):
@@ -750,7 +825,7 @@ def make_transport(kind: str, env, R: int, K: int, ld: int, dtype, n_local: int,
         return GlooTransport(*args)
     if kind == "gloo":
         raise ValueError("gloo transport is the CPU path; GPU ranks use ipc or rccl")
-    if kind in ("rccl", "loopback"):
+    if kind in ("rccl", "loopback", "rccl-self"):
         return CommTransport(*args, kind=kind)
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(env.world)))
     if kind == "auto" and local_world < env.world and env.backend != "gloo":

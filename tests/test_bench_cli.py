@@ -23,7 +23,8 @@ def _env():
 
 def test_bench_gpus3_relaunches_three_ranks(tmp_path):
     out = tmp_path / "b.json"
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", *TINY, "--json-out", str(out)],
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", *TINY, "--straggler-steps", "6",
+                        "--json-out", str(out)],
                        cwd=str(tmp_path), env=_env(), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     d = json.loads(out.read_text())
@@ -47,6 +48,15 @@ def test_bench_gpus3_relaunches_three_ranks(tmp_path):
     assert 0 < d["fraction_of_rows_used_in_decode"] <= 1
     assert d["host_driven_ms_per_step"] > 0
     assert d["loss_target"] > 0 and d["naive_iters_to_loss_floor"] is not None
+    # the reference topology (one message per rank) and the straggler sub-run, in the same JSON
+    assert d["message_placement_ms_per_step"] > 0
+    st = d["straggler"]
+    assert st["late_rank"] == 2 and st["late_workers"] == [2, 5] and st["placement"] == "message"
+    for k in ("agc_lazy", "agc_lazy_no_straggler", "naive", "naive_no_straggler"):
+        assert st[k]["ms_per_step"] > 0 and [x["rank"] for x in st[k]["ranks"]] == [0, 1, 2]
+    assert st["agc_lazy"]["drain"] == "lazy" and st["naive"]["drain"] == "carry"
+    assert st["naive"]["round_ms_mean"] >= 5.0  # naive waits for the late rank every round
+    assert st["agc_lazy_round_slowdown"] > 0 and st["naive_round_slowdown"] > 1.0
 
 
 def test_bench_world_size_mismatch_fails(tmp_path):
@@ -92,4 +102,7 @@ def test_bench_preflight_failure_rebuilds_on_comm_path(tmp_path):
     assert "payload words wrong" in d["peer_preflight_failure"] and "rank 1" in d["peer_preflight_failure"]
     assert "peer_preflight" not in d
     assert all(x["transport"] == "loopback" for x in d["ranks"])
+    fp = d["fallback_preflight"]  # the fallback was checked over its own path before timing
+    assert [x["rank"] for x in fp] == [1] and fp[0]["payload_errors"] == 0 and fp[0]["path"] == "loopback"
+    assert "same" in d["fallback_mechanism"] or "mailbox" in d["fallback_mechanism"]
     assert d["ms_per_step"] > 0

@@ -10,7 +10,8 @@ time by the native collector (csrc/runtime/collector.h), so the master's waits a
 wall-clock waits while the GPU never sleeps.
 
 Schemes (ref main.py:62-92): naive; cyclic-MDS s=2; FRC s=1 and s=3; AGC s=1 k=6, s=3 k=6 and
-the uneven s=2 k=6 extension (groups {0,1,2},{3,4,5},{6,7}).
+the uneven s=2 k=6 extension (groups {0,1,2},{3,4,5},{6,7}); and, with --drain lazy (no wait for
+the straggler tail, stale rounds skipped), cyclic s=2, FRC s=1, AGC s=1 k=6 and the uneven AGC.
 
 Per scheme:
   sum_timeset_s        reference `timeset` semantics: round start -> decoded + updated
@@ -39,15 +40,20 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-# name -> (is_coded, coded_ver, s, k)
+# name -> (is_coded, coded_ver, s, k, drain): drain None = the scheme's reference behaviour (FRC / AGC
+# wait for the tail, the others carry lag); "lazy" = no wait, stale rounds skipped (engine/trainer.py)
 SCHEMES = {
-    "naive": (0, 0, 0, 0),
-    "cyclic_s2": (1, 0, 2, 0),
-    "frc_s1": (1, 1, 1, 0),
-    "frc_s3": (1, 1, 3, 0),
-    "agc_s1_k6": (1, 3, 1, 6),
-    "agc_s3_k6": (1, 3, 3, 6),
-    "agc_s2_k6_uneven": (1, 3, 2, 6),
+    "naive": (0, 0, 0, 0, None),
+    "cyclic_s2": (1, 0, 2, 0, None),
+    "frc_s1": (1, 1, 1, 0, None),
+    "frc_s3": (1, 1, 3, 0, None),
+    "agc_s1_k6": (1, 3, 1, 6, None),
+    "agc_s3_k6": (1, 3, 3, 6, None),
+    "agc_s2_k6_uneven": (1, 3, 2, 6, None),
+    "cyclic_s2_lazy": (1, 0, 2, 0, "lazy"),
+    "frc_s1_lazy": (1, 1, 1, 0, "lazy"),
+    "agc_s1_k6_lazy": (1, 3, 1, 6, "lazy"),
+    "agc_s2_k6_uneven_lazy": (1, 3, 2, 6, "lazy"),
 }
 
 
@@ -57,13 +63,13 @@ def run_one(name: str, rounds: int, n_rows: int, n_cols: int, out: str) -> None:
     from erasurehead_amd.config import RunConfig
     from erasurehead_amd.engine import Trainer, evaluate
     from erasurehead_amd.parallel.dist import DistEnv
-    from erasurehead_amd.utils.delay import delay_floor
+    from erasurehead_amd.utils.delay import delay_floor, schedule
 
-    is_coded, ver, s, k = SCHEMES[name]
+    is_coded, ver, s, k, drain = SCHEMES[name]
     W = 8
     cfg = RunConfig(W + 1, n_rows, n_cols, "/tmp/eh_conv/", 0, "synthetic", is_coded, s, 0, ver, k, 1, "AGD",
                     num_itrs=rounds, data="synthetic", data_seed=1234, seed=0, allow_uneven_groups=True,
-                    verbose=False, round_timeout=120.0)
+                    verbose=False, round_timeout=120.0, drain=drain)
     env = DistEnv(device=torch.device("cuda" if torch.cuda.is_available() else "cpu"))
     tr = Trainer(cfg, env)
     t0 = time.perf_counter()
@@ -72,7 +78,12 @@ def run_one(name: str, rounds: int, n_rows: int, n_cols: int, out: str) -> None:
     sch = tr.scheme
     tr.cfg.fix_quirks = True
     ev = evaluate(tr, res, write=False)
-    if name == "naive":
+    if drain == "lazy":  # the event model with stale-round skipping, zero compute (utils/delay.schedule)
+        d = np.stack([np.random.RandomState(i).exponential(0.5, W) for i in range(rounds)])
+        rule = "count" if ver == 0 else "frc"
+        kk = W - s if ver == 0 else (k if ver == 3 else W)
+        floor = _schedule_floor(d, rule, kk, list(sch.group_of))
+    elif name == "naive":
         floor = delay_floor(W, rounds, stop_count=W)
     elif ver == 0:
         floor = delay_floor(W, rounds, stop_count=W - s, carry=True)
@@ -80,7 +91,8 @@ def run_one(name: str, rounds: int, n_rows: int, n_cols: int, out: str) -> None:
         kk = k if ver == 3 else W
         floor = delay_floor(W, rounds, groups=list(sch.group_of), k=kk)
     rec = {
-        "scheme": name, "s": s, "k": k, "rounds": rounds, "n_rows": n_rows, "n_cols": n_cols,
+        "scheme": name, "s": s, "k": k, "drain": tr.drain_mode, "rounds": rounds, "n_rows": n_rows, "n_cols": n_cols,
+        "stale_skipped": int(tr.rank_stats.get("stale_skipped_virtual", 0) or 0),
         "sum_timeset_s": float(np.sum(res.timeset)), "delay_floor_s": float(floor),
         "overhead_ms_per_round": 1e3 * (float(np.sum(res.timeset)) - floor) / rounds,
         "loop_wallclock_s": float(np.sum(res.loop_time)), "run_wallclock_s": wall,
@@ -93,6 +105,31 @@ def run_one(name: str, rounds: int, n_rows: int, n_cols: int, out: str) -> None:
         f.write(json.dumps(rec) + "\n")
     print(f"[{name}] done: sum timeset {rec['sum_timeset_s']:.2f} s, floor {floor:.2f} s, "
           f"loop {rec['loop_wallclock_s']:.2f} s, final loss {rec['train_loss'][-1]:.5f}", flush=True)
+
+
+def _schedule_floor(d, rule, k, groups) -> float:
+    """Sum of the master's round lengths in the zero-compute lazy-drain event model (t_R)."""
+    from erasurehead_amd.utils.delay import schedule  # noqa: F401 - the model whose stop times are summed
+
+    R, W = d.shape
+    F = np.full(W, -np.inf)
+    t = 0.0
+    n_groups = len(set(groups))
+    for i in range(R):
+        st = np.maximum(t, F)
+        a = st + d[i]
+        got, cov, t_next = 0, set(), np.inf
+        for w in sorted(range(W), key=lambda w: (a[w], w)):
+            got += 1
+            cov.add(groups[w])
+            if (rule == "count" and got >= k) or (rule == "frc" and (got >= k or len(cov) == n_groups)):
+                t_next = a[w]
+                break
+        for w in range(W):
+            if F[w] <= t or st[w] < t_next:
+                F[w] = a[w]
+        t = t_next
+    return float(t)
 
 
 def summarize(recs, out_dir: str) -> str:
@@ -110,6 +147,10 @@ def summarize(recs, out_dir: str) -> str:
         r["wallclock_s_to_target"] = float(cum_lp[hit[0]]) if hit.size else None
         rows.append(r)
     lines = ["# Convergence vs wall-clock under the reference straggler model (MI355X, one GPU)", "",
+             "Rows named *_lazy run with `--drain lazy`: the master never waits for the straggler tail and a "
+             "worker still busy when the next beta is out skips that round; the others keep the reference's "
+             "behaviour (FRC / AGC drain every round, cyclic carries lag).  `loop wall-clock` is the real "
+             "time of the rounds, drain included.", "",
              f"Headline problem {naive['n_rows']} x {naive['n_cols']} fp64, W = 8, AGD, eta = 10, add_delay = 1 "
              f"(Exp(0.5) per worker per round, seed = round), {naive['rounds']} rounds.  Common target = naive's "
              f"final training loss + 1 % = {target:.5f}.  Generated by `tools/convergence_study.py`.", "",
