@@ -1,243 +1,272 @@
-// Worker gradient for sparse (one-hot CSR) design matrices — K4 of SURVEY §2.8.
+// Worker gradient for sparse (one-hot CSR) design matrices — K4 of SURVEY §2.8, deterministic.
 //
-// Reference: the real datasets (amazon / covtype / kc_house / dna) are scipy CSR
-// matrices whose values are all 1.0 (ref src/arrange_real_data.py one-hot encoders), and
-// workers evaluate X_current.dot(beta) and X_current.T.dot(r) with scipy
-// (ref src/replication.py:63-68, src/coded.py:43-46).
+// Reference: the real datasets (amazon / covtype / kc_house / dna) are scipy CSR matrices whose
+// values are all 1.0 (ref src/arrange_real_data.py one-hot encoders); every worker evaluates
+// X_current.dot(beta) and X_current.T.dot(r) over its (s+1) partitions with scipy
+// (ref src/replication.py:63-68, src/coded.py:43-46), so co-located replicas of a partition
+// repeat the same work.
 //
-// MI355X design, two launches per round for every logical worker on this GPU:
-//   pass 1 (row pass): a 16-lane group per row sums val * beta[col] over the row's
-//     nonzeros (beta stays in L2: <= 242k fp64), reduces with lane shuffles and writes
-//     the loss residual r[row] (label encoding coefficient per row).
-//   pass 2 (column pass): the transposed product uses a CSC twin stored as COO sorted
-//     by key = slot * ld + col.  Each lane takes one entry, the wave does a segmented
-//     Hillis-Steele scan keyed on the (sorted) column, and only the last lane of each
-//     run issues one float atomic add: one atomic per distinct column per wave
-//     instead of one per nonzero.
-// Pattern-only storage: vals == nullptr means every stored value is 1.0 (one-hot).
+// MI355X design.  Every DISTINCT local partition p is processed once with coefficient 1:
+//   pass 1 (rows): u_r = residual(x_r . beta, y_r, 1) for every distinct row r.  ELL layout
+//     (constant nnz per row, every one-hot dataset): idx column-major [m][rows], 16-bit offsets into
+//     feature k's category window [lo_k, lo_k + 2^16) when every window fits (half the bytes of
+//     int32 columns), one thread per row, beta gathered from L2; CSR: a 16-lane group per row.
+//   pass 2 (columns): g_p = X_p^T u_p from a CSC twin of each partition (row indices sorted by
+//     (column, row), 16-bit when the partition has <= 65536 rows), cut into 512-entry tiles, one
+//     wave per tile.  The wave finds every entry's column from the tile's column boundaries (an
+//     integer count in LDS, then a scan), gathers u, and runs a segmented scan keyed by the column:
+//     a sequential sum over each lane's 8 entries, then a Kogge-Stone scan of (restart, sum) over
+//     the 64 lanes.  A column inside one tile is written by the lane that holds its last entry; a
+//     column crossing tiles leaves its first part in tail[t1] and its parts in later tiles in
+//     head[t] (pass 3 adds them in tile order); empty columns are written 0 by pass 3.
+//   encode (encode.hip): G[message] = sum_p coef(message, p) g_p in a fixed order -- the label
+//     encoding is linear in the coefficient (residual(z, y, c) = c residual(z, y, 1)), so one
+//     read of a partition feeds every co-located replica with its own coefficient.
+// No float atomics anywhere: the gradient is bitwise reproducible from run to run (the old column
+// passes added into g with atomics: profiles/round3/suite_nt, round-3 verdict Weak #3).
 #include <algorithm>
+#include <climits>
 
 #include "common.h"
+#include "launchers.h"
 
 namespace eh {
 
-template <typename A, int LOSS, int G>
-__global__ void __launch_bounds__(256)
-csr_rowpass(const long long* __restrict__ row_ptr, const int* __restrict__ col_idx,
-            const A* __restrict__ vals,
-            const A* __restrict__ y, const A* __restrict__ coef, const A* __restrict__ beta,
-            A* __restrict__ rbuf, long long nrows, int ld, const int* __restrict__ gate) {
-  if (gate_closed(gate)) return;
-  const long long gid = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x);
-  const long long row = gid / G;
-  const int sub = threadIdx.x % G;
-  if (row >= nrows) return;  // whole group exits together (G divides 64)
-  const long long b = row_ptr[row], e = row_ptr[row + 1];
-  A z = A(0);
-  for (long long k = b + sub; k < e; k += G) {
-    const A v = vals ? vals[k] : A(1);
-    z = fma(v, beta[col_idx[k]], z);
-  }
-#pragma unroll
-  for (int off = G / 2; off > 0; off >>= 1) z += __shfl_xor(z, off, G);
-  if (sub == 0) rbuf[row] = residual<LOSS, A>(z, y[row], coef[row]);
-}
+namespace {
 
-template <typename A>
-__global__ void __launch_bounds__(256)
-coo_colpass(const long long* __restrict__ keys, const int* __restrict__ rows,
-            const A* __restrict__ vals, const A* __restrict__ rbuf, A* __restrict__ G,
-            long long nnz, const int* __restrict__ gate) {
-  if (gate_closed(gate)) return;
-  const long long e = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  const bool live = e < nnz;
-  long long key = live ? keys[e] : -1;
-  A v = live ? (vals ? vals[e] : A(1)) * rbuf[rows[e]] : A(0);
-  // Segmented inclusive scan over equal keys (keys are sorted, runs are contiguous).
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    const A vu = __shfl_up(v, off, kWave);
-    const long long ku = __shfl_up(key, off, kWave);
-    if (lane >= off && ku == key) v += vu;
-  }
-  const long long kn = __shfl_down(key, 1, kWave);
-  const bool last = (lane == kWave - 1) || (kn != key);
-  if (live && last) atomicAdd(G + key, v);
-}
+constexpr int kTileEntries = 512;  // one wave: 64 lanes x 8 entries
+constexpr int kSpanHead = 1, kSpanTail = 2;
 
-// ----- ELL path: constant nnz per row (every one-hot dataset of the reference) -----------
-//
-// idx is column-major [m][nrows]: idx[k][row] = k-th (sorted) column of `row`.  For one-hot
-// data the k-th nonzero of every row falls in original feature k's block of categories, so
-// a wave that handles 64 consecutive rows for one k gathers beta (row pass) or scatters
-// into g (column pass) inside one small window — L1-resident gathers and LDS-resident
-// histograms instead of whole-vector random access.
-//
-// Row pass: one thread per row, z = sum_k v * beta[idx[k][row]], r = loss residual.
-template <typename A, int LOSS, bool VALS>
-__global__ void __launch_bounds__(256)
-ell_rowpass(const int* __restrict__ idx, const A* __restrict__ vals, const A* __restrict__ y,
-            const A* __restrict__ coef, const A* __restrict__ beta, A* __restrict__ rbuf,
-            long long nrows, int m, A* __restrict__ G, long long gsize, const int* __restrict__ gate) {
+// ---- pass 1: rows -------------------------------------------------------------------------------
+template <typename A, int LOSS, bool IDX16, bool VALS>
+__global__ void __launch_bounds__(256) ell_rows(const SparseArgs a, const A* __restrict__ beta, const int* gate) {
   if (gate_closed(gate)) return;
   const long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
-  // the column pass accumulates into G: zero it here (stream order) instead of a memset launch
-  const long long nthreads = static_cast<long long>(gridDim.x) * blockDim.x;
-  for (long long i = row; i < gsize; i += nthreads) G[i] = A(0);
-  if (row >= nrows) return;
-  // four independent gather chains per thread: enough loads in flight to stream idx at HBM rate
-  A z[4] = {A(0), A(0), A(0), A(0)};
+  if (row >= a.nrows) return;
+  const long long n = a.nrows;
+  const A* __restrict__ vals = static_cast<const A*>(a.vals);
+  A z[4] = {A(0), A(0), A(0), A(0)};  // four independent gather chains
   int k = 0;
-  for (; k + 3 < m; k += 4) {
+  auto col = [&](int kk) -> int {
+    if constexpr (IDX16)
+      return a.lo[kk] + static_cast<int>(__builtin_nontemporal_load(static_cast<const unsigned short*>(a.ell_idx) +
+                                                                     static_cast<long long>(kk) * n + row));
+    else
+      return __builtin_nontemporal_load(static_cast<const int*>(a.ell_idx) + static_cast<long long>(kk) * n + row);
+  };
+  for (; k + 3 < a.m; k += 4) {
     int c[4];
     A v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      c[u] = __builtin_nontemporal_load(idx + static_cast<long long>(k + u) * nrows + row);
-      v[u] = VALS ? vals[static_cast<long long>(k + u) * nrows + row] : A(1);
+      c[u] = col(k + u);
+      v[u] = VALS ? vals[static_cast<long long>(k + u) * n + row] : A(1);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) z[u] = fma(v[u], beta[c[u]], z[u]);
   }
-  for (; k < m; ++k) {
-    const int c0 = idx[static_cast<long long>(k) * nrows + row];
-    const A v0 = VALS ? vals[static_cast<long long>(k) * nrows + row] : A(1);
-    z[k & 3] = fma(v0, beta[c0], z[k & 3]);
-  }
-  const A z0 = (z[0] + z[1]) + (z[2] + z[3]), z1 = A(0);
-  rbuf[row] = residual<LOSS, A>(z0 + z1, y[row], coef[row]);
+  for (; k < a.m; ++k) z[k & 3] = fma(VALS ? vals[static_cast<long long>(k) * n + row] : A(1), beta[col(k)], z[k & 3]);
+  const A zz = (z[0] + z[1]) + (z[2] + z[3]);
+  static_cast<A*>(a.u)[row] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[row], A(1));
 }
 
-struct EllChunk {
-  int row_begin;
-  int row_end;
-  int slot;
-  int pad;
-};
-
-constexpr int kSmallW = 8;  // features with at most this many categories accumulate in registers
-
-// Column pass: block (chunk of rows of one message, feature k).  Features whose column
-// window fits the LDS budget accumulate r * v into an LDS histogram of the window and
-// flush the touched bins with one global atomic each; wider windows add straight into g.
-template <typename A, bool VALS>
-__global__ void __launch_bounds__(256)
-ell_colpass(const int* __restrict__ idx, const A* __restrict__ vals, const A* __restrict__ rbuf,
-            const EllChunk* __restrict__ chunks, const int* __restrict__ lo, const int* __restrict__ width,
-            A* __restrict__ G, long long nrows, int ld, int lds_cap, const int* __restrict__ gate) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+template <typename A, int LOSS, int G>
+__global__ void __launch_bounds__(256) csr_rows(const SparseArgs a, const A* __restrict__ beta, const int* gate) {
   if (gate_closed(gate)) return;
-  A* hist = reinterpret_cast<A*>(smem_raw);
-  const EllChunk ch = chunks[blockIdx.x];
-  const int k = blockIdx.y;
-  const int lo_k = lo[k], w = width[k];
-  const int* __restrict__ ik = idx + static_cast<long long>(k) * nrows;
-  const A* __restrict__ vk = VALS ? vals + static_cast<long long>(k) * nrows : nullptr;
-  A* __restrict__ g = G + static_cast<long long>(ch.slot) * ld;
-  if (w <= kSmallW) {
-    // Few categories (the bias column, binary columns): every lane of a wave would hit the
-    // same one or two LDS bins, serialising the atomics 32-64 ways.  Each thread keeps one
-    // register accumulator per category instead (compare-select), then the block reduces
-    // them with wave shuffles and one LDS fold: no atomics until the w global adds.
-    A acc[kSmallW];
+  const long long gid = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const long long row = gid / G;
+  const int sub = threadIdx.x % G;
+  if (row >= a.nrows) return;  // whole group exits together (G divides 64)
+  const long long b = a.row_ptr[row], e = a.row_ptr[row + 1];
+  const A* __restrict__ vals = static_cast<const A*>(a.vals);
+  A z = A(0);
+  for (long long q = b + sub; q < e; q += G) z = fma(vals ? vals[q] : A(1), beta[a.col_idx[q]], z);
 #pragma unroll
-    for (int b = 0; b < kSmallW; ++b) acc[b] = A(0);
-    for (int row = ch.row_begin + threadIdx.x; row < ch.row_end; row += blockDim.x) {
-      const A v = VALS ? rbuf[row] * vk[row] : rbuf[row];
-      const int bin = ik[row] - lo_k;
+  for (int off = G / 2; off > 0; off >>= 1) z += __shfl_xor(z, off, G);
+  if (sub == 0) static_cast<A*>(a.u)[row] = residual<LOSS, A>(z, static_cast<const A*>(a.y)[row], A(1));
+}
+
+// ---- pass 2: CSC tiles, one wave per 512-entry tile ---------------------------------------------
+template <typename A, bool ROW16, bool VALS>
+__global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* gate) {
+  __shared__ int cnt[4][kTileEntries];
+  if (gate_closed(gate)) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t = blockIdx.x * 4 + w;
+  if (t >= a.ntiles) return;  // wave-uniform; only wave barriers below
+  const int4 td = a.tiles[t];
+  const int p = td.x, base = td.y, c0 = td.z, flags = td.w;
+  const int nnz_p = a.part_nnz[p];
+  const int n = min(kTileEntries, nnz_p - base);
+  const int* __restrict__ cp = a.col_ptr + static_cast<long long>(p) * (a.d + 1);
+  int* __restrict__ cw = cnt[w];
+  // 1. column boundaries inside the tile: cnt[q] = number of columns c > c0 starting at base + q
+  //    (empty columns stack on the next non-empty one's start); integer LDS adds, order-free
 #pragma unroll
-      for (int b = 0; b < kSmallW; ++b) acc[b] += bin == b ? v : A(0);
-    }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int i = 0; i < kTileEntries / 64; ++i) cw[i * 64 + lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  for (int c = c0 + 1 + lane;; c += 64) {
+    const bool in = c <= a.d && cp[min(c, a.d)] < base + n;
+    if (in) atomicAdd(&cw[cp[c] - base], 1);
+    if (__ballot(in) == 0) break;  // column starts are monotone: none further inside
+  }
+  __builtin_amdgcn_wave_barrier();
+  // 2. the column of each of this lane's 8 entries: c0 + inclusive prefix of cnt
+  int cl[8];
+  int run = 0;
 #pragma unroll
-    for (int b = 0; b < kSmallW; ++b) {
-      if (b >= w) break;  // w is uniform over the block
-      const A sb = wave_allreduce_sum(acc[b]);
-      if (lane == 0) hist[wid * kSmallW + b] = sb;
-    }
-    __syncthreads();
-    if (threadIdx.x < w) {
-      A sb = A(0);
-      for (int q = 0; q < nw; ++q) sb += hist[q * kSmallW + threadIdx.x];
-      if (sb != A(0)) atomicAdd(&g[lo_k + threadIdx.x], sb);
-    }
-  } else if (w <= lds_cap) {
-    for (int b = threadIdx.x; b < w; b += blockDim.x) hist[b] = A(0);
-    __syncthreads();
-    for (int row = ch.row_begin + threadIdx.x; row < ch.row_end; row += blockDim.x) {
-      const A v = VALS ? rbuf[row] * vk[row] : rbuf[row];
-      atomicAdd(&hist[ik[row] - lo_k], v);
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < w; b += blockDim.x) {
-      const A h = hist[b];
-      if (h != A(0)) atomicAdd(&g[lo_k + b], h);
+  for (int i = 0; i < 8; ++i) {
+    run += cw[8 * lane + i];
+    cl[i] = run;
+  }
+  int incl = run;  // wave inclusive scan of the lane totals
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
+  }
+  const int before = incl - run;
+  int key[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) key[i] = c0 + before + cl[i];
+  // 3. this lane's entries: rows (one 16- or 32-byte load), values, gathered residuals
+  const long long e0 = a.part_entry0[p] + base + 8 * lane;
+  const A* __restrict__ up = static_cast<const A*>(a.u) + a.part_row0[p];
+  A v[8];
+  int rows[8];
+  if constexpr (ROW16) {
+    const uint4 r4 = *reinterpret_cast<const uint4*>(static_cast<const unsigned short*>(a.crow) + e0);
+    const unsigned int rw[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      rows[2 * i] = static_cast<int>(rw[i] & 0xffffu);
+      rows[2 * i + 1] = static_cast<int>(rw[i] >> 16);
     }
   } else {
-    for (int row = ch.row_begin + threadIdx.x; row < ch.row_end; row += blockDim.x) {
-      const A v = VALS ? rbuf[row] * vk[row] : rbuf[row];
-      atomicAdd(&g[ik[row]], v);
+    const int4* r4 = reinterpret_cast<const int4*>(static_cast<const int*>(a.crow) + e0);
+    const int4 x = r4[0], y = r4[1];
+    rows[0] = x.x, rows[1] = x.y, rows[2] = x.z, rows[3] = x.w;
+    rows[4] = y.x, rows[5] = y.y, rows[6] = y.z, rows[7] = y.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bool ok = 8 * lane + i < n;
+    A x = ok ? up[rows[i]] : A(0);
+    if constexpr (VALS) x *= ok ? static_cast<const A*>(a.cvals)[e0 + i] : A(0);
+    v[i] = x;
+  }
+  // 4. segmented sums: sequential inside the lane, then over the lanes
+  A s[8];
+  s[0] = v[0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) s[i] = key[i] == key[i - 1] ? s[i - 1] + v[i] : v[i];
+  const int prev_last = __shfl_up(key[7], 1, 64);
+  // affine scan x_l = g_l * x_{l-1} + b_l: g_l = 1 iff the whole lane continues the previous lane's key
+  int g = (lane > 0 && key[0] == key[7] && prev_last == key[0]) ? 1 : 0;
+  A b = s[7];
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const A bp = __shfl_up(b, off, 64);
+    const int gp = __shfl_up(g, off, 64);
+    if (lane >= off) {
+      b = g ? b + bp : b;
+      g = g & gp;
     }
+  }
+  // carry into this lane's first run: the running sum of that key up to the previous lane's end
+  const A prev_run = __shfl_up(b, 1, 64);
+  const A carry = (lane > 0 && prev_last == key[0]) ? prev_run : A(0);
+  const int next_first = __shfl_down(key[0], 1, 64);
+  A* __restrict__ gout = static_cast<A*>(a.Gb) + static_cast<long long>(p) * a.ld;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int q = 8 * lane + i;
+    if (q >= n) break;
+    const int kn = i < 7 ? key[i + 1] : next_first;
+    if (q != n - 1 && kn == key[i]) continue;  // not a run end
+    const A val = key[i] == key[0] ? s[i] + carry : s[i];
+    const bool has_head = key[i] == c0 && (flags & kSpanHead);  // the run reaches back into earlier tiles
+    const bool has_tail = q == n - 1 && (flags & kSpanTail);    // the run goes on in later tiles
+    if (has_head) static_cast<A*>(a.head)[t] = val;
+    if (has_tail) static_cast<A*>(a.tail)[t] = val;
+    if (!has_head && !has_tail) gout[key[i]] = val;
   }
 }
 
-hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals, const void* y,
-                           const void* coef, const void* beta, void* rbuf, long long nrows, int m,
-                           const void* chunks, int nchunks, const int* lo, const int* width,
-                           int max_width, void* G, long long gsize, int ld, hipStream_t st, const int* gate) {
-  const size_t esz = dtype == 0 ? sizeof(double) : sizeof(float);
-  if (nrows == 0 || m == 0) return hipMemsetAsync(G, 0, gsize * esz, st);
-  constexpr int kLdsBytes = 64 * 1024;
-  const int cap = static_cast<int>(kLdsBytes / esz);
-  const size_t sh = static_cast<size_t>(std::max(std::min(max_width, cap), 4 * kSmallW)) * esz;
-  const dim3 block(256), grid1(static_cast<unsigned>((nrows + 255) / 256)), grid2(nchunks, m);
-  const EllChunk* C = static_cast<const EllChunk*>(chunks);
-#define EH_ELL(A, VALS)                                                                                  \
-  if (loss == kLogistic)                                                                                 \
-    hipLaunchKernelGGL((ell_rowpass<A, kLogistic, VALS>), grid1, block, 0, st, idx, (const A*)vals,      \
-                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m, (A*)G, gsize, gate);   \
-  else                                                                                                   \
-    hipLaunchKernelGGL((ell_rowpass<A, kLeastSquares, VALS>), grid1, block, 0, st, idx, (const A*)vals,  \
-                       (const A*)y, (const A*)coef, (const A*)beta, (A*)rbuf, nrows, m, (A*)G, gsize, gate);   \
-  hipLaunchKernelGGL((ell_colpass<A, VALS>), grid2, block, sh, st, idx, (const A*)vals, (const A*)rbuf, C, \
-                     lo, width, (A*)G, nrows, ld, cap, gate);
-  if (dtype == 0) {
-    if (vals) { EH_ELL(double, true) } else { EH_ELL(double, false) }
-  } else {
-    if (vals) { EH_ELL(float, true) } else { EH_ELL(float, false) }
+// ---- pass 3: columns crossing tiles (tail of the first tile + head of every later one, in order)
+// and the columns no entry of the partition touches
+template <typename A>
+__global__ void __launch_bounds__(256) csc_spans(const SparseArgs a, const int* gate) {
+  if (gate_closed(gate)) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < a.nspan) {
+    const int4 sp = a.span[i];  // (partition, column, t1, t2)
+    A s = static_cast<const A*>(a.tail)[sp.z];
+    for (int t = sp.z + 1; t <= sp.w; ++t) s += static_cast<const A*>(a.head)[t];
+    static_cast<A*>(a.Gb)[static_cast<long long>(sp.x) * a.ld + sp.y] = s;
+  } else if (i < a.nspan + a.nempty) {
+    const int2 e = a.empty[i - a.nspan];
+    static_cast<A*>(a.Gb)[static_cast<long long>(e.x) * a.ld + e.y] = A(0);
   }
-#undef EH_ELL
-  return hipGetLastError();
 }
 
-hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, const int* col_idx,
-                              const void* vals, const void* y, const void* coef,
-                              const void* beta, void* rbuf, long long nrows,
-                              const long long* keys, const int* rows, const void* cvals,
-                              long long nnz, void* G, long long gsize, int ld, hipStream_t st, const int* gate) {
-  constexpr int Gs = 16;
+}  // namespace
+
+hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const void* beta, hipStream_t st,
+                              const int* gate) {
+  if (a.nrows < 0 || a.ntiles < 0 || a.d <= 0 || a.ld < a.d || !a.Gb || !a.u) return hipErrorInvalidValue;
   const dim3 block(256);
-  const dim3 grid1(static_cast<unsigned>((nrows * Gs + 255) / 256));
-  const dim3 grid2(static_cast<unsigned>((nnz + 255) / 256));
-  const size_t esz = dtype == 0 ? sizeof(double) : sizeof(float);
-  hipError_t e = hipMemsetAsync(G, 0, gsize * esz, st);
-  if (e != hipSuccess) return e;
-  if (nrows == 0) return hipSuccess;
-  if (dtype == 0) {
-    if (loss == kLogistic)
-      hipLaunchKernelGGL((csr_rowpass<double, kLogistic, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const double*)vals, (const double*)y, (const double*)coef, (const double*)beta, (double*)rbuf, nrows, ld, gate);
-    else
-      hipLaunchKernelGGL((csr_rowpass<double, kLeastSquares, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const double*)vals, (const double*)y, (const double*)coef, (const double*)beta, (double*)rbuf, nrows, ld, gate);
-    if (nnz > 0)
-      hipLaunchKernelGGL((coo_colpass<double>), grid2, block, 0, st, keys, rows, (const double*)cvals, (const double*)rbuf, (double*)G, nnz, gate);
-  } else {
-    if (loss == kLogistic)
-      hipLaunchKernelGGL((csr_rowpass<float, kLogistic, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const float*)vals, (const float*)y, (const float*)coef, (const float*)beta, (float*)rbuf, nrows, ld, gate);
-    else
-      hipLaunchKernelGGL((csr_rowpass<float, kLeastSquares, Gs>), grid1, block, 0, st, row_ptr, col_idx, (const float*)vals, (const float*)y, (const float*)coef, (const float*)beta, (float*)rbuf, nrows, ld, gate);
-    if (nnz > 0)
-      hipLaunchKernelGGL((coo_colpass<float>), grid2, block, 0, st, keys, rows, (const float*)cvals, (const float*)rbuf, (float*)G, nnz, gate);
+  if (a.nrows > 0) {
+    if (a.ell) {
+      const dim3 grid(static_cast<unsigned>((a.nrows + 255) / 256));
+#define EH_ELL(A_, L_)                                                                                          \
+  if (a.idx16) {                                                                                                \
+    if (a.vals) hipLaunchKernelGGL((ell_rows<A_, L_, true, true>), grid, block, 0, st, a, (const A_*)beta, gate);  \
+    else hipLaunchKernelGGL((ell_rows<A_, L_, true, false>), grid, block, 0, st, a, (const A_*)beta, gate);       \
+  } else {                                                                                                      \
+    if (a.vals) hipLaunchKernelGGL((ell_rows<A_, L_, false, true>), grid, block, 0, st, a, (const A_*)beta, gate); \
+    else hipLaunchKernelGGL((ell_rows<A_, L_, false, false>), grid, block, 0, st, a, (const A_*)beta, gate);      \
+  }
+      if (dtype == 0) {
+        if (loss == kLogistic) { EH_ELL(double, kLogistic) } else { EH_ELL(double, kLeastSquares) }
+      } else {
+        if (loss == kLogistic) { EH_ELL(float, kLogistic) } else { EH_ELL(float, kLeastSquares) }
+      }
+#undef EH_ELL
+    } else {
+      constexpr int Gs = 16;
+      const dim3 grid(static_cast<unsigned>((a.nrows * Gs + 255) / 256));
+      if (dtype == 0) {
+        if (loss == kLogistic)
+          hipLaunchKernelGGL((csr_rows<double, kLogistic, Gs>), grid, block, 0, st, a, (const double*)beta, gate);
+        else
+          hipLaunchKernelGGL((csr_rows<double, kLeastSquares, Gs>), grid, block, 0, st, a, (const double*)beta, gate);
+      } else {
+        if (loss == kLogistic)
+          hipLaunchKernelGGL((csr_rows<float, kLogistic, Gs>), grid, block, 0, st, a, (const float*)beta, gate);
+        else
+          hipLaunchKernelGGL((csr_rows<float, kLeastSquares, Gs>), grid, block, 0, st, a, (const float*)beta, gate);
+      }
+    }
+  }
+  if (a.ntiles > 0) {
+    const dim3 grid(static_cast<unsigned>((a.ntiles + 3) / 4));
+#define EH_TILES(A_)                                                                                     \
+  if (a.row16) {                                                                                         \
+    if (a.cvals) hipLaunchKernelGGL((csc_tiles<A_, true, true>), grid, block, 0, st, a, gate);          \
+    else hipLaunchKernelGGL((csc_tiles<A_, true, false>), grid, block, 0, st, a, gate);                 \
+  } else {                                                                                               \
+    if (a.cvals) hipLaunchKernelGGL((csc_tiles<A_, false, true>), grid, block, 0, st, a, gate);         \
+    else hipLaunchKernelGGL((csc_tiles<A_, false, false>), grid, block, 0, st, a, gate);                \
+  }
+    if (dtype == 0) { EH_TILES(double) } else { EH_TILES(float) }
+#undef EH_TILES
+  }
+  const int nout = a.nspan + a.nempty;
+  if (nout > 0) {
+    const dim3 grid(static_cast<unsigned>((nout + 255) / 256));
+    if (dtype == 0) hipLaunchKernelGGL(csc_spans<double>, grid, block, 0, st, a, gate);
+    else hipLaunchKernelGGL(csc_spans<float>, grid, block, 0, st, a, gate);
   }
   return hipGetLastError();
 }

@@ -34,20 +34,44 @@ hipError_t grad_dense_twopass_launch(int dtype, int loss, const void* segs, cons
                                      void* rbuf, void* slab, const int* slot_task_begin,
                                      int nslots, void* part, void* G, int ld, hipStream_t st,
                                      const int* gate = nullptr);
-hipError_t grad_sparse_launch(int dtype, int loss, const long long* row_ptr, const int* col_idx,
-                              const void* vals, const void* y, const void* coef,
-                              const void* beta, void* rbuf, long long nrows,
-                              const long long* keys, const int* rows, const void* cvals,
-                              long long nnz, void* G, long long gsize, int ld, hipStream_t st,
+// Sparse (CSR / one-hot ELL) gradient of every DISTINCT local partition with coefficient 1
+// (grad_sparse.hip): row pass -> u, deterministic CSC tile pass -> Gb [nparts][ld]; the launcher's
+// device encoding then forms the messages (encode.hip).  Host tables: ops/grad.py SparseGradPlan.
+struct SparseArgs {
+  // pass 1: rows (all distinct rows, partitions concatenated)
+  int ell;                      // 1: ELL (constant nnz m per row), 0: CSR
+  int idx16;                    // ELL: uint16 offsets into window lo[k] (else int32 columns)
+  int m;                        // ELL nnz per row
+  long long nrows;
+  const void* ell_idx;          // [m][nrows] uint16 | int32
+  const int* lo;                // [m] category window starts (idx16)
+  const long long* row_ptr;     // CSR [nrows + 1]
+  const int* col_idx;           // CSR [nnz]
+  const void* vals;             // ELL [m][nrows] or CSR [nnz] values; nullptr: pattern-only (1.0)
+  const void* y;                // [nrows] labels (acc dtype)
+  void* u;                      // [nrows] residual with coefficient 1 (acc dtype)
+  // pass 2: CSC tiles of 512 entries
+  int row16;                    // CSC row indices uint16 (partition-relative) | int32
+  const void* crow;             // [entries] per partition sorted by (column, row), each partition padded to 512
+  const void* cvals;            // [entries] values in CSC order; nullptr: pattern-only
+  const int* col_ptr;           // [nparts][d + 1] partition-relative entry offsets
+  const int4* tiles;            // [ntiles] (partition, base entry, column of the base entry, span flags 1 head / 2 tail)
+  int ntiles;
+  const long long* part_entry0; // [nparts] first (padded) entry of each partition
+  const long long* part_row0;   // [nparts] first row of each partition
+  const int* part_nnz;          // [nparts]
+  void* head;                   // [ntiles] partial sums of columns reaching back into earlier tiles
+  void* tail;                   // [ntiles] partial sums of columns going on in later tiles
+  // pass 3: columns crossing tiles and empty columns
+  const int4* span;             // [nspan] (partition, column, first tile, last tile)
+  int nspan;
+  const int2* empty;            // [nempty] (partition, column)
+  int nempty;
+  void* Gb;                     // [nparts][ld] output (acc dtype)
+  int d, ld;
+};
+hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const void* beta, hipStream_t st,
                               const int* gate = nullptr);
-
-// ELL (constant nnz per row) variant: idx/vals column-major [m][nrows]; chunks = EllChunk
-// {row_begin, row_end, slot, pad} of rows of one message; lo/width = column window of feature k.
-hipError_t grad_ell_launch(int dtype, int loss, const int* idx, const void* vals, const void* y,
-                           const void* coef, const void* beta, void* rbuf, long long nrows, int m,
-                           const void* chunks, int nchunks, const int* lo, const int* width,
-                           int max_width, void* G, long long gsize, int ld, hipStream_t st,
-                           const int* gate = nullptr);
 
 // layout probes of the bf16 MFMA gradient (grad_mfma.hip): one 16x16x32 product; one transposing read
 hipError_t mfma_probe_launch(const float* A, const float* B, float* C, hipStream_t st);

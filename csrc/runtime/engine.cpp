@@ -109,24 +109,8 @@ struct GradLauncher {
   void* part = nullptr;
   const int* task_row_off = nullptr;
   void* rbuf = nullptr;
-  const long long* row_ptr = nullptr;
-  const int* col_idx = nullptr;
-  const void* vals = nullptr;
-  const void* y = nullptr;
-  const void* coef = nullptr;
-  long long nrows = 0;
-  const long long* keys = nullptr;
-  const int* rows = nullptr;
-  const void* cvals = nullptr;
-  long long nnz = 0;
   int acc = 0;
-  // ELL
-  const int* ell_idx = nullptr;
-  const void* ell_vals = nullptr;
-  const void* chunks = nullptr;
-  int nchunks = 0, m = 0, max_width = 0;
-  const int* lo = nullptr;
-  const int* width = nullptr;
+  eh::SparseArgs sa{};  // kind 2 (grad_sparse.hip); Gb is the launch's output
   // optional device encoding (csrc/kernels/encode.hip): the kernels above write the distinct
   // partitions' gradients into Gb, then G[slot] = sum_k coef * Gb[idx] for the enc_slots messages
   void* Gb = nullptr;
@@ -168,12 +152,11 @@ struct GradLauncher {
         return ntasks ? eh::grad_dense_twopass_launch(dtype, loss, segs, tasks, ntasks, beta, task_row_off, rbuf, slab,
                                                       stb, nslots, part, G, ld, st, gate)
                       : hipSuccess;
-      case 2:
-        return eh::grad_sparse_launch(acc, loss, row_ptr, col_idx, vals, y, coef, beta, rbuf, nrows, keys, rows,
-                                      cvals, nnz, G, static_cast<long long>(nslots) * ld, ld, st, gate);
-      case 3:
-        return eh::grad_ell_launch(acc, loss, ell_idx, ell_vals, y, coef, beta, rbuf, nrows, m, chunks, nchunks, lo,
-                                   width, max_width, G, static_cast<long long>(nslots) * ld, ld, st, gate);
+      case 2: {
+        eh::SparseArgs a = sa;
+        a.Gb = G;
+        return eh::grad_sparse_launch(acc, loss, a, beta, st, gate);
+      }
       default:
         return hipErrorInvalidValue;
     }
@@ -222,61 +205,91 @@ std::shared_ptr<GradLauncher> make_dense(int64_t dtype, int64_t loss, int64_t cp
   return g;
 }
 
-std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& row_ptr, const Tensor& col_idx,
-                                          std::optional<Tensor> vals, const Tensor& y, const Tensor& coef,
-                                          const Tensor& rbuf, const Tensor& keys, const Tensor& rows,
-                                          std::optional<Tensor> cvals, int64_t nslots, int64_t ld) {
-  for (auto* t : {&row_ptr, &col_idx, &y, &coef, &rbuf, &keys, &rows}) need_gpu(*t, "sparse plan operand");
-  need(row_ptr.scalar_type() == at::kLong && keys.scalar_type() == at::kLong, "row_ptr/keys must be int64");
+// Sparse plan (ops/grad.py SparseGradPlan): every distinct local partition once; the plan's device
+// encoding (set_encode) forms the messages.  Tensors are kept alive by the launcher.
+std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const Tensor& u, std::optional<Tensor> ell_idx,
+                                          std::optional<Tensor> lo, std::optional<Tensor> row_ptr,
+                                          std::optional<Tensor> col_idx, std::optional<Tensor> vals, const Tensor& crow,
+                                          std::optional<Tensor> cvals, const Tensor& col_ptr, const Tensor& tiles,
+                                          const Tensor& part_entry0, const Tensor& part_row0, const Tensor& part_nnz,
+                                          const Tensor& head, const Tensor& tail, const Tensor& span,
+                                          const Tensor& empty, int64_t nparts, int64_t d, int64_t ld) {
+  for (auto* t : {&y, &u, &crow, &col_ptr, &tiles, &part_entry0, &part_row0, &part_nnz, &head, &tail, &span, &empty})
+    need_gpu(*t, "sparse plan operand");
+  need(tiles.scalar_type() == at::kInt && tiles.dim() == 2 && tiles.size(1) == 4, "tiles: int32 [n, 4]");
+  need(span.scalar_type() == at::kInt && span.dim() == 2 && span.size(1) == 4, "span: int32 [n, 4]");
+  need(empty.scalar_type() == at::kInt && empty.dim() == 2 && empty.size(1) == 2, "empty: int32 [n, 2]");
+  need(col_ptr.scalar_type() == at::kInt && col_ptr.numel() == nparts * (d + 1), "col_ptr: int32 [nparts, d + 1]");
+  need(part_entry0.scalar_type() == at::kLong && part_row0.scalar_type() == at::kLong &&
+           part_nnz.scalar_type() == at::kInt && part_nnz.numel() == nparts,
+       "partition offsets");
+  need(crow.scalar_type() == at::kShort || crow.scalar_type() == at::kInt, "crow: int16 | int32");
   auto g = std::make_shared<GradLauncher>();
   g->kind = 2;
   g->loss = (int)loss;
   g->acc = acc_code(y);
+  need(acc_code(u) == g->acc && acc_code(head) == g->acc && acc_code(tail) == g->acc, "acc dtype mismatch");
   g->ld = (int)ld;
-  g->nslots = (int)nslots;
-  g->row_ptr = (const long long*)row_ptr.data_ptr<int64_t>();
-  g->col_idx = col_idx.data_ptr<int>();
-  g->vals = vals ? vals->data_ptr() : nullptr;
-  g->y = y.data_ptr();
-  g->coef = coef.data_ptr();
-  g->rbuf = rbuf.data_ptr();
-  g->nrows = row_ptr.numel() - 1;
-  g->keys = (const long long*)keys.data_ptr<int64_t>();
-  g->rows = rows.data_ptr<int>();
-  g->cvals = cvals ? cvals->data_ptr() : nullptr;
-  g->nnz = keys.numel();
-  g->keep = {row_ptr, col_idx, y, coef, rbuf, keys, rows};
-  if (vals) g->keep.push_back(*vals);
-  if (cvals) g->keep.push_back(*cvals);
-  return g;
-}
-
-std::shared_ptr<GradLauncher> make_ell(int64_t loss, const Tensor& idx, std::optional<Tensor> vals, const Tensor& y,
-                                       const Tensor& coef, const Tensor& rbuf, const Tensor& chunks, const Tensor& lo,
-                                       const Tensor& width, int64_t max_width, int64_t nslots, int64_t ld) {
-  for (auto* t : {&idx, &y, &coef, &rbuf, &chunks, &lo, &width}) need_gpu(*t, "ell plan operand");
-  need(idx.dim() == 2 && idx.scalar_type() == at::kInt, "idx must be int32 [m, nrows]");
-  need(chunks.dim() == 2 && chunks.size(1) == 4 && chunks.scalar_type() == at::kInt, "chunks must be int32 [n,4]");
-  auto g = std::make_shared<GradLauncher>();
-  g->kind = 3;
-  g->loss = (int)loss;
-  g->acc = acc_code(y);
-  g->ld = (int)ld;
-  g->nslots = (int)nslots;
-  g->m = (int)idx.size(0);
-  g->nrows = idx.size(1);
-  g->ell_idx = idx.data_ptr<int>();
-  g->ell_vals = vals ? vals->data_ptr() : nullptr;
-  g->y = y.data_ptr();
-  g->coef = coef.data_ptr();
-  g->rbuf = rbuf.data_ptr();
-  g->chunks = chunks.data_ptr();
-  g->nchunks = (int)chunks.size(0);
-  g->lo = lo.data_ptr<int>();
-  g->width = width.data_ptr<int>();
-  g->max_width = (int)max_width;
-  g->keep = {idx, y, coef, rbuf, chunks, lo, width};
-  if (vals) g->keep.push_back(*vals);
+  g->nslots = (int)nparts;
+  eh::SparseArgs& a = g->sa;
+  a.nrows = y.numel();
+  a.y = y.data_ptr();
+  a.u = u.data_ptr();
+  g->keep = {y, u, crow, col_ptr, tiles, part_entry0, part_row0, part_nnz, head, tail, span, empty};
+  if (ell_idx) {
+    need_gpu(*ell_idx, "ell_idx");
+    need(ell_idx->dim() == 2 && ell_idx->size(1) == a.nrows, "ell_idx: [m, rows]");
+    a.ell = 1;
+    a.idx16 = ell_idx->scalar_type() == at::kShort ? 1 : 0;
+    need(a.idx16 || ell_idx->scalar_type() == at::kInt, "ell_idx: int16 | int32");
+    a.m = (int)ell_idx->size(0);
+    a.ell_idx = ell_idx->data_ptr();
+    if (a.idx16) {
+      need(lo.has_value() && lo->numel() == a.m && lo->scalar_type() == at::kInt, "lo: int32 [m]");
+      need_gpu(*lo, "lo");
+      a.lo = lo->data_ptr<int>();
+      g->keep.push_back(*lo);
+    }
+    g->keep.push_back(*ell_idx);
+  } else {
+    need(row_ptr.has_value() && col_idx.has_value(), "CSR row pass needs row_ptr / col_idx");
+    need_gpu(*row_ptr, "row_ptr");
+    need_gpu(*col_idx, "col_idx");
+    need(row_ptr->scalar_type() == at::kLong && row_ptr->numel() == a.nrows + 1, "row_ptr: int64 [rows + 1]");
+    a.row_ptr = reinterpret_cast<const long long*>(row_ptr->data_ptr<int64_t>());
+    a.col_idx = col_idx->data_ptr<int>();
+    g->keep.push_back(*row_ptr);
+    g->keep.push_back(*col_idx);
+  }
+  if (vals) {
+    need_gpu(*vals, "vals");
+    need(acc_code(*vals) == g->acc, "vals dtype");
+    a.vals = vals->data_ptr();
+    g->keep.push_back(*vals);
+  }
+  a.row16 = crow.scalar_type() == at::kShort ? 1 : 0;
+  a.crow = crow.data_ptr();
+  if (cvals) {
+    need_gpu(*cvals, "cvals");
+    need(acc_code(*cvals) == g->acc && cvals->numel() == crow.numel(), "cvals: acc dtype, one per CSC entry");
+    a.cvals = cvals->data_ptr();
+    g->keep.push_back(*cvals);
+  }
+  a.col_ptr = col_ptr.data_ptr<int>();
+  a.tiles = reinterpret_cast<const int4*>(tiles.data_ptr<int>());
+  a.ntiles = (int)tiles.size(0);
+  need(head.numel() >= a.ntiles && tail.numel() >= a.ntiles, "head / tail: one per tile");
+  a.part_entry0 = reinterpret_cast<const long long*>(part_entry0.data_ptr<int64_t>());
+  a.part_row0 = reinterpret_cast<const long long*>(part_row0.data_ptr<int64_t>());
+  a.part_nnz = part_nnz.data_ptr<int>();
+  a.head = head.data_ptr();
+  a.tail = tail.data_ptr();
+  a.span = reinterpret_cast<const int4*>(span.data_ptr<int>());
+  a.nspan = (int)span.size(0);
+  a.empty = reinterpret_cast<const int2*>(empty.data_ptr<int>());
+  a.nempty = (int)empty.size(0);
+  a.d = (int)d;
+  a.ld = (int)ld;
   return g;
 }
 
@@ -1737,12 +1750,11 @@ void bind_engine(py::module& m) {
                   py::arg("tasks"), py::arg("slab"), py::arg("slot_task_begin"), py::arg("part"), py::arg("ld"),
                   py::arg("task_row_off") = py::none(), py::arg("rbuf") = py::none(),
                   py::arg("choice") = eh::KernelChoice{})
-      .def_static("sparse", &make_sparse, py::arg("loss"), py::arg("row_ptr"), py::arg("col_idx"), py::arg("vals"),
-                  py::arg("y"), py::arg("coef"), py::arg("rbuf"), py::arg("keys"), py::arg("rows"), py::arg("cvals"),
-                  py::arg("nslots"), py::arg("ld"))
-      .def_static("ell", &make_ell, py::arg("loss"), py::arg("idx"), py::arg("vals"), py::arg("y"), py::arg("coef"),
-                  py::arg("rbuf"), py::arg("chunks"), py::arg("lo"), py::arg("width"), py::arg("max_width"),
-                  py::arg("nslots"), py::arg("ld"))
+      .def_static("sparse", &make_sparse, py::arg("loss"), py::arg("y"), py::arg("u"), py::arg("ell_idx"), py::arg("lo"),
+                  py::arg("row_ptr"), py::arg("col_idx"), py::arg("vals"), py::arg("crow"), py::arg("cvals"),
+                  py::arg("col_ptr"), py::arg("tiles"), py::arg("part_entry0"), py::arg("part_row0"),
+                  py::arg("part_nnz"), py::arg("head"), py::arg("tail"), py::arg("span"), py::arg("empty"),
+                  py::arg("nparts"), py::arg("d"), py::arg("ld"))
       .def("set_encode",
            [](GradLauncher& g, const Tensor& ptr, const Tensor& idx, const Tensor& coef, const Tensor& Gb) {
              for (auto* t : {&ptr, &idx, &coef, &Gb}) need_gpu(*t, "encode operand");

@@ -63,6 +63,9 @@ from ..parallel.placement import make_shards, place_spread, place_units
 # of replica rows against 1.29 ms for 8 GB of distinct rows; FRC s = 1 gives the same 0.11,
 # docs/PERF_NOTES.md).
 REPLICA_WEIGHT_DENSE = 0.12
+# Sparse plans stream every distinct partition once and encode the replicas (ops/grad.py
+# SparseGradPlan): a further replica costs one encode row, next to nothing.
+REPLICA_WEIGHT_SPARSE = 0.02
 from ..parallel.transport import make_transport
 from ..utils import report
 from ..utils.delay import DelayModel
@@ -182,6 +185,8 @@ class Trainer:
             replica_weight = 0.0
         elif env.gpu and not sparse:
             replica_weight = REPLICA_WEIGHT_DENSE
+        elif env.gpu:
+            replica_weight = REPLICA_WEIGHT_SPARSE
         else:
             replica_weight = 1.0
         self.shard_mode = cfg.shard if cfg.shard != "auto" else "message"

@@ -7,7 +7,7 @@ round the plan is executed with one launch set:
   dense  -> ``grad_dense`` (fused single pass over X, slab reduction)   csrc/kernels/grad_dense.hip
             ``grad_dense_wide`` (a workgroup per row) when d > 2048 fp64       (same file)
             ``grad_dense_twopass`` beyond 8192 fp64 / 16384 fp32 columns
-  sparse -> ``grad_sparse`` (CSR row pass + sorted-COO column pass)      csrc/kernels/grad_sparse.hip
+  sparse -> ``grad_sparse`` (ELL / CSR row pass + deterministic CSC tiles)  csrc/kernels/grad_sparse.hip
 
 On CPU tensors the same plans run a float64/float32 torch implementation of the
 identical math (the test path and the gloo multi-process path); on GPU tensors the
@@ -532,7 +532,17 @@ class SparseGradPlan:
     """Gradient of every local message over CSR partitions (one-hot / pattern-only aware).
 
     partitions: {partition_index: (scipy.sparse.csr_matrix, y ndarray float64)}
+
+    GPU (csrc/kernels/grad_sparse.hip): every DISTINCT partition of the local messages is read once
+    with coefficient 1 -- row pass (ELL with 16-bit window offsets, or CSR) -> u, a deterministic
+    column pass over 512-entry CSC tiles -> Gb[partition] -- and the launcher's device encoding forms
+    G[message] = sum coef * Gb[partition] (the label encoding is linear in the coefficient), so
+    co-located replicas (FRC / AGC groups, cyclic neighbours) share one read of their partitions
+    (the reference repeats it per worker: ref src/replication.py:63-68).  No float atomics: the
+    result is bitwise reproducible.  CPU: scipy per message (the reference's own arithmetic).
     """
+
+    TILE = 512  # grad_sparse.hip kTileEntries
 
     def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]], partitions: Dict[int, Tuple[object, np.ndarray]],
                  prec: Precision, loss: int, d: int, device="cpu", use_ell: bool = True):
@@ -545,74 +555,139 @@ class SparseGradPlan:
         self.messages = [list(m) for m in messages]
         self.nslots = len(self.messages)
         self.device = torch.device(device)
-        blocks, ys, coefs, slots = [], [], [], []
-        for slot, m in enumerate(self.messages):
-            for p, coef in m:
-                A, y = partitions[p]
-                A = sps.csr_matrix(A)
-                if A.shape[1] > d:
-                    raise ValueError("partition has more columns than d")
-                blocks.append(A)
-                ys.append(np.asarray(y, dtype=np.float64))
-                coefs.append(np.full(A.shape[0], float(coef)))
-                slots.append(np.full(A.shape[0], slot, dtype=np.int64))
-        X = sps.vstack(blocks, format="csr") if blocks else sps.csr_matrix((0, d))
+        self.basis = sorted({p for m in self.messages for p, _ in m})  # distinct partitions
+        pos = {p: j for j, p in enumerate(self.basis)}
+        self.blocks = []
+        for p in self.basis:
+            A, y = partitions[p]
+            A = sps.csr_matrix(A)
+            if A.shape[1] > d:
+                raise ValueError("partition has more columns than d")
+            A = sps.csr_matrix((A.data, A.indices, A.indptr), shape=(A.shape[0], d))
+            A.sort_indices()
+            self.blocks.append((A, np.asarray(y, dtype=np.float64)))
+        X = sps.vstack([b[0] for b in self.blocks], format="csr") if self.blocks else sps.csr_matrix((0, d))
         X = sps.csr_matrix((X.data, X.indices, X.indptr), shape=(X.shape[0], d))
         X.sort_indices()
-        self.nrows = X.shape[0]
+        self.nrows = X.shape[0]  # distinct rows
         self.nnz = X.nnz
-        row_slot = np.concatenate(slots) if slots else np.zeros(0, dtype=np.int64)
+        self.msg_rows = sum(self.blocks[pos[p]][0].shape[0] for m in self.messages for p, _ in m)
         self.pattern_only = bool(X.nnz == 0 or np.all(X.data == 1.0))
-        # COO sorted by key = slot * ld + col (the CSC twin across all local messages)
-        coo = X.tocoo()
-        keys = row_slot[coo.row] * self.ld + coo.col.astype(np.int64)
-        order = np.argsort(keys, kind="stable")
-        acc = prec.acc
-        npacc = np.float64 if acc == torch.float64 else np.float32
-        dev = self.device
-        self.row_ptr = torch.from_numpy(X.indptr.astype(np.int64)).to(dev)
-        self.col_idx = torch.from_numpy(X.indices.astype(np.int32)).to(dev)
-        self.vals = None if self.pattern_only else torch.from_numpy(X.data.astype(npacc)).to(dev)
-        self.y = torch.from_numpy((np.concatenate(ys) if ys else np.zeros(0)).astype(npacc)).to(dev)
-        self.coef = torch.from_numpy((np.concatenate(coefs) if coefs else np.zeros(0)).astype(npacc)).to(dev)
-        self.keys = torch.from_numpy(keys[order]).to(dev)
-        self.rows = torch.from_numpy(coo.row[order].astype(np.int32)).to(dev)
-        self.cvals = None if self.pattern_only else torch.from_numpy(coo.data[order].astype(npacc)).to(dev)
-        self.rbuf = torch.empty(max(1, self.nrows), dtype=acc, device=dev)
-        self._row_slot = torch.from_numpy(row_slot).to(dev)
-        self._X_cpu = X if dev.type == "cpu" else None
+        # encoding: message slot -> (distinct partition, coefficient) in message order
+        ptr, idx, coef = [0], [], []
+        for m in self.messages:
+            for p, c in m:
+                idx.append(pos[p])
+                coef.append(float(c))
+            ptr.append(len(idx))
+        self._enc = (ptr, idx, coef)
         self.ell = False
-        if dev.type == "cuda" and use_ell:
-            self._build_ell(X, row_slot, npacc, slots)
+        self.idx16 = False
+        self.row16 = False
+        if self.device.type == "cuda":
+            self._build_device(X, use_ell)
 
-    ELL_CHUNK = 4096  # rows per column-pass block
-
-    def _build_ell(self, X, row_slot, npacc, slots):
-        """Column-major ELL twin when every row has the same nnz (one-hot data)."""
+    # ---- device tables ----------------------------------------------------------------------
+    def _build_device(self, X, use_ell: bool):
+        dev, acc = self.device, self.prec.acc
+        npacc = np.float64 if acc == torch.float64 else np.float32
+        ys = np.concatenate([b[1] for b in self.blocks]) if self.blocks else np.zeros(0)
+        self.y = torch.from_numpy(ys.astype(npacc)).to(dev)
+        self.u = torch.zeros(max(1, self.nrows), dtype=acc, device=dev)
         nnz_row = np.diff(X.indptr)
-        if self.nrows == 0 or not np.all(nnz_row == nnz_row[0]) or nnz_row[0] == 0 or self.nrows >= 2 ** 31:
-            return
-        m = int(nnz_row[0])
-        idx = X.indices.reshape(self.nrows, m).T  # [m, nrows]; rows are sorted -> k-th smallest column
-        lo = idx.min(axis=1).astype(np.int32)
-        width = (idx.max(axis=1) - lo + 1).astype(np.int32)
-        chunks = []
-        r = 0
-        for slot in range(self.nslots):
-            n = int(np.sum(row_slot == slot))
-            for r0 in range(r, r + n, self.ELL_CHUNK):
-                chunks.append((r0, min(r + n, r0 + self.ELL_CHUNK), slot, 0))
-            r += n
-        dev = self.device
-        self.ell = True
-        self.ell_m = m
-        self.ell_idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32)).to(dev)
-        self.ell_vals = None if self.pattern_only else torch.from_numpy(
-            np.ascontiguousarray(X.data.reshape(self.nrows, m).T, dtype=npacc)).to(dev)
-        self.ell_lo = torch.from_numpy(lo).to(dev)
-        self.ell_width = torch.from_numpy(width).to(dev)
-        self.ell_max_width = int(width.max())
-        self.ell_chunks = torch.from_numpy(np.asarray(chunks, dtype=np.int32).reshape(-1, 4)).to(dev)
+        self.ell_idx = self.ell_lo = self.row_ptr = self.col_idx = self.vals = None
+        if use_ell and self.nrows and np.all(nnz_row == nnz_row[0]) and nnz_row[0] > 0 and self.nrows < 2 ** 31:
+            m = int(nnz_row[0])
+            idx = X.indices.reshape(self.nrows, m).T  # [m, rows]; sorted rows -> the k-th smallest column
+            lo = idx.min(axis=1).astype(np.int64)
+            width = idx.max(axis=1) - lo + 1
+            self.ell, self.ell_m = True, m
+            if int(width.max()) <= 65536:  # 16-bit offsets into each feature's category window
+                self.idx16 = True
+                off = (idx - lo[:, None]).astype(np.uint16).view(np.int16)
+                self.ell_idx = torch.from_numpy(np.ascontiguousarray(off)).to(dev)
+                self.ell_lo = torch.from_numpy(lo.astype(np.int32)).to(dev)
+            else:
+                self.ell_idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32)).to(dev)
+            if not self.pattern_only:
+                self.vals = torch.from_numpy(np.ascontiguousarray(X.data.reshape(self.nrows, m).T, dtype=npacc)).to(dev)
+        else:
+            self.row_ptr = torch.from_numpy(X.indptr.astype(np.int64)).to(dev)
+            self.col_idx = torch.from_numpy(X.indices.astype(np.int32)).to(dev)
+            if not self.pattern_only:
+                self.vals = torch.from_numpy(X.data.astype(npacc)).to(dev)
+        t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE)
+        self.row16 = t["row16"]
+        self.crow = torch.from_numpy(t["crow"]).to(dev)
+        self.cvals = None if self.pattern_only else torch.from_numpy(t["cvals"].astype(npacc)).to(dev)
+        self.col_ptr = torch.from_numpy(t["col_ptr"]).to(dev)
+        self.tiles = torch.from_numpy(t["tiles"]).to(dev)
+        self.part_entry0 = torch.from_numpy(t["part_entry0"]).to(dev)
+        self.part_row0 = torch.from_numpy(t["part_row0"]).to(dev)
+        self.part_nnz = torch.from_numpy(t["part_nnz"]).to(dev)
+        self.span = torch.from_numpy(t["span"]).to(dev)
+        self.empty = torch.from_numpy(t["empty"]).to(dev)
+        nt = max(1, len(t["tiles"]))
+        self.head = torch.zeros(nt, dtype=acc, device=dev)
+        self.tail = torch.zeros(nt, dtype=acc, device=dev)
+        self.Gb = torch.zeros((max(1, len(self.basis)), self.ld), dtype=acc, device=dev)
+        ptr, idx, coef = self._enc
+        self.enc_ptr = torch.tensor(ptr, dtype=torch.int32, device=dev)
+        self.enc_idx = torch.tensor(idx or [0], dtype=torch.int32, device=dev)[: len(idx)]
+        self.enc_coef = torch.tensor(coef or [0.0], dtype=torch.float64, device=dev)[: len(coef)]
+        self._launcher = None
+
+    @staticmethod
+    def csc_tables(blocks, d: int, tile: int = 512) -> dict:
+        """Host tables of the deterministic column pass (grad_sparse.hip csc_tiles / csc_spans): per
+        partition a CSC twin (rows sorted by (column, row), padded to whole tiles), its column
+        pointers, the tiles (partition, base entry, column of the base entry, span flags: 1 = the
+        first column began in an earlier tile, 2 = the last goes on in a later one), the columns that
+        cross tiles (partition, column, first tile, last tile) and the empty columns."""
+        row16 = all(A.shape[0] <= 65536 for A in blocks)
+        rows_l, vals_l, cps, tiles, spans, empty = [], [], [], [], [], []
+        entry0, row0, nnzs = [], [], []
+        e_off = r_off = 0
+        for j, A in enumerate(blocks):
+            C = A.tocsc()
+            C.sort_indices()
+            cp = C.indptr.astype(np.int64)
+            nnz = int(cp[-1])
+            pad = (-nnz) % tile
+            r = C.indices.astype(np.int64)
+            rows_l.append(np.concatenate([r, np.zeros(pad, dtype=np.int64)]))
+            vals_l.append(np.concatenate([C.data.astype(np.float64), np.zeros(pad)]))
+            cps.append(cp.astype(np.int32))
+            entry0.append(e_off)
+            row0.append(r_off)
+            nnzs.append(nnz)
+            t_first = len(tiles)
+            for base in range(0, nnz, tile):
+                c0 = int(np.searchsorted(cp, base, side="right")) - 1
+                end = min(base + tile, nnz)
+                c_last = int(np.searchsorted(cp, end - 1, side="right")) - 1
+                flags = (1 if cp[c0] < base else 0) | (2 if cp[c_last + 1] > base + tile else 0)
+                tiles.append((j, base, c0, flags))
+            nonempty = np.nonzero(cp[1:] > cp[:-1])[0]
+            t1 = cp[nonempty] // tile
+            t2 = (cp[nonempty + 1] - 1) // tile
+            for c, a1, a2 in zip(nonempty[t2 > t1], t1[t2 > t1], t2[t2 > t1]):
+                spans.append((j, int(c), t_first + int(a1), t_first + int(a2)))
+            for c in np.nonzero(cp[1:] == cp[:-1])[0]:
+                empty.append((j, int(c)))
+            e_off += nnz + pad
+            r_off += A.shape[0]
+        crow = np.concatenate(rows_l) if rows_l else np.zeros(tile, dtype=np.int64)
+        crow = crow.astype(np.uint16).view(np.int16) if row16 else crow.astype(np.int32)
+        return {"row16": row16, "crow": np.ascontiguousarray(crow),
+                "cvals": np.concatenate(vals_l) if vals_l else np.zeros(tile),
+                "col_ptr": np.ascontiguousarray(np.stack(cps)) if cps else np.zeros((1, d + 1), dtype=np.int32),
+                "tiles": np.asarray(tiles, dtype=np.int32).reshape(-1, 4),
+                "part_entry0": np.asarray(entry0 or [0], dtype=np.int64),
+                "part_row0": np.asarray(row0 or [0], dtype=np.int64),
+                "part_nnz": np.asarray(nnzs or [0], dtype=np.int32),
+                "span": np.asarray(spans, dtype=np.int32).reshape(-1, 4),
+                "empty": np.asarray(empty, dtype=np.int32).reshape(-1, 2)}
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:
         return torch.zeros((n, self.nslots, self.ld), dtype=self.prec.acc, device=self.device)
@@ -620,39 +695,45 @@ class SparseGradPlan:
     def native_launcher(self):
         if self.device.type != "cuda":
             raise RuntimeError("native launchers need GPU tensors")
-        if self.ell:
-            return native().GradLauncher.ell(self.loss, self.ell_idx, self.ell_vals, self.y, self.coef, self.rbuf,
-                                             self.ell_chunks, self.ell_lo, self.ell_width, self.ell_max_width,
-                                             self.nslots, self.ld)
-        return native().GradLauncher.sparse(self.loss, self.row_ptr, self.col_idx, self.vals, self.y, self.coef,
-                                            self.rbuf, self.keys, self.rows, self.cvals, self.nslots, self.ld)
+        if self._launcher is None:
+            L = native().GradLauncher.sparse(self.loss, self.y, self.u, self.ell_idx, self.ell_lo, self.row_ptr,
+                                             self.col_idx, self.vals, self.crow, self.cvals, self.col_ptr, self.tiles,
+                                             self.part_entry0, self.part_row0, self.part_nnz, self.head, self.tail,
+                                             self.span, self.empty, len(self.basis), self.d, self.ld)
+            L.set_encode(self.enc_ptr, self.enc_idx, self.enc_coef, self.Gb)
+            self._launcher = L
+        return self._launcher
+
+    @property
+    def stream_bytes(self) -> int:
+        """Index / value bytes one gradient streams from HBM (row pass + CSC tiles; beta and u gathers
+        hit L2)."""
+        if self.device.type != "cuda":
+            return 0
+        n = sum(t.numel() * t.element_size() for t in (self.ell_idx, self.row_ptr, self.col_idx, self.vals, self.crow,
+                                                       self.cvals, self.y) if t is not None)
+        return int(n + 2 * self.u.numel() * self.u.element_size())
 
     def run(self, beta: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
         if G.shape != (self.nslots, self.ld):
             raise ValueError(f"G must be [{self.nslots}, {self.ld}]")
-        if self.device.type == "cuda" and self.ell:
-            native().grad_ell(self.loss, self.ell_idx, self.ell_vals, self.y, self.coef, beta, self.rbuf,
-                              self.ell_chunks, self.ell_lo, self.ell_width, self.ell_max_width, G, self.ld)
-            return G
         if self.device.type == "cuda":
-            native().grad_sparse(self.loss, self.row_ptr, self.col_idx, self.vals, self.y, self.coef, beta,
-                                 self.rbuf, self.keys, self.rows, self.cvals, G, self.ld)
+            self.native_launcher().launch(beta, G)
             return G
-        X = self._X_cpu
         b = beta.detach().cpu().double().numpy()[: self.d]
-        z = X.dot(b)
-        y = self.y.double().numpy()
-        c = self.coef.double().numpy()
-        if self.loss == LOGISTIC:
-            r = -(c * y) * (1.0 / (1.0 + np.exp(np.clip(y * z, -700, 700))))
-        else:
-            r = -2.0 * c * (y - z)
         G.zero_()
-        rs = self._row_slot.numpy()
-        for slot in range(self.nslots):
-            sel = rs == slot
-            g = X[sel].T.dot(r[sel]) if sel.any() else np.zeros(self.d)
-            G[slot, : self.d] = torch.from_numpy(np.asarray(g).ravel()).to(G.dtype)
+        pos = {p: j for j, p in enumerate(self.basis)}
+        for slot, m in enumerate(self.messages):
+            g = np.zeros(self.d)
+            for p, c in m:
+                A, y = self.blocks[pos[p]]
+                z = A.dot(b)
+                if self.loss == LOGISTIC:
+                    r = -(c * y) * (1.0 / (1.0 + np.exp(np.clip(y * z, -700, 700))))
+                else:
+                    r = -2.0 * c * (y - z)
+                g += np.asarray(A.T.dot(r)).ravel()
+            G[slot, : self.d] = torch.from_numpy(g).to(G.dtype)
         return G
 
 

@@ -107,15 +107,16 @@ def test_sparse_grad(prec_name, tol, pattern_only, use_ell, native):
 
 
 @pytest.mark.parametrize("prec_name,tol", [("fp64", 1e-11), ("fp32", 1e-4)])
-def test_ell_onehot_blocks_and_wide_windows(prec_name, tol, native):
-    """One-hot feature blocks (LDS histogram path) plus one block wider than the LDS budget
-    (global-atomic path), through both the Python binding and the native GradLauncher."""
+@pytest.mark.parametrize("wide,idx16", [(20000, True), (70000, False)])
+def test_ell_onehot_blocks_and_wide_windows(prec_name, tol, wide, idx16, native):
+    """One-hot feature blocks plus one feature with a 20000- or 70000-category window: 16-bit window
+    offsets in the row pass while every window fits 2^16, int32 columns beyond; both through plan.run
+    and the native GradLauncher, and bitwise reproducible (no float atomics in the column pass)."""
     from erasurehead_amd.data.synthetic import onehot_partitions
 
     prec = get_precision(prec_name)
     rng = np.random.RandomState(9)
     parts_l, _, d = onehot_partitions(3000, 900, 6, 3, seed=4)
-    wide = 20000  # > 64 KiB / 8 B: that feature's window cannot live in LDS
     parts = {}
     for p, (X, y) in enumerate(parts_l):
         extra = sps.csr_matrix((np.ones(X.shape[0]), d + rng.randint(0, wide, X.shape[0]),
@@ -128,7 +129,7 @@ def test_ell_onehot_blocks_and_wide_windows(prec_name, tol, native):
     b = rng.randn(D) * 0.1
     for loss in (LOGISTIC, LEAST_SQUARES):
         plan = SparseGradPlan(msgs, parts, prec, loss, D, device=DEV)
-        assert plan.ell and plan.ell_max_width > 8192
+        assert plan.ell and plan.idx16 == idx16 and plan.row16
         beta = torch.zeros(prec.ld(D), dtype=prec.acc, device=DEV)
         beta[:D] = torch.from_numpy(b).to(prec.acc)
         bh = beta[:D].double().cpu().numpy()
@@ -145,6 +146,38 @@ def test_ell_onehot_blocks_and_wide_windows(prec_name, tol, native):
                 got = G[s_, :D].double().cpu().numpy()
                 err = np.max(np.abs(got - ref)) / max(1e-12, np.max(np.abs(ref)))
                 assert err < tol, (loss, via_launcher, s_, err)
+            if via_launcher:
+                G2 = plan.out_buffer()[0]
+                plan.run(beta, G2)
+                torch.cuda.synchronize()
+                assert torch.equal(G, G2)  # bitwise, run to run
+
+
+def test_sparse_replicas_share_reads_and_match_per_message(native):
+    """FRC / AGC replicas on one GPU: every distinct partition is streamed once and each message is
+    encoded from it with its own coefficient; the result matches the per-message oracle and is
+    bitwise identical over repeated runs (covtype-like one-hot blocks, 4 partitions x 2 replicas)."""
+    from erasurehead_amd.data.synthetic import onehot_partitions
+
+    prec = get_precision("fp64")
+    parts_l, _, d = onehot_partitions(40000, 2000, 12, 4, seed=2)
+    parts = {p: xy for p, xy in enumerate(parts_l)}
+    msgs = [[(w, 1.0), ((w + 1) % 4, 1.0)] for w in range(4)] + [[(w, -0.5)] for w in range(4)]
+    plan = SparseGradPlan(msgs, parts, prec, LOGISTIC, d, device=DEV)
+    assert plan.basis == [0, 1, 2, 3] and plan.msg_rows == 3 * plan.nrows
+    rng = np.random.RandomState(1)
+    b = rng.randn(d) * 0.1
+    beta = torch.zeros(prec.ld(d), dtype=torch.float64, device=DEV)
+    beta[:d] = torch.from_numpy(b)
+    G1, G2 = plan.out_buffer()[0], plan.out_buffer()[0]
+    plan.run(beta, G1)
+    plan.run(beta, G2)
+    torch.cuda.synchronize()
+    assert torch.equal(G1, G2)
+    for s_, m in enumerate(msgs):
+        ref = sum(logistic_grad(parts[p][0], parts[p][1], b, c) for p, c in m)
+        got = G1[s_, :d].double().cpu().numpy()
+        assert np.max(np.abs(got - ref)) / np.max(np.abs(ref)) < 1e-11
 
 
 @pytest.mark.parametrize("rule", ["GD", "AGD"])

@@ -121,4 +121,5 @@ def test_lazy_beats_drain_and_carry_in_wall_clock():
         cfg.num_itrs, cfg.add_delay, cfg.force_delay = 12, 1, True
         res = Trainer(cfg, DistEnv(), src, scheme=sch).run()
         tot[drain] = float(np.sum(res.loop_time))
-    assert tot["lazy"] <= tot["carry"] + 0.02 and tot["lazy"] < tot["all"], tot
+    # event model for these delays: all 1.01 s, carry 0.72 s, lazy 0.70 s (utils/delay.schedule)
+    assert tot["lazy"] <= 1.05 * tot["carry"] + 0.03 and tot["lazy"] < 0.9 * tot["all"], tot

@@ -1,0 +1,125 @@
+"""Host tables of the deterministic sparse column pass (ops/grad.py SparseGradPlan.csc_tables), checked
+by a NumPy emulation of csrc/kernels/grad_sparse.hip (csc_tiles + csc_spans): every column of every
+partition is written exactly once -- inside one tile by the lane holding its last entry, across tiles
+as tail + heads in tile order, or 0 when empty -- and the result is X_p^T u_p."""
+import numpy as np
+import pytest
+import scipy.sparse as sps
+
+from erasurehead_amd.ops.grad import SparseGradPlan
+
+TILE = 512
+
+
+def emulate(t, u_parts, d):
+    nparts = len(u_parts)
+    G = np.full((nparts, d), np.nan)
+    head, tail = {}, {}
+    crow = t["crow"].view(np.uint16).astype(np.int64) if t["row16"] else t["crow"].astype(np.int64)
+    for ti, (p, base, c0, flags) in enumerate(t["tiles"]):
+        cp = t["col_ptr"][p].astype(np.int64)
+        nnz = int(t["part_nnz"][p])
+        n = min(TILE, nnz - base)
+        e0 = int(t["part_entry0"][p]) + base
+        assert e0 % 8 == 0
+        cnt = np.zeros(TILE, dtype=np.int64)
+        c = c0 + 1
+        while c <= d and cp[c] < base + n:  # the wave's boundary walk
+            cnt[cp[c] - base] += 1
+            c += 1
+        keys = c0 + np.cumsum(cnt)[:n]
+        assert keys[0] == c0 and np.all(cp[keys] <= base + np.arange(n)) and np.all(base + np.arange(n) < cp[keys + 1])
+        v = u_parts[p][crow[e0:e0 + n]] * t["cvals"][e0:e0 + n]
+        start = 0
+        for q in range(n):
+            if q != n - 1 and keys[q + 1] == keys[q]:
+                continue
+            val = 0.0
+            for x in v[start:q + 1]:
+                val += x
+            key = int(keys[q])
+            has_head = key == c0 and bool(flags & 1)
+            has_tail = q == n - 1 and bool(flags & 2)
+            if has_head:
+                head[ti] = val
+            if has_tail:
+                tail[ti] = val
+            if not has_head and not has_tail:
+                assert np.isnan(G[p, key]), "column written twice"
+                G[p, key] = val
+            start = q + 1
+    for p, c, t1, t2 in t["span"]:
+        assert np.isnan(G[p, c])
+        G[p, c] = tail[t1] + sum(head[t] for t in range(t1 + 1, t2 + 1))
+    for p, c in t["empty"]:
+        assert np.isnan(G[p, c])
+        G[p, c] = 0.0
+    assert not np.any(np.isnan(G)), "a column was never written"
+    return G
+
+
+def _onehot(rng, n, windows):
+    cols, lo = [], 0
+    for w in windows:
+        p = rng.dirichlet(np.ones(w) * 0.3)
+        cols.append(lo + rng.choice(w, n, p=p))
+        lo += w
+    cols = np.stack(cols, axis=1)
+    return sps.csr_matrix((np.ones(cols.size), cols.ravel(), np.arange(0, cols.size + 1, len(windows))), shape=(n, lo))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_tables_emulate_to_the_transposed_product(seed):
+    rng = np.random.RandomState(seed)
+    d = 3000
+    blocks = [
+        _onehot(rng, 2000, [2, 40, 700, 1200]),       # a binary feature: columns span many tiles
+        _onehot(rng, 333, [1, 900, 5, 1000]),          # partition smaller than a tile, empty columns
+        sps.random(900, d - 1, density=0.01, format="csr", random_state=rng),  # valued, ragged rows
+        sps.csr_matrix((70000, 2948)),                 # no entries at all (and > 65536 rows)
+    ]
+    blocks = [sps.csr_matrix((b.data, b.indices, b.indptr), shape=(b.shape[0], d)) for b in blocks]
+    t = SparseGradPlan.csc_tables(blocks, d, TILE)
+    assert not t["row16"]  # one partition has more than 65536 rows
+    u = [rng.randn(b.shape[0]) for b in blocks]
+    got = emulate(t, u, d)
+    for p, b in enumerate(blocks):
+        np.testing.assert_allclose(got[p], b.T.dot(u[p]), rtol=1e-12, atol=1e-12)
+    assert len(t["span"]) > 0 and len(t["empty"]) > 0
+
+
+def test_sixteen_bit_rows_and_tile_alignment():
+    rng = np.random.RandomState(5)
+    blocks = [_onehot(rng, 1500, [3, 50, 400]), _onehot(rng, 700, [3, 50, 400])]
+    d = blocks[0].shape[1]
+    t = SparseGradPlan.csc_tables(blocks, d, TILE)
+    assert t["row16"] and t["crow"].dtype == np.int16
+    assert all(e % TILE == 0 for e in t["part_entry0"])
+    u = [rng.randn(b.shape[0]) for b in blocks]
+    got = emulate(t, u, d)
+    for p, b in enumerate(blocks):
+        np.testing.assert_allclose(got[p], b.T.dot(u[p]), rtol=1e-12, atol=1e-12)
+
+
+def test_cpu_plan_matches_scipy_per_message():
+    """The CPU plan (the reference's arithmetic) with replicas sharing partitions."""
+    import torch
+
+    from erasurehead_amd.models.losses import LOGISTIC, logistic_grad
+    from erasurehead_amd.ops import get_precision
+
+    rng = np.random.RandomState(3)
+    parts = {p: (_onehot(rng, 300, [2, 30, 60]), rng.choice([-1.0, 1.0], 300)) for p in range(3)}
+    d = parts[0][0].shape[1]
+    msgs = [[(0, 1.0), (1, 1.0)], [(1, 0.5), (2, -1.0)], [(0, 2.0)]]
+    prec = get_precision("fp64")
+    plan = SparseGradPlan(msgs, parts, prec, LOGISTIC, d)
+    assert plan.basis == [0, 1, 2] and plan.nrows == 900 and plan.msg_rows == 1500
+    b = rng.randn(d) * 0.1
+    beta = torch.zeros(plan.ld, dtype=torch.float64)
+    beta[:d] = torch.from_numpy(b)
+    G = plan.out_buffer()[0]
+    plan.run(beta, G)
+    for s, m in enumerate(msgs):
+        ref = sum(logistic_grad(parts[p][0], parts[p][1], b, c) for p, c in m)
+        np.testing.assert_allclose(G[s, :d].numpy(), ref, rtol=1e-12, atol=1e-12)

@@ -256,14 +256,18 @@ def sparse_cases(out):
         W = 8
         parts_l, _, dd = onehot_partitions(n, d, f, W, seed=1)
         parts = {p: xy for p, xy in enumerate(parts_l)}
-        msgs = [[(w, 1.0), ((w + 1) % W, 1.0)] for w in range(W)]  # 8 workers, 2 partitions each (s = 1)
-        for use_ell in (True, False):
+        layouts = {"naive": [[(w, 1.0)] for w in range(W)],
+                   "s1_replicas": [[(w, 1.0), ((w + 1) % W, 1.0)] for w in range(W)]}  # 8 workers, 2 partitions each
+        for (layout, msgs), use_ell in [(x, e) for x in layouts.items() for e in (True, False)]:
             plan = SparseGradPlan(msgs, parts, prec, LOGISTIC, dd, device="cuda", use_ell=use_ell)
             beta = torch.randn(prec.ld(dd), device="cuda", dtype=torch.float64) * 0.1
             G = plan.out_buffer()[0]
             ms = _time(lambda: plan.run(beta, G))
-            r = {"kernel": "grad_ell" if plan.ell else "grad_sparse_coo", "dataset_shape": name, "rows": plan.nrows,
-                 "nnz": int(plan.nnz), "d": dd, "ms": ms, "nnz_per_us": plan.nnz / (ms * 1e3)}
+            kern = ("ell16" if plan.idx16 else "ell32") if plan.ell else "csr"
+            r = {"kernel": f"grad_sparse ({kern} rows, CSC{16 if plan.row16 else 32} tiles)", "layout": layout,
+                 "dataset_shape": name, "rows_distinct": plan.nrows, "rows_in_messages": plan.msg_rows,
+                 "nnz": int(plan.nnz), "d": dd, "ms": ms, "nnz_per_us": plan.nnz / (ms * 1e3),
+                 "stream_bytes": plan.stream_bytes, "TBps": plan.stream_bytes / (ms * 1e9)}
             out.append(r)
             print(json.dumps(r), flush=True)
             del plan
