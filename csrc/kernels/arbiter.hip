@@ -412,14 +412,12 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
     for (int t = tid; t < a.ntarget; t += blockDim.x)
       reinterpret_cast<MsgTag*>(reinterpret_cast<char*>(a.targets[2 * t]) + a.inbox_tag_off)[i + 1] =
           MsgTag{static_cast<unsigned int>(i + 2), 0u, s_bsum};
-  __threadfence_system();
-  __syncthreads();
+  block_release_system();  // one write-back for every inbox row and tag (common.h)
   if (tid == 0) {
     if (i + 1 < a.R) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // see transport.hip: keep the counters behind the fence
-      for (int t = 0; t < a.ntarget; ++t)
+      for (int t = 0; t < a.ntarget; ++t)  // relaxed: ordered by the release above
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.targets[2 * t + 1]),
-                           static_cast<unsigned long long>(i + 2), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                           static_cast<unsigned long long>(i + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     const long long te = wall_clock64();
     tl[2] = te;

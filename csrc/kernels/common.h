@@ -302,4 +302,21 @@ __device__ __forceinline__ bool gate_closed(const int* gate) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
 }
 
+// Release of a whole workgroup's stores at system scope, the producer form of the MI355X guide
+// ("Valid forms"): every wave waits for its own stores, the workgroup joins, and ONE lane writes
+// back the XCD's L2 and waits for the write-back.  After it thread 0 issues RELAXED flag / counter
+// stores.  Replaces __threadfence_system() by every thread (one L2 write-back + invalidate per
+// wave: 16 per 1024-thread arbiter) and release-ordered flag stores (one more write-back per store:
+// the arbiter's per-target counters made its release grow with the rank count, 4.3 us at 2 ranks,
+// 12.2 at 8, profiles/round3/arbiter_books).  Call from every thread (block-uniform control flow).
+__device__ __forceinline__ void block_release_system() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    // the compiler may drop the wait behind the write-back (ROCm 7.2 / gfx950): keep it explicit
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
 }  // namespace eh

@@ -989,8 +989,8 @@ slab_reduce_final(const A* __restrict__ part, A* __restrict__ G, int ld, const i
 
 // Stage 2 fused with the worker's message put (transport.hip's put + signal protocol): every
 // block also stores its sums straight into the receiver's mailbox rows (put.dst, the same
-// [slot][ld] layout as G), fences at system scope and counts itself done; the last block
-// resets the counter and release-stores the flag.  Saves the separate put_signal launch on
+// [slot][ld] layout as G), releases them at system scope (block_release_system) and counts
+// itself done; the last block resets the counter and stores the flag behind its own release.  Saves the separate put_signal launch on
 // every worker round's critical path.  No early return: every thread reaches the barrier.
 // Tagged puts (put.tag != nullptr, integrity.h): every block also adds its columns' checksum
 // terms of its slot's row into the sender scratch put.csum[slot]; the last block turns the sums
@@ -1026,11 +1026,10 @@ slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, Put
     const unsigned long long bs = block_sum_u64(term, scratch);
     if (threadIdx.x == 0 && bs) atomicAdd(put.csum + slot, bs);
   }
-  __threadfence_system();
-  __syncthreads();
+  block_release_system();  // this block's mailbox columns (and checksum adds) are out before its count
   if (threadIdx.x == 0) {
     const unsigned int total = gridDim.x * gridDim.y;
-    const unsigned int prev = __hip_atomic_fetch_add(put.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int prev = __hip_atomic_fetch_add(put.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = prev == total - 1;
     if (s_last) __hip_atomic_store(put.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1043,11 +1042,9 @@ slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, Put
     }
     if (put.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(put.dst)[1] ^= 0x10;  // test hook
   }
-  __threadfence_system();
-  __syncthreads();
+  block_release_system();  // the tags before the flag
   if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // see transport.hip: keep the flag behind the fence
-    __hip_atomic_store(put.flag, put.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(put.flag, put.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     put_decide_next_gate(put);
   }
 }
@@ -1190,15 +1187,35 @@ static hipError_t launch_wide(int bs, int R, const Segment* segs, const Task* ta
   constexpr int NV = Vec16<T>::N == 8 ? 4 : 8;
   if (R < 1 || R > 3 || ntasks % R) return hipErrorInvalidValue;
   const dim3 grid(ntasks / R);
-#define EH_WIDE(BS_, R_) \
-  hipLaunchKernelGGL((grad_dense_wide<T, A, NV, BS_, LOSS, R_>), grid, dim3(BS_), 0, st, segs, tasks, beta, slab, ld, gate)
-  if (bs == 256) {
-    if (R == 1) EH_WIDE(256, 1); else if (R == 2) EH_WIDE(256, 2); else EH_WIDE(256, 3);
+  // Rows that fill at most half of the NV vectors (fp32 d <= 4096 at 256 threads) take the NV / 2
+  // instance: the unused half would still hold R + 3 register tiles (valid[] is a run-time mask),
+  // which halves the resident workgroups per CU.
+  const bool half = static_cast<long long>(bs) * (NV / 2) * Vec16<T>::N >= ld;
+#define EH_WIDE(NV_, BS_, R_)                                                                                     \
+  hipLaunchKernelGGL((grad_dense_wide<T, A, NV_, BS_, LOSS, R_>), grid, dim3(BS_), 0, st, segs, tasks, beta, slab, ld, \
+                     gate)
+#define EH_WIDE_NV(BS_, R_)   \
+  do {                        \
+    if (half)                 \
+      EH_WIDE(NV / 2, BS_, R_); \
+    else                      \
+      EH_WIDE(NV, BS_, R_);   \
+  } while (0)
+  if (bs == 256 && R > 1 && !half) {
+    // Replica bundles of full-width rows: 512 threads of NV / 2 vectors cover the same columns.  The
+    // 256-thread NV instance holds R + 3 tiles of 2 NV values per thread (fp64 R = 3: 256 VGPRs plus
+    // AGPR spills, 1 wave per SIMD); at 512 threads the tiles halve (150 VGPRs) and a CU keeps 8 waves
+    // of the bundle in flight instead of 4.  One such workgroup is resident per CU
+    // (ops/grad.py wide_slots_per_cu).
+    if (R == 2) EH_WIDE(NV / 2, 512, 2); else EH_WIDE(NV / 2, 512, 3);
+  } else if (bs == 256) {
+    if (R == 1) EH_WIDE_NV(256, 1); else if (R == 2) EH_WIDE_NV(256, 2); else EH_WIDE_NV(256, 3);
   } else if (bs == 512 && R == 1) {  // (replica bundles of 512-thread rows would spill: R * 16+ accumulators)
-    EH_WIDE(512, 1);
+    EH_WIDE_NV(512, 1);
   } else {
     return hipErrorInvalidValue;
   }
+#undef EH_WIDE_NV
 #undef EH_WIDE
   return hipGetLastError();
 }

@@ -8,10 +8,10 @@
 // receiver's host polls (csrc/runtime/collector.cpp flag probes / ipc.cpp).
 //
 // Ordering (the classic put + signal pattern): every block copies its chunk with
-// 16-byte loads/stores, makes its writes visible at system scope
-// (__threadfence_system), and counts itself done on a per-descriptor counter; the
-// last block of a descriptor resets the counter and release-stores the flag at system
-// scope.  So a receiver that observes flag >= value also observes the payload, without
+// 16-byte loads/stores, makes its writes visible at system scope (block_release_system:
+// every wave waits for its stores, one lane writes the L2 back), and counts itself done on
+// a per-descriptor counter; the last block of a descriptor resets the counter, releases its
+// tags the same way and stores the flag.  So a receiver that observes flag >= value also observes the payload, without
 // relying on kernel-boundary cache semantics across devices.
 //
 // Integrity (integrity.h): a tagged descriptor also checksums every row it copies (LDS sums per
@@ -88,10 +88,11 @@ __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
     for (int r = threadIdx.x; r < p.rows; r += blockDim.x)
       if (row_sum[r]) atomicAdd(p.csum + r, row_sum[r]);
   }
-  __threadfence_system();
-  __syncthreads();
+  block_release_system();  // this block's rows (and checksum adds) are out before its count
   if (threadIdx.x == 0) {
-    const unsigned int prev = __hip_atomic_fetch_add(p.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // relaxed: the release above ordered the block's stores; the last block reads only the
+    // checksum sums, which are L2 atomics
+    const unsigned int prev = __hip_atomic_fetch_add(p.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = prev == gridDim.x - 1;
     if (s_last) __hip_atomic_store(p.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -104,13 +105,9 @@ __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
     }
     if (p.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(p.dst)[1] ^= 0x10;  // test hook
   }
-  __threadfence_system();
-  __syncthreads();
+  block_release_system();  // the tags before the flag
   if (threadIdx.x == 0) {
-    // ROCm 7.2 / gfx950: after a returned atomic the compiler may drop the wait that follows
-    // the fence's write-back, letting the flag overtake it; keep the wait explicitly.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(p.flag, p.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.flag, p.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     put_decide_next_gate(p);
   }
 }

@@ -212,7 +212,9 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     shared = max_rep > 1
     if cpl >= 256:
         if shared and cpl == 256 and max_rep <= 3:
-            return KernelChoice("wide", replicas=max_rep, bundle_rows=wide_bundle_rows(distinct_rows, n_cus, part_rows))
+            return KernelChoice("wide", replicas=max_rep,
+                                bundle_rows=wide_bundle_rows(distinct_rows, n_cus, part_rows,
+                                                             wide_slots_per_cu(prec_code, ld, max_rep)))
         return KernelChoice("wide", interleave=shared)
     if not shared:
         if prec_code != 2 and 8 < cpl <= 16:  # distinct rows of 16 columns per lane: bundles of one
@@ -240,12 +242,23 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
                         pair=True, wpr=0 if long_stream else 1)
 
 
-def wide_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional[Sequence[int]] = None) -> int:
-    """Rows per wide-row replica bundle (one 256-thread workgroup per bundle, 2 resident per CU): the
+def wide_slots_per_cu(prec_code: int, ld: int, replicas: int) -> int:
+    """Resident wide-row bundles per CU (grad_dense.hip launch_wide): rows that fit half of the
+    kernel's vectors at 256 threads (fp32 d <= 4096, bf16 <= 4096) take the NV / 2 instance, two or
+    more per CU; full-width replica rows (fp64 d > 2048, fp32 > 4096) run 512-thread workgroups of
+    about 150 VGPRs, one per CU."""
+    vec = {0: 2, 1: 4, 2: 8}[prec_code]
+    half = 256 * (WIDE_EPT[vec] // 2) >= ld
+    return 2 if replicas <= 1 or half else 1
+
+
+def wide_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional[Sequence[int]] = None,
+                     per_cu: int = 2) -> int:
+    """Rows per wide-row replica bundle (one workgroup per bundle, ``per_cu`` resident per CU): the
     shortest multiple of 16 rows whose bundles (per partition) all start in the first dispatch round,
     the rule of multi_bundle_rows.  The earlier "about 4 bundles per CU" sizing put 1032 bundles of
     976 rows on 1024 slot-rounds at 1e6 rows (a third, near-empty round) and 1042 of 96 rows at 1e5."""
-    slots = 2 * n_cus
+    slots = per_cu * n_cus
     parts = [int(r) for r in part_rows if r > 0] if part_rows else [distinct_rows / 8.0] * 8
     base = max(16, 16 * int(np.ceil(distinct_rows / slots / 16)))
 

@@ -281,6 +281,9 @@ def main():
     ap.add_argument("--layout", default="agc", choices=["agc", "frc2", "frc4", "naive"],
                     help="--only choices: replica layout")
     ap.add_argument("--only", choices=["dense", "sparse", "scale", "eval", "sweep", "choices"], default=None)
+    ap.add_argument("--ds", default="256,1000,2048,4096", help="--only sweep: row widths")
+    ap.add_argument("--ns", default="1e5,1e6,4e6", help="--only sweep: row counts")
+    ap.add_argument("--precs", default="fp64,fp32", help="--only sweep: precisions")
     a = ap.parse_args()
     out = []
     if a.only in (None, "dense"):
@@ -290,7 +293,8 @@ def main():
     if a.only == "eval":
         eval_cases(out)
     if a.only == "sweep":
-        sweep_cases(out)
+        sweep_cases(out, ds=tuple(int(x) for x in a.ds.split(",")), ns=tuple(int(float(x)) for x in a.ns.split(",")),
+                    precs=tuple(a.precs.split(",")))
     if a.only == "choices":
         if a.shapes:
             choice_cases(out, [(p, int(d), int(float(n))) for p, d, n in (x.split(":") for x in a.shapes.split(","))],

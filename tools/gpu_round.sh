@@ -14,6 +14,10 @@
 #   prof     rocprofv3 --kernel-trace --stats of the fp64 / fp32 / bf16 headline
 #   pmc      counter passes (one rocprofv3 --pmc run each) of the fp64 / fp32 headline
 #   eval     evaluation phase profile (tools/profile_eval.py)
+#   wide     the d = 2048 / 4096 rows of the sweep
+#   sparse   sparse gradients at the real-data shapes (timings, then rocprofv3 kernel stats)
+#   rccl     the RCCL self-loop GPU tests under rocprofv3 --kernel-trace (RCCL kernel names)
+#   pmcbytes FETCH_SIZE / raw read requests / WRITE_SIZE over known-byte workloads (tools/pmc_calibrate.py)
 #   abtree   same-box A/B against an older tree exported and built under build/ab_old
 #            (git archive <rev> | tar -x -C build/ab_old, then __graft_entry__.build() there):
 #            fp64 / fp32 headline, 100 steps, old / new interleaved twice
@@ -58,6 +62,30 @@ for s in "${STAGES[@]}"; do
       run 900 shapes.log python -u tools/bench_rank_shapes.py --out "$OUT/shapes.jsonl" ;;
     sweep)
       run 1100 sweep.log python -u tools/bench_kernels.py --only sweep --out "$OUT/sweep.jsonl" ;;
+    wide)  # the off-headline widths only (d = 2048 / 4096, fp64 and fp32)
+      run 600 wide.log python -u tools/bench_kernels.py --only sweep --ds 2048,4096 --out "$OUT/wide.jsonl" ;;
+    sparse)  # sparse gradients at the real-data shapes, then their kernel stats
+      run 600 sparse.log python -u tools/bench_kernels.py --only sparse --out "$OUT/sparse.jsonl"
+      run 600 prof_sparse.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_sparse" -o run -- \
+        python tools/bench_kernels.py --only sparse --out /tmp/sparse_prof.jsonl ;;
+    rccl)  # the RCCL self-loop comm path under the kernel tracer (RCCL kernel names in the stats)
+      run 600 prof_rccl.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_rccl" -o run -- \
+        python -u -m pytest tests/test_rccl_gpu.py -x -q --timeout 120 --timeout-method thread ;;
+    pmcbytes)  # FETCH_SIZE against the raw memory-side read requests and known byte counts
+      run 120 counters.log rocprofv3 -L
+      i=0
+      for grp in "FETCH_SIZE" "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B" "WRITE_SIZE"; do
+        i=$((i+1))
+        want=""
+        for c in $grp; do  # only counters this box lists (an unknown name would end the stage)
+          if grep -qw "$c" "$OUT/counters.log"; then want="$want $c"; fi
+        done
+        [ -z "$want" ] && { log "skip pass $i: none of $grp listed"; continue; }
+        [ "$grp" = "FETCH_SIZE" ] || [ "$grp" = "WRITE_SIZE" ] || want=$(echo $want | sed 's/\([A-Z0-9_]*\)/\1_sum/g')
+        run 180 "pmcb_$i.log" timeout -s KILL 170 rocprofv3 --pmc $want --output-format csv -d "$OUT/pmcb" -o "p$i" -- \
+          python tools/pmc_calibrate.py --known "$OUT/known.json"
+      done
+      python tools/pmc_summary.py "$OUT/pmcb" --by-kernel > "$OUT/pmcb_summary.json" ;;
     rehearse)
       for n in 2 4 8; do
         run 600 "rehearse_$n.log" python -u bench.py --gpus $n --steps 20 --warmup 5 --no-floor \
