@@ -64,6 +64,8 @@ class KernelChoice:
                       bundles of 256-thread rows (one row load, every replica's dot product and gradient)
              twopass  wider rows / bf16 beyond the one-pass kernels: two passes over X
     bundle_rows  rows per bundle task (bundle kinds)
+    fill         folded one-wave bundles: split every partition evenly so the plan has exactly
+                 ``fill`` workgroups (fill_splits; 0 = fixed ``bundle_rows``-row bundles)
     """
     kind: str
     replicas: int = 1
@@ -75,6 +77,7 @@ class KernelChoice:
     rows: int = 2
     beta_lds: bool = False
     interleave: bool = False
+    fill: int = 0
 
     @property
     def bundled(self) -> bool:
@@ -92,11 +95,26 @@ class KernelChoice:
         opts = [o for o, on in (("folded", self.fold), ("lane epilogue", self.lane_epi), ("pair", self.pair),
                                 ("interleaved", self.interleave)) if on]
         out = name + (f" ({', '.join(opts)})" if opts else "")
-        if self.bundled:
+        if self.bundled and self.fill:
+            out += f", R={self.replicas}, partitions split evenly over {self.fill} workgroups"
+        elif self.bundled:
             out += f", R={self.replicas}, {self.bundle_rows}-row bundles"
         elif self.kind == "fused":
             out += f", {self.rows} rows in flight" + (", beta in LDS" if self.beta_lds else "")
         return out
+
+
+def multi_slots(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS, cpl: int = 16) -> int:
+    """Resident one-wave bundles of grad_dense_multi on the chip (4 per folded workgroup)."""
+    long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
+    # fp64: one workgroup (4 bundles) per CU.  Since a step waits for its own row only (the label
+    # load behind the row), 4 waves with the next row in flight keep a CU's share of HBM busy, and
+    # half as many slab rows, betas and folds are paid (profiles/round3/rows_prefetch: 1024 / 512 /
+    # 256 / 128-row bundles at 1e6 / 500k / 250k / 125k rows: 1.142 / 0.587 / 0.304 / 0.160 ms vs
+    # 1.185-1.218 / 0.611 / 0.320 / 0.171 at two workgroups per CU)
+    per_cu = (12 if not long_stream else 8) if fp32 else 4
+    per_cu *= max(1, 16 // cpl)
+    return per_cu * n_cus
 
 
 def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS, cpl: int = 16,
@@ -116,15 +134,7 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
     distinct rows -> 512 / 256 / 128 / 64-row bundles, 1.195 / 0.600 / 0.312 / 0.169 ms (768 rows,
     the default before nt: 1.26 ms; 384: 1.42 = a second partial round); fp32 -> 352 / 192 / 96 /
     64 rows (192: 0.333 vs 256: 0.341-0.350 ms at 500k; 96: 0.177 vs 128: 0.186 at 250k)."""
-    long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
-    # fp64: one workgroup (4 bundles) per CU.  Since a step waits for its own row only (the label
-    # load behind the row), 4 waves with the next row in flight keep a CU's share of HBM busy, and
-    # half as many slab rows, betas and folds are paid (profiles/round3/rows_prefetch: 1024 / 512 /
-    # 256 / 128-row bundles at 1e6 / 500k / 250k / 125k rows: 1.142 / 0.587 / 0.304 / 0.160 ms vs
-    # 1.185-1.218 / 0.611 / 0.320 / 0.171 at two workgroups per CU)
-    per_cu = (12 if not long_stream else 8) if fp32 else 4
-    per_cu *= max(1, 16 // cpl)
-    slots = per_cu * n_cus
+    slots = multi_slots(distinct_rows, fp32, n_cus, cpl)
     parts = [int(r) for r in part_rows if r > 0] if part_rows else [distinct_rows / 8.0] * 8
     per = distinct_rows / slots
     # small problems: bundles down to 8 rows (a wave with one row ahead streams ~1.4 us per row, so a
@@ -142,6 +152,34 @@ def multi_bundle_rows(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS
     while not fits(rows) and rows < max(parts):
         rows += gran
     return rows if fits(rows) else base  # more partitions than slots: short bundles keep the tail short
+
+
+def fill_splits(part_rows: Dict[int, int], wgs: int, per_wg: int = 4) -> Optional[Dict[int, List[int]]]:
+    """Row boundaries of the bundles of every partition so the folded plan has exactly ``wgs``
+    workgroups of ``per_wg`` bundles (one partition per workgroup): workgroups are apportioned to
+    the partitions by row count (largest remainder, at least one each) and each partition is cut into
+    per_wg * (its workgroups) bundles whose lengths differ by at most one row.  Fixed-length bundles
+    leave CUs idle whenever the rows do not divide evenly (125k rows in 128-row bundles: 245
+    workgroups on 256 CUs, 1e6 rows in 1024-row bundles: 245 too).  None when there are more
+    partitions than workgroups."""
+    parts = sorted(p for p, n in part_rows.items() if n > 0)
+    total = sum(part_rows[p] for p in parts)
+    if not parts or len(parts) > wgs:
+        return None
+    quota = {p: part_rows[p] * wgs / total for p in parts}
+    w = {p: max(1, int(quota[p])) for p in parts}
+    while sum(w.values()) < wgs:
+        p = max(parts, key=lambda q: (quota[q] - w[q], -q))
+        w[p] += 1
+    while sum(w.values()) > wgs:
+        p = max((q for q in parts if w[q] > 1), key=lambda q: (w[q] - quota[q], q))
+        w[p] -= 1
+    out = {}
+    for p in parts:
+        n = part_rows[p]
+        k = min(per_wg * w[p], n)
+        out[p] = [(n * j) // k for j in range(k + 1)]
+    return out
 
 
 def pair_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, fp32: bool = False, cpl: int = 8) -> int:
@@ -392,6 +430,10 @@ class DenseGradPlan:
         tasks: List[Tuple[int, int, int, int]] = []
         slot_begin = [0]
         rows_per_task = max(MIN_ROWS_PER_TASK, -(-self.total_rows // max(1, target_tasks)))
+        splits = None
+        if self.choice.fill and self.choice.kind == "multi" and self.choice.fold:
+            splits = fill_splits({p: self.partitions[p][0].shape[0] for m in self.messages for p, _ in m},
+                                 self.choice.fill)
         seg_id = 0
         keys = []  # (partition, first row) of every task: equal keys read identical rows
         for slot, m in enumerate(self.messages):
@@ -399,8 +441,9 @@ class DenseGradPlan:
                 X, y = self.partitions[p]
                 n = X.shape[0]
                 segs += _SEG.pack(X.data_ptr(), y.data_ptr(), float(coef), n)
-                for r0 in range(0, n, rows_per_task):
-                    tasks.append((slot, seg_id, r0, min(n, r0 + rows_per_task), len(tasks)))
+                bounds = splits[p] if splits else list(range(0, n, rows_per_task)) + [n]
+                for r0, r1 in zip(bounds[:-1], bounds[1:]):
+                    tasks.append((slot, seg_id, r0, r1, len(tasks)))
                     keys.append((p, r0))
                 seg_id += 1
             slot_begin.append(len(tasks))

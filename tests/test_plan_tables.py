@@ -136,3 +136,19 @@ def test_no_tuning_env_knobs_left():
     assert len(knobs) <= 10, sorted(knobs)
     assert not any(k.startswith(("ERASUREHEAD_STAGE", "ERASUREHEAD_MULTI", "ERASUREHEAD_BUNDLE", "ERASUREHEAD_MFMA",
                                  "ERASUREHEAD_PERSISTENT", "ERASUREHEAD_GRAD")) for k in knobs), sorted(knobs)
+
+
+def test_fill_splits_fill_every_workgroup_slot():
+    """fill_splits (ops/grad.py): exactly `wgs` folded workgroups, bundle lengths within one row."""
+    import numpy as np
+
+    from erasurehead_amd.ops.grad import fill_splits
+
+    for parts, wgs in (({0: 125_000}, 256), ({p: 125_000 for p in range(8)}, 256), ({0: 125_000, 1: 125_000, 2: 125_000}, 256),
+                       ({0: 1000, 1: 300_000, 2: 7}, 512)):
+        s = fill_splits(parts, wgs)
+        assert sum(-(-(len(b) - 1) // 4) for b in s.values()) == wgs
+        for p, b in s.items():
+            d = np.diff(b)
+            assert b[0] == 0 and b[-1] == parts[p] and d.min() >= 1 and d.max() - d.min() <= 1
+    assert fill_splits({p: 10 for p in range(300)}, 256) is None

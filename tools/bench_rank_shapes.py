@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0) -> dict:
+def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0, fill: bool = False) -> dict:
     import numpy as np
     import torch
 
@@ -60,6 +60,17 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
         distinct = sum(parts[p][0].shape[0] for p in need)
         choice = replace(choose_kernel(prec.code, prec.ld(1000), choose_cpl(prec.ld(1000), prec.vec), max_rep, distinct),
                          bundle_rows=bundle_rows)
+    if fill:  # the default kernel with every partition split evenly over the chip's workgroup slots
+        import collections
+
+        from erasurehead_amd.ops.grad import multi_slots
+
+        max_rep = max(collections.Counter(p for m in msgs for p, _ in m).values())
+        distinct = sum(parts[p][0].shape[0] for p in need)
+        base = choice or choose_kernel(prec.code, prec.ld(1000), choose_cpl(prec.ld(1000), prec.vec), max_rep, distinct)
+        if base.kind == "multi" and base.fold:
+            cpl = choose_cpl(prec.ld(1000), prec.vec)
+            choice = replace(base, fill=multi_slots(distinct, prec.code == 1, cpl=cpl) // 4)
     plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, choice=choice)
     beta = torch.randn(prec.ld(1000), device="cuda", dtype=prec.acc) * 0.01
     G = plan.out_buffer()[0]
@@ -74,7 +85,7 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
     ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
     return {"n_gpus": n_gpus, "precision": precision, "shard": mode, "rank": r, "partitions": len(need),
             "shards": len(mine), "bundle_rows": plan.bundle_rows, "kernel": plan.choice.label(), "ntasks": plan.ntasks,
-            "kernel_ms": ms, "distinct_TBps": plan.distinct_bytes / ms / 1e9}
+            "kernel_ms": ms, "distinct_TBps": plan.distinct_bytes / ms / 1e9, "fill": plan.choice.fill}
 
 
 def main():
@@ -87,16 +98,17 @@ def main():
     ap.add_argument("--shard", default="partition", choices=["partition", "message"])
     ap.add_argument("--one", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--rows", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--fill", action="store_true", help="also time even splits over the workgroup slots")
     a = ap.parse_args()
     if a.one:
-        print(json.dumps(one(a.one, a.precision, a.shard, a.rows)), flush=True)
+        print(json.dumps(one(a.one, a.precision, a.shard, a.rows, a.fill)), flush=True)
         return 0
     lines = []
     sweeps = [None] + ([int(x) for x in a.rows_list.split(",")] if a.rows_sweep else [])
     for n in [int(x) for x in a.gpus_list.split(",")]:
-        for rows in sweeps:
+        for rows, fill in [(r, False) for r in sweeps] + ([(None, True)] if a.fill else []):
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", str(n), "--precision",
-                                  a.precision, "--shard", a.shard, "--rows", str(rows or 0)],
+                                  a.precision, "--shard", a.shard, "--rows", str(rows or 0)] + (["--fill"] if fill else []),
                                  capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print(out.stdout[-2000:], out.stderr[-2000:], file=sys.stderr)

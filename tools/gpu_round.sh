@@ -14,6 +14,7 @@
 #   prof     rocprofv3 --kernel-trace --stats of the fp64 / fp32 / bf16 headline
 #   pmc      counter passes (one rocprofv3 --pmc run each) of the fp64 / fp32 headline
 #   eval     evaluation phase profile (tools/profile_eval.py)
+#   conv     tools/convergence_study.py (all schemes, drain and lazy rows)
 #   wide     the d = 2048 / 4096 rows of the sweep
 #   sparse   sparse gradients at the real-data shapes (timings, then rocprofv3 kernel stats)
 #   rccl     the RCCL self-loop GPU tests under rocprofv3 --kernel-trace (RCCL kernel names)
@@ -59,7 +60,9 @@ for s in "${STAGES[@]}"; do
         run 600 "bench_$p.log" $BENCH --precision $p && tail -1 "$OUT/bench_$p.log" > "$OUT/bench_$p.json"
       done ;;
     shapes)
-      run 900 shapes.log python -u tools/bench_rank_shapes.py --out "$OUT/shapes.jsonl" ;;
+      run 900 shapes.log python -u tools/bench_rank_shapes.py --fill --out "$OUT/shapes.jsonl"
+      run 300 prof_shape8.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_shape8" -o run -- \
+        python tools/bench_rank_shapes.py --one 8 ;;
     sweep)
       run 1100 sweep.log python -u tools/bench_kernels.py --only sweep --out "$OUT/sweep.jsonl" ;;
     wide)  # the off-headline widths only (d = 2048 / 4096, fp64 and fp32)
@@ -118,6 +121,8 @@ for s in "${STAGES[@]}"; do
           done
         done
       done ;;
+    conv)  # convergence vs wall-clock, every scheme incl. the lazy-drain rows (11 processes on the GPU)
+      run 900 conv.log python -u tools/convergence_study.py --out "$OUT/convergence" ;;
     eval)
       run 600 eval.log python -u tools/profile_eval.py --out "$OUT/eval.json" ;;
     *) echo "unknown stage $s"; exit 2 ;;
