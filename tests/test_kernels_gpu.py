@@ -489,10 +489,12 @@ def test_dense_grad_one_wave_bundles(native, rows, d, prec_name, loss, form):
 
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
 @pytest.mark.parametrize("rows,d,prec_name", [(16, 4096, "fp64"), (33, 3000, "fp64"), (64, 8000, "fp32"),
-                                              (17, 5000, "bf16")])
+                                              (17, 5000, "bf16"), (20, 4000, "fp32"), (16, 2100, "fp32"),
+                                              (9, 3000, "bf16")])
 def test_dense_grad_wide_row_bundles(native, rows, d, prec_name, loss):
-    """grad_dense_wide with replica bundles: a 256-thread workgroup loads each wide row once and
-    computes every replica's dot product, residual (own coefficient) and gradient from registers.
+    """grad_dense_wide with replica bundles: a workgroup loads each wide row once and computes every
+    replica's dot product, residual (own coefficient) and gradient from registers (fp32 / bf16 rows
+    of <= 4096 columns: the half-width 256-thread instance; wider rows: 512 threads).
     Bundles of 3, of 2 padded to 3 and odd-length bundles against the fp64 oracle, and equal to the
     one-replica wide kernel message by message (to rounding: the row split into tasks differs)."""
     prec = get_precision(prec_name)
