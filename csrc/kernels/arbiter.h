@@ -22,6 +22,7 @@ constexpr int kArbMaxW = 64;          // workers (bitmasks)
 constexpr int kArbMaxProbes = 512;    // expected shards per round
 constexpr int kArbMaxSrc = 64;        // worker ranks (one shared counter each)
 constexpr int kArbMaxRows = 16;       // buffer rows (shards) of one message
+constexpr int kArbLdsTable = 4096;    // decode-table doubles kept in LDS (2^W * W, W <= 9)
 constexpr int kArbLogInts = 4 + 4 * kArbMaxW;   // per round: status, n_arrivals, n_used, -, then (w, p) pairs
 // per round: t_begin, t_dec (combine done), t_end (released), t_join (poll joined), t_decoded (decode
 // done), -, -, -, then one tick per arrival

@@ -32,8 +32,11 @@ __device__ __forceinline__ bool rule_holds(int rule, int k, int W, int G, int cn
   }
 }
 
+// Polls are relaxed system-scope loads (they bypass the caches); the poll that ends step 1 is followed
+// by ONE acquire fence of wave 0 before the barrier that releases the other waves' message loads (the
+// MI355X guide's consumer form: an acquire per poll is an L1 invalidate each, 2-3x slower per hop).
 __device__ __forceinline__ unsigned long long load_counter(const unsigned long long* p) {
-  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Inclusive prefix sum over the wave (every lane active).
@@ -72,6 +75,10 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
   __shared__ int s_group[kArbMaxW], s_nsh[2 * kArbMaxW], s_nrows[2 * kArbMaxW];
   __shared__ int s_rows[2 * kArbMaxW * kArbMaxRows];
   __shared__ double s_trow[kArbMaxW];   // decode-table row of the round's completion pattern
+  // the whole decode table when it is small (2^W * W <= 4096 doubles: W <= 9, the headline's 2 KB):
+  // copied by waves 1-15 while wave 0 polls, so the completion pattern's row is an LDS read after the
+  // stop instead of a dependent global load on the stop -> release path
+  __shared__ double s_table[kArbLdsTable];
   __shared__ int arr_w[2 * kArbMaxW], arr_p[2 * kArbMaxW];
   __shared__ long long arr_t[2 * kArbMaxW];
   __shared__ const void* mptr[kMaxMsgs];
@@ -111,6 +118,12 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
   }
   __syncthreads();
 
+  const bool table_dec = (a.decode == 3 || a.decode == 4) && a.table;
+  const bool lds_table = table_dec && a.W <= 12 && (1ll << a.W) * a.W <= kArbLdsTable;
+  if (lds_table && tid >= 64) {
+    const int n = (1 << a.W) * a.W;
+    for (int e = tid - 64; e < n; e += blockDim.x - 64) s_table[e] = a.table[e];
+  }
   // this round's update constants and the first 1024 columns of beta / u, loaded while the workers
   // compute (off the stop-rule -> release path)
   const double decay = a.decay[i], gm = a.gm[i], l2 = a.l2[i], theta = a.theta[i];
@@ -220,6 +233,9 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
       }
       __builtin_amdgcn_s_sleep(2);
     }
+    // acquire for everything the flags announced (the mailbox rows every wave reads after the barrier)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // the completion pattern (every p = 0 arrival) and its decode-table row, one lane per worker
     const unsigned long long mask = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(got0)) |
                                     static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(
@@ -228,7 +244,7 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
       s_mask = mask;
       s_narr = narr;
     }
-    if ((a.decode == 3 || a.decode == 4) && a.table)
+    if (table_dec && !lds_table)
       for (int w = tid; w < a.W; w += 64)
         s_trow[w] = (mask >> w & 1) ? a.table[static_cast<long long>(mask) * a.W + w] : 0.0;
   } else if (a.tags && check_prev && tid == 64) {
@@ -247,8 +263,8 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
     }
     return;
   }
-  // (no further fence: wave 0's system-scope acquire loads of the counters invalidated this CU's
-  // caches after seeing them, and the barrier orders every wave's loads after those)
+  // (no further fence: wave 0's acquire after the poll invalidated this CU's caches, and the barrier
+  // orders every wave's loads after it)
   if (tid == 0) tl[3] = wall_clock64();
 
   // ---- 2. decode (wave 0, one lane per arrival; MasterPump::decode's message order) ------------
@@ -308,7 +324,8 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
         for (int w0 = 0; w0 < a.W; w0 += 64) {
           const int w = w0 + tid;
           const bool on = w < a.W && (mask >> w & 1);
-          const double c = on ? s_trow[w] : 0.0;
+          // (the LDS copy is complete: waves 1-15 wrote it before the barrier that ended the poll)
+          const double c = on ? (lds_table ? s_table[static_cast<int>(mask) * a.W + w] : s_trow[w]) : 0.0;
           if (__ballot(on && c != c) && tid == 0) s_status = 2;  // NaN: completion pattern without a table row
           const int nr = on ? s_nrows[2 * w] : 0;
           const int incl = scan(nr);
