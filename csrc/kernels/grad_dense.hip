@@ -1057,15 +1057,17 @@ slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, Put
 // (one launch less per round), results bitwise unchanged.  (A variant that also folded stage 1 in,
 // with the last block of each chunk finishing it, paid a device-scope release fence per block --
 // an L2 writeback on every XCD -- and took 427 us: profiles/round3/fused_update.)
+// 1024 threads: 16 waves share a chunk's slots (the headline's 22 slots took ~6 dependent rounds of
+// split loads per wave at 4 waves, 10.2 us per call: profiles/round3/prof_nt).
 template <typename A>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 slab_final_update(const A* __restrict__ part, A* __restrict__ G, int ld, int nslots, const LocalUpdate up) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lu_raw[];
   A* gs = reinterpret_cast<A*>(lu_raw);  // [nslots][64] the chunk's message sums
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = blockIdx.x * kWave + lane;
   if (up.stamp && blockIdx.x == 0 && threadIdx.x == 0) *up.stamp = wall_clock64();
-  for (int q = wid; q < nslots; q += 4) {
+  for (int q = wid; q < nslots; q += static_cast<int>(blockDim.x >> 6)) {
     A v = A(0);
     if (c < ld) {
 #pragma unroll
@@ -1385,12 +1387,12 @@ hipError_t grad_dense_update_launch(int dtype, int loss, int cpl, const void* se
   if (dtype == 0) {
     hipLaunchKernelGGL(slab_reduce_partial<double>, pgrid, dim3(256), 0, st, (const double*)slab, stb, (double*)part, ld, nullptr);
     if ((e = go(reinterpret_cast<const void*>(slab_final_update<double>))) != hipSuccess) return e;
-    hipLaunchKernelGGL(slab_final_update<double>, dim3(ceil_div(ld, kWave)), dim3(256), lds, st, (const double*)part,
+    hipLaunchKernelGGL(slab_final_update<double>, dim3(ceil_div(ld, kWave)), dim3(1024), lds, st, (const double*)part,
                        (double*)G, ld, nslots, up);
   } else {
     hipLaunchKernelGGL(slab_reduce_partial<float>, pgrid, dim3(256), 0, st, (const float*)slab, stb, (float*)part, ld, nullptr);
     if ((e = go(reinterpret_cast<const void*>(slab_final_update<float>))) != hipSuccess) return e;
-    hipLaunchKernelGGL(slab_final_update<float>, dim3(ceil_div(ld, kWave)), dim3(256), lds, st, (const float*)part,
+    hipLaunchKernelGGL(slab_final_update<float>, dim3(ceil_div(ld, kWave)), dim3(1024), lds, st, (const float*)part,
                        (float*)G, ld, nslots, up);
   }
   return hipGetLastError();
