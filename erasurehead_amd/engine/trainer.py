@@ -887,7 +887,12 @@ class Trainer:
             self.rank_stats["stale_rounds_skipped"] = len(self.skipped_rounds)
         if cfg.instrument:
             self.rank_stats.update(kernel_us=_mean_us(ker_ms, a0), msg_put_us=_mean_us(put_ms, a0))
-        env.barrier()
+        try:
+            env.barrier()
+        except RuntimeError as e:  # a peer rank is gone (gloo: connection reset): this rank's rounds are done,
+            # the master names the lost messages and fails the run (its final drain times out)
+            print(f"rank {env.rank}: final barrier failed, a peer rank is gone ({e}); "
+                  f"this worker's {R - start} rounds completed", file=sys.stderr, flush=True)
         del pump
         return None
 

@@ -47,7 +47,8 @@ BENCH="python -u bench.py --no-floor"
 for s in "${STAGES[@]}"; do
   case "$s" in
     tests)
-      run 1500 pytest.log python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+      # TESTS="files..." narrows the run (default: every GPU test)
+      run 1500 pytest.log python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 120 --timeout-method thread
       tail -3 "$OUT/pytest.log" ;;
     smoke)
       run 300 smoke.log python -c 'import __graft_entry__ as g; g.build(); g.smoke(); print("smoke ok")' ;;
