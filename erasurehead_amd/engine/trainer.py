@@ -86,12 +86,13 @@ class TrainResult:
     arrivals: List[List[Tuple[int, int, float]]] = field(default_factory=list)
 
 
-def _sabotage_exit(rank: int) -> Optional[int]:
-    """Test hook ERASUREHEAD_SABOTAGE=exit:<rank>:<round>: that worker rank exits before that round."""
+def _sabotage_exit(rank: int) -> Optional[Tuple[str, int]]:
+    """Test hook ERASUREHEAD_SABOTAGE=exit:<rank>:<round> (that worker rank exits before that round)
+    or hang:<rank>:<round> (it stops there and never sends again, alive until the job is torn down)."""
     spec = os.environ.get("ERASUREHEAD_SABOTAGE", "")
     parts = spec.split(":")
-    if len(parts) == 3 and parts[0] == "exit" and int(parts[1]) == rank:
-        return int(parts[2])
+    if len(parts) == 3 and parts[0] in ("exit", "hang") and int(parts[1]) == rank:
+        return parts[0], int(parts[2])
     return None
 
 
@@ -432,7 +433,7 @@ class Trainer:
         """After the last round: wait until every message of every round has arrived (dead workers
         excepted), bounded by the round timeout or the longest virtual lag the delays can carry.  A
         message that never lands means a worker rank is gone: the transport is aborted (its queued
-        receives released) before anything synchronises the device, and the run says so."""
+        receives released) before anything synchronises the device, and the run fails with that reason."""
         d = self.delay_table()
         fin = np.where(np.isfinite(d), d, 0.0) if d.size else d
         lag = float(np.sum(np.max(fin, axis=1))) if fin.size else 0.0
@@ -442,6 +443,10 @@ class Trainer:
             print(f"[erasurehead] WARNING: {why}", file=sys.stderr, flush=True)
             self.rank_stats["aborted"] = why
             self.tx.abort()
+            # the device is drained now (the abort released the queued receives); a rank that is gone
+            # cannot join the run's closing collectives, so the run fails here, by name
+            self._sync()
+            raise RuntimeError(why)
         return ok
 
     def _timed_fence(self):
@@ -863,11 +868,14 @@ class Trainer:
         self.rank_stats["device_wait"] = bool(pump.device_wait)
         cut = timed_start if timed_start is not None and start <= timed_start < R else None
         segments = [(start, cut), (cut, R)] if cut is not None else [(start, R)]
-        gone = _sabotage_exit(env.rank)  # test hook: this worker rank dies after that round
+        gone = _sabotage_exit(env.rank)  # test hook: this worker rank dies / hangs after that round
         if gone is not None:
-            pump.run(start, min(R, gone))
+            pump.run(start, min(R, gone[1]))
             torch.cuda.synchronize(env.device)
-            os._exit(0)
+            if gone[0] == "exit":
+                os._exit(0)
+            while True:  # silent from here on: the master's drain must give up on it
+                time.sleep(1.0)
         t0 = None
         for k, (a, b) in enumerate(segments):
             if k == 1:

@@ -288,17 +288,20 @@ def test_loopback_physically_late_ranks(tmp_path):
 
 
 def test_loopback_dead_worker_teardown_finishes(tmp_path):
-    """a worker rank that dies mid-run on the stream-ordered p2p path (the loopback twin of
-    RCCL).  Its receives and sends stay queued on the master's per-peer streams; the master's final
-    drain times out, aborts the communicator (which releases them) before anything synchronises the
-    device, and the run ends with that reason instead of hanging in a device sync."""
+    """a worker rank that stops mid-run on the stream-ordered p2p path (the loopback twin of
+    RCCL) and never sends again.  Its receives stay queued on the master's per-peer streams; the
+    master's final drain times out, aborts the communicator (which releases them) before anything
+    synchronises the device, and the run ends with that reason instead of hanging in a device sync.
+    (The rank hangs rather than exits: an exited rank resets the gloo control sockets, the surviving
+    worker's post-run collectives fail first and the launcher tears the job down before the
+    master's drain deadline.)"""
     import json
     import time
 
     over = dict(round_timeout=5.0, num_itrs=12, drain="lazy")
     t0 = time.time()
     r = _launch_raw(3, 4, "AGD", dict(EH_TEST_OUT=str(tmp_path / "x.npz"), ERASUREHEAD_TRANSPORT="loopback",
-                                      ERASUREHEAD_SABOTAGE="exit:2:4", EH_TEST_CFG=json.dumps(over)), timeout=400)
+                                      ERASUREHEAD_SABOTAGE="hang:2:4", EH_TEST_CFG=json.dumps(over)), timeout=400)
     assert time.time() - t0 < 300
     err = r.stdout + r.stderr
     assert "messages never arrived; aborting the transport" in err, err[-3000:]
