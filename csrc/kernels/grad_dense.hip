@@ -1049,6 +1049,67 @@ slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, Put
   }
 }
 
+// Stage 2 + put of a SMALL message set (nslots * ld <= kPutOneElems: the 8-GPU rank's 3 x 1000) in
+// ONE 1024-thread block: no cross-block counter and no second release -- the block sums its
+// elements two at a time (32 split loads in flight per thread), keeps the tag checksums in LDS
+// (integer adds, order-free), writes the tags, releases once and stores the flag.  The multi-block
+// form pays a device-scope atomic round trip and the last block's own release on top.
+constexpr int kPutOneElems = 4096, kPutOneSlots = 16;
+
+template <typename A>
+__global__ void __launch_bounds__(1024)
+slab_reduce_final_put1(const A* __restrict__ part, A* __restrict__ G, int ld, int nslots, PutDesc put) {
+  __shared__ unsigned long long tsum[kPutOneSlots];
+  __shared__ int s_live;
+  const int tid = threadIdx.x;
+  if (gate_closed(put.gate)) {  // a skipped stale round (launch-uniform)
+    if (tid == 0) put_decide_next_gate(put);
+    return;
+  }
+  if (tid < kPutOneSlots) tsum[tid] = 0;
+  if (tid == 0) s_live = !(put.abort && __hip_atomic_load(put.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  __syncthreads();
+  const bool live = s_live;
+  const int n = nslots * ld;
+  for (int e0 = tid; e0 < n; e0 += 2 * static_cast<int>(blockDim.x)) {
+    const int e1 = e0 + static_cast<int>(blockDim.x);
+    const int q0 = e0 / ld, c0 = e0 - q0 * ld;
+    const bool two = e1 < n;
+    const int q1 = two ? e1 / ld : q0, c1 = two ? e1 - q1 * ld : c0;
+    A v0[kSplits], v1[kSplits];
+#pragma unroll
+    for (int k = 0; k < kSplits; ++k) {
+      v0[k] = part[(static_cast<long long>(q0) * kSplits + k) * ld + c0];
+      v1[k] = part[(static_cast<long long>(q1) * kSplits + k) * ld + c1];
+    }
+    A s0 = A(0), s1 = A(0);
+#pragma unroll
+    for (int k = 0; k < kSplits; ++k) {  // slab_reduce_final's order
+      s0 += v0[k];
+      s1 += v1[k];
+    }
+    G[e0] = s0;
+    if (live) static_cast<A*>(put.dst)[e0] = s0;
+    if (put.tag) atomicAdd(&tsum[q0], tag_term(elem_bits(s0), c0));
+    if (two) {
+      G[e1] = s1;
+      if (live) static_cast<A*>(put.dst)[e1] = s1;
+      if (put.tag) atomicAdd(&tsum[q1], tag_term(elem_bits(s1), c1));
+    }
+  }
+  if (!live) return;  // block-uniform
+  if (put.tag) {
+    __syncthreads();
+    if (tid < nslots) put.tag[tid] = MsgTag{static_cast<unsigned int>(put.value), put.rank, tsum[tid]};
+    if (put.corrupt && tid == 0) static_cast<unsigned char*>(put.dst)[1] ^= 0x10;  // test hook
+  }
+  block_release_system();  // the rows and tags before the flag
+  if (tid == 0) {
+    __hip_atomic_store(put.flag, put.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    put_decide_next_gate(put);
+  }
+}
+
 // Stage 2 + the master's combine and update of a device-driven local round in one launch
 // (MasterPump::run_local; update.hip combine_update's arithmetic).  One block per 64-column chunk:
 // its waves sum the chunk's splits for every slot (slab_reduce_final's order; G rows written, sums
@@ -1106,7 +1167,9 @@ static hipError_t slab_reduce_launch(const A* slab, const int* stb, A* part, A* 
                      slab, stb, part, ld, gate);
   if (put && put->tag && (nslots > kMaxTagRows || !put->csum)) return hipErrorInvalidValue;
   if (put && put->gate != gate) return hipErrorInvalidValue;  // one round, one gate
-  if (put)
+  if (put && nslots <= kPutOneSlots && static_cast<long long>(nslots) * ld <= kPutOneElems)
+    hipLaunchKernelGGL(slab_reduce_final_put1<A>, dim3(1), dim3(1024), 0, st, part, G, ld, nslots, *put);
+  else if (put)
     hipLaunchKernelGGL(slab_reduce_final_put<A>, dim3(ceil_div(ld, 256), nslots), dim3(256), 0, st, part, G, ld, *put);
   else
     hipLaunchKernelGGL(slab_reduce_final<A>, dim3(ceil_div(ld, 256), nslots), dim3(256), 0, st, part, G, ld, gate);
