@@ -74,7 +74,7 @@ for s in "${STAGES[@]}"; do
         python tools/bench_kernels.py --only sparse --out /tmp/sparse_prof.jsonl ;;
     rccl)  # the RCCL self-loop comm path under the kernel tracer (RCCL kernel names in the stats)
       run 600 prof_rccl.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_rccl" -o run -- \
-        python -u -m pytest tests/test_rccl_gpu.py -x -q --timeout 120 --timeout-method thread ;;
+        python -u -m pytest tests/test_rccl_gpu.py -k self_loop -x -q --timeout 120 --timeout-method thread ;;
     pmcbytes)  # FETCH_SIZE against the raw memory-side read requests and known byte counts
       run 120 counters.log rocprofv3 -L
       i=0
