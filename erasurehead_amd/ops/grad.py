@@ -703,7 +703,7 @@ class SparseGradPlan:
         row16 = all(A.shape[0] <= 65536 for A in blocks)
         rows_l, vals_l, cps, tiles, spans, empty = [], [], [], [], [], []
         entry0, row0, nnzs = [], [], []
-        e_off = r_off = 0
+        e_off = r_off = n_tiles = 0
         for j, A in enumerate(blocks):
             C = A.tocsc()
             C.sort_indices()
@@ -717,20 +717,25 @@ class SparseGradPlan:
             entry0.append(e_off)
             row0.append(r_off)
             nnzs.append(nnz)
-            t_first = len(tiles)
-            for base in range(0, nnz, tile):
-                c0 = int(np.searchsorted(cp, base, side="right")) - 1
-                end = min(base + tile, nnz)
-                c_last = int(np.searchsorted(cp, end - 1, side="right")) - 1
-                flags = (1 if cp[c0] < base else 0) | (2 if cp[c_last + 1] > base + tile else 0)
-                tiles.append((j, base, c0, flags))
+            t_first = n_tiles
+            bases = np.arange(0, nnz, tile, dtype=np.int64)
+            if bases.size:
+                c0 = np.searchsorted(cp, bases, side="right") - 1
+                end = np.minimum(bases + tile, nnz)
+                c_last = np.searchsorted(cp, end - 1, side="right") - 1
+                flags = (cp[c0] < bases).astype(np.int64) | 2 * (cp[c_last + 1] > bases + tile).astype(np.int64)
+                tiles.append(np.stack([np.full(bases.size, j), bases, c0, flags], axis=1))
+                n_tiles += bases.size
             nonempty = np.nonzero(cp[1:] > cp[:-1])[0]
             t1 = cp[nonempty] // tile
             t2 = (cp[nonempty + 1] - 1) // tile
-            for c, a1, a2 in zip(nonempty[t2 > t1], t1[t2 > t1], t2[t2 > t1]):
-                spans.append((j, int(c), t_first + int(a1), t_first + int(a2)))
-            for c in np.nonzero(cp[1:] == cp[:-1])[0]:
-                empty.append((j, int(c)))
+            cross = t2 > t1
+            if cross.any():
+                spans.append(np.stack([np.full(int(cross.sum()), j), nonempty[cross], t_first + t1[cross],
+                                       t_first + t2[cross]], axis=1))
+            ec = np.nonzero(cp[1:] == cp[:-1])[0]
+            if ec.size:
+                empty.append(np.stack([np.full(ec.size, j), ec], axis=1))
             e_off += nnz + pad
             r_off += A.shape[0]
         crow = np.concatenate(rows_l) if rows_l else np.zeros(tile, dtype=np.int64)
@@ -738,12 +743,12 @@ class SparseGradPlan:
         return {"row16": row16, "crow": np.ascontiguousarray(crow),
                 "cvals": np.concatenate(vals_l) if vals_l else np.zeros(tile),
                 "col_ptr": np.ascontiguousarray(np.stack(cps)) if cps else np.zeros((1, d + 1), dtype=np.int32),
-                "tiles": np.asarray(tiles, dtype=np.int32).reshape(-1, 4),
+                "tiles": (np.concatenate(tiles) if tiles else np.zeros((0, 4))).astype(np.int32).reshape(-1, 4),
                 "part_entry0": np.asarray(entry0 or [0], dtype=np.int64),
                 "part_row0": np.asarray(row0 or [0], dtype=np.int64),
                 "part_nnz": np.asarray(nnzs or [0], dtype=np.int32),
-                "span": np.asarray(spans, dtype=np.int32).reshape(-1, 4),
-                "empty": np.asarray(empty, dtype=np.int32).reshape(-1, 2)}
+                "span": (np.concatenate(spans) if spans else np.zeros((0, 4))).astype(np.int32).reshape(-1, 4),
+                "empty": (np.concatenate(empty) if empty else np.zeros((0, 2))).astype(np.int32).reshape(-1, 2)}
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:
         return torch.zeros((n, self.nslots, self.ld), dtype=self.prec.acc, device=self.device)
