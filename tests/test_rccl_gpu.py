@@ -6,7 +6,6 @@
   exactly through the fp64 oracle.
 * RcclComm between two processes on one GPU ends with a named outcome within a deadline, never a hang.
 """
-import copy
 import json
 import os
 import subprocess
@@ -19,39 +18,24 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-# (At 4 thread ranks the one process holds ~16 streams plus RCCL's own: more than its hardware queues,
-# and a stream wait parked in a shared queue stalls the stream that would release it -- the hang the
-# per-rank processes of a real node never see, one process per GPU.  2 and 3 ranks stay within them.)
 @pytest.mark.parametrize("world,case_i", [(2, 4), (3, 1)])
 def test_rccl_self_loop_pumps_match_replay(world, case_i):
-    from oracle import replay, stops_exactly_at_last
-    from test_engine_cpu import CASES, make
-
-    from erasurehead_amd.engine import Trainer
-    from erasurehead_amd.parallel.dist import run_thread_ranks
-
-    cfg, src, sch, parts = make(CASES[case_i], "AGD")
-    cfg.num_itrs, cfg.transport = 10, "rccl-self"
-
-    def fn(env):
-        tr = Trainer(copy.deepcopy(cfg), env, src, scheme=sch)
-        res = tr.run()
-        rep = tr.rank_report()
-        sends = tr.tx.selfloop.rccl_sends
-        beta0 = getattr(tr, "beta0", None)
-        tr.close()
-        return res, beta0, rep, sends
-
-    out = run_thread_ranks(world, fn, timeout=240)
-    res, beta0, rep, sends = out[0]
-    assert rep["transport"] == "rccl-self" and rep["round_loop"] == "native pump"
-    assert all(o[2]["round_loop"] == "native pump" for o in out[1:] if o[2]["messages"])
-    R = cfg.num_itrs
-    senders = sum(1 for o in out[1:] if o[2]["messages"])
-    assert sends >= (world - 1) * R + senders * R  # every beta and every message went through ncclSend/ncclRecv
-    assert stops_exactly_at_last(sch, res.arrivals)
-    ref = replay(sch, parts, beta0, res.arrivals, "AGD", cfg.alpha_value, cfg.n_rows, cfg.eta())
-    np.testing.assert_allclose(res.betaset, ref, rtol=1e-9, atol=1e-11)
+    """In a fresh process with 32 hardware queues (tests/rccl_self_run.py): thread ranks share one
+    process, and past its hardware-queue count a stream wait parked in a shared queue stalls the
+    stream that would release it (seen at 3 ranks with 16 queues) -- what one process per GPU never
+    meets."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="32", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "rccl_self_run.py"), str(world), str(case_i)], env=env,
+                       capture_output=True, text=True, timeout=115)
+    res = [json.loads(l.split("RCCL_SELF_RESULT ", 1)[1]) for l in r.stdout.splitlines() if "RCCL_SELF_RESULT " in l]
+    assert r.returncode == 0 and len(res) == 1, r.stdout[-3000:] + r.stderr[-3000:]
+    x = res[0]
+    assert x["hw_queues"] == 32
+    assert x["transport"] == "rccl-self" and x["round_loop"] == "native pump"
+    assert all(l == "native pump" for l in x["worker_loops"])
+    assert x["sends"] >= x["min_sends"]  # every beta and every message went through ncclSend/ncclRecv
+    assert x["stops_exactly"]
+    assert x["rel_err"] < 1e-9
 
 
 def test_rccl_comm_two_processes_one_gpu_named_outcome(tmp_path):
