@@ -49,7 +49,7 @@ def test_rccl_comm_two_processes_one_gpu_named_outcome(tmp_path):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(HERE, "rccl_dup_gpu.py")]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     res = [json.loads(l.split("RCCL_RESULT ", 1)[1]) for l in r.stdout.splitlines() if "RCCL_RESULT " in l]
     assert len(res) == 2, r.stdout[-3000:] + r.stderr[-3000:]
     for x in res:
