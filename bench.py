@@ -93,6 +93,7 @@ def parse(argv=None):
     ap.add_argument("--late-ms", type=float, default=5.0,
                     help="N > 1 straggler sub-run: the last rank is physically late by this much every round")
     ap.add_argument("--straggler-steps", type=int, default=40, help="timed rounds of each straggler sub-run")
+    ap.add_argument("--slab-mode", type=int, default=None, help=argparse.SUPPRESS)  # A/B of the slab reduction form
     ap.add_argument("--no-straggler", action="store_true",
                     help="N > 1: skip the reference-topology and straggler sub-runs")
     return ap.parse_args(argv)
@@ -138,6 +139,10 @@ def main(argv=None) -> int:
     from erasurehead_amd.parallel.transport import TransportError
 
     env = init_distributed("auto")
+    if a.slab_mode is not None and torch.cuda.is_available():
+        from erasurehead_amd._ext import native
+
+        native().set_slab_reduce_mode(a.slab_mode)
 
     def make_cfg(rounds: int, naive: bool = a.naive, **kw) -> RunConfig:
         opts = dict(add_delay=a.add_delay, num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234,

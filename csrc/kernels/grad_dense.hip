@@ -952,6 +952,11 @@ grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks
 // 16 splits x 16 column chunks x slots gives thousands of workgroups for what used to be
 // a 32-workgroup serial loop (70 us -> a few us at 2048 tasks x 1000 columns).
 constexpr int kSplits = 16;
+// Slab reduction form of the non-update paths (set_slab_reduce_mode, for same-box A/B by
+// tools/bench_kernels.py --only reduce): 1 = one fused launch for plain reductions and puts
+// (slab_reduce_fused[_put]); 2 = fused plain reductions, puts as stage 1 + the put kernel;
+// 0 = the two stages everywhere.
+static int g_slab_mode = 1;
 
 template <typename A>
 __global__ void __launch_bounds__(256)
@@ -985,6 +990,105 @@ slab_reduce_final(const A* __restrict__ part, A* __restrict__ G, int ld, const i
 #pragma unroll
   for (int k = 0; k < kSplits; ++k) s += part[(static_cast<long long>(slot) * kSplits + k) * ld + c];
   G[static_cast<long long>(slot) * ld + c] = s;
+}
+
+// Both stages in ONE launch, bitwise the same sums: a 1024-thread block per (64-column chunk, slot),
+// wave k = split k.  Lane c of wave k keeps the four interleaved sums stage 1's waves kept (rows
+// t0 + w, t0 + w + 4, ... of its split, each in row order; eight rows loaded per step), folds them
+// as (s0 + s1) + (s2 + s3), and wave 0 adds the 16 splits in order from A(0) like stage 2.  One launch
+// and no partial buffer in HBM instead of two back-to-back launches (5.7 + 4.7 us at the 8-GPU rank
+// shape, profiles/round4/prof_shape8).
+template <typename A>
+__device__ __forceinline__ A fused_split_sum(const A* __restrict__ slab, int t0, int t1, int ld, int c) {
+  A acc[4] = {A(0), A(0), A(0), A(0)};
+  int t = t0;
+  for (; t + 8 <= t1; t += 8) {
+    A v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = slab[static_cast<long long>(t + j) * ld + c];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j & 3] += v[j];  // accumulator (t - t0) % 4, rows in order
+  }
+  for (; t < t1; ++t) acc[(t - t0) & 3] += slab[static_cast<long long>(t) * ld + c];
+  return (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+
+template <typename A>
+__device__ __forceinline__ A fused_slab_sum(const A* __restrict__ slab, const int* __restrict__ slot_task_begin,
+                                            A (*red)[kWave], int slot, int ld, int c) {
+  const int lane = threadIdx.x & 63, k = threadIdx.x >> 6;
+  const int tb = slot_task_begin[slot], te = slot_task_begin[slot + 1];
+  const int per = (te - tb + kSplits - 1) / kSplits;
+  const int t0 = tb + k * per;
+  const int t1 = min(te, t0 + per);
+  red[k][lane] = c < ld && t0 < t1 ? fused_split_sum(slab, t0, t1, ld, c) : A(0);
+  __syncthreads();
+  A s = A(0);
+  if (k == 0)
+#pragma unroll
+    for (int q = 0; q < kSplits; ++q) s += red[q][lane];
+  return s;  // meaningful in wave 0
+}
+
+template <typename A>
+__global__ void __launch_bounds__(1024)
+slab_reduce_fused(const A* __restrict__ slab, const int* __restrict__ slot_task_begin, A* __restrict__ G, int ld,
+                  const int* __restrict__ gate) {
+  __shared__ A red[kSplits][kWave];
+  if (gate_closed(gate)) return;
+  const int slot = blockIdx.y, c = blockIdx.x * kWave + (threadIdx.x & 63);
+  const A s = fused_slab_sum(slab, slot_task_begin, red, slot, ld, c);
+  if ((threadIdx.x >> 6) == 0 && c < ld) G[static_cast<long long>(slot) * ld + c] = s;
+}
+
+// The same with the worker's message put (slab_reduce_final_put's protocol: every block releases its
+// columns and counts itself done; the last block writes the tags, releases them and stores the flag).
+template <typename A>
+__global__ void __launch_bounds__(1024)
+slab_reduce_fused_put(const A* __restrict__ slab, const int* __restrict__ slot_task_begin, A* __restrict__ G, int ld,
+                      PutDesc put) {
+  __shared__ A red[kSplits][kWave];
+  __shared__ int s_last, s_live;
+  const int slot = blockIdx.y, c = blockIdx.x * kWave + (threadIdx.x & 63);
+  const bool w0 = (threadIdx.x >> 6) == 0;
+  if (gate_closed(put.gate)) {  // a skipped stale round (launch-uniform): decide the next one's gate
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) put_decide_next_gate(put);
+    return;
+  }
+  if (threadIdx.x == 0) s_live = !(put.abort && __hip_atomic_load(put.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  const A s = fused_slab_sum(slab, slot_task_begin, red, slot, ld, c);  // (its barrier publishes s_live)
+  const bool live = s_live;
+  if (w0 && c < ld) {
+    const long long o = static_cast<long long>(slot) * ld + c;
+    G[o] = s;
+    if (live) static_cast<A*>(put.dst)[o] = s;
+  }
+  if (!live) return;  // block-uniform
+  if (put.tag && w0) {
+    const unsigned long long ws = wave_sum_u64(c < ld ? tag_term(elem_bits(s), c) : 0ull);
+    if (threadIdx.x == 0 && ws) atomicAdd(put.csum + slot, ws);
+  }
+  block_release_system();  // this block's mailbox columns (and checksum adds) are out before its count
+  if (threadIdx.x == 0) {
+    const unsigned int total = gridDim.x * gridDim.y;
+    const unsigned int prev = __hip_atomic_fetch_add(put.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == total - 1;
+    if (s_last) __hip_atomic_store(put.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;  // block-uniform
+  if (put.tag) {
+    for (int r = threadIdx.x; r < static_cast<int>(gridDim.y); r += blockDim.x) {
+      const unsigned long long sum = atomicExch(put.csum + r, 0ull);
+      put.tag[r] = MsgTag{static_cast<unsigned int>(put.value), put.rank, sum};
+    }
+    if (put.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(put.dst)[1] ^= 0x10;  // test hook
+  }
+  block_release_system();  // the tags before the flag
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(put.flag, put.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    put_decide_next_gate(put);
+  }
 }
 
 // Stage 2 fused with the worker's message put (transport.hip's put + signal protocol): every
@@ -1163,10 +1267,19 @@ slab_final_update(const A* __restrict__ part, A* __restrict__ G, int ld, int nsl
 template <typename A>
 static hipError_t slab_reduce_launch(const A* slab, const int* stb, A* part, A* G, int nslots, int ld,
                                      hipStream_t st, const PutDesc* put = nullptr, const int* gate = nullptr) {
-  hipLaunchKernelGGL(slab_reduce_partial<A>, dim3(ceil_div(ld, kWave), nslots, kSplits), dim3(256), 0, st,
-                     slab, stb, part, ld, gate);
   if (put && put->tag && (nslots > kMaxTagRows || !put->csum)) return hipErrorInvalidValue;
   if (put && put->gate != gate) return hipErrorInvalidValue;  // one round, one gate
+  const dim3 fgrid(ceil_div(ld, kWave), nslots);
+  if (g_slab_mode != 0 && !put) {  // both stages in one launch (bitwise the same sums)
+    hipLaunchKernelGGL(slab_reduce_fused<A>, fgrid, dim3(1024), 0, st, slab, stb, G, ld, gate);
+    return hipGetLastError();
+  }
+  if (g_slab_mode == 1 && put) {
+    hipLaunchKernelGGL(slab_reduce_fused_put<A>, fgrid, dim3(1024), 0, st, slab, stb, G, ld, *put);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(slab_reduce_partial<A>, dim3(ceil_div(ld, kWave), nslots, kSplits), dim3(256), 0, st,
+                     slab, stb, part, ld, gate);
   if (put && nslots <= kPutOneSlots && static_cast<long long>(nslots) * ld <= kPutOneElems)
     hipLaunchKernelGGL(slab_reduce_final_put1<A>, dim3(1), dim3(1024), 0, st, part, G, ld, nslots, *put);
   else if (put)
@@ -1242,6 +1355,9 @@ xt_r_tiles(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
 // ---------------------------------------------------------------------------------
 // Host launchers (called from bindings.cpp).
 namespace eh {
+
+void set_slab_reduce_mode(int mode) { g_slab_mode = mode; }
+int slab_reduce_mode() { return g_slab_mode; }
 
 // Wide kernel: 16 elements per thread per row for fp64 (NV = 8), 32 for fp32 (NV = 8) and
 // bf16 (NV = 4); the block size BS (256 / 512) covers ld.  (1024-thread blocks would cap a

@@ -23,6 +23,10 @@ inline long long slab_part_bytes(long long nslots, long long ld, long long acc_b
 
 struct PutDesc;
 struct KernelChoice;
+// Slab reduction form (grad_dense.hip g_slab_mode): 1 fused launches (default), 2 fused plain /
+// two-stage puts, 0 two stages.
+void set_slab_reduce_mode(int mode);
+int slab_reduce_mode();
 // put (optional): fuse the message put + signal into the final slab reduction; put->dst
 // receives the nslots x ld result rows, put->bytes is ignored.
 hipError_t grad_dense_launch(int dtype, int loss, int cpl, const void* segs, const void* tasks,

@@ -289,6 +289,32 @@ def test_dense_grad_interleaved_dispatch_is_bitwise_identical(prec_name, native)
     assert torch.equal(Ga, Gb)
 
 
+@pytest.mark.parametrize("prec_name", ["fp64", "fp32"])
+@pytest.mark.parametrize("d,rows", [(1000, [3000, 2000, 1000]), (3000, [700, 300, 90]), (17000, [300, 200, 50])])
+def test_fused_slab_reduction_is_bitwise_the_two_stages(prec_name, d, rows, native):
+    """slab_reduce_fused (one launch, the default) sums the slab rows in exactly the two-stage order:
+    the messages are bitwise equal to set_slab_reduce_mode(0) (one-wave bundles, wide rows, two-pass)."""
+    C = native
+    prec = get_precision(prec_name)
+    rng = np.random.RandomState(13)
+    parts, _ = _parts(rng, rows, d, prec)
+    msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
+    plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, d)
+    beta = torch.randn(plan.ld, dtype=prec.acc, device=DEV) * 0.05
+    out = {}
+    try:
+        for mode in (0, 1):
+            C.set_slab_reduce_mode(mode)
+            G = plan.out_buffer()[0]
+            plan.run(beta, G)
+            torch.cuda.synchronize()
+            out[mode] = G.clone()
+    finally:
+        C.set_slab_reduce_mode(1)
+    assert torch.equal(out[0], out[1])
+    assert torch.count_nonzero(out[1]) > 0
+
+
 @pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
 def test_dense_grad_staged_is_the_replica_default(prec_name, native):
     """Co-located replicas in bundles of more than 3 default to the LDS-staged bundles for fp64/fp32

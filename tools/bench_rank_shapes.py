@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0, fill: bool = False) -> dict:
+def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0, fill: bool = False,
+        slab_mode: int = 1) -> dict:
     import numpy as np
     import torch
 
@@ -34,6 +35,9 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
     from erasurehead_amd.ops.grad import choose_cpl, choose_kernel
     from erasurehead_amd.parallel.placement import make_shards, place_spread, place_units
 
+    from erasurehead_amd._ext import native
+
+    native().set_slab_reduce_mode(slab_mode)
     prec = get_precision(precision)
     sch = make_scheme("approx", 8, 2, 1_000_000, 6, 0, allow_uneven=True)
     rows = sch.rows_per_partition
@@ -85,7 +89,8 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
     ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
     return {"n_gpus": n_gpus, "precision": precision, "shard": mode, "rank": r, "partitions": len(need),
             "shards": len(mine), "bundle_rows": plan.bundle_rows, "kernel": plan.choice.label(), "ntasks": plan.ntasks,
-            "kernel_ms": ms, "distinct_TBps": plan.distinct_bytes / ms / 1e9, "fill": plan.choice.fill}
+            "kernel_ms": ms, "distinct_TBps": plan.distinct_bytes / ms / 1e9, "fill": plan.choice.fill,
+            "slab_mode": slab_mode}
 
 
 def main():
@@ -99,16 +104,21 @@ def main():
     ap.add_argument("--one", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--rows", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--fill", action="store_true", help="also time even splits over the workgroup slots")
+    ap.add_argument("--ab-slab", action="store_true", help="also time the two-stage slab reduction (mode 0)")
+    ap.add_argument("--slab-mode", type=int, default=1, help=argparse.SUPPRESS)
     a = ap.parse_args()
     if a.one:
-        print(json.dumps(one(a.one, a.precision, a.shard, a.rows, a.fill)), flush=True)
+        print(json.dumps(one(a.one, a.precision, a.shard, a.rows, a.fill, a.slab_mode)), flush=True)
         return 0
     lines = []
     sweeps = [None] + ([int(x) for x in a.rows_list.split(",")] if a.rows_sweep else [])
     for n in [int(x) for x in a.gpus_list.split(",")]:
-        for rows, fill in [(r, False) for r in sweeps] + ([(None, True)] if a.fill else []):
+        variants = ([(r, False, 1) for r in sweeps] + ([(None, True, 1)] if a.fill else [])
+                    + ([(None, False, 0)] if a.ab_slab else []))
+        for rows, fill, mode in variants:
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", str(n), "--precision",
-                                  a.precision, "--shard", a.shard, "--rows", str(rows or 0)] + (["--fill"] if fill else []),
+                                  a.precision, "--shard", a.shard, "--rows", str(rows or 0), "--slab-mode", str(mode)]
+                                 + (["--fill"] if fill else []),
                                  capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print(out.stdout[-2000:], out.stderr[-2000:], file=sys.stderr)

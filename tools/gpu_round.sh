@@ -61,7 +61,7 @@ for s in "${STAGES[@]}"; do
         run 600 "bench_$p.log" $BENCH --precision $p && tail -1 "$OUT/bench_$p.log" > "$OUT/bench_$p.json"
       done ;;
     shapes)
-      run 900 shapes.log python -u tools/bench_rank_shapes.py --fill --out "$OUT/shapes.jsonl"
+      run 900 shapes.log python -u tools/bench_rank_shapes.py --ab-slab --out "$OUT/shapes.jsonl"
       run 300 prof_shape8.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_shape8" -o run -- \
         python tools/bench_rank_shapes.py --one 8 ;;
     sweep)
@@ -122,6 +122,10 @@ for s in "${STAGES[@]}"; do
           done
         done
       done ;;
+    overhead)  # per-round chain on a tiny problem (tools/probes/overhead_tiny.sh), 2 and 8 ranks, arbiter on,
+               # slab reduction forms 1 (fused put) and 2 (two-stage put)
+      run 900 overhead.log env TAG=_r4 NO_BF16=1 MODES=on SLAB="1 2" bash tools/probes/overhead_tiny.sh
+      cp -r gpurun_out/overhead_r4 "$OUT/" ;;
     conv)  # convergence vs wall-clock, every scheme incl. the lazy-drain rows (11 processes on the GPU)
       run 900 conv.log python -u tools/convergence_study.py --out "$OUT/convergence" ;;
     eval)
