@@ -25,11 +25,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def clock_warm(fn, ms: float = 150.0, min_calls: int = 5):
+    """Run fn back to back for ~ms of wall-clock before timing: the GPU idles at ~160 MHz and its clock
+    ramps over ~100 ms of streaming (profiles/round3/clocks); a 0.03-0.3 ms kernel timed after 5
+    warm-up calls was measured on the ramp."""
+    import time
+
+    import torch
+
+    t0, n = time.perf_counter(), 0
+    while n < min_calls or (time.perf_counter() - t0) * 1e3 < ms:
+        fn()
+        n += 1
+        if n % 8 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+
+
 def _time(fn, reps=50, warm=5):
     import torch
 
-    for _ in range(warm):
-        fn()
+    clock_warm(fn, min_calls=warm)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for a, b in evs:
         a.record()
