@@ -812,7 +812,7 @@ grad_dense_fused_pair(const Segment* __restrict__ segs, const Task* __restrict__
 // row is loaded once and every replica computes its own dot product, residual (own coefficient) and
 // gradient from the registers, so the replicated messages cost one HBM stream (the interleaved
 // dispatch re-read them through L2 at ~4 TB/s, profiles/round3/choices).
-template <typename T, typename A, int NV, int BS, int LOSS, int R>
+template <typename T, typename A, int NV, int BS, int LOSS, int R, bool PF = false>
 __global__ void __launch_bounds__(BS)
 grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
                 const A* __restrict__ beta, A* __restrict__ slab, int ld, const int* __restrict__ gate) {
@@ -848,22 +848,8 @@ grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks
     }
   }
   int buf = 0;
-  for (int r = lead.row_begin; r < lead.row_end; r += 2) {
-    const bool two = r + 1 < lead.row_end;
-    const T* x0 = X + static_cast<long long>(r) * ld;
-    const T* x1 = X + static_cast<long long>(two ? r + 1 : r) * ld;
-    A a0[NV][VN], a1[NV][VN];
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int c0 = (j * BS + tid) * VN;
-      if (valid[j]) {
-        Vec16<T>::template load<A, true>(x0 + c0, a0[j]);
-        Vec16<T>::template load<A, true>(x1 + c0, a1[j]);
-      } else {
-#pragma unroll
-        for (int v = 0; v < VN; ++v) { a0[j][v] = A(0); a1[j][v] = A(0); }
-      }
-    }
+  // one row pair: R dot products each, cross-wave sums through LDS (one barrier), residuals, gradients
+  auto pair = [&](const A (&a0)[NV][VN], const A (&a1)[NV][VN], A y0, A y1, bool two) {
     A z0[R], z1[R];
 #pragma unroll
     for (int q = 0; q < R; ++q) {
@@ -890,7 +876,6 @@ grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks
       }
     }
     __syncthreads();
-    const A y0 = Y[r], y1 = two ? Y[r + 1] : A(0);
     A r0[R], r1[R];
     if constexpr (R == 1) {
       A s0 = A(0), s1 = A(0);
@@ -929,6 +914,71 @@ grad_dense_wide(const Segment* __restrict__ segs, const Task* __restrict__ tasks
       for (int v = 0; v < VN; ++v)
 #pragma unroll
         for (int q = 0; q < R; ++q) g[q][j][v] = fma(r1[q], a1[j][v], fma(r0[q], a0[j][v], g[q][j][v]));
+  };
+  if constexpr (PF) {
+    // The next pair's loads are issued before this pair's reductions and barrier: with one workgroup
+    // per CU (the 512-thread replica rows) nothing else keeps the CU's loads in flight across the
+    // barrier.  Buffer loads over the row (range-checked: columns past ld read zeros, no branches)
+    // are unconditional -- past the bundle the last pair is read again -- so each step waits for its
+    // own pair only.
+    using Rw = typename Vec16<T>::raw;
+    const int rowbytes = ld * static_cast<int>(sizeof(T));
+    auto ldrow = [&](Rw (&x)[NV], int r) {
+      const auto rs = make_rsrc(X + static_cast<long long>(r) * ld, rowbytes);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) x[j] = buf_load16<Rw>(rs, (j * BS + tid) * VN * static_cast<int>(sizeof(T)));
+    };
+    const int rb = lead.row_begin, re = lead.row_end;
+    // labels through a descriptor too, issued ahead of the next pair's rows (a flat load issued after
+    // them would make its wait drain the prefetch)
+    const auto yrs = make_rsrc(Y + rb, (re - rb) * static_cast<int>(sizeof(A)));
+    Rw xa[NV], xb[NV];
+    if (rb < re) {
+      ldrow(xa, rb);
+      ldrow(xb, min(rb + 1, re - 1));
+    }
+    for (int r = rb; r < re; r += 2) {
+      const bool two = r + 1 < re;
+      const int rn = r + 2 < re ? r + 2 : r;
+      const A y0 = buf_load_scalar<A>(yrs, (r - rb) * static_cast<int>(sizeof(A)));
+      const A y1 = buf_load_scalar<A>(yrs, (two ? r + 1 - rb : r - rb) * static_cast<int>(sizeof(A)));
+      Rw na[NV], nb[NV];
+      ldrow(na, rn);
+      ldrow(nb, min(rn + 1, re - 1));
+      A a0[NV][VN], a1[NV][VN];
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+#pragma unroll
+        for (int v = 0; v < VN; ++v) {
+          a0[j][v] = Vec16<T>::template elem<A>(xa[j], v);
+          a1[j][v] = two ? Vec16<T>::template elem<A>(xb[j], v) : A(0);
+        }
+      pair(a0, a1, y0, two ? y1 : A(0), two);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        xa[j] = na[j];
+        xb[j] = nb[j];
+      }
+    }
+  } else {
+    for (int r = lead.row_begin; r < lead.row_end; r += 2) {
+      const bool two = r + 1 < lead.row_end;
+      const T* x0 = X + static_cast<long long>(r) * ld;
+      const T* x1 = X + static_cast<long long>(two ? r + 1 : r) * ld;
+      A a0[NV][VN], a1[NV][VN];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int c0 = (j * BS + tid) * VN;
+        if (valid[j]) {
+          Vec16<T>::template load<A, true>(x0 + c0, a0[j]);
+          Vec16<T>::template load<A, true>(x1 + c0, a1[j]);
+        } else {
+#pragma unroll
+          for (int v = 0; v < VN; ++v) { a0[j][v] = A(0); a1[j][v] = A(0); }
+        }
+      }
+      pair(a0, a1, Y[r], two ? Y[r + 1] : A(0), two);
+    }
   }
 #pragma unroll
   for (int q = 0; q < R; ++q) {
@@ -1388,7 +1438,12 @@ static hipError_t launch_wide(int bs, int R, const Segment* segs, const Task* ta
     // AGPR spills, 1 wave per SIMD); at 512 threads the tiles halve (150 VGPRs) and a CU keeps 8 waves
     // of the bundle in flight instead of 4.  One such workgroup is resident per CU
     // (ops/grad.py wide_slots_per_cu).
-    if (R == 2) EH_WIDE(NV / 2, 512, 2); else EH_WIDE(NV / 2, 512, 3);
+    if (R == 2)
+      hipLaunchKernelGGL((grad_dense_wide<T, A, NV / 2, 512, LOSS, 2, true>), grid, dim3(512), 0, st, segs, tasks, beta,
+                         slab, ld, gate);
+    else
+      hipLaunchKernelGGL((grad_dense_wide<T, A, NV / 2, 512, LOSS, 3, true>), grid, dim3(512), 0, st, segs, tasks, beta,
+                         slab, ld, gate);
   } else if (bs == 256) {
     if (R == 1) EH_WIDE_NV(256, 1); else if (R == 2) EH_WIDE_NV(256, 2); else EH_WIDE_NV(256, 3);
   } else if (bs == 512 && R == 1) {  // (replica bundles of 512-thread rows would spill: R * 16+ accumulators)
