@@ -39,34 +39,47 @@ constexpr int kTileEntries = 512;  // one wave: 64 lanes x 8 entries
 constexpr int kSpanHead = 1, kSpanTail = 2;
 
 // ---- pass 1: rows -------------------------------------------------------------------------------
+// A row's fields are processed KB at a time: the KB index loads (HBM) of the next batch are issued
+// before the KB beta gathers (L2) of this one, so a thread waits about one HBM and one L2 latency per
+// batch instead of per four fields (covtype's 55 fields: 14 dependent HBM + L2 steps per thread were
+// 38 us, profiles/round4/r4g).  Past the last field the loads are clamped to it and masked out; the
+// sums stay in four chains z[k % 4] in field order (the old order, bitwise).
 template <typename A, int LOSS, bool IDX16, bool VALS>
 __global__ void __launch_bounds__(256) ell_rows(const SparseArgs a, const A* __restrict__ beta, const int* gate) {
+  constexpr int KB = 16;
   if (gate_closed(gate)) return;
   const long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (row >= a.nrows) return;
   const long long n = a.nrows;
+  const int m = a.m;
   const A* __restrict__ vals = static_cast<const A*>(a.vals);
-  A z[4] = {A(0), A(0), A(0), A(0)};  // four independent gather chains
-  int k = 0;
-  auto col = [&](int kk) -> int {
+  A z[4] = {A(0), A(0), A(0), A(0)};
+  auto idx = [&](int kk) -> int {
     if constexpr (IDX16)
-      return a.lo[kk] + static_cast<int>(__builtin_nontemporal_load(static_cast<const unsigned short*>(a.ell_idx) +
-                                                                     static_cast<long long>(kk) * n + row));
+      return static_cast<int>(__builtin_nontemporal_load(static_cast<const unsigned short*>(a.ell_idx) +
+                                                         static_cast<long long>(kk) * n + row));
     else
       return __builtin_nontemporal_load(static_cast<const int*>(a.ell_idx) + static_cast<long long>(kk) * n + row);
   };
-  for (; k + 3 < a.m; k += 4) {
-    int c[4];
-    A v[4];
+  int cn[KB];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      c[u] = col(k + u);
-      v[u] = VALS ? vals[static_cast<long long>(k + u) * n + row] : A(1);
+  for (int u = 0; u < KB; ++u) cn[u] = idx(min(u, m - 1));
+  for (int k0 = 0; k0 < m; k0 += KB) {
+    int c[KB];
+#pragma unroll
+    for (int u = 0; u < KB; ++u) c[u] = (IDX16 ? a.lo[min(k0 + u, m - 1)] : 0) + cn[u];
+#pragma unroll
+    for (int u = 0; u < KB; ++u) cn[u] = idx(min(k0 + KB + u, m - 1));  // next batch in flight
+    A bv[KB], v[KB];
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      bv[u] = beta[c[u]];
+      v[u] = VALS ? vals[static_cast<long long>(min(k0 + u, m - 1)) * n + row] : A(1);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) z[u] = fma(v[u], beta[c[u]], z[u]);
+    for (int u = 0; u < KB; ++u)
+      if (k0 + u < m) z[u & 3] = fma(v[u], bv[u], z[u & 3]);
   }
-  for (; k < a.m; ++k) z[k & 3] = fma(VALS ? vals[static_cast<long long>(k) * n + row] : A(1), beta[col(k)], z[k & 3]);
   const A zz = (z[0] + z[1]) + (z[2] + z[3]);
   static_cast<A*>(a.u)[row] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[row], A(1));
 }
@@ -101,6 +114,41 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
   const int n = min(kTileEntries, nnz_p - base);
   const int* __restrict__ cp = a.col_ptr + static_cast<long long>(p) * (a.d + 1);
   int* __restrict__ cw = cnt[w];
+  // 0. this lane's 8 entries first -- row indices, values, the gathered residuals -- through buffer
+  //    descriptors: they count in vmcnt only, so the LDS waits of the boundary walk below do not wait
+  //    for them (pointer loads from the argument struct are flat loads, which count in lgkmcnt too),
+  //    and the tile's chain is one HBM + one L2 latency beside the walk instead of after it.  Entries
+  //    past n are the partition's zero padding (row 0), masked below.
+  const long long e0 = a.part_entry0[p] + base + 8 * lane;
+  const long long r0 = a.part_row0[p];
+  int rows[8];
+  if constexpr (ROW16) {
+    const auto rs = make_rsrc(static_cast<const unsigned short*>(a.crow) + a.part_entry0[p] + base, 2 * kTileEntries);
+    const uint4 r4 = buf_load16<uint4>(rs, 16 * lane);
+    const unsigned int rw[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      rows[2 * i] = static_cast<int>(rw[i] & 0xffffu);
+      rows[2 * i + 1] = static_cast<int>(rw[i] >> 16);
+    }
+  } else {
+    const auto rs = make_rsrc(static_cast<const int*>(a.crow) + a.part_entry0[p] + base, 4 * kTileEntries);
+    const int4 x = buf_load16<int4>(rs, 32 * lane), y = buf_load16<int4>(rs, 32 * lane + 16);
+    rows[0] = x.x, rows[1] = x.y, rows[2] = x.z, rows[3] = x.w;
+    rows[4] = y.x, rows[5] = y.y, rows[6] = y.z, rows[7] = y.w;
+  }
+  const long long ubytes = (a.nrows - r0) * static_cast<long long>(sizeof(A));
+  const auto urs = make_rsrc(static_cast<const A*>(a.u) + r0, static_cast<int>(min(ubytes, static_cast<long long>(INT_MAX))));
+  A v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = buf_load_scalar<A>(urs, rows[i] * static_cast<int>(sizeof(A)));
+  A cv[8];
+  if constexpr (VALS) {
+    const auto vrs = make_rsrc(static_cast<const A*>(a.cvals) + a.part_entry0[p] + base,
+                               kTileEntries * static_cast<int>(sizeof(A)));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cv[i] = buf_load_scalar<A>(vrs, (8 * lane + i) * static_cast<int>(sizeof(A)));
+  }
   // 1. column boundaries inside the tile: cnt[q] = number of columns c > c0 starting at base + q
   //    (empty columns stack on the next non-empty one's start); integer LDS adds, order-free
 #pragma unroll
@@ -130,32 +178,15 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
   int key[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) key[i] = c0 + before + cl[i];
-  // 3. this lane's entries: rows (one 16- or 32-byte load), values, gathered residuals
-  const long long e0 = a.part_entry0[p] + base + 8 * lane;
-  const A* __restrict__ up = static_cast<const A*>(a.u) + a.part_row0[p];
-  A v[8];
-  int rows[8];
-  if constexpr (ROW16) {
-    const uint4 r4 = *reinterpret_cast<const uint4*>(static_cast<const unsigned short*>(a.crow) + e0);
-    const unsigned int rw[4] = {r4.x, r4.y, r4.z, r4.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      rows[2 * i] = static_cast<int>(rw[i] & 0xffffu);
-      rows[2 * i + 1] = static_cast<int>(rw[i] >> 16);
-    }
-  } else {
-    const int4* r4 = reinterpret_cast<const int4*>(static_cast<const int*>(a.crow) + e0);
-    const int4 x = r4[0], y = r4[1];
-    rows[0] = x.x, rows[1] = x.y, rows[2] = x.z, rows[3] = x.w;
-    rows[4] = y.x, rows[5] = y.y, rows[6] = y.z, rows[7] = y.w;
-  }
+  // 3. mask the padding
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const bool ok = 8 * lane + i < n;
-    A x = ok ? up[rows[i]] : A(0);
-    if constexpr (VALS) x *= ok ? static_cast<const A*>(a.cvals)[e0 + i] : A(0);
+    A x = ok ? v[i] : A(0);
+    if constexpr (VALS) x *= ok ? cv[i] : A(0);
     v[i] = x;
   }
+  (void)e0;
   // 4. segmented sums: sequential inside the lane, then over the lanes
   A s[8];
   s[0] = v[0];
