@@ -1492,9 +1492,9 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
       return grad_mfma_launch(LOSS, segs, tasks, ntasks, k.replicas, beta, slab, ld, st, gate);
     return hipErrorInvalidValue;
   }
-  if (k.kind == kGradWide || cpl >= 256)
-    return launch_wide<T, A, LOSS>(cpl, k.kind == kGradWide ? k.replicas : 1, segs, tasks, ntasks, beta, slab, ld, st,
-                                   gate);
+  if (k.kind == kGradWide || cpl >= 256)  // (rows of 32 columns per lane run 256-thread wide rows too)
+    return launch_wide<T, A, LOSS>(cpl >= 256 ? cpl : 256, k.kind == kGradWide ? k.replicas : 1, segs, tasks, ntasks,
+                                   beta, slab, ld, st, gate);
   const int R = k.replicas;
   const bool bundled = k.kind == kGradStaged || k.kind == kGradMulti;
   if (bundled && (R < 1 || ntasks % R != 0)) return hipErrorInvalidValue;

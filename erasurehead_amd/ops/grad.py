@@ -411,8 +411,8 @@ class DenseGradPlan:
             raise ValueError("one-wave bundles hold at most 3 fp64/fp32 replicas of d <= 1024")
         if c.kind == "multi" and c.pair and (self.cpl > 8 or not c.fold):
             raise ValueError("pair-row one-wave bundles need <= 8 columns per lane and the fold")
-        if c.kind == "wide" and c.replicas > 1 and (self.cpl != 256 or c.replicas > 3):
-            raise ValueError("wide-row bundles are 256-thread rows of at most 3 replicas")
+        if c.kind == "wide" and c.replicas > 1 and (self.cpl not in (32, 256) or c.replicas > 3):
+            raise ValueError("wide-row bundles are 256-thread rows (32 or 256 columns per lane) of at most 3 replicas")
         if c.kind == "mfma" and (prec.code != 2 or self.ld > 1024 or self.ld % 8 or self.max_rep > 16):
             raise ValueError("MFMA bundles are bf16, d <= 1024, d % 8 == 0, at most 16 replicas")
         self.bundle_rows = c.bundle_rows if c.bundled else 0
