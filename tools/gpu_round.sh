@@ -68,6 +68,9 @@ for s in "${STAGES[@]}"; do
       run 1100 sweep.log python -u tools/bench_kernels.py --only sweep --out "$OUT/sweep.jsonl" ;;
     wide)  # the off-headline widths only (d = 2048 / 4096, fp64 and fp32)
       run 600 wide.log python -u tools/bench_kernels.py --only sweep --ds 2048,4096 --out "$OUT/wide.jsonl" ;;
+    choices)  # every valid kernel choice at the d = 2048 replica shapes (CHOICE_SHAPES overrides)
+      run 900 choices.log python -u tools/bench_kernels.py --only choices \
+        --shapes "${CHOICE_SHAPES:-fp64:2048:1e6,fp32:2048:1e6,fp64:2048:1e5,fp32:2048:1e5}" --out "$OUT/choices.jsonl" ;;
     sparse)  # sparse gradients at the real-data shapes, then their kernel stats
       run 600 sparse.log python -u tools/bench_kernels.py --only sparse --out "$OUT/sparse.jsonl"
       run 600 prof_sparse.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_sparse" -o run -- \
