@@ -50,7 +50,12 @@ def test_rccl_comm_two_processes_one_gpu_named_outcome(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(HERE, "rccl_dup_gpu.py")]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
-    res = [json.loads(l.split("RCCL_RESULT ", 1)[1]) for l in r.stdout.splitlines() if "RCCL_RESULT " in l]
+    # the two ranks share the launcher's stdout: their lines can interleave, so decode each JSON
+    # object where its marker starts
+    dec, res, i = json.JSONDecoder(), [], r.stdout.find("RCCL_RESULT ")
+    while i >= 0:
+        res.append(dec.raw_decode(r.stdout, i + len("RCCL_RESULT "))[0])
+        i = r.stdout.find("RCCL_RESULT ", i + 1)
     assert len(res) == 2, r.stdout[-3000:] + r.stderr[-3000:]
     for x in res:
         if "refused" in x:
