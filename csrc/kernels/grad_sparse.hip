@@ -84,6 +84,48 @@ __global__ void __launch_bounds__(256) ell_rows(const SparseArgs a, const A* __r
   static_cast<A*>(a.u)[row] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[row], A(1));
 }
 
+// beta staged in LDS when it fits (d * sizeof(A) <= kEllLdsBytes: covtype's 15509 columns are 124 KB
+// fp64).  Gathered from global memory, each 8-byte beta read pulled a 128-byte L2 line into a 32 KB L1
+// that the fields' windows (55 per row) keep thrashing: 21.8M gathers, ~2.8 GB of L2 -> L1 traffic,
+// 38-41 us (profiles/round4/r4g, r4i).  From LDS they cost a few cycles.  One 1024-thread workgroup per
+// CU (the LDS copy of beta is per workgroup), rows strided over the grid.
+constexpr int kEllLdsBytes = 152 * 1024;
+
+template <typename A, int LOSS, bool IDX16, bool VALS>
+__global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A* __restrict__ beta, const int* gate) {
+  constexpr int KB = 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ell_lds[];
+  A* sb = reinterpret_cast<A*>(ell_lds);
+  if (gate_closed(gate)) return;
+  for (int c = threadIdx.x; c < a.d; c += blockDim.x) sb[c] = beta[c];
+  __syncthreads();
+  const long long n = a.nrows;
+  const int m = a.m;
+  const A* __restrict__ vals = static_cast<const A*>(a.vals);
+  const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
+  for (long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; row < n; row += stride) {
+    A z[4] = {A(0), A(0), A(0), A(0)};
+    auto idx = [&](int kk) -> int {
+      if constexpr (IDX16)
+        return static_cast<int>(__builtin_nontemporal_load(static_cast<const unsigned short*>(a.ell_idx) +
+                                                           static_cast<long long>(kk) * n + row));
+      else
+        return __builtin_nontemporal_load(static_cast<const int*>(a.ell_idx) + static_cast<long long>(kk) * n + row);
+    };
+    for (int k0 = 0; k0 < m; k0 += KB) {
+      int c[KB];
+#pragma unroll
+      for (int u = 0; u < KB; ++u) c[u] = (IDX16 ? a.lo[min(k0 + u, m - 1)] : 0) + idx(min(k0 + u, m - 1));
+#pragma unroll
+      for (int u = 0; u < KB; ++u)
+        if (k0 + u < m)
+          z[u & 3] = fma(VALS ? vals[static_cast<long long>(k0 + u) * n + row] : A(1), sb[c[u]], z[u & 3]);
+    }
+    const A zz = (z[0] + z[1]) + (z[2] + z[3]);
+    static_cast<A*>(a.u)[row] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[row], A(1));
+  }
+}
+
 template <typename A, int LOSS, int G>
 __global__ void __launch_bounds__(256) csr_rows(const SparseArgs a, const A* __restrict__ beta, const int* gate) {
   if (gate_closed(gate)) return;
@@ -257,7 +299,41 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
   if (a.nrows < 0 || a.ntiles < 0 || a.d <= 0 || a.ld < a.d || !a.Gb || !a.u) return hipErrorInvalidValue;
   const dim3 block(256);
   if (a.nrows > 0) {
-    if (a.ell) {
+    const size_t blds = static_cast<size_t>(a.d) * (dtype == 0 ? 8 : 4);
+    if (a.ell && blds <= static_cast<size_t>(kEllLdsBytes)) {
+      static int cus = 0;
+      if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+          cus = 256;
+      }
+      const dim3 grid(static_cast<unsigned>(std::min<long long>(cus, (a.nrows + 1023) / 1024)));
+      auto go = [&](const void* kern) -> hipError_t {
+        return blds > 64 * 1024 ? hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      static_cast<int>(blds))
+                                : hipSuccess;
+      };
+#define EH_ELLL(A_, L_, I_, V_)                                                                                  \
+  {                                                                                                              \
+    const hipError_t e = go(reinterpret_cast<const void*>(ell_rows_lds<A_, L_, I_, V_>));                        \
+    if (e != hipSuccess) return e;                                                                               \
+    hipLaunchKernelGGL((ell_rows_lds<A_, L_, I_, V_>), grid, dim3(1024), blds, st, a, (const A_*)beta, gate);   \
+  }
+#define EH_ELLV(A_, L_)                                              \
+  if (a.idx16) {                                                     \
+    if (a.vals) EH_ELLL(A_, L_, true, true) else EH_ELLL(A_, L_, true, false)      \
+  } else {                                                           \
+    if (a.vals) EH_ELLL(A_, L_, false, true) else EH_ELLL(A_, L_, false, false)    \
+  }
+      if (dtype == 0) {
+        if (loss == kLogistic) { EH_ELLV(double, kLogistic) } else { EH_ELLV(double, kLeastSquares) }
+      } else {
+        if (loss == kLogistic) { EH_ELLV(float, kLogistic) } else { EH_ELLV(float, kLeastSquares) }
+      }
+#undef EH_ELLV
+#undef EH_ELLL
+    } else if (a.ell) {
       const dim3 grid(static_cast<unsigned>((a.nrows + 255) / 256));
 #define EH_ELL(A_, L_)                                                                                          \
   if (a.idx16) {                                                                                                \
