@@ -217,7 +217,10 @@ def staged_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, fp32: bool = Fals
     fp64 1e5 256: 0.326 (128: 0.334-0.376); d = 1000 ranks (round 2, profiles/round2/s1_shapes):
     128 at N = 8 (0.238 vs 0.415 ms at 512)."""
     if distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus:
-        return 384 if fp32 and cpl >= 32 else 512
+        # fp32 rows of 32 columns per lane (d = 2048): 1024 rows 1.223 ms vs 384 1.402 with the clock
+        # warmed before every candidate (profiles/round4/r4i/choices.jsonl; the round-3 sweep that
+        # picked 384 timed the first candidates on the clock ramp)
+        return 1024 if fp32 and cpl >= 32 else 512
     return 256 if cpl >= 32 and not fp32 else 128  # 16 KB rows (fp64 d > 1024); fp32 2048 at 1e5: 128 rows 0.169 vs 256 0.194 ms
 
 
@@ -243,7 +246,8 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
         ms, 4 replicas at d = 1000 fp64 1.532-1.542 vs 1.668; one-wave bundles of 4 replicas need
         276 registers, 1 wave per SIMD, and measured 1.76 ms: profiles/round3/choices_nt/frc4.jsonl);
       * bf16 replicas: MFMA bundles (d <= 1024, d % 8 == 0), else the fused kernel interleaved;
-      * 2048 < d (fp64, 4096 fp32): the wide kernel; beyond 8192 / 16384 or cpl unknown: two passes.
+      * 2048 < d (fp64, 4096 fp32): the wide kernel; fp64 replicas at 1024 < d <= 2048 too (its half-width
+        instance); beyond 8192 / 16384 or cpl unknown: two passes.
     """
     if cpl is None:
         return KernelChoice("twopass")
@@ -270,6 +274,13 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
         return KernelChoice("multi", replicas=3, bundle_rows=pair_bundle_rows(distinct_rows, n_cus, prec_code == 1, cpl),
                             fold=True,
                             pair=True)
+    if prec_code == 0 and cpl == 32 and max_rep <= 3:
+        # fp64 rows of 32 columns per lane (1024 < d <= 2048): 256-thread wide-row bundles (the
+        # half-width instance) over the LDS-staged pair form: d = 2048 1e6 rows 2.466 vs 2.719 ms, 1e5
+        # rows 0.268 vs 0.335 (profiles/round4/r4i/choices.jsonl)
+        return KernelChoice("wide", replicas=max_rep,
+                            bundle_rows=wide_bundle_rows(distinct_rows, n_cus, part_rows,
+                                                         wide_slots_per_cu(prec_code, ld, max_rep)))
     if cpl <= 16 and max_rep in (2, 3):
         return KernelChoice("multi", replicas=max_rep,
                             bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl, part_rows),

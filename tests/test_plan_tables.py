@@ -94,10 +94,12 @@ def test_kernel_selection_table():
         KernelChoice("multi", replicas=1, bundle_rows=1024, fold=True),
         KernelChoice("multi", replicas=1, bundle_rows=512, fold=True), KernelChoice("fused", rows=1)]
     assert pick(0, 256, 1, 1_000_000) == KernelChoice("fused", rows=2)  # narrow distinct rows: fused
-    # wide rows: d = 2048 fp64 (32 columns per lane) stays on staged bundles (pair form); 4096 takes the wide kernel
-    assert pick(0, 2048, 3, 1_000_000) == KernelChoice("staged", replicas=3, bundle_rows=512, pair=True)
-    assert pick(1, 2048, 3, 1_000_000) == KernelChoice("staged", replicas=3, bundle_rows=384, pair=True)
-    assert pick(0, 2048, 3, 100_000) == KernelChoice("staged", replicas=3, bundle_rows=256, pair=True, wpr=1)
+    # d = 2048: fp64 replicas on 256-thread wide-row bundles, fp32 on LDS-staged bundles (pair form,
+    # 1024 rows in the long stream); 4096 takes the wide kernel
+    assert pick(0, 2048, 3, 1_000_000) == KernelChoice("wide", replicas=3, bundle_rows=1968)
+    assert pick(1, 2048, 3, 1_000_000) == KernelChoice("staged", replicas=3, bundle_rows=1024, pair=True)
+    assert pick(0, 2048, 3, 100_000) == KernelChoice("wide", replicas=3, bundle_rows=208)
+    assert pick(1, 2048, 3, 100_000) == KernelChoice("staged", replicas=3, bundle_rows=128, pair=True, wpr=1)
     # fp64 full-width replica rows run 512-thread workgroups, one resident per CU (wide_slots_per_cu)
     assert pick(0, 4096, 3, 1_000_000) == KernelChoice("wide", replicas=3, bundle_rows=3920)
     assert pick(1, 4096, 2, 100_000) == KernelChoice("wide", replicas=2, bundle_rows=208)
