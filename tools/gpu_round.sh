@@ -48,7 +48,12 @@ for s in "${STAGES[@]}"; do
   case "$s" in
     tests)
       # TESTS="files..." narrows the run (default: every GPU test)
-      run 1500 pytest.log python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 120 --timeout-method thread
+      # KEXPR="expr" selects tests by keyword expression (pytest -k)
+      if [ -n "${KEXPR:-}" ]; then
+        run 1500 pytest.log python -u -m pytest ${TESTS:-tests} -m gpu -k "$KEXPR" -x -v --timeout 120 --timeout-method thread
+      else
+        run 1500 pytest.log python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 120 --timeout-method thread
+      fi
       tail -3 "$OUT/pytest.log" ;;
     smoke)
       run 300 smoke.log python -c 'import __graft_entry__ as g; g.build(); g.smoke(); print("smoke ok")' ;;
