@@ -143,26 +143,20 @@ __global__ void __launch_bounds__(256) csr_rows(const SparseArgs a, const A* __r
 }
 
 // ---- pass 2: CSC tiles, one wave per 512-entry tile ---------------------------------------------
-template <typename A, bool ROW16, bool VALS>
-__global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* gate) {
-  __shared__ int cnt[4][kTileEntries];
-  if (gate_closed(gate)) return;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int t = blockIdx.x * 4 + w;
-  if (t >= a.ntiles) return;  // wave-uniform; only wave barriers below
+// The tile body: `gather(rows, v)` fills v[i] = u[rows[i]] (sub-block relative rows) -- from global
+// memory through a buffer descriptor, or from the workgroup's LDS copy of the sub-block's residuals.
+template <typename A, bool ROW16, bool VALS, typename Gather>
+__device__ __forceinline__ void tile_pass(const SparseArgs& a, int t, int* __restrict__ cw, Gather gather) {
+  const int lane = threadIdx.x & 63;
   const int4 td = a.tiles[t];
   const int p = td.x, base = td.y, c0 = td.z, flags = td.w;
   const int nnz_p = a.part_nnz[p];
   const int n = min(kTileEntries, nnz_p - base);
   const int* __restrict__ cp = a.col_ptr + static_cast<long long>(p) * (a.d + 1);
-  int* __restrict__ cw = cnt[w];
   // 0. this lane's 8 entries first -- row indices, values, the gathered residuals -- through buffer
-  //    descriptors: they count in vmcnt only, so the LDS waits of the boundary walk below do not wait
-  //    for them (pointer loads from the argument struct are flat loads, which count in lgkmcnt too),
-  //    and the tile's chain is one HBM + one L2 latency beside the walk instead of after it.  Entries
-  //    past n are the partition's zero padding (row 0), masked below.
-  const long long e0 = a.part_entry0[p] + base + 8 * lane;
-  const long long r0 = a.part_row0[p];
+  //    descriptors (vmcnt only: the LDS waits of the boundary walk below do not wait for them;
+  //    pointer loads from the argument struct are flat loads, which count in lgkmcnt too).  Entries
+  //    past n are the sub-block's zero padding (row 0), masked below.
   int rows[8];
   if constexpr (ROW16) {
     const auto rs = make_rsrc(static_cast<const unsigned short*>(a.crow) + a.part_entry0[p] + base, 2 * kTileEntries);
@@ -179,11 +173,6 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
     rows[0] = x.x, rows[1] = x.y, rows[2] = x.z, rows[3] = x.w;
     rows[4] = y.x, rows[5] = y.y, rows[6] = y.z, rows[7] = y.w;
   }
-  const long long ubytes = (a.nrows - r0) * static_cast<long long>(sizeof(A));
-  const auto urs = make_rsrc(static_cast<const A*>(a.u) + r0, static_cast<int>(min(ubytes, static_cast<long long>(INT_MAX))));
-  A v[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = buf_load_scalar<A>(urs, rows[i] * static_cast<int>(sizeof(A)));
   A cv[8];
   if constexpr (VALS) {
     const auto vrs = make_rsrc(static_cast<const A*>(a.cvals) + a.part_entry0[p] + base,
@@ -191,6 +180,8 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
 #pragma unroll
     for (int i = 0; i < 8; ++i) cv[i] = buf_load_scalar<A>(vrs, (8 * lane + i) * static_cast<int>(sizeof(A)));
   }
+  A v[8];
+  gather(p, rows, v);
   // 1. column boundaries inside the tile: cnt[q] = number of columns c > c0 starting at base + q
   //    (empty columns stack on the next non-empty one's start); integer LDS adds, order-free
 #pragma unroll
@@ -213,8 +204,8 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
   int incl = run;  // wave inclusive scan of the lane totals
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const int v = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += v;
+    const int vv = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += vv;
   }
   const int before = incl - run;
   int key[8];
@@ -228,7 +219,6 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
     if constexpr (VALS) x *= ok ? cv[i] : A(0);
     v[i] = x;
   }
-  (void)e0;
   // 4. segmented sums: sequential inside the lane, then over the lanes
   A s[8];
   s[0] = v[0];
@@ -251,7 +241,7 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
   const A prev_run = __shfl_up(b, 1, 64);
   const A carry = (lane > 0 && prev_last == key[0]) ? prev_run : A(0);
   const int next_first = __shfl_down(key[0], 1, 64);
-  A* __restrict__ gout = static_cast<A*>(a.Gb) + static_cast<long long>(p) * a.ld;
+  A* __restrict__ gout = static_cast<A*>(a.Gs) + static_cast<long long>(p) * a.ld;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int q = 8 * lane + i;
@@ -265,6 +255,58 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
     if (has_tail) static_cast<A*>(a.tail)[t] = val;
     if (!has_head && !has_tail) gout[key[i]] = val;
   }
+}
+
+// One wave per tile, residuals gathered from global memory (one partition = one sub-block).
+template <typename A, bool ROW16, bool VALS>
+__global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* gate) {
+  __shared__ int cnt[4][kTileEntries];
+  if (gate_closed(gate)) return;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= a.ntiles) return;  // wave-uniform; only wave barriers below
+  tile_pass<A, ROW16, VALS>(a, t, cnt[threadIdx.x >> 6], [&](int p, const int (&rows)[8], A (&v)[8]) {
+    const long long r0 = a.part_row0[p];
+    const long long ubytes = (a.nrows - r0) * static_cast<long long>(sizeof(A));
+    const auto urs = make_rsrc(static_cast<const A*>(a.u) + r0, static_cast<int>(min(ubytes, static_cast<long long>(INT_MAX))));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = buf_load_scalar<A>(urs, rows[i] * static_cast<int>(sizeof(A)));
+  });
+}
+
+// Row-blocked column pass: a 1024-thread workgroup takes up to 16 tiles of ONE sub-block (a.wg) and
+// first copies that sub-block's residuals into LDS (coalesced), so every gather is an LDS read.  From
+// global memory each 8-byte gather pulled a 128-byte L2 line into L1 with no reuse (rows of a column
+// are spread over the partition): covtype's 21.8M gathers moved ~2.8 GB L2 -> L1, 88-92 us
+// (profiles/round4/r4g, r4i).
+constexpr int kWgTiles = 16;
+template <typename A, bool ROW16, bool VALS>
+__global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const int* gate) {
+  __shared__ int cnt[kWgTiles][kTileEntries];
+  extern __shared__ __attribute__((aligned(16))) unsigned char usub_raw[];
+  A* su = reinterpret_cast<A*>(usub_raw);
+  if (gate_closed(gate)) return;
+  const int4 wd = a.wg[blockIdx.x];  // (sub-block, first tile, tiles, rows)
+  const A* __restrict__ ug = static_cast<const A*>(a.u) + a.part_row0[wd.x];
+  for (int i = threadIdx.x; i < wd.w; i += blockDim.x) su[i] = ug[i];
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  if (w >= wd.z) return;  // wave-uniform; no block barrier after this
+  tile_pass<A, ROW16, VALS>(a, wd.y + w, cnt[w], [&](int, const int (&rows)[8], A (&v)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = su[min(rows[i], wd.w - 1)];  // (padding rows are 0; clamp an empty sub-block)
+  });
+}
+
+// Sub-block sums added per partition in sub-block order: Gb[j][c] = sum_s Gs[s][c].
+template <typename A>
+__global__ void __launch_bounds__(256) sub_reduce(const SparseArgs a, const int* gate) {
+  if (gate_closed(gate)) return;
+  const int j = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.ld) return;
+  const A* __restrict__ gs = static_cast<const A*>(a.Gs);
+  A s = A(0);
+  for (int q = a.sub_begin[j]; q < a.sub_begin[j + 1]; ++q) s += gs[static_cast<long long>(q) * a.ld + c];
+  static_cast<A*>(a.Gb)[static_cast<long long>(j) * a.ld + c] = s;
 }
 
 // ---- pass 3: columns crossing tiles (tail of the first tile + the heads of every later one) and
@@ -282,13 +324,13 @@ __global__ void __launch_bounds__(256) csc_spans(const SparseArgs a, int span_bl
     A h = A(0);
     for (int t = sp.z + 1 + lane; t <= sp.w; t += 64) h += static_cast<const A*>(a.head)[t];
     h = wave_allreduce_sum(h);
-    if (lane == 0) static_cast<A*>(a.Gb)[static_cast<long long>(sp.x) * a.ld + sp.y] = static_cast<const A*>(a.tail)[sp.z] + h;
+    if (lane == 0) static_cast<A*>(a.Gs)[static_cast<long long>(sp.x) * a.ld + sp.y] = static_cast<const A*>(a.tail)[sp.z] + h;
     return;
   }
   const int i = (blockIdx.x - span_blocks) * blockDim.x + threadIdx.x;
   if (i < a.nempty) {
     const int2 e = a.empty[i];
-    static_cast<A*>(a.Gb)[static_cast<long long>(e.x) * a.ld + e.y] = A(0);
+    static_cast<A*>(a.Gs)[static_cast<long long>(e.x) * a.ld + e.y] = A(0);
   }
 }
 
@@ -296,7 +338,8 @@ __global__ void __launch_bounds__(256) csc_spans(const SparseArgs a, int span_bl
 
 hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const void* beta, hipStream_t st,
                               const int* gate) {
-  if (a.nrows < 0 || a.ntiles < 0 || a.d <= 0 || a.ld < a.d || !a.Gb || !a.u) return hipErrorInvalidValue;
+  if (a.nrows < 0 || a.ntiles < 0 || a.d <= 0 || a.ld < a.d || !a.Gb || !a.Gs || !a.u) return hipErrorInvalidValue;
+  if (a.sub_begin && a.Gs == a.Gb) return hipErrorInvalidValue;
   const dim3 block(256);
   if (a.nrows > 0) {
     const size_t blds = static_cast<size_t>(a.d) * (dtype == 0 ? 8 : 4);
@@ -365,7 +408,27 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
       }
     }
   }
-  if (a.ntiles > 0) {
+  if (a.ntiles > 0 && a.wg) {
+    const size_t ulds = static_cast<size_t>(std::max(a.u_lds, 1)) * (dtype == 0 ? 8 : 4);
+    if (ulds > 96 * 1024) return hipErrorInvalidValue;  // (plus the 32 KB of tile counts)
+    const dim3 grid(static_cast<unsigned>(a.nwg));
+#define EH_TLDS(A_, R_, V_)                                                                                    \
+  {                                                                                                            \
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(csc_tiles_lds<A_, R_, V_>),          \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ulds)); \
+    if (e != hipSuccess) return e;                                                                             \
+    hipLaunchKernelGGL((csc_tiles_lds<A_, R_, V_>), grid, dim3(1024), ulds, st, a, gate);                       \
+  }
+#define EH_TILES(A_)                                                                    \
+  if (a.row16) {                                                                        \
+    if (a.cvals) EH_TLDS(A_, true, true) else EH_TLDS(A_, true, false)                   \
+  } else {                                                                              \
+    if (a.cvals) EH_TLDS(A_, false, true) else EH_TLDS(A_, false, false)                 \
+  }
+    if (dtype == 0) { EH_TILES(double) } else { EH_TILES(float) }
+#undef EH_TILES
+#undef EH_TLDS
+  } else if (a.ntiles > 0) {
     const dim3 grid(static_cast<unsigned>((a.ntiles + 3) / 4));
 #define EH_TILES(A_)                                                                                     \
   if (a.row16) {                                                                                         \
@@ -383,6 +446,11 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
     const dim3 grid(static_cast<unsigned>(span_blocks + empty_blocks));
     if (dtype == 0) hipLaunchKernelGGL(csc_spans<double>, grid, block, 0, st, a, span_blocks, gate);
     else hipLaunchKernelGGL(csc_spans<float>, grid, block, 0, st, a, span_blocks, gate);
+  }
+  if (a.sub_begin && a.nparts > 0) {  // sub-block sums -> partitions
+    const dim3 grid(static_cast<unsigned>((a.ld + 255) / 256), static_cast<unsigned>(a.nparts));
+    if (dtype == 0) hipLaunchKernelGGL(sub_reduce<double>, grid, block, 0, st, a, gate);
+    else hipLaunchKernelGGL(sub_reduce<float>, grid, block, 0, st, a, gate);
   }
   return hipGetLastError();
 }

@@ -73,6 +73,14 @@ struct SparseArgs {
   int nempty;
   void* Gb;                     // [nparts][ld] output (acc dtype)
   int d, ld;
+  // row-blocked column pass (ops/grad.py csc_tables row_block): the "partitions" of pass 2 / 3 above
+  // are sub-blocks of rows; wg == nullptr: one wave per tile gathering the residuals from memory
+  const int4* wg;               // [nwg] (sub-block, first tile, tiles <= 16, rows): one workgroup each
+  int nwg;
+  int u_lds;                    // rows of the largest sub-block (its residuals staged in LDS)
+  void* Gs;                     // [nsub][ld] pass 2 / 3 output (== Gb without sub-blocks)
+  const int* sub_begin;         // [nparts + 1] sub-blocks of each partition; nullptr: Gs is Gb
+  int nparts;
 };
 hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const void* beta, hipStream_t st,
                               const int* gate = nullptr);

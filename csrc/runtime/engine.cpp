@@ -155,6 +155,7 @@ struct GradLauncher {
       case 2: {
         eh::SparseArgs a = sa;
         a.Gb = G;
+        if (!a.sub_begin) a.Gs = G;  // no sub-blocks: pass 2 / 3 write the partitions directly
         return eh::grad_sparse_launch(acc, loss, a, beta, st, gate);
       }
       default:
@@ -213,7 +214,9 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
                                           std::optional<Tensor> cvals, const Tensor& col_ptr, const Tensor& tiles,
                                           const Tensor& part_entry0, const Tensor& part_row0, const Tensor& part_nnz,
                                           const Tensor& head, const Tensor& tail, const Tensor& span,
-                                          const Tensor& empty, int64_t nparts, int64_t d, int64_t ld) {
+                                          const Tensor& empty, int64_t nparts, int64_t d, int64_t ld,
+                                          std::optional<Tensor> wg, int64_t u_lds, std::optional<Tensor> Gs,
+                                          std::optional<Tensor> sub_begin) {
   for (auto* t : {&y, &u, &crow, &col_ptr, &tiles, &part_entry0, &part_row0, &part_nnz, &head, &tail, &span, &empty})
     need_gpu(*t, "sparse plan operand");
   need(tiles.scalar_type() == at::kInt && tiles.dim() == 2 && tiles.size(1) == 4, "tiles: int32 [n, 4]");
@@ -290,6 +293,29 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
   a.nempty = (int)empty.size(0);
   a.d = (int)d;
   a.ld = (int)ld;
+  if (wg) {  // row-blocked column pass: `nparts` above counts sub-blocks
+    need_gpu(*wg, "wg");
+    need(wg->scalar_type() == at::kInt && wg->dim() == 2 && wg->size(1) == 4, "wg: int32 [n, 4]");
+    need(u_lds > 0 && u_lds * (g->acc == 0 ? 8 : 4) <= 96 * 1024, "u_lds: sub-block rows staged in LDS (<= 96 KB)");
+    a.wg = reinterpret_cast<const int4*>(wg->data_ptr<int>());
+    a.nwg = (int)wg->size(0);
+    a.u_lds = (int)u_lds;
+    g->keep.push_back(*wg);
+  }
+  if (sub_begin) {
+    need(Gs.has_value(), "sub-blocks need their Gs buffer");
+    need_gpu(*sub_begin, "sub_begin");
+    need_gpu(*Gs, "Gs");
+    need(sub_begin->scalar_type() == at::kInt && sub_begin->numel() >= 2, "sub_begin: int32 [partitions + 1]");
+    need(Gs->dim() == 2 && Gs->size(0) == nparts && Gs->size(1) == ld && acc_code(*Gs) == g->acc,
+         "Gs: [sub-blocks, ld] in the accumulator dtype");
+    a.sub_begin = sub_begin->data_ptr<int>();
+    a.nparts = (int)sub_begin->numel() - 1;
+    a.Gs = Gs->data_ptr();
+    g->nslots = a.nparts;  // Gb rows: the partitions
+    g->keep.push_back(*sub_begin);
+    g->keep.push_back(*Gs);
+  }
   return g;
 }
 
@@ -1754,7 +1780,8 @@ void bind_engine(py::module& m) {
                   py::arg("row_ptr"), py::arg("col_idx"), py::arg("vals"), py::arg("crow"), py::arg("cvals"),
                   py::arg("col_ptr"), py::arg("tiles"), py::arg("part_entry0"), py::arg("part_row0"),
                   py::arg("part_nnz"), py::arg("head"), py::arg("tail"), py::arg("span"), py::arg("empty"),
-                  py::arg("nparts"), py::arg("d"), py::arg("ld"))
+                  py::arg("nparts"), py::arg("d"), py::arg("ld"), py::arg("wg") = py::none(), py::arg("u_lds") = 0,
+                  py::arg("Gs") = py::none(), py::arg("sub_begin") = py::none())
       .def("set_encode",
            [](GradLauncher& g, const Tensor& ptr, const Tensor& idx, const Tensor& coef, const Tensor& Gb) {
              for (auto* t : {&ptr, &idx, &coef, &Gb}) need_gpu(*t, "encode operand");

@@ -610,6 +610,7 @@ class SparseGradPlan:
     """
 
     TILE = 512  # grad_sparse.hip kTileEntries
+    ROW_BLOCK_BYTES = 32 * 1024  # residuals of one column-pass sub-block, staged in LDS
 
     def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]], partitions: Dict[int, Tuple[object, np.ndarray]],
                  prec: Precision, loss: int, d: int, device="cpu", use_ell: bool = True):
@@ -683,7 +684,11 @@ class SparseGradPlan:
             self.col_idx = torch.from_numpy(X.indices.astype(np.int32)).to(dev)
             if not self.pattern_only:
                 self.vals = torch.from_numpy(X.data.astype(npacc)).to(dev)
-        t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE)
+        # residual sub-blocks staged in LDS by the column pass: 32 KB (4096 fp64 / 8192 fp32 rows)
+        rb = self.ROW_BLOCK_BYTES // torch.tensor([], dtype=acc).element_size()
+        t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE, row_block=rb)
+        self.row_block = rb
+        self.nsub = t["nsub"]
         self.row16 = t["row16"]
         self.crow = torch.from_numpy(t["crow"]).to(dev)
         self.cvals = None if self.pattern_only else torch.from_numpy(t["cvals"].astype(npacc)).to(dev)
@@ -698,6 +703,11 @@ class SparseGradPlan:
         self.head = torch.zeros(nt, dtype=acc, device=dev)
         self.tail = torch.zeros(nt, dtype=acc, device=dev)
         self.Gb = torch.zeros((max(1, len(self.basis)), self.ld), dtype=acc, device=dev)
+        self.wg = torch.from_numpy(t["wg"]).to(dev)
+        self.u_lds = int(t["wg"][:, 3].max()) if len(t["wg"]) else 1
+        blocked = self.nsub != len(self.basis)  # some partition spans several sub-blocks
+        self.sub_begin = torch.from_numpy(t["sub_begin"]).to(dev) if blocked else None
+        self.Gs = torch.zeros((self.nsub, self.ld), dtype=acc, device=dev) if blocked else None
         ptr, idx, coef = self._enc
         self.enc_ptr = torch.tensor(ptr, dtype=torch.int32, device=dev)
         self.enc_idx = torch.tensor(idx or [0], dtype=torch.int32, device=dev)[: len(idx)]
@@ -705,12 +715,29 @@ class SparseGradPlan:
         self._launcher = None
 
     @staticmethod
-    def csc_tables(blocks, d: int, tile: int = 512) -> dict:
+    def csc_tables(blocks, d: int, tile: int = 512, row_block: int = 0, wg_tiles: int = 16) -> dict:
         """Host tables of the deterministic column pass (grad_sparse.hip csc_tiles / csc_spans): per
         partition a CSC twin (rows sorted by (column, row), padded to whole tiles), its column
         pointers, the tiles (partition, base entry, column of the base entry, span flags: 1 = the
         first column began in an earlier tile, 2 = the last goes on in a later one), the columns that
-        cross tiles (partition, column, first tile, last tile) and the empty columns."""
+        cross tiles (partition, column, first tile, last tile) and the empty columns.
+
+        row_block > 0: every partition is cut into sub-blocks of at most that many rows and the tables
+        are built per sub-block (the "partitions" of the kernels are then the sub-blocks; sub_begin[j]
+        lists partition j's).  A workgroup takes up to wg_tiles tiles of ONE sub-block and stages
+        that sub-block's residuals in LDS (wg: sub-block, first tile, tiles, rows), so the column
+        pass's gathers never leave the CU; the sub-block sums are added per partition afterwards."""
+        import scipy.sparse as sps
+
+        sub_begin = None
+        if row_block > 0:
+            subs, sub_begin = [], [0]
+            for A in blocks:
+                n = A.shape[0]
+                for r in range(0, max(n, 1), row_block):
+                    subs.append(sps.csr_matrix(A[r:min(n, r + row_block)]))
+                sub_begin.append(len(subs))
+            blocks = subs
         row16 = all(A.shape[0] <= 65536 for A in blocks)
         rows_l, vals_l, cps, tiles, spans, empty = [], [], [], [], [], []
         entry0, row0, nnzs = [], [], []
@@ -751,7 +778,18 @@ class SparseGradPlan:
             r_off += A.shape[0]
         crow = np.concatenate(rows_l) if rows_l else np.zeros(tile, dtype=np.int64)
         crow = crow.astype(np.uint16).view(np.int16) if row16 else crow.astype(np.int32)
-        return {"row16": row16, "crow": np.ascontiguousarray(crow),
+        wg = []
+        if row_block > 0:
+            t_of = np.concatenate(tiles)[:, 0] if tiles else np.zeros(0, dtype=np.int64)
+            firsts = np.searchsorted(t_of, np.arange(len(blocks)), side="left")
+            lasts = np.searchsorted(t_of, np.arange(len(blocks)), side="right")
+            for j, A in enumerate(blocks):
+                for t0 in range(int(firsts[j]), int(lasts[j]), wg_tiles):
+                    wg.append((j, t0, min(wg_tiles, int(lasts[j]) - t0), A.shape[0]))
+        extra = {"sub_begin": np.asarray(sub_begin, dtype=np.int32) if sub_begin is not None else None,
+                 "wg": np.asarray(wg, dtype=np.int32).reshape(-1, 4), "nsub": len(blocks),
+                 "row_block": int(row_block)}
+        return {**extra, "row16": row16, "crow": np.ascontiguousarray(crow),
                 "cvals": np.concatenate(vals_l) if vals_l else np.zeros(tile),
                 "col_ptr": np.ascontiguousarray(np.stack(cps)) if cps else np.zeros((1, d + 1), dtype=np.int32),
                 "tiles": (np.concatenate(tiles) if tiles else np.zeros((0, 4))).astype(np.int32).reshape(-1, 4),
@@ -771,7 +809,9 @@ class SparseGradPlan:
             L = native().GradLauncher.sparse(self.loss, self.y, self.u, self.ell_idx, self.ell_lo, self.row_ptr,
                                              self.col_idx, self.vals, self.crow, self.cvals, self.col_ptr, self.tiles,
                                              self.part_entry0, self.part_row0, self.part_nnz, self.head, self.tail,
-                                             self.span, self.empty, len(self.basis), self.d, self.ld)
+                                             self.span, self.empty, self.nsub, self.d, self.ld,
+                                             wg=self.wg if len(self.wg) else None, u_lds=self.u_lds, Gs=self.Gs,
+                                             sub_begin=self.sub_begin)
             L.set_encode(self.enc_ptr, self.enc_idx, self.enc_coef, self.Gb)
             self._launcher = L
         return self._launcher

@@ -123,3 +123,37 @@ def test_cpu_plan_matches_scipy_per_message():
     for s, m in enumerate(msgs):
         ref = sum(logistic_grad(parts[p][0], parts[p][1], b, c) for p, c in m)
         np.testing.assert_allclose(G[s, :d].numpy(), ref, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("row_block", [64, 700, 4096])
+def test_row_blocked_tables_sum_to_the_transposed_product(row_block):
+    """Row-blocked tables (SparseGradPlan.csc_tables(row_block=...)): every partition cut into
+    sub-blocks of at most row_block rows; the emulated sub-block sums, added per partition in
+    sub-block order (grad_sparse.hip sub_reduce), are X_p^T u_p; the workgroup table covers every
+    tile of every sub-block exactly once, never mixing sub-blocks."""
+    rng = np.random.RandomState(7)
+    d = 2500
+    blocks = [_onehot(rng, 1800, [2, 40, 700, 1200]), _onehot(rng, 333, [1, 900, 5, 1000]),
+              sps.csr_matrix((0, 2403))]
+    blocks = [sps.csr_matrix((b.data, b.indices, b.indptr), shape=(b.shape[0], d)) for b in blocks]
+    t = SparseGradPlan.csc_tables(blocks, d, TILE, row_block=row_block, wg_tiles=16)
+    sb = t["sub_begin"]
+    assert len(sb) == len(blocks) + 1 and sb[-1] == t["nsub"]
+    u = [rng.randn(b.shape[0]) for b in blocks]
+    u_sub = []
+    for j, b in enumerate(blocks):
+        for r in range(0, max(b.shape[0], 1), row_block):
+            u_sub.append(u[j][r:r + row_block])
+    assert len(u_sub) == t["nsub"]
+    got = emulate(t, u_sub, d)
+    seen = []
+    for s, t0, nt, rows in t["wg"]:
+        assert 1 <= nt <= 16 and rows == len(u_sub[s])
+        assert all(t["tiles"][k][0] == s for k in range(t0, t0 + nt))
+        seen += list(range(t0, t0 + nt))
+    assert sorted(seen) == list(range(len(t["tiles"])))
+    for j, b in enumerate(blocks):
+        acc = np.zeros(d)
+        for s in range(sb[j], sb[j + 1]):
+            acc = acc + got[s]
+        np.testing.assert_allclose(acc, b.T.dot(u[j]), rtol=1e-12, atol=1e-12)
