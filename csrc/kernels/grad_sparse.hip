@@ -89,15 +89,21 @@ __global__ void __launch_bounds__(256) ell_rows(const SparseArgs a, const A* __r
 // that the fields' windows (55 per row) keep thrashing: 21.8M gathers, ~2.8 GB of L2 -> L1 traffic,
 // 38-41 us (profiles/round4/r4g, r4i).  From LDS they cost a few cycles.  One 1024-thread workgroup per
 // CU (the LDS copy of beta is per workgroup), rows strided over the grid.
-constexpr int kEllLdsBytes = 152 * 1024;
+constexpr int kEllLdsBytes = 148 * 1024;
+constexpr int kEllMaxFields = 1024;
 
 template <typename A, int LOSS, bool IDX16, bool VALS>
 __global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A* __restrict__ beta, const int* gate) {
-  constexpr int KB = 16;
+  // one LDS-bound workgroup per CU (16 waves): a row's fields are loaded 32 at a time (covtype's 55
+  // in two batches), the window starts come from LDS
+  constexpr int KB = 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char ell_lds[];
   A* sb = reinterpret_cast<A*>(ell_lds);
+  __shared__ int slo[kEllMaxFields];  // the fields' window starts (idx16), read per lane from LDS
   if (gate_closed(gate)) return;
   for (int c = threadIdx.x; c < a.d; c += blockDim.x) sb[c] = beta[c];
+  if (IDX16)
+    for (int k = threadIdx.x; k < a.m && k < kEllMaxFields; k += blockDim.x) slo[k] = a.lo[k];
   __syncthreads();
   const long long n = a.nrows;
   const int m = a.m;
@@ -115,11 +121,12 @@ __global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A
     for (int k0 = 0; k0 < m; k0 += KB) {
       int c[KB];
 #pragma unroll
-      for (int u = 0; u < KB; ++u) c[u] = (IDX16 ? a.lo[min(k0 + u, m - 1)] : 0) + idx(min(k0 + u, m - 1));
+      for (int u = 0; u < KB; ++u) c[u] = idx(min(k0 + u, m - 1));
 #pragma unroll
       for (int u = 0; u < KB; ++u)
         if (k0 + u < m)
-          z[u & 3] = fma(VALS ? vals[static_cast<long long>(k0 + u) * n + row] : A(1), sb[c[u]], z[u & 3]);
+          z[u & 3] = fma(VALS ? vals[static_cast<long long>(k0 + u) * n + row] : A(1),
+                         sb[(IDX16 ? slo[k0 + u] : 0) + c[u]], z[u & 3]);
     }
     const A zz = (z[0] + z[1]) + (z[2] + z[3]);
     static_cast<A*>(a.u)[row] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[row], A(1));
@@ -273,15 +280,15 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
   });
 }
 
-// Row-blocked column pass: a 1024-thread workgroup takes up to 16 tiles of ONE sub-block (a.wg) and
+// Row-blocked column pass: a 1024-thread workgroup takes up to kWgTiles tiles of ONE sub-block (a.wg) and
 // first copies that sub-block's residuals into LDS (coalesced), so every gather is an LDS read.  From
 // global memory each 8-byte gather pulled a 128-byte L2 line into L1 with no reuse (rows of a column
 // are spread over the partition): covtype's 21.8M gathers moved ~2.8 GB L2 -> L1, 88-92 us
 // (profiles/round4/r4g, r4i).
-constexpr int kWgTiles = 16;
+constexpr int kWgTiles = 48;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES), 3 per wave
 template <typename A, bool ROW16, bool VALS>
 __global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const int* gate) {
-  __shared__ int cnt[kWgTiles][kTileEntries];
+  __shared__ int cnt[16][kTileEntries];
   extern __shared__ __attribute__((aligned(16))) unsigned char usub_raw[];
   A* su = reinterpret_cast<A*>(usub_raw);
   if (gate_closed(gate)) return;
@@ -290,11 +297,13 @@ __global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const 
   for (int i = threadIdx.x; i < wd.w; i += blockDim.x) su[i] = ug[i];
   __syncthreads();
   const int w = threadIdx.x >> 6;
-  if (w >= wd.z) return;  // wave-uniform; no block barrier after this
-  tile_pass<A, ROW16, VALS>(a, wd.y + w, cnt[w], [&](int, const int (&rows)[8], A (&v)[8]) {
+  // wave w takes tiles w, w + 16, ... of the workgroup's chunk (up to kWgTiles): the staging of the
+  // residuals is paid once per chunk
+  for (int k = w; k < wd.z; k += static_cast<int>(blockDim.x >> 6))  // wave-uniform; no block barrier inside
+    tile_pass<A, ROW16, VALS>(a, wd.y + k, cnt[w], [&](int, const int (&rows)[8], A (&v)[8]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = su[min(rows[i], wd.w - 1)];  // (padding rows are 0; clamp an empty sub-block)
-  });
+      for (int i = 0; i < 8; ++i) v[i] = su[min(rows[i], wd.w - 1)];  // (padding rows are 0; clamp an empty sub-block)
+    });
 }
 
 // Sub-block sums added per partition in sub-block order: Gb[j][c] = sum_s Gs[s][c].
@@ -343,7 +352,7 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
   const dim3 block(256);
   if (a.nrows > 0) {
     const size_t blds = static_cast<size_t>(a.d) * (dtype == 0 ? 8 : 4);
-    if (a.ell && blds <= static_cast<size_t>(kEllLdsBytes)) {
+    if (a.ell && blds <= static_cast<size_t>(kEllLdsBytes) && a.m <= kEllMaxFields) {
       static int cus = 0;
       if (!cus) {
         int dev = 0;

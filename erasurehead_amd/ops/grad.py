@@ -611,6 +611,7 @@ class SparseGradPlan:
 
     TILE = 512  # grad_sparse.hip kTileEntries
     ROW_BLOCK_BYTES = 32 * 1024  # residuals of one column-pass sub-block, staged in LDS
+    WG_TILES = 48  # tiles per column-pass workgroup (grad_sparse.hip kWgTiles)
 
     def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]], partitions: Dict[int, Tuple[object, np.ndarray]],
                  prec: Precision, loss: int, d: int, device="cpu", use_ell: bool = True):
@@ -686,7 +687,7 @@ class SparseGradPlan:
                 self.vals = torch.from_numpy(X.data.astype(npacc)).to(dev)
         # residual sub-blocks staged in LDS by the column pass: 32 KB (4096 fp64 / 8192 fp32 rows)
         rb = self.ROW_BLOCK_BYTES // torch.tensor([], dtype=acc).element_size()
-        t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE, row_block=rb)
+        t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE, row_block=rb, wg_tiles=self.WG_TILES)
         self.row_block = rb
         self.nsub = t["nsub"]
         self.row16 = t["row16"]
