@@ -54,26 +54,12 @@ __global__ void __launch_bounds__(256) ell_rows(const SparseArgs a, const A* __r
   const int m = a.m;
   const A* __restrict__ vals = static_cast<const A*>(a.vals);
   A z[4] = {A(0), A(0), A(0), A(0)};
-  if constexpr (IDX16) {  // row-major 16-bit offsets: 8 fields per 16-byte load
-    const unsigned short* ir = static_cast<const unsigned short*>(a.ell_idx) + row * a.m_pad;
-    for (int j0 = 0; j0 < m; j0 += 8) {
-      const uint4 q = load16_nt<uint4>(ir + j0);
-      const unsigned int qw[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int k = j0 + e;
-        if (k < m) {
-          const int c = a.lo[k] + static_cast<int>((qw[e >> 1] >> (16 * (e & 1))) & 0xffffu);
-          z[k & 3] = fma(VALS ? vals[static_cast<long long>(k) * n + row] : A(1), beta[c], z[k & 3]);
-        }
-      }
-    }
-    const A zz = (z[0] + z[1]) + (z[2] + z[3]);
-    static_cast<A*>(a.u)[row] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[row], A(1));
-    return;
-  }
   auto idx = [&](int kk) -> int {
-    return __builtin_nontemporal_load(static_cast<const int*>(a.ell_idx) + static_cast<long long>(kk) * n + row);
+    if constexpr (IDX16)
+      return static_cast<int>(__builtin_nontemporal_load(static_cast<const unsigned short*>(a.ell_idx) +
+                                                         static_cast<long long>(kk) * n + row));
+    else
+      return __builtin_nontemporal_load(static_cast<const int*>(a.ell_idx) + static_cast<long long>(kk) * n + row);
   };
   int cn[KB];
 #pragma unroll
@@ -81,7 +67,7 @@ __global__ void __launch_bounds__(256) ell_rows(const SparseArgs a, const A* __r
   for (int k0 = 0; k0 < m; k0 += KB) {
     int c[KB];
 #pragma unroll
-    for (int u = 0; u < KB; ++u) c[u] = cn[u];
+    for (int u = 0; u < KB; ++u) c[u] = (IDX16 ? a.lo[min(k0 + u, m - 1)] : 0) + cn[u];
 #pragma unroll
     for (int u = 0; u < KB; ++u) cn[u] = idx(min(k0 + KB + u, m - 1));  // next batch in flight
     A bv[KB], v[KB];
@@ -125,30 +111,12 @@ __global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A
   const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
   for (long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; row < n; row += stride) {
     A z[4] = {A(0), A(0), A(0), A(0)};
-    if constexpr (IDX16) {  // row-major 16-bit offsets: 8 fields per 16-byte load, 32 fields in flight
-      const unsigned short* ir = static_cast<const unsigned short*>(a.ell_idx) + row * a.m_pad;
-      for (int j0 = 0; j0 < m; j0 += 32) {
-        uint4 q[4];
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) q[jj] = load16_nt<uint4>(ir + min(j0 + 8 * jj, a.m_pad - 8));
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const unsigned int qw[4] = {q[jj].x, q[jj].y, q[jj].z, q[jj].w};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int k = j0 + 8 * jj + e;
-            if (k < m)
-              z[k & 3] = fma(VALS ? vals[static_cast<long long>(k) * n + row] : A(1),
-                             sb[slo[k] + static_cast<int>((qw[e >> 1] >> (16 * (e & 1))) & 0xffffu)], z[k & 3]);
-          }
-        }
-      }
-      const A zz = (z[0] + z[1]) + (z[2] + z[3]);
-      static_cast<A*>(a.u)[row] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[row], A(1));
-      continue;
-    }
     auto idx = [&](int kk) -> int {
-      return __builtin_nontemporal_load(static_cast<const int*>(a.ell_idx) + static_cast<long long>(kk) * n + row);
+      if constexpr (IDX16)
+        return static_cast<int>(__builtin_nontemporal_load(static_cast<const unsigned short*>(a.ell_idx) +
+                                                           static_cast<long long>(kk) * n + row));
+      else
+        return __builtin_nontemporal_load(static_cast<const int*>(a.ell_idx) + static_cast<long long>(kk) * n + row);
     };
     for (int k0 = 0; k0 < m; k0 += KB) {
       int c[KB];
@@ -156,7 +124,9 @@ __global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A
       for (int u = 0; u < KB; ++u) c[u] = idx(min(k0 + u, m - 1));
 #pragma unroll
       for (int u = 0; u < KB; ++u)
-        if (k0 + u < m) z[u & 3] = fma(VALS ? vals[static_cast<long long>(k0 + u) * n + row] : A(1), sb[c[u]], z[u & 3]);
+        if (k0 + u < m)
+          z[u & 3] = fma(VALS ? vals[static_cast<long long>(k0 + u) * n + row] : A(1),
+                         sb[(IDX16 ? slo[k0 + u] : 0) + c[u]], z[u & 3]);
     }
     const A zz = (z[0] + z[1]) + (z[2] + z[3]);
     static_cast<A*>(a.u)[row] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[row], A(1));
@@ -315,8 +285,7 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
 // global memory each 8-byte gather pulled a 128-byte L2 line into L1 with no reuse (rows of a column
 // are spread over the partition): covtype's 21.8M gathers moved ~2.8 GB L2 -> L1, 88-92 us
 // (profiles/round4/r4g, r4i).
-constexpr int kWgTiles = 16;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES), one per wave
-// (48, three per wave in turn, measured slower: 66.8 vs 47 us at covtype's shape, profiles/round4/r4k)
+constexpr int kWgTiles = 48;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES), 3 per wave
 template <typename A, bool ROW16, bool VALS>
 __global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const int* gate) {
   __shared__ int cnt[16][kTileEntries];

@@ -47,8 +47,7 @@ struct SparseArgs {
   int idx16;                    // ELL: uint16 offsets into window lo[k] (else int32 columns)
   int m;                        // ELL nnz per row
   long long nrows;
-  const void* ell_idx;          // idx16: [nrows][m_pad] uint16 row-major; else [m][nrows] int32
-  int m_pad;                    // idx16 row length (m rounded up to 8: 16-byte loads of 8 fields)
+  const void* ell_idx;          // [m][nrows] uint16 | int32
   const int* lo;                // [m] category window starts (idx16)
   const long long* row_ptr;     // CSR [nrows + 1]
   const int* col_idx;           // CSR [nnz]

@@ -241,19 +241,11 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
   g->keep = {y, u, crow, col_ptr, tiles, part_entry0, part_row0, part_nnz, head, tail, span, empty};
   if (ell_idx) {
     need_gpu(*ell_idx, "ell_idx");
+    need(ell_idx->dim() == 2 && ell_idx->size(1) == a.nrows, "ell_idx: [m, rows]");
     a.ell = 1;
     a.idx16 = ell_idx->scalar_type() == at::kShort ? 1 : 0;
     need(a.idx16 || ell_idx->scalar_type() == at::kInt, "ell_idx: int16 | int32");
-    if (a.idx16) {  // [rows, m_pad] row-major; m = the window starts' count
-      need(ell_idx->dim() == 2 && ell_idx->size(0) == a.nrows && ell_idx->size(1) % 8 == 0, "ell_idx16: [rows, m_pad]");
-      need(lo.has_value(), "idx16 needs lo");
-      a.m = (int)lo->numel();
-      a.m_pad = (int)ell_idx->size(1);
-      need(a.m <= a.m_pad && a.m_pad - a.m < 8, "ell_idx16: m_pad = m rounded up to 8");
-    } else {
-      need(ell_idx->dim() == 2 && ell_idx->size(1) == a.nrows, "ell_idx: [m, rows]");
-      a.m = (int)ell_idx->size(0);
-    }
+    a.m = (int)ell_idx->size(0);
     a.ell_idx = ell_idx->data_ptr();
     if (a.idx16) {
       need(lo.has_value() && lo->numel() == a.m && lo->scalar_type() == at::kInt, "lo: int32 [m]");

@@ -611,7 +611,7 @@ class SparseGradPlan:
 
     TILE = 512  # grad_sparse.hip kTileEntries
     ROW_BLOCK_BYTES = 32 * 1024  # residuals of one column-pass sub-block, staged in LDS
-    WG_TILES = 16  # tiles per column-pass workgroup (grad_sparse.hip kWgTiles)
+    WG_TILES = 48  # tiles per column-pass workgroup (grad_sparse.hip kWgTiles)
 
     def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]], partitions: Dict[int, Tuple[object, np.ndarray]],
                  prec: Precision, loss: int, d: int, device="cpu", use_ell: bool = True):
@@ -673,11 +673,8 @@ class SparseGradPlan:
             self.ell, self.ell_m = True, m
             if int(width.max()) <= 65536:  # 16-bit offsets into each feature's category window
                 self.idx16 = True
-                # row-major, rows padded to 8 fields: one 16-byte load per 8 fields of a row
-                m_pad = -(-m // 8) * 8
-                off = np.zeros((self.nrows, m_pad), dtype=np.uint16)
-                off[:, :m] = (idx - lo[:, None]).T.astype(np.uint16)
-                self.ell_idx = torch.from_numpy(off.view(np.int16)).to(dev)
+                off = (idx - lo[:, None]).astype(np.uint16).view(np.int16)
+                self.ell_idx = torch.from_numpy(np.ascontiguousarray(off)).to(dev)
                 self.ell_lo = torch.from_numpy(lo.astype(np.int32)).to(dev)
             else:
                 self.ell_idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32)).to(dev)
