@@ -152,8 +152,9 @@ __global__ void __launch_bounds__(256) csr_rows(const SparseArgs a, const A* __r
 // ---- pass 2: CSC tiles, one wave per 512-entry tile ---------------------------------------------
 // The tile body: `gather(rows, v)` fills v[i] = u[rows[i]] (sub-block relative rows) -- from global
 // memory through a buffer descriptor, or from the workgroup's LDS copy of the sub-block's residuals.
-template <typename A, bool ROW16, bool VALS, typename Gather>
-__device__ __forceinline__ void tile_pass(const SparseArgs& a, int t, int* __restrict__ cw, Gather gather) {
+template <typename A, bool ROW16, bool VALS, typename Gather, typename Mid>
+__device__ __forceinline__ void tile_pass(const SparseArgs& a, int t, int* __restrict__ cw, Gather gather, Mid mid,
+                                          bool late_gather) {
   const int lane = threadIdx.x & 63;
   const int4 td = a.tiles[t];
   const int p = td.x, base = td.y, c0 = td.z, flags = td.w;
@@ -188,7 +189,7 @@ __device__ __forceinline__ void tile_pass(const SparseArgs& a, int t, int* __res
     for (int i = 0; i < 8; ++i) cv[i] = buf_load_scalar<A>(vrs, (8 * lane + i) * static_cast<int>(sizeof(A)));
   }
   A v[8];
-  gather(p, rows, v);
+  if (!late_gather) gather(p, rows, v);
   // 1. column boundaries inside the tile: cnt[q] = number of columns c > c0 starting at base + q
   //    (empty columns stack on the next non-empty one's start); integer LDS adds, order-free
 #pragma unroll
@@ -218,6 +219,10 @@ __device__ __forceinline__ void tile_pass(const SparseArgs& a, int t, int* __res
   int key[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) key[i] = c0 + before + cl[i];
+  if (late_gather) {  // the LDS path: the staged residuals are published by mid() (a block barrier)
+    mid();
+    gather(p, rows, v);
+  }
   // 3. mask the padding
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -277,7 +282,7 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
     const auto urs = make_rsrc(static_cast<const A*>(a.u) + r0, static_cast<int>(min(ubytes, static_cast<long long>(INT_MAX))));
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = buf_load_scalar<A>(urs, rows[i] * static_cast<int>(sizeof(A)));
-  });
+  }, [] {}, false);
 }
 
 // Row-blocked column pass: a 1024-thread workgroup takes up to kWgTiles tiles of ONE sub-block (a.wg) and
@@ -285,7 +290,8 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
 // global memory each 8-byte gather pulled a 128-byte L2 line into L1 with no reuse (rows of a column
 // are spread over the partition): covtype's 21.8M gathers moved ~2.8 GB L2 -> L1, 88-92 us
 // (profiles/round4/r4g, r4i).
-constexpr int kWgTiles = 48;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES), 3 per wave
+constexpr int kWgTiles = 16;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES), one per wave
+constexpr int kStageRegs = 4;  // staged residuals per thread: 4096 rows per sub-block (32 KB fp64 / 16 KB fp32)
 template <typename A, bool ROW16, bool VALS>
 __global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const int* gate) {
   __shared__ int cnt[16][kTileEntries];
@@ -293,17 +299,36 @@ __global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const 
   A* su = reinterpret_cast<A*>(usub_raw);
   if (gate_closed(gate)) return;
   const int4 wd = a.wg[blockIdx.x];  // (sub-block, first tile, tiles, rows)
+  // the sub-block's residuals: loaded into registers first, stored to LDS only after this wave's
+  // tile has its row indices and column boundaries (step 0-2 of tile_pass), so the staging latency
+  // overlaps those loads instead of preceding them
   const A* __restrict__ ug = static_cast<const A*>(a.u) + a.part_row0[wd.x];
-  for (int i = threadIdx.x; i < wd.w; i += blockDim.x) su[i] = ug[i];
-  __syncthreads();
-  const int w = threadIdx.x >> 6;
-  // wave w takes tiles w, w + 16, ... of the workgroup's chunk (up to kWgTiles): the staging of the
-  // residuals is paid once per chunk
-  for (int k = w; k < wd.z; k += static_cast<int>(blockDim.x >> 6))  // wave-uniform; no block barrier inside
-    tile_pass<A, ROW16, VALS>(a, wd.y + k, cnt[w], [&](int, const int (&rows)[8], A (&v)[8]) {
+  A st[kStageRegs];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = su[min(rows[i], wd.w - 1)];  // (padding rows are 0; clamp an empty sub-block)
-    });
+  for (int j = 0; j < kStageRegs; ++j) {
+    const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
+    st[j] = i < wd.w ? ug[i] : A(0);
+  }
+  auto publish = [&] {
+#pragma unroll
+    for (int j = 0; j < kStageRegs; ++j) {
+      const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
+      if (i < wd.w) su[i] = st[j];
+    }
+    __syncthreads();
+  };
+  const int w = threadIdx.x >> 6;
+  if (w >= wd.z) {  // no tile for this wave: it still stages and joins the one barrier
+    publish();
+    return;
+  }
+  // one tile per wave: a loop over several (48 tiles per workgroup, 3 per wave) needed more than 64
+  // VGPRs, one resident workgroup per CU instead of two, and measured 66.8-70.5 vs 47 us at covtype's
+  // shape (profiles/round4/r4k, r4l)
+  tile_pass<A, ROW16, VALS>(a, wd.y + w, cnt[w], [&](int, const int (&rows)[8], A (&v)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = su[min(rows[i], wd.w - 1)];  // (padding rows are 0; clamp an empty sub-block)
+  }, publish, true);
 }
 
 // Sub-block sums added per partition in sub-block order: Gb[j][c] = sum_s Gs[s][c].
@@ -419,7 +444,7 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
   }
   if (a.ntiles > 0 && a.wg) {
     const size_t ulds = static_cast<size_t>(std::max(a.u_lds, 1)) * (dtype == 0 ? 8 : 4);
-    if (ulds > 96 * 1024) return hipErrorInvalidValue;  // (plus the 32 KB of tile counts)
+    if (a.u_lds > kStageRegs * 1024) return hipErrorInvalidValue;  // (sub-blocks of at most 4096 rows)
     const dim3 grid(static_cast<unsigned>(a.nwg));
 #define EH_TLDS(A_, R_, V_)                                                                                    \
   {                                                                                                            \

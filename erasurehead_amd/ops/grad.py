@@ -610,8 +610,8 @@ class SparseGradPlan:
     """
 
     TILE = 512  # grad_sparse.hip kTileEntries
-    ROW_BLOCK_BYTES = 32 * 1024  # residuals of one column-pass sub-block, staged in LDS
-    WG_TILES = 48  # tiles per column-pass workgroup (grad_sparse.hip kWgTiles)
+    ROW_BLOCK_ROWS = 4096  # residuals of one column-pass sub-block, staged in LDS
+    WG_TILES = 16  # tiles per column-pass workgroup (grad_sparse.hip kWgTiles), one per wave
 
     def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]], partitions: Dict[int, Tuple[object, np.ndarray]],
                  prec: Precision, loss: int, d: int, device="cpu", use_ell: bool = True):
@@ -685,8 +685,9 @@ class SparseGradPlan:
             self.col_idx = torch.from_numpy(X.indices.astype(np.int32)).to(dev)
             if not self.pattern_only:
                 self.vals = torch.from_numpy(X.data.astype(npacc)).to(dev)
-        # residual sub-blocks staged in LDS by the column pass: 32 KB (4096 fp64 / 8192 fp32 rows)
-        rb = self.ROW_BLOCK_BYTES // torch.tensor([], dtype=acc).element_size()
+        # residual sub-blocks staged in LDS by the column pass: 4096 rows (32 KB fp64, 16 KB fp32; four
+        # staged values per thread of its 1024-thread workgroups, grad_sparse.hip kStageRegs)
+        rb = self.ROW_BLOCK_ROWS
         t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE, row_block=rb, wg_tiles=self.WG_TILES)
         self.row_block = rb
         self.nsub = t["nsub"]
