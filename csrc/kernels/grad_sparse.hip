@@ -343,27 +343,21 @@ __global__ void __launch_bounds__(256) sub_reduce(const SparseArgs a, const int*
   static_cast<A*>(a.Gb)[static_cast<long long>(j) * a.ld + c] = s;
 }
 
-// ---- pass 3: columns crossing tiles (tail of the first tile + the heads of every later one) and
-// the columns no entry of the partition touches.  One wave per crossing column: a binary feature's
-// column spans ~70 tiles per partition at covtype's shape, so a serial walk would be ~70 dependent
-// steps; lane j sums heads t1+1+j, t1+1+j+64, ... in order, then a fixed-pattern wave reduction
-// (bitwise the same every run).  Blocks past the spans write the empty columns, a thread each.
+// ---- pass 3: columns crossing tiles (tail of the first tile + the heads of the later ones, in tile
+// order) and the columns no entry of the sub-block touches, a thread each.  Within a sub-block of at
+// most 4096 rows a column covers at most 9 tiles, so the walk is short (it was one wave per column
+// while a partition's column could span ~70 tiles).
 template <typename A>
-__global__ void __launch_bounds__(256) csc_spans(const SparseArgs a, int span_blocks, const int* gate) {
+__global__ void __launch_bounds__(256) csc_spans(const SparseArgs a, int, const int* gate) {
   if (gate_closed(gate)) return;
-  if (static_cast<int>(blockIdx.x) < span_blocks) {
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (i >= a.nspan) return;  // wave-uniform
-    const int4 sp = a.span[i];  // (partition, column, t1, t2)
-    A h = A(0);
-    for (int t = sp.z + 1 + lane; t <= sp.w; t += 64) h += static_cast<const A*>(a.head)[t];
-    h = wave_allreduce_sum(h);
-    if (lane == 0) static_cast<A*>(a.Gs)[static_cast<long long>(sp.x) * a.ld + sp.y] = static_cast<const A*>(a.tail)[sp.z] + h;
-    return;
-  }
-  const int i = (blockIdx.x - span_blocks) * blockDim.x + threadIdx.x;
-  if (i < a.nempty) {
-    const int2 e = a.empty[i];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < a.nspan) {
+    const int4 sp = a.span[i];  // (sub-block, column, t1, t2)
+    A s = static_cast<const A*>(a.tail)[sp.z];
+    for (int t = sp.z + 1; t <= sp.w; ++t) s += static_cast<const A*>(a.head)[t];
+    static_cast<A*>(a.Gs)[static_cast<long long>(sp.x) * a.ld + sp.y] = s;
+  } else if (i < a.nspan + a.nempty) {
+    const int2 e = a.empty[i - a.nspan];
     static_cast<A*>(a.Gs)[static_cast<long long>(e.x) * a.ld + e.y] = A(0);
   }
 }
@@ -475,11 +469,11 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
     if (dtype == 0) { EH_TILES(double) } else { EH_TILES(float) }
 #undef EH_TILES
   }
-  const int span_blocks = (a.nspan + 3) / 4, empty_blocks = (a.nempty + 255) / 256;
-  if (span_blocks + empty_blocks > 0) {
-    const dim3 grid(static_cast<unsigned>(span_blocks + empty_blocks));
-    if (dtype == 0) hipLaunchKernelGGL(csc_spans<double>, grid, block, 0, st, a, span_blocks, gate);
-    else hipLaunchKernelGGL(csc_spans<float>, grid, block, 0, st, a, span_blocks, gate);
+  const int nout = a.nspan + a.nempty;
+  if (nout > 0) {
+    const dim3 grid(static_cast<unsigned>((nout + 255) / 256));
+    if (dtype == 0) hipLaunchKernelGGL(csc_spans<double>, grid, block, 0, st, a, 0, gate);
+    else hipLaunchKernelGGL(csc_spans<float>, grid, block, 0, st, a, 0, gate);
   }
   if (a.sub_begin && a.nparts > 0) {  // sub-block sums -> partitions
     const dim3 grid(static_cast<unsigned>((a.ld + 255) / 256), static_cast<unsigned>(a.nparts));
