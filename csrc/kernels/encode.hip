@@ -18,27 +18,42 @@
 
 namespace eh {
 
+// sub_begin != nullptr: Gb holds row-block sums (grad_sparse.hip row-blocked column pass) and
+// partition p's gradient is the sum of its rows sub_begin[p] .. sub_begin[p + 1] - 1, added first in
+// row-block order -- the sub_reduce kernel's arithmetic, one launch less.
 template <typename A>
 __global__ void __launch_bounds__(256)
 encode_messages(const A* __restrict__ Gb, const int* __restrict__ ptr, const int* __restrict__ idx,
-                const double* __restrict__ coef, A* __restrict__ G, int ld, const int* __restrict__ gate) {
+                const double* __restrict__ coef, A* __restrict__ G, int ld, const int* __restrict__ gate,
+                const int* __restrict__ sub_begin) {
   const int slot = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= ld || gate_closed(gate)) return;
   const int b = ptr[slot], e = ptr[slot + 1];
   A s = A(0);
-  for (int k = b; k < e; ++k) s = fma(static_cast<A>(coef[k]), Gb[static_cast<long long>(idx[k]) * ld + c], s);
+  for (int k = b; k < e; ++k) {
+    A g;
+    if (sub_begin) {
+      g = A(0);
+      for (int q = sub_begin[idx[k]]; q < sub_begin[idx[k] + 1]; ++q) g += Gb[static_cast<long long>(q) * ld + c];
+    } else {
+      g = Gb[static_cast<long long>(idx[k]) * ld + c];
+    }
+    s = fma(static_cast<A>(coef[k]), g, s);
+  }
   G[static_cast<long long>(slot) * ld + c] = s;
 }
 
 hipError_t encode_messages_launch(int dtype, const void* Gb, const int* ptr, const int* idx, const double* coef,
-                                  void* G, int nslots, int ld, hipStream_t st, const int* gate) {
+                                  void* G, int nslots, int ld, hipStream_t st, const int* gate, const int* sub_begin) {
   if (nslots == 0) return hipSuccess;
   const dim3 block(256), grid(ceil_div(ld, 256), nslots);
   if (dtype == 0)
-    hipLaunchKernelGGL(encode_messages<double>, grid, block, 0, st, (const double*)Gb, ptr, idx, coef, (double*)G, ld, gate);
+    hipLaunchKernelGGL(encode_messages<double>, grid, block, 0, st, (const double*)Gb, ptr, idx, coef, (double*)G, ld, gate,
+                       sub_begin);
   else
-    hipLaunchKernelGGL(encode_messages<float>, grid, block, 0, st, (const float*)Gb, ptr, idx, coef, (float*)G, ld, gate);
+    hipLaunchKernelGGL(encode_messages<float>, grid, block, 0, st, (const float*)Gb, ptr, idx, coef, (float*)G, ld, gate,
+                       sub_begin);
   return hipGetLastError();
 }
 

@@ -475,7 +475,7 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
     if (dtype == 0) hipLaunchKernelGGL(csc_spans<double>, grid, block, 0, st, a, 0, gate);
     else hipLaunchKernelGGL(csc_spans<float>, grid, block, 0, st, a, 0, gate);
   }
-  if (a.sub_begin && a.nparts > 0) {  // sub-block sums -> partitions
+  if (a.sub_begin && a.nparts > 0 && !a.encode_from_subs) {  // sub-block sums -> partitions
     const dim3 grid(static_cast<unsigned>((a.ld + 255) / 256), static_cast<unsigned>(a.nparts));
     if (dtype == 0) hipLaunchKernelGGL(sub_reduce<double>, grid, block, 0, st, a, gate);
     else hipLaunchKernelGGL(sub_reduce<float>, grid, block, 0, st, a, gate);

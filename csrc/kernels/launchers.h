@@ -81,6 +81,7 @@ struct SparseArgs {
   void* Gs;                     // [nsub][ld] pass 2 / 3 output (== Gb without sub-blocks)
   const int* sub_begin;         // [nparts + 1] sub-blocks of each partition; nullptr: Gs is Gb
   int nparts;
+  int encode_from_subs;         // 1: the encoding that follows adds the sub-block sums itself (no sub_reduce)
 };
 hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const void* beta, hipStream_t st,
                               const int* gate = nullptr);
@@ -92,7 +93,8 @@ hipError_t tr_probe_launch(const float* tile, int rowlen, float* out, hipStream_
 // ---- device encoding of shared-partition gradients (encode.hip) ---------------------------
 // G[slot] = sum_{k in [ptr[slot], ptr[slot+1])} coef[k] * Gb[idx[k]]; dtype 0 fp64, 1 fp32
 hipError_t encode_messages_launch(int dtype, const void* Gb, const int* ptr, const int* idx, const double* coef,
-                                  void* G, int nslots, int ld, hipStream_t st, const int* gate = nullptr);
+                                  void* G, int nslots, int ld, hipStream_t st, const int* gate = nullptr,
+                                  const int* sub_begin = nullptr);
 
 // ---- post-hoc evaluation GEMM (eval.hip) -----------------------------------------------
 hipError_t eval_gemm_loss_launch(int x_dtype, int loss_kind, const void* X, long long ldx,

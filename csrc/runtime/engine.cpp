@@ -123,6 +123,15 @@ struct GradLauncher {
   // gate: a lazy-drain worker round's stale-round gate (common.h gate_closed); nullptr = always run
   hipError_t launch(const void* beta, void* G, hipStream_t st, const int* gate = nullptr) const {
     if (!Gb) return launch_raw(beta, G, st, gate);
+    if (kind == 2 && sa.sub_begin) {  // row-blocked sparse pass: the encoding adds the sub-block sums
+      eh::SparseArgs a = sa;
+      a.Gb = Gb;
+      a.encode_from_subs = 1;
+      const hipError_t e = eh::grad_sparse_launch(acc, loss, a, beta, st, gate);
+      if (e != hipSuccess) return e;
+      return eh::encode_messages_launch(acc, sa.Gs, enc_ptr, enc_idx, enc_coef, G, enc_slots, ld, st, gate,
+                                        sa.sub_begin);
+    }
     const hipError_t e = launch_raw(beta, Gb, st, gate);
     if (e != hipSuccess) return e;
     return eh::encode_messages_launch(acc, Gb, enc_ptr, enc_idx, enc_coef, G, enc_slots, ld, st, gate);
