@@ -85,16 +85,16 @@ def test_sparse_grad_row_blocks(prec_name, tol, pattern_only, use_ell, native):
     d = 3000
     parts = {}
     for p, n in enumerate((9000, 4097, 300)):
-        cols = np.stack([rng.choice(d, 8, replace=False) for _ in range(n)])
-        cols[:, 0] = rng.choice(3, n)  # a few heavy columns: spans crossing tiles inside sub-blocks
-        cols = np.sort(cols, axis=1)
+        heavy = rng.choice(3, (n, 1))  # a few heavy columns: spans crossing tiles inside sub-blocks
+        rest = np.stack([3 + rng.choice(d - 3, 7, replace=False) for _ in range(n)])
+        cols = np.sort(np.concatenate([heavy, rest], axis=1), axis=1)
         vals = np.ones(cols.size) if pattern_only else rng.randn(cols.size)
         X = sps.csr_matrix((vals, cols.ravel(), np.arange(0, cols.size + 1, 8)), shape=(n, d))
-        X.sum_duplicates()
         parts[p] = (X, rng.choice([-1.0, 1.0], n))
     msgs = [[(0, 1.0), (1, 0.5)], [(2, -1.5), (0, 2.0)], [(1, 1.0)]]
     plan = SparseGradPlan(msgs, parts, prec, LOGISTIC, d, device=DEV, use_ell=use_ell)
     assert plan.nsub == 3 + 2 + 1 and plan.sub_begin is not None
+    assert plan.ell == use_ell and plan.pattern_only == pattern_only
     b = rng.randn(d) * 0.2
     beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
     beta[:d] = torch.from_numpy(b).to(prec.acc)
