@@ -1422,15 +1422,19 @@ static hipError_t launch_wide(int bs, int R, const Segment* segs, const Task* ta
   // instance: the unused half would still hold R + 3 register tiles (valid[] is a run-time mask),
   // which halves the resident workgroups per CU.
   const bool half = static_cast<long long>(bs) * (NV / 2) * Vec16<T>::N >= ld;
+  // fp32 / bf16 rows of <= 2048 columns (32 per lane) fit a quarter of the vectors
+  const bool quarter = NV >= 8 && static_cast<long long>(bs) * (NV / 4) * Vec16<T>::N >= ld;
 #define EH_WIDE(NV_, BS_, R_)                                                                                     \
   hipLaunchKernelGGL((grad_dense_wide<T, A, NV_, BS_, LOSS, R_>), grid, dim3(BS_), 0, st, segs, tasks, beta, slab, ld, \
                      gate)
-#define EH_WIDE_NV(BS_, R_)   \
-  do {                        \
-    if (half)                 \
-      EH_WIDE(NV / 2, BS_, R_); \
-    else                      \
-      EH_WIDE(NV, BS_, R_);   \
+#define EH_WIDE_NV(BS_, R_)       \
+  do {                            \
+    if (quarter)                  \
+      EH_WIDE(NV / 4, BS_, R_);   \
+    else if (half)                \
+      EH_WIDE(NV / 2, BS_, R_);   \
+    else                          \
+      EH_WIDE(NV, BS_, R_);       \
   } while (0)
   if (bs == 256 && R > 1 && !half) {
     // Replica bundles of full-width rows: 512 threads of NV / 2 vectors cover the same columns.  The
