@@ -274,7 +274,9 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
         return KernelChoice("multi", replicas=3, bundle_rows=pair_bundle_rows(distinct_rows, n_cus, prec_code == 1, cpl),
                             fold=True,
                             pair=True)
-    if prec_code == 0 and cpl == 32 and max_rep <= 3:
+    if cpl == 32 and max_rep <= 3 and (prec_code == 0 or (prec_code == 1 and not long_stream)):
+        # (fp32 d = 2048 short streams: the quarter-width instance, 1e5 rows 0.152 vs 0.158 ms staged,
+        # profiles/round4/r4o/choices.jsonl; long fp32 streams keep the staged bundles)
         # fp64 rows of 32 columns per lane (1024 < d <= 2048): 256-thread wide-row bundles (the
         # half-width instance) over the LDS-staged pair form: d = 2048 1e6 rows 2.466 vs 2.719 ms, 1e5
         # rows 0.268 vs 0.335 (profiles/round4/r4i/choices.jsonl)
@@ -294,11 +296,12 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
 def wide_slots_per_cu(prec_code: int, ld: int, replicas: int) -> int:
     """Resident wide-row bundles per CU (grad_dense.hip launch_wide): rows that fit half of the
     kernel's vectors at 256 threads (fp32 d <= 4096, bf16 <= 4096) take the NV / 2 instance, two or
-    more per CU; full-width replica rows (fp64 d > 2048, fp32 > 4096) run 512-thread workgroups of
-    about 150 VGPRs, one per CU."""
+    more per CU (fp32 d <= 2048: the NV / 4 instance, counted as four); full-width replica rows (fp64
+    d > 2048, fp32 > 4096) run 512-thread workgroups of about 150 VGPRs, one per CU."""
     vec = {0: 2, 1: 4, 2: 8}[prec_code]
     half = 256 * (WIDE_EPT[vec] // 2) >= ld
-    return 2 if replicas <= 1 or half else 1
+    quarter = prec_code == 1 and 256 * (WIDE_EPT[vec] // 4) >= ld  # fp32 d <= 2048: the quarter instance
+    return 4 if quarter else 2 if replicas <= 1 or half else 1
 
 
 def wide_bundle_rows(distinct_rows: int, n_cus: int = N_CUS, part_rows: Optional[Sequence[int]] = None,

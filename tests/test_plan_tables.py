@@ -99,7 +99,7 @@ def test_kernel_selection_table():
     assert pick(0, 2048, 3, 1_000_000) == KernelChoice("wide", replicas=3, bundle_rows=1968)
     assert pick(1, 2048, 3, 1_000_000) == KernelChoice("staged", replicas=3, bundle_rows=1024, pair=True)
     assert pick(0, 2048, 3, 100_000) == KernelChoice("wide", replicas=3, bundle_rows=208)
-    assert pick(1, 2048, 3, 100_000) == KernelChoice("staged", replicas=3, bundle_rows=128, pair=True, wpr=1)
+    assert pick(1, 2048, 3, 100_000) == KernelChoice("wide", replicas=3, bundle_rows=112)  # quarter-width rows
     # fp64 full-width replica rows run 512-thread workgroups, one resident per CU (wide_slots_per_cu)
     assert pick(0, 4096, 3, 1_000_000) == KernelChoice("wide", replicas=3, bundle_rows=3920)
     assert pick(1, 4096, 2, 100_000) == KernelChoice("wide", replicas=2, bundle_rows=208)
