@@ -94,9 +94,9 @@ constexpr int kEllMaxFields = 1024;
 
 template <typename A, int LOSS, bool IDX16, bool VALS>
 __global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A* __restrict__ beta, const int* gate) {
-  // one LDS-bound workgroup per CU (16 waves): a row's fields are loaded 32 at a time (covtype's 55
-  // in two batches), the window starts come from LDS
-  constexpr int KB = 32;
+  // one LDS-bound workgroup per CU (16 waves): two rows' fields are loaded 16 at a time (32 loads in
+  // flight per lane), the window starts come from LDS
+  constexpr int KB = VALS ? 8 : 16;  // (valued rows also hold their values: half the batch, no spills)
   extern __shared__ __attribute__((aligned(16))) unsigned char ell_lds[];
   A* sb = reinterpret_cast<A*>(ell_lds);
   __shared__ int slo[kEllMaxFields];  // the fields' window starts (idx16), read per lane from LDS
@@ -109,27 +109,42 @@ __global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A
   const int m = a.m;
   const A* __restrict__ vals = static_cast<const A*>(a.vals);
   const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
-  for (long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; row < n; row += stride) {
-    A z[4] = {A(0), A(0), A(0), A(0)};
-    auto idx = [&](int kk) -> int {
-      if constexpr (IDX16)
-        return static_cast<int>(__builtin_nontemporal_load(static_cast<const unsigned short*>(a.ell_idx) +
-                                                           static_cast<long long>(kk) * n + row));
-      else
-        return __builtin_nontemporal_load(static_cast<const int*>(a.ell_idx) + static_cast<long long>(kk) * n + row);
-    };
+  auto idx = [&](int kk, long long r) -> int {
+    if constexpr (IDX16)
+      return static_cast<int>(__builtin_nontemporal_load(static_cast<const unsigned short*>(a.ell_idx) +
+                                                         static_cast<long long>(kk) * n + r));
+    else
+      return __builtin_nontemporal_load(static_cast<const int*>(a.ell_idx) + static_cast<long long>(kk) * n + r);
+  };
+  // two rows per thread at a time (rows `row` and `row + stride`): twice the index loads in flight
+  // per wave -- the workgroup is alone on its CU (beta fills the LDS), so its 16 waves are all the
+  // latency hiding there is
+  for (long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; row < n; row += 2 * stride) {
+    const long long row1 = row + stride;
+    const bool two = row1 < n;
+    const long long r1 = two ? row1 : row;
+    A z[4] = {A(0), A(0), A(0), A(0)}, y[4] = {A(0), A(0), A(0), A(0)};
     for (int k0 = 0; k0 < m; k0 += KB) {
-      int c[KB];
+      int c[KB], e[KB];
 #pragma unroll
-      for (int u = 0; u < KB; ++u) c[u] = idx(min(k0 + u, m - 1));
+      for (int u = 0; u < KB; ++u) {
+        c[u] = idx(min(k0 + u, m - 1), row);
+        e[u] = idx(min(k0 + u, m - 1), r1);
+      }
 #pragma unroll
       for (int u = 0; u < KB; ++u)
-        if (k0 + u < m)
-          z[u & 3] = fma(VALS ? vals[static_cast<long long>(k0 + u) * n + row] : A(1),
-                         sb[(IDX16 ? slo[k0 + u] : 0) + c[u]], z[u & 3]);
+        if (k0 + u < m) {
+          const int lo = IDX16 ? slo[k0 + u] : 0;
+          z[u & 3] = fma(VALS ? vals[static_cast<long long>(k0 + u) * n + row] : A(1), sb[lo + c[u]], z[u & 3]);
+          y[u & 3] = fma(VALS ? vals[static_cast<long long>(k0 + u) * n + r1] : A(1), sb[lo + e[u]], y[u & 3]);
+        }
     }
     const A zz = (z[0] + z[1]) + (z[2] + z[3]);
     static_cast<A*>(a.u)[row] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[row], A(1));
+    if (two) {
+      const A yy = (y[0] + y[1]) + (y[2] + y[3]);
+      static_cast<A*>(a.u)[row1] = residual<LOSS, A>(yy, static_cast<const A*>(a.y)[row1], A(1));
+    }
   }
 }
 
