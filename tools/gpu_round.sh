@@ -14,6 +14,7 @@
 #   prof     rocprofv3 --kernel-trace --stats of the fp64 / fp32 / bf16 headline
 #   pmc      counter passes (one rocprofv3 --pmc run each) of the fp64 / fp32 headline
 #   eval     evaluation phase profile (tools/profile_eval.py)
+#   suite    tools/bench_suite.py (every BASELINE.json config)
 #   conv     tools/convergence_study.py (all schemes, drain and lazy rows)
 #   wide     the d = 2048 / 4096 rows of the sweep
 #   sparse   sparse gradients at the real-data shapes (timings, then rocprofv3 kernel stats)
@@ -134,6 +135,8 @@ for s in "${STAGES[@]}"; do
                # slab reduction forms 1 (fused put) and 2 (two-stage put)
       run 900 overhead.log env TAG=_r4 NO_BF16=1 MODES=on SLAB="1 2" bash tools/probes/overhead_tiny.sh
       cp -r gpurun_out/overhead_r4 "$OUT/" ;;
+    suite)  # every BASELINE.json config (tools/bench_suite.py)
+      run 1000 suite.log python -u tools/bench_suite.py --out "$OUT/suite" ;;
     conv)  # convergence vs wall-clock, every scheme incl. the lazy-drain rows (11 processes on the GPU)
       run 900 conv.log python -u tools/convergence_study.py --out "$OUT/convergence" ;;
     eval)
