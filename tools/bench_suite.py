@@ -68,6 +68,13 @@ def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_
     t0 = time.perf_counter()
     tr = Trainer(cfg, env, source)
     setup = time.perf_counter() - t0
+    if torch.cuda.is_available() and tr.local_msgs:
+        # ~150 ms of back-to-back gradients first: the clock ramps from idle over ~100 ms of streaming
+        # (profiles/round3/clocks), and 100 rounds of ~1 ms would otherwise be timed on the ramp
+        tw = time.perf_counter()
+        while time.perf_counter() - tw < 0.15:
+            tr.warmup()
+            torch.cuda.synchronize()
     res = tr.run(timed_start=timed_from)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
