@@ -165,81 +165,58 @@ __global__ void __launch_bounds__(256) csr_rows(const SparseArgs a, const A* __r
 }
 
 // ---- pass 2: CSC tiles, one wave per 512-entry tile ---------------------------------------------
-// A tile in three steps (loads issued / columns from the boundary walk / masked segmented sums
-// written), so a wave can keep a second tile's loads in flight while it works on its first.
-template <typename A>
-struct TileIn {
-  int p, base, c0, flags, n;
-  unsigned int rw[4];  // ROW16: 8 packed row indices; else rows 0-3 (rows 4-7 in rows4)
-  int rows4[4];
-  A cv[8];
-};
-
-// step 1: the tile's descriptor and this lane's 8 row indices / values, through buffer descriptors
-// (they count in vmcnt only: the LDS waits of the boundary walk do not wait for them; pointer loads
-// from the argument struct are flat loads, which count in lgkmcnt too).  Entries past n are the
-// sub-block's zero padding (row 0), masked in step 3.
-template <typename A, bool ROW16, bool VALS>
-__device__ __forceinline__ void tile_load(const SparseArgs& a, int t, TileIn<A>& T) {
+// The tile body: `gather(rows, v)` fills v[i] = u[rows[i]] (sub-block relative rows) -- from global
+// memory through a buffer descriptor, or from the workgroup's LDS copy of the sub-block's residuals.
+template <typename A, bool ROW16, bool VALS, typename Gather, typename Mid>
+__device__ __forceinline__ void tile_pass(const SparseArgs& a, int t, int* __restrict__ cw, Gather gather, Mid mid,
+                                          bool late_gather) {
   const int lane = threadIdx.x & 63;
   const int4 td = a.tiles[t];
-  T.p = td.x;
-  T.base = td.y;
-  T.c0 = td.z;
-  T.flags = td.w;
-  T.n = min(kTileEntries, a.part_nnz[T.p] - T.base);
+  const int p = td.x, base = td.y, c0 = td.z, flags = td.w;
+  const int nnz_p = a.part_nnz[p];
+  const int n = min(kTileEntries, nnz_p - base);
+  const int* __restrict__ cp = a.col_ptr + static_cast<long long>(p) * (a.d + 1);
+  // 0. this lane's 8 entries first -- row indices, values, the gathered residuals -- through buffer
+  //    descriptors (vmcnt only: the LDS waits of the boundary walk below do not wait for them;
+  //    pointer loads from the argument struct are flat loads, which count in lgkmcnt too).  Entries
+  //    past n are the sub-block's zero padding (row 0), masked below.
+  int rows[8];
   if constexpr (ROW16) {
-    const auto rs = make_rsrc(static_cast<const unsigned short*>(a.crow) + a.part_entry0[T.p] + T.base, 2 * kTileEntries);
+    const auto rs = make_rsrc(static_cast<const unsigned short*>(a.crow) + a.part_entry0[p] + base, 2 * kTileEntries);
     const uint4 r4 = buf_load16<uint4>(rs, 16 * lane);
-    T.rw[0] = r4.x, T.rw[1] = r4.y, T.rw[2] = r4.z, T.rw[3] = r4.w;
+    const unsigned int rw[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      rows[2 * i] = static_cast<int>(rw[i] & 0xffffu);
+      rows[2 * i + 1] = static_cast<int>(rw[i] >> 16);
+    }
   } else {
-    const auto rs = make_rsrc(static_cast<const int*>(a.crow) + a.part_entry0[T.p] + T.base, 4 * kTileEntries);
+    const auto rs = make_rsrc(static_cast<const int*>(a.crow) + a.part_entry0[p] + base, 4 * kTileEntries);
     const int4 x = buf_load16<int4>(rs, 32 * lane), y = buf_load16<int4>(rs, 32 * lane + 16);
-    T.rw[0] = x.x, T.rw[1] = x.y, T.rw[2] = x.z, T.rw[3] = x.w;
-    T.rows4[0] = y.x, T.rows4[1] = y.y, T.rows4[2] = y.z, T.rows4[3] = y.w;
+    rows[0] = x.x, rows[1] = x.y, rows[2] = x.z, rows[3] = x.w;
+    rows[4] = y.x, rows[5] = y.y, rows[6] = y.z, rows[7] = y.w;
   }
+  A cv[8];
   if constexpr (VALS) {
-    const auto vrs = make_rsrc(static_cast<const A*>(a.cvals) + a.part_entry0[T.p] + T.base,
+    const auto vrs = make_rsrc(static_cast<const A*>(a.cvals) + a.part_entry0[p] + base,
                                kTileEntries * static_cast<int>(sizeof(A)));
 #pragma unroll
-    for (int i = 0; i < 8; ++i) T.cv[i] = buf_load_scalar<A>(vrs, (8 * lane + i) * static_cast<int>(sizeof(A)));
+    for (int i = 0; i < 8; ++i) cv[i] = buf_load_scalar<A>(vrs, (8 * lane + i) * static_cast<int>(sizeof(A)));
   }
-}
-
-template <typename A, bool ROW16>
-__device__ __forceinline__ void tile_rows(const TileIn<A>& T, int (&rows)[8]) {
-  if constexpr (ROW16) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      rows[2 * i] = static_cast<int>(T.rw[i] & 0xffffu);
-      rows[2 * i + 1] = static_cast<int>(T.rw[i] >> 16);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      rows[i] = static_cast<int>(T.rw[i]);
-      rows[4 + i] = T.rows4[i];
-    }
-  }
-}
-
-// step 2: the column of each of this lane's 8 entries.  Column boundaries inside the tile:
-// cnt[q] = number of columns c > c0 starting at base + q (empty columns stack on the next non-empty
-// one's start; integer LDS adds, order-free), then c0 + the inclusive prefix of cnt.
-template <typename A>
-__device__ __forceinline__ void tile_keys(const SparseArgs& a, const TileIn<A>& T, int* __restrict__ cw,
-                                          int (&key)[8]) {
-  const int lane = threadIdx.x & 63;
-  const int* __restrict__ cp = a.col_ptr + static_cast<long long>(T.p) * (a.d + 1);
+  A v[8];
+  if (!late_gather) gather(p, rows, v);
+  // 1. column boundaries inside the tile: cnt[q] = number of columns c > c0 starting at base + q
+  //    (empty columns stack on the next non-empty one's start); integer LDS adds, order-free
 #pragma unroll
   for (int i = 0; i < kTileEntries / 64; ++i) cw[i * 64 + lane] = 0;
   __builtin_amdgcn_wave_barrier();
-  for (int c = T.c0 + 1 + lane;; c += 64) {
-    const bool in = c <= a.d && cp[min(c, a.d)] < T.base + T.n;
-    if (in) atomicAdd(&cw[cp[c] - T.base], 1);
+  for (int c = c0 + 1 + lane;; c += 64) {
+    const bool in = c <= a.d && cp[min(c, a.d)] < base + n;
+    if (in) atomicAdd(&cw[cp[c] - base], 1);
     if (__ballot(in) == 0) break;  // column starts are monotone: none further inside
   }
   __builtin_amdgcn_wave_barrier();
+  // 2. the column of each of this lane's 8 entries: c0 + inclusive prefix of cnt
   int cl[8];
   int run = 0;
 #pragma unroll
@@ -254,26 +231,22 @@ __device__ __forceinline__ void tile_keys(const SparseArgs& a, const TileIn<A>& 
     if (lane >= off) incl += vv;
   }
   const int before = incl - run;
+  int key[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) key[i] = T.c0 + before + cl[i];
-}
-
-// step 3: mask the padding, segmented sums (sequential inside the lane, then an affine Kogge-Stone
-// scan of (restart, sum) over the lanes), and every run end written: inside the tile by the lane
-// holding the column's last entry; a column reaching back into earlier tiles leaves head[t], one
-// going on in later tiles tail[t] (pass 3 adds them in tile order).
-template <typename A, bool VALS>
-__device__ __forceinline__ void tile_finish(const SparseArgs& a, int t, const TileIn<A>& T, const int (&key)[8],
-                                            A (&v)[8]) {
-  const int lane = threadIdx.x & 63;
-  const int n = T.n, c0 = T.c0, flags = T.flags;
+  for (int i = 0; i < 8; ++i) key[i] = c0 + before + cl[i];
+  if (late_gather) {  // the LDS path: the staged residuals are published by mid() (a block barrier)
+    mid();
+    gather(p, rows, v);
+  }
+  // 3. mask the padding
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const bool ok = 8 * lane + i < n;
     A x = ok ? v[i] : A(0);
-    if constexpr (VALS) x *= ok ? T.cv[i] : A(0);
+    if constexpr (VALS) x *= ok ? cv[i] : A(0);
     v[i] = x;
   }
+  // 4. segmented sums: sequential inside the lane, then over the lanes
   A s[8];
   s[0] = v[0];
 #pragma unroll
@@ -295,7 +268,7 @@ __device__ __forceinline__ void tile_finish(const SparseArgs& a, int t, const Ti
   const A prev_run = __shfl_up(b, 1, 64);
   const A carry = (lane > 0 && prev_last == key[0]) ? prev_run : A(0);
   const int next_first = __shfl_down(key[0], 1, 64);
-  A* __restrict__ gout = static_cast<A*>(a.Gs) + static_cast<long long>(T.p) * a.ld;
+  A* __restrict__ gout = static_cast<A*>(a.Gs) + static_cast<long long>(p) * a.ld;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int q = 8 * lane + i;
@@ -311,83 +284,66 @@ __device__ __forceinline__ void tile_finish(const SparseArgs& a, int t, const Ti
   }
 }
 
-// One wave per tile, residuals gathered from global memory (used when there is no workgroup table).
+// One wave per tile, residuals gathered from global memory (one partition = one sub-block).
 template <typename A, bool ROW16, bool VALS>
 __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* gate) {
   __shared__ int cnt[4][kTileEntries];
   if (gate_closed(gate)) return;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= a.ntiles) return;  // wave-uniform; only wave barriers below
-  TileIn<A> T;
-  tile_load<A, ROW16, VALS>(a, t, T);
-  int rows[8];
-  tile_rows<A, ROW16>(T, rows);
-  const long long r0 = a.part_row0[T.p];
-  const long long ubytes = (a.nrows - r0) * static_cast<long long>(sizeof(A));
-  const auto urs = make_rsrc(static_cast<const A*>(a.u) + r0, static_cast<int>(min(ubytes, static_cast<long long>(INT_MAX))));
-  A v[8];
+  tile_pass<A, ROW16, VALS>(a, t, cnt[threadIdx.x >> 6], [&](int p, const int (&rows)[8], A (&v)[8]) {
+    const long long r0 = a.part_row0[p];
+    const long long ubytes = (a.nrows - r0) * static_cast<long long>(sizeof(A));
+    const auto urs = make_rsrc(static_cast<const A*>(a.u) + r0, static_cast<int>(min(ubytes, static_cast<long long>(INT_MAX))));
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = buf_load_scalar<A>(urs, rows[i] * static_cast<int>(sizeof(A)));
-  int key[8];
-  tile_keys<A>(a, T, cnt[threadIdx.x >> 6], key);
-  tile_finish<A, VALS>(a, t, T, key, v);
+    for (int i = 0; i < 8; ++i) v[i] = buf_load_scalar<A>(urs, rows[i] * static_cast<int>(sizeof(A)));
+  }, [] {}, false);
 }
 
-// Row-blocked column pass, two tiles per wave: 512-thread workgroups (8 waves, up to 16 tiles of ONE
-// sub-block, a.wg), three resident per CU (48 KB of LDS each).  Gathered from global memory, each
-// 8-byte residual read pulled a 128-byte L2 line into L1 with no reuse (a column's rows spread over
-// the partition): ~2.8 GB of L2 -> L1 traffic, 88-92 us at covtype's shape (profiles/round4/r4g).
-// Here the sub-block's residuals are loaded into registers first and published to LDS by one barrier
-// once the first tile's columns are known, and a wave issues its second tile's loads before it works
-// on the first, so that tile's HBM latency hides behind the first's work.  (One tile per wave in
-// 1024-thread workgroups measured 47-50 us; three per wave in turn 67-71 us: more than 64 VGPRs.)
-constexpr int kPfWaves = 8;
-constexpr int kPfStage = 8;  // residuals staged per thread: 4096 rows / 512 threads
+// Row-blocked column pass: a 1024-thread workgroup takes up to kWgTiles tiles of ONE sub-block (a.wg) and
+// first copies that sub-block's residuals into LDS (coalesced), so every gather is an LDS read.  From
+// global memory each 8-byte gather pulled a 128-byte L2 line into L1 with no reuse (rows of a column
+// are spread over the partition): covtype's 21.8M gathers moved ~2.8 GB L2 -> L1, 88-92 us
+// (profiles/round4/r4g, r4i).
+constexpr int kWgTiles = 16;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES), one per wave
+constexpr int kStageRegs = 4;  // staged residuals per thread: 4096 rows per sub-block (32 KB fp64 / 16 KB fp32)
 template <typename A, bool ROW16, bool VALS>
-__global__ void __launch_bounds__(512) csc_tiles_pf(const SparseArgs a, const int* gate) {
-  __shared__ int cnt[kPfWaves][kTileEntries];
-  extern __shared__ __attribute__((aligned(16))) unsigned char upf_raw[];
-  A* su = reinterpret_cast<A*>(upf_raw);
+__global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const int* gate) {
+  __shared__ int cnt[16][kTileEntries];
+  extern __shared__ __attribute__((aligned(16))) unsigned char usub_raw[];
+  A* su = reinterpret_cast<A*>(usub_raw);
   if (gate_closed(gate)) return;
-  const int4 wd = a.wg[blockIdx.x];  // (sub-block, first tile, tiles <= 16, rows)
+  const int4 wd = a.wg[blockIdx.x];  // (sub-block, first tile, tiles, rows)
+  // the sub-block's residuals: loaded into registers first, stored to LDS only after this wave's
+  // tile has its row indices and column boundaries (step 0-2 of tile_pass), so the staging latency
+  // overlaps those loads instead of preceding them
   const A* __restrict__ ug = static_cast<const A*>(a.u) + a.part_row0[wd.x];
-  A st[kPfStage];
+  A st[kStageRegs];
 #pragma unroll
-  for (int j = 0; j < kPfStage; ++j) {
+  for (int j = 0; j < kStageRegs; ++j) {
     const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
     st[j] = i < wd.w ? ug[i] : A(0);
   }
-  const int w = threadIdx.x >> 6;
-  const bool hasA = w < wd.z, hasB = w + kPfWaves < wd.z;
-  TileIn<A> TA, TB;
-  if (hasA) tile_load<A, ROW16, VALS>(a, wd.y + w, TA);
-  if (hasB) tile_load<A, ROW16, VALS>(a, wd.y + w + kPfWaves, TB);
-  int keyA[8];
-  if (hasA) tile_keys<A>(a, TA, cnt[w], keyA);
+  auto publish = [&] {
 #pragma unroll
-  for (int j = 0; j < kPfStage; ++j) {  // publish the residuals (every wave reaches the barrier)
-    const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
-    if (i < wd.w) su[i] = st[j];
+    for (int j = 0; j < kStageRegs; ++j) {
+      const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
+      if (i < wd.w) su[i] = st[j];
+    }
+    __syncthreads();
+  };
+  const int w = threadIdx.x >> 6;
+  if (w >= wd.z) {  // no tile for this wave: it still stages and joins the one barrier
+    publish();
+    return;
   }
-  __syncthreads();
-  auto gather = [&](const TileIn<A>& T, A (&v)[8]) {
-    int rows[8];
-    tile_rows<A, ROW16>(T, rows);
+  // one tile per wave: a loop over several (48 tiles per workgroup, 3 per wave) needed more than 64
+  // VGPRs, one resident workgroup per CU instead of two, and measured 66.8-70.5 vs 47 us at covtype's
+  // shape (profiles/round4/r4k, r4l)
+  tile_pass<A, ROW16, VALS>(a, wd.y + w, cnt[w], [&](int, const int (&rows)[8], A (&v)[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = su[min(rows[i], wd.w - 1)];  // (padding rows are 0; clamp an empty sub-block)
-  };
-  if (hasA) {
-    A v[8];
-    gather(TA, v);
-    tile_finish<A, VALS>(a, wd.y + w, TA, keyA, v);
-  }
-  if (hasB) {
-    int keyB[8];
-    tile_keys<A>(a, TB, cnt[w], keyB);
-    A v[8];
-    gather(TB, v);
-    tile_finish<A, VALS>(a, wd.y + w + kPfWaves, TB, keyB, v);
-  }
+  }, publish, true);
 }
 
 // Sub-block sums added per partition in sub-block order: Gb[j][c] = sum_s Gs[s][c].
@@ -497,14 +453,14 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
   }
   if (a.ntiles > 0 && a.wg) {
     const size_t ulds = static_cast<size_t>(std::max(a.u_lds, 1)) * (dtype == 0 ? 8 : 4);
-    if (a.u_lds > kPfStage * kPfWaves * 64) return hipErrorInvalidValue;  // (sub-blocks of at most 4096 rows)
+    if (a.u_lds > kStageRegs * 1024) return hipErrorInvalidValue;  // (sub-blocks of at most 4096 rows)
     const dim3 grid(static_cast<unsigned>(a.nwg));
 #define EH_TLDS(A_, R_, V_)                                                                                    \
   {                                                                                                            \
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(csc_tiles_pf<A_, R_, V_>),           \
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(csc_tiles_lds<A_, R_, V_>),          \
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ulds)); \
     if (e != hipSuccess) return e;                                                                             \
-    hipLaunchKernelGGL((csc_tiles_pf<A_, R_, V_>), grid, dim3(kPfWaves * 64), ulds, st, a, gate);               \
+    hipLaunchKernelGGL((csc_tiles_lds<A_, R_, V_>), grid, dim3(1024), ulds, st, a, gate);                       \
   }
 #define EH_TILES(A_)                                                                    \
   if (a.row16) {                                                                        \
