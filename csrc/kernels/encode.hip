@@ -34,8 +34,21 @@ encode_messages(const A* __restrict__ Gb, const int* __restrict__ ptr, const int
   for (int k = b; k < e; ++k) {
     A g;
     if (sub_begin) {
+      // the sub-block rows four loads at a time, added in row order (bitwise the serial loop; a
+      // partition of covtype's shape has 13 of them: one dependent load each was ~6 us)
       g = A(0);
-      for (int q = sub_begin[idx[k]]; q < sub_begin[idx[k] + 1]; ++q) g += Gb[static_cast<long long>(q) * ld + c];
+      int q = sub_begin[idx[k]];
+      const int q1 = sub_begin[idx[k] + 1];
+      const A* __restrict__ col = Gb + c;
+      for (; q + 4 <= q1; q += 4) {
+        const A x0 = col[static_cast<long long>(q) * ld], x1 = col[static_cast<long long>(q + 1) * ld];
+        const A x2 = col[static_cast<long long>(q + 2) * ld], x3 = col[static_cast<long long>(q + 3) * ld];
+        g += x0;
+        g += x1;
+        g += x2;
+        g += x3;
+      }
+      for (; q < q1; ++q) g += col[static_cast<long long>(q) * ld];
     } else {
       g = Gb[static_cast<long long>(idx[k]) * ld + c];
     }

@@ -27,6 +27,7 @@
 // passes added into g with atomics: profiles/round3/suite_nt, round-3 verdict Weak #3).
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 
 #include "common.h"
 #include "launchers.h"
@@ -50,7 +51,7 @@ __global__ void __launch_bounds__(256) ell_rows(const SparseArgs a, const A* __r
   if (gate_closed(gate)) return;
   const long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (row >= a.nrows) return;
-  const long long n = a.nrows;
+  const long long n = a.ell_ld;  // row stride of the [m][rows] index / value arrays
   const int m = a.m;
   const A* __restrict__ vals = static_cast<const A*>(a.vals);
   A z[4] = {A(0), A(0), A(0), A(0)};
@@ -88,62 +89,110 @@ __global__ void __launch_bounds__(256) ell_rows(const SparseArgs a, const A* __r
 // fp64).  Gathered from global memory, each 8-byte beta read pulled a 128-byte L2 line into a 32 KB L1
 // that the fields' windows (55 per row) keep thrashing: 21.8M gathers, ~2.8 GB of L2 -> L1 traffic,
 // 38-41 us (profiles/round4/r4g, r4i).  From LDS they cost a few cycles.  One 1024-thread workgroup per
-// CU (the LDS copy of beta is per workgroup), rows strided over the grid.
+// CU (the LDS copy of beta is per workgroup).
+//
+// A thread takes a PAIR of adjacent rows: the [m][rows] arrays have an even row stride (ops/grad.py
+// pads them), so one 4-byte load brings both rows' 16-bit offsets of a field (8 bytes of int32
+// columns, 2 values) -- half the load instructions of a row per thread, twice the bytes each.  The
+// next batch of fields (or the next pair's first batch) is in flight while this one is gathered, and
+// the first batch is issued before beta is staged; the staging itself issues all of a thread's
+// loads (16-byte vectors) before its first LDS store.
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kEllLdsBytes = 148 * 1024;
 constexpr int kEllMaxFields = 1024;
+constexpr int kEllStageVecs = (kEllLdsBytes / 16 + 1023) / 1024;  // 16-byte staging loads per thread
 
 template <typename A, int LOSS, bool IDX16, bool VALS>
 __global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A* __restrict__ beta, const int* gate) {
-  // one LDS-bound workgroup per CU (16 waves): two rows' fields are loaded 16 at a time (32 loads in
-  // flight per lane), the window starts come from LDS
-  constexpr int KB = VALS ? 8 : 16;  // (valued rows also hold their values: half the batch, no spills)
+  // fields per batch: two batches (this one and the next) of loads stay within 128 VGPRs, no spills
+  constexpr int KB = VALS ? 4 : IDX16 ? 16 : 8;
+  using IW = std::conditional_t<IDX16, unsigned int, i32x2>;                    // a field of a row pair
+  using V2 = std::conditional_t<sizeof(A) == 8, f64x2, f32x2>;                   // its two values
+  using V4 = std::conditional_t<sizeof(A) == 8, f64x2, f32x4>;                   // a 16-byte staging vector
   extern __shared__ __attribute__((aligned(16))) unsigned char ell_lds[];
   A* sb = reinterpret_cast<A*>(ell_lds);
   __shared__ int slo[kEllMaxFields];  // the fields' window starts (idx16), read per lane from LDS
   if (gate_closed(gate)) return;
-  for (int c = threadIdx.x; c < a.d; c += blockDim.x) sb[c] = beta[c];
-  if (IDX16)
-    for (int k = threadIdx.x; k < a.m && k < kEllMaxFields; k += blockDim.x) slo[k] = a.lo[k];
-  __syncthreads();
-  const long long n = a.nrows;
+  const long long n = a.nrows, ld = a.ell_ld;
   const int m = a.m;
-  const A* __restrict__ vals = static_cast<const A*>(a.vals);
+  const long long npair = (n + 1) >> 1;
   const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
-  auto idx = [&](int kk, long long r) -> int {
-    if constexpr (IDX16)
-      return static_cast<int>(__builtin_nontemporal_load(static_cast<const unsigned short*>(a.ell_idx) +
-                                                         static_cast<long long>(kk) * n + r));
-    else
-      return __builtin_nontemporal_load(static_cast<const int*>(a.ell_idx) + static_cast<long long>(kk) * n + r);
+  const IW* __restrict__ idx = static_cast<const IW*>(a.ell_idx);  // [m][ld / 2] row pairs
+  const V2* __restrict__ vals = static_cast<const V2*>(a.vals);
+  const long long ldp = ld >> 1;
+  auto load = [&](IW (&w)[KB], V2 (&v)[KB], long long q, int k0) {
+    const long long qq = min(q, npair - 1);  // (past the last pair: a valid, unused address)
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      const long long o = static_cast<long long>(min(k0 + u, m - 1)) * ldp + qq;
+      w[u] = __builtin_nontemporal_load(idx + o);
+      if constexpr (VALS) v[u] = __builtin_nontemporal_load(vals + o);
+    }
   };
-  // two rows per thread at a time (rows `row` and `row + stride`): twice the index loads in flight
-  // per wave -- the workgroup is alone on its CU (beta fills the LDS), so its 16 waves are all the
-  // latency hiding there is
-  for (long long row = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; row < n; row += 2 * stride) {
-    const long long row1 = row + stride;
-    const bool two = row1 < n;
-    const long long r1 = two ? row1 : row;
+  long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  {  // stage beta (and the window starts): every load of this thread in flight before its stores
+    const int nv = a.d * static_cast<int>(sizeof(A)) / 16;
+    const V4* __restrict__ bv = reinterpret_cast<const V4*>(beta);
+    V4 t[kEllStageVecs];
+#pragma unroll
+    for (int j = 0; j < kEllStageVecs; ++j) {
+      const int i = threadIdx.x + j * 1024;
+      if (i < nv) t[j] = bv[i];
+    }
+    int lo = 0;
+    if (IDX16 && static_cast<int>(threadIdx.x) < m) lo = a.lo[threadIdx.x];
+    const int tail0 = nv * 16 / static_cast<int>(sizeof(A));
+    A tl = A(0);
+    if (static_cast<int>(threadIdx.x) < a.d - tail0) tl = beta[tail0 + threadIdx.x];
+#pragma unroll
+    for (int j = 0; j < kEllStageVecs; ++j) {
+      const int i = threadIdx.x + j * 1024;
+      if (i < nv) reinterpret_cast<V4*>(sb)[i] = t[j];
+    }
+    if (static_cast<int>(threadIdx.x) < a.d - tail0) sb[tail0 + threadIdx.x] = tl;
+    if (IDX16 && static_cast<int>(threadIdx.x) < m) slo[threadIdx.x] = lo;
+  }
+  __syncthreads();
+  IW w[KB];
+  V2 v[KB];
+  load(w, v, q, 0);
+  for (; q < npair; q += stride) {
     A z[4] = {A(0), A(0), A(0), A(0)}, y[4] = {A(0), A(0), A(0), A(0)};
     for (int k0 = 0; k0 < m; k0 += KB) {
-      int c[KB], e[KB];
-#pragma unroll
-      for (int u = 0; u < KB; ++u) {
-        c[u] = idx(min(k0 + u, m - 1), row);
-        e[u] = idx(min(k0 + u, m - 1), r1);
-      }
+      IW wn[KB];
+      V2 vn[KB];
+      if (k0 + KB < m) load(wn, vn, q, k0 + KB);  // the next batch, or the next pair's first
+      else load(wn, vn, q + stride, 0);
 #pragma unroll
       for (int u = 0; u < KB; ++u)
         if (k0 + u < m) {
           const int lo = IDX16 ? slo[k0 + u] : 0;
-          z[u & 3] = fma(VALS ? vals[static_cast<long long>(k0 + u) * n + row] : A(1), sb[lo + c[u]], z[u & 3]);
-          y[u & 3] = fma(VALS ? vals[static_cast<long long>(k0 + u) * n + r1] : A(1), sb[lo + e[u]], y[u & 3]);
+          int c0, c1;
+          if constexpr (IDX16) {
+            c0 = static_cast<int>(w[u] & 0xffffu);
+            c1 = static_cast<int>(w[u] >> 16);
+          } else {
+            c0 = w[u].x;
+            c1 = w[u].y;
+          }
+          z[u & 3] = fma(VALS ? v[u].x : A(1), sb[lo + c0], z[u & 3]);
+          y[u & 3] = fma(VALS ? v[u].y : A(1), sb[lo + c1], y[u & 3]);
         }
+#pragma unroll
+      for (int u = 0; u < KB; ++u) {
+        w[u] = wn[u];
+        if constexpr (VALS) v[u] = vn[u];
+      }
     }
+    const long long r = 2 * q;
     const A zz = (z[0] + z[1]) + (z[2] + z[3]);
-    static_cast<A*>(a.u)[row] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[row], A(1));
-    if (two) {
+    static_cast<A*>(a.u)[r] = residual<LOSS, A>(zz, static_cast<const A*>(a.y)[r], A(1));
+    if (r + 1 < n) {
       const A yy = (y[0] + y[1]) + (y[2] + y[3]);
-      static_cast<A*>(a.u)[row1] = residual<LOSS, A>(yy, static_cast<const A*>(a.y)[row1], A(1));
+      static_cast<A*>(a.u)[r + 1] = residual<LOSS, A>(yy, static_cast<const A*>(a.y)[r + 1], A(1));
     }
   }
 }
@@ -165,80 +214,70 @@ __global__ void __launch_bounds__(256) csr_rows(const SparseArgs a, const A* __r
 }
 
 // ---- pass 2: CSC tiles, one wave per 512-entry tile ---------------------------------------------
-// The tile body: `gather(rows, v)` fills v[i] = u[rows[i]] (sub-block relative rows) -- from global
-// memory through a buffer descriptor, or from the workgroup's LDS copy of the sub-block's residuals.
-template <typename A, bool ROW16, bool VALS, typename Gather, typename Mid>
-__device__ __forceinline__ void tile_pass(const SparseArgs& a, int t, int* __restrict__ cw, Gather gather, Mid mid,
-                                          bool late_gather) {
+// Row indices carry a run-start flag in their top bit (bit 15 of 16-bit rows, bit 31 of 32-bit ones):
+// set on the first entry of every column and of every tile (ops/grad.py csc_tables).  Tile t's
+// entries are crow[512 t, 512 t + 512) (every partition is padded to whole tiles).
+template <bool ROW16>
+__device__ __forceinline__ unsigned tile_rows(const SparseArgs& a, int t, int (&rows)[8]) {
   const int lane = threadIdx.x & 63;
-  const int4 td = a.tiles[t];
-  const int p = td.x, base = td.y, c0 = td.z, flags = td.w;
-  const int nnz_p = a.part_nnz[p];
-  const int n = min(kTileEntries, nnz_p - base);
-  const int* __restrict__ cp = a.col_ptr + static_cast<long long>(p) * (a.d + 1);
-  // 0. this lane's 8 entries first -- row indices, values, the gathered residuals -- through buffer
-  //    descriptors (vmcnt only: the LDS waits of the boundary walk below do not wait for them;
-  //    pointer loads from the argument struct are flat loads, which count in lgkmcnt too).  Entries
-  //    past n are the sub-block's zero padding (row 0), masked below.
-  int rows[8];
+  unsigned fl = 0;  // bit i: entry 8 * lane + i starts a run
   if constexpr (ROW16) {
-    const auto rs = make_rsrc(static_cast<const unsigned short*>(a.crow) + a.part_entry0[p] + base, 2 * kTileEntries);
+    const auto rs = make_rsrc(static_cast<const unsigned short*>(a.crow) + static_cast<long long>(t) * kTileEntries,
+                              2 * kTileEntries);
     const uint4 r4 = buf_load16<uint4>(rs, 16 * lane);
     const unsigned int rw[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      rows[2 * i] = static_cast<int>(rw[i] & 0xffffu);
-      rows[2 * i + 1] = static_cast<int>(rw[i] >> 16);
+      rows[2 * i] = static_cast<int>(rw[i] & 0x7fffu);
+      rows[2 * i + 1] = static_cast<int>((rw[i] >> 16) & 0x7fffu);
+      fl |= ((rw[i] >> 15) & 1u) << (2 * i);
+      fl |= (rw[i] >> 31) << (2 * i + 1);
     }
   } else {
-    const auto rs = make_rsrc(static_cast<const int*>(a.crow) + a.part_entry0[p] + base, 4 * kTileEntries);
+    const auto rs = make_rsrc(static_cast<const int*>(a.crow) + static_cast<long long>(t) * kTileEntries,
+                              4 * kTileEntries);
     const int4 x = buf_load16<int4>(rs, 32 * lane), y = buf_load16<int4>(rs, 32 * lane + 16);
-    rows[0] = x.x, rows[1] = x.y, rows[2] = x.z, rows[3] = x.w;
-    rows[4] = y.x, rows[5] = y.y, rows[6] = y.z, rows[7] = y.w;
+    const int r[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      rows[i] = r[i] & 0x7fffffff;
+      fl |= (static_cast<unsigned>(r[i]) >> 31) << i;
+    }
   }
-  A cv[8];
+  return fl;
+}
+
+template <typename A, bool VALS>
+__device__ __forceinline__ void tile_vals(const SparseArgs& a, int t, A (&cv)[8]) {
   if constexpr (VALS) {
-    const auto vrs = make_rsrc(static_cast<const A*>(a.cvals) + a.part_entry0[p] + base,
+    const int lane = threadIdx.x & 63;
+    const auto vrs = make_rsrc(static_cast<const A*>(a.cvals) + static_cast<long long>(t) * kTileEntries,
                                kTileEntries * static_cast<int>(sizeof(A)));
 #pragma unroll
     for (int i = 0; i < 8; ++i) cv[i] = buf_load_scalar<A>(vrs, (8 * lane + i) * static_cast<int>(sizeof(A)));
   }
-  A v[8];
-  if (!late_gather) gather(p, rows, v);
-  // 1. column boundaries inside the tile: cnt[q] = number of columns c > c0 starting at base + q
-  //    (empty columns stack on the next non-empty one's start); integer LDS adds, order-free
-#pragma unroll
-  for (int i = 0; i < kTileEntries / 64; ++i) cw[i * 64 + lane] = 0;
-  __builtin_amdgcn_wave_barrier();
-  for (int c = c0 + 1 + lane;; c += 64) {
-    const bool in = c <= a.d && cp[min(c, a.d)] < base + n;
-    if (in) atomicAdd(&cw[cp[c] - base], 1);
-    if (__ballot(in) == 0) break;  // column starts are monotone: none further inside
-  }
-  __builtin_amdgcn_wave_barrier();
-  // 2. the column of each of this lane's 8 entries: c0 + inclusive prefix of cnt
-  int cl[8];
-  int run = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    run += cw[8 * lane + i];
-    cl[i] = run;
-  }
-  int incl = run;  // wave inclusive scan of the lane totals
+}
+
+// Wave exclusive prefix of the lane totals `run` (cl: this lane's inclusive counts)
+__device__ __forceinline__ int wave_before(int run) {
+  const int lane = threadIdx.x & 63;
+  int incl = run;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const int vv = __shfl_up(incl, off, 64);
     if (lane >= off) incl += vv;
   }
-  const int before = incl - run;
-  int key[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) key[i] = c0 + before + cl[i];
-  if (late_gather) {  // the LDS path: the staged residuals are published by mid() (a block barrier)
-    mid();
-    gather(p, rows, v);
-  }
-  // 3. mask the padding
+  return incl - run;
+}
+
+// The tile's tail end, shared by both column passes: mask the padding, then the segmented sums of
+// the 8 entries per lane keyed by column, each run written once (Gs, or head / tail when the column
+// crosses tiles).  key[i] is the column of entry 8 * lane + i; v[i] its gathered residual.
+template <typename A, bool VALS>
+__device__ __forceinline__ void tile_finish(const SparseArgs& a, int t, int p, int n, int c0, int flags,
+                                            const int (&key)[8], A (&v)[8], const A (&cv)[8]) {
+  const int lane = threadIdx.x & 63;
+  // mask the padding
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const bool ok = 8 * lane + i < n;
@@ -246,7 +285,7 @@ __device__ __forceinline__ void tile_pass(const SparseArgs& a, int t, int* __res
     if constexpr (VALS) x *= ok ? cv[i] : A(0);
     v[i] = x;
   }
-  // 4. segmented sums: sequential inside the lane, then over the lanes
+  // segmented sums: sequential inside the lane, then over the lanes
   A s[8];
   s[0] = v[0];
 #pragma unroll
@@ -284,6 +323,51 @@ __device__ __forceinline__ void tile_pass(const SparseArgs& a, int t, int* __res
   }
 }
 
+// Walked boundaries (one partition = one sub-block, residuals gathered from global memory): the wave
+// finds every entry's column from the partition's column pointers -- an integer count in LDS, then a
+// scan.  `gather(p, rows, v)` fills v[i] = u[rows[i]].
+template <typename A, bool ROW16, bool VALS, typename Gather>
+__device__ __forceinline__ void tile_pass(const SparseArgs& a, int t, int* __restrict__ cw, Gather gather) {
+  const int lane = threadIdx.x & 63;
+  const int4 td = a.tiles[t];
+  const int p = td.x, base = td.y, c0 = td.z, flags = td.w;
+  const int n = min(kTileEntries, a.part_nnz[p] - base);
+  const int* __restrict__ cp = a.col_ptr + static_cast<long long>(p) * (a.d + 1);
+  // 0. this lane's 8 entries first -- row indices, values, the gathered residuals -- through buffer
+  //    descriptors (vmcnt only: the LDS waits of the boundary walk below do not wait for them).
+  //    Entries past n are the partition's zero padding (row 0), masked in tile_finish.
+  int rows[8];
+  tile_rows<ROW16>(a, t, rows);
+  A cv[8];
+  tile_vals<A, VALS>(a, t, cv);
+  A v[8];
+  gather(p, rows, v);
+  // 1. column boundaries inside the tile: cnt[q] = number of columns c > c0 starting at base + q
+  //    (empty columns stack on the next non-empty one's start); integer LDS adds, order-free
+#pragma unroll
+  for (int i = 0; i < kTileEntries / 64; ++i) cw[i * 64 + lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  for (int c = c0 + 1 + lane;; c += 64) {
+    const bool in = c <= a.d && cp[min(c, a.d)] < base + n;
+    if (in) atomicAdd(&cw[cp[c] - base], 1);
+    if (__ballot(in) == 0) break;  // column starts are monotone: none further inside
+  }
+  __builtin_amdgcn_wave_barrier();
+  // 2. the column of each of this lane's 8 entries: c0 + inclusive prefix of cnt
+  int cl[8];
+  int run = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    run += cw[8 * lane + i];
+    cl[i] = run;
+  }
+  const int before = wave_before(run);
+  int key[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) key[i] = c0 + before + cl[i];
+  tile_finish<A, VALS>(a, t, p, n, c0, flags, key, v, cv);
+}
+
 // One wave per tile, residuals gathered from global memory (one partition = one sub-block).
 template <typename A, bool ROW16, bool VALS>
 __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* gate) {
@@ -297,7 +381,7 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
     const auto urs = make_rsrc(static_cast<const A*>(a.u) + r0, static_cast<int>(min(ubytes, static_cast<long long>(INT_MAX))));
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = buf_load_scalar<A>(urs, rows[i] * static_cast<int>(sizeof(A)));
-  }, [] {}, false);
+  });
 }
 
 // Row-blocked column pass: a 1024-thread workgroup takes up to kWgTiles tiles of ONE sub-block (a.wg) and
@@ -305,45 +389,70 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
 // global memory each 8-byte gather pulled a 128-byte L2 line into L1 with no reuse (rows of a column
 // are spread over the partition): covtype's 21.8M gathers moved ~2.8 GB L2 -> L1, 88-92 us
 // (profiles/round4/r4g, r4i).
+//
+// The columns come from the run-start flags and the tile's run list (a.runs[tk.x ...]: the column of
+// each run, in order) instead of a walk over the column pointers: the rows, the run list and the staged
+// residuals are all one load away from the workgroup's descriptor, where the walk waited on the tile
+// descriptor, then the partition's entry offset and column pointers, then the LDS counts (the
+// workgroup's lifetime is a chain of dependent loads: the pass is latency-bound, profiles/round4/r4q).
 constexpr int kWgTiles = 16;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES), one per wave
 constexpr int kStageRegs = 4;  // staged residuals per thread: 4096 rows per sub-block (32 KB fp64 / 16 KB fp32)
 template <typename A, bool ROW16, bool VALS>
 __global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const int* gate) {
-  __shared__ int cnt[16][kTileEntries];
+  __shared__ int runs_lds[16][kTileEntries];
   extern __shared__ __attribute__((aligned(16))) unsigned char usub_raw[];
   A* su = reinterpret_cast<A*>(usub_raw);
   if (gate_closed(gate)) return;
-  const int4 wd = a.wg[blockIdx.x];  // (sub-block, first tile, tiles, rows)
-  // the sub-block's residuals: loaded into registers first, stored to LDS only after this wave's
-  // tile has its row indices and column boundaries (step 0-2 of tile_pass), so the staging latency
-  // overlaps those loads instead of preceding them
-  const A* __restrict__ ug = static_cast<const A*>(a.u) + a.part_row0[wd.x];
+  const int4 wd = a.wg[blockIdx.x];  // (first row of the sub-block, first tile, tiles, rows)
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = wd.y + min(w, max(wd.z - 1, 0));  // (a wave past the chunk's tiles only stages)
+  // the wave's rows and values first, then the sub-block's residuals into registers: stored to LDS
+  // after the keys, so the staging latency overlaps the rest of the tile's loads
+  int rows[8];
+  const unsigned fl = tile_rows<ROW16>(a, t, rows);
+  A cv[8];
+  tile_vals<A, VALS>(a, t, cv);
+  const A* __restrict__ ug = static_cast<const A*>(a.u) + wd.x;
   A st[kStageRegs];
 #pragma unroll
   for (int j = 0; j < kStageRegs; ++j) {
     const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
     st[j] = i < wd.w ? ug[i] : A(0);
   }
-  auto publish = [&] {
+  const int4 tk = a.tkeys[t];  // (first run, n | runs << 10 | span flags << 20, sub-block, first column)
+  const int n = tk.y & 1023, nruns = (tk.y >> 10) & 1023, flags = tk.y >> 20, p = tk.z, c0 = tk.w;
+  // the tile's run list into this wave's LDS row (at most 512 runs)
+  int* __restrict__ rl = runs_lds[w];
+  const auto rrs = make_rsrc(a.runs + tk.x, 4 * nruns);
+  const int ra = buf_load_scalar<int>(rrs, 4 * lane), rb = buf_load_scalar<int>(rrs, 4 * (lane + 64));
+  rl[lane] = ra;
+  rl[lane + 64] = rb;
+  for (int j = 128 + lane; j < nruns; j += 64) rl[j] = buf_load_scalar<int>(rrs, 4 * j);
+  // the run of each of this lane's 8 entries: the wave prefix of the flags (the tile's first entry
+  // is always flagged, padding entries are not: they join the last run and are masked)
+  int cl[8];
+  int run = 0;
 #pragma unroll
-    for (int j = 0; j < kStageRegs; ++j) {
-      const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
-      if (i < wd.w) su[i] = st[j];
-    }
-    __syncthreads();
-  };
-  const int w = threadIdx.x >> 6;
-  if (w >= wd.z) {  // no tile for this wave: it still stages and joins the one barrier
-    publish();
-    return;
+  for (int i = 0; i < 8; ++i) {
+    run += (fl >> i) & 1;
+    cl[i] = run;
   }
-  // one tile per wave: a loop over several (48 tiles per workgroup, 3 per wave) needed more than 64
-  // VGPRs, one resident workgroup per CU instead of two, and measured 66.8-70.5 vs 47 us at covtype's
-  // shape (profiles/round4/r4k, r4l)
-  tile_pass<A, ROW16, VALS>(a, wd.y + w, cnt[w], [&](int, const int (&rows)[8], A (&v)[8]) {
+  const int before = wave_before(run);
+  __builtin_amdgcn_wave_barrier();
+  int key[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = su[min(rows[i], wd.w - 1)];  // (padding rows are 0; clamp an empty sub-block)
-  }, publish, true);
+  for (int i = 0; i < 8; ++i) key[i] = rl[max(before + cl[i] - 1, 0)];
+#pragma unroll
+  for (int j = 0; j < kStageRegs; ++j) {
+    const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
+    if (i < wd.w) su[i] = st[j];
+  }
+  __syncthreads();
+  if (w >= wd.z) return;  // wave-uniform, after the one block barrier
+  A v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = su[min(rows[i], wd.w - 1)];  // (padding rows are 0; clamp an empty sub-block)
+  tile_finish<A, VALS>(a, t, p, n, c0, flags, key, v, cv);
 }
 
 // Sub-block sums added per partition in sub-block order: Gb[j][c] = sum_s Gs[s][c].
@@ -386,7 +495,7 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
   const dim3 block(256);
   if (a.nrows > 0) {
     const size_t blds = static_cast<size_t>(a.d) * (dtype == 0 ? 8 : 4);
-    if (a.ell && blds <= static_cast<size_t>(kEllLdsBytes) && a.m <= kEllMaxFields) {
+    if (a.ell && blds <= static_cast<size_t>(kEllLdsBytes) && a.m <= kEllMaxFields && a.ell_ld % 2 == 0) {
       static int cus = 0;
       if (!cus) {
         int dev = 0;
@@ -394,7 +503,7 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
           cus = 256;
       }
-      const dim3 grid(static_cast<unsigned>(std::min<long long>(cus, (a.nrows + 1023) / 1024)));
+      const dim3 grid(static_cast<unsigned>(std::min<long long>(cus, ((a.nrows + 1) / 2 + 1023) / 1024)));
       auto go = [&](const void* kern) -> hipError_t {
         return blds > 64 * 1024 ? hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                       static_cast<int>(blds))

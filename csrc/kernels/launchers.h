@@ -47,16 +47,18 @@ struct SparseArgs {
   int idx16;                    // ELL: uint16 offsets into window lo[k] (else int32 columns)
   int m;                        // ELL nnz per row
   long long nrows;
-  const void* ell_idx;          // [m][nrows] uint16 | int32
+  const void* ell_idx;          // [m][ell_ld] uint16 | int32 (rows past nrows: padding)
+  long long ell_ld;             // ELL row stride (>= nrows; even: the LDS row pass loads row pairs)
   const int* lo;                // [m] category window starts (idx16)
   const long long* row_ptr;     // CSR [nrows + 1]
   const int* col_idx;           // CSR [nnz]
-  const void* vals;             // ELL [m][nrows] or CSR [nnz] values; nullptr: pattern-only (1.0)
+  const void* vals;             // ELL [m][ell_ld] or CSR [nnz] values; nullptr: pattern-only (1.0)
   const void* y;                // [nrows] labels (acc dtype)
   void* u;                      // [nrows] residual with coefficient 1 (acc dtype)
   // pass 2: CSC tiles of 512 entries
   int row16;                    // CSC row indices uint16 (partition-relative) | int32
-  const void* crow;             // [entries] per partition sorted by (column, row), each partition padded to 512
+  const void* crow;             // [entries] per partition sorted by (column, row), each partition padded to 512;
+                                //   top bit: the entry starts a run (first of its column or of its tile)
   const void* cvals;            // [entries] values in CSC order; nullptr: pattern-only
   const int* col_ptr;           // [nparts][d + 1] partition-relative entry offsets
   const int4* tiles;            // [ntiles] (partition, base entry, column of the base entry, span flags 1 head / 2 tail)
@@ -75,13 +77,15 @@ struct SparseArgs {
   int d, ld;
   // row-blocked column pass (ops/grad.py csc_tables row_block): the "partitions" of pass 2 / 3 above
   // are sub-blocks of rows; wg == nullptr: one wave per tile gathering the residuals from memory
-  const int4* wg;               // [nwg] (sub-block, first tile, tiles <= 16, rows): one workgroup each
+  const int4* wg;               // [nwg] (first row of the sub-block, first tile, tiles <= 16, rows): one workgroup each
   int nwg;
   int u_lds;                    // rows of the largest sub-block (its residuals staged in LDS)
   void* Gs;                     // [nsub][ld] pass 2 / 3 output (== Gb without sub-blocks)
   const int* sub_begin;         // [nparts + 1] sub-blocks of each partition; nullptr: Gs is Gb
   int nparts;
   int encode_from_subs;         // 1: the encoding that follows adds the sub-block sums itself (no sub_reduce)
+  const int* runs;              // row-blocked pass: the column of every run (CSC rows flag run starts), per tile
+  const int4* tkeys;            // [ntiles] (first run, n | runs << 10 | span flags << 20, sub-block, first column)
 };
 hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const void* beta, hipStream_t st,
                               const int* gate = nullptr);

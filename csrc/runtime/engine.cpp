@@ -225,7 +225,8 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
                                           const Tensor& head, const Tensor& tail, const Tensor& span,
                                           const Tensor& empty, int64_t nparts, int64_t d, int64_t ld,
                                           std::optional<Tensor> wg, int64_t u_lds, std::optional<Tensor> Gs,
-                                          std::optional<Tensor> sub_begin) {
+                                          std::optional<Tensor> sub_begin, std::optional<Tensor> runs,
+                                          std::optional<Tensor> tkeys) {
   for (auto* t : {&y, &u, &crow, &col_ptr, &tiles, &part_entry0, &part_row0, &part_nnz, &head, &tail, &span, &empty})
     need_gpu(*t, "sparse plan operand");
   need(tiles.scalar_type() == at::kInt && tiles.dim() == 2 && tiles.size(1) == 4, "tiles: int32 [n, 4]");
@@ -250,7 +251,8 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
   g->keep = {y, u, crow, col_ptr, tiles, part_entry0, part_row0, part_nnz, head, tail, span, empty};
   if (ell_idx) {
     need_gpu(*ell_idx, "ell_idx");
-    need(ell_idx->dim() == 2 && ell_idx->size(1) == a.nrows, "ell_idx: [m, rows]");
+    need(ell_idx->dim() == 2 && ell_idx->size(1) >= a.nrows, "ell_idx: [m, >= rows]");
+    a.ell_ld = ell_idx->size(1);
     a.ell = 1;
     a.idx16 = ell_idx->scalar_type() == at::kShort ? 1 : 0;
     need(a.idx16 || ell_idx->scalar_type() == at::kInt, "ell_idx: int16 | int32");
@@ -276,6 +278,7 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
   if (vals) {
     need_gpu(*vals, "vals");
     need(acc_code(*vals) == g->acc, "vals dtype");
+    need(!ell_idx || vals->sizes() == ell_idx->sizes(), "ELL vals: the shape of ell_idx");
     a.vals = vals->data_ptr();
     g->keep.push_back(*vals);
   }
@@ -290,6 +293,7 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
   a.col_ptr = col_ptr.data_ptr<int>();
   a.tiles = reinterpret_cast<const int4*>(tiles.data_ptr<int>());
   a.ntiles = (int)tiles.size(0);
+  need(crow.numel() >= static_cast<int64_t>(a.ntiles) * 512, "crow: every partition padded to whole 512-entry tiles");
   need(head.numel() >= a.ntiles && tail.numel() >= a.ntiles, "head / tail: one per tile");
   a.part_entry0 = reinterpret_cast<const long long*>(part_entry0.data_ptr<int64_t>());
   a.part_row0 = reinterpret_cast<const long long*>(part_row0.data_ptr<int64_t>());
@@ -310,6 +314,16 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
     a.nwg = (int)wg->size(0);
     a.u_lds = (int)u_lds;
     g->keep.push_back(*wg);
+    need(runs.has_value() && tkeys.has_value(), "the row-blocked column pass needs the run lists (runs, tkeys)");
+    need_gpu(*runs, "runs");
+    need_gpu(*tkeys, "tkeys");
+    need(runs->scalar_type() == at::kInt && runs->numel() >= 1, "runs: int32 [runs]");
+    need(tkeys->scalar_type() == at::kInt && tkeys->dim() == 2 && tkeys->size(0) == a.ntiles && tkeys->size(1) == 4,
+         "tkeys: int32 [tiles, 4]");
+    a.runs = runs->data_ptr<int>();
+    a.tkeys = reinterpret_cast<const int4*>(tkeys->data_ptr<int>());
+    g->keep.push_back(*runs);
+    g->keep.push_back(*tkeys);
   }
   if (sub_begin) {
     need(Gs.has_value(), "sub-blocks need their Gs buffer");
@@ -1790,7 +1804,8 @@ void bind_engine(py::module& m) {
                   py::arg("col_ptr"), py::arg("tiles"), py::arg("part_entry0"), py::arg("part_row0"),
                   py::arg("part_nnz"), py::arg("head"), py::arg("tail"), py::arg("span"), py::arg("empty"),
                   py::arg("nparts"), py::arg("d"), py::arg("ld"), py::arg("wg") = py::none(), py::arg("u_lds") = 0,
-                  py::arg("Gs") = py::none(), py::arg("sub_begin") = py::none())
+                  py::arg("Gs") = py::none(), py::arg("sub_begin") = py::none(),
+                  py::arg("runs") = py::none(), py::arg("tkeys") = py::none())
       .def("set_encode",
            [](GradLauncher& g, const Tensor& ptr, const Tensor& idx, const Tensor& coef, const Tensor& Gb) {
              for (auto* t : {&ptr, &idx, &coef, &Gb}) need_gpu(*t, "encode operand");

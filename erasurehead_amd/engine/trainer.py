@@ -42,7 +42,6 @@ from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
 from .._ext import native as native_ext
 from .loops import LoopInputs, select_round_loop

@@ -674,15 +674,22 @@ class SparseGradPlan:
             lo = idx.min(axis=1).astype(np.int64)
             width = idx.max(axis=1) - lo + 1
             self.ell, self.ell_m = True, m
+            # an even row stride: the LDS row pass loads a row pair's field at once (grad_sparse.hip
+            # ell_rows_lds); the padding row points at each window's first column with value 0
+            pad = self.nrows % 2
+
+            def padded(x):
+                return np.ascontiguousarray(np.pad(x, ((0, 0), (0, pad))) if pad else x)
+
             if int(width.max()) <= 65536:  # 16-bit offsets into each feature's category window
                 self.idx16 = True
                 off = (idx - lo[:, None]).astype(np.uint16).view(np.int16)
-                self.ell_idx = torch.from_numpy(np.ascontiguousarray(off)).to(dev)
+                self.ell_idx = torch.from_numpy(padded(off)).to(dev)
                 self.ell_lo = torch.from_numpy(lo.astype(np.int32)).to(dev)
             else:
-                self.ell_idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32)).to(dev)
+                self.ell_idx = torch.from_numpy(padded(idx.astype(np.int32))).to(dev)
             if not self.pattern_only:
-                self.vals = torch.from_numpy(np.ascontiguousarray(X.data.reshape(self.nrows, m).T, dtype=npacc)).to(dev)
+                self.vals = torch.from_numpy(padded(X.data.reshape(self.nrows, m).T.astype(npacc))).to(dev)
         else:
             self.row_ptr = torch.from_numpy(X.indptr.astype(np.int64)).to(dev)
             self.col_idx = torch.from_numpy(X.indices.astype(np.int32)).to(dev)
@@ -709,6 +716,8 @@ class SparseGradPlan:
         self.tail = torch.zeros(nt, dtype=acc, device=dev)
         self.Gb = torch.zeros((max(1, len(self.basis)), self.ld), dtype=acc, device=dev)
         self.wg = torch.from_numpy(t["wg"]).to(dev)
+        self.runs = torch.from_numpy(t["runs"]).to(dev)
+        self.tkeys = torch.from_numpy(t["tkeys"]).to(dev)
         self.u_lds = int(t["wg"][:, 3].max()) if len(t["wg"]) else 1
         blocked = self.nsub != len(self.basis)  # some partition spans several sub-blocks
         self.sub_begin = torch.from_numpy(t["sub_begin"]).to(dev) if blocked else None
@@ -727,11 +736,18 @@ class SparseGradPlan:
         first column began in an earlier tile, 2 = the last goes on in a later one), the columns that
         cross tiles (partition, column, first tile, last tile) and the empty columns.
 
+        Every row index carries a run-start flag in its top bit (bit 15 of 16-bit rows, so those need
+        <= 32768 rows; bit 31 otherwise): set on the first entry of each column and of each tile.
+        runs / tkeys: every tile's run columns in order, and per tile (first run, n | runs << 10 |
+        span flags << 20, partition, first column) -- the keyed column pass reads a tile's columns
+        from there instead of walking the column pointers.
+
         row_block > 0: every partition is cut into sub-blocks of at most that many rows and the tables
         are built per sub-block (the "partitions" of the kernels are then the sub-blocks; sub_begin[j]
         lists partition j's).  A workgroup takes up to wg_tiles tiles of ONE sub-block and stages
-        that sub-block's residuals in LDS (wg: sub-block, first tile, tiles, rows), so the column
-        pass's gathers never leave the CU; the sub-block sums are added per partition afterwards."""
+        that sub-block's residuals in LDS (wg: first row of the sub-block, first tile, tiles, rows),
+        so the column pass's gathers never leave the CU; the sub-block sums are added per partition
+        afterwards."""
         import scipy.sparse as sps
 
         sub_begin = None
@@ -743,8 +759,11 @@ class SparseGradPlan:
                     subs.append(sps.csr_matrix(A[r:min(n, r + row_block)]))
                 sub_begin.append(len(subs))
             blocks = subs
-        row16 = all(A.shape[0] <= 65536 for A in blocks)
+        row16 = all(A.shape[0] <= 32768 for A in blocks)
+        flag = np.int64(1 << 15) if row16 else np.int64(1 << 31)
         rows_l, vals_l, cps, tiles, spans, empty = [], [], [], [], [], []
+        runs_l, tkeys = [], []
+        n_runs = 0
         entry0, row0, nnzs = [], [], []
         e_off = r_off = n_tiles = 0
         for j, A in enumerate(blocks):
@@ -754,6 +773,11 @@ class SparseGradPlan:
             nnz = int(cp[-1])
             pad = (-nnz) % tile
             r = C.indices.astype(np.int64)
+            col_of = np.repeat(np.arange(d, dtype=np.int64), np.diff(cp))  # each entry's column
+            start = np.zeros(nnz, dtype=bool)  # run starts: first entry of a column or of a tile
+            start[cp[:-1][cp[:-1] < cp[1:]]] = True
+            start[::tile] = True
+            r = np.where(start, r | flag, r)
             rows_l.append(np.concatenate([r, np.zeros(pad, dtype=np.int64)]))
             vals_l.append(np.concatenate([C.data.astype(np.float64), np.zeros(pad)]))
             cps.append(cp.astype(np.int32))
@@ -769,6 +793,14 @@ class SparseGradPlan:
                 flags = (cp[c0] < bases).astype(np.int64) | 2 * (cp[c_last + 1] > bases + tile).astype(np.int64)
                 tiles.append(np.stack([np.full(bases.size, j), bases, c0, flags], axis=1))
                 n_tiles += bases.size
+                sidx = np.nonzero(start)[0]
+                runs_l.append(col_of[sidx])
+                r_first = np.searchsorted(sidx, bases)  # runs before each tile
+                r_cnt = np.diff(np.append(r_first, sidx.size))
+                ns = end - bases
+                tkeys.append(np.stack([n_runs + r_first, ns | (r_cnt << 10) | (flags << 20),
+                                       np.full(bases.size, j), c0], axis=1))
+                n_runs += sidx.size
             nonempty = np.nonzero(cp[1:] > cp[:-1])[0]
             t1 = cp[nonempty] // tile
             t2 = (cp[nonempty + 1] - 1) // tile
@@ -782,7 +814,7 @@ class SparseGradPlan:
             e_off += nnz + pad
             r_off += A.shape[0]
         crow = np.concatenate(rows_l) if rows_l else np.zeros(tile, dtype=np.int64)
-        crow = crow.astype(np.uint16).view(np.int16) if row16 else crow.astype(np.int32)
+        crow = crow.astype(np.uint16).view(np.int16) if row16 else crow.astype(np.uint32).view(np.int32)
         wg = []
         if row_block > 0:
             t_of = np.concatenate(tiles)[:, 0] if tiles else np.zeros(0, dtype=np.int64)
@@ -790,7 +822,7 @@ class SparseGradPlan:
             lasts = np.searchsorted(t_of, np.arange(len(blocks)), side="right")
             for j, A in enumerate(blocks):
                 for t0 in range(int(firsts[j]), int(lasts[j]), wg_tiles):
-                    wg.append((j, t0, min(wg_tiles, int(lasts[j]) - t0), A.shape[0]))
+                    wg.append((row0[j], t0, min(wg_tiles, int(lasts[j]) - t0), A.shape[0]))
         extra = {"sub_begin": np.asarray(sub_begin, dtype=np.int32) if sub_begin is not None else None,
                  "wg": np.asarray(wg, dtype=np.int32).reshape(-1, 4), "nsub": len(blocks),
                  "row_block": int(row_block)}
@@ -802,7 +834,9 @@ class SparseGradPlan:
                 "part_row0": np.asarray(row0 or [0], dtype=np.int64),
                 "part_nnz": np.asarray(nnzs or [0], dtype=np.int32),
                 "span": (np.concatenate(spans) if spans else np.zeros((0, 4))).astype(np.int32).reshape(-1, 4),
-                "empty": (np.concatenate(empty) if empty else np.zeros((0, 2))).astype(np.int32).reshape(-1, 2)}
+                "empty": (np.concatenate(empty) if empty else np.zeros((0, 2))).astype(np.int32).reshape(-1, 2),
+                "runs": (np.concatenate(runs_l) if runs_l else np.zeros(1)).astype(np.int32),
+                "tkeys": (np.concatenate(tkeys) if tkeys else np.zeros((0, 4))).astype(np.int32).reshape(-1, 4)}
 
     def out_buffer(self, n: int = 1) -> torch.Tensor:
         return torch.zeros((n, self.nslots, self.ld), dtype=self.prec.acc, device=self.device)
@@ -811,12 +845,15 @@ class SparseGradPlan:
         if self.device.type != "cuda":
             raise RuntimeError("native launchers need GPU tensors")
         if self._launcher is None:
+            # sub-blocks: Gs is this plan's own zero-initialised buffer and no pass writes a column that
+            # is empty in a sub-block, so those zeros stay and the per-round zero writes are skipped
+            empty = self.empty[:0] if self.sub_begin is not None else self.empty
             L = native().GradLauncher.sparse(self.loss, self.y, self.u, self.ell_idx, self.ell_lo, self.row_ptr,
                                              self.col_idx, self.vals, self.crow, self.cvals, self.col_ptr, self.tiles,
                                              self.part_entry0, self.part_row0, self.part_nnz, self.head, self.tail,
-                                             self.span, self.empty, self.nsub, self.d, self.ld,
+                                             self.span, empty, self.nsub, self.d, self.ld,
                                              wg=self.wg if len(self.wg) else None, u_lds=self.u_lds, Gs=self.Gs,
-                                             sub_begin=self.sub_begin)
+                                             sub_begin=self.sub_begin, runs=self.runs, tkeys=self.tkeys)
             L.set_encode(self.enc_ptr, self.enc_idx, self.enc_coef, self.Gb)
             self._launcher = L
         return self._launcher

@@ -11,7 +11,6 @@ import os
 import subprocess
 import sys
 
-import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu

@@ -11,11 +11,33 @@ from erasurehead_amd.ops.grad import SparseGradPlan
 TILE = 512
 
 
-def emulate(t, u_parts, d):
+def rows_and_flags(t):
+    """CSC row indices and their run-start flags (the top bit)."""
+    if t["row16"]:
+        raw = t["crow"].view(np.uint16).astype(np.int64)
+        return raw & 0x7FFF, raw >> 15
+    raw = t["crow"].view(np.uint32).astype(np.int64)
+    return raw & 0x7FFFFFFF, raw >> 31
+
+
+def tile_keys(t, ti, flag):
+    """The keyed column pass's columns of tile ti (grad_sparse.hip csc_tiles_lds): the run list read at
+    the wave prefix of the run-start flags."""
+    r0, packed, p, c0 = (int(x) for x in t["tkeys"][ti])
+    n, nruns, flags = packed & 1023, (packed >> 10) & 1023, packed >> 20
+    f = flag[TILE * ti:TILE * ti + TILE]
+    assert f[0] == 1 and int(f[:n].sum()) == nruns and not f[n:].any()
+    ridx = np.cumsum(f) - 1
+    keys = t["runs"][r0 + ridx].astype(np.int64)
+    assert keys[0] == c0
+    return keys[:n], n, p, c0, flags
+
+
+def emulate(t, u_parts, d, keyed=False):
     nparts = len(u_parts)
     G = np.full((nparts, d), np.nan)
     head, tail = {}, {}
-    crow = t["crow"].view(np.uint16).astype(np.int64) if t["row16"] else t["crow"].astype(np.int64)
+    crow, flag = rows_and_flags(t)
     for ti, (p, base, c0, flags) in enumerate(t["tiles"]):
         cp = t["col_ptr"][p].astype(np.int64)
         nnz = int(t["part_nnz"][p])
@@ -29,6 +51,12 @@ def emulate(t, u_parts, d):
             c += 1
         keys = c0 + np.cumsum(cnt)[:n]
         assert keys[0] == c0 and np.all(cp[keys] <= base + np.arange(n)) and np.all(base + np.arange(n) < cp[keys + 1])
+        assert e0 == TILE * ti  # the kernels address tile ti's entries directly
+        if keyed:
+            k2, n2, p2, c02, f2 = tile_keys(t, ti, flag)
+            assert (n2, p2, c02, f2) == (n, p, c0, flags)
+            np.testing.assert_array_equal(k2, keys)
+            keys = k2
         v = u_parts[p][crow[e0:e0 + n]] * t["cvals"][e0:e0 + n]
         start = 0
         for q in range(n):
@@ -82,7 +110,7 @@ def test_tables_emulate_to_the_transposed_product(seed):
     t = SparseGradPlan.csc_tables(blocks, d, TILE)
     assert not t["row16"]  # one partition has more than 65536 rows
     u = [rng.randn(b.shape[0]) for b in blocks]
-    got = emulate(t, u, d)
+    got = emulate(t, u, d, keyed=True)
     for p, b in enumerate(blocks):
         np.testing.assert_allclose(got[p], b.T.dot(u[p]), rtol=1e-12, atol=1e-12)
     assert len(t["span"]) > 0 and len(t["empty"]) > 0
@@ -96,7 +124,7 @@ def test_sixteen_bit_rows_and_tile_alignment():
     assert t["row16"] and t["crow"].dtype == np.int16
     assert all(e % TILE == 0 for e in t["part_entry0"])
     u = [rng.randn(b.shape[0]) for b in blocks]
-    got = emulate(t, u, d)
+    got = emulate(t, u, d, keyed=True)
     for p, b in enumerate(blocks):
         np.testing.assert_allclose(got[p], b.T.dot(u[p]), rtol=1e-12, atol=1e-12)
 
@@ -145,10 +173,11 @@ def test_row_blocked_tables_sum_to_the_transposed_product(row_block):
         for r in range(0, max(b.shape[0], 1), row_block):
             u_sub.append(u[j][r:r + row_block])
     assert len(u_sub) == t["nsub"]
-    got = emulate(t, u_sub, d)
+    got = emulate(t, u_sub, d, keyed=True)
     seen = []
-    for s, t0, nt, rows in t["wg"]:
-        assert 1 <= nt <= 16 and rows == len(u_sub[s])
+    for row0, t0, nt, rows in t["wg"]:
+        s = int(t["tiles"][t0][0])
+        assert row0 == t["part_row0"][s] and 1 <= nt <= 16 and rows == len(u_sub[s])
         assert all(t["tiles"][k][0] == s for k in range(t0, t0 + nt))
         seen += list(range(t0, t0 + nt))
     assert sorted(seen) == list(range(len(t["tiles"])))
