@@ -574,6 +574,7 @@ class MasterPump {
   bool integrity() const { return tags_; }
 
   // Raise the first integrity failure any deferred check of this pump reported (host-mapped record).
+  int64_t check_rows_cut() const { return check_rows_cut_; }
   void check_integrity() const {
     const auto* e = static_cast<const eh::IntegrityErr*>(err_->host);
     if (__atomic_load_n(&e->flag, __ATOMIC_ACQUIRE)) throw std::runtime_error(integrity_message(*e, false));
@@ -1134,7 +1135,10 @@ class MasterPump {
       cl.tags = reinterpret_cast<const eh::MsgTag*>(mbox_tags_) + static_cast<int64_t>(slot) * r_rows_;
       for (const auto& u : used)
         if (u.row >= 0) {
-          need(cl.n < eh::kMaxCheckRows, "integrity check list: more mailbox rows than one decode holds");
+          if (cl.n >= eh::kMaxCheckRows) {  // the check list is full: counted, reported by the trainer
+            ++check_rows_cut_;
+            continue;
+          }
           cl.row[cl.n] = u.p;
           cl.mrow[cl.n] = u.row;
           cl.rank[cl.n] = row_rank_[u.row];
@@ -1393,6 +1397,7 @@ class MasterPump {
   std::vector<hipEvent_t> rev_;                        // [K][sender] receive-done events (collector probes)
   hipEvent_t bev_ = nullptr;                           // beta(j) written (the sends wait on it)
   bool tags_ = false;               // integrity tags on (set_integrity)
+  int64_t check_rows_cut_ = 0;      // decoded mailbox rows past a round's check list (kMaxCheckRows): unchecked
   uintptr_t mbox_tags_ = 0;         // device address of the mailbox tag slots [K][r_rows]
   int64_t inbox_tag_off_ = 0;       // worker inbox base -> its tag slots
   std::vector<int> row_rank_;       // [r_rows] sender rank of each mailbox row
@@ -1852,6 +1857,7 @@ void bind_engine(py::module& m) {
       .def("set_integrity", &MasterPump::set_integrity, py::arg("mbox_tags"), py::arg("inbox_tag_off"), py::arg("on"))
       .def_property_readonly("integrity", &MasterPump::integrity)
       .def("check_integrity", &MasterPump::check_integrity)
+      .def("check_rows_cut", &MasterPump::check_rows_cut)
       .def("final_check", &MasterPump::final_check)
       .def("set_sources", &MasterPump::set_sources)
       .def("device_blocker", &MasterPump::device_blocker)

@@ -791,6 +791,11 @@ class Trainer:
         self._final_drain(col)
         upd = pump.update_ms()
         pump.final_check()  # the last round's mailbox rows (earlier rounds were checked as the run went)
+        cut = int(pump.check_rows_cut())
+        if cut:  # decodes of more mailbox rows than one check list holds: the rest went unchecked
+            why = f"{cut} decoded mailbox rows were past a round's integrity check list and went unchecked"
+            print(f"[erasurehead] WARNING: {why}", file=sys.stderr, flush=True)
+            self.rank_stats["integrity_unchecked_rows"] = cut
         if not device_mode and not arb_mode:
             timeset[start:] += 1e-3 * np.asarray(upd[start:])
         a0 = timed_start if timed_start is not None else start
