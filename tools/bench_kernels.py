@@ -259,7 +259,7 @@ def eval_cases(out):
         del X
 
 
-def sparse_cases(out):
+def sparse_cases(out, names=("covtype", "kc_house_data", "amazon-dataset"), ell_only=False):
     import torch
 
     from erasurehead_amd.data.synthetic import REAL_SHAPES, onehot_partitions
@@ -267,14 +267,14 @@ def sparse_cases(out):
     from erasurehead_amd.ops import SparseGradPlan, get_precision
 
     prec = get_precision("fp64")
-    for name in ("covtype", "kc_house_data", "amazon-dataset"):
+    for name in names:
         n, d, f = REAL_SHAPES[name]
         W = 8
         parts_l, _, dd = onehot_partitions(n, d, f, W, seed=1)
         parts = {p: xy for p, xy in enumerate(parts_l)}
         layouts = {"naive": [[(w, 1.0)] for w in range(W)],
                    "s1_replicas": [[(w, 1.0), ((w + 1) % W, 1.0)] for w in range(W)]}  # 8 workers, 2 partitions each
-        for (layout, msgs), use_ell in [(x, e) for x in layouts.items() for e in (True, False)]:
+        for (layout, msgs), use_ell in [(x, e) for x in layouts.items() for e in ((True,) if ell_only else (True, False))]:
             plan = SparseGradPlan(msgs, parts, prec, LOGISTIC, dd, device="cuda", use_ell=use_ell)
             beta = torch.randn(prec.ld(dd), device="cuda", dtype=torch.float64) * 0.1
             G = plan.out_buffer()[0]
@@ -300,6 +300,8 @@ def main():
     ap.add_argument("--ds", default="256,1000,2048,4096", help="--only sweep: row widths")
     ap.add_argument("--ns", default="1e5,1e6,4e6", help="--only sweep: row counts")
     ap.add_argument("--precs", default="fp64,fp32", help="--only sweep: precisions")
+    ap.add_argument("--sparse-shapes", default="covtype,kc_house_data,amazon-dataset", help="--only sparse: datasets")
+    ap.add_argument("--ell-only", action="store_true", help="--only sparse: skip the CSR row pass")
     a = ap.parse_args()
     out = []
     if a.only in (None, "dense"):
@@ -318,7 +320,7 @@ def main():
         else:
             choice_cases(out, layout=a.layout)
     if a.only in (None, "sparse"):
-        sparse_cases(out)
+        sparse_cases(out, names=tuple(a.sparse_shapes.split(",")), ell_only=a.ell_only)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         for r in out:

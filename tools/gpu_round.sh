@@ -19,6 +19,7 @@
 #   wide     the d = 2048 / 4096 rows of the sweep
 #   sparse   sparse gradients at the real-data shapes (timings, then rocprofv3 kernel stats)
 #   rccl     the RCCL self-loop GPU tests under rocprofv3 --kernel-trace (RCCL kernel names)
+#   pmcsparse counter passes over the covtype-shaped sparse gradient
 #   pmcbytes FETCH_SIZE / raw read requests / WRITE_SIZE over known-byte workloads (tools/pmc_calibrate.py)
 #   abtree   same-box A/B against an older tree exported and built under build/ab_old
 #            (git archive <rev> | tar -x -C build/ab_old, then __graft_entry__.build() there):
@@ -99,6 +100,22 @@ for s in "${STAGES[@]}"; do
           python tools/pmc_calibrate.py --known "$OUT/known.json"
       done
       python tools/pmc_summary.py "$OUT/pmcb" --by-kernel > "$OUT/pmcb_summary.json" ;;
+    pmcsparse)  # counter passes over the covtype-shaped sparse gradient (ELL rows)
+      run 120 counters.log rocprofv3 -L
+      i=0
+      for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY" \
+                 "SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \
+                 "FETCH_SIZE"; do
+        i=$((i+1))
+        want=""
+        for c in $grp; do
+          if grep -qw "$c" "$OUT/counters.log"; then want="$want $c"; fi
+        done
+        [ -z "$want" ] && { log "skip pass $i: none of $grp listed"; continue; }
+        run 180 "pmcs_$i.log" timeout -s KILL 170 rocprofv3 --pmc $want --output-format csv -d "$OUT/pmcs" -o "p$i" -- \
+          python tools/bench_kernels.py --only sparse --sparse-shapes covtype --ell-only --out /tmp/sparse_pmc.jsonl
+      done
+      python tools/pmc_summary.py "$OUT/pmcs" --by-kernel > "$OUT/pmcs_summary.json" ;;
     rehearse)
       for n in 2 4 8; do
         run 600 "rehearse_$n.log" python -u bench.py --gpus $n --steps 20 --warmup 5 --no-floor \
