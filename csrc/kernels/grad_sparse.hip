@@ -133,6 +133,9 @@ __global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A
     }
   };
   long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  IW w[KB];
+  V2 v[KB];
+  load(w, v, q, 0);  // in flight while beta is staged
   {  // stage beta (and the window starts): every load of this thread in flight before its stores
     const int nv = a.d * static_cast<int>(sizeof(A)) / 16;
     const V4* __restrict__ bv = reinterpret_cast<const V4*>(beta);
@@ -156,9 +159,6 @@ __global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A
     if (IDX16 && static_cast<int>(threadIdx.x) < m) slo[threadIdx.x] = lo;
   }
   __syncthreads();
-  IW w[KB];
-  V2 v[KB];
-  load(w, v, q, 0);
   for (; q < npair; q += stride) {
     A z[4] = {A(0), A(0), A(0), A(0)}, y[4] = {A(0), A(0), A(0), A(0)};
     for (int k0 = 0; k0 < m; k0 += KB) {
@@ -384,30 +384,81 @@ __global__ void __launch_bounds__(256) csc_tiles(const SparseArgs a, const int* 
   });
 }
 
+// ---- wave scans on DPP: row_shr 1 / 2 / 4 / 8 inside each row of 16 lanes, then row_bcast 15 / 31
+// across rows (GFX9 DPP; gfx950 keeps it) -- one VALU op per step, no LDS round trip.  A lane with no
+// source in a step takes `old`, the operator's identity.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_i(int old, int x) {
+  return __builtin_amdgcn_update_dpp(old, x, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS, typename A>
+__device__ __forceinline__ A dpp_a(A old, A x) {
+  if constexpr (sizeof(A) == 8) {
+    const long long xi = __builtin_bit_cast(long long, x), oi = __builtin_bit_cast(long long, old);
+    const unsigned lo = static_cast<unsigned>(dpp_i<CTRL, ROWS>(static_cast<int>(oi), static_cast<int>(xi)));
+    const unsigned hi = static_cast<unsigned>(dpp_i<CTRL, ROWS>(static_cast<int>(oi >> 32), static_cast<int>(xi >> 32)));
+    return __builtin_bit_cast(A, (static_cast<unsigned long long>(hi) << 32) | lo);
+  } else {
+    return __builtin_bit_cast(A, dpp_i<CTRL, ROWS>(__builtin_bit_cast(int, old), __builtin_bit_cast(int, x)));
+  }
+}
+__device__ __forceinline__ int wave_incl_sum(int x) {
+  x += dpp_i<0x111, 0xf>(0, x);
+  x += dpp_i<0x112, 0xf>(0, x);
+  x += dpp_i<0x114, 0xf>(0, x);
+  x += dpp_i<0x118, 0xf>(0, x);
+  x += dpp_i<0x142, 0xa>(0, x);  // row_bcast:15 -> rows 1, 3
+  x += dpp_i<0x143, 0xc>(0, x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+// inclusive scan of x_l = g_l x_{l-1} + b_l over the lanes (identity g = 1, b = 0)
+template <int CTRL, int ROWS, typename A>
+__device__ __forceinline__ void affine_step(int& g, A& b) {
+  const A bp = dpp_a<CTRL, ROWS>(A(0), b);
+  const int gp = dpp_i<CTRL, ROWS>(1, g);
+  b = fma(static_cast<A>(g), bp, b);  // b + bp or b (g is 0 / 1), one op for a select of two doubles
+  g &= gp;
+}
+template <typename A>
+__device__ __forceinline__ void wave_affine_scan(int& g, A& b) {
+  affine_step<0x111, 0xf>(g, b);
+  affine_step<0x112, 0xf>(g, b);
+  affine_step<0x114, 0xf>(g, b);
+  affine_step<0x118, 0xf>(g, b);
+  affine_step<0x142, 0xa>(g, b);
+  affine_step<0x143, 0xc>(g, b);
+}
+
 // Row-blocked column pass: a 1024-thread workgroup takes up to kWgTiles tiles of ONE sub-block (a.wg) and
 // first copies that sub-block's residuals into LDS (coalesced), so every gather is an LDS read.  From
 // global memory each 8-byte gather pulled a 128-byte L2 line into L1 with no reuse (rows of a column
 // are spread over the partition): covtype's 21.8M gathers moved ~2.8 GB L2 -> L1, 88-92 us
 // (profiles/round4/r4g, r4i).
 //
-// The columns come from the run-start flags and the tile's run list (a.runs[tk.x ...]: the column of
-// each run, in order) instead of a walk over the column pointers: the rows, the run list and the staged
-// residuals are all one load away from the workgroup's descriptor, where the walk waited on the tile
-// descriptor, then the partition's entry offset and column pointers, then the LDS counts (the
-// workgroup's lifetime is a chain of dependent loads: the pass is latency-bound, profiles/round4/r4q).
-constexpr int kWgTiles = 16;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES), one per wave
+// Keyed runs: the row indices' top bit flags every run start (first entry of a column or of the
+// tile), so the segmented sums need no column keys at all -- the flags are the segment boundaries --
+// and a run's column is looked up only once, when its sum is written: run r of the tile is column
+// a.runs[tk.x + r].  The run sums are compacted into LDS by run index and written by lane r % 64,
+// consecutive columns side by side.  (The column-pointer walk before it waited on two more dependent
+// loads per workgroup and ran ~420 VALU instructions per tile: the pass was VALU-bound at ~70 % busy,
+// profiles/round4/r4y.)
+constexpr int kWgTiles = 16;   // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES), one per wave
 constexpr int kStageRegs = 4;  // staged residuals per thread: 4096 rows per sub-block (32 KB fp64 / 16 KB fp32)
+constexpr int kRunCap = 128;   // runs per tile compacted in LDS (covtype: 33 on average, 0.7 % of tiles above)
 template <typename A, bool ROW16, bool VALS>
-__global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const int* gate) {
-  __shared__ int runs_lds[16][kTileEntries];
+__global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, const int* gate) {
+  __shared__ int run_col[kWgTiles][kRunCap];
+  __shared__ A run_val[kWgTiles][kRunCap];
   extern __shared__ __attribute__((aligned(16))) unsigned char usub_raw[];
   A* su = reinterpret_cast<A*>(usub_raw);
   if (gate_closed(gate)) return;
   const int4 wd = a.wg[blockIdx.x];  // (first row of the sub-block, first tile, tiles, rows)
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave-uniform in SGPRs: the tile's descriptor is a scalar load and its buffer descriptors need no
+  // waterfall loops (a VGPR-held base costs ~60 VALU + 70 SALU instructions of readfirstlane loops)
+  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const int t = wd.y + min(w, max(wd.z - 1, 0));  // (a wave past the chunk's tiles only stages)
   // the wave's rows and values first, then the sub-block's residuals into registers: stored to LDS
-  // after the keys, so the staging latency overlaps the rest of the tile's loads
+  // after the run bookkeeping, so the staging latency overlaps it
   int rows[8];
   const unsigned fl = tile_rows<ROW16>(a, t, rows);
   A cv[8];
@@ -420,28 +471,25 @@ __global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const 
     st[j] = i < wd.w ? ug[i] : A(0);
   }
   const int4 tk = a.tkeys[t];  // (first run, n | runs << 10 | span flags << 20, sub-block, first column)
-  const int n = tk.y & 1023, nruns = (tk.y >> 10) & 1023, flags = tk.y >> 20, p = tk.z, c0 = tk.w;
-  // the tile's run list into this wave's LDS row (at most 512 runs)
-  int* __restrict__ rl = runs_lds[w];
-  const auto rrs = make_rsrc(a.runs + tk.x, 4 * nruns);
-  const int ra = buf_load_scalar<int>(rrs, 4 * lane), rb = buf_load_scalar<int>(rrs, 4 * (lane + 64));
-  rl[lane] = ra;
-  rl[lane + 64] = rb;
-  for (int j = 128 + lane; j < nruns; j += 64) rl[j] = buf_load_scalar<int>(rrs, 4 * j);
-  // the run of each of this lane's 8 entries: the wave prefix of the flags (the tile's first entry
-  // is always flagged, padding entries are not: they join the last run and are masked)
-  int cl[8];
-  int run = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    run += (fl >> i) & 1;
-    cl[i] = run;
+  const int tky = __builtin_amdgcn_readfirstlane(tk.y);
+  const int n = tky & 1023, nruns = (tky >> 10) & 1023, flags = tky >> 20;
+  const int p = __builtin_amdgcn_readfirstlane(tk.z), run0 = __builtin_amdgcn_readfirstlane(tk.x);
+  const bool compact = nruns <= kRunCap;  // wave-uniform
+  const auto rrs = make_rsrc(a.runs + run0, 4 * nruns);
+  if (compact) {
+    run_col[w][lane] = buf_load_scalar<int>(rrs, 4 * lane);
+    run_col[w][lane + 64] = buf_load_scalar<int>(rrs, 4 * (lane + 64));
   }
-  const int before = wave_before(run);
-  __builtin_amdgcn_wave_barrier();
-  int key[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) key[i] = rl[max(before + cl[i] - 1, 0)];
+  // runs before this lane (the tile's first entry is always flagged; padding entries never are)
+  const int cnt = __builtin_popcount(fl);
+  const int before = wave_incl_sum(cnt) - cnt;
+  // this lane's run ends: the entry before a flagged one, and the tile's last entry
+  const unsigned long long f0 = __ballot(fl & 1u);
+  const unsigned next0 = lane < 63 ? static_cast<unsigned>((f0 >> (lane + 1)) & 1ull) : 1u;
+  const int q0 = 8 * lane;
+  const unsigned valid = n >= q0 + 8 ? 0xffu : n > q0 ? (1u << (n - q0)) - 1u : 0u;
+  unsigned ends = ((fl >> 1) | (next0 << 7)) & valid;
+  if (n - 1 >= q0 && n - 1 < q0 + 8) ends |= 1u << (n - 1 - q0);
 #pragma unroll
   for (int j = 0; j < kStageRegs; ++j) {
     const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
@@ -451,8 +499,58 @@ __global__ void __launch_bounds__(1024) csc_tiles_lds(const SparseArgs a, const 
   if (w >= wd.z) return;  // wave-uniform, after the one block barrier
   A v[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = su[min(rows[i], wd.w - 1)];  // (padding rows are 0; clamp an empty sub-block)
-  tile_finish<A, VALS>(a, t, p, n, c0, flags, key, v, cv);
+  for (int i = 0; i < 8; ++i) v[i] = su[rows[i]];
+  if (n < kTileEntries) {  // the sub-block's last tile: padding entries (row 0) count nothing
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (valid >> i) & 1u ? v[i] : A(0);
+  }
+  if constexpr (VALS) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] *= cv[i];
+  }
+  // segmented sums: sequential inside the lane, restarting at a flag (fma(keep, s, v) with keep 0 / 1:
+  // exactly s + v or v, one op where a select of two doubles took three), then an affine scan over lanes
+  A sm[8];
+  sm[0] = v[0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) sm[i] = fma(static_cast<A>(((fl >> i) & 1u) ^ 1u), sm[i - 1], v[i]);
+  int g = fl == 0u ? 1 : 0;  // the whole lane continues the previous lane's run
+  A b = sm[7];
+  wave_affine_scan(g, b);
+  const A prev = dpp_a<0x138, 0xf>(A(0), b);  // wave_shr:1 -- the previous lane's running sum
+  const A carry = fl & 1u ? A(0) : prev;       // into this lane's entries before its first flag
+  const unsigned cmask = fl ? (fl & (0u - fl)) - 1u : 0xffu;
+  if (compact) {
+    // each run end stores its lane-local sum at its run index; the one run that began in an earlier
+    // lane (it ends first here, run index before - 1) then gets the carry: sm + carry, as before
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if ((ends >> i) & 1u) run_val[w][before - 1 + __builtin_popcount(fl & ((2u << i) - 1u))] = sm[i];
+    if (!(fl & 1u) && ends) run_val[w][before - 1] += carry;
+    __builtin_amdgcn_wave_barrier();
+    A* __restrict__ gout = static_cast<A*>(a.Gs) + static_cast<long long>(p) * a.ld;
+    for (int r = lane; r < nruns; r += 64) {
+      const A val = run_val[w][r];
+      const bool has_head = r == 0 && (flags & kSpanHead);            // the run reaches back into earlier tiles
+      const bool has_tail = r == nruns - 1 && (flags & kSpanTail);    // the run goes on in later tiles
+      if (has_head) static_cast<A*>(a.head)[t] = val;
+      if (has_tail) static_cast<A*>(a.tail)[t] = val;
+      if (!has_head && !has_tail) gout[run_col[w][r]] = val;
+    }
+  } else {  // many short runs: every run end writes its own sum, the column from global memory
+    A* __restrict__ gout = static_cast<A*>(a.Gs) + static_cast<long long>(p) * a.ld;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if ((ends >> i) & 1u) {
+        const int r = before + __builtin_popcount(fl & ((2u << i) - 1u)) - 1;
+        const A val = (cmask >> i) & 1u ? sm[i] + carry : sm[i];
+        const bool has_head = r == 0 && (flags & kSpanHead);
+        const bool has_tail = r == nruns - 1 && (flags & kSpanTail);
+        if (has_head) static_cast<A*>(a.head)[t] = val;
+        if (has_tail) static_cast<A*>(a.tail)[t] = val;
+        if (!has_head && !has_tail) gout[buf_load_scalar<int>(rrs, 4 * r)] = val;
+      }
+  }
 }
 
 // Sub-block sums added per partition in sub-block order: Gb[j][c] = sum_s Gs[s][c].
@@ -477,8 +575,17 @@ __global__ void __launch_bounds__(256) csc_spans(const SparseArgs a, int, const 
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < a.nspan) {
     const int4 sp = a.span[i];  // (sub-block, column, t1, t2)
+    const A* __restrict__ head = static_cast<const A*>(a.head);
     A s = static_cast<const A*>(a.tail)[sp.z];
-    for (int t = sp.z + 1; t <= sp.w; ++t) s += static_cast<const A*>(a.head)[t];
+    int t = sp.z + 1;
+    for (; t + 4 <= sp.w + 1; t += 4) {  // four loads in flight, added in tile order
+      const A h0 = head[t], h1 = head[t + 1], h2 = head[t + 2], h3 = head[t + 3];
+      s += h0;
+      s += h1;
+      s += h2;
+      s += h3;
+    }
+    for (; t <= sp.w; ++t) s += head[t];
     static_cast<A*>(a.Gs)[static_cast<long long>(sp.x) * a.ld + sp.y] = s;
   } else if (i < a.nspan + a.nempty) {
     const int2 e = a.empty[i - a.nspan];
