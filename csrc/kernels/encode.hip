@@ -34,28 +34,20 @@ encode_messages(const A* __restrict__ Gb, const int* __restrict__ ptr, const int
   for (int k = b; k < e; ++k) {
     A g;
     if (sub_begin) {
-      // the sub-block rows eight / four loads at a time, added in row order (bitwise the serial loop;
-      // a partition of covtype's shape has 13 of them: one dependent load each was ~6 us)
+      // the sub-block rows sixteen loads at a time, added in row order (bitwise the serial loop; a
+      // partition of covtype's shape has 13 of them: one dependent load each was ~6 us)
       g = A(0);
       int q = sub_begin[idx[k]];
       const int q1 = sub_begin[idx[k] + 1];
       const A* __restrict__ col = Gb + c;
-      for (; q + 8 <= q1; q += 8) {
-        A x[8];
+      for (; q < q1; q += 16) {  // up to 16 loads in flight, predicated past the last one
+        A x[16];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = col[static_cast<long long>(q + j) * ld];
+        for (int j = 0; j < 16; ++j) x[j] = q + j < q1 ? col[static_cast<long long>(q + j) * ld] : A(0);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g += x[j];
+        for (int j = 0; j < 16; ++j)
+          if (q + j < q1) g += x[j];
       }
-      for (; q + 4 <= q1; q += 4) {
-        const A x0 = col[static_cast<long long>(q) * ld], x1 = col[static_cast<long long>(q + 1) * ld];
-        const A x2 = col[static_cast<long long>(q + 2) * ld], x3 = col[static_cast<long long>(q + 3) * ld];
-        g += x0;
-        g += x1;
-        g += x2;
-        g += x3;
-      }
-      for (; q < q1; ++q) g += col[static_cast<long long>(q) * ld];
     } else {
       g = Gb[static_cast<long long>(idx[k]) * ld + c];
     }

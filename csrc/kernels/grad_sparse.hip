@@ -577,15 +577,14 @@ __global__ void __launch_bounds__(256) csc_spans(const SparseArgs a, int, const 
     const int4 sp = a.span[i];  // (sub-block, column, t1, t2)
     const A* __restrict__ head = static_cast<const A*>(a.head);
     A s = static_cast<const A*>(a.tail)[sp.z];
-    int t = sp.z + 1;
-    for (; t + 4 <= sp.w + 1; t += 4) {  // four loads in flight, added in tile order
-      const A h0 = head[t], h1 = head[t + 1], h2 = head[t + 2], h3 = head[t + 3];
-      s += h0;
-      s += h1;
-      s += h2;
-      s += h3;
+    for (int t = sp.z + 1; t <= sp.w; t += 8) {  // eight loads in flight, added in tile order
+      A h[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) h[j] = t + j <= sp.w ? head[t + j] : A(0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (t + j <= sp.w) s += h[j];
     }
-    for (; t <= sp.w; ++t) s += head[t];
     static_cast<A*>(a.Gs)[static_cast<long long>(sp.x) * a.ld + sp.y] = s;
   } else if (i < a.nspan + a.nempty) {
     const int2 e = a.empty[i - a.nspan];
