@@ -10,16 +10,17 @@
 //   pass 1 (rows): u_r = residual(x_r . beta, y_r, 1) for every distinct row r.  ELL layout
 //     (constant nnz per row, every one-hot dataset): idx column-major [m][rows], 16-bit offsets into
 //     feature k's category window [lo_k, lo_k + 2^16) when every window fits (half the bytes of
-//     int32 columns), one thread per row, beta gathered from L2; CSR: a 16-lane group per row.
+//     int32 columns), a row pair per thread gathering beta from LDS when it fits (else one row per
+//     thread, beta from L2); CSR: a 16-lane group per row.
 //   pass 2 (columns): g_p = X_p^T u_p from a CSC twin of each partition (row indices sorted by
-//     (column, row), 16-bit when the partition has <= 65536 rows), cut into 512-entry tiles, one
-//     wave per tile.  The wave finds every entry's column from the tile's column boundaries (an
-//     integer count in LDS, then a scan), gathers u, and runs a segmented scan keyed by the column:
-//     a sequential sum over each lane's 8 entries, then a Kogge-Stone scan of (restart, sum) over
-//     the 64 lanes.  A column inside one tile is written by the lane that holds its last entry; a
-//     column crossing tiles leaves its first part in tail[t1] and its parts in later tiles in
-//     head[t] (pass 3 adds them, one wave per column, in a fixed order); empty columns are written
-//     0 by pass 3.
+//     (column, row)), cut into 4096-row sub-blocks and 512-entry tiles.  A 1024-thread workgroup
+//     stages one sub-block's residuals in LDS and takes 16 of its tiles, one wave each, 8 entries
+//     per lane.  The row indices' top bit flags every run start (first entry of a column or of the
+//     tile): the segmented sums restart at the flags -- a sequential sum over the lane's 8 entries,
+//     then an affine scan of (continues, sum) over the 64 lanes on DPP -- and each run's sum is
+//     compacted in LDS by run index and written to the run's column (the tile's run list).  A column
+//     crossing tiles leaves its first part in tail[t1] and its later parts in head[t] (pass 3 adds
+//     them in tile order); the sub-block sums are added per partition inside the encoding.
 //   encode (encode.hip): G[message] = sum_p coef(message, p) g_p in a fixed order -- the label
 //     encoding is linear in the coefficient (residual(z, y, c) = c residual(z, y, 1)), so one
 //     read of a partition feeds every co-located replica with its own coefficient.
