@@ -28,6 +28,10 @@ Reported on rank 0 as ONE JSON line:
                           loss_target = naive (exact, uncoded GD) 100-round loss + 1 %
   ranks                   per-rank breakdown: hosted workers, transport, kernel / put /
                           wait / decode+update microseconds (Trainer.rank_report)
+  straggler_virtual       N = 1: the paper's claim under the reference's straggler model -- naive,
+                          AGC with the reference's drain and AGC with the lazy drain under
+                          Exp(--straggler-mean-ms) virtual delays: Σtimeset, loop wall-clock, their
+                          delay floors and wall-clock to the common loss target (virtual_straggler_block)
 """
 from __future__ import annotations
 
@@ -93,9 +97,13 @@ def parse(argv=None):
     ap.add_argument("--late-ms", type=float, default=5.0,
                     help="N > 1 straggler sub-run: the last rank is physically late by this much every round")
     ap.add_argument("--straggler-steps", type=int, default=40, help="timed rounds of each straggler sub-run")
+    ap.add_argument("--straggler-mean-ms", type=float, default=5.0,
+                    help="N = 1 straggler block: mean of the Exp virtual delays (the reference's 0.5 s scaled "
+                         "down 100x; every delay floor scales linearly in it)")
     ap.add_argument("--slab-mode", type=int, default=None, help=argparse.SUPPRESS)  # A/B of the slab reduction form
     ap.add_argument("--no-straggler", action="store_true",
-                    help="N > 1: skip the reference-topology and straggler sub-runs")
+                    help="skip the straggler runs (N = 1: the virtual-delay block; N > 1: the reference-topology "
+                         "and physically-late-rank sub-runs)")
     return ap.parse_args(argv)
 
 
@@ -144,7 +152,7 @@ def main(argv=None) -> int:
 
         native().set_slab_reduce_mode(a.slab_mode)
 
-    def make_cfg(rounds: int, naive: bool = a.naive, **kw) -> RunConfig:
+    def make_cfg(rounds: int, naive: bool = a.naive, ver: int = a.coded_ver, **kw) -> RunConfig:
         opts = dict(add_delay=a.add_delay, num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234,
                     seed=0, allow_uneven_groups=True, verbose=False, tasks=a.tasks, transport=a.transport,
                     round_timeout=a.round_timeout, share_partitions=a.share_partitions, device_loop=a.device_loop,
@@ -154,7 +162,7 @@ def main(argv=None) -> int:
         opts.update(kw)
         add_delay = opts.pop("add_delay")
         return RunConfig(a.workers + 1, a.n_rows, a.n_cols, "/tmp/erasurehead_bench/", 0, "synthetic",
-                         0 if naive else 1, a.stragglers, 0, a.coded_ver, a.num_collect, add_delay, a.update_rule,
+                         0 if naive else 1, a.stragglers, 0, ver, a.num_collect, add_delay, a.update_rule,
                          **opts)
 
     def free(tr):
@@ -401,6 +409,20 @@ def main(argv=None) -> int:
             out["naive_final_train_loss"] = float(ev_n.training_loss[-1])
             out["final_test_auc"] = float(ev.auc[-1])
             out["floor_run_wallclock_s"] = float(r2.total_time)
+
+    # ---- 4. N = 1: the paper's claim under the reference straggler model ----------------------------
+    # The reference's delay model (Exp per worker per round, seeded by the round index, after compute
+    # and before the send: ref src/approximate_coding.py:198-205) with its mean scaled from 0.5 s to
+    # --straggler-mean-ms, applied as virtual arrival times by the native collector (the GPU never
+    # sleeps).  naive (waits for every worker), AGC with the reference's Waitall drain (ref :182-183)
+    # and AGC with the lazy drain (no wait for the tail, a worker still busy skips the stale round: the
+    # replacement of the reference's send Cancel, ref src/coded.py:178-180) run one after another, each
+    # for --floor-rounds rounds, and are compared on wall-clock to the common loss target.
+    if env.world == 1 and not a.no_straggler and not a.no_floor:
+        blk = virtual_straggler_block(a, make_cfg, env, free, Trainer, evaluate,
+                                      out.get("ms_per_step", 0.0) / 1e3 if env.is_master else 0.0)
+        if env.is_master:
+            out["straggler_virtual"] = blk
     env.barrier()
     if env.is_master:
         line = json.dumps(out)
@@ -410,6 +432,84 @@ def main(argv=None) -> int:
                 f.write(line + "\n")
     env.shutdown()
     return 0
+
+
+STRAGGLER_RUNS = (("naive", True, None), ("agc_drain", False, "all"), ("agc_lazy", False, "lazy"))
+
+
+def virtual_straggler_block(a, make_cfg, env, free, Trainer, evaluate, compute_s: float) -> dict:
+    """Run naive / AGC drain / AGC lazy under Exp(--straggler-mean-ms) virtual delays (section 4 of
+    main) and summarise them (straggler_summary); None on ranks other than the master."""
+    from erasurehead_amd.utils.delay import schedule_floors
+
+    mean = a.straggler_mean_ms / 1e3
+    R, W = a.floor_rounds, a.workers
+    delays = np.stack([np.random.RandomState(i).exponential(mean, W) for i in range(R)])  # ref src/naive.py:146
+    runs = {}
+    for name, naive, drain in STRAGGLER_RUNS:
+        tr = Trainer(make_cfg(R, naive=naive, ver=3, add_delay=1, delay_mode="exp", delay_mean=mean,
+                              delay_on="collector", drain=drain), env)
+        r = tr.run()
+        free(tr)
+        if not env.is_master:
+            continue
+        groups = list(tr.scheme.group_of)
+        rule, k = ("all", W) if naive else ("frc", a.num_collect)
+        fl_dec, fl_loop = schedule_floors(delays, rule, k, groups, drain=tr.drain_mode)
+        _, model_loop = schedule_floors(delays, rule, k, groups, drain=tr.drain_mode, compute=compute_s)
+        tr.cfg.fix_quirks = True  # training loss over every partition
+        ev = evaluate(tr, r, write=False)
+        runs[name] = {
+            "drain": tr.drain_mode,
+            "round_loop": tr.device_loop or ("native pump" if tr.native_loop else "python"),
+            "timeset": [float(x) for x in r.timeset], "loop_time": [float(x) for x in r.loop_time],
+            "train_loss": [float(x) for x in ev.training_loss], "final_test_auc": float(ev.auc[-1]),
+            "floor_timeset_s": fl_dec, "floor_loop_s": fl_loop, "model_loop_s": model_loop,
+            "run_wallclock_s": float(r.total_time),
+            "stale_skipped": int(tr.rank_stats.get("stale_skipped_virtual", 0) or 0),
+            "used_workers_per_round": float(np.mean([(np.asarray(x) >= 0).sum() for x in r.worker_timeset])),
+        }
+        del tr, r
+    return straggler_summary(runs, R, mean) if env.is_master else None
+
+
+def straggler_summary(runs: dict, rounds: int, mean_s: float) -> dict:
+    """The straggler block's JSON: per run Σtimeset, loop wall-clock, their zero-compute delay floors,
+    overheads, iterations / Σtimeset / wall-clock to the common target (naive's final training loss
+    + 1 %), and the headline comparison: AGC-lazy wall-clock to target against naive's."""
+    target = float(runs["naive"]["train_loss"][-1]) * 1.01
+    out = {"delay_model": f"Exp(mean {1e3 * mean_s:g} ms) per worker per round, seed = round (the reference's "
+                          f"0.5 s mean scaled down; virtual arrival times on the collector's clock)",
+           "delay_mean_s": mean_s, "rounds": rounds, "loss_target": target,
+           "loss_target_definition": "naive (exact uncoded GD) training loss after %d rounds + 1%%" % rounds,
+           "floor_definition": "zero-compute replay of the same delays under the run's stop rule and drain "
+                               "(utils/delay.schedule_floors); model_loop_s adds the headline round time as "
+                               "every worker's compute"}
+    for name, r in runs.items():
+        tl = np.asarray(r["train_loss"])
+        hit = np.nonzero(tl <= target)[0]
+        cum_ts, cum_lp = np.cumsum(r["timeset"]), np.cumsum(r["loop_time"])
+        sum_ts, sum_lp = float(cum_ts[-1]), float(cum_lp[-1])
+        out[name] = {
+            "drain": r["drain"], "round_loop": r["round_loop"],
+            "sum_timeset_s": sum_ts, "loop_wallclock_s": sum_lp, "run_wallclock_s": r["run_wallclock_s"],
+            "floor_timeset_s": r["floor_timeset_s"], "floor_loop_s": r["floor_loop_s"],
+            "model_loop_s": r["model_loop_s"],
+            "overhead_ms_per_round": 1e3 * (sum_ts - r["floor_timeset_s"]) / rounds,
+            "loop_overhead_ms_per_round": 1e3 * (sum_lp - r["floor_loop_s"]) / rounds,
+            "iters_to_target": int(hit[0]) + 1 if hit.size else None,
+            "timeset_s_to_target": float(cum_ts[hit[0]]) if hit.size else None,
+            "wallclock_s_to_target": float(cum_lp[hit[0]]) if hit.size else None,
+            "final_train_loss": float(tl[-1]), "final_test_auc": r["final_test_auc"],
+            "stale_skipped": r["stale_skipped"], "used_workers_per_round": r["used_workers_per_round"],
+        }
+    base = out["naive"]["wallclock_s_to_target"]
+    for name in runs:
+        w = out[name]["wallclock_s_to_target"]
+        out[name]["speedup_to_target_vs_naive"] = base / w if base and w else None
+    lazy = out.get("agc_lazy", {}).get("wallclock_s_to_target")
+    out["agc_lazy_beats_naive_to_target"] = bool(lazy is not None and base is not None and lazy < base)
+    return out
 
 
 def decode_row_fraction(scheme, arrivals_log, Arrival) -> float:

@@ -66,6 +66,7 @@ struct ArbArgs {
   long long inbox_tag_off;               // bytes from a worker inbox base to its tag slots
   CheckList* checks;                     // [2] device memory: the mailbox rows rounds i-1 / i decoded
   IntegrityErr* err;                     // host-mapped: the first failed check
+  int strict;                            // set by arbiter_round_launch (launchers.h strict_release)
 };
 // Round statuses in the log: 0 ok, 1 timeout, 2 not decodable, 3 skipped, 4 integrity failure of the
 // PREVIOUS round's messages (found by its arbiter_check; details in ArbArgs::err).

@@ -35,7 +35,9 @@ __device__ __forceinline__ bool rule_holds(int rule, int k, int W, int G, int cn
 // Polls are relaxed system-scope loads (they bypass the caches); the poll that ends step 1 is followed
 // by ONE acquire fence of wave 0 before the barrier that releases the other waves' message loads (the
 // MI355X guide's consumer form: an acquire per poll is an L1 invalidate each, 2-3x slower per hop).
-__device__ __forceinline__ unsigned long long load_counter(const unsigned long long* p) {
+// strict (launchers.h strict_release): every poll is an acquire load, the form before round 4.
+__device__ __forceinline__ unsigned long long load_counter(const unsigned long long* p, bool strict) {
+  if (strict) return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
   return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -141,7 +143,7 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
     int cnt0 = 0, cnt1 = 0, cntg = 0, stopped = 0, narr = 0;
     for (int it = 0;; ++it) {
       const long long t = wall_clock64();
-      const bool mine = tid < a.nsrc && !(seen >> tid & 1) && load_counter(reinterpret_cast<const unsigned long long*>(a.src_flag[tid])) >= static_cast<unsigned long long>(i + 1);
+      const bool mine = tid < a.nsrc && !(seen >> tid & 1) && load_counter(reinterpret_cast<const unsigned long long*>(a.src_flag[tid]), a.strict) >= static_cast<unsigned long long>(i + 1);
       const unsigned long long nm = __ballot(mine);
       if (it == 0 || nm) {
         // (a) this poll's batch: its probes in probe-id order (the local ones on the first poll)
@@ -404,7 +406,7 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
     const long long t0 = wall_clock64();
     const unsigned long long all_src = a.nsrc >= 64 ? ~0ull : ((1ull << a.nsrc) - 1);
     for (;;) {
-      const bool mine = tid < a.nsrc && !(seen >> tid & 1) && load_counter(reinterpret_cast<const unsigned long long*>(a.src_flag[tid])) >= static_cast<unsigned long long>(i + 1);
+      const bool mine = tid < a.nsrc && !(seen >> tid & 1) && load_counter(reinterpret_cast<const unsigned long long*>(a.src_flag[tid]), a.strict) >= static_cast<unsigned long long>(i + 1);
       seen |= __ballot(mine);
       if ((seen & all_src) == all_src) break;
       if (wall_clock64() - t0 > a.deadline_ticks) {
@@ -429,12 +431,12 @@ __global__ void __launch_bounds__(1024) arbiter_round(const ArbArgs a, int i, in
     for (int t = tid; t < a.ntarget; t += blockDim.x)
       reinterpret_cast<MsgTag*>(reinterpret_cast<char*>(a.targets[2 * t]) + a.inbox_tag_off)[i + 1] =
           MsgTag{static_cast<unsigned int>(i + 2), 0u, s_bsum};
-  block_release_system();  // one write-back for every inbox row and tag (common.h)
+  block_release_system(a.strict);  // one write-back for every inbox row and tag (common.h)
   if (tid == 0) {
     if (i + 1 < a.R) {
-      for (int t = 0; t < a.ntarget; ++t)  // relaxed: ordered by the release above
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.targets[2 * t + 1]),
-                           static_cast<unsigned long long>(i + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int t = 0; t < a.ntarget; ++t)  // relaxed unless strict: ordered by the release above
+        publish_u64(reinterpret_cast<unsigned long long*>(a.targets[2 * t + 1]), static_cast<unsigned long long>(i + 2),
+                    a.strict);
     }
     const long long te = wall_clock64();
     tl[2] = te;
@@ -482,10 +484,12 @@ __global__ void __launch_bounds__(1024) arbiter_check(const ArbArgs a, int i) {
 
 hipError_t arbiter_round_launch(const ArbArgs& a, int round, int msg_dtype, hipStream_t st, bool check_prev) {
   if (a.W > kArbMaxW || a.nprobe > kArbMaxProbes || a.nsrc > kArbMaxSrc || a.nsrc > 64) return hipErrorInvalidValue;
+  ArbArgs b = a;
+  b.strict = strict_release() ? 1 : 0;
   if (msg_dtype == 0)
-    hipLaunchKernelGGL(arbiter_round<double>, dim3(1), dim3(1024), 0, st, a, round, check_prev ? 1 : 0);
+    hipLaunchKernelGGL(arbiter_round<double>, dim3(1), dim3(1024), 0, st, b, round, check_prev ? 1 : 0);
   else
-    hipLaunchKernelGGL(arbiter_round<float>, dim3(1), dim3(1024), 0, st, a, round, check_prev ? 1 : 0);
+    hipLaunchKernelGGL(arbiter_round<float>, dim3(1), dim3(1024), 0, st, b, round, check_prev ? 1 : 0);
   return hipGetLastError();
 }
 

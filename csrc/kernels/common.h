@@ -309,14 +309,32 @@ __device__ __forceinline__ bool gate_closed(const int* gate) {
 // wave: 16 per 1024-thread arbiter) and release-ordered flag stores (one more write-back per store:
 // the arbiter's per-target counters made its release grow with the rank count, 4.3 us at 2 ranks,
 // 12.2 at 8, profiles/round3/arbiter_books).  Call from every thread (block-uniform control flow).
-__device__ __forceinline__ void block_release_system() {
+//
+// strict (launchers.h strict_release(), ERASUREHEAD_STRICT_RELEASE=1): the forms before round 4 on top
+// -- every thread also fences at system scope, and publish_u64 / the block counters are release /
+// acq_rel ordered.  A switch for first contact with a cross-GPU (xGMI) node: the relaxed forms are
+// measured only with every rank on one GPU so far.
+__device__ __forceinline__ void block_release_system(bool strict = false) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (strict) __threadfence_system();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     // the compiler may drop the wait behind the write-back (ROCm 7.2 / gfx950): keep it explicit
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+}
+// A flag / counter store that announces what block_release_system released (one thread calls it).
+__device__ __forceinline__ void publish_u64(unsigned long long* p, unsigned long long v, bool strict) {
+  if (strict)
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  else
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// The per-launch block counter of a multi-block put: the previous count.
+__device__ __forceinline__ unsigned int count_block_done(unsigned int* counter, bool strict) {
+  return strict ? __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
+                : __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace eh

@@ -1118,10 +1118,10 @@ slab_reduce_fused_put(const A* __restrict__ slab, const int* __restrict__ slot_t
     const unsigned long long ws = wave_sum_u64(c < ld ? tag_term(elem_bits(s), c) : 0ull);
     if (threadIdx.x == 0 && ws) atomicAdd(put.csum + slot, ws);
   }
-  block_release_system();  // this block's mailbox columns (and checksum adds) are out before its count
+  block_release_system(put.strict);  // this block's mailbox columns (and checksum adds) are out before its count
   if (threadIdx.x == 0) {
     const unsigned int total = gridDim.x * gridDim.y;
-    const unsigned int prev = __hip_atomic_fetch_add(put.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int prev = count_block_done(put.counter, put.strict);
     s_last = prev == total - 1;
     if (s_last) __hip_atomic_store(put.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1134,9 +1134,9 @@ slab_reduce_fused_put(const A* __restrict__ slab, const int* __restrict__ slot_t
     }
     if (put.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(put.dst)[1] ^= 0x10;  // test hook
   }
-  block_release_system();  // the tags before the flag
+  block_release_system(put.strict);  // the tags before the flag
   if (threadIdx.x == 0) {
-    __hip_atomic_store(put.flag, put.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    publish_u64(put.flag, put.value, put.strict);
     put_decide_next_gate(put);
   }
 }
@@ -1180,10 +1180,10 @@ slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, Put
     const unsigned long long bs = block_sum_u64(term, scratch);
     if (threadIdx.x == 0 && bs) atomicAdd(put.csum + slot, bs);
   }
-  block_release_system();  // this block's mailbox columns (and checksum adds) are out before its count
+  block_release_system(put.strict);  // this block's mailbox columns (and checksum adds) are out before its count
   if (threadIdx.x == 0) {
     const unsigned int total = gridDim.x * gridDim.y;
-    const unsigned int prev = __hip_atomic_fetch_add(put.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int prev = count_block_done(put.counter, put.strict);
     s_last = prev == total - 1;
     if (s_last) __hip_atomic_store(put.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1196,9 +1196,9 @@ slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, Put
     }
     if (put.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(put.dst)[1] ^= 0x10;  // test hook
   }
-  block_release_system();  // the tags before the flag
+  block_release_system(put.strict);  // the tags before the flag
   if (threadIdx.x == 0) {
-    __hip_atomic_store(put.flag, put.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    publish_u64(put.flag, put.value, put.strict);
     put_decide_next_gate(put);
   }
 }
@@ -1257,9 +1257,9 @@ slab_reduce_final_put1(const A* __restrict__ part, A* __restrict__ G, int ld, in
     if (tid < nslots) put.tag[tid] = MsgTag{static_cast<unsigned int>(put.value), put.rank, tsum[tid]};
     if (put.corrupt && tid == 0) static_cast<unsigned char*>(put.dst)[1] ^= 0x10;  // test hook
   }
-  block_release_system();  // the rows and tags before the flag
+  block_release_system(put.strict);  // the rows and tags before the flag
   if (tid == 0) {
-    __hip_atomic_store(put.flag, put.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    publish_u64(put.flag, put.value, put.strict);
     put_decide_next_gate(put);
   }
 }
@@ -1319,6 +1319,12 @@ static hipError_t slab_reduce_launch(const A* slab, const int* stb, A* part, A* 
                                      hipStream_t st, const PutDesc* put = nullptr, const int* gate = nullptr) {
   if (put && put->tag && (nslots > kMaxTagRows || !put->csum)) return hipErrorInvalidValue;
   if (put && put->gate != gate) return hipErrorInvalidValue;  // one round, one gate
+  PutDesc pd{};
+  if (put) {  // the process's release form (launchers.h strict_release)
+    pd = *put;
+    pd.strict = strict_release() ? 1 : 0;
+    put = &pd;
+  }
   const dim3 fgrid(ceil_div(ld, kWave), nslots);
   if (g_slab_mode != 0 && !put) {  // both stages in one launch (bitwise the same sums)
     hipLaunchKernelGGL(slab_reduce_fused<A>, fgrid, dim3(1024), 0, st, slab, stb, G, ld, gate);

@@ -7,9 +7,22 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "integrity.h"
 
 namespace eh {
+
+// ERASUREHEAD_STRICT_RELEASE=1: every put / signal / arbiter release in this process uses the
+// release-ordered forms (common.h block_release_system(strict), publish_u64) and the arbiter polls
+// with acquire loads.  Read once; the launchers stamp it into PutDesc::strict / ArbArgs::strict.
+inline bool strict_release() {
+  static const bool on = [] {
+    const char* e = std::getenv("ERASUREHEAD_STRICT_RELEASE");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
 
 // ---- worker gradient (grad_dense.hip, grad_sparse.hip) -------------------------------
 // dtype: 0 fp64 storage/acc, 1 fp32/fp32, 2 bf16 storage/fp32 acc; loss: 0 logistic, 1 least squares
@@ -180,6 +193,7 @@ struct PutDesc {
   int* next_gate;
   const unsigned long long* beta_flag;
   unsigned long long stale_next;
+  int strict;  // set by the launchers from strict_release() (common.h block_release_system)
 };
 #if defined(__HIPCC__)
 // The next round's gate word (one thread of the launch calls it).
@@ -196,6 +210,8 @@ struct PutArgs {
 };
 hipError_t put_signal_launch(const PutArgs& args, int blocks, hipStream_t st);
 hipError_t signal_launch(unsigned long long* flag, unsigned long long value, hipStream_t st);
+// *gate = (*counter >= at_least), one thread, stream-ordered (a p2p worker round's stale-round gate).
+hipError_t gate_launch(const unsigned long long* counter, unsigned long long at_least, int* gate, hipStream_t st);
 
 // Receiver-side check of the tagged rows of one put (integrity.h): rows [nrows][ld] of es-byte
 // elements against tags[nrows] for counter value round1 and sender `rank`; first failure -> err.

@@ -88,11 +88,11 @@ __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
     for (int r = threadIdx.x; r < p.rows; r += blockDim.x)
       if (row_sum[r]) atomicAdd(p.csum + r, row_sum[r]);
   }
-  block_release_system();  // this block's rows (and checksum adds) are out before its count
+  block_release_system(p.strict);  // this block's rows (and checksum adds) are out before its count
   if (threadIdx.x == 0) {
     // relaxed: the release above ordered the block's stores; the last block reads only the
     // checksum sums, which are L2 atomics
-    const unsigned int prev = __hip_atomic_fetch_add(p.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int prev = count_block_done(p.counter, p.strict);
     s_last = prev == gridDim.x - 1;
     if (s_last) __hip_atomic_store(p.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -105,9 +105,9 @@ __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
     }
     if (p.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(p.dst)[1] ^= 0x10;  // test hook
   }
-  block_release_system();  // the tags before the flag
+  block_release_system(p.strict);  // the tags before the flag
   if (threadIdx.x == 0) {
-    __hip_atomic_store(p.flag, p.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    publish_u64(p.flag, p.value, p.strict);
     put_decide_next_gate(p);
   }
 }
@@ -117,6 +117,15 @@ __global__ void signal_only(unsigned long long* flag, unsigned long long value) 
   __threadfence_system();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Stale-round gate of a p2p worker round (engine.cpp WorkerPump::set_skip_stale_comm): the worker's
+// beta counter (bumped behind every beta receive on its beta stream) against `at_least`, snapshotted
+// into the round's gate word so every kernel of the round reads one launch-uniform value.
+__global__ void gate_from_counter(const unsigned long long* counter, unsigned long long at_least, int* gate) {
+  const unsigned long long v =
+      __hip_atomic_load(const_cast<unsigned long long*>(counter), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(gate, v >= at_least ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Receiver check of the tagged rows of one put: one block, rows in turn (beta: one row).
@@ -232,7 +241,15 @@ hipError_t put_signal_launch(const PutArgs& args, int blocks, hipStream_t st) {
                   (p.bytes / 16) % p.rows != 0))
       return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(put_signal, dim3(blocks, args.n), dim3(256), 0, st, args);
+  PutArgs a = args;
+  for (int k = 0; k < a.n; ++k) a.d[k].strict = strict_release() ? 1 : 0;  // launchers.h
+  hipLaunchKernelGGL(put_signal, dim3(blocks, a.n), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t gate_launch(const unsigned long long* counter, unsigned long long at_least, int* gate, hipStream_t st) {
+  if (!counter || !gate) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gate_from_counter, dim3(1), dim3(1), 0, st, counter, at_least, gate);
   return hipGetLastError();
 }
 

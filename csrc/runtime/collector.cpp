@@ -29,7 +29,7 @@ Collector::Collector(int n_workers, std::vector<int> group_of, int n_groups)
   group_done_.assign(std::max(n_groups_, 1), 0);
   nsh_.assign(2 * W_, 1);
   got_sh_.assign(2 * W_, 0);
-  last_seen_.assign(2 * W_, -kInf);
+  seen_at_.assign(2 * W_, {});
 }
 
 void Collector::set_shards(int worker, int part, int n) {
@@ -122,6 +122,14 @@ bool Collector::maybe_skip(Probe& p) {
   return true;
 }
 
+double Collector::busy_from(int mi, int round, double t_start) const {
+  // the latest earlier round in which this message was seen (rounds a worker skipped have no entry)
+  const auto& sa = seen_at_[mi];
+  for (int r = std::min(round, static_cast<int>(sa.size())) - 1; r >= 0; --r)
+    if (sa[r] > -kInf) return std::max(t_start, sa[r]);
+  return t_start;
+}
+
 double Collector::finish_of(int worker, int round) const {
   if (round < 0) return -kInf;
   const auto& f = finish_[worker];
@@ -135,9 +143,11 @@ void Collector::mark_seen(int id, double t) {
   p.seen = true;
   p.t_seen = t;
   const double ts = p.round < static_cast<int>(round_start_.size()) ? round_start_[p.round] : t;
-  double& last = last_seen_[2 * p.worker + (p.part ? 1 : 0)];
-  const double busy_from = std::max(ts, last);  // this round's work began after the previous round's
-  last = std::max(last, t);
+  const int mi = 2 * p.worker + (p.part ? 1 : 0);
+  const double from = busy_from(mi, p.round, ts);  // this round's work began after the previous round's
+  auto& sa = seen_at_[mi];
+  if (static_cast<int>(sa.size()) <= p.round) sa.resize(p.round + 1, -kInf);
+  sa[p.round] = std::max(sa[p.round], t);
   auto& f = finish_[p.worker];
   if (static_cast<int>(f.size()) <= p.round) f.resize(p.round + 1, -kInf);
   if (p.physical) {  // a really late rank: seen = arrived
@@ -145,7 +155,7 @@ void Collector::mark_seen(int id, double t) {
     p.ready = t + p.delay;
   } else {
     p.start = std::max(ts, finish_of(p.worker, p.round - 1));
-    p.ready = p.start + std::max(0.0, t - busy_from) + p.delay;
+    p.ready = p.start + std::max(0.0, t - from) + p.delay;
     if (maybe_skip(p)) return;
   }
   f[p.round] = std::max(f[p.round], p.ready);

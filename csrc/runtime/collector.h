@@ -39,8 +39,10 @@
 // Physical probes: with physically late worker ranks (--delay-on worker) a remote message's seen
 // time IS its arrival (ready = t_seen, or +inf for a dead worker): no virtual carry-over, the rank
 // really was late.  Compute time of a virtual probe is the physical busy time of THIS round:
-// t_seen - max(t_start, the previous round's seen time of that message), so work queued behind an
-// earlier round on one stream is not counted twice when lag carries over.
+// t_seen - max(t_start, the seen time of that message in the latest earlier round it was seen), so work
+// queued behind an earlier round on one stream is not counted twice when lag carries over.  The seen
+// times are kept per round: shards of ONE round seen at t1 < t2 both count from the round start (not
+// the second from the first).
 //
 // Stale-round skipping (drain "lazy", engine/trainer.py): a worker that is still busy with an
 // earlier round when the round AFTER a probe's round begins skips that round, exactly like a
@@ -164,7 +166,9 @@ class Collector {
   std::vector<int> got_sh_;    // [2 * worker + part] shards of the current round ready so far
   std::vector<double> round_start_;
   std::vector<std::vector<double>> finish_;  // [worker][round] virtual finish
-  std::vector<double> last_seen_;            // [2 * worker + part] seen time of the latest probe
+  // [2 * worker + part][round] latest seen time over that round's shards of the message (-inf: none yet)
+  std::vector<std::vector<double>> seen_at_;
+  double busy_from(int mi, int round, double t_start) const;
   bool skip_stale_ = false;
   int n_skipped_ = 0, n_stale_ = 0;
   std::vector<Probe> probes_;

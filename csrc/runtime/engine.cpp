@@ -644,7 +644,10 @@ class MasterPump {
   void finish_run() {
     if (!skip_) return;
     col_->end_run(eh::Collector::now());
-    if (comm_) return;
+    if (comm_) {  // p2p: the end-of-run beta(R) to every worker rank (WorkerPump::run_comm_skip's last wait)
+      put_beta_comm(R_);
+      return;
+    }
     for (const auto& t : targets_)
       hcheck(eh::signal_launch(reinterpret_cast<unsigned long long*>(t.second), static_cast<unsigned long long>(R_) + 1,
                                stream_),
@@ -1279,15 +1282,19 @@ class MasterPump {
   }
 
   // push beta(j) into every worker inbox (put + signal kernels on the pump stream)
+  // one send of beta(j) per worker rank, each on its own stream behind the update that wrote it
+  void put_beta_comm(int j) {
+    const void* src = static_cast<const char*>(beta_in_.data_ptr()) + static_cast<int64_t>(j) * ld_ * es_;
+    hcheck(hipEventRecord(bev_, stream_), "hipEventRecord(beta)");
+    for (int r : comm_peers_) {
+      hcheck(hipStreamWaitEvent(send_st_.at(r), bev_, 0), "hipStreamWaitEvent(beta)");
+      comm_->send(r, src, static_cast<int64_t>(ld_) * es_, send_st_.at(r));
+    }
+  }
   void put_beta(int j) {
-    if (comm_) {  // one send per worker rank, each on its own stream behind the update that wrote beta(j)
-      const void* src = static_cast<const char*>(beta_in_.data_ptr()) + static_cast<int64_t>(j) * ld_ * es_;
+    if (comm_) {
       if (timing_) record_t(j, 0);
-      hcheck(hipEventRecord(bev_, stream_), "hipEventRecord(beta)");
-      for (int r : comm_peers_) {
-        hcheck(hipStreamWaitEvent(send_st_.at(r), bev_, 0), "hipStreamWaitEvent(beta)");
-        comm_->send(r, src, static_cast<int64_t>(ld_) * es_, send_st_.at(r));
-      }
+      put_beta_comm(j);
       if (timing_) record_t(j, 1);
       return;
     }
@@ -1528,7 +1535,25 @@ class WorkerPump {
     skip_flag_ = reinterpret_cast<const unsigned long long*>(beta_flag_dev);
     gate_ = at::zeros({R_ + 1}, at::TensorOptions().dtype(at::kInt).device(at::Device(at::kCUDA, device_)));
   }
-  bool skip_stale() const { return skip_flag_ != nullptr; }
+  // The same over stream-ordered p2p (RCCL / loopback / rccl-self), where a send cannot be skipped: the
+  // rank receives beta on a stream of its own, one round AHEAD of its compute (the reference pre-posts
+  // every Irecv, ref src/naive.py:66-70), and bumps a device counter behind every receive (value j + 1
+  // <=> beta(j) landed).  Round i's gate is snapshotted from it just before the round's gradient: closed
+  // iff beta(i+1) already landed, i.e. the master decided round i before this rank could start it.  A
+  // skipped round still SENDS (its stale rows keep the FIFO pairing of the master's receives) and lands
+  // after its round ended, so the master drains it and never decodes it (collector.h stale arrivals).
+  // The master's end-of-run beta(R) (MasterPump::finish_run) closes every round still queued.
+  void set_skip_stale_comm() {
+    need(comm_ != nullptr, "p2p stale-round skipping needs a communicator");
+    if (skip_comm_) return;
+    skip_comm_ = true;
+    gate_ = at::zeros({R_ + 1}, at::TensorOptions().dtype(at::kInt).device(at::Device(at::kCUDA, device_)));
+    bcount_ = at::zeros({1}, at::TensorOptions().dtype(at::kLong).device(at::Device(at::kCUDA, device_)));
+    hcheck(hipStreamCreateWithFlags(&bst_, hipStreamNonBlocking), "hipStreamCreate(beta)");
+    bev_.assign(R_ + 1, nullptr);
+    for (auto& e : bev_) hcheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  }
+  bool skip_stale() const { return skip_flag_ != nullptr || skip_comm_; }
   // Rounds this rank skipped as stale (syncs the stream).
   std::vector<int> skipped_rounds() {
     std::vector<int> out;
@@ -1565,6 +1590,10 @@ class WorkerPump {
   ~WorkerPump() {
     for (auto e : rev_)
       if (e) hipEventDestroy(e);
+    if (bst_) hipStreamSynchronize(bst_);
+    for (auto e : bev_)
+      if (e) hipEventDestroy(e);
+    if (bst_) hipStreamDestroy(bst_);
     for (auto& t : tev_)
       for (auto e : t)
         if (e) hipEventDestroy(e);
@@ -1666,7 +1695,62 @@ class WorkerPump {
   }
 
  private:
+  // Beta receives of rounds <= j on the beta stream (set_skip_stale_comm), each followed by the counter
+  // bump and its event.
+  void post_beta_upto(int j) {
+    const int64_t bbytes = static_cast<int64_t>(ld_) * es_;
+    auto* cnt = reinterpret_cast<unsigned long long*>(bcount_.data_ptr<int64_t>());
+    for (; posted_ <= std::min(j, R_); ++posted_) {
+      char* beta = static_cast<char*>(inbox_.data_ptr()) + static_cast<int64_t>(posted_) * bbytes;
+      comm_->recv(0, beta, bbytes, bst_);
+      hcheck(eh::signal_launch(cnt, static_cast<unsigned long long>(posted_) + 1, bst_), "signal(beta landed)");
+      hcheck(hipEventRecord(bev_[posted_], bst_), "hipEventRecord(beta)");
+    }
+  }
+  // run_comm with stale-round skipping (set_skip_stale_comm).
+  int run_comm_skip(int a, int b) {
+    py::gil_scoped_release nogil;
+    need(posted_ >= a, "rounds must run in order");
+    auto* cnt = reinterpret_cast<const unsigned long long*>(bcount_.data_ptr<int64_t>());
+    int* gw = gate_.data_ptr<int>();
+    for (int i = a; i < b; ++i) {
+      need(i >= 0 && i < R_, "round out of range");
+      Range tr("eh.worker.round");
+      if (i > a && !event_wait(bev_[i - 1], i - 1)) {  // beta(i-1) never came: the master is gone
+        comm_->abort();
+        return i - 1;
+      }
+      post_beta_upto(i + 1);  // beta(i+1) (or the end-of-run beta(R)) may land while round i waits
+      hcheck(hipStreamWaitEvent(stream_, bev_[i], 0), "hipStreamWaitEvent(beta)");
+      if (n_ == 0) continue;
+      const char* beta = static_cast<const char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * ld_ * es_;
+      char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(i % K_) * g_rows_ * ld_ * es_;
+      // closed iff beta(i+1) landed before this round starts (value i + 2)
+      hcheck(eh::gate_launch(cnt, static_cast<unsigned long long>(i) + 2, gw + i, stream_), "gate(stale round)");
+      if (timing_) record_t(i, 0);
+      for (int k = 0; k < repeat_; ++k) hcheck(g_->launch(beta, g, stream_, gw + i), "worker gradient");
+      if (timing_) record_t(i, 1);
+      if (!late_ticks_.empty() && late_ticks_[i] > 0)  // a skipped round does not spin; the end of the run stops one
+        hcheck(eh::spin_launch(late_ticks_[i], stream_, gw + i, cnt, static_cast<unsigned long long>(R_) + 1),
+               "late worker spin");
+      comm_->send(0, g, static_cast<int64_t>(n_) * ld_ * es_, stream_);  // always: the FIFO pairing
+      if (timing_) record_t(i, 2);
+    }
+    if (b > a && !event_wait(bev_[b - 1], b - 1)) {
+      comm_->abort();
+      return b - 1;
+    }
+    if (b == R_) {  // the master's end-of-run beta(R): nothing may stay posted on the communicator
+      post_beta_upto(R_);
+      if (!event_wait(bev_[R_], R_ - 1)) {
+        comm_->abort();
+        return R_ - 1;
+      }
+    }
+    return -1;
+  }
   int run_comm(int a, int b) {
+    if (skip_comm_) return run_comm_skip(a, b);
     py::gil_scoped_release nogil;
     const int64_t bbytes = static_cast<int64_t>(ld_) * es_;
     for (int i = a; i < b; ++i) {
@@ -1787,6 +1871,11 @@ class WorkerPump {
   std::vector<long long> late_ticks_;    // [R] device spin before the put (--delay-on worker)
   const unsigned long long* skip_flag_ = nullptr;  // beta counter read by the stale-round gates (lazy drain)
   Tensor gate_;                          // int32 [R + 1] stale-round gates (1 = round skipped)
+  bool skip_comm_ = false;               // p2p stale-round skipping (set_skip_stale_comm)
+  Tensor bcount_;                        // int64 [1]: j + 1 once beta(j) landed (p2p skipping)
+  hipStream_t bst_ = nullptr;            // beta receive stream (p2p skipping)
+  std::vector<hipEvent_t> bev_;          // [R + 1] beta(j) landed (p2p skipping)
+  int posted_ = 0;                       // beta receives posted on bst_ so far
   int repeat_ = 1;                       // gradient launches per round (--slow-ranks)
   int device_ = 0;
   std::shared_ptr<eh::P2PComm> comm_;    // stream-ordered p2p (null: IPC mailbox)
@@ -1894,6 +1983,7 @@ void bind_engine(py::module& m) {
       .def("set_delays", &WorkerPump::set_delays)
       .def("set_repeat", &WorkerPump::set_repeat)
       .def("set_skip_stale", &WorkerPump::set_skip_stale, py::arg("beta_flag_dev"))
+      .def("set_skip_stale_comm", &WorkerPump::set_skip_stale_comm)
       .def_property_readonly("skip_stale", &WorkerPump::skip_stale)
       .def("skipped_rounds", &WorkerPump::skipped_rounds)
       .def("set_integrity", &WorkerPump::set_integrity, py::arg("mbox_tags"), py::arg("inbox_tags"), py::arg("rank"),

@@ -66,6 +66,8 @@ REPLICA_WEIGHT_DENSE = 0.12
 # SparseGradPlan): a further replica costs one encode row, next to nothing.
 REPLICA_WEIGHT_SPARSE = 0.02
 from ..parallel.transport import make_transport
+
+P2P_TRANSPORTS = ("rccl", "loopback", "rccl-self")  # stream-ordered p2p (csrc/runtime/comm.h)
 from ..utils import report
 from ..utils.delay import DelayModel
 from ..utils.tracing import PhaseTimer
@@ -377,6 +379,13 @@ class Trainer:
         env.barrier()
         self.loop, self.loop_reason = select_round_loop(self.loop_inputs(start))
         native_loop = self.native_loop
+        if self.skip_stale and not native_loop and self.tx is not None and self.tx.name in P2P_TRANSPORTS:
+            # the Python round loop receives beta in stream order (no look-ahead), so a p2p worker cannot
+            # tell that a round is stale before computing it: lazy runs as carry there, and says so
+            why = f"drain lazy runs as carry in the Python round loop over {self.tx.name} (no stale-round skipping)"
+            if env.is_master:
+                print(f"[erasurehead] WARNING: {why}", file=sys.stderr, flush=True)
+            self.rank_stats["drain_downgraded"] = why
         try:
             if env.is_master:
                 res = (self._master_loop_native if native_loop else self._master_loop)(timed_start, log, start)
@@ -599,7 +608,7 @@ class Trainer:
         kern = self._kernel_label()
         if kern:
             rep["grad_kernel"] = kern
-        if self.tx is not None and self.tx.name in ("rccl", "loopback", "rccl-self"):
+        if self.tx is not None and self.tx.name in P2P_TRANSPORTS:
             from .. import HW_QUEUES
 
             rep["hw_queues"] = int(HW_QUEUES)  # what HIP started with, not the (possibly later) environment
@@ -866,8 +875,10 @@ class Trainer:
         pump.set_repeat(self.repeat)
         if self.physical:
             pump.set_delays(self._rank_delays())
-        if self.skip_stale and tx.name == "ipc" and self.n_loc:  # stale-round gates (p2p sends cannot be skipped)
+        if self.skip_stale and tx.name == "ipc" and self.n_loc:  # stale-round gates read the beta counter
             pump.set_skip_stale(tx.flags.dev_addr(env.rank))
+        elif self.skip_stale and tx.name != "ipc":  # p2p: beta received a round ahead, gates from its counter;
+            pump.set_skip_stale_comm()  # every rank, the end-of-run beta(R) goes to all of them
         self.rank_stats["fused_put"] = bool(pump.fused_put)
         self.rank_stats["device_wait"] = bool(pump.device_wait)
         cut = timed_start if timed_start is not None and start <= timed_start < R else None

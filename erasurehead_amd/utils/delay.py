@@ -123,12 +123,26 @@ def schedule(delays: np.ndarray, rule: str, k: int, groups, drain: str = "lazy",
     the stop, a busy worker's start against t_{i+1}) is more than ``margin`` apart -- the rounds a
     physical run with timing noise below the margin must reproduce exactly.
     """
+    out, sep, _, _ = _run_schedule(delays, rule, k, groups, drain, compute, margin)
+    return out, sep
+
+
+def schedule_floors(delays: np.ndarray, rule: str, k: int, groups, drain: str = "lazy", compute: float = 0.0):
+    """(Σ time-to-decode, Σ round length) in seconds of :func:`schedule`'s event model: the floors of a
+    run's Σtimeset and of its loop wall-clock under ``drain`` (zero compute: the injected delays alone).
+    drain "all": a round lasts until its last arrival, its decode happens at the stop; "carry" / "lazy":
+    the next beta leaves at the stop, so both sums are equal."""
+    _, _, dec, rnd = _run_schedule(delays, rule, k, groups, drain, compute, 0.0)
+    return float(np.sum(dec)), float(np.sum(rnd))
+
+
+def _run_schedule(delays, rule, k, groups, drain, compute, margin):
     delays = np.asarray(delays, dtype=np.float64)
     R, W = delays.shape
     n_groups = len(set(groups))
     F = np.full(W, -np.inf)
     t = 0.0
-    out, sep = [], []
+    out, sep, dec, rnd = [], [], [], []
     for i in range(R):
         s = np.maximum(t, F)
         a = s + compute + delays[i]
@@ -159,8 +173,10 @@ def schedule(delays: np.ndarray, rule: str, k: int, groups, drain: str = "lazy",
                 F[w] = a[w]
         out.append(got)
         sep.append(ok)
+        dec.append(t_stop - t)
+        rnd.append(t_next - t)
         t = t_next
-    return out, sep
+    return out, sep, dec, rnd
 
 
 def _carried_floor(n_workers, rounds, stop_count, groups, k, mean) -> float:

@@ -59,6 +59,37 @@ def test_bench_gpus3_relaunches_three_ranks(tmp_path):
     assert st["agc_lazy_round_slowdown"] > 0 and st["naive_round_slowdown"] > 1.0
 
 
+def test_bench_one_gpu_straggler_block(tmp_path):
+    """N = 1 carries the paper's claim in the driver's own JSON: naive, AGC with the reference's drain
+    and AGC with the lazy drain under Exp virtual delays, with floors and wall-clock to the common target
+    (ref src/approximate_coding.py:144-158,182-183,198-205)."""
+    out = tmp_path / "b1.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", *TINY[:-1], "30",
+                        "--straggler-mean-ms", "3", "--no-breakdown", "--clock-warmup-ms", "0",
+                        "--json-out", str(out)],
+                       cwd=str(tmp_path), env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads(out.read_text())
+    st = d["straggler_virtual"]
+    assert st["rounds"] == 30 and st["delay_mean_s"] == pytest.approx(0.003)
+    assert st["loss_target"] == pytest.approx(st["naive"]["final_train_loss"] * 1.01)
+    for name, drain in (("naive", "carry"), ("agc_drain", "all"), ("agc_lazy", "lazy")):
+        x = st[name]
+        assert x["drain"] == drain
+        for k in ("sum_timeset_s", "loop_wallclock_s", "floor_timeset_s", "floor_loop_s", "model_loop_s",
+                  "overhead_ms_per_round", "iters_to_target", "wallclock_s_to_target", "timeset_s_to_target"):
+            assert x[k] is not None, (name, k)
+        # a run never beats the zero-compute replay of its own delays
+        assert x["sum_timeset_s"] >= x["floor_timeset_s"] and x["loop_wallclock_s"] >= x["floor_loop_s"]
+    # AGC decodes with fewer workers; the drain waits for the tail (the naive floor), lazy does not
+    assert st["agc_drain"]["used_workers_per_round"] < 8 == st["naive"]["used_workers_per_round"]
+    assert st["agc_drain"]["floor_loop_s"] == pytest.approx(st["naive"]["floor_loop_s"])
+    assert st["agc_lazy"]["floor_loop_s"] < st["naive"]["floor_loop_s"]
+    assert st["agc_lazy"]["stale_skipped"] > 0
+    assert st["agc_lazy_beats_naive_to_target"] is True
+    assert st["agc_lazy"]["speedup_to_target_vs_naive"] > 1
+
+
 def test_bench_world_size_mismatch_fails(tmp_path):
     env = _env()
     env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")

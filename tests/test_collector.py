@@ -305,3 +305,47 @@ def test_schedule_model_matches_the_collector_rules():
     d2[2, 0] = 0.25  # worker 0 lands at 0.25: before carry's 0.3, after lazy's 0.2
     assert schedule(d2, "count", 1, [0, 1], "lazy")[0][2] == [1]
     assert schedule(d2, "count", 1, [0, 1], "carry")[0][2] == [0]
+
+
+def test_shards_seen_at_different_times_count_from_the_round_start(C):
+    """A message computed as two partition shards on different ranks, seen at t1 < t2 in the same round:
+    each shard's compute counts from the round start (t2 - ts for the second, not t2 - t1), so the
+    message's virtual arrival is at its slowest shard, t2."""
+    c = C.Collector(2, [0, 1], 2)
+    c.set_shards(0, 0, 2)
+    t0 = C.Collector.now() - 1.0  # the round began a second ago: every time below is in the past
+    c.begin_round(0, t0, RULE_ALL, 2)
+    a = c.add_host_probe(0, 0, 0, 0.0)
+    b = c.add_host_probe(0, 0, 0, 0.0)
+    w1 = c.add_host_probe(1, 0, 0, 0.0)
+    c.mark_seen(a, t0 + 0.01)
+    c.mark_seen(b, t0 + 0.03)
+    c.mark_seen(w1, t0 + 0.02)
+    assert c.wait(1.0)
+    got = {x.worker: x.t_rel for x in c.arrivals()}
+    assert got[0] == pytest.approx(0.03, abs=1e-9)
+    assert got[1] == pytest.approx(0.02, abs=1e-9)
+    # round 1: each shard's busy time starts at the round start or at round 0's last shard (t0 + 0.03)
+    t1 = t0 + 0.025
+    c.begin_round(1, t1, RULE_ALL, 2)
+    a = c.add_host_probe(0, 0, 1, 0.0)
+    b = c.add_host_probe(0, 0, 1, 0.0)
+    w1 = c.add_host_probe(1, 0, 1, 0.0)
+    c.mark_seen(a, t1 + 0.015)
+    c.mark_seen(b, t1 + 0.02)
+    c.mark_seen(w1, t1 + 0.001)
+    assert c.wait(1.0)
+    got = {x.worker: x.t_rel for x in c.arrivals()}
+    # worker 0 starts round 1 at its round-0 finish t0 + 0.03 and is busy t1 + 0.02 - (t0 + 0.03) = 0.015
+    assert got[0] == pytest.approx(0.03 + 0.015 - 0.025, abs=1e-9)
+
+
+def test_schedule_floors_sum_the_event_model():
+    import numpy as np
+
+    from erasurehead_amd.utils.delay import schedule_floors
+
+    d = np.array([[0.0, 0.2], [0.0, 0.1], [0.5, 0.0]])
+    assert schedule_floors(d, "count", 1, [0, 1], "lazy") == pytest.approx((0.2, 0.2))
+    # drain all: every round lasts until its last arrival (0.2, 0.1, 0.5); decodes at the first one
+    assert schedule_floors(d, "count", 1, [0, 1], "all") == pytest.approx((0.0, 0.8))

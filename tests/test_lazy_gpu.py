@@ -196,13 +196,25 @@ def test_lazy_fixed_straggler_is_skipped_and_costs_nothing(arbiter, tmp_path):
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
 
 
-def test_carry_keeps_every_round_of_a_late_rank(tmp_path):
+@pytest.mark.parametrize("arbiter", [False, True])
+def test_carry_keeps_every_round_of_a_late_rank(arbiter, tmp_path):
     """The reference's no-Waitall semantics (drain carry): the late rank computes and sends every
-    round in order (no skipping), so it is still busy after the master's last round."""
+    round in order (no skipping), so it is still busy after the master's last round; its late messages
+    of earlier rounds land during later ones and are never decoded.  On the host pump and on the device
+    arbiter, the trajectory replays exactly through the fp64 oracle."""
+    from oracle import replay
+    from test_engine_cpu import make
+
     case, R = (1, 0, 3, 5, 1, 3), 8
     over = dict(add_delay=1, delay_mode="fixed", fixed_stragglers=[4], fixed_sleep=0.03, delay_on="worker",
                 shard="message", drain="carry", num_itrs=R)
-    r, owner, skipped = _lazy_run(4, case, over, tmp_path)
+    env = {"ERASUREHEAD_DEVICE_MASTER": "on"} if arbiter else {}
+    r, owner, skipped = _lazy_run(4, case, over, tmp_path, **env)
+    assert json.loads(str(r["rank_report"]))["round_loop"] == ("arbiter" if arbiter else "native pump")
     assert all(len(v) == 0 for v in skipped)
     for a in r["arrivals"]:
         assert 3 not in {int(w) for (w, p) in a}
+    cfg, src, sch, parts = make(case, "GD")
+    full = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], full, "GD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(R))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)

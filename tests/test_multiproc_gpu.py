@@ -110,6 +110,24 @@ def test_device_arbiter_rounds(world, case_i, wait, drain, tmp_path):
     assert np.all(r["timeset"] > 0)
 
 
+@pytest.mark.parametrize("master", ["on", "off"])
+def test_strict_release_forms(master, tmp_path):
+    """ERASUREHEAD_STRICT_RELEASE=1 (launchers.h strict_release): every put, signal and arbiter release
+    in the job uses the release-ordered stores and acquire polls of before round 4, the switch for a
+    first cross-GPU node; 3 integrity-tagged ranks on the arbiter and on the host pump replay exactly."""
+    from oracle import replay
+    from test_engine_cpu import CASES, make
+
+    r = _launch(3, 4, "AGD", str(tmp_path / "s.npz"), ERASUREHEAD_STRICT_RELEASE="1", ERASUREHEAD_DEVICE_MASTER=master,
+                ERASUREHEAD_WORKER_WAIT="device", EH_TEST_ROUND_TIMEOUT="20")
+    assert str(r["transport"]) == "ipc"
+    assert (str(r["round_loop"]) == "arbiter") == (master == "on")
+    cfg, src, sch, parts = make(CASES[4], "AGD")
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
+
+
 def test_ipc_multiprocess_delayed_agc(tmp_path):
     """AGC (W=6, s=2, k=4) with the reference delay model: the decode only uses fast workers."""
     from oracle import replay

@@ -109,27 +109,9 @@ def run_one(name: str, rounds: int, n_rows: int, n_cols: int, out: str) -> None:
 
 def _schedule_floor(d, rule, k, groups) -> float:
     """Sum of the master's round lengths in the zero-compute lazy-drain event model (t_R)."""
-    from erasurehead_amd.utils.delay import schedule  # noqa: F401 - the model whose stop times are summed
+    from erasurehead_amd.utils.delay import schedule_floors
 
-    R, W = d.shape
-    F = np.full(W, -np.inf)
-    t = 0.0
-    n_groups = len(set(groups))
-    for i in range(R):
-        st = np.maximum(t, F)
-        a = st + d[i]
-        got, cov, t_next = 0, set(), np.inf
-        for w in sorted(range(W), key=lambda w: (a[w], w)):
-            got += 1
-            cov.add(groups[w])
-            if (rule == "count" and got >= k) or (rule == "frc" and (got >= k or len(cov) == n_groups)):
-                t_next = a[w]
-                break
-        for w in range(W):
-            if F[w] <= t or st[w] < t_next:
-                F[w] = a[w]
-        t = t_next
-    return float(t)
+    return schedule_floors(d, rule, k, groups, drain="lazy")[1]
 
 
 def summarize(recs, out_dir: str) -> str:
