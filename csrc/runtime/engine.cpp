@@ -32,6 +32,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -449,7 +450,8 @@ class MasterPump {
       if (e) hipEventDestroy(e);
     if (bev_) hipEventDestroy(bev_);
     for (auto& [r, st] : send_st_) hipStreamDestroy(st);
-    for (auto& [r, st] : recv_st_) hipStreamDestroy(st);
+    for (auto& [r, st] : recv_st_)
+      if (!send_st_.count(r) || send_st_.at(r) != st) hipStreamDestroy(st);  // a shared link stream once
   }
 
   // Per-round HIP-event timing of the beta puts and the local gradient launch (bench.py's
@@ -539,9 +541,19 @@ class MasterPump {
 
   // Stream-ordered p2p instead of the IPC mailbox (runtime/comm.h: RCCL, or its single-GPU loopback):
   // ranks = (worker rank, first mailbox row, rows) of every rank that sends messages; `peers` = every
-  // worker rank (each receives beta).  Call before set_remote.  beta(i) goes out with one send per
-  // peer on that peer's own stream; round i's messages of rank r arrive with one receive into its
-  // mailbox rows on r's receive stream, and the HIP event behind it is the collector's probe.
+  // worker rank (each receives beta).  Call after set_skip_stale, before set_remote.  beta(i) goes out
+  // with one send per peer on that peer's own stream; round i's messages of rank r arrive with one
+  // receive into its mailbox rows, and the HIP event behind it is the collector's probe.
+  //
+  // Streams (each parks its own waits: a stream that shares a hardware queue would hold back the
+  // other streams of that queue, so the count must stay within GPU_MAX_HW_QUEUES):
+  //   drain all / carry  ONE link stream per peer, beta(i) send then round i's receive.  Per pair this
+  //                      is the order both sides need anyway (a worker cannot use beta(i+1) before it
+  //                      has sent round i), and a late peer still blocks only its own link: W - 1 + the
+  //                      compute stream, 8 at 8 ranks.
+  //   lazy               a send and a receive stream per peer: beta(i+1) must reach a late rank while its
+  //                      round-i receive is still pending, so it can find round i stale (WorkerPump::
+  //                      set_skip_stale_comm): 2 (W - 1) + 1, 15 at 8 ranks.
   void set_comm(std::shared_ptr<eh::P2PComm> comm, const std::vector<std::tuple<int, int, int>>& ranks,
                 const std::vector<int>& peers) {
     need(comm != nullptr, "null communicator");
@@ -553,7 +565,10 @@ class MasterPump {
     for (int r : peers) mk(&send_st_[r]);
     for (const auto& [r, row0, n] : ranks) {
       need(n > 0 && row0 >= 0, "bad mailbox rows of a rank");
-      mk(&recv_st_[r]);
+      if (!skip_ && send_st_.count(r))
+        recv_st_[r] = send_st_.at(r);  // the pair's link stream
+      else
+        mk(&recv_st_[r]);
     }
     rev_.assign(static_cast<size_t>(K_) * ranks.size(), nullptr);
     for (auto& e : rev_) hcheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
@@ -635,8 +650,31 @@ class MasterPump {
   // Drain "lazy" (engine/trainer.py): the collector skips stale virtual rounds (collector.h) and, with
   // IPC targets, finish_run() tells every worker rank the run is over so its queued rounds are stale.
   void set_skip_stale(bool on) {
+    need(!(on && comm_ && !comm_streams_split()), "set_skip_stale(true) after set_comm: the link streams are shared");
     skip_ = on;
     col_->set_skip_stale(on);
+  }
+  // Whether every peer's receive has a stream of its own (lazy drain) rather than the pair's link stream.
+  bool comm_streams_split() const {
+    for (const auto& [r, st] : recv_st_)
+      if (send_st_.count(r) && send_st_.at(r) == st) return false;
+    return true;
+  }
+  // The compute stream and every distinct comm stream, in creation order (tests: stream_wait_probe).
+  std::vector<uintptr_t> stream_handles() const {
+    std::vector<uintptr_t> out{reinterpret_cast<uintptr_t>(stream_)};
+    std::set<hipStream_t> seen;
+    for (const auto* m : {&send_st_, &recv_st_})
+      for (const auto& [r, st] : *m)
+        if (seen.insert(st).second) out.push_back(reinterpret_cast<uintptr_t>(st));
+    return out;
+  }
+  // Distinct comm streams this pump created (rank_report: hardware-queue budget).
+  int comm_streams() const {
+    std::set<hipStream_t> all;
+    for (const auto& [r, st] : send_st_) all.insert(st);
+    for (const auto& [r, st] : recv_st_) all.insert(st);
+    return static_cast<int>(all.size());
   }
   // End of the master's rounds (stream-ordered after its last beta put): with skip_stale on, every
   // worker's beta counter goes to R + 1 (as if beta(R) were out), so whatever a late worker rank still
@@ -1887,7 +1925,51 @@ class WorkerPump {
 }  // namespace
 
 namespace eh {
+// Test probe of hardware-queue independence: a wait on its own host flag, then an event, on every given
+// stream; the flags are released in REVERSE order and each stream's event must complete before the next
+// release.  A stream sharing an in-order hardware queue with an earlier one stays parked behind that
+// stream's unreleased wait (its event times out).  Every flag is released before returning, so nothing
+// stays queued.  Returns, per stream, whether its event completed within `timeout` seconds of its release.
+std::vector<bool> stream_wait_probe(const std::vector<uintptr_t>& streams, double timeout) {
+  const size_t n = streams.size();
+  uint64_t* h = nullptr;
+  hcheck(hipHostMalloc(reinterpret_cast<void**>(&h), sizeof(uint64_t) * std::max<size_t>(1, n),
+                       hipHostMallocMapped | hipHostMallocCoherent),
+         "hipHostMalloc(probe flags)");
+  for (size_t k = 0; k < n; ++k) h[k] = 0;
+  uint64_t* d = nullptr;
+  hcheck(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0), "hipHostGetDevicePointer");
+  std::vector<hipEvent_t> ev(n, nullptr);
+  std::vector<bool> ok(n, false);
+  for (size_t k = 0; k < n; ++k) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(streams[k]);
+    hcheck(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "hipEventCreate");
+    hcheck(hipStreamWaitValue64(st, d + k, 1, hipStreamWaitValueGte), "hipStreamWaitValue64(probe)");
+    hcheck(hipEventRecord(ev[k], st), "hipEventRecord(probe)");
+  }
+  {
+    py::gil_scoped_release nogil;
+    for (size_t j = 0; j < n; ++j) {
+      const size_t k = n - 1 - j;
+      __atomic_store_n(h + k, uint64_t{1}, __ATOMIC_RELEASE);
+      const auto t0 = std::chrono::steady_clock::now();
+      for (;;) {
+        const hipError_t q = hipEventQuery(ev[k]);
+        if (q == hipSuccess) { ok[k] = true; break; }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    }
+    for (size_t k = 0; k < n; ++k) __atomic_store_n(h + k, uint64_t{1}, __ATOMIC_RELEASE);
+    for (size_t k = 0; k < n; ++k) hipEventSynchronize(ev[k]);
+  }
+  for (auto e : ev) hipEventDestroy(e);
+  hipHostFree(h);
+  return ok;
+}
+
 void bind_engine(py::module& m) {
+  m.def("stream_wait_probe", &stream_wait_probe, py::arg("streams"), py::arg("timeout"));
   py::class_<GradLauncher, std::shared_ptr<GradLauncher>>(m, "GradLauncher")
       .def_static("dense", &make_dense, py::arg("dtype"), py::arg("loss"), py::arg("cpl"), py::arg("segs"),
                   py::arg("tasks"), py::arg("slab"), py::arg("slot_task_begin"), py::arg("part"), py::arg("ld"),
@@ -1940,6 +2022,8 @@ void bind_engine(py::module& m) {
       .def_property_readonly("comm_kind", &MasterPump::comm_kind)
       .def("set_repeat", &MasterPump::set_repeat)
       .def("set_skip_stale", &MasterPump::set_skip_stale, py::arg("on"))
+      .def_property_readonly("comm_streams", &MasterPump::comm_streams)
+      .def("stream_handles", &MasterPump::stream_handles)
       .def("finish_run", &MasterPump::finish_run)
       .def_property_readonly("skipped", &MasterPump::skipped)
       .def_property_readonly("stale_arrivals", &MasterPump::stale_arrivals)

@@ -645,6 +645,7 @@ class Trainer:
         tx = self.tx
         if tx is not None and tx.name != "ipc":  # RCCL / loopback p2p: receives + events, no IPC counters
             pump.set_comm(tx.comm, tx.sender_rows(), list(range(1, env.world)))
+            self.rank_stats.update(tx.check_queue_budget(int(pump.comm_streams)))
             rem = [(m.worker, m.part, self.rem_slot[(m.worker, m.part, m.shard)], 0, r)
                    for r in sorted(self.remote_msgs) for m in self.remote_msgs[r]]
             pump.set_remote(self.Rbuf, rem)

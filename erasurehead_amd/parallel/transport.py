@@ -210,14 +210,6 @@ class CommTransport(Transport):
             raise ValueError(f"unknown communicator {kind!r}")
         env.barrier()
         self.pairs = []
-        need = 2 * (env.world - 1) + 2  # master: a send and a receive stream per worker rank + compute
-        from .. import HW_QUEUES
-
-        have = HW_QUEUES  # the value the HIP runtime of this process started with (erasurehead_amd/__init__.py)
-        if env.is_master and have < need:
-            print(f"[erasurehead] WARNING: GPU_MAX_HW_QUEUES={have} < {need}: per-peer receive streams share hardware "
-                  "queues, so a straggler's receive can hold back another worker's (set it before HIP starts)",
-                  file=sys.stderr, flush=True)
         self._ps: Dict[int, torch.cuda.Stream] = {}  # python round loop's per-peer streams (created on use)
         if env.is_master:
             self.beta_ev = torch.cuda.Event()
@@ -347,6 +339,19 @@ class CommTransport(Transport):
         return out
 
     # ---- native pumps --------------------------------------------------------------------
+    def check_queue_budget(self, comm_streams: int) -> dict:
+        """Master: the pump's comm streams + the compute stream against the hardware queues HIP started
+        with (erasurehead_amd/__init__.py); streams beyond them share queues, and a receive parked on a
+        straggler would then hold back another worker's.  Warns when over; returns the record."""
+        from .. import HW_QUEUES
+
+        need = comm_streams + 1
+        if need > HW_QUEUES:
+            print(f"[erasurehead] WARNING: {need} streams (comm + compute) > GPU_MAX_HW_QUEUES={HW_QUEUES}: per-peer "
+                  "streams share hardware queues, so a straggler's receive can hold back another worker's (set it "
+                  "before HIP starts)", file=sys.stderr, flush=True)
+        return {"comm_streams": int(comm_streams), "hw_queues": int(HW_QUEUES), "queue_headroom": int(HW_QUEUES - need)}
+
     def sender_rows(self):
         """(rank, first mailbox row, rows) of every worker rank that sends messages (master)."""
         return [(r, self.row0[r], n) for r, n in sorted(self.remote_counts.items()) if n]

@@ -132,12 +132,18 @@ def _lazy_run(world, case, over, tmp_path, **env):
     return r, owner, skipped
 
 
-@pytest.mark.parametrize("world,case,rule,k,groups,mean,R", [
-    (3, (1, 0, 0, 4, 1, 0), "count", 2, [0, 1, 2], 0.12, 14),                  # cyclic W=3 s=1
-    (4, (1, 0, 3, 5, 1, 3), "frc", 3, [0, 0, 1, 1], 0.12, 14),                 # AGC W=4 s=1 k=3
-    (8, (1, 0, 3, 9, 2, 6), "frc", 6, [0, 0, 0, 1, 1, 1, 2, 2], 0.3, 18),      # AGC W=8 s=2 k=6, 8 ranks
+@pytest.mark.parametrize("world,case,rule,k,groups,mean,R,transport,margin", [
+    (3, (1, 0, 0, 4, 1, 0), "count", 2, [0, 1, 2], 0.12, 14, "ipc", MARGIN),                  # cyclic W=3 s=1
+    (4, (1, 0, 3, 5, 1, 3), "frc", 3, [0, 0, 1, 1], 0.12, 14, "ipc", MARGIN),                 # AGC W=4 s=1 k=3
+    (8, (1, 0, 3, 9, 2, 6), "frc", 6, [0, 0, 0, 1, 1, 1, 2, 2], 0.3, 18, "ipc", MARGIN),      # AGC W=8 s=2 k=6
+    # the same over stream-ordered p2p (loopback: RCCL's code path).  Its receives and sends are device-side
+    # stream waits, and 8 processes' parked waits on ONE GPU oversubscribe its hardware queue slots (the
+    # scheduler rotates them): tens of ms of noise that one rank per GPU does not have, so 8 ranks here
+    # get longer delays and a wider margin
+    (3, (1, 0, 0, 4, 1, 0), "count", 2, [0, 1, 2], 0.12, 14, "loopback", MARGIN),
+    (8, (1, 0, 3, 9, 2, 6), "frc", 6, [0, 0, 0, 1, 1, 1, 2, 2], 0.8, 14, "loopback", 0.06),
 ])
-def test_lazy_drain_physically_late_ranks(world, case, rule, k, groups, mean, R, tmp_path):
+def test_lazy_drain_physically_late_ranks(world, case, rule, k, groups, mean, R, transport, margin, tmp_path):
     """--delay-on worker --drain lazy, one logical worker per rank: every worker rank spins Exp(mean)
     after its gradient; the master never waits for the tail and a rank still busy when the next beta
     is out skips that round on the device.  Checked against the event model replayed along the run's
@@ -150,13 +156,15 @@ def test_lazy_drain_physically_late_ranks(world, case, rule, k, groups, mean, R,
 
     over = dict(add_delay=1, delay_mode="exp", delay_mean=mean, delay_on="worker", shard="message", drain="lazy",
                 num_itrs=R)
-    r, owner, skipped = _lazy_run(world, case, over, tmp_path)
+    env = {"ERASUREHEAD_TRANSPORT": transport} if transport != "ipc" else {}
+    r, owner, skipped = _lazy_run(world, case, over, tmp_path, **env)
+    assert str(r["transport"]) == transport
     cfg, src, sch, parts = make(case, "GD")
     W = cfg.n_workers
     d = np.stack([np.random.RandomState(i).exponential(mean, W) for i in range(R)])
     arrivals = [[int(w) for (w, p) in a] for a in r["arrivals"]]
     by_worker = {w: skipped[o] for w, o in owner.items() if o != 0}
-    n_rounds, n_skips = check_lazy(arrivals, r["loop_time"], d, rule, k, groups, MARGIN, by_worker,
+    n_rounds, n_skips = check_lazy(arrivals, r["loop_time"], d, rule, k, groups, margin, by_worker,
                                    local={w for w, o in owner.items() if o == 0})
     assert n_rounds >= 3 and n_skips >= W
     assert sum(len(v) for v in skipped) >= 1  # some rank fell behind and skipped a stale round
@@ -171,20 +179,23 @@ def test_lazy_drain_physically_late_ranks(world, case, rule, k, groups, mean, R,
     assert sum(x.get("stale_rounds_skipped", 0) for x in reports) == sum(len(v) for v in skipped)
 
 
-@pytest.mark.parametrize("arbiter", [False, True])
-def test_lazy_fixed_straggler_is_skipped_and_costs_nothing(arbiter, tmp_path):
+@pytest.mark.parametrize("loop", ["pump", "arbiter", "loopback"])
+def test_lazy_fixed_straggler_is_skipped_and_costs_nothing(loop, tmp_path):
     """AGC W=4 s=1 k=3 on 4 ranks, worker 3's rank 40 ms late every round (fixed straggler, physically
     spun): with drain lazy the master's rounds never wait for it, the rank computes one round, then
-    finds every later round stale and skips it; on the host pump and on the device arbiter."""
+    finds every later round stale and skips it; on the host pump and on the device arbiter over the IPC
+    mailbox, and on the host pump over stream-ordered p2p (loopback, RCCL's code path: the skipped
+    rounds still send their stale rows, which land after their round and are never decoded)."""
     from oracle import replay
     from test_engine_cpu import make
 
     case, R = (1, 0, 3, 5, 1, 3), 16
     over = dict(add_delay=1, delay_mode="fixed", fixed_stragglers=[4], fixed_sleep=0.04, delay_on="worker",
                 shard="message", drain="lazy", num_itrs=R)
-    env = {"ERASUREHEAD_DEVICE_MASTER": "on"} if arbiter else {}
+    env = {"arbiter": {"ERASUREHEAD_DEVICE_MASTER": "on"}, "loopback": {"ERASUREHEAD_TRANSPORT": "loopback"}}.get(loop, {})
     r, owner, skipped = _lazy_run(4, case, over, tmp_path, **env)
-    assert json.loads(str(r["rank_report"]))["round_loop"] == ("arbiter" if arbiter else "native pump")
+    assert json.loads(str(r["rank_report"]))["round_loop"] == ("arbiter" if loop == "arbiter" else "native pump")
+    assert str(r["transport"]) == ("loopback" if loop == "loopback" else "ipc")
     for a in r["arrivals"]:
         assert 3 not in {int(w) for (w, p) in a}
     assert float(np.sum(r["loop_time"])) < 0.04 * R / 4  # the straggler's 40 ms never enter the rounds
