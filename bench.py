@@ -240,6 +240,9 @@ def main(argv=None) -> int:
                 "parallelism": f"ps-master + {a.workers} logical workers on {env.world} GPU rank(s) (dp{env.world})",
                 "transport": trainer.transport,
                 "tie_break": a.tie_break,
+                # replica messages: every replica's own arithmetic ("separate", the headline) or one
+                # gradient per distinct partition encoded into the replicas ("encoded": --share-partitions)
+                "replicas": trainer.replica_policy,
             },
             "time_to_decode_ms_median": float(1e3 * np.median(ts)),
             "loop_ms_median": float(1e3 * np.median(lt)),

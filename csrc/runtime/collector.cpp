@@ -170,7 +170,21 @@ void Collector::poll_events(double t) {
     Probe& p = probes_[id];
     if (p.seen || p.host || p.arrived) continue;
     if (p.flag) {
-      if (__atomic_load_n(p.flag, __ATOMIC_ACQUIRE) >= p.fval) mark_seen(id, t);
+      const uint64_t v = __atomic_load_n(p.flag, __ATOMIC_ACQUIRE);
+      if (v < p.fval) continue;
+      // Lazy drain, virtual probe, counter already PAST this round when first seen: a later round's put
+      // landed, so this round is over at the master either way -- and the worker rank may have skipped it
+      // on the device (its gate found beta(i+1) out), i.e. it never ran.  Charging it compute time would
+      // push the worker's virtual finish out for rounds that follow, so it leaves as skipped.
+      if (skip_stale_ && !p.physical && v > p.fval && p.round < round_) {
+        p.skipped = p.arrived = true;
+        ++n_skipped_;
+        auto& f = finish_[p.worker];
+        if (static_cast<int>(f.size()) <= p.round) f.resize(p.round + 1, -kInf);
+        f[p.round] = finish_of(p.worker, p.round - 1);
+        continue;
+      }
+      mark_seen(id, t);
       continue;
     }
     int hit = -1;

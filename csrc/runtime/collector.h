@@ -49,7 +49,10 @@
 // physical worker whose gate finds the next beta already published (csrc/kernels/common.h
 // gate_closed): the probe never arrives, the worker's finish time carries over to its next round.
 // The decision for a probe of round j is taken when round j+1 begins (or when the probe is seen, if
-// later): skipped iff its virtual start max(t_start(j), finish(w, j-1)) >= t_start(j+1).
+// later): skipped iff its virtual start max(t_start(j), finish(w, j-1)) >= t_start(j+1).  An IPC flag
+// probe first seen with its counter already past round j (a later round's put landed) is skipped too:
+// the worker rank may have skipped round j on the device, and round j is over at the master either way.
+// Both parts of a partial scheme's worker share one virtual start, so they skip together.
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -33,6 +33,7 @@ MI355X design:
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 import sys
@@ -307,6 +308,22 @@ class Trainer:
     @property
     def transport(self) -> str:
         return self.tx.name if self.tx is not None else "local"
+
+    @property
+    def replica_policy(self) -> str:
+        """How this rank's plan forms the replica messages of a partition it hosts several times:
+        "separate" -- every replica does its own arithmetic from the shared read (dense plans, the
+        headline: ref src/approximate_coding.py:185-196 computes each worker's message by itself);
+        "encoded" -- each distinct partition's gradient is computed once with coefficient 1 and the
+        replicas are formed by the device encoding (sparse plans, --share-partitions); "none" -- no
+        partition is hosted twice (naive, ignore-stragglers, one message per rank)."""
+        plan = getattr(self, "plan", None)
+        counts = collections.Counter(p for m in self.local_msgs for p, _ in m.segments)
+        if not counts or max(counts.values()) < 2:
+            return "none"
+        if isinstance(plan, (SharedGradPlan, SparseGradPlan)):
+            return "encoded"
+        return "separate"
 
     # --------------------------------------------------------------------------- helpers
     def _init_beta(self):
@@ -600,6 +617,7 @@ class Trainer:
                                   "round_loop": self.device_loop or ("native pump" if self.native_loop else "python"),
                                   "loop_reason": getattr(self, "loop_reason", None),
                                   "drain": self.drain_mode,
+                                  "replicas": self.replica_policy,
                                   "workers": sorted({int(m.worker) for m in self.local_msgs}),
                                   "messages": len(self.local_msgs),
                                   "partitions": len({p for m in self.local_msgs for p, _ in m.segments})}

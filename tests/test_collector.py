@@ -349,3 +349,28 @@ def test_schedule_floors_sum_the_event_model():
     assert schedule_floors(d, "count", 1, [0, 1], "lazy") == pytest.approx((0.2, 0.2))
     # drain all: every round lasts until its last arrival (0.2, 0.1, 0.5); decodes at the first one
     assert schedule_floors(d, "count", 1, [0, 1], "all") == pytest.approx((0.0, 0.8))
+
+
+def test_lazy_flag_probe_past_its_round_leaves_as_skipped(C):
+    """Drain lazy over the IPC mailbox: a worker rank whose device gate skipped round 0 never signals it;
+    its counter goes straight to round 1's value.  The round-0 probe, first seen with the counter already
+    past it, leaves as skipped (no compute time charged to a round that never ran) instead of arriving."""
+    import numpy as np
+
+    flag = np.zeros(1, dtype=np.uint64)
+    addr = flag.ctypes.data
+    c = C.Collector(2, [0, 1], 2)
+    c.set_skip_stale(True)
+    t0 = C.Collector.now() - 1.0
+    c.begin_round(0, t0, RULE_COUNT, 1)
+    c.mark_seen(c.add_host_probe(0, 0, 0, 0.0), t0)
+    c.add_flag_probe(1, 0, 0, addr, 1, 0.0)
+    assert c.step() and [a.worker for a in c.arrivals()] == [0]
+    c.begin_round(1, t0 + 0.5, RULE_COUNT, 2)
+    c.add_flag_probe(1, 0, 1, addr, 2, 0.0)
+    c.mark_seen(c.add_host_probe(0, 0, 1, 0.0), t0 + 0.5)
+    flag[0] = 2  # round 1's put landed; round 0 was skipped on the device
+    assert c.wait(1.0)
+    assert sorted(a.worker for a in c.arrivals()) == [0, 1]
+    assert c.skipped == 1 and c.stale_arrivals == 0
+    assert c.drain(1, 1.0)

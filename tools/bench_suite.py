@@ -18,8 +18,9 @@ data/synthetic.py onehot_partitions):
   ls_kc_house_*      least squares on kc_house-shaped one-hot (17290 x 27654): naive vs AGC with
                      num_collect in {4,5,6,7}, W=8 s=1
   agc_amazon         AGC W=8 s=1 k=6 on amazon-shaped one-hot (26215 x 241915, 45 nnz/row; 1.94 MB
-                     messages), host-driven with HIP-event instrumentation (gradient / combine+update
-                     kernel microseconds), and naive on the same data (the family's loss target).
+                     messages), and naive on the same data (the family's loss target), both on the same
+                     device-driven loop; agc_amazon_instrumented: the same AGC host-driven with HIP-event
+                     instrumentation (gradient / combine+update kernel microseconds), its own row.
                      Synthetic stand-in: parity unpinned.
 
 Per config: seconds per round (timed, device-synchronised), time-to-decode (reference
@@ -99,6 +100,9 @@ def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_
         "native_loop": tr.native_loop,
         "round_loop": tr.device_loop or ("host-native" if tr.native_loop else "host-python"),
         "precision": cfg.precision,
+        # replica messages (Trainer.replica_policy): "separate" arithmetic per replica (dense), "encoded"
+        # from one gradient per distinct partition (sparse plans), "none" (no partition hosted twice)
+        "replicas": tr.replica_policy,
         "message_bytes": int(tr.ld * torch.tensor([], dtype=tr.prec.acc).element_size()),
         "eval_s": eval_s,
         "grad_kernel_us_isolated": tr.time_local_grad(),
@@ -178,8 +182,11 @@ def main():
     base_am = dict(n_procs=W + 1, n_rows=na, n_cols=da, input_dir="/tmp/eh_suite/", is_real=1,
                    dataset="amazon-dataset", update_rule="AGD")
     configs.append(("naive_amazon", dict(base_am, is_coded=0), src_am, None, False, "amazon"))
+    # the AGC / naive pair runs the same (device-driven) loop; the instrumented host-driven run is its own row
     configs.append(("agc_amazon", dict(base_am, is_coded=1, n_stragglers=1, coded_ver=3, num_collect=6), src_am, None,
-                    True, "amazon"))
+                    False, "amazon"))
+    configs.append(("agc_amazon_instrumented", dict(base_am, is_coded=1, n_stragglers=1, coded_ver=3, num_collect=6),
+                    src_am, None, True, "amazon"))
     if a.only:
         keep = set(a.only.split(","))
         configs = [c for c in configs if c[0] in keep]
@@ -200,16 +207,22 @@ def main():
         t = targets.get(r["family"])
         r["loss_target"] = t
         r["iters_to_target"] = _target_iters(r["train_loss"], t) if t is not None else None
-    hdr = ("| config | scheme | W | s | k | loop | ms/round | timeset ms | iters to naive target | iters to own floor | "
-           "final train loss | AUC | delay floor s | overhead ms/round | msg KB | grad µs | combine µs | eval s |\n"
-           "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|\n")
+    hdr = ("Column `replicas`: how the replica messages of a partition hosted several times are formed -- `separate` "
+           "(every replica's own arithmetic from one shared read: the dense plans, the headline), `encoded` (one "
+           "gradient per distinct partition, replicas formed by the device encoding: the sparse plans) or `none` (no "
+           "partition hosted twice).  Compare AGC against naive within one policy and one loop only.\n\n"
+           "| config | scheme | W | s | k | replicas | loop | ms/round | timeset ms | iters to naive target | "
+           "iters to own floor | final train loss | AUC | delay floor s | overhead ms/round | msg KB | grad µs | "
+           "combine µs | eval s |\n"
+           "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|\n")
     lines = []
     for r in rows:
         tgt = "-" if r["iters_to_target"] is None else str(r["iters_to_target"])
         auc = "%.4f" % r["final_auc"] if r.get("final_auc") is not None else "-"
         fl = "%.2f" % r["delay_floor_s"] if "delay_floor_s" in r else "-"
         ov = "%.3f" % r["overhead_above_floor_ms_per_round"] if "delay_floor_s" in r else "-"
-        lines.append(f"| {r['config']} | {r['scheme']} | {r['W']} | {r['s']} | {r['num_collect']} | {r['round_loop']} | "
+        lines.append(f"| {r['config']} | {r['scheme']} | {r['W']} | {r['s']} | {r['num_collect']} | "
+                     f"{r.get('replicas', '-')} | {r['round_loop']} | "
                      f"{1e3 * r['sec_per_round']:.3f} | {r['timeset_mean_ms']:.3f} | {tgt} | {r['iters_to_loss_floor']} | "
                      f"{r['final_train_loss']:.5f} | {auc} | {fl} | {ov} | {r['message_bytes'] / 1024:.0f} | "
                      f"{r.get('kernel_us', r.get('grad_kernel_us_isolated') or 0):.0f} | "
