@@ -193,10 +193,13 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
 // residual, and both rows' gradients accumulate from four row buffers (the next pair in flight).
 // Narrow rows spend most of their time in the per-row cross-lane reductions (d = 256:
 // profiles/round3/choices), which this halves.
+// stamps (a timeline probe, tools/probes/bundle_stamps.py; nullptr in every production launch): per
+// bundle {start, rows done, slab written, XCC id} in wall_clock64 ticks, one vector store of lane 0 each.
 template <typename T, typename A, int CPL, int LOSS, int R, bool FOLD, int EPI = 0>
 __global__ void __launch_bounds__(256)
 grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ tasks, int nbundles,
-                 const A* __restrict__ beta, A* __restrict__ slab, int ld, const int* __restrict__ gate) {
+                 const A* __restrict__ beta, A* __restrict__ slab, int ld, const int* __restrict__ gate,
+                 long long* __restrict__ stamps) {
   constexpr int VN = Vec16<T>::N;
   constexpr int NV = CPL / VN;
   using Rw = typename Vec16<T>::raw;
@@ -205,6 +208,12 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int bundle = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + wv);
   if (!FOLD && bundle >= nbundles) return;  // FOLD: every wave reaches the barrier (nbundles % 4 == 0)
+  if (stamps && lane == 0) {
+    stamps[4 * bundle] = wall_clock64();
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    stamps[4 * bundle + 3] = xcc;
+  }
   const Task lead = tasks[bundle * R];
   const bool live = lead.seg >= 0;  // FOLD pad bundles: no rows, zero accumulators
   const Segment ls = segs[live ? lead.seg : 0];
@@ -363,6 +372,7 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
       step(xb, yb);
     }
   }
+  if (stamps && lane == 0) stamps[4 * bundle + 1] = wall_clock64();
   if constexpr (FOLD) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fold_raw[];
     A* fb = reinterpret_cast<A*>(fold_raw);  // [3 waves][R][NV * VN][64 lanes]
@@ -396,6 +406,10 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
       for (int v = 0; v < VN; ++v)
         if (c0 + v < ld) out[c0 + v] = g[q][j][v];
     }
+  }
+  if (stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) stamps[4 * bundle + 2] = wall_clock64();
   }
 }
 
@@ -1007,6 +1021,8 @@ constexpr int kSplits = 16;
 // (slab_reduce_fused[_put]); 2 = fused plain reductions, puts as stage 1 + the put kernel;
 // 0 = the two stages everywhere.
 static int g_slab_mode = 1;
+// Timeline probe of grad_dense_multi (set_grad_stamps; nullptr = off, every production launch).
+static long long* g_stamps = nullptr;
 
 template <typename A>
 __global__ void __launch_bounds__(256)
@@ -1413,6 +1429,7 @@ xt_r_tiles(const Segment* __restrict__ segs, const Task* __restrict__ tasks,
 namespace eh {
 
 void set_slab_reduce_mode(int mode) { g_slab_mode = mode; }
+void set_grad_stamps(void* stamps) { g_stamps = static_cast<long long*>(stamps); }
 int slab_reduce_mode() { return g_slab_mode; }
 
 // Wide kernel: 16 elements per thread per row for fp64 (NV = 8), 32 for fp32 (NV = 8) and
@@ -1473,7 +1490,7 @@ static hipError_t launch_multi(bool fold, bool lane_epi, bool pair, dim3 grid, d
                                const int* gate) {
   if (!fold) {  // (the lane / pair-row epilogues come with the fold only)
     hipLaunchKernelGGL((grad_dense_multi<T, A, C, LOSS, R, false, 0>), grid, block, 0, st, segs, tasks, nb, beta, slab, ld,
-                       gate);
+                       gate, g_stamps);
     return hipGetLastError();
   }
   const size_t lds = 3ull * R * C * kWave * sizeof(A);
@@ -1489,7 +1506,7 @@ static hipError_t launch_multi(bool fold, bool lane_epi, bool pair, dim3 grid, d
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, grid, block, lds, st, segs, tasks, nb, beta, slab, ld, gate);
+  hipLaunchKernelGGL(kern, grid, block, lds, st, segs, tasks, nb, beta, slab, ld, gate, g_stamps);
   return hipGetLastError();
 }
 

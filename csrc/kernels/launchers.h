@@ -39,6 +39,9 @@ struct KernelChoice;
 // Slab reduction form (grad_dense.hip g_slab_mode): 1 fused launches (default), 2 fused plain /
 // two-stage puts, 0 two stages.
 void set_slab_reduce_mode(int mode);
+// Timeline probe: grad_dense_multi launches write {start, rows done, slab written, XCC} ticks per bundle
+// into `stamps` (int64 [4 * bundles]); nullptr turns it off (tools/probes/bundle_stamps.py).
+void set_grad_stamps(void* stamps);
 int slab_reduce_mode();
 // put (optional): fuse the message put + signal into the final slab reduction; put->dst
 // receives the nslots x ld result rows, put->bytes is ignored.

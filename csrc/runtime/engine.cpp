@@ -1758,7 +1758,10 @@ class WorkerPump {
         comm_->abort();
         return i - 1;
       }
-      post_beta_upto(i + 1);  // beta(i+1) (or the end-of-run beta(R)) may land while round i waits
+      // beta(i+1) (or the end-of-run beta(R)) may land while round i waits.  Never past the segment: the
+      // master publishes beta(b) only after the fence between segments (Trainer.run timed_start), and a
+      // receive still posted would hold this rank's device synchronisation at that fence.
+      post_beta_upto(b == R_ ? i + 1 : std::min(i + 1, b - 1));
       hcheck(hipStreamWaitEvent(stream_, bev_[i], 0), "hipStreamWaitEvent(beta)");
       if (n_ == 0) continue;
       const char* beta = static_cast<const char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * ld_ * es_;

@@ -44,7 +44,8 @@ def main():
         cfg.integrity = False
     tr = Trainer(cfg, env, src, scheme=sch)
     pf = tr.preflight(int(os.environ["EH_TEST_PREFLIGHT"])) if os.environ.get("EH_TEST_PREFLIGHT") else None
-    res = tr.run()
+    ts = int(os.environ["EH_TEST_TIMED_START"]) if os.environ.get("EH_TEST_TIMED_START") else None
+    res = tr.run(timed_start=ts)  # timed_start: the rounds run in two segments with a fence between them
     reports = env.gather_objects(tr.rank_report())  # every rank's (stale rounds skipped, ...)
     skipped = env.gather_objects([int(i) for i in getattr(tr, "skipped_rounds", [])])
     if env.is_master:

@@ -192,7 +192,10 @@ def test_lazy_fixed_straggler_is_skipped_and_costs_nothing(loop, tmp_path):
     case, R = (1, 0, 3, 5, 1, 3), 16
     over = dict(add_delay=1, delay_mode="fixed", fixed_stragglers=[4], fixed_sleep=0.04, delay_on="worker",
                 shard="message", drain="lazy", num_itrs=R)
-    env = {"arbiter": {"ERASUREHEAD_DEVICE_MASTER": "on"}, "loopback": {"ERASUREHEAD_TRANSPORT": "loopback"}}.get(loop, {})
+    # loopback also runs its rounds in two segments with a fence between them (bench.py's timed_start): the
+    # beta receives a p2p worker posts ahead must not cross the fence
+    env = {"arbiter": {"ERASUREHEAD_DEVICE_MASTER": "on"},
+           "loopback": {"ERASUREHEAD_TRANSPORT": "loopback", "EH_TEST_TIMED_START": "3"}}.get(loop, {})
     r, owner, skipped = _lazy_run(4, case, over, tmp_path, **env)
     assert json.loads(str(r["rank_report"]))["round_loop"] == ("arbiter" if loop == "arbiter" else "native pump")
     assert str(r["transport"]) == ("loopback" if loop == "loopback" else "ipc")

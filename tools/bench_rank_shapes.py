@@ -21,9 +21,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0, fill: bool = False,
-        slab_mode: int = 1) -> dict:
-    import numpy as np
+def build_plan(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0, fill: bool = False):
+    """(plan, beta, G) of the heaviest rank's local gradient at the N-GPU placement (also
+    tools/probes/bundle_stamps.py)."""
     import torch
 
     from erasurehead_amd.codes import make_scheme
@@ -35,9 +35,6 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
     from erasurehead_amd.ops.grad import choose_cpl, choose_kernel
     from erasurehead_amd.parallel.placement import make_shards, place_spread, place_units
 
-    from erasurehead_amd._ext import native
-
-    native().set_slab_reduce_mode(slab_mode)
     prec = get_precision(precision)
     sch = make_scheme("approx", 8, 2, 1_000_000, 6, 0, allow_uneven=True)
     rows = sch.rows_per_partition
@@ -76,8 +73,22 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
             cpl = choose_cpl(prec.ld(1000), prec.vec)
             choice = replace(base, fill=multi_slots(distinct, prec.code == 1, cpl=cpl) // 4)
     plan = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, choice=choice)
+    plan.rank, plan.n_parts, plan.n_shards, plan.shard_mode = r, len(need), len(mine), mode
     beta = torch.randn(prec.ld(1000), device="cuda", dtype=prec.acc) * 0.01
     G = plan.out_buffer()[0]
+    return plan, beta, G
+
+
+def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0, fill: bool = False,
+        slab_mode: int = 1) -> dict:
+    import numpy as np
+    import torch
+
+    from erasurehead_amd._ext import native
+
+    native().set_slab_reduce_mode(slab_mode)
+    plan, beta, G = build_plan(n_gpus, precision, shard, rows_override, fill)
+    r, mode = plan.rank, plan.shard_mode
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from bench_kernels import clock_warm  # ~150 ms of back-to-back launches: the clock ramp is over
 
@@ -89,8 +100,8 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
         b.record()
     torch.cuda.synchronize()
     ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
-    return {"n_gpus": n_gpus, "precision": precision, "shard": mode, "rank": r, "partitions": len(need),
-            "shards": len(mine), "bundle_rows": plan.bundle_rows, "kernel": plan.choice.label(), "ntasks": plan.ntasks,
+    return {"n_gpus": n_gpus, "precision": precision, "shard": mode, "rank": r, "partitions": plan.n_parts,
+            "shards": plan.n_shards, "bundle_rows": plan.bundle_rows, "kernel": plan.choice.label(), "ntasks": plan.ntasks,
             "kernel_ms": ms, "distinct_TBps": plan.distinct_bytes / ms / 1e9, "fill": plan.choice.fill,
             "slab_mode": slab_mode}
 
