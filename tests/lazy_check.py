@@ -53,11 +53,15 @@ def replay_along(delays, t, ran, rule, k, groups, margin):
 
 
 def decode_key(workers, rule, groups):
-    """What the decode depends on: the arrived set, plus the first arrival of each group for FRC."""
+    """What the decode depends on: the arrived set (count rules), or for FRC / AGC the first arrival of
+    each covered group -- later members of a covered group never enter the decode, so the order of such a
+    member against another group's first arrival does not matter (and is not separated by the margin)."""
+    if rule != "frc":
+        return (sorted(workers), None)
     first = {}
     for w in workers:
         first.setdefault(groups[w], w)
-    return (sorted(workers), sorted(first.items()) if rule == "frc" else None)
+    return (None, sorted(first.items()))
 
 
 def check_lazy(arrivals, loop_time, delays, rule, k, groups, margin, skipped_by_worker=None, local=()):

@@ -69,11 +69,12 @@ def run_one(name: str, rounds: int, n_rows: int, n_cols: int, out: str) -> None:
     W = 8
     cfg = RunConfig(W + 1, n_rows, n_cols, "/tmp/eh_conv/", 0, "synthetic", is_coded, s, 0, ver, k, 1, "AGD",
                     num_itrs=rounds, data="synthetic", data_seed=1234, seed=0, allow_uneven_groups=True,
-                    verbose=False, round_timeout=120.0, drain=drain)
+                    verbose=True, round_timeout=120.0, drain=drain)
     env = DistEnv(device=torch.device("cuda" if torch.cuda.is_available() else "cpu"))
     tr = Trainer(cfg, env)
     t0 = time.perf_counter()
-    res = tr.run()
+    # progress every 10 rounds (a 100-round naive run waits ~130 s of virtual delays)
+    res = tr.run(log=lambda line: print(f"[{name}] {line.strip()}", flush=True))
     wall = time.perf_counter() - t0
     sch = tr.scheme
     tr.cfg.fix_quirks = True

@@ -16,6 +16,7 @@
 #   eval     evaluation phase profile (tools/profile_eval.py)
 #   suite    tools/bench_suite.py (every BASELINE.json config)
 #   conv     tools/convergence_study.py (all schemes, drain and lazy rows)
+#   convlazy the same for the lazy rows + naive + drained uneven AGC, serially (one scheme at a time)
 #   wide     the d = 2048 / 4096 rows of the sweep
 #   sparse   sparse gradients at the real-data shapes (timings, then rocprofv3 kernel stats)
 #   rccl     the RCCL self-loop GPU tests under rocprofv3 --kernel-trace (RCCL kernel names)
@@ -156,6 +157,10 @@ for s in "${STAGES[@]}"; do
       run 1000 suite.log python -u tools/bench_suite.py --out "$OUT/suite" ;;
     conv)  # convergence vs wall-clock, every scheme incl. the lazy-drain rows (11 processes on the GPU)
       run 900 conv.log python -u tools/convergence_study.py --out "$OUT/convergence" ;;
+    convlazy)  # the lazy rows, naive and the drained uneven AGC, ONE scheme at a time (no GPU sharing)
+      run 1100 convlazy.log python -u tools/convergence_study.py --serial \
+        --only naive,agc_s2_k6_uneven,cyclic_s2_lazy,frc_s1_lazy,agc_s1_k6_lazy,agc_s2_k6_uneven_lazy \
+        --out "$OUT/convergence_lazy" ;;
     eval)
       run 600 eval.log python -u tools/profile_eval.py --out "$OUT/eval.json" ;;
     *) echo "unknown stage $s"; exit 2 ;;

@@ -51,11 +51,13 @@ def main():
         torch.cuda.synchronize()
         C._set_grad_stamps(0)
         v = st.view(-1, 4).cpu().numpy()
-        v = v[v[:, 0] > 0]
+        ids = np.nonzero(v[:, 0] > 0)[0]  # bundle ids (the grid's wave index)
+        v = v[ids]
         t0 = v[:, 0].min()
         start = (v[:, 0] - t0) / hz * 1e6
         rows_done = (v[:, 1] - t0) / hz * 1e6
-        done = (v[:, 2] - t0) / hz * 1e6
+        has_done = v[:, 2] > 0  # FOLD: waves 1-3 of a workgroup return after the fold, wave 0 writes the slab
+        done = (v[has_done, 2] - t0) / hz * 1e6
         xcc = v[:, 3]
         pct = lambda x, q: float(np.percentile(x, q))  # noqa: E731
         rec = {"gpus": a.gpus, "bundle_rows": plan.bundle_rows, "bundles": int(len(v)), "event_us": 1e3 * e0.elapsed_time(e1),
@@ -64,11 +66,18 @@ def main():
                "stream_us_p0_p50_p100": [float((rows_done - start).min()), pct(rows_done - start, 50),
                                           float((rows_done - start).max())],
                "rows_done_p0_p50_p100_us": [float(rows_done.min()), pct(rows_done, 50), float(rows_done.max())],
-               "slab_tail_us_p50_p100": [pct(done - rows_done, 50), float((done - rows_done).max())],
+               "slab_tail_us_p50_p100": [pct(done - rows_done[has_done], 50), float((done - rows_done[has_done]).max())],
                "done_p0_p10_p50_p90_p100_us": [float(done.min()), pct(done, 10), pct(done, 50), pct(done, 90),
                                                float(done.max())],
-               "per_xcc_done_mean_us": {int(x): float(done[xcc == x].mean()) for x in sorted(set(xcc.tolist()))},
+               "rows_done_p10_p25_p75_p90_p99_us": [pct(rows_done, q) for q in (10, 25, 75, 90, 99)],
+               "per_xcc_rows_done_p50_max_us": {int(x): [pct(rows_done[xcc == x], 50), float(rows_done[xcc == x].max())]
+                                                for x in sorted(set(xcc.tolist()))},
                "per_xcc_bundles": {int(x): int((xcc == x).sum()) for x in sorted(set(xcc.tolist()))}}
+        live = rows_done > 5.0  # pad bundles finish at once
+        order = np.argsort(-rows_done)
+        rec["slowest_bundles"] = [[int(ids[b]), int(xcc[b]), round(float(rows_done[b]), 2), round(float(start[b]), 2)]
+                                  for b in order[:12]]
+        rec["live_bundles"] = int(live.sum())
         recs.append(rec)
         print(json.dumps(rec), flush=True)
     if a.out:
