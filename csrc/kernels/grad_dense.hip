@@ -195,6 +195,11 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
 // profiles/round3/choices), which this halves.
 // stamps (a timeline probe, tools/probes/bundle_stamps.py; nullptr in every production launch): per
 // bundle {start, rows done, slab written, XCC id} in wall_clock64 ticks, one vector store of lane 0 each.
+// Rows in flight per wave of grad_dense_multi: 2 for fp64 / fp32 rows (8 / 4 KB at d = 1000), 6 for
+// bf16 (2 KB rows: 12 KB in flight per wave; 3 waves per SIMD at R = 3, 169 VGPRs and 2 waves with 8).
+template <typename T>
+constexpr int kMultiDepth = std::is_same<T, bf16_t>::value ? 6 : 2;
+
 template <typename T, typename A, int CPL, int LOSS, int R, bool FOLD, int EPI = 0>
 __global__ void __launch_bounds__(256)
 grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ tasks, int nbundles,
@@ -359,6 +364,23 @@ grad_dense_multi(const Segment* __restrict__ segs, const Task* __restrict__ task
       load(xa, ya, r + 4);
       load(xb, yb, r + 5);
       step2(xc, xd, yc, yd, r + 3 < r1);
+    }
+  } else if constexpr (kMultiDepth<T> > 2) {
+    // Short rows (bf16: 2 KB at d = 1000, two 16-byte vectors per lane): two rows in flight would be 4 KB
+    // per wave, too little to cover HBM latency at a CU's share of the stream, so D rows are in flight: a
+    // ring of D row buffers, each step issuing the load D - 1 rows ahead before consuming its own row.
+    constexpr int D = kMultiDepth<T>;
+    Rw xr[D][NV];
+    A yr[D];
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k) load(xr[k], yr[k], r0 + k);
+    for (int r = r0; r < r1; r += D) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        load(xr[(k + D - 1) % D], yr[(k + D - 1) % D], r + k + D - 1);
+        step(xr[k], yr[k]);
+        if (r + k + 1 >= r1) break;
+      }
     }
   } else {
     Rw xa[NV], xb[NV];
@@ -1548,7 +1570,7 @@ static hipError_t launch_fused_cpl(int cpl, const Segment* segs, const Task* tas
         return hipGetLastError();                                                                      \
       }                                                                                                \
       if (k.kind == kGradMulti) { /* every replica of a bundle in one wave, rows in registers */       \
-        if constexpr (C <= 16 && !std::is_same<T, bf16_t>::value) {                                    \
+        if constexpr (C <= 16) {                                                                       \
           const int nb_ = ntasks / R;                                                                  \
           if (k.fold && nb_ % 4) return hipErrorInvalidValue;                                          \
           const dim3 mg((nb_ + 3) / 4), mb(256);                                                       \

@@ -421,8 +421,8 @@ class DenseGradPlan:
             raise ValueError("the two-pass kernel is for rows wider than the one-pass kernels")
         if c.kind in ("multi", "staged", "mfma") and (self.cpl is None or self.cpl > MAX_CPL):
             raise ValueError(f"{c.kind} bundles need d <= {64 * MAX_CPL} columns per vector width")
-        if c.kind == "multi" and (self.cpl > 16 or prec.code == 2 or self.max_rep > 3):
-            raise ValueError("one-wave bundles hold at most 3 fp64/fp32 replicas of d <= 1024")
+        if c.kind == "multi" and (self.cpl > 16 or self.max_rep > 3):
+            raise ValueError("one-wave bundles hold at most 3 replicas of rows of <= 16 columns per lane")
         if c.kind == "multi" and c.pair and (self.cpl > 8 or not c.fold):
             raise ValueError("pair-row one-wave bundles need <= 8 columns per lane and the fold")
         if c.kind == "wide" and c.replicas > 1 and (self.cpl not in (32, 256) or c.replicas > 3):

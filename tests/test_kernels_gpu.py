@@ -516,7 +516,11 @@ def test_frc_pairs_default_to_one_wave_bundles(native):
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
 @pytest.mark.parametrize("rows,d,prec_name", [(64, 1000, "fp64"), (37, 1000, "fp64"), (256, 250, "fp64"),
                                               (33, 500, "fp64"), (64, 1000, "fp32"), (33, 130, "fp32"),
-                                              (35, 512, "fp32"), (8, 250, "fp32"), (8, 1000, "fp64")])
+                                              (35, 512, "fp32"), (8, 250, "fp32"), (8, 1000, "fp64"),
+                                              # bf16 rows: six in flight per wave (kMultiDepth), bundles ending
+                                              # anywhere in the ring
+                                              (64, 1000, "bf16"), (37, 1000, "bf16"), (13, 504, "bf16"),
+                                              (5, 1000, "bf16")])
 def test_dense_grad_one_wave_bundles(native, rows, d, prec_name, loss, form):
     """grad_dense_multi: one wave computes every replica of its bundle from rows double-buffered in
     registers, each replica with its own dot product, residual and gradient.  Bundles of 3 replicas,
