@@ -1628,7 +1628,8 @@ class WorkerPump {
   ~WorkerPump() {
     for (auto e : rev_)
       if (e) hipEventDestroy(e);
-    if (bst_) hipStreamSynchronize(bst_);
+    // the beta stream is destroyed without a sync (a receive from a master that is gone may never end; the
+    // transport aborts its communicator at close), like the master's per-peer streams
     for (auto e : bev_)
       if (e) hipEventDestroy(e);
     if (bst_) hipStreamDestroy(bst_);
@@ -1748,6 +1749,7 @@ class WorkerPump {
   // run_comm with stale-round skipping (set_skip_stale_comm).
   int run_comm_skip(int a, int b) {
     py::gil_scoped_release nogil;
+    if (posted_ == 0) posted_ = a;  // a resumed run: the master's first beta is beta(a)
     need(posted_ >= a, "rounds must run in order");
     auto* cnt = reinterpret_cast<const unsigned long long*>(bcount_.data_ptr<int64_t>());
     int* gw = gate_.data_ptr<int>();

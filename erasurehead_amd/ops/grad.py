@@ -233,8 +233,9 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     Measured choices (docs/PERF_NOTES.md):
       * distinct rows (naive, message-placed ranks): one-wave bundles of one replica at 16 columns per
         lane (profiles/round3/choices_nt/naive.jsonl: fp64 1e6 rows 1.160 vs 1.197-1.213 ms fused,
-        fp32 0.581 vs 0.639, fp64 375k rows 0.447-0.456 vs 0.491); otherwise the fused kernel, fp64
-        the interleaved pair kernel, fp32 4 rows, bf16 1 row;
+        fp32 0.581 vs 0.639, fp64 375k rows 0.447-0.456 vs 0.491; bf16, six rows in flight per wave:
+        0.302 vs 0.367, profiles/round5/bf16); otherwise the fused kernel, fp64 the interleaved pair
+        kernel, fp32 4 rows, bf16 1 row;
       * replicas, 3 per bundle, narrow rows (<= 8 columns per lane, d <= 512 fp64 / 1024 fp32):
         one-wave bundles with two rows per reduce-scatter (d = 256: 5.2 vs 2.3 TB/s before);
       * replicas, fp64 / fp32, 2 or 3 per bundle (AGC / cyclic s = 2, FRC s = 1): one-wave bundles,
@@ -245,7 +246,9 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
         (two rows per reduction; with the nt stream it wins everywhere: d = 2048 fp64 2.676 vs 2.751
         ms, 4 replicas at d = 1000 fp64 1.532-1.542 vs 1.668; one-wave bundles of 4 replicas need
         276 registers, 1 wave per SIMD, and measured 1.76 ms: profiles/round3/choices_nt/frc4.jsonl);
-      * bf16 replicas: MFMA bundles (d <= 1024, d % 8 == 0), else the fused kernel interleaved;
+      * bf16 replicas: MFMA bundles (d <= 1024, d % 8 == 0; one-wave bundles of 3 bf16 replicas are
+        VALU-bound: 0.367 vs 0.321 ms, profiles/round5/bf16/choices_agc.jsonl), else the fused kernel
+        interleaved;
       * 2048 < d (fp64, 4096 fp32): the wide kernel; fp64 replicas at 1024 < d <= 2048 too (its half-width
         instance); beyond 8192 / 16384 or cpl unknown: two passes.
     """
@@ -259,9 +262,11 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
                                                              wide_slots_per_cu(prec_code, ld, max_rep)))
         return KernelChoice("wide", interleave=shared)
     if not shared:
-        if prec_code != 2 and 8 < cpl <= 16:  # distinct rows of 16 columns per lane: bundles of one
+        if 8 < cpl <= 16:  # distinct rows of 16 columns per lane: bundles of one
+            # (bf16: six rows in flight per wave, grad_dense.hip kMultiDepth; 1e6 x 1000 rows 0.302 ms vs
+            # 0.367 on the fused kernel, profiles/round5/bf16/choices_naive.jsonl; sized like fp32)
             return KernelChoice("multi", replicas=1,
-                                bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl, part_rows),
+                                bundle_rows=multi_bundle_rows(distinct_rows, prec_code != 0, n_cus, cpl, part_rows),
                                 fold=True)
         return KernelChoice("fused", rows={0: 2, 1: 4, 2: 1}[prec_code])
     long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
