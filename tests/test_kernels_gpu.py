@@ -479,7 +479,7 @@ def test_dense_grad_one_wave_bundles_of_two(native, rows, d, prec_name, loss, fo
         np.testing.assert_allclose(G[s, :d].double().cpu().numpy(), ref, rtol=tol, atol=atol)
 
 
-@pytest.mark.parametrize("prec_name", ["fp64", "fp32"])
+@pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
 def test_distinct_rows_default_to_one_wave_bundles_of_one(native, prec_name, loss):
     """Distinct rows (naive, message-placed ranks) at 16 columns per lane pick grad_dense_multi with
