@@ -52,7 +52,11 @@
 // later): skipped iff its virtual start max(t_start(j), finish(w, j-1)) >= t_start(j+1).  An IPC flag
 // probe first seen with its counter already past round j (a later round's put landed) is skipped too:
 // the worker rank may have skipped round j on the device, and round j is over at the master either way.
-// Both parts of a partial scheme's worker share one virtual start, so they skip together.
+// Both parts of a partial scheme's worker share one virtual start, so they skip together.  Over
+// stream-ordered p2p (RCCL / loopback) a round the worker skipped on the device still sends its stale
+// rows (FIFO pairing): they land after their round ended and are drained as stale, never decoded.  The
+// event probe cannot tell them from a computed round, so with virtual delays on top of physical skipping
+// the carried virtual finish of that worker can come out late; the decode is unaffected.
 #pragma once
 
 #include <hip/hip_runtime.h>

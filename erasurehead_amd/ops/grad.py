@@ -620,9 +620,14 @@ class SparseGradPlan:
     TILE = 512  # grad_sparse.hip kTileEntries
     ROW_BLOCK_ROWS = 4096  # residuals of one column-pass sub-block, staged in LDS
     WG_TILES = 16  # tiles per column-pass workgroup (grad_sparse.hip kWgTiles), one per wave
+    # beta bytes the ELL row pass stages in LDS (grad_sparse.hip kEllLdsBytes).  ELL rows pay off there
+    # (covtype-shaped, 124 KB of fp64 beta: 54.7 vs 105.3 us with CSR rows); a beta that does not fit
+    # leaves ELL one row per thread gathering from L2, which the CSR pass (16 lanes per row) beats on
+    # the real shapes (amazon 33.1 vs 37.9 us, kc_house 18.4 vs 18.9: profiles/round4/r5a/breakdown.txt)
+    ELL_LDS_BYTES = 148 * 1024
 
     def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]], partitions: Dict[int, Tuple[object, np.ndarray]],
-                 prec: Precision, loss: int, d: int, device="cpu", use_ell: bool = True):
+                 prec: Precision, loss: int, d: int, device="cpu", use_ell="auto"):
         import scipy.sparse as sps
 
         if prec.name == "bf16":
@@ -661,6 +666,7 @@ class SparseGradPlan:
         self.ell = False
         self.idx16 = False
         self.row16 = False
+        self.identity = False  # set by _build_device: messages are the distinct partitions themselves
         if self.device.type == "cuda":
             self._build_device(X, use_ell)
 
@@ -673,6 +679,9 @@ class SparseGradPlan:
         self.u = torch.zeros(max(1, self.nrows), dtype=acc, device=dev)
         nnz_row = np.diff(X.indptr)
         self.ell_idx = self.ell_lo = self.row_ptr = self.col_idx = self.vals = None
+        beta_lds = self.d * torch.tensor([], dtype=acc).element_size() <= self.ELL_LDS_BYTES
+        if use_ell == "auto":
+            use_ell = beta_lds
         if use_ell and self.nrows and np.all(nnz_row == nnz_row[0]) and nnz_row[0] > 0 and self.nrows < 2 ** 31:
             m = int(nnz_row[0])
             idx = X.indices.reshape(self.nrows, m).T  # [m, rows]; sorted rows -> the k-th smallest column
@@ -728,6 +737,13 @@ class SparseGradPlan:
         self.sub_begin = torch.from_numpy(t["sub_begin"]).to(dev) if blocked else None
         self.Gs = torch.zeros((self.nsub, self.ld), dtype=acc, device=dev) if blocked else None
         ptr, idx, coef = self._enc
+        # identity encoding (naive: message i is distinct partition i with coefficient 1, no sub-blocks):
+        # the column pass writes the messages themselves, no Gb and no encode launch (amazon-shaped
+        # naive: 15.5 MB read + 15.5 MB written per round).  The pass never writes a column that is empty
+        # in its partition, so those stay as the caller's G holds them: zero in every buffer the plans
+        # and the trainer allocate (out_buffer, the trainer's G ring).
+        self.identity = (not blocked and len(self.messages) == len(self.basis)
+                         and all(m == [(self.basis[i], 1.0)] for i, m in enumerate(self.messages)))
         self.enc_ptr = torch.tensor(ptr, dtype=torch.int32, device=dev)
         self.enc_idx = torch.tensor(idx or [0], dtype=torch.int32, device=dev)[: len(idx)]
         self.enc_coef = torch.tensor(coef or [0.0], dtype=torch.float64, device=dev)[: len(coef)]
@@ -861,7 +877,8 @@ class SparseGradPlan:
                                              self.span, empty, self.nsub, self.d, self.ld,
                                              wg=self.wg if len(self.wg) else None, u_lds=self.u_lds, Gs=self.Gs,
                                              sub_begin=self.sub_begin, runs=self.runs, tkeys=self.tkeys)
-            L.set_encode(self.enc_ptr, self.enc_idx, self.enc_coef, self.Gb)
+            if not self.identity:
+                L.set_encode(self.enc_ptr, self.enc_idx, self.enc_coef, self.Gb)
             self._launcher = L
         return self._launcher
 

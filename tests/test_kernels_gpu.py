@@ -145,6 +145,40 @@ def test_sparse_grad(prec_name, tol, pattern_only, use_ell, native):
             assert err < tol, (loss, s, err)
 
 
+@pytest.mark.parametrize("d", [700, 30000])
+def test_sparse_naive_identity_plan_writes_the_messages(d, native):
+    """Naive (message i = distinct partition i, coefficient 1, no sub-blocks): no device encoding, the column
+    pass writes the message rows themselves; a second launch into the same buffer gives the same bits; the
+    row format follows the beta footprint (ELL with beta in LDS at d = 700, CSR rows at d = 30000: 240 KB of
+    fp64 beta does not fit)."""
+    prec = get_precision("fp64")
+    rng = np.random.RandomState(11)
+    parts = {}
+    for p in range(3):
+        n = 300 + 41 * p
+        cols = np.stack([rng.choice(d, 6, replace=False) for _ in range(n)])
+        X = sps.csr_matrix((np.ones(cols.size), cols.ravel(), np.arange(0, cols.size + 1, 6)), shape=(n, d))
+        parts[p] = (X, rng.choice([-1.0, 1.0], n))
+    msgs = [[(p, 1.0)] for p in range(3)]
+    plan = SparseGradPlan(msgs, parts, prec, LOGISTIC, d, device=DEV)
+    assert plan.identity and plan.ell == (d == 700)
+    beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
+    beta[:d] = torch.from_numpy(rng.randn(d) * 0.2)
+    bh = beta[:d].double().cpu().numpy()
+    G = plan.out_buffer()[0]
+    plan.run(beta, G)
+    torch.cuda.synchronize()
+    first = G.clone()
+    plan.run(beta, G)
+    torch.cuda.synchronize()
+    assert torch.equal(G, first)
+    for s, m in enumerate(msgs):
+        ref = sum(logistic_grad(parts[p][0], parts[p][1], bh, c) for p, c in m)
+        got = G[s, :d].double().cpu().numpy()
+        assert np.max(np.abs(got - ref)) / max(1e-12, np.max(np.abs(ref))) < 1e-11
+    assert torch.all(G[:, d:] == 0)
+
+
 @pytest.mark.parametrize("prec_name,tol", [("fp64", 1e-11), ("fp32", 1e-4)])
 @pytest.mark.parametrize("wide,idx16", [(20000, True), (70000, False)])
 def test_ell_onehot_blocks_and_wide_windows(prec_name, tol, wide, idx16, native):
@@ -167,7 +201,7 @@ def test_ell_onehot_blocks_and_wide_windows(prec_name, tol, wide, idx16, native)
     msgs = [[(0, 1.0), (1, 0.5)], [(2, -1.5)]]
     b = rng.randn(D) * 0.1
     for loss in (LOGISTIC, LEAST_SQUARES):
-        plan = SparseGradPlan(msgs, parts, prec, loss, D, device=DEV)
+        plan = SparseGradPlan(msgs, parts, prec, loss, D, device=DEV, use_ell=True)  # (auto: CSR past LDS)
         assert plan.ell and plan.idx16 == idx16 and plan.row16
         beta = torch.zeros(prec.ld(D), dtype=prec.acc, device=DEV)
         beta[:D] = torch.from_numpy(b).to(prec.acc)
