@@ -102,6 +102,11 @@ struct SparseArgs {
   int encode_from_subs;         // 1: the encoding that follows adds the sub-block sums itself (no sub_reduce)
   const int* runs;              // row-blocked pass: the column of every run (CSC rows flag run starts), per tile
   const int4* tkeys;            // [ntiles] (first run, n | runs << 10 | span flags << 20, sub-block, first column)
+  // column-aligned chunks (csc_tables wg_spans): workgroup k adds its own crossing columns
+  // wspan[wspan_ptr[k] .. wspan_ptr[k + 1]) = (sub-block, column, first, last tile of the chunk) from
+  // LDS after its tiles; nullptr: heads / tails go through memory to csc_spans
+  const int4* wspan;
+  const int* wspan_ptr;         // [nwg + 1]
 };
 hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const void* beta, hipStream_t st,
                               const int* gate = nullptr);

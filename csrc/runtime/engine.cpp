@@ -227,7 +227,8 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
                                           const Tensor& empty, int64_t nparts, int64_t d, int64_t ld,
                                           std::optional<Tensor> wg, int64_t u_lds, std::optional<Tensor> Gs,
                                           std::optional<Tensor> sub_begin, std::optional<Tensor> runs,
-                                          std::optional<Tensor> tkeys) {
+                                          std::optional<Tensor> tkeys, std::optional<Tensor> wspan,
+                                          std::optional<Tensor> wspan_ptr) {
   for (auto* t : {&y, &u, &crow, &col_ptr, &tiles, &part_entry0, &part_row0, &part_nnz, &head, &tail, &span, &empty})
     need_gpu(*t, "sparse plan operand");
   need(tiles.scalar_type() == at::kInt && tiles.dim() == 2 && tiles.size(1) == 4, "tiles: int32 [n, 4]");
@@ -311,6 +312,14 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
     need_gpu(*wg, "wg");
     need(wg->scalar_type() == at::kInt && wg->dim() == 2 && wg->size(1) == 4, "wg: int32 [n, 4]");
     need(u_lds > 0 && u_lds * (g->acc == 0 ? 8 : 4) <= 96 * 1024, "u_lds: sub-block rows staged in LDS (<= 96 KB)");
+    {  // the column pass's chunks: 1..64 tiles each (grad_sparse.hip kMaxWgTiles), rows staged in LDS
+      const Tensor wc = wg->cpu();
+      const int* W = wc.data_ptr<int>();
+      for (int64_t k = 0; k < wg->size(0); ++k)
+        need(W[4 * k + 2] >= 1 && W[4 * k + 2] <= 64 && W[4 * k + 1] >= 0 && W[4 * k + 1] + W[4 * k + 2] <= tiles.size(0) &&
+                 W[4 * k + 3] <= u_lds,
+             "wg: (row0, first tile, 1..64 tiles, rows <= u_lds)");
+    }
     a.wg = reinterpret_cast<const int4*>(wg->data_ptr<int>());
     a.nwg = (int)wg->size(0);
     a.u_lds = (int)u_lds;
@@ -325,6 +334,32 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
     a.tkeys = reinterpret_cast<const int4*>(tkeys->data_ptr<int>());
     g->keep.push_back(*runs);
     g->keep.push_back(*tkeys);
+    if (wspan_ptr) {  // column-aligned chunks: every crossing column summed inside its workgroup
+      need(wspan.has_value(), "wspan_ptr needs wspan");
+      need_gpu(*wspan, "wspan");
+      need_gpu(*wspan_ptr, "wspan_ptr");
+      need(a.nspan == 0, "column-aligned chunks leave no global spans");
+      need(wspan->scalar_type() == at::kInt && wspan->dim() == 2 && wspan->size(1) == 4, "wspan: int32 [n, 4]");
+      need(wspan_ptr->scalar_type() == at::kInt && wspan_ptr->numel() == a.nwg + 1, "wspan_ptr: int32 [workgroups + 1]");
+      // the kernel indexes its LDS head / tail arrays with these: checked once, on the host
+      const Tensor sp = wspan->cpu(), pp = wspan_ptr->cpu(), wc = wg->cpu();
+      const int* P = pp.data_ptr<int>();
+      const int* S = sp.data_ptr<int>();
+      const int* W = wc.data_ptr<int>();
+      need(P[0] == 0 && P[a.nwg] == sp.size(0), "wspan_ptr: [0, .., spans]");
+      for (int k = 0; k < a.nwg; ++k) {
+        need(P[k] <= P[k + 1] && P[k + 1] - P[k] < 64, "wspan_ptr: non-decreasing, < 64 spans per workgroup");
+        for (int i = P[k]; i < P[k + 1]; ++i) {
+          const int* e = S + 4 * i;
+          need(e[0] >= 0 && e[0] < nparts && e[1] >= 0 && e[1] < d && e[2] >= 0 && e[2] < e[3] && e[3] < W[4 * k + 2],
+               "wspan: (sub-block, column, first tile < last tile < the workgroup's tiles)");
+        }
+      }
+      a.wspan = reinterpret_cast<const int4*>(wspan->data_ptr<int>());
+      a.wspan_ptr = wspan_ptr->data_ptr<int>();
+      g->keep.push_back(*wspan);
+      g->keep.push_back(*wspan_ptr);
+    }
   }
   if (sub_begin) {
     need(Gs.has_value(), "sub-blocks need their Gs buffer");
@@ -1986,7 +2021,8 @@ void bind_engine(py::module& m) {
                   py::arg("part_nnz"), py::arg("head"), py::arg("tail"), py::arg("span"), py::arg("empty"),
                   py::arg("nparts"), py::arg("d"), py::arg("ld"), py::arg("wg") = py::none(), py::arg("u_lds") = 0,
                   py::arg("Gs") = py::none(), py::arg("sub_begin") = py::none(),
-                  py::arg("runs") = py::none(), py::arg("tkeys") = py::none())
+                  py::arg("runs") = py::none(), py::arg("tkeys") = py::none(), py::arg("wspan") = py::none(),
+                  py::arg("wspan_ptr") = py::none())
       .def("set_encode",
            [](GradLauncher& g, const Tensor& ptr, const Tensor& idx, const Tensor& coef, const Tensor& Gb) {
              for (auto* t : {&ptr, &idx, &coef, &Gb}) need_gpu(*t, "encode operand");

@@ -619,7 +619,14 @@ class SparseGradPlan:
 
     TILE = 512  # grad_sparse.hip kTileEntries
     ROW_BLOCK_ROWS = 4096  # residuals of one column-pass sub-block, staged in LDS
-    WG_TILES = 16  # tiles per column-pass workgroup (grad_sparse.hip kWgTiles), one per wave
+    # tiles per column-pass workgroup (<= grad_sparse.hip kMaxWgTiles; wave w takes w, w + 16, ...); None:
+    # by size -- 64 when chunks of 16 would fill the 512 workgroup slots four times over, else 16 (covtype-
+    # shaped naive 51.7 us at 64 vs 57.0 at 16; kc_house / amazon, 0.6k / 2.3k tiles: 13.7 / 21.3 us at 16,
+    # 22.8 / 35.8 at 64: fewer workgroups than slots; profiles/round5/sparse/)
+    WG_TILES = None
+    # column-aligned workgroup chunks (csc_tables wg_spans): the crossing columns are summed inside the
+    # column pass's workgroups, no csc_spans launch and no head / tail round trip
+    WG_SPANS = True  # (False: the csc_spans launch; tools/bench_kernels.py --no-wg-spans, for A/B)
     # beta bytes the ELL row pass stages in LDS (grad_sparse.hip kEllLdsBytes).  ELL rows pay off there
     # (covtype-shaped, 124 KB of fp64 beta: 54.7 vs 105.3 us with CSR rows); a beta that does not fit
     # leaves ELL one row per thread gathering from L2, which the CSR pass (16 lanes per row) beats on
@@ -712,7 +719,12 @@ class SparseGradPlan:
         # residual sub-blocks staged in LDS by the column pass: 4096 rows (32 KB fp64, 16 KB fp32; four
         # staged values per thread of its 1024-thread workgroups, grad_sparse.hip kStageRegs)
         rb = self.ROW_BLOCK_ROWS
-        t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE, row_block=rb, wg_tiles=self.WG_TILES)
+        wgt = self.WG_TILES
+        if wgt is None:
+            wgt = 64 if self.nnz >= self.TILE * 16 * 512 * 4 else 16
+        self.wg_tiles = wgt
+        t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE, row_block=rb, wg_tiles=wgt,
+                            wg_spans=self.WG_SPANS)
         self.row_block = rb
         self.nsub = t["nsub"]
         self.row16 = t["row16"]
@@ -733,6 +745,9 @@ class SparseGradPlan:
         self.runs = torch.from_numpy(t["runs"]).to(dev)
         self.tkeys = torch.from_numpy(t["tkeys"]).to(dev)
         self.u_lds = int(t["wg"][:, 3].max()) if len(t["wg"]) else 1
+        self.wg_spans = bool(t["wg_spans"]) and len(t["wg"]) > 0
+        self.wspan = torch.from_numpy(t["wspan"]).to(dev) if self.wg_spans else None
+        self.wspan_ptr = torch.from_numpy(t["wspan_ptr"]).to(dev) if self.wg_spans else None
         blocked = self.nsub != len(self.basis)  # some partition spans several sub-blocks
         self.sub_begin = torch.from_numpy(t["sub_begin"]).to(dev) if blocked else None
         self.Gs = torch.zeros((self.nsub, self.ld), dtype=acc, device=dev) if blocked else None
@@ -750,7 +765,8 @@ class SparseGradPlan:
         self._launcher = None
 
     @staticmethod
-    def csc_tables(blocks, d: int, tile: int = 512, row_block: int = 0, wg_tiles: int = 16) -> dict:
+    def csc_tables(blocks, d: int, tile: int = 512, row_block: int = 0, wg_tiles: int = 16,
+                   wg_spans: bool = False) -> dict:
         """Host tables of the deterministic column pass (grad_sparse.hip csc_tiles / csc_spans): per
         partition a CSC twin (rows sorted by (column, row), padded to whole tiles), its column
         pointers, the tiles (partition, base entry, column of the base entry, span flags: 1 = the
@@ -768,7 +784,15 @@ class SparseGradPlan:
         lists partition j's).  A workgroup takes up to wg_tiles tiles of ONE sub-block and stages
         that sub-block's residuals in LDS (wg: first row of the sub-block, first tile, tiles, rows),
         so the column pass's gathers never leave the CU; the sub-block sums are added per partition
-        afterwards."""
+        afterwards.
+
+        wg_spans (with row_block > 0): a workgroup's chunk of tiles ends on a column boundary -- its
+        last tile is cut short (padded) before the first column that would not fit -- so no column
+        crosses workgroups and the workgroup adds its own crossing columns from LDS after its tiles
+        (wspan: sub-block, column, first and last tile relative to the chunk; wspan_ptr: each
+        workgroup's range).  No csc_spans launch, no head / tail round trip through memory.  Tile t's
+        entries still sit at crow[tile * t ...]; its entry count is tkeys' n (< tile for a cut tile).
+        Falls back to whole chunks (span = the global list) when a column is longer than a chunk."""
         import scipy.sparse as sps
 
         sub_begin = None
@@ -780,73 +804,107 @@ class SparseGradPlan:
                     subs.append(sps.csr_matrix(A[r:min(n, r + row_block)]))
                 sub_begin.append(len(subs))
             blocks = subs
+        cuts = wg_spans and row_block > 0
+        cscs = []
+        for A in blocks:
+            C = A.tocsc()
+            C.sort_indices()
+            cscs.append(C)
+            if cuts and C.nnz and int(np.diff(C.indptr).max()) > tile * wg_tiles:
+                cuts = False  # a column longer than a chunk: whole chunks and the global spans
         row16 = all(A.shape[0] <= 32768 for A in blocks)
         flag = np.int64(1 << 15) if row16 else np.int64(1 << 31)
         rows_l, vals_l, cps, tiles, spans, empty = [], [], [], [], [], []
         runs_l, tkeys = [], []
+        wg, wspan, wspan_ptr = [], [], [0]
         n_runs = 0
         entry0, row0, nnzs = [], [], []
         e_off = r_off = n_tiles = 0
-        for j, A in enumerate(blocks):
-            C = A.tocsc()
-            C.sort_indices()
+        for j, (A, C) in enumerate(zip(blocks, cscs)):
             cp = C.indptr.astype(np.int64)
             nnz = int(cp[-1])
-            pad = (-nnz) % tile
             r = C.indices.astype(np.int64)
             col_of = np.repeat(np.arange(d, dtype=np.int64), np.diff(cp))  # each entry's column
+            nonempty = np.nonzero(cp[1:] > cp[:-1])[0]
+            cstart = cp[nonempty]  # first entry of every non-empty column
+            # tiles [bases, ends) and the chunks of tiles (first tile, tiles) of this block
+            if cuts:
+                bl, chunks, pos = [], [], 0
+                while pos < nnz:
+                    lim = pos + tile * wg_tiles
+                    end = nnz if lim >= nnz else int(cstart[np.searchsorted(cstart, lim, side="right") - 1])
+                    chunks.append((len(bl), -(-(end - pos) // tile)))
+                    bl.extend(range(pos, end, tile))
+                    pos = end
+                bases = np.asarray(bl, dtype=np.int64)
+                ends = np.minimum(bases + tile, np.append(bases[1:], nnz)) if bases.size else bases
+            else:
+                bases = np.arange(0, nnz, tile, dtype=np.int64)
+                ends = np.minimum(bases + tile, nnz)
+                chunks = [(t0, min(wg_tiles, bases.size - t0)) for t0 in range(0, bases.size, wg_tiles)]
+            nt = bases.size
             start = np.zeros(nnz, dtype=bool)  # run starts: first entry of a column or of a tile
-            start[cp[:-1][cp[:-1] < cp[1:]]] = True
-            start[::tile] = True
+            start[cstart] = True
+            start[bases] = True
             r = np.where(start, r | flag, r)
-            rows_l.append(np.concatenate([r, np.zeros(pad, dtype=np.int64)]))
-            vals_l.append(np.concatenate([C.data.astype(np.float64), np.zeros(pad)]))
+            # tile k's entries at slots [tile * k, tile * k + (ends - bases)), the rest zero padding
+            slot = np.zeros(nnz, dtype=np.int64)
+            if nnz:
+                tof = np.searchsorted(bases, np.arange(nnz), side="right") - 1
+                slot = tof * tile + (np.arange(nnz) - bases[tof])
+            rr = np.zeros(nt * tile, dtype=np.int64)
+            vv = np.zeros(nt * tile)
+            rr[slot] = r
+            vv[slot] = C.data.astype(np.float64)
+            rows_l.append(rr)
+            vals_l.append(vv)
             cps.append(cp.astype(np.int32))
             entry0.append(e_off)
             row0.append(r_off)
             nnzs.append(nnz)
             t_first = n_tiles
-            bases = np.arange(0, nnz, tile, dtype=np.int64)
-            if bases.size:
+            if nt:
                 c0 = np.searchsorted(cp, bases, side="right") - 1
-                end = np.minimum(bases + tile, nnz)
-                c_last = np.searchsorted(cp, end - 1, side="right") - 1
-                flags = (cp[c0] < bases).astype(np.int64) | 2 * (cp[c_last + 1] > bases + tile).astype(np.int64)
-                tiles.append(np.stack([np.full(bases.size, j), bases, c0, flags], axis=1))
-                n_tiles += bases.size
+                c_last = np.searchsorted(cp, ends - 1, side="right") - 1
+                flags = (cp[c0] < bases).astype(np.int64) | 2 * (cp[c_last + 1] > ends).astype(np.int64)
+                tiles.append(np.stack([np.full(nt, j), bases, c0, flags], axis=1))
+                n_tiles += nt
                 sidx = np.nonzero(start)[0]
                 runs_l.append(col_of[sidx])
                 r_first = np.searchsorted(sidx, bases)  # runs before each tile
                 r_cnt = np.diff(np.append(r_first, sidx.size))
-                ns = end - bases
+                ns = ends - bases
                 tkeys.append(np.stack([n_runs + r_first, ns | (r_cnt << 10) | (flags << 20),
-                                       np.full(bases.size, j), c0], axis=1))
+                                       np.full(nt, j), c0], axis=1))
                 n_runs += sidx.size
-            nonempty = np.nonzero(cp[1:] > cp[:-1])[0]
-            t1 = cp[nonempty] // tile
-            t2 = (cp[nonempty + 1] - 1) // tile
+            t1 = np.searchsorted(bases, cp[nonempty], side="right") - 1
+            t2 = np.searchsorted(bases, cp[nonempty + 1] - 1, side="right") - 1
             cross = t2 > t1
-            if cross.any():
+            if row_block > 0:
+                for k, (c_t0, c_nt) in enumerate(chunks):
+                    wg.append((r_off, t_first + c_t0, c_nt, A.shape[0]))
+                    if cuts:
+                        inside = cross & (t1 >= c_t0) & (t1 < c_t0 + c_nt)
+                        assert np.all(t2[inside] < c_t0 + c_nt) and inside.sum() < wg_tiles  # one per boundary
+                        if inside.any():
+                            wspan.append(np.stack([np.full(int(inside.sum()), j), nonempty[inside],
+                                                   t1[inside] - c_t0, t2[inside] - c_t0], axis=1))
+                        wspan_ptr.append(wspan_ptr[-1] + int(inside.sum()))
+            if cross.any() and not cuts:
                 spans.append(np.stack([np.full(int(cross.sum()), j), nonempty[cross], t_first + t1[cross],
                                        t_first + t2[cross]], axis=1))
             ec = np.nonzero(cp[1:] == cp[:-1])[0]
             if ec.size:
                 empty.append(np.stack([np.full(ec.size, j), ec], axis=1))
-            e_off += nnz + pad
+            e_off += nt * tile
             r_off += A.shape[0]
         crow = np.concatenate(rows_l) if rows_l else np.zeros(tile, dtype=np.int64)
         crow = crow.astype(np.uint16).view(np.int16) if row16 else crow.astype(np.uint32).view(np.int32)
-        wg = []
-        if row_block > 0:
-            t_of = np.concatenate(tiles)[:, 0] if tiles else np.zeros(0, dtype=np.int64)
-            firsts = np.searchsorted(t_of, np.arange(len(blocks)), side="left")
-            lasts = np.searchsorted(t_of, np.arange(len(blocks)), side="right")
-            for j, A in enumerate(blocks):
-                for t0 in range(int(firsts[j]), int(lasts[j]), wg_tiles):
-                    wg.append((row0[j], t0, min(wg_tiles, int(lasts[j]) - t0), A.shape[0]))
         extra = {"sub_begin": np.asarray(sub_begin, dtype=np.int32) if sub_begin is not None else None,
                  "wg": np.asarray(wg, dtype=np.int32).reshape(-1, 4), "nsub": len(blocks),
-                 "row_block": int(row_block)}
+                 "row_block": int(row_block), "wg_spans": bool(cuts),
+                 "wspan": (np.concatenate(wspan) if wspan else np.zeros((0, 4))).astype(np.int32).reshape(-1, 4),
+                 "wspan_ptr": np.asarray(wspan_ptr if cuts else [0], dtype=np.int32)}
         return {**extra, "row16": row16, "crow": np.ascontiguousarray(crow),
                 "cvals": np.concatenate(vals_l) if vals_l else np.zeros(tile),
                 "col_ptr": np.ascontiguousarray(np.stack(cps)) if cps else np.zeros((1, d + 1), dtype=np.int32),
@@ -876,7 +934,8 @@ class SparseGradPlan:
                                              self.part_entry0, self.part_row0, self.part_nnz, self.head, self.tail,
                                              self.span, empty, self.nsub, self.d, self.ld,
                                              wg=self.wg if len(self.wg) else None, u_lds=self.u_lds, Gs=self.Gs,
-                                             sub_begin=self.sub_begin, runs=self.runs, tkeys=self.tkeys)
+                                             sub_begin=self.sub_begin, runs=self.runs, tkeys=self.tkeys,
+                                             wspan=self.wspan, wspan_ptr=self.wspan_ptr)
             if not self.identity:
                 L.set_encode(self.enc_ptr, self.enc_idx, self.enc_coef, self.Gb)
             self._launcher = L

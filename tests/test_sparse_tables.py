@@ -41,8 +41,9 @@ def emulate(t, u_parts, d, keyed=False):
     for ti, (p, base, c0, flags) in enumerate(t["tiles"]):
         cp = t["col_ptr"][p].astype(np.int64)
         nnz = int(t["part_nnz"][p])
-        n = min(TILE, nnz - base)
-        e0 = int(t["part_entry0"][p]) + base
+        cut = bool(t.get("wg_spans"))  # column-aligned chunks: a tile's entry count is tkeys' n
+        n = int(t["tkeys"][ti][1]) & 1023 if cut else min(TILE, nnz - base)
+        e0 = TILE * ti if cut else int(t["part_entry0"][p]) + base
         assert e0 % 8 == 0
         cnt = np.zeros(TILE, dtype=np.int64)
         c = c0 + 1
@@ -79,6 +80,12 @@ def emulate(t, u_parts, d, keyed=False):
     for p, c, t1, t2 in t["span"]:
         assert np.isnan(G[p, c])
         G[p, c] = tail[t1] + sum(head[t] for t in range(t1 + 1, t2 + 1))
+    if t.get("wg_spans"):  # each workgroup's own crossing columns, chunk-relative tiles (from LDS)
+        assert len(t["span"]) == 0 and len(t["wspan_ptr"]) == len(t["wg"]) + 1
+        for k, (_, t0, nt, _) in enumerate(t["wg"]):
+            for p, c, t1, t2 in t["wspan"][t["wspan_ptr"][k]:t["wspan_ptr"][k + 1]]:
+                assert np.isnan(G[p, c]) and 0 <= t1 < t2 < nt
+                G[p, c] = tail[t0 + t1] + sum(head[t0 + t] for t in range(t1 + 1, t2 + 1))
     for p, c in t["empty"]:
         assert np.isnan(G[p, c])
         G[p, c] = 0.0
@@ -153,18 +160,23 @@ def test_cpu_plan_matches_scipy_per_message():
         np.testing.assert_allclose(G[s, :d].numpy(), ref, rtol=1e-12, atol=1e-12)
 
 
-@pytest.mark.parametrize("row_block", [64, 700, 4096])
-def test_row_blocked_tables_sum_to_the_transposed_product(row_block):
+@pytest.mark.parametrize("row_block,wg_spans", [(64, False), (700, False), (4096, False), (64, True), (700, True),
+                                                (4096, True)])
+def test_row_blocked_tables_sum_to_the_transposed_product(row_block, wg_spans):
     """Row-blocked tables (SparseGradPlan.csc_tables(row_block=...)): every partition cut into
     sub-blocks of at most row_block rows; the emulated sub-block sums, added per partition in
     sub-block order (grad_sparse.hip sub_reduce), are X_p^T u_p; the workgroup table covers every
-    tile of every sub-block exactly once, never mixing sub-blocks."""
+    tile of every sub-block exactly once, never mixing sub-blocks.  wg_spans: chunks end on column
+    boundaries and every crossing column is summed inside its workgroup."""
     rng = np.random.RandomState(7)
     d = 2500
     blocks = [_onehot(rng, 1800, [2, 40, 700, 1200]), _onehot(rng, 333, [1, 900, 5, 1000]),
               sps.csr_matrix((0, 2403))]
     blocks = [sps.csr_matrix((b.data, b.indices, b.indptr), shape=(b.shape[0], d)) for b in blocks]
-    t = SparseGradPlan.csc_tables(blocks, d, TILE, row_block=row_block, wg_tiles=16)
+    t = SparseGradPlan.csc_tables(blocks, d, TILE, row_block=row_block, wg_tiles=16, wg_spans=wg_spans)
+    assert t["wg_spans"] == wg_spans
+    if wg_spans and row_block > 512:  # (64-row sub-blocks fit one tile each)
+        assert len(t["wspan"]) > 0
     sb = t["sub_begin"]
     assert len(sb) == len(blocks) + 1 and sb[-1] == t["nsub"]
     u = [rng.randn(b.shape[0]) for b in blocks]

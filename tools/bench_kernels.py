@@ -302,7 +302,15 @@ def main():
     ap.add_argument("--precs", default="fp64,fp32", help="--only sweep: precisions")
     ap.add_argument("--sparse-shapes", default="covtype,kc_house_data,amazon-dataset", help="--only sparse: datasets")
     ap.add_argument("--ell-only", action="store_true", help="--only sparse: skip the CSR row pass")
+    ap.add_argument("--wg-tiles", type=int, default=0, help="--only sparse: tiles per column-pass workgroup (A/B)")
+    ap.add_argument("--no-wg-spans", action="store_true",
+                    help="--only sparse: whole 16-tile chunks and the csc_spans launch (A/B of SparseGradPlan.WG_SPANS)")
     a = ap.parse_args()
+    if a.no_wg_spans or a.wg_tiles:
+        from erasurehead_amd.ops import SparseGradPlan
+
+        SparseGradPlan.WG_SPANS = not a.no_wg_spans
+        SparseGradPlan.WG_TILES = a.wg_tiles or SparseGradPlan.WG_TILES
     out = []
     if a.only in (None, "dense"):
         dense_cases(out)
