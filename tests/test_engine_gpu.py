@@ -260,7 +260,8 @@ def test_gpu_share_partitions_sparse(ver, k, native):
 def test_gpu_amazon_scale_onehot(native):
     """Amazon-shaped stand-in (26215 x 241915 one-hot, 45 nnz per row; ref run_approx_coding.sh:30-32,
     src/arrange_real_data.py:34-91; synthetic, parity unpinned): AGC W=8, s=1, k=6 through the
-    native launcher (ELL gradient, 1.94 MB messages, 242k-column combine+update) and the native
+    native launcher (CSR row pass -- a 1.94 MB beta does not fit the LDS of the ELL one --, 1.94 MB
+    messages, 242k-column combine+update) and the native
     sparse evaluation, against the fp64 CPU engine + scipy/torch evaluation."""
     from erasurehead_amd.codes import make_scheme
     from erasurehead_amd.data.synthetic import REAL_SHAPES, onehot_partitions
@@ -278,7 +279,7 @@ def test_gpu_amazon_scale_onehot(native):
         sch = make_scheme("approx", W, s, n, k, 0)
         tr = Trainer(cfg, DistEnv(device=torch.device(dev)), src, scheme=sch)
         if dev == "cuda":
-            assert tr.plan.ell and tr.native_loop
+            assert not tr.plan.ell and tr.native_loop  # (ops/grad.py SparseGradPlan use_ell="auto")
         res = tr.run()
         ev = evaluate(tr, res, write=False)
         out[dev] = (res.betaset, ev.training_loss, ev.testing_loss, ev.auc)
