@@ -122,12 +122,30 @@ def run_config(name, cfg_kw, source=None, rounds=100, timed_from=5, delay_floor_
     return out
 
 
+def run_child(name, a) -> dict:
+    """One config in a fresh process (tools/bench_suite.py --only NAME --in-process); its suite row."""
+    import subprocess
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as tmp:
+        cmd = [sys.executable, os.path.abspath(__file__), "--only", name, "--in-process", "--out", tmp,
+               "--device-loop", a.device_loop] + (["--quick"] if a.quick else [])
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        if out.returncode != 0:
+            raise RuntimeError(f"{name}: child exited {out.returncode}: {out.stderr[-2000:]}")
+        with open(os.path.join(tmp, "suite.jsonl")) as f:
+            return json.loads(f.readline())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="10x smaller problems (plumbing check)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out"))
     ap.add_argument("--only", default=None, help="comma-separated config names")
     ap.add_argument("--device-loop", default="auto", choices=["auto", "graph", "stream", "off"])
+    ap.add_argument("--in-process", action="store_true",
+                    help="run the dense configs in this process too (default: one fresh process each, like bench.py: "
+                         "8 GB of X allocated after another config's freed 8 GB streamed up to 9 %% slower)")
     a = ap.parse_args()
     from erasurehead_amd.data.source import ArraySource
     from erasurehead_amd.data.synthetic import REAL_SHAPES, onehot_partitions
@@ -144,49 +162,77 @@ def main():
     configs.append(("cyclic_dense", dict(dense, is_coded=1, n_stragglers=2, coded_ver=0), None, None, False, "dense"))
     configs.append(("frc_dense", dict(dense, is_coded=1, n_stragglers=1, coded_ver=1), None, None, False, "dense"))
 
-    # covtype-shaped one-hot; partial schemes need (P - s) * W partition files
+    # covtype-shaped one-hot; partial schemes need (P - s) * W partition files.  Sources are built on first
+    # use (a dense-only child process never generates the one-hot ones)
+    import functools
+
     n_cov, d_cov, f_cov = REAL_SHAPES["covtype"]
     n_cov //= scale
     W, s, P = 8, 1, 4
-    cov_parts, cov_test, dc = onehot_partitions(n_cov, d_cov, f_cov, (P - s) * W, seed=3)
-    src_pr = ArraySource(cov_parts, cov_test, sparse=True)
-    n_pr = sum(p[0].shape[0] for p in cov_parts)
-    base_cov = dict(n_procs=W + 1, n_rows=n_pr, n_cols=dc, input_dir="/tmp/eh_suite/", is_real=1, dataset="covtype",
-                    update_rule="AGD", add_delay=1, force_delay=True, delay_mean=0.05)
-    configs.append(("partialrep_covtype", dict(base_cov, is_coded=1, n_stragglers=s, partitions=P, coded_ver=1),
-                    src_pr, {"stop_count": W}, False, "covtype_24parts"))
-    cov8, cov8_test, _ = onehot_partitions(n_cov, d_cov, f_cov, W, seed=3)
-    n8 = sum(p[0].shape[0] for p in cov8)
-    src8 = ArraySource(cov8, cov8_test, sparse=True)
-    configs.append(("naive_covtype", dict(base_cov, n_rows=n8, is_coded=0, add_delay=0, force_delay=False), src8,
-                    None, False, "covtype"))
-    configs.append(("avoid_covtype", dict(base_cov, n_rows=n8, is_coded=1, n_stragglers=s, coded_ver=2),
-                    src8, {"stop_count": W - s, "carry": True}, False, "covtype"))
-    configs.append(("agc_covtype", dict(base_cov, n_rows=n8, is_coded=1, n_stragglers=s, coded_ver=3, num_collect=6,
-                                        add_delay=0, force_delay=False), src8, None, False, "covtype"))
+
+    @functools.lru_cache(None)
+    def cov_pr():
+        cov_parts, cov_test, dc = onehot_partitions(n_cov, d_cov, f_cov, (P - s) * W, seed=3)
+        return ArraySource(cov_parts, cov_test, sparse=True), sum(p[0].shape[0] for p in cov_parts), dc
+
+    @functools.lru_cache(None)
+    def cov8():
+        parts, test, dc = onehot_partitions(n_cov, d_cov, f_cov, W, seed=3)
+        return ArraySource(parts, test, sparse=True), sum(p[0].shape[0] for p in parts), dc
+
+    def base_cov(src):
+        return dict(n_procs=W + 1, n_rows=src[1], n_cols=src[2], input_dir="/tmp/eh_suite/", is_real=1,
+                    dataset="covtype", update_rule="AGD", add_delay=1, force_delay=True, delay_mean=0.05)
+
+    configs.append(("partialrep_covtype", lambda: dict(base_cov(cov_pr()), is_coded=1, n_stragglers=s, partitions=P,
+                                                       coded_ver=1),
+                    lambda: cov_pr()[0], {"stop_count": W}, False, "covtype_24parts"))
+    configs.append(("naive_covtype", lambda: dict(base_cov(cov8()), is_coded=0, add_delay=0, force_delay=False),
+                    lambda: cov8()[0], None, False, "covtype"))
+    configs.append(("avoid_covtype", lambda: dict(base_cov(cov8()), is_coded=1, n_stragglers=s, coded_ver=2),
+                    lambda: cov8()[0], {"stop_count": W - s, "carry": True}, False, "covtype"))
+    configs.append(("agc_covtype", lambda: dict(base_cov(cov8()), is_coded=1, n_stragglers=s, coded_ver=3,
+                                                num_collect=6, add_delay=0, force_delay=False),
+                    lambda: cov8()[0], None, False, "covtype"))
 
     n_kc, d_kc, f_kc = REAL_SHAPES["kc_house_data"]
-    kc, kc_test, dk = onehot_partitions(n_kc, d_kc, f_kc, W, seed=5, least_squares=True)
-    src_kc = ArraySource(kc, kc_test, sparse=True)
-    nk = sum(p[0].shape[0] for p in kc)
-    base_kc = dict(n_procs=W + 1, n_rows=nk, n_cols=dk, input_dir="/tmp/eh_suite/", is_real=1,
-                   dataset="kc_house_data", update_rule="AGD", loss="least_squares", lr=0.2)
-    configs.append(("ls_kc_house_naive", dict(base_kc, is_coded=0), src_kc, None, False, "kc_house"))
+
+    @functools.lru_cache(None)
+    def kc():
+        parts, test, dk = onehot_partitions(n_kc, d_kc, f_kc, W, seed=5, least_squares=True)
+        return ArraySource(parts, test, sparse=True), sum(p[0].shape[0] for p in parts), dk
+
+    def base_kc():
+        src = kc()
+        return dict(n_procs=W + 1, n_rows=src[1], n_cols=src[2], input_dir="/tmp/eh_suite/", is_real=1,
+                    dataset="kc_house_data", update_rule="AGD", loss="least_squares", lr=0.2)
+
+    configs.append(("ls_kc_house_naive", lambda: dict(base_kc(), is_coded=0), lambda: kc()[0], None, False,
+                    "kc_house"))
     for k in (4, 5, 6, 7):
-        configs.append((f"ls_kc_house_agc_k{k}", dict(base_kc, is_coded=1, n_stragglers=1, coded_ver=3,
-                                                      num_collect=k), src_kc, None, False, "kc_house"))
+        configs.append((f"ls_kc_house_agc_k{k}",
+                        functools.partial(lambda k: dict(base_kc(), is_coded=1, n_stragglers=1, coded_ver=3,
+                                                         num_collect=k), k),
+                        lambda: kc()[0], None, False, "kc_house"))
     n_am, d_am, f_am = REAL_SHAPES["amazon-dataset"]
-    am, am_test, da = onehot_partitions(n_am // scale, d_am, f_am, W, seed=21)
-    src_am = ArraySource(am, am_test, sparse=True)
-    na = sum(p[0].shape[0] for p in am)
-    base_am = dict(n_procs=W + 1, n_rows=na, n_cols=da, input_dir="/tmp/eh_suite/", is_real=1,
-                   dataset="amazon-dataset", update_rule="AGD")
-    configs.append(("naive_amazon", dict(base_am, is_coded=0), src_am, None, False, "amazon"))
+
+    @functools.lru_cache(None)
+    def am():
+        parts, test, da = onehot_partitions(n_am // scale, d_am, f_am, W, seed=21)
+        return ArraySource(parts, test, sparse=True), sum(p[0].shape[0] for p in parts), da
+
+    def base_am():
+        src = am()
+        return dict(n_procs=W + 1, n_rows=src[1], n_cols=src[2], input_dir="/tmp/eh_suite/", is_real=1,
+                    dataset="amazon-dataset", update_rule="AGD")
+
+    configs.append(("naive_amazon", lambda: dict(base_am(), is_coded=0), lambda: am()[0], None, False, "amazon"))
     # the AGC / naive pair runs the same (device-driven) loop; the instrumented host-driven run is its own row
-    configs.append(("agc_amazon", dict(base_am, is_coded=1, n_stragglers=1, coded_ver=3, num_collect=6), src_am, None,
-                    False, "amazon"))
-    configs.append(("agc_amazon_instrumented", dict(base_am, is_coded=1, n_stragglers=1, coded_ver=3, num_collect=6),
-                    src_am, None, True, "amazon"))
+    configs.append(("agc_amazon", lambda: dict(base_am(), is_coded=1, n_stragglers=1, coded_ver=3, num_collect=6),
+                    lambda: am()[0], None, False, "amazon"))
+    configs.append(("agc_amazon_instrumented",
+                    lambda: dict(base_am(), is_coded=1, n_stragglers=1, coded_ver=3, num_collect=6),
+                    lambda: am()[0], None, True, "amazon"))
     if a.only:
         keep = set(a.only.split(","))
         configs = [c for c in configs if c[0] in keep]
@@ -194,7 +240,11 @@ def main():
     rows = []
     with open(os.path.join(a.out, "suite.jsonl"), "w") as f:
         for name, kw, src, floor_kw, inst, fam in configs:
-            r = run_config(name, kw, src, delay_floor_kw=floor_kw, device_loop=a.device_loop, instrument=inst)
+            if fam == "dense" and not a.in_process:
+                r = run_child(name, a)
+            else:
+                r = run_config(name, kw() if callable(kw) else kw, src() if callable(src) else src,
+                               delay_floor_kw=floor_kw, device_loop=a.device_loop, instrument=inst)
             r["family"] = fam
             rows.append(r)
             f.write(json.dumps(r) + "\n")
