@@ -69,10 +69,17 @@ __device__ __forceinline__ bf16x4 tr_read(const unsigned char* p) {
 // S = rows per stage = K of GEMM2: 32 (v_mfma_f32_16x16x32_bf16, two transposing reads per
 // fragment) or 16 (v_mfma_f32_16x16x16_bf16, one read): 16-row stages fit a 4-deep ring, so three
 // stages (96 KB at d = 1000) are in flight per CU instead of one 64 KB stage.
-template <int LOSS, int kMfS>
+//
+// PACK (R <= 4): the three bf16 terms of each fp32 operand are rows of the M dimension instead of three
+// MFMAs -- A row m = 4 r + s holds term s of replica r (s < 3; row 4 r + 3 and replicas >= R are zero) --
+// so each GEMM step is ONE MFMA: the 16-row M tile had 13 of its 16 rows zero at R = 3.  Lane group g of
+// the C fragment then holds replica g's three partial sums in registers 0..2, added small terms first.
+// (3x fewer MFMAs: the compute of a 32-row stage, measured alone, was 191 us per 2 GB.)
+template <int LOSS, int kMfS, bool PACK>
 __global__ void __launch_bounds__(512)
 grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ tasks, const float* __restrict__ beta,
-                 float* __restrict__ slab, int ld, int R, int pieces, int nstage, const int* __restrict__ gate) {
+                 float* __restrict__ slab, int ld, int R, int pieces, int nstage, const int* __restrict__ gate,
+                 int probe) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   if (gate_closed(gate)) return;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -91,17 +98,19 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
   float* zred = reinterpret_cast<float*>(smem_raw + nstage * buf_bytes);  // [wave][16][32] partial Zᵀ
   __bf16* rres = reinterpret_cast<__bf16*>(zred + kMfNW * 16 * kMfS);      // [split][16][32] residual terms
 
-  // residual role of this thread: (replica rm, stage row rn); threads past 16 * S idle there
+  // residual role of this thread: (replica rm, stage row rn); threads past 16 * S (PACK: 4 * S) idle there
   const int rm = tid / kMfS, rn = tid % kMfS;
-  const bool rrole = tid < 16 * kMfS;
+  const bool rrole = tid < (PACK ? 4 : 16) * kMfS;
   float rcoef = 0.f;
   if (rrole && rm < R) {
     const Task tq = tasks[blockIdx.x * R + rm];
     if (tq.seg >= 0) rcoef = static_cast<float>(segs[tq.seg].coef);
   }
   // GEMM1 A fragments: A[m = lane & 15][k = 8 (lane >> 4) + j] = beta[k] for replica rows m < R
-  const bool rep_ok = (lane & 15) < R;
-  bf16x8 bfr[kMfKPW][kMfSplit];
+  // (PACK: term m & 3 of beta[k] for replica m >> 2 < R, m & 3 < 3)
+  constexpr int NSP = PACK ? 1 : kMfSplit;
+  const bool rep_ok = PACK ? ((lane & 15) >> 2) < R && (lane & 3) < kMfSplit : (lane & 15) < R;
+  bf16x8 bfr[kMfKPW][NSP];
 #pragma unroll
   for (int kk = 0; kk < kMfKPW; ++kk) {
     const int k0 = (w * kMfKPW + kk) * 32 + 8 * (lane >> 4);
@@ -109,8 +118,13 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
     for (int j = 0; j < 8; ++j) {
       __bf16 t[kMfSplit];
       split_bf16(rep_ok && k0 + j < ld ? beta[k0 + j] : 0.f, t);
+      if constexpr (PACK) {
+        const int sm = lane & 3;
+        bfr[kk][0][j] = sm == 0 ? t[0] : sm == 1 ? t[1] : t[2];  // (sm == 3: rep_ok false, t all zero)
+      } else {
 #pragma unroll
-      for (int s = 0; s < kMfSplit; ++s) bfr[kk][s][j] = t[s];
+        for (int s = 0; s < kMfSplit; ++s) bfr[kk][s][j] = t[s];
+      }
     }
   }
   f32x4 g[kMfTPW];
@@ -118,10 +132,11 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
   for (int t = 0; t < kMfTPW; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   // slab rows of the replicas whose G elements this lane holds (m = 4 (lane >> 4) + reg); looked up
   // before the stage pipeline so no vector load is issued inside it (lds_dma.h, vmcnt counting)
+  // (PACK: lane group g holds replica g's three terms: slab_row[0] is replica g's row)
   int slab_row[4];
 #pragma unroll
   for (int reg = 0; reg < 4; ++reg) {
-    const int m = 4 * (lane >> 4) + reg;
+    const int m = PACK ? (reg == 0 ? lane >> 4 : R) : 4 * (lane >> 4) + reg;
     slab_row[reg] = -1;
     if (m < R) {
       const Task tq = tasks[blockIdx.x * R + m];
@@ -137,6 +152,7 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
   const int nblk = (full_bytes + 1023) >> 10;
   const int cnt_stage = (nblk > w ? (nblk - w + kMfNW - 1) / kMfNW : 0) + (w == 0 ? 1 : 0);
   auto issue = [&](int t) {
+    if (probe == 2) return;  // timing probe: no stage loads (the GEMMs read whatever LDS holds)
     const unsigned dst = lds_base + (t % nstage) * buf_bytes;
     const long long r0 = lead.row_begin + static_cast<long long>(t) * kMfS;
     const int ns = min(kMfS, static_cast<int>(lead.row_end - r0));
@@ -152,9 +168,11 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
   const int fi = lane & 15, fq = fi >> 2, fp = fi & 3, fg = lane >> 4;
   for (int t = 0; t < nst; ++t) {
     const int later = (min(t + nstage - 2, nst - 1) - t) * cnt_stage;
-    wait_vmcnt(later);  // this wave's pieces of stage t landed
+    if (probe == 2) wait_vmcnt(0);
+    else wait_vmcnt(later);  // this wave's pieces of stage t landed
     __syncthreads();    // every wave's pieces; stage t-1, zred and the residuals fully consumed
     if (t + nstage - 1 < nst) issue(t + nstage - 1);
+    if (probe == 1) continue;  // timing probe: the stage stream alone
     const unsigned char* buf = smem_raw + (t % nstage) * buf_bytes;
     const float* lab = reinterpret_cast<const float*>(buf + data_bytes);
     const int ns = min(kMfS, nrows - t * kMfS);
@@ -175,15 +193,21 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
       for (int nt = 0; nt < NT; ++nt) {
         const bf16x8 x = *reinterpret_cast<const bf16x8*>(buf + (16 * nt + fi) * rowbytes + col * 2);
 #pragma unroll
-        for (int s = kMfSplit - 1; s >= 0; --s) z[nt] = mma(bfr[kk][s], x, z[nt]);  // small terms first
+        for (int s = NSP - 1; s >= 0; --s) z[nt] = mma(bfr[kk][s], x, z[nt]);  // small terms first
       }
     }
-    // C layout: lane holds C[m = 4 (lane >> 4) + reg][n = lane & 15]  (replica m, stage row n)
+    // C layout: lane holds C[m = 4 (lane >> 4) + reg][n = lane & 15]  (replica m, stage row n; PACK:
+    // replica lane >> 4, its three terms in reg 0..2, added here)
     float* zw = zred + w * 16 * kMfS;
+    if constexpr (PACK) {
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg)
+      for (int nt = 0; nt < NT; ++nt) zw[fg * kMfS + 16 * nt + fi] = (z[nt][2] + z[nt][1]) + z[nt][0];
+    } else {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) zw[(4 * fg + reg) * kMfS + 16 * nt + fi] = z[nt][reg];
+      for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) zw[(4 * fg + reg) * kMfS + 16 * nt + fi] = z[nt][reg];
+    }
     __syncthreads();
     // ---- residual of (replica rm, row rn): fixed-order sum of the waves' K slices
     if (rrole) {
@@ -193,16 +217,21 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
       const float r = rm < R && rn < ns ? residual_hw<LOSS>(zs, lab[rn], rcoef) : 0.f;
       __bf16 t[kMfSplit];
       split_bf16(r, t);
+      if constexpr (PACK) {  // A row 4 rm + s; row 4 rm + 3 zero
 #pragma unroll
-      for (int s = 0; s < kMfSplit; ++s) rres[(s * 16 + rm) * kMfS + rn] = t[s];
+        for (int s = 0; s < 4; ++s) rres[(4 * rm + s) * kMfS + rn] = s < kMfSplit ? t[s < kMfSplit ? s : 0] : __bf16(0.f);
+      } else {
+#pragma unroll
+        for (int s = 0; s < kMfSplit; ++s) rres[(s * 16 + rm) * kMfS + rn] = t[s];
+      }
     }
     __syncthreads();
     // ---- GEMM2: G[replica][column] += Rm · X_stage over this wave's column tiles
     if constexpr (kMfS == 32) {
-      // A[m = replica lane & 15][k = row 8 (lane >> 4) + j]
-      bf16x8 ar[kMfSplit];
+      // A[m = replica lane & 15][k = row 8 (lane >> 4) + j]  (PACK: m = 4 replica + term)
+      bf16x8 ar[NSP];
 #pragma unroll
-      for (int s = 0; s < kMfSplit; ++s) ar[s] = *reinterpret_cast<const bf16x8*>(rres + (s * 16 + fi) * kMfS + 8 * fg);
+      for (int s = 0; s < NSP; ++s) ar[s] = *reinterpret_cast<const bf16x8*>(rres + (s * 16 + fi) * kMfS + 8 * fg);
 #pragma unroll
       for (int tt = 0; tt < kMfTPW; ++tt) {
         const int c0 = (w * kMfTPW + tt) * 16;
@@ -214,13 +243,13 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
         const bf16x4 t1 = tr_read(a0 + 4 * rowbytes);
         const bf16x8 xb = bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
 #pragma unroll
-        for (int s = kMfSplit - 1; s >= 0; --s) g[tt] = mma(ar[s], xb, g[tt]);
+        for (int s = NSP - 1; s >= 0; --s) g[tt] = mma(ar[s], xb, g[tt]);
       }
     } else {
-      // A[m = replica lane & 15][k = row 4 (lane >> 4) + j]
-      bf16x4 ar[kMfSplit];
+      // A[m = replica lane & 15][k = row 4 (lane >> 4) + j]  (PACK: m = 4 replica + term)
+      bf16x4 ar[NSP];
 #pragma unroll
-      for (int s = 0; s < kMfSplit; ++s) ar[s] = *reinterpret_cast<const bf16x4*>(rres + (s * 16 + fi) * kMfS + 4 * fg);
+      for (int s = 0; s < NSP; ++s) ar[s] = *reinterpret_cast<const bf16x4*>(rres + (s * 16 + fi) * kMfS + 4 * fg);
 #pragma unroll
       for (int tt = 0; tt < kMfTPW; ++tt) {
         const int c0 = (w * kMfTPW + tt) * 16;
@@ -228,7 +257,7 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
         // B[k = row 4 g + q][n = column c0 + i]: one transposing read of rows 4g..4g+3
         const bf16x4 xb = tr_read(buf + (4 * fg + fq) * rowbytes + (c0 + 4 * fp) * 2);
 #pragma unroll
-        for (int s = kMfSplit - 1; s >= 0; --s) g[tt] = mma(ar[s], xb, g[tt]);
+        for (int s = NSP - 1; s >= 0; --s) g[tt] = mma(ar[s], xb, g[tt]);
       }
     }
   }
@@ -238,9 +267,14 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
     const int c0 = (w * kMfTPW + tt) * 16;
     if (c0 >= ld) break;
     const int col = c0 + fi;
+    if constexpr (PACK) {
+      if (slab_row[0] >= 0 && col < ld)
+        slab[static_cast<long long>(slab_row[0]) * ld + col] = (g[tt][2] + g[tt][1]) + g[tt][0];
+    } else {
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg)
-      if (slab_row[reg] >= 0 && col < ld) slab[static_cast<long long>(slab_row[reg]) * ld + col] = g[tt][reg];
+      for (int reg = 0; reg < 4; ++reg)
+        if (slab_row[reg] >= 0 && col < ld) slab[static_cast<long long>(slab_row[reg]) * ld + col] = g[tt][reg];
+    }
   }
 }
 
@@ -286,9 +320,19 @@ hipError_t tr_probe_launch(const float* tile, int rowlen, float* out, hipStream_
 // Geometry of grad_staged_mfma: rows per stage S (32, 2-stage ring: 0.48 vs 0.59 ms for 16-row
 // stages in a 4-deep ring at the bf16 headline, profiles/round2/s1_mfma), LDS-DMA pieces per wave per
 // stage, ring depth and LDS bytes; false when ld does not fit.
+static int g_mfma_rows = 32;
+void set_mfma_stage_rows(int rows) { g_mfma_rows = rows == 16 ? 16 : 32; }
+// timing probes of grad_staged_mfma (tools/bench_rank_shapes.py --mfma-probe; results are NOT a
+// gradient): 1 = the LDS-DMA stage stream and barriers only, 2 = the GEMMs / residuals without loads
+static int g_mfma_probe = 0;
+void set_mfma_probe(int mode) { g_mfma_probe = mode == 1 || mode == 2 ? mode : 0; }
+// the packed-term form for R <= 4 (default) or the three-MFMA form, for A/B
+static bool g_mfma_pack = true;
+void set_mfma_pack(bool on) { g_mfma_pack = on; }
+
 bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds) {
   if (ld < 8 || ld > kMfNW * kMfKPW * 32 || ld % 8) return false;
-  const int S = 32;  // measured: 32-row stages (fewer barriers per byte) win
+  const int S = g_mfma_rows;  // measured: 32-row stages (fewer barriers per byte) win
   const int rowbytes = ld * 2;
   *rows = S;
   *pieces = (S * rowbytes + kMfNW * 1024 - 1) / (kMfNW * 1024);
@@ -311,13 +355,19 @@ hipError_t grad_mfma_launch(int loss, const Segment* segs, const Task* tasks, in
   int rows = 0, pieces = 0, nstage = 0;
   size_t lds = 0;
   if (!mfma_geometry(ld, &rows, &pieces, &nstage, &lds)) return hipErrorInvalidValue;
-  auto kern = rows == 32 ? (loss == kLogistic ? grad_staged_mfma<kLogistic, 32> : grad_staged_mfma<kLeastSquares, 32>)
-                         : (loss == kLogistic ? grad_staged_mfma<kLogistic, 16> : grad_staged_mfma<kLeastSquares, 16>);
+  const bool pack = R <= 4 && g_mfma_pack;
+  auto pick = [&](auto p32l, auto p32q, auto p16l, auto p16q) {
+    return rows == 32 ? (loss == kLogistic ? p32l : p32q) : (loss == kLogistic ? p16l : p16q);
+  };
+  auto kern = pack ? pick(grad_staged_mfma<kLogistic, 32, true>, grad_staged_mfma<kLeastSquares, 32, true>,
+                          grad_staged_mfma<kLogistic, 16, true>, grad_staged_mfma<kLeastSquares, 16, true>)
+                   : pick(grad_staged_mfma<kLogistic, 32, false>, grad_staged_mfma<kLeastSquares, 32, false>,
+                          grad_staged_mfma<kLogistic, 16, false>, grad_staged_mfma<kLeastSquares, 16, false>);
   const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
   if (ea != hipSuccess) return ea;
   hipLaunchKernelGGL(kern, dim3(ntasks / R), dim3(64 * kMfNW), lds, st, segs, tasks, beta, slab, ld, R, pieces,
-                     nstage, gate);
+                     nstage, gate, g_mfma_probe);
   return hipGetLastError();
 }
 

@@ -39,6 +39,10 @@ struct KernelChoice;
 // Slab reduction form (grad_dense.hip g_slab_mode): 1 fused launches (default), 2 fused plain /
 // two-stage puts, 0 two stages.
 void set_slab_reduce_mode(int mode);
+// rows per LDS stage of the bf16 MFMA bundles (grad_mfma.hip): 32 (default) or 16 (a 4-deep ring), for A/B
+void set_mfma_stage_rows(int rows);
+void set_mfma_probe(int mode);  // timing probes only (grad_mfma.hip): 1 stage stream alone, 2 compute alone
+void set_mfma_pack(bool on);    // bf16 MFMA bundles with R <= 4: bf16 terms packed into M (default) or 3 MFMAs
 // Timeline probe: grad_dense_multi launches write {start, rows done, slab written, XCC} ticks per bundle
 // into `stamps` (int64 [4 * bundles]); nullptr turns it off (tools/probes/bundle_stamps.py).
 void set_grad_stamps(void* stamps);

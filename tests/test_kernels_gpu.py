@@ -688,10 +688,20 @@ def test_lds_transpose_read_map(rowlen, native):
 
 @pytest.mark.parametrize("d", [1000, 1024, 333, 8])
 @pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
-def test_mfma_bf16_replica_bundles(d, loss, native):
+@pytest.mark.parametrize("pack", [True, False])
+def test_mfma_bf16_replica_bundles(d, loss, pack, native):
     """bf16 replica bundles on MFMA (grad_mfma.hip) at the staged geometry: the headline's uneven FRC
     layout (bundles of 3 and 2 replicas) plus cyclic-style distinct coefficients, every message
-    against the fp64 oracle on the stored bf16 values; and close to the VALU kernels."""
+    against the fp64 oracle on the stored bf16 values; and close to the VALU kernels.  pack: the
+    bf16 terms as M rows (R <= 4, the default) or one MFMA per term."""
+    native.set_mfma_pack(pack)
+    try:
+        _mfma_bundles_case(d, loss)
+    finally:
+        native.set_mfma_pack(True)
+
+
+def _mfma_bundles_case(d, loss):
     prec = get_precision("bf16")
     rng = np.random.RandomState(d + 7 * loss)
     parts, host = _parts(rng, [1500, 1501, 777], d, prec)

@@ -80,13 +80,15 @@ def build_plan(n_gpus: int, precision: str, shard: str = "partition", rows_overr
 
 
 def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0, fill: bool = False,
-        slab_mode: int = 1) -> dict:
+        slab_mode: int = 1, mfma_rows: int = 32, mfma_probe: int = 0) -> dict:
     import numpy as np
     import torch
 
     from erasurehead_amd._ext import native
 
     native().set_slab_reduce_mode(slab_mode)
+    native().set_mfma_stage_rows(mfma_rows)
+    native().set_mfma_probe(mfma_probe)  # (1 / 2: timing probes, not a gradient)
     plan, beta, G = build_plan(n_gpus, precision, shard, rows_override, fill)
     r, mode = plan.rank, plan.shard_mode
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -99,11 +101,13 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
         plan.run(beta, G)
         b.record()
     torch.cuda.synchronize()
-    ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    all_ms = [a.elapsed_time(b) for a, b in evs]
+    ms = float(np.median(all_ms))
     return {"n_gpus": n_gpus, "precision": precision, "shard": mode, "rank": r, "partitions": plan.n_parts,
             "shards": plan.n_shards, "bundle_rows": plan.bundle_rows, "kernel": plan.choice.label(), "ntasks": plan.ntasks,
-            "kernel_ms": ms, "distinct_TBps": plan.distinct_bytes / ms / 1e9, "fill": plan.choice.fill,
-            "slab_mode": slab_mode}
+            "kernel_ms": ms, "kernel_ms_min": float(np.min(all_ms)), "kernel_ms_max": float(np.max(all_ms)),
+            "distinct_TBps": plan.distinct_bytes / ms / 1e9, "fill": plan.choice.fill,
+            "slab_mode": slab_mode, "mfma_rows": mfma_rows, "mfma_probe": mfma_probe}
 
 
 def main():
@@ -119,9 +123,12 @@ def main():
     ap.add_argument("--fill", action="store_true", help="also time even splits over the workgroup slots")
     ap.add_argument("--ab-slab", action="store_true", help="also time the two-stage slab reduction (mode 0)")
     ap.add_argument("--slab-mode", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--mfma-rows", type=int, default=32, help="bf16 MFMA bundles: rows per LDS stage (32 / 16)")
+    ap.add_argument("--mfma-probe", type=int, default=0, help="bf16 MFMA timing probe: 1 loads only, 2 compute only")
     a = ap.parse_args()
     if a.one:
-        print(json.dumps(one(a.one, a.precision, a.shard, a.rows, a.fill, a.slab_mode)), flush=True)
+        print(json.dumps(one(a.one, a.precision, a.shard, a.rows, a.fill, a.slab_mode, a.mfma_rows, a.mfma_probe)),
+              flush=True)
         return 0
     lines = []
     sweeps = [None] + ([int(x) for x in a.rows_list.split(",")] if a.rows_sweep else [])
