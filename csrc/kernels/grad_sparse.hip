@@ -108,7 +108,9 @@ constexpr int kEllStageVecs = (kEllLdsBytes / 16 + 1023) / 1024;  // 16-byte sta
 
 template <typename A, int LOSS, bool IDX16, bool VALS>
 __global__ void __launch_bounds__(1024) ell_rows_lds(const SparseArgs a, const A* __restrict__ beta, const int* gate) {
-  // fields per batch: two batches (this one and the next) of loads stay within 128 VGPRs, no spills
+  // fields per batch: two batches (this one and the next) of loads stay within the 64 VGPRs the compiler
+  // gives a 1024-thread workgroup, no spills.  (28 fields per batch -- covtype's 55 in two dependent round
+  // trips instead of four -- spilled to scratch and took 29.7 vs 17.1 us, also with __launch_bounds__(1024, 1).)
   constexpr int KB = VALS ? 4 : IDX16 ? 16 : 8;
   using IW = std::conditional_t<IDX16, unsigned int, i32x2>;                    // a field of a row pair
   using V2 = std::conditional_t<sizeof(A) == 8, f64x2, f32x2>;                   // its two values
