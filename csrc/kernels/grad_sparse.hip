@@ -433,7 +433,7 @@ __device__ __forceinline__ void wave_affine_scan(int& g, A& b) {
 }
 
 constexpr int kWgWaves = 16;     // waves per column-pass workgroup
-constexpr int kMaxWgTiles = 64;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES <= this):
+constexpr int kMaxWgTiles = 128;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES <= this):
                                  // wave w takes the chunk's tiles w, w + 16, ...
 constexpr int kStageRegs = 4;    // staged residuals per thread: 4096 rows per sub-block (32 KB fp64 / 16 KB fp32)
 constexpr int kRunCap = 128;     // runs per tile compacted in LDS (covtype: 33 on average, 0.7 % of tiles above)

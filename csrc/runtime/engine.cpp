@@ -312,13 +312,13 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
     need_gpu(*wg, "wg");
     need(wg->scalar_type() == at::kInt && wg->dim() == 2 && wg->size(1) == 4, "wg: int32 [n, 4]");
     need(u_lds > 0 && u_lds * (g->acc == 0 ? 8 : 4) <= 96 * 1024, "u_lds: sub-block rows staged in LDS (<= 96 KB)");
-    {  // the column pass's chunks: 1..64 tiles each (grad_sparse.hip kMaxWgTiles), rows staged in LDS
+    {  // the column pass's chunks: 1..128 tiles each (grad_sparse.hip kMaxWgTiles), rows staged in LDS
       const Tensor wc = wg->cpu();
       const int* W = wc.data_ptr<int>();
       for (int64_t k = 0; k < wg->size(0); ++k)
-        need(W[4 * k + 2] >= 1 && W[4 * k + 2] <= 64 && W[4 * k + 1] >= 0 && W[4 * k + 1] + W[4 * k + 2] <= tiles.size(0) &&
+        need(W[4 * k + 2] >= 1 && W[4 * k + 2] <= 128 && W[4 * k + 1] >= 0 && W[4 * k + 1] + W[4 * k + 2] <= tiles.size(0) &&
                  W[4 * k + 3] <= u_lds,
-             "wg: (row0, first tile, 1..64 tiles, rows <= u_lds)");
+             "wg: (row0, first tile, 1..128 tiles, rows <= u_lds)");
     }
     a.wg = reinterpret_cast<const int4*>(wg->data_ptr<int>());
     a.nwg = (int)wg->size(0);
@@ -348,7 +348,7 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
       const int* W = wc.data_ptr<int>();
       need(P[0] == 0 && P[a.nwg] == sp.size(0), "wspan_ptr: [0, .., spans]");
       for (int k = 0; k < a.nwg; ++k) {
-        need(P[k] <= P[k + 1] && P[k + 1] - P[k] < 64, "wspan_ptr: non-decreasing, < 64 spans per workgroup");
+        need(P[k] <= P[k + 1] && P[k + 1] - P[k] < 128, "wspan_ptr: non-decreasing, < 128 spans per workgroup");
         for (int i = P[k]; i < P[k + 1]; ++i) {
           const int* e = S + 4 * i;
           need(e[0] >= 0 && e[0] < nparts && e[1] >= 0 && e[1] < d && e[2] >= 0 && e[2] < e[3] && e[3] < W[4 * k + 2],

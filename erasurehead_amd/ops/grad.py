@@ -619,11 +619,14 @@ class SparseGradPlan:
 
     TILE = 512  # grad_sparse.hip kTileEntries
     ROW_BLOCK_ROWS = 4096  # residuals of one column-pass sub-block, staged in LDS
-    # tiles per column-pass workgroup (<= grad_sparse.hip kMaxWgTiles; wave w takes w, w + 16, ...); None:
-    # by size -- 64 when chunks of 16 would fill the 512 workgroup slots four times over, else 16 (covtype-
-    # shaped naive 51.7 us at 64 vs 57.0 at 16; kc_house / amazon, 0.6k / 2.3k tiles: 13.7 / 21.3 us at 16,
-    # 22.8 / 35.8 at 64: fewer workgroups than slots; profiles/round5/sparse/)
+    # tiles per column-pass workgroup (wave w takes w, w + 16, ...): a fixed count (<= grad_sparse.hip
+    # kMaxWgTiles), or None -- balanced chunks sized to the chip (csc_tables slots): at most WG_SLOTS
+    # workgroups (256 CUs x 2 resident), chunks of 16 tiles when there are few.  Fixed 16 / 32 / 48 / 64 at
+    # covtype-shaped naive: 57.0 / 54.5 / 53.2 / 51.7 us (64: 680 workgroups, a second partial dispatch round);
+    # kc_house / amazon (0.6k / 2.3k tiles) want 16 (13.7 / 21.3 us; 22.8 / 35.8 at 64); profiles/round5/sparse/
     WG_TILES = None
+    MAX_WG_TILES = 128
+    WG_SLOTS = 512
     # column-aligned workgroup chunks (csc_tables wg_spans): the crossing columns are summed inside the
     # column pass's workgroups, no csc_spans launch and no head / tail round trip
     WG_SPANS = True  # (False: the csc_spans launch; tools/bench_kernels.py --no-wg-spans, for A/B)
@@ -720,11 +723,9 @@ class SparseGradPlan:
         # staged values per thread of its 1024-thread workgroups, grad_sparse.hip kStageRegs)
         rb = self.ROW_BLOCK_ROWS
         wgt = self.WG_TILES
-        if wgt is None:
-            wgt = 64 if self.nnz >= self.TILE * 16 * 512 * 4 else 16
-        self.wg_tiles = wgt
-        t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE, row_block=rb, wg_tiles=wgt,
-                            wg_spans=self.WG_SPANS)
+        self.wg_tiles = wgt or self.MAX_WG_TILES
+        t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE, row_block=rb, wg_tiles=self.wg_tiles,
+                            wg_spans=self.WG_SPANS, slots=0 if wgt else self.WG_SLOTS)
         self.row_block = rb
         self.nsub = t["nsub"]
         self.row16 = t["row16"]
@@ -766,7 +767,7 @@ class SparseGradPlan:
 
     @staticmethod
     def csc_tables(blocks, d: int, tile: int = 512, row_block: int = 0, wg_tiles: int = 16,
-                   wg_spans: bool = False) -> dict:
+                   wg_spans: bool = False, slots: int = 0) -> dict:
         """Host tables of the deterministic column pass (grad_sparse.hip csc_tiles / csc_spans): per
         partition a CSC twin (rows sorted by (column, row), padded to whole tiles), its column
         pointers, the tiles (partition, base entry, column of the base entry, span flags: 1 = the
@@ -792,7 +793,12 @@ class SparseGradPlan:
         (wspan: sub-block, column, first and last tile relative to the chunk; wspan_ptr: each
         workgroup's range).  No csc_spans launch, no head / tail round trip through memory.  Tile t's
         entries still sit at crow[tile * t ...]; its entry count is tkeys' n (< tile for a cut tile).
-        Falls back to whole chunks (span = the global list) when a column is longer than a chunk."""
+        Falls back to whole chunks (span = the global list) when a column is longer than a chunk.
+
+        slots > 0 (with wg_spans): balanced chunks sized to the chip -- sub-block s (T_s tiles of T in
+        all) is cut into n_s = max(1, min(ceil(T_s / 16), floor(T_s * slots / T))) chunks of about
+        T_s / n_s tiles (at most wg_tiles), so at most `slots` workgroups (one dispatch round of the
+        column pass's 2 per CU) when the tiles are many, and chunks of 16 when they are few."""
         import scipy.sparse as sps
 
         sub_begin = None
@@ -812,6 +818,7 @@ class SparseGradPlan:
             cscs.append(C)
             if cuts and C.nnz and int(np.diff(C.indptr).max()) > tile * wg_tiles:
                 cuts = False  # a column longer than a chunk: whole chunks and the global spans
+        total_tiles = sum(-(-C.nnz // tile) for C in cscs)
         row16 = all(A.shape[0] <= 32768 for A in blocks)
         flag = np.int64(1 << 15) if row16 else np.int64(1 << 31)
         rows_l, vals_l, cps, tiles, spans, empty = [], [], [], [], [], []
@@ -830,8 +837,13 @@ class SparseGradPlan:
             # tiles [bases, ends) and the chunks of tiles (first tile, tiles) of this block
             if cuts:
                 bl, chunks, pos = [], [], 0
+                per = tile * wg_tiles  # entries per chunk
+                if slots > 0 and nnz:
+                    ts = -(-nnz // tile)
+                    n_s = max(1, min(-(-ts // 16), (ts * slots) // max(1, total_tiles)))
+                    per = min(per, -(-nnz // n_s))
                 while pos < nnz:
-                    lim = pos + tile * wg_tiles
+                    lim = pos + per
                     end = nnz if lim >= nnz else int(cstart[np.searchsorted(cstart, lim, side="right") - 1])
                     chunks.append((len(bl), -(-(end - pos) // tile)))
                     bl.extend(range(pos, end, tile))

@@ -198,3 +198,30 @@ def test_row_blocked_tables_sum_to_the_transposed_product(row_block, wg_spans):
         for s in range(sb[j], sb[j + 1]):
             acc = acc + got[s]
         np.testing.assert_allclose(acc, b.T.dot(u[j]), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("slots", [4, 16, 512])
+def test_chip_sized_chunks(slots):
+    """csc_tables(slots=...): balanced column-aligned chunks, at most `slots` workgroups when the tiles are
+    many (and at least one per sub-block), chunks of about 16 tiles when they are few; every chunk at most
+    wg_tiles tiles; the emulated sums still give X_p^T u_p."""
+    rng = np.random.RandomState(11)
+    d = 2500
+    blocks = [_onehot(rng, 3000, [2, 40, 700, 1200]), _onehot(rng, 2500, [1, 900, 5, 1000])]
+    blocks = [sps.csr_matrix((b.data, b.indices, b.indptr), shape=(b.shape[0], d)) for b in blocks]
+    t = SparseGradPlan.csc_tables(blocks, d, TILE, row_block=1000, wg_tiles=128, wg_spans=True, slots=slots)
+    assert t["wg_spans"]
+    nsub = t["nsub"]
+    ntiles = len(t["tiles"])
+    assert len(t["wg"]) <= max(slots, nsub) and all(1 <= nt <= 128 for _, _, nt, _ in t["wg"])
+    if slots >= 512:  # few tiles for the chip: chunks of about 16
+        assert len(t["wg"]) >= ntiles // 17
+    u = [rng.randn(b.shape[0]) for b in blocks]
+    u_sub = [u[j][r:r + 1000] for j, b in enumerate(blocks) for r in range(0, b.shape[0], 1000)]
+    got = emulate(t, u_sub, d, keyed=True)
+    sb = t["sub_begin"]
+    for j, b in enumerate(blocks):
+        acc = np.zeros(d)
+        for s_ in range(sb[j], sb[j + 1]):
+            acc = acc + got[s_]
+        np.testing.assert_allclose(acc, b.T.dot(u[j]), rtol=1e-12, atol=1e-12)
