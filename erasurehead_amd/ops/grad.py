@@ -289,8 +289,12 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
                             bundle_rows=wide_bundle_rows(distinct_rows, n_cus, part_rows,
                                                          wide_slots_per_cu(prec_code, ld, max_rep)))
     if cpl <= 16 and max_rep in (2, 3):
+        # fp32 rows of 16 columns per lane size their replica bundles like fp64 (one folded workgroup per
+        # CU): AGC R = 3 at the 1 / 2 / 4 / 8-GPU rank shapes 586.7 / 299.0 / 155.5 / 86.3 us vs 587.6 /
+        # 303.4 / 170.6 / 87.4 with the 12-per-CU fp32 sizing (profiles/round5/shapes/fp32_rows_*.jsonl)
         return KernelChoice("multi", replicas=max_rep,
-                            bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1, n_cus, cpl, part_rows),
+                            bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 1 and cpl < 16, n_cus, cpl,
+                                                          part_rows),
                             fold=True, lane_epi=True)
     # more replicas than a workgroup's task slots: bundles of MAX_BUNDLE (and the remainder, padded)
     return KernelChoice("staged", replicas=min(max_rep, MAX_BUNDLE),

@@ -426,7 +426,8 @@ def test_dense_grad_one_wave_bundles_are_the_fp64_default(prec_name, native):
     b = DenseGradPlan(msgs, parts, prec, LOGISTIC, 1000, choice=MESSAGE_MAJOR)
     assert a.choice.kind == {"fp64": "multi", "fp32": "multi", "bf16": "mfma"}[prec_name]
     if a.choice.kind == "multi":
-        assert a.choice.fold and a.choice.lane_epi and a.bundle_rows == multi_bundle_rows(6000, prec_name == "fp32")
+        # (fp32 rows of 16 columns per lane: sized like fp64, ops/grad.py choose_kernel)
+        assert a.choice.fold and a.choice.lane_epi and a.bundle_rows == multi_bundle_rows(6000, False)
     beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
     Ga, Gb = a.out_buffer()[0], b.out_buffer()[0]
     a.native_launcher().launch(beta, Ga)

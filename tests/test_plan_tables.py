@@ -72,14 +72,15 @@ def test_kernel_selection_table():
 
     # the headline (AGC W=8 s=2: bundles of 3 replicas), one GPU (1e6 distinct rows): long stream
     assert pick(0, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=1024, fold=True, lane_epi=True)
-    assert pick(1, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=512, fold=True, lane_epi=True)
+    # (fp32 replica bundles sized like fp64: one folded workgroup per CU, profiles/round5/shapes/fp32_rows_*)
+    assert pick(1, 1000, 3, 1_000_000) == KernelChoice("multi", replicas=3, bundle_rows=1024, fold=True, lane_epi=True)
     assert pick(2, 1000, 3, 1_000_000) == KernelChoice("mfma", replicas=3, bundle_rows=4096)
     # bf16 MFMA bundles: every workgroup (one per CU) in the first dispatch round
     assert [pick(2, 1000, 3, n).bundle_rows for n in (500_000, 250_000, 125_000, 10_000)] == [2048, 1024, 512, 256]
     # the 8-GPU partition-shard rank (125k rows): fill every wave slot, lane epilogue
     assert pick(0, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=128, fold=True, lane_epi=True)
-    assert pick(1, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=64, fold=True, lane_epi=True)
-    assert pick(1, 1000, 3, 500_000).bundle_rows == 256 and pick(1, 1000, 3, 250_000).bundle_rows == 96
+    assert pick(1, 1000, 3, 125_000) == KernelChoice("multi", replicas=3, bundle_rows=128, fold=True, lane_epi=True)
+    assert pick(1, 1000, 3, 500_000).bundle_rows == 512 and pick(1, 1000, 3, 250_000).bundle_rows == 256
     # FRC s=1 (bundles of 2): one-wave bundles too, one GPU / a sharded rank
     assert pick(0, 1000, 2, 1_000_000) == KernelChoice("multi", replicas=2, bundle_rows=1024, fold=True, lane_epi=True)
     assert pick(0, 1000, 2, 250_000) == KernelChoice("multi", replicas=2, bundle_rows=256, fold=True, lane_epi=True)
@@ -120,8 +121,9 @@ def test_kernel_selection_table():
     # the regime boundary is a rows-per-CU rule, not a row count: 4x the CUs -> 4x the rows
     assert pick(0, 1000, 4, 700_000).wpr == 1 and pick(0, 1000, 4, 800_000).wpr == 0
     assert choose_kernel(0, 1000, 16, 4, 2_800_000, n_cus=1024).wpr == 1
-    # fp32 one-wave bundles: 12 per CU below the long-stream regime, 8 in it
-    assert pick(1, 1000, 3, 700_000).bundle_rows == 256 and pick(1, 1000, 3, 800_000).bundle_rows == 512
+    # fp32 replica bundles of 16 columns per lane: 4 per CU like fp64 at every size; narrower fp32 rows keep
+    # the 12-per-CU sizing below the long-stream regime, 8 in it
+    assert pick(1, 1000, 3, 700_000).bundle_rows == 768 and pick(1, 1000, 3, 800_000).bundle_rows == 896
 
 
 def test_no_tuning_env_knobs_left():
