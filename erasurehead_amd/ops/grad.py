@@ -105,7 +105,10 @@ class KernelChoice:
 
 
 def multi_slots(distinct_rows: int, fp32: bool = False, n_cus: int = N_CUS, cpl: int = 16) -> int:
-    """Resident one-wave bundles of grad_dense_multi on the chip (4 per folded workgroup)."""
+    """Resident one-wave bundles of grad_dense_multi on the chip (4 per folded workgroup).  ``fp32``
+    selects the 12 / 8-per-CU rule measured for fp32 in round 3; since round 5 it sizes bf16 distinct
+    rows and fp32 rows narrower than 16 columns per lane only, while fp32 rows of 16 columns per lane
+    take the fp64 rule (choose_kernel; profiles/round5/shapes/fp32_*)."""
     long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus
     # fp64: one workgroup (4 bundles) per CU.  Since a step waits for its own row only (the label
     # load behind the row), 4 waves with the next row in flight keep a CU's share of HBM busy, and
@@ -264,9 +267,11 @@ def choose_kernel(prec_code: int, ld: int, cpl: Optional[int], max_rep: int, dis
     if not shared:
         if 8 < cpl <= 16:  # distinct rows of 16 columns per lane: bundles of one
             # (bf16: six rows in flight per wave, grad_dense.hip kMultiDepth; 1e6 x 1000 rows 0.302 ms vs
-            # 0.367 on the fused kernel, profiles/round5/bf16/choices_naive.jsonl; sized like fp32)
+            # 0.367 on the fused kernel, profiles/round5/bf16/choices_naive.jsonl; sized with the 12 / 8 per CU
+            # rule: 1024-row bundles 0.350.  fp32 sized like fp64: 250k rows 152.2 us with 256-row bundles
+            # vs 161.3 with 96, 1e6 rows 577.0 vs 579.4, profiles/round5/shapes/fp32_naive_choices.jsonl)
             return KernelChoice("multi", replicas=1,
-                                bundle_rows=multi_bundle_rows(distinct_rows, prec_code != 0, n_cus, cpl, part_rows),
+                                bundle_rows=multi_bundle_rows(distinct_rows, prec_code == 2, n_cus, cpl, part_rows),
                                 fold=True)
         return KernelChoice("fused", rows={0: 2, 1: 4, 2: 1}[prec_code])
     long_stream = distinct_rows >= LONG_STREAM_ROWS_PER_CU * n_cus

@@ -90,11 +90,12 @@ def test_kernel_selection_table():
     assert pick(0, 1000, 4, 250_000) == KernelChoice("staged", replicas=4, bundle_rows=128, pair=True, wpr=1)
     # more co-located replicas than task slots per workgroup (a cyclic W = 9 table on one rank): bundles of 8
     assert pick(0, 1000, 9, 1_000_000).replicas == 8 and pick(2, 1000, 9, 1_000_000).replicas == 8
-    # distinct rows (naive): one-wave bundles of one replica (bf16 sized like fp32)
+    # distinct rows (naive): one-wave bundles of one replica (fp32 sized like fp64, bf16 with the 12 / 8 per CU rule)
     assert [pick(p, 1000, 1, 1_000_000) for p in (0, 1, 2)] == [
         KernelChoice("multi", replicas=1, bundle_rows=1024, fold=True),
-        KernelChoice("multi", replicas=1, bundle_rows=512, fold=True),
+        KernelChoice("multi", replicas=1, bundle_rows=1024, fold=True),
         KernelChoice("multi", replicas=1, bundle_rows=512, fold=True)]
+    assert pick(1, 1000, 1, 250_000).bundle_rows == 256
     assert pick(0, 256, 1, 1_000_000) == KernelChoice("fused", rows=2)  # narrow distinct rows: fused
     # d = 2048: fp64 replicas on 256-thread wide-row bundles, fp32 on LDS-staged bundles (pair form,
     # 1024 rows in the long stream); 4096 takes the wide kernel
