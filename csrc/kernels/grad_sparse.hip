@@ -19,8 +19,11 @@
 //     tile): the segmented sums restart at the flags -- a sequential sum over the lane's 8 entries,
 //     then an affine scan of (continues, sum) over the 64 lanes on DPP -- and each run's sum is
 //     compacted in LDS by run index and written to the run's column (the tile's run list).  A column
-//     crossing tiles leaves its first part in tail[t1] and its later parts in head[t] (pass 3 adds
-//     them in tile order); the sub-block sums are added per partition inside the encoding.
+//     crossing tiles leaves its first part in tail[t1] and its later parts in head[t], added in tile
+//     order: by the workgroup itself from LDS when its chunk of tiles ends on a column boundary (the
+//     default: chunks sized to one dispatch round of the chip, a wave looping over its tiles with the
+//     next one in flight), else by pass 3 (csc_spans); the sub-block sums are added per partition
+//     inside the encoding (a naive plan without sub-blocks writes its messages directly).
 //   encode (encode.hip): G[message] = sum_p coef(message, p) g_p in a fixed order -- the label
 //     encoding is linear in the coefficient (residual(z, y, c) = c residual(z, y, 1)), so one
 //     read of a partition feeds every co-located replica with its own coefficient.
