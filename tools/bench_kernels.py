@@ -303,14 +303,16 @@ def main():
     ap.add_argument("--sparse-shapes", default="covtype,kc_house_data,amazon-dataset", help="--only sparse: datasets")
     ap.add_argument("--ell-only", action="store_true", help="--only sparse: skip the CSR row pass")
     ap.add_argument("--wg-tiles", type=int, default=0, help="--only sparse: tiles per column-pass workgroup (A/B)")
+    ap.add_argument("--wg-slots", type=int, default=0, help="--only sparse: workgroup budget of the chip-sized chunks (A/B)")
     ap.add_argument("--no-wg-spans", action="store_true",
                     help="--only sparse: whole 16-tile chunks and the csc_spans launch (A/B of SparseGradPlan.WG_SPANS)")
     a = ap.parse_args()
-    if a.no_wg_spans or a.wg_tiles:
+    if a.no_wg_spans or a.wg_tiles or a.wg_slots:
         from erasurehead_amd.ops import SparseGradPlan
 
         SparseGradPlan.WG_SPANS = not a.no_wg_spans
         SparseGradPlan.WG_TILES = a.wg_tiles or SparseGradPlan.WG_TILES
+        SparseGradPlan.WG_SLOTS = a.wg_slots or SparseGradPlan.WG_SLOTS
     out = []
     if a.only in (None, "dense"):
         dense_cases(out)
