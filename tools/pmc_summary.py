@@ -40,6 +40,7 @@ def kernel_summary(d):
     vals = defaultdict(lambda: defaultdict(list))
     for _, row in _rows(d):
         name = row.get("Kernel_Name", "")
+        name = name.replace("(anonymous namespace)::", "")  # (its parenthesis would cut the name short)
         name = name.split("(")[0] if name.startswith("void ") else name
         vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {}
