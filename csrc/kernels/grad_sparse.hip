@@ -417,22 +417,53 @@ __device__ __forceinline__ int wave_incl_sum(int x) {
   x += dpp_i<0x143, 0xc>(0, x);  // row_bcast:31 -> rows 2, 3
   return x;
 }
-// inclusive scan of x_l = g_l x_{l-1} + b_l over the lanes (identity g = 1, b = 0)
+// DPP move over full rows with bound_ctrl: a lane without a source reads 0, so no old value is set up
+// (one v_mov_b32_dpp per dword instead of a v_mov of the identity and the DPP move)
+template <int CTRL, typename A>
+__device__ __forceinline__ A dpp_a0(A x) {
+  if constexpr (sizeof(A) == 8) {
+    const unsigned long long xi = __builtin_bit_cast(unsigned long long, x);
+    const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_mov_dpp(static_cast<int>(xi), CTRL, 0xf, 0xf, true));
+    const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_mov_dpp(static_cast<int>(xi >> 32), CTRL, 0xf, 0xf, true));
+    return __builtin_bit_cast(A, (static_cast<unsigned long long>(hi) << 32) | lo);
+  } else {
+    return __builtin_bit_cast(A, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xf, 0xf, true));
+  }
+}
+// h |= h of the DPP source lane, for h in {0.0, 1.0}: the high dword carries the whole value (the low one
+// is 0 for both), and an unsigned max with identity 0 folds into one v_max_u32_dpp
 template <int CTRL, int ROWS, typename A>
-__device__ __forceinline__ void affine_step(int& g, A& b) {
-  const A bp = dpp_a<CTRL, ROWS>(A(0), b);
-  const int gp = dpp_i<CTRL, ROWS>(1, g);
-  b = fma(static_cast<A>(g), bp, b);  // b + bp or b (g is 0 / 1), one op for a select of two doubles
-  g &= gp;
+__device__ __forceinline__ A dpp_or01(A h) {
+  if constexpr (sizeof(A) == 8) {
+    const unsigned hi = static_cast<unsigned>(__builtin_bit_cast(unsigned long long, h) >> 32);
+    const unsigned hp = static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(hi), CTRL, ROWS, 0xf, ROWS == 0xf));
+    return __builtin_bit_cast(A, static_cast<unsigned long long>(max(hi, hp)) << 32);
+  } else {
+    const unsigned u = __builtin_bit_cast(unsigned, h);
+    const unsigned up = static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(u), CTRL, ROWS, 0xf, ROWS == 0xf));
+    return __builtin_bit_cast(A, max(u, up));
+  }
+}
+// inclusive scan of x_l = g_l x_{l-1} + b_l over the lanes, carried as h = 1 - g (1: this lane's run, or one
+// between it and the source lane, starts a new segment) so every lane without a source holds the
+// identity (h = 0, b = 0) that bound_ctrl supplies.  b + g bp is fma(g, bp, b) with g = 1 - h exactly 0 / 1:
+// exactly b + bp or b, one op where a select of two doubles took three.
+template <int CTRL, int ROWS, typename A>
+__device__ __forceinline__ void affine_step(A& h, A& b) {
+  A bp;
+  if constexpr (ROWS == 0xf) bp = dpp_a0<CTRL>(b);
+  else bp = dpp_a<CTRL, ROWS>(A(0), b);
+  b = fma(A(1) - h, bp, b);
+  h = dpp_or01<CTRL, ROWS>(h);
 }
 template <typename A>
-__device__ __forceinline__ void wave_affine_scan(int& g, A& b) {
-  affine_step<0x111, 0xf>(g, b);
-  affine_step<0x112, 0xf>(g, b);
-  affine_step<0x114, 0xf>(g, b);
-  affine_step<0x118, 0xf>(g, b);
-  affine_step<0x142, 0xa>(g, b);
-  affine_step<0x143, 0xc>(g, b);
+__device__ __forceinline__ void wave_affine_scan(A h, A& b) {
+  affine_step<0x111, 0xf>(h, b);
+  affine_step<0x112, 0xf>(h, b);
+  affine_step<0x114, 0xf>(h, b);
+  affine_step<0x118, 0xf>(h, b);
+  affine_step<0x142, 0xa>(h, b);
+  affine_step<0x143, 0xc>(h, b);
 }
 
 constexpr int kWgWaves = 16;     // waves per column-pass workgroup
@@ -602,10 +633,9 @@ __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, con
     sm[0] = v[0];
 #pragma unroll
     for (int i = 1; i < 8; ++i) sm[i] = fma(static_cast<A>(((fl >> i) & 1u) ^ 1u), sm[i - 1], v[i]);
-    int g = fl == 0u ? 1 : 0;  // the whole lane continues the previous lane's run
     A b = sm[7];
-    wave_affine_scan(g, b);
-    const A prev = dpp_a<0x138, 0xf>(A(0), b);  // wave_shr:1 -- the previous lane's running sum
+    wave_affine_scan(fl ? A(1) : A(0), b);  // h = 0: the whole lane continues the previous lane's run
+    const A prev = dpp_a0<0x138>(b);        // wave_shr:1 -- the previous lane's running sum
     const A carry = fl & 1u ? A(0) : prev;       // into this lane's entries before its first flag
     const unsigned cmask = fl ? (fl & (0u - fl)) - 1u : 0xffu;
     A* __restrict__ gout = static_cast<A*>(a.Gs) + static_cast<long long>(p) * a.ld;
