@@ -409,10 +409,10 @@ __device__ __forceinline__ A dpp_a(A old, A x) {
   }
 }
 __device__ __forceinline__ int wave_incl_sum(int x) {
-  x += dpp_i<0x111, 0xf>(0, x);
-  x += dpp_i<0x112, 0xf>(0, x);
-  x += dpp_i<0x114, 0xf>(0, x);
-  x += dpp_i<0x118, 0xf>(0, x);
+  x += __builtin_amdgcn_mov_dpp(x, 0x111, 0xf, 0xf, true);  // full rows: bound_ctrl's 0, no identity to set up
+  x += __builtin_amdgcn_mov_dpp(x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_mov_dpp(x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_mov_dpp(x, 0x118, 0xf, 0xf, true);
   x += dpp_i<0x142, 0xa>(0, x);  // row_bcast:15 -> rows 1, 3
   x += dpp_i<0x143, 0xc>(0, x);  // row_bcast:31 -> rows 2, 3
   return x;
@@ -500,9 +500,14 @@ __device__ __forceinline__ unsigned tile_rows_decode(const TileRaw& r, int (&row
     for (int i = 0; i < 4; ++i) {
       rows[2 * i] = static_cast<int>(rw[i] & 0x7fffu);
       rows[2 * i + 1] = static_cast<int>((rw[i] >> 16) & 0x7fffu);
-      fl |= ((rw[i] >> 15) & 1u) << (2 * i);
-      fl |= (rw[i] >> 31) << (2 * i + 1);
     }
+    // the 8 flag bits (bit 15 / 31 of each dword): v_perm_b32 gathers the high byte of every entry (flags at
+    // bits 7, 15, 23, 31), the two words' flags interleave to bits 8k and 8k + 4, and one multiply moves
+    // entry e's bit to 24 + e (its partial products land on distinct bits: no carries)
+    const unsigned p01 = __builtin_amdgcn_perm(rw[1], rw[0], 0x07050301u);
+    const unsigned p23 = __builtin_amdgcn_perm(rw[3], rw[2], 0x07050301u);
+    const unsigned q = ((p01 >> 7) & 0x01010101u) | ((p23 >> 3) & 0x10101010u);
+    fl = (q * 0x01020408u) >> 24;
   } else {
     const unsigned int rw[8] = {r.x.x, r.x.y, r.x.z, r.x.w, r.y.x, r.y.y, r.y.z, r.y.w};
 #pragma unroll
