@@ -90,6 +90,10 @@ def parse(argv=None):
     ap.add_argument("--tie-break", default="permute", choices=["permute", "worker"])
     ap.add_argument("--preflight", type=int, default=1000,
                     help="N > 1: put -> flag round trips per worker/master pair before the timed rounds (0: off)")
+    ap.add_argument("--selfcheck", type=int, default=30,
+                    help="N > 1: integrity-tagged rounds on the headline's executor before timing (first_contact)")
+    ap.add_argument("--selfcheck-timeout", type=float, default=10.0,
+                    help="first_contact: round timeout of the check run (worker beta waits: 2.5x + 5 s)")
     ap.add_argument("--share-partitions", action="store_true",
                     help="co-located workers stream each distinct partition once (not the headline)")
     ap.add_argument("--drain", default=None, choices=["all", "carry", "lazy"],
@@ -180,30 +184,22 @@ def main(argv=None) -> int:
     est_round_ms = max(0.02, a.n_rows * a.n_cols * esize / world / 6e9)  # distinct rows at ~6 TB/s
     clock_rounds = min(1000, int(np.ceil(a.clock_warmup_ms / est_round_ms))) if a.clock_warmup_ms > 0 else 0
     w0 = clock_rounds + a.warmup  # first timed round
+    # N > 1: the job checks the exact path its headline will take before anything is timed (preflight
+    # round trips per pair, then a bounded integrity-tagged run), stepping down arbiter -> native pump ->
+    # RCCL p2p on any failure, in this process (first_contact)
+    contact = first_contact(a, make_cfg, env, free, Trainer, TransportError) if env.world > 1 else None
     t_setup = time.perf_counter()
     trainer = Trainer(make_cfg(w0 + a.steps), env)
     setup_s = time.perf_counter() - t_setup
-    # the first multi-GPU run checks itself: put -> flag latency and payload checks per worker/master pair
-    preflight_failure = fallback_preflight = None
-    try:
-        preflight = trainer.preflight(a.preflight) if env.world > 1 and a.preflight > 0 else None
-    except TransportError as e:
-        # every rank raised the same verdict (IpcTransport.preflight): the IPC mailbox lost a payload or a
-        # signal.  Unless the IPC path was asked for by name, rebuild on RCCL p2p under the same pumps
-        # (the loud fallback make_transport takes when the handshake fails) and record why.
-        if a.transport == "ipc" or os.environ.get("ERASUREHEAD_NO_FALLBACK"):
-            raise
-        preflight_failure, preflight = str(e), None
-        a.transport = "rccl" if env.backend == "nccl" else "loopback"
+    res, why = trainer.run_contained(timed_start=w0)
+    if why is not None:  # the headline itself failed after a clean first contact: one rung down, once
+        step = step_down(a, env, trainer, why)
         if env.is_master:
-            print(f"[bench] WARNING: {e}; rebuilding on {a.transport}", file=sys.stderr, flush=True)
+            print(f"[bench] WARNING: headline run failed ({why}); rebuilding: {step}", file=sys.stderr, flush=True)
         free(trainer)
+        contact = dict(contact or {}, headline_failure=why, headline_step_down=step)
         trainer = Trainer(make_cfg(w0 + a.steps), env)
-        # the fallback checks itself before anything is timed: round trips over its own send/recv
-        # path (loopback runs over the same IPC mappings and shared counters as the mailbox whose
-        # check failed, so it is no independent path until it has passed this)
-        fallback_preflight = trainer.tx.preflight(min(200, a.preflight))
-    res = trainer.run(timed_start=w0)
+        res = trainer.run(timed_start=w0)
     mine = res.timed_seconds if env.is_master else trainer.worker_timed_seconds
     timed = env.allreduce_max(mine)
     sch = trainer.scheme
@@ -267,19 +263,27 @@ def main(argv=None) -> int:
         if a.delay_on == "worker" or a.slow_ranks:
             out["config"]["delay_on"] = a.delay_on
             out["config"]["slow_ranks"] = parse_slow_ranks(a.slow_ranks)
-        if preflight is not None:
-            out["peer_preflight"] = preflight
-        if preflight_failure is not None:
-            out["peer_preflight_failure"] = preflight_failure
-            out["fallback_preflight"] = fallback_preflight
-            out["fallback_mechanism"] = ("loopback: device copies through IPC staging rings + shared counters (the "
-                                         "mailbox's mechanism), checked by fallback_preflight before timing"
-                                         if trainer.transport == "loopback" else "RCCL p2p (ncclSend / ncclRecv)")
+        # what the first multi-GPU contact will run, and why (first_contact; README "First contact")
+        out["release_form"] = trainer.release_form
+        out["release_reason"] = trainer.release_reason
+        out["device_map"] = {str(r): b for r, b in enumerate(trainer.device_map)}
+        if contact is not None:
+            out["first_contact"] = contact
+            if contact.get("preflight") is not None:
+                out["peer_preflight"] = contact["preflight"]
+            if contact.get("preflight_failure") is not None:
+                out["peer_preflight_failure"] = contact["preflight_failure"]
+                out["fallback_preflight"] = contact.get("fallback_preflight")
+                out["fallback_mechanism"] = ("loopback: device copies through IPC staging rings + shared counters "
+                                             "(the mailbox's mechanism), checked by fallback_preflight before timing"
+                                             if trainer.transport == "loopback" else "RCCL p2p (ncclSend / ncclRecv)")
         if n_gpu_dev and env.world > n_gpu_dev:
             out["config"]["ranks_per_gpu"] = env.world / n_gpu_dev  # rehearsal: ranks time-share GPUs
         out["config"]["round_loop"] = {"graph": "device-driven, hipGraph", "stream": "device-driven",
                                           "arbiter": "device-driven (arbiter kernel polls the workers)"}.get(
             trainer.device_loop, "host-driven (native pump)" if trainer.native_loop else "host-driven (python)")
+        out["config"]["round_loop_reason"] = trainer.loop_reason
+        out["config"]["release_form"] = trainer.release_form
         if a.share_partitions:
             out["config"]["share_partitions"] = True
         ref = _ref_cpu_equiv()
@@ -435,6 +439,87 @@ def main(argv=None) -> int:
                 f.write(line + "\n")
     env.shutdown()
     return 0
+
+
+def step_down(a, env, trainer, why: str) -> str:
+    """One rung down the N > 1 executor ladder after ``trainer``'s run failed collectively (every rank
+    calls it with the same trainer state): arbiter -> native pump on the same transport (for the rest
+    of the job: ERASUREHEAD_DEVICE_MASTER=off), IPC mailbox -> RCCL p2p (loopback where ranks share a
+    GPU, which RCCL refuses).  Raises when nothing is left below."""
+    if trainer.loop == "arbiter":
+        os.environ["ERASUREHEAD_DEVICE_MASTER"] = "off"
+        return "arbiter -> native pump (ERASUREHEAD_DEVICE_MASTER=off for the rest of the job)"
+    if trainer.transport == "ipc" and a.transport != "ipc" and not os.environ.get("ERASUREHEAD_NO_FALLBACK"):
+        a.transport = "rccl" if env.backend == "nccl" else "loopback"
+        return f"ipc -> {a.transport} (native pump)"
+    raise RuntimeError(f"first contact: the {trainer.loop} loop over {trainer.transport} failed and no path is "
+                       f"left below it: {why}")
+
+
+def first_contact(a, make_cfg, env, free, Trainer, TransportError) -> dict:
+    """N > 1, before the headline trainer exists: check the path it will take, in this process.
+
+    1. --preflight put -> flag round trips per master/worker pair over the IPC mailbox (device clock,
+       payload checked both ways; IpcTransport.preflight), plus RCCL p2p round trips for comparison.
+    2. --selfcheck rounds of the real problem on the executor the headline will select (the arbiter
+       where ranks own their GPUs), every message and beta integrity-tagged, every wait bounded by
+       --selfcheck-timeout (Trainer.run_contained: a failure on any rank becomes one verdict that
+       every rank holds, with the job still collectively consistent).
+    Any failure steps one rung down (step_down) and checks again: arbiter -> native pump -> RCCL p2p.
+    Nothing re-execs.  Returns the record bench.py reports as ``first_contact``: the device map and
+    release form, the preflight, and one entry per rung tried (loop, transport, verdict, seconds).
+    Test hook ERASUREHEAD_SABOTAGE=firstcontact:<spec>: ERASUREHEAD_SABOTAGE=<spec> for the first rung only."""
+    rec = {"rounds": a.selfcheck, "round_timeout_s": a.selfcheck_timeout, "ladder": []}
+    once = None
+    if os.environ.get("ERASUREHEAD_SABOTAGE", "").startswith("firstcontact:"):
+        once = os.environ.pop("ERASUREHEAD_SABOTAGE").split(":", 1)[1]
+    while True:
+        if once:
+            os.environ["ERASUREHEAD_SABOTAGE"] = once
+        tr = Trainer(make_cfg(max(1, a.selfcheck), round_timeout=a.selfcheck_timeout, integrity=True), env)
+        rec.setdefault("device_map", {str(r): b for r, b in enumerate(tr.device_map)})
+        rec.setdefault("release_form", tr.release_form)
+        rec.setdefault("release_reason", tr.release_reason)
+        if tr.transport == "ipc" and a.preflight > 0 and "preflight" not in rec:
+            try:
+                rec["preflight"] = tr.preflight(a.preflight)
+            except TransportError as e:
+                # every rank raised the same verdict: the mailbox lost a payload or a signal
+                rec["preflight"], rec["preflight_failure"] = None, str(e)
+                if a.transport == "ipc" or os.environ.get("ERASUREHEAD_NO_FALLBACK"):
+                    raise
+                a.transport = "rccl" if env.backend == "nccl" else "loopback"
+                if env.is_master:
+                    print(f"[bench] WARNING: {e}; rebuilding on {a.transport}", file=sys.stderr, flush=True)
+                rec["ladder"].append({"transport": "ipc", "ok": False, "failure": str(e), "stage": "preflight",
+                                      "step_down": f"ipc -> {a.transport}"})
+                free(tr)
+                continue
+        if tr.transport != "ipc" and "fallback_preflight" not in rec and hasattr(tr.tx, "preflight") \
+                and rec.get("preflight_failure"):
+            # loopback runs over the same IPC mappings as the mailbox whose check failed: it proves itself
+            rec["fallback_preflight"] = tr.tx.preflight(min(200, max(1, a.preflight)))
+        tr.native_loop  # noqa: B018 -- selects tr.loop / tr.loop_reason from this run's facts
+        step = {"transport": tr.transport, "round_loop": tr.loop, "reason": tr.loop_reason,
+                "release_form": tr.release_form}
+        t0 = time.perf_counter()
+        _, why = tr.run_contained()
+        step.update(ok=why is None, seconds=round(time.perf_counter() - t0, 3),
+                    round_loop_ran=tr.device_loop or ("native pump" if tr.native_loop else "python"))
+        if once:
+            os.environ.pop("ERASUREHEAD_SABOTAGE", None)
+            once = None
+        if why is not None:
+            step["failure"] = why
+            step["step_down"] = step_down(a, env, tr, why)
+            if env.is_master:
+                print(f"[bench] WARNING: first contact failed on {tr.loop} over {tr.transport}: {why}; "
+                      f"{step['step_down']}", file=sys.stderr, flush=True)
+        rec["ladder"].append(step)
+        free(tr)
+        if why is None:
+            rec["round_loop"], rec["transport"] = step["round_loop"], step["transport"]
+            return rec
 
 
 STRAGGLER_RUNS = (("naive", True, None), ("agc_drain", False, "all"), ("agc_lazy", False, "lazy"))

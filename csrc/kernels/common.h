@@ -310,10 +310,10 @@ __device__ __forceinline__ bool gate_closed(const int* gate) {
 // the arbiter's per-target counters made its release grow with the rank count, 4.3 us at 2 ranks,
 // 12.2 at 8, profiles/round3/arbiter_books).  Call from every thread (block-uniform control flow).
 //
-// strict (launchers.h strict_release(), ERASUREHEAD_STRICT_RELEASE=1): the forms before round 4 on top
-// -- every thread also fences at system scope, and publish_u64 / the block counters are release /
-// acq_rel ordered.  A switch for first contact with a cross-GPU (xGMI) node: the relaxed forms are
-// measured only with every rank on one GPU so far.
+// strict (launchers.h strict_release()): the forms before round 4 on top -- every thread also fences
+// at system scope, and publish_u64 / the block counters are release / acq_rel ordered.  The default of
+// any job whose ranks sit on different GPUs (engine/loops.py select_release_form): the relaxed forms
+// are measured only with every rank on one GPU so far.
 __device__ __forceinline__ void block_release_system(bool strict = false) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

@@ -13,16 +13,14 @@
 
 namespace eh {
 
-// ERASUREHEAD_STRICT_RELEASE=1: every put / signal / arbiter release in this process uses the
-// release-ordered forms (common.h block_release_system(strict), publish_u64) and the arbiter polls
-// with acquire loads.  Read once; the launchers stamp it into PutDesc::strict / ArbArgs::strict.
-inline bool strict_release() {
-  static const bool on = [] {
-    const char* e = std::getenv("ERASUREHEAD_STRICT_RELEASE");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on;
-}
+// Release form of every put / signal / arbiter release in this process (transport.hip).  strict: the
+// release-ordered forms (common.h block_release_system(strict), publish_u64) and acquire polls in the
+// arbiter; relaxed: one lane's system fence + relaxed flag stores (measured with ranks on one GPU).
+// The launchers stamp it into PutDesc::strict / ArbArgs::strict at every launch.  STRICT until the
+// job says otherwise: the Trainer picks the form from the ranks' device map before any transport
+// exists (engine/loops.py select_release_form: relaxed only when every rank shares one GPU).
+bool strict_release();
+void set_release_form(bool strict);
 
 // ---- worker gradient (grad_dense.hip, grad_sparse.hip) -------------------------------
 // dtype: 0 fp64 storage/acc, 1 fp32/fp32, 2 bf16 storage/fp32 acc; loss: 0 logistic, 1 least squares

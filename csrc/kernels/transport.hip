@@ -17,6 +17,8 @@
 // Integrity (integrity.h): a tagged descriptor also checksums every row it copies (LDS sums per
 // row, one global add per row and block into the sender's scratch) and the last block writes
 // one {round + 1, rank, checksum} tag per row into the receiver's tag slots before the flag.
+#include <atomic>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -232,6 +234,12 @@ hipError_t ping_pong_launch(const PingArgs& a, bool master, hipStream_t st) {
   hipLaunchKernelGGL(ping_pong, dim3(1), dim3(256), 0, st, a, master ? 1 : 0);
   return hipGetLastError();
 }
+
+namespace {
+std::atomic<int> g_strict_release{1};  // launchers.h: strict until the Trainer chose the job's form
+}  // namespace
+bool strict_release() { return g_strict_release.load(std::memory_order_relaxed) != 0; }
+void set_release_form(bool strict) { g_strict_release.store(strict ? 1 : 0, std::memory_order_relaxed); }
 
 hipError_t put_signal_launch(const PutArgs& args, int blocks, hipStream_t st) {
   if (args.n <= 0) return hipSuccess;

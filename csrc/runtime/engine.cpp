@@ -405,13 +405,12 @@ struct HostMapped {
 
 // Test hook ERASUREHEAD_SABOTAGE=<what>:<rank>:<round> (what: msg | beta): the named put flips one
 // payload byte after its checksum, so the receiver must report a torn message.  ("handshake:<rank>":
-// that rank never answers the IPC handshake, parallel/transport.py.)
+// that rank never answers the IPC handshake, parallel/transport.py.)  Read at every put, so a test can
+// arm it for one Trainer of a process and disarm it before the next (bench.py first-contact ladder).
 bool sabotage(const char* what, int rank, int round) {
-  static const std::string spec = [] {
-    const char* e = std::getenv("ERASUREHEAD_SABOTAGE");
-    return std::string(e ? e : "");
-  }();
-  if (spec.empty()) return false;
+  const char* e = std::getenv("ERASUREHEAD_SABOTAGE");
+  if (e == nullptr || e[0] == '\0') return false;
+  const std::string spec(e);
   return spec == std::string(what) + ":" + std::to_string(rank) + ":" + std::to_string(round);
 }
 
@@ -717,8 +716,8 @@ class MasterPump {
   void finish_run() {
     if (!skip_) return;
     col_->end_run(eh::Collector::now());
-    if (comm_) {  // p2p: the end-of-run beta(R) to every worker rank (WorkerPump::run_comm_skip's last wait)
-      put_beta_comm(R_);
+    if (comm_) {  // p2p: the end-of-run beta(R) to every message-sending rank (WorkerPump::run_comm_skip's last wait)
+      put_beta_comm(R_, true);
       return;
     }
     for (const auto& t : targets_)
@@ -1356,10 +1355,17 @@ class MasterPump {
 
   // push beta(j) into every worker inbox (put + signal kernels on the pump stream)
   // one send of beta(j) per worker rank, each on its own stream behind the update that wrote it
-  void put_beta_comm(int j) {
+  // senders_only: only the ranks that send messages -- the end-of-run beta(R) goes to the WorkerPumps
+  // with stale-round skipping (set_skip_stale_comm) and nowhere else: a rank hosting no message runs
+  // the Python worker loop, which receives beta(0..R-1) only, and an unmatched send could hold the
+  // pump's stream (comm.h: a send blocks until the peer's matching call).
+  void put_beta_comm(int j, bool senders_only = false) {
     const void* src = static_cast<const char*>(beta_in_.data_ptr()) + static_cast<int64_t>(j) * ld_ * es_;
     hcheck(hipEventRecord(bev_, stream_), "hipEventRecord(beta)");
     for (int r : comm_peers_) {
+      if (senders_only && std::none_of(comm_ranks_.begin(), comm_ranks_.end(),
+                                       [r](const auto& c) { return std::get<0>(c) == r && std::get<2>(c) > 0; }))
+        continue;
       hcheck(hipStreamWaitEvent(send_st_.at(r), bev_, 0), "hipStreamWaitEvent(beta)");
       comm_->send(r, src, static_cast<int64_t>(ld_) * es_, send_st_.at(r));
     }

@@ -27,8 +27,9 @@ in a decode, decode tables above 16 workers) come in as ``blocker``: MasterPump.
 from __future__ import annotations
 
 import itertools
+import os
 from dataclasses import dataclass, replace
-from typing import List, Tuple
+from typing import List, Sequence, Tuple
 
 
 @dataclass(frozen=True)
@@ -96,6 +97,35 @@ def select_round_loop(x: LoopInputs) -> Tuple[str, str]:
     return "arbiter", "ranks own their GPUs, IPC counters, no virtual delay, nothing needs the host"
 
 
+def select_release_form(device_map: Sequence[str], override: str = "auto") -> Tuple[str, str]:
+    """(strict | relaxed, reason): the release form of every put, signal and arbiter release of a job
+    whose rank r runs on the GPU ``device_map[r]`` (PCI bus ids; csrc/kernels/launchers.h).
+
+    relaxed -- one lane's system-scope write-back, then relaxed flag / counter stores and relaxed
+    polls (common.h block_release_system, arbiter.hip load_counter): measured correct and faster with
+    every rank on ONE GPU, the only topology it has run on.  strict -- every thread fences at system
+    scope, flags are release stores, block counters acq_rel and the arbiter polls with acquire loads:
+    the default as soon as any two ranks sit on different GPUs (stores cross xGMI), until a multi-GPU
+    record validates the relaxed forms there.  ``override``: ERASUREHEAD_RELEASE=strict|relaxed|auto."""
+    if override in ("strict", "relaxed"):
+        return override, f"ERASUREHEAD_RELEASE={override}"
+    if override not in ("auto", ""):
+        raise ValueError(f"ERASUREHEAD_RELEASE={override!r}: expected strict, relaxed or auto")
+    if len(device_map) <= 1:
+        return "relaxed", "one rank: no put or flag crosses a process"
+    if len(set(device_map)) == 1:
+        return "relaxed", "every rank time-shares one GPU (the topology the relaxed forms are measured on)"
+    n = len(set(device_map))
+    return "strict", (f"ranks on {n} different GPUs: puts and flags cross xGMI, where the relaxed forms have "
+                      f"not run yet (ERASUREHEAD_RELEASE=relaxed opts in)")
+
+
+def release_override(environ=None) -> str:
+    """The job's release-form override from the environment (select_release_form)."""
+    environ = os.environ if environ is None else environ
+    return environ.get("ERASUREHEAD_RELEASE", "auto").strip().lower() or "auto"
+
+
 def worker_loop(master_loop: str) -> str:
     """The worker ranks' executor for a master loop."""
     return "python" if master_loop == "python" else "native pump"
@@ -153,4 +183,5 @@ def describe(x: LoopInputs) -> dict:
     return {"master": loop, "workers": worker_loop(loop), "reason": why}
 
 
-__all__ = ["LoopInputs", "select_round_loop", "worker_loop", "loop_table", "loop_table_markdown", "describe", "replace"]
+__all__ = ["LoopInputs", "select_round_loop", "select_release_form", "release_override", "worker_loop", "loop_table",
+           "loop_table_markdown", "describe", "replace"]

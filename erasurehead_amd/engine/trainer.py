@@ -45,7 +45,7 @@ import numpy as np
 import torch
 
 from .._ext import native as native_ext
-from .loops import LoopInputs, select_round_loop
+from .loops import LoopInputs, release_override, select_release_form, select_round_loop
 from ..codes.schemes import Arrival, Scheme, SchemeError, make_scheme, scheme_key
 from ..config import RunConfig
 from ..data import io as dio
@@ -88,12 +88,18 @@ class TrainResult:
     arrivals: List[List[Tuple[int, int, float]]] = field(default_factory=list)
 
 
+class ContainedFailure(RuntimeError):
+    """A rank's round loop failed, and the rank has since drained its device and joined the run's
+    closing barrier (Trainer.run(contain=True)): the job is collectively consistent again."""
+
+
 def _sabotage_exit(rank: int) -> Optional[Tuple[str, int]]:
-    """Test hook ERASUREHEAD_SABOTAGE=exit:<rank>:<round> (that worker rank exits before that round)
-    or hang:<rank>:<round> (it stops there and never sends again, alive until the job is torn down)."""
+    """Test hook ERASUREHEAD_SABOTAGE=exit:<rank>:<round> (that worker rank exits before that round),
+    hang:<rank>:<round> (it stops there and never sends again, alive until the job is torn down) or
+    raise:<rank>:<round> (its round loop raises there: Trainer.run(contain=True) must contain it)."""
     spec = os.environ.get("ERASUREHEAD_SABOTAGE", "")
     parts = spec.split(":")
-    if len(parts) == 3 and parts[0] in ("exit", "hang") and int(parts[1]) == rank:
+    if len(parts) == 3 and parts[0] in ("exit", "hang", "raise") and int(parts[1]) == rank:
         return parts[0], int(parts[2])
     return None
 
@@ -267,6 +273,7 @@ class Trainer:
         self.G = torch.zeros((self.K, max(1, n_loc), ld), dtype=acc, device=dev)
         self.n_loc = n_loc
         remote_counts = {r: len(v) for r, v in self.remote_msgs.items() if v} if env.is_master else {}
+        self._choose_release_form()  # before the transport: its handshake puts already use the form
         self.tx = make_transport(cfg.transport, env, R, self.K, ld, acc, n_loc, remote_counts, cfg.round_timeout) \
             if env.world > 1 else None
         if env.is_master:
@@ -285,6 +292,27 @@ class Trainer:
             self.loc_ev = [torch.cuda.Event() for _ in range(self.K)]
             if env.is_master:
                 self.upd_ev = torch.cuda.Event()
+
+    def _choose_release_form(self) -> None:
+        """Collective on GPU ranks: gather every rank's GPU (PCI bus id) and set this process's release
+        form for every later put / signal / arbiter launch (engine/loops.py select_release_form; the
+        native default is strict).  ERASUREHEAD_FAKE_DEVICE_MAP=<id>,<id>,... (one per rank) stands in
+        for the bus ids, so a one-GPU box can exercise the cross-device selection."""
+        env = self.env
+        self.device_map: List[str] = []
+        self.release_form, self.release_reason = "n/a", "CPU ranks: no device puts"
+        if not env.gpu:
+            return
+        C = native_ext()
+        dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
+        mine = C.pci_bus_id(dev)
+        buses = env.broadcast_object(env.gather_objects(mine), 0) if env.world > 1 else [mine]
+        fake = [x.strip() for x in os.environ.get("ERASUREHEAD_FAKE_DEVICE_MAP", "").split(",") if x.strip()]
+        if fake and len(fake) == env.world:
+            buses = [f"fake:{x}" for x in fake]
+        self.device_map = list(buses)
+        self.release_form, self.release_reason = select_release_form(self.device_map, release_override())
+        C.set_release_form(self.release_form == "strict")
 
     def preflight(self, iters: int = 1000) -> Optional[List[dict]]:
         """Collective: per-pair put -> flag round trips over the IPC mailbox (IpcTransport.preflight);
@@ -375,11 +403,17 @@ class Trainer:
         return 1e6 * (time.perf_counter() - t0) / reps
 
     # ------------------------------------------------------------------------------ run
-    def run(self, timed_start: Optional[int] = None, log=None) -> Optional[TrainResult]:
+    def run(self, timed_start: Optional[int] = None, log=None, contain: bool = False) -> Optional[TrainResult]:
         """Train for cfg.num_itrs rounds; returns the master's TrainResult (None on workers).
 
         timed_start: if set, all ranks synchronise (device sync + barrier) before that round
         and after the last one, and the result carries the timed wall-clock (bench.py).
+        contain: a failure inside the round loop (a timeout, an integrity-tag verdict, a device
+        round that did not decode) does not leave the job split across collectives: the failing
+        rank drains its device (bounded), joins the barriers its loop had not reached yet (the timed
+        fences and the closing barrier, counted), and raises :class:`ContainedFailure`.  Every rank
+        then stands at the same point, so the caller can agree on a verdict (:meth:`run_contained`)
+        and rebuild.  Not with cfg.verify_beta (its gather sits between the loops' barriers).
         """
         log = log or report.log
         cfg, env = self.cfg, self.env
@@ -396,23 +430,75 @@ class Trainer:
         env.barrier()
         self.loop, self.loop_reason = select_round_loop(self.loop_inputs(start))
         native_loop = self.native_loop
-        if self.skip_stale and not native_loop and self.tx is not None and self.tx.name in P2P_TRANSPORTS:
+        if self.skip_stale and self.loop == "python" and self.tx is not None and self.tx.name in P2P_TRANSPORTS:
             # the Python round loop receives beta in stream order (no look-ahead), so a p2p worker cannot
-            # tell that a round is stale before computing it: lazy runs as carry there, and says so
-            why = f"drain lazy runs as carry in the Python round loop over {self.tx.name} (no stale-round skipping)"
+            # tell that a round is stale before computing it: the run switches to the carry drain -- the
+            # master's collector included, so the books and the rank report say what ran
+            why = (f"drain lazy -> carry: in the Python round loop over {self.tx.name} the workers cannot skip "
+                   f"stale rounds (beta arrives in stream order, no look-ahead)")
             if env.is_master:
                 print(f"[erasurehead] WARNING: {why}", file=sys.stderr, flush=True)
             self.rank_stats["drain_downgraded"] = why
+            self.drain_mode, self.skip_stale = "carry", False
+        self._coll_done = 0
+        contain = contain and not cfg.verify_beta
         try:
             if env.is_master:
                 res = (self._master_loop_native if native_loop else self._master_loop)(timed_start, log, start)
             else:
                 res = (self._worker_loop_native if native_loop else self._worker_loop)(timed_start, start)
-        except BaseException:
+        except BaseException as e:
             if self.tx is not None:  # release queued p2p work on peers that will not answer
                 self.tx.abort()
+            if contain and isinstance(e, Exception) and not isinstance(e, ContainedFailure):
+                self._contain_failure(e, self._loop_collectives(timed_start, start) - self._coll_done)
+                raise ContainedFailure(f"rank {env.rank}: {type(e).__name__}: {e}") from e
             raise
         return res
+
+    def _contain_failure(self, e: Exception, barriers: int, drain_s: float = 60.0) -> None:
+        """run(contain=True) after a failure inside a round loop: wait (bounded) for this rank's device
+        work to drain -- the pumps have released their queued waits (WorkerPump stop_queued, the
+        arbiter's abort word) -- then call the ``barriers`` barriers the loop had left.  A device that
+        does not drain cannot be recovered in this process: the original error is re-raised unchanged."""
+        import threading
+
+        print(f"[erasurehead] rank {self.env.rank}: round loop failed ({type(e).__name__}: {str(e)[:300]}); "
+              f"draining the device and joining the closing barrier", file=sys.stderr, flush=True)
+        if self.env.gpu:
+            done = threading.Event()
+
+            def drain():
+                torch.cuda.synchronize(self.env.device)
+                done.set()
+
+            threading.Thread(target=drain, name="eh-contain-drain", daemon=True).start()
+            if not done.wait(drain_s):
+                raise e
+        for _ in range(max(0, barriers)):
+            self.env.barrier()
+
+    def run_contained(self, timed_start: Optional[int] = None, log=None) -> Tuple[Optional[TrainResult], Optional[str]]:
+        """Collective.  run(contain=True) on every rank, then one verdict every rank agrees on:
+        (result, None) after a clean run (result None on workers), or (None, reasons) when any rank's
+        round loop failed -- the reasons of every failing rank, joined."""
+        res, err = None, None
+        try:
+            res = self.run(timed_start, log, contain=True)
+        except ContainedFailure as e:
+            err = str(e)
+        if self.env.world > 1:
+            errs = self.env.gather_objects(err)
+            verdict = self.env.broadcast_object("; ".join(x for x in errs if x) if self.env.is_master else None, 0)
+        else:
+            verdict = err
+        if verdict:
+            return None, verdict
+        if res is not None and not bool(np.all(np.isfinite(res.betaset))):
+            verdict = "the trajectory has non-finite entries"
+        if self.env.world > 1:
+            verdict = self.env.broadcast_object(verdict if self.env.is_master else None, 0)
+        return (None, verdict) if verdict else (res, None)
 
     def loop_inputs(self, start: int = 0, blocker: str = "") -> LoopInputs:
         """This run's facts for engine/loops.py select_round_loop (the same on every rank)."""
@@ -476,8 +562,23 @@ class Trainer:
 
     def _timed_fence(self):
         self._sync()
+        self._coll_done += 1
         self.env.barrier()
         return time.perf_counter()
+
+    def _closing_barrier(self):
+        """The barrier every round loop ends with (counted: run(contain=True) replays what is left)."""
+        self._coll_done += 1
+        self.env.barrier()
+
+    def _loop_collectives(self, timed_start: Optional[int], start: int) -> int:
+        """Barriers a round loop calls on its success path, in order: the timed fences around the timed
+        rounds (the opening one only when the timed start is inside the run) and the closing barrier.
+        The same count on every rank and in every loop (the race check's gather is outside contain)."""
+        n = 1
+        if timed_start is not None:
+            n += 1 + int(start <= timed_start < self.cfg.num_itrs)
+        return n
 
     def _master_loop(self, timed_start, log, start: int = 0) -> TrainResult:
         cfg, env, sch = self.cfg, self.env, self.scheme
@@ -486,6 +587,8 @@ class Trainer:
         col = ArrivalCollector(W, sch.group_of, sch.n_groups, env.gpu, cfg.tie_seed_value)
         col.set_shards(self.n_shards)
         col.set_skip_stale(self.skip_stale)
+        if self.tx is not None and hasattr(self.tx, "check_queue_budget") and env.gpu:
+            self.rank_stats.update(self.tx.check_queue_budget(len(self.tx.ps)))  # its per-peer streams
         timeset = np.zeros(R)
         loop_time = np.zeros(R)
         worker_timeset = np.zeros((R, W))
@@ -588,7 +691,7 @@ class Trainer:
             for i, ev0, ev1 in upd_events:  # + the update kernel's own duration (reference: decode + update)
                 timeset[i] += 1e-3 * ev0.elapsed_time(ev1)
         self._sync()
-        env.barrier()
+        self._closing_barrier()
         total = time.perf_counter() - orig_start
         a0 = (timed_start or start) - start
         self.rank_stats.update({f"{k}_us": float(1e6 * np.mean(v[a0:])) for k, v in self.timer.t.items()
@@ -617,6 +720,7 @@ class Trainer:
                                   "round_loop": self.device_loop or ("native pump" if self.native_loop else "python"),
                                   "loop_reason": getattr(self, "loop_reason", None),
                                   "drain": self.drain_mode,
+                                  "release_form": getattr(self, "release_form", None),
                                   "replicas": self.replica_policy,
                                   "workers": sorted({int(m.worker) for m in self.local_msgs}),
                                   "messages": len(self.local_msgs),
@@ -837,7 +941,7 @@ class Trainer:
                                   for k, v in self.timer.t.items() if len(v) > a0 - start})
         col.close()
         self._sync()
-        env.barrier()
+        self._closing_barrier()
         total = time.perf_counter() - orig_start
         res = TrainResult(self.key, self.hist[:, : self.d].double().cpu().numpy(), timeset, worker_timeset, loop_time,
                           total, timeouts=timeouts, phases=self.timer.summary(), arrivals=arrivals_log)
@@ -897,15 +1001,17 @@ class Trainer:
         if self.skip_stale and tx.name == "ipc" and self.n_loc:  # stale-round gates read the beta counter
             pump.set_skip_stale(tx.flags.dev_addr(env.rank))
         elif self.skip_stale and tx.name != "ipc":  # p2p: beta received a round ahead, gates from its counter;
-            pump.set_skip_stale_comm()  # every rank, the end-of-run beta(R) goes to all of them
+            pump.set_skip_stale_comm()  # the end-of-run beta(R) goes to every rank that sends messages
         self.rank_stats["fused_put"] = bool(pump.fused_put)
         self.rank_stats["device_wait"] = bool(pump.device_wait)
         cut = timed_start if timed_start is not None and start <= timed_start < R else None
         segments = [(start, cut), (cut, R)] if cut is not None else [(start, R)]
-        gone = _sabotage_exit(env.rank)  # test hook: this worker rank dies / hangs after that round
+        gone = _sabotage_exit(env.rank)  # test hook: this worker rank dies / hangs / fails after that round
         if gone is not None:
             pump.run(start, min(R, gone[1]))
             torch.cuda.synchronize(env.device)
+            if gone[0] == "raise":
+                raise RuntimeError(f"test hook: rank {env.rank} fails at round {gone[1]}")
             if gone[0] == "exit":
                 os._exit(0)
             while True:  # silent from here on: the master's drain must give up on it
@@ -930,7 +1036,7 @@ class Trainer:
         if cfg.instrument:
             self.rank_stats.update(kernel_us=_mean_us(ker_ms, a0), msg_put_us=_mean_us(put_ms, a0))
         try:
-            env.barrier()
+            self._closing_barrier()
         except RuntimeError as e:  # a peer rank is gone (gloo: connection reset): this rank's rounds are done,
             # the master names the lost messages and fails the run (its final drain times out)
             print(f"rank {env.rank}: final barrier failed, a peer rank is gone ({e}); "
@@ -980,7 +1086,10 @@ class Trainer:
         t0 = None
         bsum = torch.full((R, 2), float("nan"), dtype=torch.float64, device=env.device) if cfg.verify_beta else None
         self.skipped_rounds = []
+        gone = _sabotage_exit(env.rank)
         for i in range(start, R):
+            if gone is not None and gone[0] == "raise" and i == gone[1]:
+                raise RuntimeError(f"test hook: rank {env.rank} fails at round {i}")
             if timed_start is not None and i == timed_start:
                 t0 = self._timed_fence()
             slot = i % K
@@ -1014,7 +1123,7 @@ class Trainer:
         self.rank_stats.update({f"{k}_us": float(1e6 * np.mean(v[a0:])) for k, v in self.timer.t.items()
                                 if len(v) > a0})
         self._sync()
-        env.barrier()
+        self._closing_barrier()
         return None
 
     def close(self) -> None:

@@ -764,15 +764,18 @@ class SparseGradPlan:
         ptr, idx, coef = self._enc
         # identity encoding (naive: message i is distinct partition i with coefficient 1, no sub-blocks):
         # the column pass writes the messages themselves, no Gb and no encode launch (amazon-shaped
-        # naive: 15.5 MB read + 15.5 MB written per round).  The pass never writes a column that is empty
-        # in its partition, so those stay as the caller's G holds them: zero in every buffer the plans
-        # and the trainer allocate (out_buffer, the trainer's G ring).
+        # naive: 15.5 MB read + 15.5 MB written per round).  Two kinds of G columns are then never
+        # written: the columns empty in a partition (native_launcher hands the kernels no empty-column
+        # list) and the padding columns [d, ld).  Both stay as the caller's G holds them, so an identity
+        # plan needs a G that is zero there -- every buffer the plans and the trainer allocate is
+        # (out_buffer, the trainer's G ring); run() checks it the first time it sees a buffer.
         self.identity = (not blocked and len(self.messages) == len(self.basis)
                          and all(m == [(self.basis[i], 1.0)] for i, m in enumerate(self.messages)))
         self.enc_ptr = torch.tensor(ptr, dtype=torch.int32, device=dev)
         self.enc_idx = torch.tensor(idx or [0], dtype=torch.int32, device=dev)[: len(idx)]
         self.enc_coef = torch.tensor(coef or [0.0], dtype=torch.float64, device=dev)[: len(coef)]
         self._launcher = None
+        self._zero_checked = set()  # G buffers run() has seen zero in the padding columns
 
     @staticmethod
     def csc_tables(blocks, d: int, tile: int = 512, row_block: int = 0, wg_tiles: int = 16,
@@ -973,9 +976,15 @@ class SparseGradPlan:
         return int(n + 2 * self.u.numel() * self.u.element_size())
 
     def run(self, beta: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
+        """G [nslots, ld]: the messages.  An identity plan (see _build_device) leaves the columns empty
+        in a partition and the padding columns [d, ld) as G holds them: pass a G that is zero there."""
         if G.shape != (self.nslots, self.ld):
             raise ValueError(f"G must be [{self.nslots}, {self.ld}]")
         if self.device.type == "cuda":
+            if self.identity and self.ld > self.d and G.data_ptr() not in self._zero_checked:
+                if bool((G[:, self.d:] != 0).any()):  # once per buffer (a host sync), off the round path
+                    raise ValueError("identity sparse plan: G's padding columns [d, ld) must be zero")
+                self._zero_checked.add(G.data_ptr())
             self.native_launcher().launch(beta, G)
             return G
         b = beta.detach().cpu().double().numpy()[: self.d]

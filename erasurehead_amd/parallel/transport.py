@@ -122,21 +122,28 @@ class Transport:
 # ===================================================================================== gloo
 class GlooTransport(Transport):
     name = "gloo"
+    _generation = 0  # transports built so far in this process (every rank builds them in the same order)
 
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
         self._sends: List[List] = [[] for _ in range(self.K)]
         self.bbuf = torch.zeros((2, self.ld), dtype=self.dtype)
+        # Tags of this transport live above every earlier transport's: a send or receive a failed run
+        # left pending on the process group (Trainer.run_contained) can never match a later run's.
+        GlooTransport._generation += 1
+        self.tag0 = 2 * TAG_STRIDE * (self.R + 1) * (GlooTransport._generation - 1)
+        if self.tag0 + 2 * TAG_STRIDE * (self.R + 1) >= 2 ** 31:
+            GlooTransport._generation, self.tag0 = 1, 0
 
     def send_beta(self, i, beta):
         for r in range(1, self.env.world):
-            self._sends[i % self.K].append(dist.isend(beta, r, tag=_tag_beta(i)))
+            self._sends[i % self.K].append(dist.isend(beta, r, tag=self.tag0 + _tag_beta(i)))
 
     def post_recvs(self, i, slot, col, rbuf, msgs_by_rank, delays, physical=False):
         for r in sorted(msgs_by_rank):
             for jj, m in enumerate(msgs_by_rank[r]):
                 j = self.row0[r] + jj
-                w = dist.irecv(rbuf[slot, j], r, tag=_tag_msg(i, jj))
+                w = dist.irecv(rbuf[slot, j], r, tag=self.tag0 + _tag_msg(i, jj))
                 col.add_work(m.worker, m.part, i, w, delays[m.worker], src=r, physical=physical)
 
     def recv_beta(self, i):
@@ -145,12 +152,13 @@ class GlooTransport(Transport):
             w.wait()
         self._sends[slot] = []
         b = self.bbuf[i % 2]
-        dist.irecv(b, 0, tag=_tag_beta(i)).wait()
+        dist.irecv(b, 0, tag=self.tag0 + _tag_beta(i)).wait()
         self._cur = i
         return b
 
     def send_msgs(self, i, G_slot):
-        self._sends[i % self.K] = [dist.isend(G_slot[j], 0, tag=_tag_msg(i, j)) for j in range(G_slot.shape[0])]
+        self._sends[i % self.K] = [dist.isend(G_slot[j], 0, tag=self.tag0 + _tag_msg(i, j))
+                                   for j in range(G_slot.shape[0])]
 
     def finish(self):
         for lst in self._sends:
@@ -442,7 +450,7 @@ class IpcTransport(Transport):
 
     name = "ipc"
     FINE = True  # mailboxes in fine-grained (coherent) device memory
-    HANDSHAKE_TIMEOUT = float(os.environ.get("ERASUREHEAD_HANDSHAKE_TIMEOUT", "30"))  # whole setup handshake
+    HANDSHAKE_TIMEOUT = 30.0  # whole setup handshake, at most (a run's round timeout can shorten it)
 
     def __init__(self, *a, timeout: float = 600.0, **kw):
         super().__init__(*a, **kw)
@@ -451,6 +459,7 @@ class IpcTransport(Transport):
         self.C = C = native()
         env = self.env
         self.timeout = timeout
+        self.HANDSHAKE_TIMEOUT = min(self.HANDSHAKE_TIMEOUT, max(5.0, float(timeout)))  # 5..30 s
         self.dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
         self.es = torch.tensor([], dtype=self.dtype).element_size()
         dname = {torch.float64: "float64", torch.float32: "float32"}[self.dtype]

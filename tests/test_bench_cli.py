@@ -57,6 +57,11 @@ def test_bench_gpus3_relaunches_three_ranks(tmp_path):
     assert st["agc_lazy"]["drain"] == "lazy" and st["naive"]["drain"] == "carry"
     assert st["naive"]["round_ms_mean"] >= 5.0  # naive waits for the late rank every round
     assert st["agc_lazy_round_slowdown"] > 0 and st["naive_round_slowdown"] > 1.0
+    # first contact (bench.first_contact): a bounded check run on the headline's loop before timing
+    fc = d["first_contact"]
+    assert fc["rounds"] == 30 and [x["ok"] for x in fc["ladder"]] == [True]
+    assert fc["ladder"][0]["round_loop"] == "python" and fc["transport"] == "gloo"
+    assert d["release_form"] == "n/a" and d["config"]["round_loop_reason"]
 
 
 def test_bench_one_gpu_straggler_block(tmp_path):
@@ -141,4 +146,52 @@ def test_bench_preflight_failure_rebuilds_on_comm_path(tmp_path):
     fp = d["fallback_preflight"]  # the fallback was checked over its own path before timing
     assert [x["rank"] for x in fp] == [1] and fp[0]["payload_errors"] == 0 and fp[0]["path"] == "loopback"
     assert "same" in d["fallback_mechanism"] or "mailbox" in d["fallback_mechanism"]
+    assert d["ms_per_step"] > 0
+
+
+def _gpu_bench(tmp_path, name, extra_env, *args):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", **extra_env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = tmp_path / name
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *TINY, "--no-floor",
+                        "--no-straggler", "--preflight", "50", "--json-out", str(out), *args],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return json.loads(out.read_text())
+
+
+@pytest.mark.gpu
+def test_bench_first_contact_cross_device_selection(tmp_path):
+    """The first 8-GPU run's path, forced on the one-GPU box: a faked device map (two GPUs) selects the
+    strict release forms, the arbiter runs (ERASUREHEAD_DEVICE_MASTER=on) and checks itself with
+    integrity-tagged rounds before timing; the JSON carries the release form, the loop and why, the
+    device map and the per-pair preflight round trips."""
+    d = _gpu_bench(tmp_path, "x.json", dict(ERASUREHEAD_DEVICE_MASTER="on", ERASUREHEAD_FAKE_DEVICE_MAP="g0,g1"))
+    assert d["release_form"] == "strict" and "different GPUs" in d["release_reason"]
+    assert d["device_map"] == {"0": "fake:g0", "1": "fake:g1"}
+    fc = d["first_contact"]
+    assert [(x["round_loop"], x["ok"]) for x in fc["ladder"]] == [("arbiter", True)]
+    assert fc["ladder"][0]["release_form"] == "strict" and fc["round_loop"] == "arbiter"
+    assert d["config"]["round_loop"].startswith("device-driven (arbiter") and d["config"]["round_loop_reason"]
+    assert [x["rank"] for x in d["peer_preflight"]] == [1] and d["peer_preflight"][0]["rtt_us_p50"] > 0
+    assert all(x["release_form"] == "strict" for x in d["ranks"])
+    assert d["ms_per_step"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_first_contact_steps_down_on_integrity_failure(tmp_path):
+    """A torn message in the first-contact check (rank 1's put of round 3 flips a byte after its
+    checksum, for that check run only): the arbiter's integrity check fails the round, every rank
+    agrees on the verdict, the job steps down to the native pump in the same processes, checks that,
+    and times the headline on it -- the JSON says what failed and what ran."""
+    d = _gpu_bench(tmp_path, "s.json", dict(ERASUREHEAD_DEVICE_MASTER="on", ERASUREHEAD_FAKE_DEVICE_MAP="g0,g1",
+                                           ERASUREHEAD_SABOTAGE="firstcontact:msg:1:3"), "--selfcheck-timeout", "4",
+                   "--naive")  # naive: every message enters the decode, so the torn rows are read
+    fc = d["first_contact"]
+    lad = fc["ladder"]
+    assert [(x["round_loop"], x["ok"]) for x in lad] == [("arbiter", False), ("native pump", True)], lad
+    assert "rank" in lad[0]["failure"] and "arbiter -> native pump" in lad[0]["step_down"]
+    assert fc["round_loop"] == "native pump"
+    assert d["config"]["round_loop"] == "host-driven (native pump)"
     assert d["ms_per_step"] > 0

@@ -60,3 +60,32 @@ def test_readme_loop_table_is_generated():
     with open(os.path.join(ROOT, "README.md")) as f:
         text = f.read()
     assert loop_table_markdown() in text
+
+
+@pytest.mark.parametrize("device_map,override,form", [
+    (["0000:05:00.0"], "auto", "relaxed"),                                   # one rank
+    (["0000:05:00.0"] * 8, "auto", "relaxed"),                               # 8 ranks time-share one GPU
+    (["0000:05:00.0", "0000:15:00.0"], "auto", "strict"),                    # two GPUs: xGMI
+    ([f"0000:{b:02x}:00.0" for b in (5, 0x15, 0x65, 0x75, 0x85, 0x95, 0xe5, 0xf5)], "auto", "strict"),  # a node
+    (["a", "a", "b"], "auto", "strict"),                                     # any pair across devices
+    (["0000:05:00.0", "0000:15:00.0"], "relaxed", "relaxed"),                # explicit opt-in only
+    (["0000:05:00.0"] * 4, "strict", "strict"),
+])
+def test_release_form_from_device_map(device_map, override, form):
+    """Round-5 verdict, first item: the strict release / acquire forms are the default whenever any two
+    ranks sit on different GPUs; relaxed stays for ranks sharing one GPU (where it is measured) and is
+    otherwise an explicit opt-in (ERASUREHEAD_RELEASE=relaxed)."""
+    from erasurehead_amd.engine.loops import select_release_form
+
+    got, why = select_release_form(device_map, override)
+    assert got == form and why
+
+
+def test_release_override_from_environment():
+    from erasurehead_amd.engine.loops import release_override, select_release_form
+
+    assert release_override({}) == "auto"
+    assert release_override({"ERASUREHEAD_RELEASE": "Relaxed"}) == "relaxed"
+    assert release_override({"ERASUREHEAD_RELEASE": " STRICT"}) == "strict"
+    with pytest.raises(ValueError):
+        select_release_form(["a", "b"], "fast")

@@ -112,13 +112,13 @@ def test_device_arbiter_rounds(world, case_i, wait, drain, tmp_path):
 
 @pytest.mark.parametrize("master", ["on", "off"])
 def test_strict_release_forms(master, tmp_path):
-    """ERASUREHEAD_STRICT_RELEASE=1 (launchers.h strict_release): every put, signal and arbiter release
+    """ERASUREHEAD_RELEASE=strict (launchers.h strict_release): every put, signal and arbiter release
     in the job uses the release-ordered stores and acquire polls of before round 4, the switch for a
     first cross-GPU node; 3 integrity-tagged ranks on the arbiter and on the host pump replay exactly."""
     from oracle import replay
     from test_engine_cpu import CASES, make
 
-    r = _launch(3, 4, "AGD", str(tmp_path / "s.npz"), ERASUREHEAD_STRICT_RELEASE="1", ERASUREHEAD_DEVICE_MASTER=master,
+    r = _launch(3, 4, "AGD", str(tmp_path / "s.npz"), ERASUREHEAD_RELEASE="strict", ERASUREHEAD_DEVICE_MASTER=master,
                 ERASUREHEAD_WORKER_WAIT="device", EH_TEST_ROUND_TIMEOUT="20")
     assert str(r["transport"]) == "ipc"
     assert (str(r["round_loop"]) == "arbiter") == (master == "on")
@@ -198,7 +198,7 @@ def test_ipc_handshake_failure_names_pair_and_step(tmp_path, monkeypatch):
     naming the pair and the step instead of training on garbage or hanging."""
     monkeypatch.setenv("ERASUREHEAD_TRANSPORT", "ipc")
     monkeypatch.setenv("ERASUREHEAD_SABOTAGE", "handshake:1")
-    monkeypatch.setenv("ERASUREHEAD_HANDSHAKE_TIMEOUT", "3")
+    monkeypatch.setenv("EH_TEST_ROUND_TIMEOUT", "3")  # the handshake waits at most the run's round timeout
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(HERE, "mp_engine_run.py"),
@@ -323,3 +323,27 @@ def test_loopback_dead_worker_teardown_finishes(tmp_path):
     assert time.time() - t0 < 300
     err = r.stdout + r.stderr
     assert "messages never arrived; aborting the transport" in err, err[-3000:]
+
+
+def test_loopback_lazy_with_ranks_hosting_no_message(tmp_path):
+    """over stream-ordered p2p with the lazy drain, the master's end-of-run beta(R) goes only
+    to the ranks that send messages (their WorkerPumps wait for it); ranks hosting no logical worker
+    run the Python worker loop, which receives beta(0..R-1) only, so an end-of-run send to them would
+    stay unmatched.  AGC W=6 on 8 ranks (workers on ranks 0-5, ranks 6 and 7 idle) completes and
+    replays through the oracle."""
+    import json
+
+    from oracle import replay
+    from test_engine_cpu import CASES, make
+
+    over = dict(shard="message", drain="lazy", round_timeout=20.0)
+    r = _launch(8, 4, "AGD", str(tmp_path / "i.npz"), ERASUREHEAD_TRANSPORT="loopback", EH_TEST_CFG=json.dumps(over))
+    assert str(r["transport"]) == "loopback"
+    owner = json.loads(str(r["owner"]))
+    assert sorted(set(owner.values())) == [0, 1, 2, 3, 4, 5]
+    reps = json.loads(str(r["reports"]))
+    assert [x["messages"] for x in reps][6:] == [0, 0] and all(x["drain"] == "lazy" for x in reps)
+    cfg, src, sch, parts = make(CASES[4], "AGD")
+    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)

@@ -149,6 +149,9 @@ for s in "${STAGES[@]}"; do
           done
         done
       done ;;
+    release)  # what the strict release forms cost per round: 2 and 8 ranks on this GPU, arbiter on, auto vs strict
+      run 900 release.log env TAG=_rel NO_BF16=1 MODES=on RELEASE="auto strict" bash tools/probes/overhead_tiny.sh
+      cp -r gpurun_out/overhead_rel "$OUT/" ;;
     overhead)  # per-round chain on a tiny problem (tools/probes/overhead_tiny.sh), 2 and 8 ranks, arbiter on,
                # slab reduction forms 1 (fused put) and 2 (two-stage put)
       run 900 overhead.log env TAG=_r4 NO_BF16=1 MODES=on SLAB="1 2" bash tools/probes/overhead_tiny.sh

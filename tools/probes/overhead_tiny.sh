@@ -2,6 +2,7 @@
 # so the round time is mostly messaging + arbiter / host pump; 2 and 8 ranks, arbiter off / on.
 #   gpurun -- bash tools/probes/overhead_tiny.sh   (writes gpurun_out/overhead${TAG}/)
 #   RANKS="2 8" MODES="on off" SLAB="1 2" (slab reduction forms to A/B: bench.py --slab-mode)
+#   RELEASE="auto strict relaxed" (ERASUREHEAD_RELEASE: ranks sharing one GPU select relaxed by default)
 set -o pipefail
 O=gpurun_out/overhead${TAG:-}
 mkdir -p $O
@@ -12,10 +13,13 @@ fi
 for n in ${RANKS:-2 8}; do
   for m in ${MODES:-off on}; do
     for sm in ${SLAB:-1}; do
-      ERASUREHEAD_DEVICE_MASTER=$m timeout -k 10 300 python -u bench.py --gpus $n --steps 200 --warmup 20 --no-floor \
-        --no-straggler --slab-mode $sm --n-rows ${NROWS:-16000} --n-cols 1000 --json-out $O/tiny_${n}_${m}_s$sm.json \
-        > $O/tiny_${n}_${m}_s$sm.log 2>&1 || exit 1
-      echo "tiny $n $m slab $sm done"
+      for rel in ${RELEASE:-auto}; do
+        t=tiny_${n}_${m}_s$sm; [ "$rel" = auto ] || t=${t}_$rel
+        ERASUREHEAD_RELEASE=$rel ERASUREHEAD_DEVICE_MASTER=$m timeout -k 10 300 python -u bench.py --gpus $n --steps 200 \
+          --warmup 20 --no-floor --no-straggler --slab-mode $sm --n-rows ${NROWS:-16000} --n-cols 1000 \
+          --json-out $O/$t.json > $O/$t.log 2>&1 || exit 1
+        echo "tiny $n $m slab $sm release $rel done"
+      done
     done
   done
 done
