@@ -94,6 +94,8 @@ def parse(argv=None):
                     help="N > 1: integrity-tagged rounds on the headline's executor before timing (first_contact)")
     ap.add_argument("--selfcheck-timeout", type=float, default=10.0,
                     help="first_contact: round timeout of the check run (worker beta waits: 2.5x + 5 s)")
+    ap.add_argument("--no-single-ref", dest="single_ref", action="store_false",
+                    help="N > 1: skip rank 0's single-GPU run of the same config (the scaling denominator)")
     ap.add_argument("--share-partitions", action="store_true",
                     help="co-located workers stream each distinct partition once (not the headline)")
     ap.add_argument("--drain", default=None, choices=["all", "carry", "lazy"],
@@ -297,6 +299,7 @@ def main(argv=None) -> int:
             out["hbm_distinct_TBps"] = out["x_distinct_bytes_rank0"] / sec_per_iter / 1e12
         out["fraction_of_rows_used_in_decode"] = decode_row_fraction(sch, res.arrivals[w0:], Arrival)
     reports = env.gather_objects(trainer.rank_report())
+    trainer_shard = trainer.shard_mode
     kernel_iso = None
     for r in range(env.world):  # one rank at a time: ranks may share a GPU (rehearsals)
         if r == env.rank and trainer.local_msgs:
@@ -343,27 +346,27 @@ def main(argv=None) -> int:
         keys = ("rank", "workers", "round_loop", "kernel_us", "wait_k_us", "beta_wait_us", "stale_rounds_skipped",
                 "stale_arrivals", "stale_skipped_virtual", "arbiter_poll_us")
 
-        def sub_run(naive: bool, late: bool, **kw):
+        def sub_run(naive: bool, late: bool, warm: int = a.warmup, steps: int = S, **kw):
             extra = dict(shard="message", drain=kw.pop("drain", None), **kw)
             if late:
                 extra.update(add_delay=1, delay_mode="fixed", delay_on="worker", fixed_sleep=a.late_ms / 1e3,
                              fixed_stragglers=[w + 1 for w in late_workers], force_delay=True)
             else:
                 extra.update(add_delay=0)
-            tr_s = Trainer(make_cfg(a.warmup + S, naive=naive, **extra), env)
-            r_s = tr_s.run(timed_start=a.warmup)
+            tr_s = Trainer(make_cfg(warm + steps, naive=naive, **extra), env)
+            r_s = tr_s.run(timed_start=warm)
             t_s = env.allreduce_max(r_s.timed_seconds if env.is_master else tr_s.worker_timed_seconds)
             reps = env.gather_objects(tr_s.rank_report())
             rec = None
             if env.is_master:
-                lt = np.asarray(r_s.loop_time[a.warmup:])
-                rec = {"ms_per_step": 1e3 * t_s / S, "round_ms_mean": float(1e3 * np.mean(lt)),
+                lt = np.asarray(r_s.loop_time[warm:])
+                rec = {"ms_per_step": 1e3 * t_s / steps, "steps": steps, "round_ms_mean": float(1e3 * np.mean(lt)),
                        "round_ms_median": float(1e3 * np.median(lt)), "drain": tr_s.drain_mode,
                        "ranks": [{k: x[k] for k in keys if k in x} for x in reps]}
             free(tr_s)
             return rec
 
-        topo = sub_run(a.naive, False)
+        topo = sub_run(a.naive, False, warm=w0, steps=a.steps)  # the headline's warm-up and step count
         straggler = {
             "late_rank": late_rank, "late_workers": late_workers, "late_ms": a.late_ms, "placement": "message",
             "steps": S, "agc_lazy": sub_run(False, True, drain="lazy"),
@@ -372,6 +375,11 @@ def main(argv=None) -> int:
         if env.is_master:
             out["message_placement_ms_per_step"] = topo["ms_per_step"]
             out["message_placement"] = topo
+            # the straggler-tolerant co-headline: the reference topology (one worker's s+1 partitions per
+            # rank, ref run_approx_coding.sh:47-49, src/approximate_coding.py:47-53), where a slow GPU
+            # erases only its own workers -- `value` uses the bandwidth placement (--shard)
+            out["value_tolerant"] = topo["ms_per_step"] / 1e3
+            out["value_tolerant_placement"] = "message"
             for name in ("agc_lazy", "naive"):  # the master's round period: late vs on time
                 straggler[f"{name}_round_slowdown"] = (straggler[name]["round_ms_mean"]
                                                       / straggler[f"{name}_no_straggler"]["round_ms_mean"])
@@ -379,6 +387,19 @@ def main(argv=None) -> int:
                                        "rounds; ms_per_step: fenced wall-clock / steps (includes the late rank's "
                                        "last in-flight round)")
             out["straggler"] = straggler
+
+    # ---- 2c. N > 1: the same problem on rank 0's GPU alone, in this job (the scaling denominator) --------
+    if env.world > 1 and a.single_ref:
+        single = single_gpu_reference(a, make_cfg, env, free, Trainer, clock_rounds)
+        if env.is_master:
+            out["single_gpu_s_per_iter"] = single
+            out["single_gpu_definition"] = ("the headline config on rank 0's GPU alone (world 1, every message "
+                                            "local), timed in this job right after the N-rank runs")
+            out["scaling_efficiency"] = single / (env.world * out["value"])
+            if "value_tolerant" in out:
+                out["scaling_efficiency_tolerant"] = single / (env.world * out["value_tolerant"])
+            out["scaling_placements"] = {"value": f"{trainer_shard} (--shard)",
+                                         "value_tolerant": "message (the reference topology)"}
 
     # ---- 3. convergence: naive (exact GD) sets the common loss target, then the scheme -------------
     if not a.no_floor:
@@ -439,6 +460,27 @@ def main(argv=None) -> int:
                 f.write(line + "\n")
     env.shutdown()
     return 0
+
+
+def single_gpu_reference(a, make_cfg, env, free, Trainer, clock_rounds: int):
+    """N > 1: rank 0 runs the headline configuration by itself (a world-1 Trainer on its own GPU: every
+    message local, the single-process device loop) for --steps timed rounds after the same warm-up,
+    while the other ranks wait at a barrier.  Returns its s/iter on rank 0 (None elsewhere): the
+    denominator of the job's own scaling efficiencies, measured on the same node in the same job."""
+    from erasurehead_amd.parallel.dist import DistEnv
+
+    env.barrier()
+    sec = None
+    if env.is_master:
+        solo = DistEnv(rank=0, world=1, local_rank=env.local_rank, device=env.device, backend="none")
+        w0 = clock_rounds + a.warmup
+        tr = Trainer(make_cfg(w0 + a.steps), solo)
+        r = tr.run(timed_start=w0)
+        sec = r.timed_seconds / a.steps
+        free(tr)
+        del tr, r
+    env.barrier()
+    return sec
 
 
 def step_down(a, env, trainer, why: str) -> str:

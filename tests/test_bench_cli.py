@@ -64,6 +64,28 @@ def test_bench_gpus3_relaunches_three_ranks(tmp_path):
     assert d["release_form"] == "n/a" and d["config"]["round_loop_reason"]
 
 
+def test_bench_world8_tolerant_co_headline(tmp_path):
+    """Round-5 verdict item 6: at N > 1 the JSON carries the straggler-tolerant topology as a co-headline
+    (value_tolerant: message placement, the reference's one worker per process) next to `value` (partition
+    shards), both timed like the headline, with the job's own scaling efficiencies against rank 0's
+    single-GPU run of the same config; 8 gloo ranks (the 8-GPU code path on the CPU)."""
+    out = tmp_path / "b8.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", *TINY, "--no-floor",
+                        "--straggler-steps", "4", "--late-ms", "2", "--json-out", str(out)],
+                       cwd=str(tmp_path), env=_env(), capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["n_gpus"] == 8 and d["shard"] == "partition"
+    assert d["value_tolerant"] > 0 and d["value_tolerant_placement"] == "message"
+    assert d["value_tolerant"] == d["message_placement"]["ms_per_step"] / 1e3
+    assert d["message_placement"]["steps"] == d["steps"]
+    assert d["single_gpu_s_per_iter"] > 0
+    assert d["scaling_efficiency"] == d["single_gpu_s_per_iter"] / (8 * d["value"])
+    assert d["scaling_efficiency_tolerant"] == d["single_gpu_s_per_iter"] / (8 * d["value_tolerant"])
+    assert set(d["scaling_placements"]) == {"value", "value_tolerant"}
+    assert "agc_lazy" in d["straggler"] and d["first_contact"]["ladder"][-1]["ok"]
+
+
 def test_bench_one_gpu_straggler_block(tmp_path):
     """N = 1 carries the paper's claim in the driver's own JSON: naive, AGC with the reference's drain
     and AGC with the lazy drain under Exp virtual delays, with floors and wall-clock to the common target
