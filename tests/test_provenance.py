@@ -61,3 +61,20 @@ def test_build_lock_serializes_processes():
     spans = sorted(q.get(timeout=5) for _ in ps)
     for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
         assert b0 >= a1, f"overlapping build-lock holders: {spans}"
+
+
+def test_baseline_md_mi355x_section_is_generated():
+    """Round-5 verdict item 7: every MI355X number in BASELINE.md comes from a measurement file --
+    the section is tools/baseline_md.py's rendering of the driver's newest BENCH_r*.json and the
+    newest profiles/round*/ records, verbatim (regenerate with `python tools/baseline_md.py --write`)."""
+    import importlib.util
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("baseline_md", os.path.join(root, "tools", "baseline_md.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    with open(os.path.join(root, "BASELINE.md")) as f:
+        text = f.read()
+    assert mod.render() in text
+    assert text.count("## MI355X measurements") == 1
