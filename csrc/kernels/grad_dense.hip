@@ -1172,7 +1172,8 @@ slab_reduce_fused_put(const A* __restrict__ slab, const int* __restrict__ slot_t
     }
     if (put.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(put.dst)[1] ^= 0x10;  // test hook
   }
-  block_release_system(put.strict);  // the tags before the flag
+  if (threadIdx.x == 0) put_stamp(put);
+  block_release_system(put.strict);  // the tags (and the landing stamp) before the flag
   if (threadIdx.x == 0) {
     publish_u64(put.flag, put.value, put.strict);
     put_decide_next_gate(put);
@@ -1234,7 +1235,8 @@ slab_reduce_final_put(const A* __restrict__ part, A* __restrict__ G, int ld, Put
     }
     if (put.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(put.dst)[1] ^= 0x10;  // test hook
   }
-  block_release_system(put.strict);  // the tags before the flag
+  if (threadIdx.x == 0) put_stamp(put);
+  block_release_system(put.strict);  // the tags (and the landing stamp) before the flag
   if (threadIdx.x == 0) {
     publish_u64(put.flag, put.value, put.strict);
     put_decide_next_gate(put);
@@ -1295,7 +1297,8 @@ slab_reduce_final_put1(const A* __restrict__ part, A* __restrict__ G, int ld, in
     if (tid < nslots) put.tag[tid] = MsgTag{static_cast<unsigned int>(put.value), put.rank, tsum[tid]};
     if (put.corrupt && tid == 0) static_cast<unsigned char*>(put.dst)[1] ^= 0x10;  // test hook
   }
-  block_release_system(put.strict);  // the rows and tags before the flag
+  if (tid == 0) put_stamp(put);
+  block_release_system(put.strict);  // the rows, tags (and the landing stamp) before the flag
   if (tid == 0) {
     publish_u64(put.flag, put.value, put.strict);
     put_decide_next_gate(put);

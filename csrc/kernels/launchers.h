@@ -204,8 +204,21 @@ struct PutDesc {
   const unsigned long long* beta_flag;
   unsigned long long stale_next;
   int strict;  // set by the launchers from strict_release() (common.h block_release_system)
+  // Landing stamp (nullptr = off): the last block writes wall_clock64 here just before the flag's
+  // release, so a receiver that sees the flag reads when the put landed on the sender's clock (the
+  // collector orders physically late ranks' messages by it: csrc/runtime/collector.h "Device times").
+  // stamp: the receiver-visible slot (host-mapped ring); stamp_log: the sender's own per-round record.
+  long long* stamp;
+  long long* stamp_log;
 };
 #if defined(__HIPCC__)
+// The landing stamp of a put (one thread of the last block, before the release that precedes the flag).
+__device__ __forceinline__ void put_stamp(const PutDesc& p) {
+  if (!p.stamp && !p.stamp_log) return;
+  const long long t = static_cast<long long>(wall_clock64());
+  if (p.stamp) *p.stamp = t;
+  if (p.stamp_log) *p.stamp_log = t;
+}
 // The next round's gate word (one thread of the launch calls it).
 __device__ __forceinline__ void put_decide_next_gate(const PutDesc& p) {
   if (!p.next_gate) return;
@@ -247,7 +260,9 @@ hipError_t ping_pong_launch(const PingArgs& a, bool master, hipStream_t st);
 // Spin on the device for `ticks` wall_clock64 ticks (a physically late worker, --delay-on worker), after
 // the round's gradient and before its put; a skipped round (gate_closed) does not spin, and a spin
 // ends early once *stop >= stop_at (the master's end-of-run release of a lazy-drain run).
+// rec (nullptr = off): [start, end] of the spin in wall_clock64 ticks (not written when the gate is closed).
 hipError_t spin_launch(long long ticks, hipStream_t st, const int* gate = nullptr,
-                       const unsigned long long* stop = nullptr, unsigned long long stop_at = 0);
+                       const unsigned long long* stop = nullptr, unsigned long long stop_at = 0,
+                       long long* rec = nullptr);
 
 }  // namespace eh

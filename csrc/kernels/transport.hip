@@ -107,7 +107,8 @@ __global__ void __launch_bounds__(256) put_signal(PutArgs args) {
     }
     if (p.corrupt && threadIdx.x == 0) static_cast<unsigned char*>(p.dst)[1] ^= 0x10;  // test hook
   }
-  block_release_system(p.strict);  // the tags before the flag
+  if (threadIdx.x == 0) put_stamp(p);
+  block_release_system(p.strict);  // the tags (and the landing stamp) before the flag
   if (threadIdx.x == 0) {
     publish_u64(p.flag, p.value, p.strict);
     put_decide_next_gate(p);
@@ -159,14 +160,21 @@ __global__ void __launch_bounds__(1024) check_list(const CheckList cl, Integrity
   check_rows_waves(cl, 0, static_cast<int>(blockDim.x >> 6), err, &claim);
 }
 
-__global__ void spin_ticks(long long ticks, const int* gate, const unsigned long long* stop, unsigned long long stop_at) {
+__global__ void spin_ticks(long long ticks, const int* gate, const unsigned long long* stop, unsigned long long stop_at,
+                           long long* rec) {
   if (gate_closed(gate)) return;
   const long long t0 = wall_clock64();
-  while (wall_clock64() - t0 < ticks) {
+  long long t = t0;
+  while (t - t0 < ticks) {
     // the master's run is over (its end-of-run release): nothing this rank still does can matter
     if (stop && __hip_atomic_load(const_cast<unsigned long long*>(stop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= stop_at)
-      return;
+      break;
     __builtin_amdgcn_s_sleep(127);
+    t = wall_clock64();
+  }
+  if (rec && threadIdx.x == 0) {
+    rec[0] = t0;
+    rec[1] = t;
   }
 }
 
@@ -284,9 +292,9 @@ hipError_t check_list_launch(const CheckList& cl, IntegrityErr* err, hipStream_t
 }
 
 hipError_t spin_launch(long long ticks, hipStream_t st, const int* gate, const unsigned long long* stop,
-                       unsigned long long stop_at) {
+                       unsigned long long stop_at, long long* rec) {
   if (ticks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(spin_ticks, dim3(1), dim3(64), 0, st, ticks, gate, stop, stop_at);
+  hipLaunchKernelGGL(spin_ticks, dim3(1), dim3(64), 0, st, ticks, gate, stop, stop_at, rec);
   return hipGetLastError();
 }
 

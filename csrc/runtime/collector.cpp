@@ -96,9 +96,13 @@ int Collector::add_probe(const Probe& p) {
   return static_cast<int>(probes_.size()) - 1;
 }
 
-int Collector::add_event_probe(int worker, int part, int round, uintptr_t event, double delay, bool physical) {
-  return add_probe(Probe{worker, part, round, reinterpret_cast<hipEvent_t>(event), nullptr, 0, false, false, false, 0.0,
-                         delay, kInf, physical, false, 0.0});
+int Collector::add_event_probe(int worker, int part, int round, uintptr_t event, double delay, bool physical,
+                               uintptr_t ref_event, double ref_t) {
+  Probe p{worker, part, round, reinterpret_cast<hipEvent_t>(event), nullptr, 0, false, false, false, 0.0,
+          delay, kInf, physical, false, 0.0};
+  p.ref_ev = reinterpret_cast<hipEvent_t>(ref_event);
+  p.ref_t = ref_t;
+  return add_probe(p);
 }
 
 int Collector::add_host_probe(int worker, int part, int round, double delay, bool physical) {
@@ -107,16 +111,32 @@ int Collector::add_host_probe(int worker, int part, int round, double delay, boo
 }
 
 int Collector::add_flag_probe(int worker, int part, int round, uintptr_t flag_addr, uint64_t value, double delay,
-                              bool physical) {
+                              bool physical, uintptr_t stamp_addr, DeviceClock clk) {
   if (flag_addr == 0) throw std::invalid_argument("Collector: null flag");
-  return add_probe(Probe{worker, part, round, nullptr, reinterpret_cast<const uint64_t*>(flag_addr), value, false,
-                         false, false, 0.0, delay, kInf, physical, false, 0.0});
+  if (stamp_addr != 0 && !(clk.hz > 0.0)) throw std::invalid_argument("Collector: a stamp needs a device clock");
+  Probe p{worker, part, round, nullptr, reinterpret_cast<const uint64_t*>(flag_addr), value, false,
+          false, false, 0.0, delay, kInf, physical, false, 0.0};
+  p.stamp = reinterpret_cast<const int64_t*>(stamp_addr);
+  p.clk = clk;
+  return add_probe(p);
+}
+
+std::vector<ProbeRecord> Collector::probe_log() const {
+  std::vector<ProbeRecord> out;
+  out.reserve(probes_.size());
+  for (const Probe& p : probes_) {
+    const double ts = p.round < static_cast<int>(round_start_.size()) ? round_start_[p.round] : 0.0;
+    out.push_back({p.worker, p.part, p.round, p.seen ? p.t_seen - ts : std::numeric_limits<double>::quiet_NaN(),
+                   p.outcome});
+  }
+  return out;
 }
 
 bool Collector::maybe_skip(Probe& p) {
   if (!skip_stale_ || p.physical || !p.seen || p.arrived || p.round >= round_) return false;
   if (p.start < round_start_[p.round + 1]) return false;  // the worker began it before the next beta
   p.skipped = p.arrived = true;
+  p.outcome = kSkipped;
   ++n_skipped_;
   finish_[p.worker][p.round] = finish_of(p.worker, p.round - 1);  // never ran: the finish carries over
   return true;
@@ -178,13 +198,15 @@ void Collector::poll_events(double t) {
       // push the worker's virtual finish out for rounds that follow, so it leaves as skipped.
       if (skip_stale_ && !p.physical && v > p.fval && p.round < round_) {
         p.skipped = p.arrived = true;
+        p.outcome = kSkipped;
         ++n_skipped_;
         auto& f = finish_[p.worker];
         if (static_cast<int>(f.size()) <= p.round) f.resize(p.round + 1, -kInf);
         f[p.round] = finish_of(p.worker, p.round - 1);
         continue;
       }
-      mark_seen(id, t);
+      // the landing stamp was written before the flag's release: after the acquire above it is this round's
+      mark_seen(id, p.stamp ? p.clk.to_host(static_cast<double>(__atomic_load_n(p.stamp, __ATOMIC_RELAXED))) : t);
       continue;
     }
     int hit = -1;
@@ -197,7 +219,11 @@ void Collector::poll_events(double t) {
       done.emplace_back(p.ev, e == hipSuccess);
       hit = static_cast<int>(done.size()) - 1;
     }
-    if (done[hit].second) mark_seen(id, t);
+    if (!done[hit].second) continue;
+    double ts = t;
+    float ms = 0.f;
+    if (p.ref_ev && hipEventElapsedTime(&ms, p.ref_ev, p.ev) == hipSuccess) ts = p.ref_t + 1e-3 * ms;
+    mark_seen(id, ts);
   }
 }
 
@@ -240,14 +266,20 @@ bool Collector::process_ready(double t, bool /*stop_at_rule*/) {
     const Arrival a{p.worker, p.part, p.round, p.ready - round_start_[p.round], id};
     if (p.round != round_) {  // stale message of an earlier round: drained, ignored
       ++n_stale_;
+      p.outcome = kStale;
       continue;
     }
     const int mi = 2 * p.worker + (p.part ? 1 : 0);
-    if (++got_sh_[mi] < nsh_[mi]) continue;  // more shards of this message still to come
-    if (stopped_) {
-      late_.push_back(a);
+    if (++got_sh_[mi] < nsh_[mi]) {  // more shards of this message still to come
+      p.outcome = kShard;
       continue;
     }
+    if (stopped_) {
+      late_.push_back(a);
+      p.outcome = kLate;
+      continue;
+    }
+    p.outcome = kDecoded;
     cur_.push_back(a);
     if (p.part == 0) {
       if (!got0_[p.worker]) {

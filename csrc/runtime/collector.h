@@ -57,6 +57,14 @@
 // rows (FIFO pairing): they land after their round ended and are drained as stale, never decoded.  The
 // event probe cannot tell them from a computed round, so with virtual delays on top of physical skipping
 // the carried virtual finish of that worker can come out late; the decode is unaffected.
+//
+// Device times (physical probes): the seen time of a physically late rank's message is by default
+// the host's poll time, so when the host thread is descheduled two messages that landed far apart
+// can be seen in one sweep and ordered by the tie permutation.  With a device time source the seen
+// time is WHEN THE MESSAGE LANDED on a GPU clock mapped to the host clock: an IPC flag probe reads
+// the landing stamp its put kernel wrote just before the flag (launchers.h PutDesc::stamp), an event
+// probe reads its timing event against a reference event.  Arrival order is then the landing order
+// up to the flag's visibility latency (microseconds), whatever the host scheduler did.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -72,6 +80,21 @@ enum RuleKind : int {
   kRuleFrc = 2,           // k workers OR every group covered
   kRulePartialFrc = 3,    // all part-1 AND every group covered by part 0
   kRulePartialCount = 4,  // all part-1 AND k part-0 arrivals
+};
+
+// Device clock -> host clock (Collector::now): t = t0 + (ticks - tick0) / hz.
+struct DeviceClock {
+  double tick0 = 0.0, t0 = 0.0, hz = 0.0;
+  double to_host(double ticks) const { return t0 + (ticks - tick0) / hz; }
+};
+
+// What became of a probe (Collector::probe_log).
+enum ProbeOutcome : int { kPending = -1, kDecoded = 0, kLate = 1, kStale = 2, kSkipped = 3, kShard = 4 };
+
+struct ProbeRecord {
+  int worker, part, round;
+  double t_seen;  // relative to the round's start; NaN if never seen
+  int outcome;    // ProbeOutcome
 };
 
 struct Arrival {
@@ -97,12 +120,18 @@ class Collector {
   // Message (worker, part) is delivered as n >= 1 shards (probes); default 1.
   void set_shards(int worker, int part, int n);
   // physical: the probe's seen time is its arrival (see "Physical probes" above).
-  int add_event_probe(int worker, int part, int round, uintptr_t event, double delay, bool physical = false);
+  // ref_event (timing-enabled, like `event`; 0 = host poll time): the event's device time relative to
+  // ref_event, plus ref_t, is its seen time (see "Device times").
+  int add_event_probe(int worker, int part, int round, uintptr_t event, double delay, bool physical = false,
+                      uintptr_t ref_event = 0, double ref_t = 0.0);
   int add_host_probe(int worker, int part, int round, double delay, bool physical = false);
   // IPC mailbox probe: arrived once the 64-bit flag at `flag_addr` (shared host memory,
-  // release-stored by the sending GPU) reaches `value` (csrc/runtime/ipc.cpp).
+  // release-stored by the sending GPU) reaches `value` (csrc/runtime/ipc.cpp).  stamp_addr (0 = host
+  // poll time): the put's landing stamp on the sender's clock `clk` (see "Device times").
   int add_flag_probe(int worker, int part, int round, uintptr_t flag_addr, uint64_t value, double delay,
-                     bool physical = false);
+                     bool physical = false, uintptr_t stamp_addr = 0, DeviceClock clk = {});
+  // Every probe so far: (worker, part, round, seen time from its round's start, outcome).
+  std::vector<ProbeRecord> probe_log() const;
   void mark_seen(int probe, double t);
   // Stale-round skipping of virtual probes (drain "lazy"; see above).  Off: lag carries over and
   // every round's message is delivered in order (the reference's no-Waitall schemes).
@@ -150,6 +179,11 @@ class Collector {
     bool physical;
     bool skipped;
     double start;  // virtual start (seen virtual probes)
+    const int64_t* stamp = nullptr;  // device landing stamp (flag probes; see "Device times")
+    DeviceClock clk{};
+    hipEvent_t ref_ev = nullptr;     // reference event of a device-timed event probe
+    double ref_t = 0.0;
+    int outcome = kPending;
   };
   int add_probe(const Probe& p);
   // Skip a seen virtual probe whose next round began before its start (skip_stale_).

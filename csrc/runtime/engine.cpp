@@ -483,6 +483,7 @@ class MasterPump {
     for (auto e : rev_)
       if (e) hipEventDestroy(e);
     if (bev_) hipEventDestroy(bev_);
+    if (ref_ev_) hipEventDestroy(ref_ev_);
     for (auto& [r, st] : send_st_) hipStreamDestroy(st);
     for (auto& [r, st] : recv_st_)
       if (!send_st_.count(r) || send_st_.at(r) != st) hipStreamDestroy(st);  // a shared link stream once
@@ -681,6 +682,43 @@ class MasterPump {
     need((int64_t)delays.size() >= (int64_t)R_ * W_, "remote delays must be [R*W]");
     remote_delays_ = delays;
   }
+  // Device times of physically late ranks' messages (collector.h "Device times").  IPC: worker rank r's
+  // puts write their landing stamps into ring slots [r][i % ring] of shared host memory (ring_host) on
+  // that rank's GPU clock clocks[r] = (tick0, t0, hz).  p2p: the receive events become timing events,
+  // read against a reference event of this GPU calibrated against the host clock here.
+  void set_device_times(const std::vector<std::tuple<int, double, double, double>>& clocks, uintptr_t ring_host,
+                        int ring) {
+    need(ring >= 1 || comm_, "stamp ring must have >= 1 slot");
+    dev_times_ = true;
+    for (const auto& [r, tick0, t0, hz] : clocks) {
+      need(hz > 0.0, "device clock rate must be > 0");
+      clocks_[r] = eh::DeviceClock{tick0, t0, hz};
+    }
+    ring_host_ = ring_host;
+    ring_ = ring;
+    if (comm_) {
+      for (auto& e : rev_) {  // timing events: the collector reads their device times
+        hcheck(hipEventDestroy(e), "hipEventDestroy");
+        hcheck(hipEventCreate(&e), "hipEventCreate");
+      }
+      calibrate_ref_event();
+    }
+  }
+  // Per-round device records (tests/lazy_check.py): [R + 1][2] wall_clock64 stamps just before and just
+  // after round j's beta put kernels (-1: not put by put_beta, e.g. released by the arbiter).
+  void set_records(bool on) {
+    rec_ = on ? at::full({R_ + 1, 2}, -1, at::TensorOptions().dtype(at::kLong).device(at::Device(at::kCUDA, device_)))
+              : Tensor();
+  }
+  Tensor records() {
+    hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    return rec_.defined() ? rec_.cpu() : Tensor();
+  }
+  py::list probe_log() const {
+    py::list out;
+    for (const auto& r : col_->probe_log()) out.append(py::make_tuple(r.worker, r.part, r.round, r.t_seen, r.outcome));
+    return out;
+  }
   // Drain "lazy" (engine/trainer.py): the collector skips stale virtual rounds (collector.h) and, with
   // IPC targets, finish_run() tells every worker rank the run is over so its queued rounds are stale.
   void set_skip_stale(bool on) {
@@ -785,12 +823,23 @@ class MasterPump {
         hcheck(hipEventRecord(ev, rs), "hipEventRecord(recv)");
         for (const auto& m : remote_)
           if (m.row >= row0 && m.row < row0 + n)
-            col_->add_event_probe(m.w, m.p, i, reinterpret_cast<uintptr_t>(ev), dr[m.w], !remote_delays_.empty());
+            col_->add_event_probe(m.w, m.p, i, reinterpret_cast<uintptr_t>(ev), dr[m.w], !remote_delays_.empty(),
+                                  dev_times_ && !remote_delays_.empty() ? reinterpret_cast<uintptr_t>(ref_ev_) : 0,
+                                  ref_t_);
       }
       return;
     }
-    for (const auto& m : remote_)  // physically late ranks (remote delays set): seen = arrived
-      col_->add_flag_probe(m.w, m.p, i, m.flag, static_cast<uint64_t>(i + 1), dr[m.w], !remote_delays_.empty());
+    for (const auto& m : remote_) {  // physically late ranks (remote delays set): seen = arrived
+      const bool physical = !remote_delays_.empty();
+      uintptr_t stamp = 0;
+      eh::DeviceClock clk{};
+      const int r = row_rank_[m.row];
+      if (physical && dev_times_ && ring_host_ && clocks_.count(r)) {  // its landing time on its own GPU clock
+        stamp = ring_host_ + sizeof(int64_t) * (static_cast<uintptr_t>(r) * ring_ + i % ring_);
+        clk = clocks_.at(r);
+      }
+      col_->add_flag_probe(m.w, m.p, i, m.flag, static_cast<uint64_t>(i + 1), dr[m.w], physical, stamp, clk);
+    }
   }
 
   // Returns (status, arrivals [(worker, part, t_rel)], t_start, t_decoded, t_end, t_waited):
@@ -1371,6 +1420,34 @@ class MasterPump {
     }
   }
   void put_beta(int j) {
+    int64_t* rec = rec_.defined() && j <= R_ ? rec_.data_ptr<int64_t>() + 2 * static_cast<int64_t>(j) : nullptr;
+    if (rec) hcheck(eh::stamp_launch(reinterpret_cast<long long*>(rec), stream_), "stamp(beta put)");
+    put_beta_kernels(j);
+    if (rec) hcheck(eh::stamp_launch(reinterpret_cast<long long*>(rec + 1), stream_), "stamp(beta put)");
+  }
+  // The reference event of device-timed receive events: the sample with the shortest host round trip.
+  void calibrate_ref_event() {
+    std::vector<hipEvent_t> evs(8, nullptr);
+    double best = 1e30;
+    int pick = 0;
+    for (size_t k = 0; k < evs.size(); ++k) {
+      hcheck(hipEventCreate(&evs[k]), "hipEventCreate");
+      const double ta = eh::Collector::now();
+      hcheck(hipEventRecord(evs[k], stream_), "hipEventRecord(ref)");
+      hcheck(hipEventSynchronize(evs[k]), "hipEventSynchronize(ref)");
+      const double tb = eh::Collector::now();
+      if (tb - ta < best) {
+        best = tb - ta;
+        pick = static_cast<int>(k);
+        ref_t_ = 0.5 * (ta + tb);
+      }
+    }
+    if (ref_ev_) hipEventDestroy(ref_ev_);
+    ref_ev_ = evs[pick];
+    for (size_t k = 0; k < evs.size(); ++k)
+      if (static_cast<int>(k) != pick) hipEventDestroy(evs[k]);
+  }
+  void put_beta_kernels(int j) {
     if (comm_) {
       if (timing_) record_t(j, 0);
       put_beta_comm(j);
@@ -1477,6 +1554,14 @@ class MasterPump {
   std::vector<std::pair<uintptr_t, uintptr_t>> drain_flags_;
   int prepub_ = -1;  // round whose beta is already queued (device-side drain / the arbiter)
   std::shared_ptr<eh::P2PComm> comm_;                 // stream-ordered p2p (set_comm); null: IPC mailbox
+  // device times of physically late ranks (set_device_times) and per-round records (set_records)
+  bool dev_times_ = false;
+  std::map<int, eh::DeviceClock> clocks_;
+  uintptr_t ring_host_ = 0;
+  int ring_ = 1;
+  hipEvent_t ref_ev_ = nullptr;
+  double ref_t_ = 0.0;
+  Tensor rec_;
   std::vector<std::tuple<int, int, int>> comm_ranks_;  // (rank, first mailbox row, rows) of every sender
   std::vector<int> comm_peers_;                        // every worker rank (beta receivers)
   std::map<int, hipStream_t> send_st_, recv_st_;       // per-peer streams
@@ -1633,6 +1718,30 @@ class WorkerPump {
     for (auto& e : bev_) hcheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
   }
   bool skip_stale() const { return skip_flag_ != nullptr || skip_comm_; }
+
+  // IPC: every message put writes its landing stamp into this rank's ring of shared host memory, slot
+  // i % ring (ring_dev: device address of the ring), read by the master's collector (collector.h
+  // "Device times").
+  void set_stamp_ring(uintptr_t ring_dev, int ring) {
+    need(ring_dev == 0 || ring >= 1, "stamp ring must have >= 1 slot");
+    ring_dev_ = ring_dev;
+    ring_ = ring;
+  }
+  // Per-round device records (wall_clock64 ticks, -1 = not recorded), tests/lazy_check.py:
+  //   [0] landing stamp of the round's put (IPC, written by the put kernel before its flag)
+  //   [1] [2] just before / after the round's put or send      [3] [4] spin start / end (--delay-on worker)
+  //   [5] [6] just before / after the stale-round gate (p2p)    [7] [8] just before / after the counter bump
+  //   that announces beta(i) landed on this rank (p2p with stale-round skipping)
+  static constexpr int kRec = 9;
+  void set_records(bool on) {
+    rec_ = on ? at::full({R_ + 1, kRec}, -1, at::TensorOptions().dtype(at::kLong).device(at::Device(at::kCUDA, device_)))
+              : Tensor();
+  }
+  Tensor records() {
+    hcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    if (bst_) hcheck(hipStreamSynchronize(bst_), "hipStreamSynchronize");
+    return rec_.defined() ? rec_.cpu() : Tensor();
+  }
   // Rounds this rank skipped as stale (syncs the stream).
   std::vector<int> skipped_rounds() {
     std::vector<int> out;
@@ -1741,6 +1850,8 @@ class WorkerPump {
         pd.rank = static_cast<unsigned int>(rank_);
         pd.corrupt = sabotage("msg", rank_, i) ? 1 : 0;
       }
+      if (ring_dev_) pd.stamp = reinterpret_cast<long long*>(ring_dev_) + i % ring_;
+      pd.stamp_log = rec_at(i, 0);
       if (timing_) record_t(i, 0);
       for (int k = 1; k < repeat_; ++k) hcheck(g_->launch(beta, g, stream_, gate), "worker gradient (slow rank)");
       if (fuse_put_) {  // gradient + put + signal in one stream order, no separate put kernel
@@ -1750,13 +1861,16 @@ class WorkerPump {
         hcheck(g_->launch(beta, g, stream_, gate), "worker gradient");
         if (timing_) record_t(i, 1);
         if (!late_ticks_.empty() && late_ticks_[i] > 0)  // after compute, before the send (ref src/naive.py:141-148)
-          hcheck(eh::spin_launch(late_ticks_[i], stream_, gate, skip_flag_, static_cast<unsigned long long>(R_) + 1),
+          hcheck(eh::spin_launch(late_ticks_[i], stream_, gate, skip_flag_, static_cast<unsigned long long>(R_) + 1,
+                                 rec_at(i, 3)),
                  "late worker spin");
         eh::PutArgs pa{};
         pa.n = 1;
         pa.d[0] = pd;
         const int blocks = (int)std::max<long long>(1, std::min<long long>(64, (bytes / 16 + 4095) / 4096));
+        stamp(i, 1, stream_);
         hcheck(eh::put_signal_launch(pa, blocks, stream_), "put_signal(messages)");
+        stamp(i, 2, stream_);
       }
       if (timing_) record_t(i, 2);
       if (tags_)  // beta(i) against its tag, behind the round that read it (off the critical path)
@@ -1783,7 +1897,9 @@ class WorkerPump {
     for (; posted_ <= std::min(j, R_); ++posted_) {
       char* beta = static_cast<char*>(inbox_.data_ptr()) + static_cast<int64_t>(posted_) * bbytes;
       comm_->recv(0, beta, bbytes, bst_);
+      stamp(posted_, 7, bst_);
       hcheck(eh::signal_launch(cnt, static_cast<unsigned long long>(posted_) + 1, bst_), "signal(beta landed)");
+      stamp(posted_, 8, bst_);
       hcheck(hipEventRecord(bev_[posted_], bst_), "hipEventRecord(beta)");
     }
   }
@@ -1810,14 +1926,19 @@ class WorkerPump {
       const char* beta = static_cast<const char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * ld_ * es_;
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(i % K_) * g_rows_ * ld_ * es_;
       // closed iff beta(i+1) landed before this round starts (value i + 2)
+      stamp(i, 5, stream_);
       hcheck(eh::gate_launch(cnt, static_cast<unsigned long long>(i) + 2, gw + i, stream_), "gate(stale round)");
+      stamp(i, 6, stream_);
       if (timing_) record_t(i, 0);
       for (int k = 0; k < repeat_; ++k) hcheck(g_->launch(beta, g, stream_, gw + i), "worker gradient");
       if (timing_) record_t(i, 1);
       if (!late_ticks_.empty() && late_ticks_[i] > 0)  // a skipped round does not spin; the end of the run stops one
-        hcheck(eh::spin_launch(late_ticks_[i], stream_, gw + i, cnt, static_cast<unsigned long long>(R_) + 1),
+        hcheck(eh::spin_launch(late_ticks_[i], stream_, gw + i, cnt, static_cast<unsigned long long>(R_) + 1,
+                               rec_at(i, 3)),
                "late worker spin");
+      stamp(i, 1, stream_);
       comm_->send(0, g, static_cast<int64_t>(n_) * ld_ * es_, stream_);  // always: the FIFO pairing
+      stamp(i, 2, stream_);
       if (timing_) record_t(i, 2);
     }
     if (b > a && !event_wait(bev_[b - 1], b - 1)) {
@@ -1853,8 +1974,10 @@ class WorkerPump {
       for (int k = 0; k < repeat_; ++k) hcheck(g_->launch(beta, g, stream_), "worker gradient");
       if (timing_) record_t(i, 1);
       if (!late_ticks_.empty() && late_ticks_[i] > 0)  // after compute, before the send (ref src/naive.py:141-148)
-        hcheck(eh::spin_launch(late_ticks_[i], stream_), "late worker spin");
+        hcheck(eh::spin_launch(late_ticks_[i], stream_, nullptr, nullptr, 0, rec_at(i, 3)), "late worker spin");
+      stamp(i, 1, stream_);
       comm_->send(0, g, static_cast<int64_t>(n_) * ld_ * es_, stream_);
+      stamp(i, 2, stream_);
       if (timing_) record_t(i, 2);
     }
     if (b > a && !event_wait(rev_[(b - 1) % 2], b - 1)) {
@@ -1928,6 +2051,14 @@ class WorkerPump {
     if (!e) hcheck(hipEventCreate(&e), "hipEventCreate");
     hcheck(hipEventRecord(e, stream_), "hipEventRecord");
   }
+  // Address of record field `f` of round i (nullptr when records are off).
+  long long* rec_at(int i, int f) {
+    if (!rec_.defined() || i < 0 || i > R_) return nullptr;
+    return reinterpret_cast<long long*>(rec_.data_ptr<int64_t>()) + static_cast<int64_t>(i) * kRec + f;
+  }
+  void stamp(int i, int f, hipStream_t st) {
+    if (long long* p = rec_at(i, f)) hcheck(eh::stamp_launch(p, st), "stamp(record)");
+  }
 
   std::shared_ptr<GradLauncher> g_;
   Tensor inbox_, G_;
@@ -1936,6 +2067,9 @@ class WorkerPump {
   int mbox_rows_, row0_;
   uint64_t* bflag_;
   void* bflag_dev_ = nullptr;
+  uintptr_t ring_dev_ = 0;  // set_stamp_ring
+  int ring_ = 1;
+  Tensor rec_;              // set_records
   unsigned long long* mflag_;
   Tensor counters_;
   int K_;
@@ -2014,8 +2148,44 @@ std::vector<bool> stream_wait_probe(const std::vector<uintptr_t>& streams, doubl
   return ok;
 }
 
+// This GPU's wall_clock64 against the host clock (Collector::now): (tick0, t0, hz) such that
+// t = t0 + (ticks - tick0) / hz.  A one-thread kernel stores its clock into host-mapped memory and the
+// host spins until it lands; of `tries` samples the one with the shortest launch -> seen time wins (its
+// t0 lags the device store by the store's visibility latency, about a microsecond).
+std::tuple<double, double, double> device_clock(int device, int tries) {
+  int khz = 0;
+  hcheck(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device), "hipDeviceGetAttribute");
+  need(khz > 0, "device reports no wall clock rate");
+  HostMapped slot(sizeof(long long));
+  auto* h = static_cast<volatile long long*>(slot.host);
+  hipStream_t st = c10::hip::getCurrentHIPStream(device).stream();
+  hcheck(hipStreamSynchronize(st), "hipStreamSynchronize");
+  double best = 1e30, tick0 = 0.0, t0 = 0.0;
+  py::gil_scoped_release nogil;
+  for (int k = 0; k < std::max(1, tries); ++k) {
+    *h = -1;
+    const double ta = eh::Collector::now();
+    hcheck(eh::stamp_launch(static_cast<long long*>(slot.dev), st), "stamp(clock)");
+    double tb = ta;
+    for (;;) {
+      tb = eh::Collector::now();
+      if (*h != -1) break;
+      if (tb - ta > 5.0) throw std::runtime_error("device_clock: the stamp never landed");
+    }
+    if (tb - ta < best) {
+      best = tb - ta;
+      tick0 = static_cast<double>(*h);
+      t0 = tb;
+    }
+  }
+  hcheck(hipStreamSynchronize(st), "hipStreamSynchronize");
+  return {tick0, t0, 1e3 * khz};
+}
+
 void bind_engine(py::module& m) {
   m.def("stream_wait_probe", &stream_wait_probe, py::arg("streams"), py::arg("timeout"));
+  m.def("device_clock", &device_clock, py::arg("device"), py::arg("tries") = 16,
+        "(tick0, t0, hz): this GPU's wall_clock64 against the host clock, t = t0 + (ticks - tick0) / hz");
   py::class_<GradLauncher, std::shared_ptr<GradLauncher>>(m, "GradLauncher")
       .def_static("dense", &make_dense, py::arg("dtype"), py::arg("loss"), py::arg("cpl"), py::arg("segs"),
                   py::arg("tasks"), py::arg("slab"), py::arg("slot_task_begin"), py::arg("part"), py::arg("ld"),
@@ -2095,7 +2265,11 @@ void bind_engine(py::module& m) {
       .def("set_timing", &MasterPump::set_timing)
       .def("timing_ms", &MasterPump::timing_ms)
       .def("graphs_launched", &MasterPump::graphs_launched)
-      .def("set_fused_update", &MasterPump::set_fused_update, py::arg("on"));
+      .def("set_fused_update", &MasterPump::set_fused_update, py::arg("on"))
+      .def("set_device_times", &MasterPump::set_device_times, py::arg("clocks"), py::arg("ring_host"), py::arg("ring"))
+      .def("set_records", &MasterPump::set_records, py::arg("on"))
+      .def("records", &MasterPump::records)
+      .def("probe_log", [](MasterPump& p) { return p.probe_log(); });
   py::class_<WorkerPump>(m, "WorkerPump")
       .def(py::init<std::shared_ptr<GradLauncher>, const Tensor&, const Tensor&, int, uintptr_t, int, int, uintptr_t,
                     uintptr_t, const Tensor&, int, int, double, uintptr_t>(),
@@ -2120,6 +2294,9 @@ void bind_engine(py::module& m) {
       .def("set_integrity", &WorkerPump::set_integrity, py::arg("mbox_tags"), py::arg("inbox_tags"), py::arg("rank"),
            py::arg("on"))
       .def("check_integrity", &WorkerPump::check_integrity)
-      .def("timing", &WorkerPump::timing);
+      .def("timing", &WorkerPump::timing)
+      .def("set_stamp_ring", &WorkerPump::set_stamp_ring, py::arg("ring_dev"), py::arg("ring"))
+      .def("set_records", &WorkerPump::set_records, py::arg("on"))
+      .def("records", &WorkerPump::records);
 }
 }  // namespace eh

@@ -94,6 +94,13 @@ class RunConfig:
     instrument: bool = False  # per-round HIP-event timing of puts / gradient launches (Trainer.rank_report)
     # IPC messages carry (round, rank, checksum) tags that the receiver verifies (csrc/kernels/integrity.h)
     integrity: bool = True
+    # the reference topology's master: rank 0 runs the master only and hosts no logical worker (worker
+    # w on rank 1 + w mod (world - 1); ref main.py:16-18, run_approx_coding.sh:47-49).  Default: rank 0
+    # hosts workers too (one process per GPU, no GPU idles)
+    dedicated_master: bool = False
+    # per-round device records of every rank (beta put / message put / spin / gate stamps on the GPU
+    # clocks) and the master's probe log, kept as Trainer.device_records (tests/lazy_check.py)
+    device_records: bool = False
 
     def __post_init__(self):
         self.update_rule = str(self.update_rule)

@@ -201,10 +201,16 @@ class Trainer:
         self.shard_mode = cfg.shard if cfg.shard != "auto" else "message"
         self.shards = make_shards(scheme.messages, self.shard_mode)
         parts = [[(p, rows) for p, _ in u.segments] for u in self.shards]
+        # --dedicated-master: the worker ranks are 1..world-1, rank 0 only runs the master (the reference
+        # topology); otherwise rank 0 hosts workers too
+        dedicated = bool(cfg.dedicated_master) and env.world > 1
+        ranks = env.world - 1 if dedicated else env.world
         if self.shard_mode == "partition":
-            self.owner = place_units(parts, env.world, replica_weight)
+            self.owner = place_units(parts, ranks, replica_weight)
         else:
-            self.owner = place_spread([u.worker for u in self.shards], env.world)
+            self.owner = place_spread([u.worker for u in self.shards], ranks)
+        if dedicated:
+            self.owner = [o + 1 for o in self.owner]
         self.by_rank = {r: sorted({u.worker for u, o in zip(self.shards, self.owner) if o == r})
                         for r in range(env.world)}
         self.local_msgs = [u for u, o in zip(self.shards, self.owner) if o == env.rank]
@@ -429,6 +435,14 @@ class Trainer:
         start = env.broadcast_object(start, 0)
         env.barrier()
         self.loop, self.loop_reason = select_round_loop(self.loop_inputs(start))
+        self.device_records = None
+        # physically late ranks: every rank's GPU clock against the host clock, so the master's collector
+        # orders their messages by when they landed (collector.h "Device times")
+        self._clocks = None
+        if env.gpu and env.world > 1 and self.loop != "python" and (self.physical or cfg.device_records):
+            C = native_ext()
+            dev = env.device.index if env.device.index is not None else torch.cuda.current_device()
+            self._clocks = env.broadcast_object(env.gather_objects((env.rank, *C.device_clock(dev))), 0)
         native_loop = self.native_loop
         if self.skip_stale and self.loop == "python" and self.tx is not None and self.tx.name in P2P_TRANSPORTS:
             # the Python round loop receives beta in stream order (no look-ahead), so a p2p worker cannot
@@ -792,6 +806,11 @@ class Trainer:
                           self.rule_k, bool(self.drain))
         if self.physical:  # remote messages are really late: the collector applies no virtual delay to them
             pump.set_remote_delays([float(x) for x in self._remote_delays(delay_table).ravel()])
+        if self._clocks and tx is not None and (self.physical or cfg.device_records):
+            ring = (tx.flags.host_addr(tx.stamp_base), tx.K) if tx.name == "ipc" else (0, 1)
+            pump.set_device_times([tuple(c) for c in self._clocks if c[0] != 0], *ring)
+        if cfg.device_records:
+            pump.set_records(True)
         pump.set_repeat(self.repeat)
         # device-driven local rounds: combine + update inside the slab reduction (off: separate launches)
         pump.set_fused_update(bool(getattr(self, "fused_update", True)))
@@ -939,6 +958,9 @@ class Trainer:
         self.rank_stats.update(update_kernel_us=_mean_us(upd, a0),
                                **{f"{k}_us": float(1e6 * np.mean(v[a0 - start:]))
                                   for k, v in self.timer.t.items() if len(v) > a0 - start})
+        if cfg.device_records:
+            self.device_records = {"rank": 0, "clock": self._clocks[0] if self._clocks else None,
+                                   "beta_put": pump.records().numpy(), "probes": list(pump.probe_log())}
         col.close()
         self._sync()
         self._closing_barrier()
@@ -996,6 +1018,10 @@ class Trainer:
                 self.rank_stats["integrity_off"] = why
         pump.set_timing(bool(cfg.instrument))
         pump.set_repeat(self.repeat)
+        if tx.name == "ipc":  # landing stamps of this rank's puts, read by the master's collector
+            pump.set_stamp_ring(tx.flags.dev_addr(tx.stamp_base + env.rank * tx.K), tx.K)
+        if cfg.device_records:
+            pump.set_records(True)
         if self.physical:
             pump.set_delays(self._rank_delays())
         if self.skip_stale and tx.name == "ipc" and self.n_loc:  # stale-round gates read the beta counter
@@ -1029,6 +1055,9 @@ class Trainer:
         self._sync()
         a0 = cut if cut is not None else start
         wait_s, ker_ms, put_ms = pump.timing()
+        if cfg.device_records:
+            self.device_records = {"rank": env.rank, "clock": self._clocks[env.rank] if self._clocks else None,
+                                   "rounds": pump.records().numpy(), "delay_ticks": None}
         self.rank_stats.update(beta_wait_us=_mean_us([1e3 * x if x >= 0 else -1.0 for x in wait_s], a0))
         if pump.skip_stale:
             self.skipped_rounds = list(pump.skipped_rounds())

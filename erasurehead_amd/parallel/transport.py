@@ -445,7 +445,9 @@ class IpcTransport(Transport):
 
     Flag layout (one ShmFlags array created by the master): index r (1..world-1) = the
     round counter of beta pushed to rank r (value i+1 <=> beta of round i is in the inbox),
-    index world + r = the round counter of rank r's messages in the master mailbox.
+    index world + r = the round counter of rank r's messages in the master mailbox, and from
+    ``stamp_base`` on one ring of K landing stamps per rank (slot stamp_base + r * K + i % K: when rank
+    r's put of round i landed, on its GPU clock; csrc/runtime/collector.h "Device times").
     """
 
     name = "ipc"
@@ -484,12 +486,14 @@ class IpcTransport(Transport):
         # every region ends with 16-byte integrity tags, one per payload row (csrc/kernels/integrity.h)
         self.inbox_tag_off = (self.R + 1) * self.ld * self.es
         ibytes = self.inbox_tag_off + (self.R + 1) * TAG_BYTES
+        self.stamp_base = 2 * env.world + 1
+        nflags = self.stamp_base + env.world * self.K
         if env.is_master:
             name = "/eh_" + uuid.uuid4().hex[:16]
             rbytes = self.K * max(1, self.n_rem) * (self.ld * self.es + TAG_BYTES)
 
             def _mk():
-                self.flags = C.ShmFlags(name, 2 * env.world + 1, True)
+                self.flags = C.ShmFlags(name, nflags, True)
                 self.rreg = C.IpcRegion(rbytes, self.dev, self.FINE)
                 return (name, self.rreg.handle(), rbytes)
 
@@ -504,7 +508,7 @@ class IpcTransport(Transport):
 
             def _open():
                 name, h, rbytes = info
-                self.flags = C.ShmFlags(name, 2 * env.world + 1, False)
+                self.flags = C.ShmFlags(name, nflags, False)
                 self.rremote = C.IpcRegion(h, rbytes, self.dev)
                 self._imports.append(self.rremote)
                 self.inbox_reg = C.IpcRegion(ibytes, self.dev, self.FINE)

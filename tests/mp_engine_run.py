@@ -48,6 +48,16 @@ def main():
     res = tr.run(timed_start=ts)  # timed_start: the rounds run in two segments with a fence between them
     reports = env.gather_objects(tr.rank_report())  # every rank's (stale rounds skipped, ...)
     skipped = env.gather_objects([int(i) for i in getattr(tr, "skipped_rounds", [])])
+
+    def plain(x):
+        if isinstance(x, np.ndarray):
+            return x.tolist()
+        if isinstance(x, dict):
+            return {k: plain(v) for k, v in x.items()}
+        if isinstance(x, (list, tuple)):
+            return [plain(v) for v in x]
+        return x
+    records = env.gather_objects(plain(tr.device_records)) if cfg.device_records else None
     if env.is_master:
         arr = np.array([[(w, p) for (w, p, _) in a] for a in res.arrivals], dtype=object)
         t_rel = np.array([[t for (_, _, t) in a] for a in res.arrivals], dtype=object)
@@ -55,7 +65,9 @@ def main():
                  timeset=res.timeset, loop_time=res.loop_time, round_loop=np.array(tr.device_loop or "host"),
                  preflight=np.array(json.dumps(pf)), rank_report=np.array(json.dumps(tr.rank_report())),
                  reports=np.array(json.dumps(reports)), skipped=np.array(json.dumps(skipped)),
-                 owner=np.array(json.dumps({int(u.worker): int(o) for u, o in zip(tr.shards, tr.owner)})))
+                 owner=np.array(json.dumps({int(u.worker): int(o) for u, o in zip(tr.shards, tr.owner)})),
+                 records=np.array(json.dumps(records).replace("NaN", "null")),
+                 delays=np.array(json.dumps(tr.delay_table().tolist()).replace("Infinity", "1e308")))
     env.barrier()
     tr.close()
     env.shutdown()

@@ -209,31 +209,38 @@ def test_ipc_handshake_failure_names_pair_and_step(tmp_path, monkeypatch):
     assert "IPC mailbox handshake failed" in err and "rank 1 -> rank 0: message flag never signalled" in err, err[-3000:]
 
 
-def test_physically_late_worker_ranks_match_virtual_model(tmp_path):
-    """--delay-on worker on the native pumps: each worker rank spins on the device between its
-    gradient and its put (Exp delays, one logical worker per rank), the master's collector sees
-    the real flags.  Cyclic W=3 s=1 with a drain: the arrival sets equal the virtual model's (the
-    2 fastest) on every well-separated round, and the trajectory replays through the oracle."""
+@pytest.mark.parametrize("transport", ["ipc", "loopback"])
+def test_physically_late_worker_ranks_decode_in_landing_order(transport, tmp_path):
+    """--delay-on worker on the native pumps, the reference topology (rank 0 the master only, one logical
+    worker per worker rank): each worker rank spins Exp delays on the device between its gradient and its
+    put, the master's collector sees the real flags / receive events.  Cyclic W=3 s=1 with a drain:
+    checked against the ranks' own device records (tests/lazy_check.py, no host-timing model): every
+    round decodes the first 2 messages in landing order, every round spun its full delay, and the
+    trajectory replays through the oracle.  Over the IPC mailbox and over the RCCL code path (loopback)."""
     import json
 
+    from lazy_check import check_lazy_device
     from oracle import replay
     from test_engine_cpu import make
-    from test_physical_delay import MARGIN, _predict
 
-    case, mean = (1, 0, 0, 4, 1, 0), 0.08
-    over = dict(add_delay=1, delay_mode="exp", delay_mean=mean, delay_on="worker", shard="message", drain="all")
-    r = _launch(3, 0, "GD", str(tmp_path / "p.npz"), EH_TEST_CASE=json.dumps(case), EH_TEST_CFG=json.dumps(over),
-                EH_TEST_ROUND_TIMEOUT="30")
+    case, mean, R = (1, 0, 0, 4, 1, 0), 0.03, 12
+    over = dict(add_delay=1, delay_mode="exp", delay_mean=mean, delay_on="worker", shard="message", drain="all",
+                dedicated_master=True, device_records=True)
+    env = {"ERASUREHEAD_TRANSPORT": transport} if transport != "ipc" else {}
+    r = _launch(4, 0, "GD", str(tmp_path / "p.npz"), EH_TEST_CASE=json.dumps(case), EH_TEST_CFG=json.dumps(over),
+                EH_TEST_ROUND_TIMEOUT="30", **env)
+    assert str(r["transport"]) == transport
     cfg, src, sch, parts = make(case, "GD")
-    checked = 0
-    for i, a in enumerate(r["arrivals"]):
-        d = np.random.RandomState(i).exponential(mean, 3)
-        if np.all(np.diff(np.sort(d)) > MARGIN):
-            assert [w for (w, p) in a] == _predict(d, "count", 2, [0, 1, 2]), (i, d, a)
-            checked += 1
-    assert checked >= 2
-    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
-    ref = replay(sch, parts, r["beta0"], arrivals, "GD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
+    owner = {int(w): int(o) for w, o in json.loads(str(r["owner"])).items()}
+    skipped = json.loads(str(r["skipped"]))
+    d = np.asarray(json.loads(str(r["delays"])))
+    arrivals = [[int(w) for (w, p) in a] for a in r["arrivals"]]
+    got = check_lazy_device(arrivals, json.loads(str(r["records"])), owner, skipped, d, "count", 2, [0, 1, 2],
+                            transport)
+    assert got["rounds"] == R and got["spins"] >= 2 * R and got["inversions"] <= 1
+    assert all(len(a) == 2 for a in arrivals)
+    full = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
+    ref = replay(sch, parts, r["beta0"], full, "GD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(full)))
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
     rep = json.loads(str(r["rank_report"]))
     assert rep["round_loop"] == "native pump"
@@ -277,31 +284,6 @@ def test_loopback_comm_matches_replay(world, case_i, native, tmp_path):
     cfg, src, sch, parts = make(CASES[case_i], "AGD")
     arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
     ref = replay(sch, parts, r["beta0"], arrivals, "AGD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
-    np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
-
-
-def test_loopback_physically_late_ranks(tmp_path):
-    """--delay-on worker over the comm path: the late rank's spin sits between its gradient and its send."""
-    import json
-
-    from oracle import replay
-    from test_engine_cpu import make
-    from test_physical_delay import MARGIN, _predict
-
-    case, mean = (1, 0, 0, 4, 1, 0), 0.08
-    over = dict(add_delay=1, delay_mode="exp", delay_mean=mean, delay_on="worker", shard="message", drain="all")
-    r = _launch(3, 0, "GD", str(tmp_path / "q.npz"), EH_TEST_CASE=json.dumps(case), EH_TEST_CFG=json.dumps(over),
-                ERASUREHEAD_TRANSPORT="loopback", EH_TEST_ROUND_TIMEOUT="30")
-    cfg, src, sch, parts = make(case, "GD")
-    checked = 0
-    for i, a in enumerate(r["arrivals"]):
-        d = np.random.RandomState(i).exponential(mean, 3)
-        if np.all(np.diff(np.sort(d)) > MARGIN):
-            assert [w for (w, p) in a] == _predict(d, "count", 2, [0, 1, 2]), (i, d, a)
-            checked += 1
-    assert checked >= 2
-    arrivals = [[(w, p, 0.0) for (w, p) in a] for a in r["arrivals"]]
-    ref = replay(sch, parts, r["beta0"], arrivals, "GD", cfg.alpha_value, cfg.n_rows, 10.0 * np.ones(len(arrivals)))
     np.testing.assert_allclose(r["betaset"], ref, rtol=1e-9, atol=1e-11)
 
 

@@ -88,7 +88,7 @@ def test_lazy_drain_virtual_model(case, rule, k, groups):
     round (csrc/runtime/collector.h).  The decode inputs match the event model replayed along the
     run's own round starts on every round it can call with a margin, late messages are never decoded
     (the stop rule re-derived from the logged arrivals), and the trajectory replays exactly."""
-    from lazy_check import check_lazy
+    from lazy_model import check_lazy
     from oracle import replay, stops_exactly_at_last
 
     from erasurehead_amd.engine import Trainer
