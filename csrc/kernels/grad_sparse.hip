@@ -469,7 +469,8 @@ __device__ __forceinline__ void wave_affine_scan(A h, A& b) {
 constexpr int kWgWaves = 16;     // waves per column-pass workgroup
 constexpr int kMaxWgTiles = 128;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES <= this):
                                  // wave w takes the chunk's tiles w, w + 16, ...
-constexpr int kStageRegs = 4;    // staged residuals per thread: 4096 rows per sub-block (32 KB fp64 / 16 KB fp32)
+constexpr int kStageRegs = 4;    // staged residuals per thread: 4096 rows per sub-block (32 KB fp64 / 16 KB fp32);
+                                 // 8 (8192 rows) for merged FRC / AGC units (csc_tiles_lds STAGE)
 constexpr int kRunCap = 128;     // runs per tile compacted in LDS (covtype: 33 on average, 0.7 % of tiles above)
 
 // A tile's 8 row indices per lane as loaded (16-bit rows: one 16-byte vector, 32-bit rows: two), decoded
@@ -541,7 +542,7 @@ __device__ __forceinline__ unsigned tile_rows_decode(const TileRaw& r, int (&row
 // columns itself (tail of the first tile + the heads of the later ones, in tile order: csc_spans'
 // order).  LOCAL is a template parameter so the head / tail stores are LDS or global stores (a pointer
 // that may be either is a flat store, which every later wait has to count on both counters).
-template <typename A, bool ROW16, bool VALS, bool LOCAL>
+template <typename A, bool ROW16, bool VALS, bool LOCAL, int STAGE>
 __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, const int* gate) {
   __shared__ int run_col[kWgWaves][kRunCap];
   __shared__ A run_val[kWgWaves][kRunCap];
@@ -573,14 +574,14 @@ __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, con
     tk = a.tkeys[t];  // (first run, n | runs << 10 | span flags << 20, sub-block, first column)
   }
   const A* __restrict__ ug = static_cast<const A*>(a.u) + wd.x;
-  A st[kStageRegs];
+  A st[STAGE];
 #pragma unroll
-  for (int j = 0; j < kStageRegs; ++j) {
+  for (int j = 0; j < STAGE; ++j) {
     const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
     st[j] = i < wd.w ? ug[i] : A(0);
   }
 #pragma unroll
-  for (int j = 0; j < kStageRegs; ++j) {
+  for (int j = 0; j < STAGE; ++j) {
     const int i = threadIdx.x + j * static_cast<int>(blockDim.x);
     if (i < wd.w) su[i] = st[j];
   }
@@ -643,7 +644,22 @@ __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, con
     const A prev = dpp_a0<0x138>(b);        // wave_shr:1 -- the previous lane's running sum
     const A carry = fl & 1u ? A(0) : prev;       // into this lane's entries before its first flag
     const unsigned cmask = fl ? (fl & (0u - fl)) - 1u : 0xffu;
-    A* __restrict__ gout = static_cast<A*>(a.Gs) + static_cast<long long>(p) * a.ld;
+    // the output rows of sub-block p (wave-uniform): row p, or its shared message rows (SparseArgs::dst)
+    long long doff[kSparseMaxDst];
+    int nd = 1;
+    doff[0] = static_cast<long long>(p) * a.ld;
+    if (a.dst) {
+      nd = 0;
+#pragma unroll
+      for (int q = 0; q < kSparseMaxDst; ++q) {
+        const int r = __builtin_amdgcn_readfirstlane(a.dst[p * kSparseMaxDst + q]);
+        if (r >= 0) doff[nd++] = static_cast<long long>(r) * a.ld;
+      }
+    }
+    A* __restrict__ gbase = static_cast<A*>(a.Gs);
+    auto put = [&](int col, A val) {
+      for (int q = 0; q < nd; ++q) gbase[doff[q] + col] = val;
+    };
     if (compact) {
       // each run end stores its lane-local sum at its run index; the one run that began in an earlier
       // lane (it ends first here, run index before - 1) then gets the carry: sm + carry, as before
@@ -658,7 +674,7 @@ __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, con
         const bool has_tail = r == nruns - 1 && (flags & kSpanTail);    // the run goes on in later tiles
         if (has_head) hd[j] = val;
         if (has_tail) tl[j] = val;
-        if (!has_head && !has_tail) gout[run_col[w][r]] = val;
+        if (!has_head && !has_tail) put(run_col[w][r], val);
       }
     } else {  // many short runs: every run end writes its own sum, the column from global memory
 #pragma unroll
@@ -670,7 +686,7 @@ __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, con
           const bool has_tail = r == nruns - 1 && (flags & kSpanTail);
           if (has_head) hd[j] = val;
           if (has_tail) tl[j] = val;
-          if (!has_head && !has_tail) gout[buf_load_scalar<int>(rrs, 4 * r)] = val;
+          if (!has_head && !has_tail) put(buf_load_scalar<int>(rrs, 4 * r), val);
         }
     }
     if (!more) break;
@@ -684,7 +700,15 @@ __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, con
   if (my_span.w >= 0) {  // (sub-block, column, first tile, last tile), chunk-relative tiles
     A sum = s_tail[my_span.z];
     for (int k = my_span.z + 1; k <= my_span.w; ++k) sum += s_head[k];
-    static_cast<A*>(a.Gs)[static_cast<long long>(my_span.x) * a.ld + my_span.y] = sum;
+    A* __restrict__ gs = static_cast<A*>(a.Gs);
+    if (a.dst) {
+      for (int q = 0; q < kSparseMaxDst; ++q) {
+        const int r = a.dst[my_span.x * kSparseMaxDst + q];
+        if (r >= 0) gs[static_cast<long long>(r) * a.ld + my_span.y] = sum;
+      }
+    } else {
+      gs[static_cast<long long>(my_span.x) * a.ld + my_span.y] = sum;
+    }
   }
 }
 
@@ -805,14 +829,21 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
   }
   if (a.ntiles > 0 && a.wg) {
     const size_t ulds = static_cast<size_t>(std::max(a.u_lds, 1)) * (dtype == 0 ? 8 : 4);
-    if (a.u_lds > kStageRegs * 1024) return hipErrorInvalidValue;  // (sub-blocks of at most 4096 rows)
+    if (a.u_lds > 2 * kStageRegs * 1024) return hipErrorInvalidValue;  // (sub-blocks of at most 8192 rows)
+    if (a.dst && (a.sub_begin || a.nspan || a.nempty)) return hipErrorInvalidValue;  // shared rows: unblocked only
+    const bool wide = a.u_lds > kStageRegs * 1024;  // merged units: 8192-row sub-blocks, 8 staged per thread
     const dim3 grid(static_cast<unsigned>(a.nwg));
-#define EH_TLDS2(A_, R_, V_, L_)                                                                                \
+#define EH_TLDS3(A_, R_, V_, L_, S_)                                                                            \
   {                                                                                                              \
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(csc_tiles_lds<A_, R_, V_, L_>),        \
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(csc_tiles_lds<A_, R_, V_, L_, S_>),    \
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ulds));   \
     if (e != hipSuccess) return e;                                                                               \
-    hipLaunchKernelGGL((csc_tiles_lds<A_, R_, V_, L_>), grid, dim3(1024), ulds, st, a, gate);                     \
+    hipLaunchKernelGGL((csc_tiles_lds<A_, R_, V_, L_, S_>), grid, dim3(1024), ulds, st, a, gate);                 \
+  }
+#define EH_TLDS2(A_, R_, V_, L_)                                   \
+  {                                                                \
+    if (wide) EH_TLDS3(A_, R_, V_, L_, 2 * kStageRegs)             \
+    else EH_TLDS3(A_, R_, V_, L_, kStageRegs)                      \
   }
 #define EH_TLDS(A_, R_, V_)                     \
   {                                               \
@@ -829,6 +860,7 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
 #undef EH_TILES
 #undef EH_TLDS
 #undef EH_TLDS2
+#undef EH_TLDS3
   } else if (a.ntiles > 0) {
     const dim3 grid(static_cast<unsigned>((a.ntiles + 3) / 4));
 #define EH_TILES(A_)                                                                                     \

@@ -109,7 +109,12 @@ struct SparseArgs {
   // LDS after its tiles; nullptr: heads / tails go through memory to csc_spans
   const int4* wspan;
   const int* wspan_ptr;         // [nwg + 1]
+  // shared message rows (ops/grad.py SparseGradPlan units): the column pass writes sub-block p's sums to
+  // rows dst[p][0..] of Gs (at most kSparseMaxDst, -1 padded) instead of row p: every replica of an
+  // identical message (an FRC / AGC group's members) gets its row from the one pass over its rows
+  const int* dst;
 };
+constexpr int kSparseMaxDst = 4;
 hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const void* beta, hipStream_t st,
                               const int* gate = nullptr);
 

@@ -228,7 +228,7 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
                                           std::optional<Tensor> wg, int64_t u_lds, std::optional<Tensor> Gs,
                                           std::optional<Tensor> sub_begin, std::optional<Tensor> runs,
                                           std::optional<Tensor> tkeys, std::optional<Tensor> wspan,
-                                          std::optional<Tensor> wspan_ptr) {
+                                          std::optional<Tensor> wspan_ptr, std::optional<Tensor> dst) {
   for (auto* t : {&y, &u, &crow, &col_ptr, &tiles, &part_entry0, &part_row0, &part_nnz, &head, &tail, &span, &empty})
     need_gpu(*t, "sparse plan operand");
   need(tiles.scalar_type() == at::kInt && tiles.dim() == 2 && tiles.size(1) == 4, "tiles: int32 [n, 4]");
@@ -360,6 +360,18 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
       g->keep.push_back(*wspan);
       g->keep.push_back(*wspan_ptr);
     }
+  }
+  if (dst) {  // shared message rows of merged FRC / AGC units (ops/grad.py SparseGradPlan.units)
+    need_gpu(*dst, "dst");
+    need(!sub_begin && wg && a.nspan == 0, "shared message rows need unblocked units and the row-blocked column pass");
+    need(dst->scalar_type() == at::kInt && dst->dim() == 2 && dst->size(0) == nparts &&
+             dst->size(1) == eh::kSparseMaxDst,
+         "dst: int32 [units, 4]");
+    const Tensor dc = dst->cpu();
+    const int* D = dc.data_ptr<int>();
+    for (int64_t k = 0; k < dst->numel(); ++k) need(D[k] >= -1 && D[k] < 4096, "dst: message rows or -1");
+    a.dst = dst->data_ptr<int>();
+    g->keep.push_back(*dst);
   }
   if (sub_begin) {
     need(Gs.has_value(), "sub-blocks need their Gs buffer");
@@ -2198,7 +2210,7 @@ void bind_engine(py::module& m) {
                   py::arg("nparts"), py::arg("d"), py::arg("ld"), py::arg("wg") = py::none(), py::arg("u_lds") = 0,
                   py::arg("Gs") = py::none(), py::arg("sub_begin") = py::none(),
                   py::arg("runs") = py::none(), py::arg("tkeys") = py::none(), py::arg("wspan") = py::none(),
-                  py::arg("wspan_ptr") = py::none())
+                  py::arg("wspan_ptr") = py::none(), py::arg("dst") = py::none())
       .def("set_encode",
            [](GradLauncher& g, const Tensor& ptr, const Tensor& idx, const Tensor& coef, const Tensor& Gb) {
              for (auto* t : {&ptr, &idx, &coef, &Gb}) need_gpu(*t, "encode operand");

@@ -83,6 +83,10 @@ def build_parser() -> argparse.ArgumentParser:
                         "partition shards (bandwidth, no physical straggler tolerance)")
     g.add_argument("--no-integrity", action="store_true",
                    help="IPC messages without (round, rank, checksum) tags (A/B runs only)")
+    g.add_argument("--dedicated-master", action="store_true",
+                   help="rank 0 runs the master only, the workers go on ranks 1..N-1 (the reference topology)")
+    g.add_argument("--device-records", action="store_true",
+                   help="keep per-round device stamps of every rank (put landed, spins, gates, beta puts)")
     return p
 
 
@@ -113,7 +117,8 @@ def parse(argv: List[str]):
                     checkpoint_every=a.checkpoint_every, checkpoint_path=a.checkpoint_path, resume=a.resume, trace=a.trace, verify_beta=a.verify_beta,
                     transport=a.transport, share_partitions=a.share_partitions, device_loop=a.device_loop,
                     tie_break=a.tie_break, tie_seed=a.tie_seed, shard=a.shard,
-                    integrity=not a.no_integrity, delay_on=a.delay_on, slow_ranks=parse_slow_ranks(a.slow_ranks))
+                    integrity=not a.no_integrity, delay_on=a.delay_on, slow_ranks=parse_slow_ranks(a.slow_ranks),
+                    dedicated_master=a.dedicated_master, device_records=a.device_records)
     return cfg, a
 
 

@@ -644,6 +644,14 @@ class SparseGradPlan:
     # leaves ELL one row per thread gathering from L2, which the CSR pass (16 lanes per row) beats on
     # the real shapes (amazon 33.1 vs 37.9 us, kc_house 18.4 vs 18.9: profiles/round4/r5a/breakdown.txt)
     ELL_LDS_BYTES = 148 * 1024
+    # FRC / AGC units: a group's replicas all send the SAME message (the sum of the group's partitions,
+    # coefficient 1: ref src/replication.py:56-68), so the device stacks the group's partitions into one
+    # unit and the column pass writes the unit's sums straight into every member's message row
+    # (SparseArgs::dst) -- no per-partition rows and no encoding launch, the naive plan's work.  Units
+    # up to this many rows are staged whole (grad_sparse.hip csc_tiles_lds STAGE 8); larger ones keep the
+    # partition basis and the encoding.
+    UNIT_ROWS = 8192
+    MAX_DST = 4  # grad_sparse.hip kSparseMaxDst: replicas per unit
 
     def __init__(self, messages: Sequence[Sequence[Tuple[int, float]]], partitions: Dict[int, Tuple[object, np.ndarray]],
                  prec: Precision, loss: int, d: int, device="cpu", use_ell="auto"):
@@ -686,14 +694,49 @@ class SparseGradPlan:
         self.idx16 = False
         self.row16 = False
         self.identity = False  # set by _build_device: messages are the distinct partitions themselves
+        self.units = None  # set on the GPU for FRC / AGC groups (UNIT_ROWS): the message sets, stacked
         if self.device.type == "cuda":
-            self._build_device(X, use_ell)
+            self.units = self._merge_units()
+            if self.units is not None:  # the device's rows in unit order: each unit's partitions stacked
+                dev_blocks = []
+                for u in self.units:
+                    mats = [self.blocks[pos[p]] for p in u]
+                    Au = sps.vstack([m[0] for m in mats], format="csr")
+                    Au = sps.csr_matrix((Au.data, Au.indices, Au.indptr), shape=(Au.shape[0], d))
+                    Au.sort_indices()
+                    dev_blocks.append((Au, np.concatenate([m[1] for m in mats])))
+                X = sps.vstack([b[0] for b in dev_blocks], format="csr")
+                X = sps.csr_matrix((X.data, X.indices, X.indptr), shape=(X.shape[0], d))
+                X.sort_indices()
+            else:
+                dev_blocks = self.blocks
+            self._build_device(X, use_ell, dev_blocks)
+
+    def _merge_units(self):
+        """The FRC / AGC message sets as device units (see UNIT_ROWS), or None: every coefficient 1, some
+        set used by several messages, any two sets identical or disjoint, at most MAX_DST messages per
+        set, and every unit at most UNIT_ROWS rows."""
+        sets = [tuple(sorted(p for p, _ in m)) for m in self.messages]
+        if not sets or any(float(c) != 1.0 for m in self.messages for _, c in m) or len(set(sets)) == len(sets):
+            return None
+        units = sorted(set(sets))
+        seen = set()
+        for u in units:
+            if seen & set(u) or sets.count(u) > self.MAX_DST:
+                return None
+            seen |= set(u)
+        pos = {p: j for j, p in enumerate(self.basis)}
+        if max(sum(self.blocks[pos[p]][0].shape[0] for p in u) for u in units) > self.UNIT_ROWS:
+            return None
+        return units
 
     # ---- device tables ----------------------------------------------------------------------
-    def _build_device(self, X, use_ell: bool):
+    def _build_device(self, X, use_ell: bool, dev_blocks):
+        """dev_blocks: the device's (matrix, labels) units in row order -- the distinct partitions, or the
+        merged FRC / AGC units (self.units)."""
         dev, acc = self.device, self.prec.acc
         npacc = np.float64 if acc == torch.float64 else np.float32
-        ys = np.concatenate([b[1] for b in self.blocks]) if self.blocks else np.zeros(0)
+        ys = np.concatenate([b[1] for b in dev_blocks]) if dev_blocks else np.zeros(0)
         self.y = torch.from_numpy(ys.astype(npacc)).to(dev)
         self.u = torch.zeros(max(1, self.nrows), dtype=acc, device=dev)
         nnz_row = np.diff(X.indptr)
@@ -733,7 +776,9 @@ class SparseGradPlan:
         rb = self.ROW_BLOCK_ROWS
         wgt = self.WG_TILES
         self.wg_tiles = wgt or self.MAX_WG_TILES
-        t = self.csc_tables([b[0] for b in self.blocks], self.d, self.TILE, row_block=rb, wg_tiles=self.wg_tiles,
+        if self.units is not None:  # a unit is one sub-block of up to UNIT_ROWS rows (csc_tiles_lds STAGE 8)
+            rb = max(rb, max(b[0].shape[0] for b in dev_blocks))
+        t = self.csc_tables([b[0] for b in dev_blocks], self.d, self.TILE, row_block=rb, wg_tiles=self.wg_tiles,
                             wg_spans=self.WG_SPANS, slots=0 if wgt else self.WG_SLOTS)
         self.row_block = rb
         self.nsub = t["nsub"]
@@ -758,7 +803,7 @@ class SparseGradPlan:
         self.wg_spans = bool(t["wg_spans"]) and len(t["wg"]) > 0
         self.wspan = torch.from_numpy(t["wspan"]).to(dev) if self.wg_spans else None
         self.wspan_ptr = torch.from_numpy(t["wspan_ptr"]).to(dev) if self.wg_spans else None
-        blocked = self.nsub != len(self.basis)  # some partition spans several sub-blocks
+        blocked = self.nsub != len(dev_blocks)  # some partition spans several sub-blocks
         self.sub_begin = torch.from_numpy(t["sub_begin"]).to(dev) if blocked else None
         self.Gs = torch.zeros((self.nsub, self.ld), dtype=acc, device=dev) if blocked else None
         ptr, idx, coef = self._enc
@@ -771,6 +816,17 @@ class SparseGradPlan:
         # (out_buffer, the trainer's G ring); run() checks it the first time it sees a buffer.
         self.identity = (not blocked and len(self.messages) == len(self.basis)
                          and all(m == [(self.basis[i], 1.0)] for i, m in enumerate(self.messages)))
+        self.dst = None
+        if self.units is not None:
+            if blocked:
+                raise AssertionError("a merged unit must be one sub-block")
+            sets = [tuple(sorted(p for p, _ in m)) for m in self.messages]
+            dst = np.full((len(self.units), self.MAX_DST), -1, dtype=np.int32)
+            for j, u in enumerate(self.units):
+                rows = [i for i, s in enumerate(sets) if s == u]
+                dst[j, : len(rows)] = rows
+            self.dst = torch.from_numpy(dst).to(dev)
+            self.identity = True  # the column pass writes the messages themselves
         self.enc_ptr = torch.tensor(ptr, dtype=torch.int32, device=dev)
         self.enc_idx = torch.tensor(idx or [0], dtype=torch.int32, device=dev)[: len(idx)]
         self.enc_coef = torch.tensor(coef or [0.0], dtype=torch.float64, device=dev)[: len(coef)]
@@ -959,7 +1015,7 @@ class SparseGradPlan:
                                              self.span, empty, self.nsub, self.d, self.ld,
                                              wg=self.wg if len(self.wg) else None, u_lds=self.u_lds, Gs=self.Gs,
                                              sub_begin=self.sub_begin, runs=self.runs, tkeys=self.tkeys,
-                                             wspan=self.wspan, wspan_ptr=self.wspan_ptr)
+                                             wspan=self.wspan, wspan_ptr=self.wspan_ptr, dst=self.dst)
             if not self.identity:
                 L.set_encode(self.enc_ptr, self.enc_idx, self.enc_coef, self.Gb)
             self._launcher = L

@@ -253,6 +253,41 @@ def test_sparse_replicas_share_reads_and_match_per_message(native):
         assert np.max(np.abs(got - ref)) / np.max(np.abs(ref)) < 1e-11
 
 
+@pytest.mark.parametrize("prec_name,tol", [("fp64", 1e-11), ("fp32", 1e-4)])
+@pytest.mark.parametrize("rows,use_ell", [(1500, True), (3100, True), (3100, False)])
+def test_sparse_frc_units_write_every_replica(prec_name, tol, rows, use_ell, native):
+    """FRC / AGC messages (each group's members send the sum of the group's partitions, coefficient 1,
+    ref src/replication.py:56-68): the device stacks a group's partitions into one unit, the column pass
+    stages the whole unit (<= 4096 rows: 4 residuals per thread, up to 8192: 8) and writes its sums into
+    every member's message row -- no partition rows, no encoding launch.  Every row against the scipy
+    oracle, bitwise run to run, through plan.run and the native launcher, padding columns untouched."""
+    from erasurehead_amd.data.synthetic import onehot_partitions
+
+    prec = get_precision(prec_name)
+    parts_l, _, d = onehot_partitions(4 * rows, 1800, 9, 4, seed=6)
+    parts = {p: xy for p, xy in enumerate(parts_l)}
+    msgs = [[(0, 1.0), (1, 1.0)], [(0, 1.0), (1, 1.0)], [(2, 1.0), (3, 1.0)], [(2, 1.0), (3, 1.0)], [(2, 1.0), (3, 1.0)]]
+    plan = SparseGradPlan(msgs, parts, prec, LOGISTIC, d, device=DEV, use_ell=use_ell)
+    assert plan.units == [(0, 1), (2, 3)] and plan.identity and plan.sub_begin is None
+    assert plan.dst.cpu().tolist() == [[0, 1, -1, -1], [2, 3, 4, -1]]
+    rng = np.random.RandomState(2)
+    b = rng.randn(d) * 0.1
+    beta = torch.zeros(prec.ld(d), dtype=prec.acc, device=DEV)
+    beta[:d] = torch.from_numpy(b).to(prec.acc)
+    bh = beta[:d].double().cpu().numpy()
+    G1, G2 = plan.out_buffer()[0], plan.out_buffer()[0]
+    plan.run(beta, G1)
+    plan.native_launcher().launch(beta, G2)
+    torch.cuda.synchronize()
+    assert torch.equal(G1, G2)
+    for s_, m in enumerate(msgs):
+        ref = sum(logistic_grad(parts[p][0], parts[p][1], bh, c) for p, c in m)
+        got = G1[s_, :d].double().cpu().numpy()
+        assert np.max(np.abs(got - ref)) / np.max(np.abs(ref)) < tol, s_
+    assert torch.equal(G1[0], G1[1]) and torch.equal(G1[2], G1[4])
+    assert torch.all(G1[:, d:] == 0)
+
+
 @pytest.mark.parametrize("rule", ["GD", "AGD"])
 @pytest.mark.parametrize("msg_dtype", [torch.float64, torch.float32])
 def test_combine_update(rule, msg_dtype, native):

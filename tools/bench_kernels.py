@@ -273,7 +273,9 @@ def sparse_cases(out, names=("covtype", "kc_house_data", "amazon-dataset"), ell_
         parts_l, _, dd = onehot_partitions(n, d, f, W, seed=1)
         parts = {p: xy for p, xy in enumerate(parts_l)}
         layouts = {"naive": [[(w, 1.0)] for w in range(W)],
-                   "s1_replicas": [[(w, 1.0), ((w + 1) % W, 1.0)] for w in range(W)]}  # 8 workers, 2 partitions each
+                   "s1_replicas": [[(w, 1.0), ((w + 1) % W, 1.0)] for w in range(W)],  # 8 workers, 2 partitions each
+                   # FRC / AGC s = 1: groups {2g, 2g + 1} send the sum of both partitions (merged units when small)
+                   "frc_s1": [[(w - w % 2, 1.0), (w - w % 2 + 1, 1.0)] for w in range(W)]}
         for (layout, msgs), use_ell in [(x, e) for x in layouts.items() for e in ((True,) if ell_only else (True, False))]:
             plan = SparseGradPlan(msgs, parts, prec, LOGISTIC, dd, device="cuda", use_ell=use_ell)
             beta = torch.randn(prec.ld(dd), device="cuda", dtype=torch.float64) * 0.1
@@ -281,6 +283,7 @@ def sparse_cases(out, names=("covtype", "kc_house_data", "amazon-dataset"), ell_
             ms = _time(lambda: plan.run(beta, G))
             kern = ("ell16" if plan.idx16 else "ell32") if plan.ell else "csr"
             r = {"kernel": f"grad_sparse ({kern} rows, CSC{16 if plan.row16 else 32} tiles)", "layout": layout,
+                 "units": len(plan.units) if plan.units else None, "identity": bool(plan.identity),
                  "dataset_shape": name, "rows_distinct": plan.nrows, "rows_in_messages": plan.msg_rows,
                  "nnz": int(plan.nnz), "d": dd, "ms": ms, "nnz_per_us": plan.nnz / (ms * 1e3),
                  "stream_bytes": plan.stream_bytes, "TBps": plan.stream_bytes / (ms * 1e9)}
