@@ -209,10 +209,12 @@ struct PutDesc {
   const unsigned long long* beta_flag;
   unsigned long long stale_next;
   int strict;  // set by the launchers from strict_release() (common.h block_release_system)
-  // Landing stamp (nullptr = off): the last block writes wall_clock64 here just before the flag's
-  // release, so a receiver that sees the flag reads when the put landed on the sender's clock (the
-  // collector orders physically late ranks' messages by it: csrc/runtime/collector.h "Device times").
-  // stamp: the receiver-visible slot (host-mapped ring); stamp_log: the sender's own per-round record.
+  // Landing stamp (nullptr = off): the last block writes {value, wall_clock64} here just before the
+  // flag's release, so a receiver that sees the flag at `value` reads when that put landed on the
+  // sender's clock (the collector orders physically late ranks' messages by it: csrc/runtime/
+  // collector.h "Device times"); the value tells a slot of this round from one an older round (or a
+  // skipped round) left.  stamp: the receiver-visible 16-byte slot (host-mapped ring); stamp_log: the
+  // sender's own per-round record (ticks only).
   long long* stamp;
   long long* stamp_log;
 };
@@ -221,7 +223,10 @@ struct PutDesc {
 __device__ __forceinline__ void put_stamp(const PutDesc& p) {
   if (!p.stamp && !p.stamp_log) return;
   const long long t = static_cast<long long>(wall_clock64());
-  if (p.stamp) *p.stamp = t;
+  if (p.stamp) {
+    p.stamp[0] = static_cast<long long>(p.value);
+    p.stamp[1] = t;
+  }
   if (p.stamp_log) *p.stamp_log = t;
 }
 // The next round's gate word (one thread of the launch calls it).

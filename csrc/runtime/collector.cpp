@@ -205,8 +205,12 @@ void Collector::poll_events(double t) {
         f[p.round] = finish_of(p.worker, p.round - 1);
         continue;
       }
-      // the landing stamp was written before the flag's release: after the acquire above it is this round's
-      mark_seen(id, p.stamp ? p.clk.to_host(static_cast<double>(__atomic_load_n(p.stamp, __ATOMIC_RELAXED))) : t);
+      // the landing stamp was written before the flag's release: after the acquire above the slot holds this
+      // round's put iff the flag reads exactly its value and the slot names that value
+      double ts = t;
+      if (p.stamp && v == p.fval && static_cast<uint64_t>(__atomic_load_n(p.stamp, __ATOMIC_RELAXED)) == p.fval)
+        ts = p.clk.to_host(static_cast<double>(__atomic_load_n(p.stamp + 1, __ATOMIC_RELAXED)));
+      mark_seen(id, ts);
       continue;
     }
     int hit = -1;

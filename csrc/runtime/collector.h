@@ -127,7 +127,9 @@ class Collector {
   int add_host_probe(int worker, int part, int round, double delay, bool physical = false);
   // IPC mailbox probe: arrived once the 64-bit flag at `flag_addr` (shared host memory,
   // release-stored by the sending GPU) reaches `value` (csrc/runtime/ipc.cpp).  stamp_addr (0 = host
-  // poll time): the put's landing stamp on the sender's clock `clk` (see "Device times").
+  // poll time): the put's {value, landing ticks} slot on the sender's clock `clk` (see "Device times");
+  // used only when the flag reads exactly `value` and the slot names it (a skipped round leaves an
+  // older round's slot, an end-of-run signal no slot at all: those fall back to the poll time).
   int add_flag_probe(int worker, int part, int round, uintptr_t flag_addr, uint64_t value, double delay,
                      bool physical = false, uintptr_t stamp_addr = 0, DeviceClock clk = {});
   // Every probe so far: (worker, part, round, seen time from its round's start, outcome).
@@ -179,7 +181,7 @@ class Collector {
     bool physical;
     bool skipped;
     double start;  // virtual start (seen virtual probes)
-    const int64_t* stamp = nullptr;  // device landing stamp (flag probes; see "Device times")
+    const int64_t* stamp = nullptr;  // {flag value, device landing ticks} slot (flag probes; see "Device times")
     DeviceClock clk{};
     hipEvent_t ref_ev = nullptr;     // reference event of a device-timed event probe
     double ref_t = 0.0;

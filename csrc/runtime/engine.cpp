@@ -695,7 +695,7 @@ class MasterPump {
     remote_delays_ = delays;
   }
   // Device times of physically late ranks' messages (collector.h "Device times").  IPC: worker rank r's
-  // puts write their landing stamps into ring slots [r][i % ring] of shared host memory (ring_host) on
+  // puts write {round + 1, landing ticks} into 16-byte ring slots [r][i % ring] of shared host memory (ring_host) on
   // that rank's GPU clock clocks[r] = (tick0, t0, hz).  p2p: the receive events become timing events,
   // read against a reference event of this GPU calibrated against the host clock here.
   void set_device_times(const std::vector<std::tuple<int, double, double, double>>& clocks, uintptr_t ring_host,
@@ -847,7 +847,7 @@ class MasterPump {
       eh::DeviceClock clk{};
       const int r = row_rank_[m.row];
       if (physical && dev_times_ && ring_host_ && clocks_.count(r)) {  // its landing time on its own GPU clock
-        stamp = ring_host_ + sizeof(int64_t) * (static_cast<uintptr_t>(r) * ring_ + i % ring_);
+        stamp = ring_host_ + 2 * sizeof(int64_t) * (static_cast<uintptr_t>(r) * ring_ + i % ring_);
         clk = clocks_.at(r);
       }
       col_->add_flag_probe(m.w, m.p, i, m.flag, static_cast<uint64_t>(i + 1), dr[m.w], physical, stamp, clk);
@@ -1731,9 +1731,9 @@ class WorkerPump {
   }
   bool skip_stale() const { return skip_flag_ != nullptr || skip_comm_; }
 
-  // IPC: every message put writes its landing stamp into this rank's ring of shared host memory, slot
-  // i % ring (ring_dev: device address of the ring), read by the master's collector (collector.h
-  // "Device times").
+  // IPC: every message put writes {round + 1, landing ticks} into this rank's ring of shared host memory,
+  // 16-byte slot i % ring (ring_dev: device address of the ring), read by the master's collector
+  // (collector.h "Device times").
   void set_stamp_ring(uintptr_t ring_dev, int ring) {
     need(ring_dev == 0 || ring >= 1, "stamp ring must have >= 1 slot");
     ring_dev_ = ring_dev;
@@ -1862,7 +1862,7 @@ class WorkerPump {
         pd.rank = static_cast<unsigned int>(rank_);
         pd.corrupt = sabotage("msg", rank_, i) ? 1 : 0;
       }
-      if (ring_dev_) pd.stamp = reinterpret_cast<long long*>(ring_dev_) + i % ring_;
+      if (ring_dev_) pd.stamp = reinterpret_cast<long long*>(ring_dev_) + 2 * (i % ring_);
       pd.stamp_log = rec_at(i, 0);
       if (timing_) record_t(i, 0);
       for (int k = 1; k < repeat_; ++k) hcheck(g_->launch(beta, g, stream_, gate), "worker gradient (slow rank)");

@@ -1019,7 +1019,7 @@ class Trainer:
         pump.set_timing(bool(cfg.instrument))
         pump.set_repeat(self.repeat)
         if tx.name == "ipc":  # landing stamps of this rank's puts, read by the master's collector
-            pump.set_stamp_ring(tx.flags.dev_addr(tx.stamp_base + env.rank * tx.K), tx.K)
+            pump.set_stamp_ring(tx.flags.dev_addr(tx.stamp_base + 2 * env.rank * tx.K), tx.K)
         if cfg.device_records:
             pump.set_records(True)
         if self.physical:

@@ -446,8 +446,9 @@ class IpcTransport(Transport):
     Flag layout (one ShmFlags array created by the master): index r (1..world-1) = the
     round counter of beta pushed to rank r (value i+1 <=> beta of round i is in the inbox),
     index world + r = the round counter of rank r's messages in the master mailbox, and from
-    ``stamp_base`` on one ring of K landing stamps per rank (slot stamp_base + r * K + i % K: when rank
-    r's put of round i landed, on its GPU clock; csrc/runtime/collector.h "Device times").
+    ``stamp_base`` on one ring of K landing stamps per rank (two words at stamp_base + 2 (r * K + i % K):
+    round i + 1 and when rank r's put of round i landed, on its GPU clock; csrc/runtime/collector.h
+    "Device times").
     """
 
     name = "ipc"
@@ -487,7 +488,7 @@ class IpcTransport(Transport):
         self.inbox_tag_off = (self.R + 1) * self.ld * self.es
         ibytes = self.inbox_tag_off + (self.R + 1) * TAG_BYTES
         self.stamp_base = 2 * env.world + 1
-        nflags = self.stamp_base + env.world * self.K
+        nflags = self.stamp_base + 2 * env.world * self.K
         if env.is_master:
             name = "/eh_" + uuid.uuid4().hex[:16]
             rbytes = self.K * max(1, self.n_rem) * (self.ld * self.es + TAG_BYTES)

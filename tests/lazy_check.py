@@ -67,16 +67,21 @@ def check_lazy_device(arrivals, records, owner, skipped, delays, rule, k, groups
             assert early_late and all(last - p[3] <= VIS for p in early_late), (i, order, dec, mine)
             out["inversions"] += 1
         out["rounds"] += 1
-        # the collector's order is the workers' own landing order (IPC: the stamps it read)
+        # the collector's order of the round's decoded and late messages is the workers' own landing order
+        # (IPC: the stamps it read; a stale message may have been seen after its sender's next put, at the
+        # host's poll time, and a rank that skipped the round has no landing stamp)
         if transport == "ipc":
-            land = {w: recs[rank_of[w]]["rounds"][i][0] for w in order}
+            cur = [int(p[0]) for p in mine if p[4] in (DECODED, LATE)]
+            land = {w: recs[rank_of[w]]["rounds"][i][0] for w in cur}
             assert all(v >= 0 for v in land.values()), (i, land)
-            assert order == sorted(order, key=lambda w: (land[w], w)), (i, order, land)
+            assert cur == sorted(cur, key=lambda w: (land[w], w)), (i, cur, land)
             out["order"] += 1
             # the lazy drain: some message of this round landed after the next beta had left
             if i + 1 < R and bp[i + 1][1] >= 0:
-                out["tail_after_next_beta"] += sum(1 for p in mine if p[4] != DECODED
-                                                   and land[int(p[0])] > bp[i + 1][1])
+                for p in mine:
+                    w = int(p[0])
+                    lw = recs[rank_of[w]]["rounds"][i][0]
+                    out["tail_after_next_beta"] += int(p[4] != DECODED and lw >= 0 and lw > bp[i + 1][1])
     for r, rec in recs.items():
         if r == 0:
             continue

@@ -306,10 +306,15 @@ def main():
     ap.add_argument("--sparse-shapes", default="covtype,kc_house_data,amazon-dataset", help="--only sparse: datasets")
     ap.add_argument("--ell-only", action="store_true", help="--only sparse: skip the CSR row pass")
     ap.add_argument("--wg-tiles", type=int, default=0, help="--only sparse: tiles per column-pass workgroup (A/B)")
+    ap.add_argument("--row-block", type=int, default=0, help="--only sparse: column-pass sub-block rows (A/B, <= 8192)")
     ap.add_argument("--wg-slots", type=int, default=0, help="--only sparse: workgroup budget of the chip-sized chunks (A/B)")
     ap.add_argument("--no-wg-spans", action="store_true",
                     help="--only sparse: whole 16-tile chunks and the csc_spans launch (A/B of SparseGradPlan.WG_SPANS)")
     a = ap.parse_args()
+    if a.row_block:
+        from erasurehead_amd.ops import SparseGradPlan
+
+        SparseGradPlan.ROW_BLOCK_ROWS = a.row_block  # > 4096: 8 staged residuals per thread (csc_tiles_lds STAGE)
     if a.no_wg_spans or a.wg_tiles or a.wg_slots:
         from erasurehead_amd.ops import SparseGradPlan
 

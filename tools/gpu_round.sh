@@ -83,6 +83,15 @@ for s in "${STAGES[@]}"; do
       run 600 sparse.log python -u tools/bench_kernels.py --only sparse --out "$OUT/sparse.jsonl"
       run 600 prof_sparse.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_sparse" -o run -- \
         python tools/bench_kernels.py --only sparse --out /tmp/sparse_prof.jsonl ;;
+    sparseab)  # sparse gradients at the real shapes (naive / cyclic-style / FRC layouts), then covtype with
+               # 8192-row sub-blocks (2 and 1 workgroups per CU), then the sparse suite rows
+      run 600 sparse.log python -u tools/bench_kernels.py --only sparse --out "$OUT/sparse.jsonl"
+      run 300 sparse_rb8k.log python -u tools/bench_kernels.py --only sparse --sparse-shapes covtype --ell-only \
+        --row-block 8192 --out "$OUT/sparse_rb8k.jsonl"
+      run 300 sparse_rb8k_s256.log python -u tools/bench_kernels.py --only sparse --sparse-shapes covtype --ell-only \
+        --row-block 8192 --wg-slots 256 --out "$OUT/sparse_rb8k_s256.jsonl"
+      run 900 suite_sparse.log python -u tools/bench_suite.py --out "$OUT/suite" \
+        --only naive_covtype,agc_covtype,ls_kc_house_naive,ls_kc_house_agc_k6,naive_amazon,agc_amazon ;;
     rccl)  # the RCCL self-loop comm path under the kernel tracer (RCCL kernel names in the stats)
       run 600 prof_rccl.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_rccl" -o run -- \
         python -u -m pytest tests/test_rccl_gpu.py -k self_loop -x -q --timeout 120 --timeout-method thread ;;
