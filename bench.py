@@ -107,6 +107,7 @@ def parse(argv=None):
                     help="N = 1 straggler block: mean of the Exp virtual delays (the reference's 0.5 s scaled "
                          "down 100x; every delay floor scales linearly in it)")
     ap.add_argument("--slab-mode", type=int, default=None, help=argparse.SUPPRESS)  # A/B of the slab reduction form
+    ap.add_argument("--mfma-stream", type=int, default=None, help=argparse.SUPPRESS)  # A/B of the bf16 MFMA stream
     ap.add_argument("--no-straggler", action="store_true",
                     help="skip the straggler runs (N = 1: the virtual-delay block; N > 1: the reference-topology "
                          "and physically-late-rank sub-runs)")
@@ -157,6 +158,10 @@ def main(argv=None) -> int:
         from erasurehead_amd._ext import native
 
         native().set_slab_reduce_mode(a.slab_mode)
+    if a.mfma_stream is not None and torch.cuda.is_available():
+        from erasurehead_amd._ext import native
+
+        native().set_mfma_stream(bool(a.mfma_stream))
 
     def make_cfg(rounds: int, naive: bool = a.naive, ver: int = a.coded_ver, **kw) -> RunConfig:
         opts = dict(add_delay=a.add_delay, num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234,

@@ -423,6 +423,39 @@ def test_fused_slab_reduction_is_bitwise_the_two_stages(prec_name, d, rows, nati
     assert torch.count_nonzero(out[1]) > 0
 
 
+@pytest.mark.parametrize("d,sizes", [(1000, [3000, 2000, 1000]), (1000, [37, 5, 70]), (504, [900, 33, 64]),
+                                     (256, [129, 64, 7])])
+@pytest.mark.parametrize("loss", [LOGISTIC, LEAST_SQUARES])
+def test_bf16_mfma_vgpr_stream_is_bitwise_the_lds_ring(d, sizes, loss, native):
+    """grad_stream_mfma (each wave streams its column slice into registers, two stages in flight, and
+    keeps a private LDS image only for GEMM2's transposing reads) against the LDS-DMA stage ring: the
+    same MFMAs on the same operands in the same order, so bitwise the same messages -- bundles of 1-3
+    replicas, partial last stages, d below a full wave slice -- and against message-major order."""
+    prec = get_precision("bf16")
+    rng = np.random.RandomState(d + sum(sizes))
+    parts, _ = _parts(rng, sizes, d, prec)
+    msgs = [[(0, 1.0), (1, 1.0)]] * 3 + [[(1, 0.5), (2, -1.0)]] * 2 + [[(2, 1.0)]]
+    a = DenseGradPlan(msgs, parts, prec, loss, d)
+    b = DenseGradPlan(msgs, parts, prec, loss, d, choice=MESSAGE_MAJOR)
+    assert a.choice.kind == "mfma"
+    beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
+    out = []
+    try:
+        for on in (False, True):
+            native.set_mfma_stream(on)
+            G = a.out_buffer()[0]
+            a.native_launcher().launch(beta, G)
+            torch.cuda.synchronize()
+            out.append(G)
+    finally:
+        native.set_mfma_stream(False)
+    assert torch.equal(out[0], out[1])
+    Gb = b.out_buffer()[0]
+    b.run(beta, Gb)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out[1], Gb, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("prec_name", ["fp64", "fp32", "bf16"])
 def test_dense_grad_staged_is_the_replica_default(prec_name, native):
     """Co-located replicas in bundles of more than 3 default to the LDS-staged bundles for fp64/fp32

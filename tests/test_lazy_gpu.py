@@ -135,9 +135,11 @@ def _lazy_run(world, case, over, tmp_path, **env):
     (4, (1, 0, 0, 4, 1, 0), "count", 2, [0, 1, 2], 0.05, 16, "ipc"),                  # cyclic W=3 s=1
     (5, (1, 0, 3, 5, 1, 3), "frc", 3, [0, 0, 1, 1], 0.05, 16, "ipc"),                 # AGC W=4 s=1 k=3
     (9, (1, 0, 3, 9, 2, 6), "frc", 6, [0, 0, 0, 1, 1, 1, 2, 2], 0.05, 18, "ipc"),     # AGC W=8 s=2 k=6
-    # the same over stream-ordered p2p (loopback: RCCL's code path)
+    # the same over stream-ordered p2p (loopback: RCCL's code path).  9 processes parking device-side waits
+    # on ONE GPU oversubscribe its hardware queues, whose rotation paces the rounds by tens of ms: longer
+    # delays there, so ranks still fall behind (the checks themselves need no margin)
     (4, (1, 0, 0, 4, 1, 0), "count", 2, [0, 1, 2], 0.05, 16, "loopback"),
-    (9, (1, 0, 3, 9, 2, 6), "frc", 6, [0, 0, 0, 1, 1, 1, 2, 2], 0.05, 16, "loopback"),
+    (9, (1, 0, 3, 9, 2, 6), "frc", 6, [0, 0, 0, 1, 1, 1, 2, 2], 0.3, 14, "loopback"),
 ])
 def test_lazy_drain_physically_late_ranks(world, case, rule, k, groups, mean, R, transport, tmp_path):
     """--delay-on worker --drain lazy, the reference topology (rank 0 the master only, one logical worker

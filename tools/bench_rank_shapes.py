@@ -80,7 +80,7 @@ def build_plan(n_gpus: int, precision: str, shard: str = "partition", rows_overr
 
 
 def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0, fill: bool = False,
-        slab_mode: int = 1, mfma_rows: int = 32, mfma_probe: int = 0) -> dict:
+        slab_mode: int = 1, mfma_rows: int = 32, mfma_probe: int = 0, mfma_stream: int = 0) -> dict:
     import numpy as np
     import torch
 
@@ -89,6 +89,7 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
     native().set_slab_reduce_mode(slab_mode)
     native().set_mfma_stage_rows(mfma_rows)
     native().set_mfma_probe(mfma_probe)  # (1 / 2: timing probes, not a gradient)
+    native().set_mfma_stream(bool(mfma_stream))
     plan, beta, G = build_plan(n_gpus, precision, shard, rows_override, fill)
     r, mode = plan.rank, plan.shard_mode
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -107,7 +108,7 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
             "shards": plan.n_shards, "bundle_rows": plan.bundle_rows, "kernel": plan.choice.label(), "ntasks": plan.ntasks,
             "kernel_ms": ms, "kernel_ms_min": float(np.min(all_ms)), "kernel_ms_max": float(np.max(all_ms)),
             "distinct_TBps": plan.distinct_bytes / ms / 1e9, "fill": plan.choice.fill,
-            "slab_mode": slab_mode, "mfma_rows": mfma_rows, "mfma_probe": mfma_probe}
+            "slab_mode": slab_mode, "mfma_rows": mfma_rows, "mfma_probe": mfma_probe, "mfma_stream": mfma_stream}
 
 
 def main():
@@ -125,9 +126,11 @@ def main():
     ap.add_argument("--slab-mode", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--mfma-rows", type=int, default=32, help="bf16 MFMA bundles: rows per LDS stage (32 / 16)")
     ap.add_argument("--mfma-probe", type=int, default=0, help="bf16 MFMA timing probe: 1 loads only, 2 compute only")
+    ap.add_argument("--mfma-stream", type=int, default=0, help="bf16 packed bundles through the VGPR stream (A/B)")
     a = ap.parse_args()
     if a.one:
-        print(json.dumps(one(a.one, a.precision, a.shard, a.rows, a.fill, a.slab_mode, a.mfma_rows, a.mfma_probe)),
+        print(json.dumps(one(a.one, a.precision, a.shard, a.rows, a.fill, a.slab_mode, a.mfma_rows, a.mfma_probe,
+                             a.mfma_stream)),
               flush=True)
         return 0
     lines = []
