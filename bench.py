@@ -317,10 +317,17 @@ def main(argv=None) -> int:
     # ---- 2. the same rounds host-driven, instrumented: real wait-for-k path + per-rank breakdown -----
     if not a.no_breakdown:
         headline = reports
-        tr = Trainer(make_cfg(w0 + a.steps, device_loop="off", instrument=True), env)
+        # N > 1: device records too, for the worker half of the round chain (worker_round_start_latency)
+        tr = Trainer(make_cfg(w0 + a.steps, device_loop="off", instrument=True, device_records=env.world > 1), env)
         r = tr.run(timed_start=w0)
         t = env.allreduce_max(r.timed_seconds if env.is_master else tr.worker_timed_seconds)
         reports = env.gather_objects(tr.rank_report())
+        if env.world > 1:
+            lat = worker_round_start_latency(env.gather_objects(tr.device_records), w0)
+            if env.is_master:
+                for rep in reports:
+                    if rep["rank"] in lat:
+                        rep["beta_to_round_start_us"] = lat[rep["rank"]]
         if env.is_master:  # the headline run's device-side master ticks (arbiter: poll / update / release)
             for rep, h in zip(reports, headline):
                 rep.update({f"headline_{k}": v for k, v in h.items()
@@ -465,6 +472,29 @@ def main(argv=None) -> int:
                 f.write(line + "\n")
     env.shutdown()
     return 0
+
+
+def worker_round_start_latency(records, first: int) -> dict:
+    """The worker half of the round chain, per worker rank: median over rounds >= ``first`` of the time
+    from the master's beta(i) put (the stamp right after its put kernels) to the worker's round i start on
+    its own stream (the stamp right behind its beta wait), both GPU clocks mapped to the host clock
+    (Trainer device_records; accurate to the clocks' calibration, a few microseconds).  {} on workers."""
+    if not records or records[0] is None or records[0].get("clock") is None:
+        return {}
+    m = records[0]
+    bp = np.asarray(m["beta_put"], dtype=np.float64)
+    _, k0, t0, hz0 = m["clock"]
+    out = {}
+    for x in records[1:]:
+        if not x or x.get("clock") is None:
+            continue
+        rows = np.asarray(x["rounds"], dtype=np.float64)
+        _, k1, t1, hz1 = x["clock"]
+        lat = [(t1 + (rows[i][9] - k1) / hz1) - (t0 + (bp[i][1] - k0) / hz0)
+               for i in range(first, min(len(bp), len(rows))) if bp[i][1] >= 0 and rows[i][9] >= 0]
+        if lat:
+            out[int(x["rank"])] = round(1e6 * float(np.median(lat)), 2)
+    return out
 
 
 def single_gpu_reference(a, make_cfg, env, free, Trainer, clock_rounds: int):

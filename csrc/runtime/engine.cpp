@@ -1744,7 +1744,9 @@ class WorkerPump {
   //   [1] [2] just before / after the round's put or send      [3] [4] spin start / end (--delay-on worker)
   //   [5] [6] just before / after the stale-round gate (p2p)    [7] [8] just before / after the counter bump
   //   that announces beta(i) landed on this rank (p2p with stale-round skipping)
-  static constexpr int kRec = 9;
+  //   [9] the round's start on this rank's stream: right behind its beta wait (device wait / receive), or
+  //   where the host enqueued the round after its own wait -- the worker half of the master's chain
+  static constexpr int kRec = 10;
   void set_records(bool on) {
     rec_ = on ? at::full({R_ + 1, kRec}, -1, at::TensorOptions().dtype(at::kLong).device(at::Device(at::kCUDA, device_)))
               : Tensor();
@@ -1837,6 +1839,7 @@ class WorkerPump {
         check_integrity();
         if (n_ == 0) continue;
       }
+      stamp(i, 9, stream_);
       const int slot = i % K_;
       const char* beta = static_cast<const char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * ld_ * es_;
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(slot) * g_rows_ * ld_ * es_;
@@ -1935,6 +1938,7 @@ class WorkerPump {
       post_beta_upto(b == R_ ? i + 1 : std::min(i + 1, b - 1));
       hcheck(hipStreamWaitEvent(stream_, bev_[i], 0), "hipStreamWaitEvent(beta)");
       if (n_ == 0) continue;
+      stamp(i, 9, stream_);
       const char* beta = static_cast<const char*>(inbox_.data_ptr()) + static_cast<int64_t>(i) * ld_ * es_;
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(i % K_) * g_rows_ * ld_ * es_;
       // closed iff beta(i+1) landed before this round starts (value i + 2)
@@ -1981,6 +1985,7 @@ class WorkerPump {
       comm_->recv(0, beta, bbytes, stream_);
       hcheck(hipEventRecord(rev_[i % 2], stream_), "hipEventRecord(beta)");
       if (n_ == 0) continue;
+      stamp(i, 9, stream_);
       char* g = static_cast<char*>(G_.data_ptr()) + static_cast<int64_t>(i % K_) * g_rows_ * ld_ * es_;
       if (timing_) record_t(i, 0);
       for (int k = 0; k < repeat_; ++k) hcheck(g_->launch(beta, g, stream_), "worker gradient");
