@@ -161,7 +161,7 @@ def main(argv=None) -> int:
     if a.mfma_stream is not None and torch.cuda.is_available():
         from erasurehead_amd._ext import native
 
-        native().set_mfma_stream(bool(a.mfma_stream))
+        native().set_mfma_stream(int(a.mfma_stream))
 
     def make_cfg(rounds: int, naive: bool = a.naive, ver: int = a.coded_ver, **kw) -> RunConfig:
         opts = dict(add_delay=a.add_delay, num_itrs=rounds, precision=a.precision, data="synthetic", data_seed=1234,

@@ -35,10 +35,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, in
 // churn L2 / MALL.  Measured on a plain 8 KB-row read stream (tools/probes/nt_stream.hip,
 // profiles/round3/nt_stream): 5.92 -> 6.62 TB/s at 8 GB, 5.82 -> 6.57 TB/s at 1 GB; sc0 = default.
 constexpr int kStreamAux = 2;
-template <typename V>
+template <typename V, int AUX = kStreamAux>
 __device__ __forceinline__ V buf_load16(__amdgpu_buffer_rsrc_t rs, int byte_off) {
   static_assert(sizeof(V) == 16, "16-byte vector");
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, kStreamAux);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, AUX);
   V out;
   __builtin_memcpy(&out, &v, 16);
   return out;

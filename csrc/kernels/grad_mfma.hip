@@ -286,11 +286,17 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
 // (two in flight: 128 KB per CU); GEMM1 reads the registers, and the wave copies its slice into a
 // private LDS image only for GEMM2's transposing reads of the SAME columns (its own column tiles).  No
 // other wave reads that image, so the only barriers left are the two around the cross-wave residual.
+// MEASURED SLOWER, kept as an A/B (bench.py --mfma-stream): 0.475 ms with nt loads, 0.345 ms with the
+// default policy, against the ring's 0.316 ms (profiles/round6/bf16ab).  The B-fragment layout fixes every
+// load instruction at 16 rows x 64 bytes -- half of each 128-byte line per request -- which only the
+// LDS-DMA stage (whole rows per wave instruction) avoids.
 constexpr int kMsRowPitch = 272;                 // bytes per row of a wave's image: 256 + 16 (spreads the tr reads)
 constexpr int kMsSlice = 32 * kMsRowPitch;       // one stage's image, per wave
 constexpr int kMsLds = kMfNW * kMsSlice + kMfNW * 4 * 32 * 4 + 16 * 32 * 2;  // images + partial z + residuals
 
-template <int LOSS>
+// AUX: the loads' cache policy -- nt like every X stream, or the default one: a wave's load instruction
+// covers 16 rows x 64 bytes, so the next K step's load reads the other half of each 128-byte line
+template <int LOSS, int AUX>
 __global__ void __launch_bounds__(512)
 grad_stream_mfma(const Segment* __restrict__ segs, const Task* __restrict__ tasks, const float* __restrict__ beta,
                  float* __restrict__ slab, int ld, int R, const int* __restrict__ gate) {
@@ -354,7 +360,7 @@ grad_stream_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
     for (int nt = 0; nt < 2; ++nt) {
       const int row = min(t * 32 + 16 * nt + fi, nrows - 1);
 #pragma unroll
-      for (int kk = 0; kk < kMfKPW; ++kk) xr[nt * kMfKPW + kk] = buf_load16<uint4>(rs, row * rowbytes + coff[kk]);
+      for (int kk = 0; kk < kMfKPW; ++kk) xr[nt * kMfKPW + kk] = buf_load16<uint4, AUX>(rs, row * rowbytes + coff[kk]);
     }
     yv = buf_load_scalar<float>(yrs, 4 * min(t * 32 + (tid & 31), nrows - 1));  // (a flat load would count in lgkmcnt too)
   };
@@ -475,9 +481,10 @@ void set_mfma_probe(int mode) { g_mfma_probe = mode == 1 || mode == 2 ? mode : 0
 // the packed-term form for R <= 4 (default) or the three-MFMA form, for A/B
 static bool g_mfma_pack = true;
 void set_mfma_pack(bool on) { g_mfma_pack = on; }
-// packed bundles (R <= 4) through the VGPR stream (grad_stream_mfma) or the LDS-DMA stage ring, for A/B
-static bool g_mfma_stream = false;
-void set_mfma_stream(bool on) { g_mfma_stream = on; }
+// packed bundles (R <= 4) through the VGPR stream (grad_stream_mfma: 1 nt loads, 2 default-policy loads) or
+// the LDS-DMA stage ring (0), for A/B
+static int g_mfma_stream = 0;
+void set_mfma_stream(int mode) { g_mfma_stream = mode == 1 || mode == 2 ? mode : 0; }
 
 bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds) {
   if (ld < 8 || ld > kMfNW * kMfKPW * 32 || ld % 8) return false;
@@ -506,7 +513,9 @@ hipError_t grad_mfma_launch(int loss, const Segment* segs, const Task* tasks, in
   if (!mfma_geometry(ld, &rows, &pieces, &nstage, &lds)) return hipErrorInvalidValue;
   const bool pack = R <= 4 && g_mfma_pack;
   if (pack && g_mfma_stream && g_mfma_probe == 0) {  // (ld <= 1024, ld % 8 == 0: mfma_geometry above)
-    auto kern = loss == kLogistic ? grad_stream_mfma<kLogistic> : grad_stream_mfma<kLeastSquares>;
+    auto kern = g_mfma_stream == 1 ? (loss == kLogistic ? grad_stream_mfma<kLogistic, kStreamAux>
+                                                        : grad_stream_mfma<kLeastSquares, kStreamAux>)
+                                   : (loss == kLogistic ? grad_stream_mfma<kLogistic, 0> : grad_stream_mfma<kLeastSquares, 0>);
     const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, kMsLds);
     if (ea != hipSuccess) return ea;

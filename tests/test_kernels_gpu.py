@@ -441,15 +441,15 @@ def test_bf16_mfma_vgpr_stream_is_bitwise_the_lds_ring(d, sizes, loss, native):
     beta = torch.randn(a.ld, dtype=prec.acc, device=DEV) * 0.05
     out = []
     try:
-        for on in (False, True):
+        for on in (0, 1, 2):
             native.set_mfma_stream(on)
             G = a.out_buffer()[0]
             a.native_launcher().launch(beta, G)
             torch.cuda.synchronize()
             out.append(G)
     finally:
-        native.set_mfma_stream(False)
-    assert torch.equal(out[0], out[1])
+        native.set_mfma_stream(0)
+    assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])
     Gb = b.out_buffer()[0]
     b.run(beta, Gb)
     torch.cuda.synchronize()

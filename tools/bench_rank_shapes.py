@@ -89,7 +89,7 @@ def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: in
     native().set_slab_reduce_mode(slab_mode)
     native().set_mfma_stage_rows(mfma_rows)
     native().set_mfma_probe(mfma_probe)  # (1 / 2: timing probes, not a gradient)
-    native().set_mfma_stream(bool(mfma_stream))
+    native().set_mfma_stream(int(mfma_stream))
     plan, beta, G = build_plan(n_gpus, precision, shard, rows_override, fill)
     r, mode = plan.rank, plan.shard_mode
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
