@@ -470,7 +470,7 @@ constexpr int kWgWaves = 16;     // waves per column-pass workgroup
 constexpr int kMaxWgTiles = 128;  // tiles per workgroup chunk (ops/grad.py SparseGradPlan.WG_TILES <= this):
                                  // wave w takes the chunk's tiles w, w + 16, ...
 constexpr int kStageRegs = 4;    // staged residuals per thread: 4096 rows per sub-block (32 KB fp64 / 16 KB fp32);
-                                 // 8 (8192 rows) for merged FRC / AGC units (csc_tiles_lds STAGE)
+                                 // 8 (8192 rows) for merged FRC / AGC units (csc_tiles_lds UNITS)
 constexpr int kRunCap = 128;     // runs per tile compacted in LDS (covtype: 33 on average, 0.7 % of tiles above)
 
 // A tile's 8 row indices per lane as loaded (16-bit rows: one 16-byte vector, 32-bit rows: two), decoded
@@ -542,7 +542,11 @@ __device__ __forceinline__ unsigned tile_rows_decode(const TileRaw& r, int (&row
 // columns itself (tail of the first tile + the heads of the later ones, in tile order: csc_spans'
 // order).  LOCAL is a template parameter so the head / tail stores are LDS or global stores (a pointer
 // that may be either is a flat store, which every later wait has to count on both counters).
-template <typename A, bool ROW16, bool VALS, bool LOCAL, int STAGE>
+// UNITS: merged FRC / AGC units (SparseArgs::dst) -- 8192-row sub-blocks and every sum stored into each
+// of the unit's message rows; a compile-time variant, so the single-row form keeps its instruction
+// stream (a run-time destination loop in the tile loop cost 1.4-5 us per launch on every sparse shape:
+// profiles/round6/sparse/tree_ab.txt)
+template <typename A, bool ROW16, bool VALS, bool LOCAL, bool UNITS>
 __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, const int* gate) {
   __shared__ int run_col[kWgWaves][kRunCap];
   __shared__ A run_val[kWgWaves][kRunCap];
@@ -574,6 +578,7 @@ __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, con
     tk = a.tkeys[t];  // (first run, n | runs << 10 | span flags << 20, sub-block, first column)
   }
   const A* __restrict__ ug = static_cast<const A*>(a.u) + wd.x;
+  constexpr int STAGE = UNITS ? 2 * kStageRegs : kStageRegs;
   A st[STAGE];
 #pragma unroll
   for (int j = 0; j < STAGE; ++j) {
@@ -645,20 +650,22 @@ __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, con
     const A carry = fl & 1u ? A(0) : prev;       // into this lane's entries before its first flag
     const unsigned cmask = fl ? (fl & (0u - fl)) - 1u : 0xffu;
     // the output rows of sub-block p (wave-uniform): row p, or its shared message rows (SparseArgs::dst)
+    A* __restrict__ gout = static_cast<A*>(a.Gs) + static_cast<long long>(p) * a.ld;
     long long doff[kSparseMaxDst];
-    int nd = 1;
-    doff[0] = static_cast<long long>(p) * a.ld;
-    if (a.dst) {
-      nd = 0;
+    int nd = 0;
+    if constexpr (UNITS) {
 #pragma unroll
       for (int q = 0; q < kSparseMaxDst; ++q) {
         const int r = __builtin_amdgcn_readfirstlane(a.dst[p * kSparseMaxDst + q]);
         if (r >= 0) doff[nd++] = static_cast<long long>(r) * a.ld;
       }
     }
-    A* __restrict__ gbase = static_cast<A*>(a.Gs);
     auto put = [&](int col, A val) {
-      for (int q = 0; q < nd; ++q) gbase[doff[q] + col] = val;
+      if constexpr (UNITS) {
+        for (int q = 0; q < nd; ++q) static_cast<A*>(a.Gs)[doff[q] + col] = val;
+      } else {
+        gout[col] = val;
+      }
     };
     if (compact) {
       // each run end stores its lane-local sum at its run index; the one run that began in an earlier
@@ -701,7 +708,7 @@ __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, con
     A sum = s_tail[my_span.z];
     for (int k = my_span.z + 1; k <= my_span.w; ++k) sum += s_head[k];
     A* __restrict__ gs = static_cast<A*>(a.Gs);
-    if (a.dst) {
+    if constexpr (UNITS) {
       for (int q = 0; q < kSparseMaxDst; ++q) {
         const int r = a.dst[my_span.x * kSparseMaxDst + q];
         if (r >= 0) gs[static_cast<long long>(r) * a.ld + my_span.y] = sum;
@@ -829,9 +836,9 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
   }
   if (a.ntiles > 0 && a.wg) {
     const size_t ulds = static_cast<size_t>(std::max(a.u_lds, 1)) * (dtype == 0 ? 8 : 4);
-    if (a.u_lds > 2 * kStageRegs * 1024) return hipErrorInvalidValue;  // (sub-blocks of at most 8192 rows)
-    if (a.dst && (a.sub_begin || a.nspan || a.nempty)) return hipErrorInvalidValue;  // shared rows: unblocked only
-    const bool wide = a.u_lds > kStageRegs * 1024;  // merged units: 8192-row sub-blocks, 8 staged per thread
+    // sub-blocks of at most 4096 rows, merged units (shared rows, unblocked only) of at most 8192
+    if (a.u_lds > (a.dst ? 2 : 1) * kStageRegs * 1024) return hipErrorInvalidValue;
+    if (a.dst && (a.sub_begin || a.nspan || a.nempty)) return hipErrorInvalidValue;
     const dim3 grid(static_cast<unsigned>(a.nwg));
 #define EH_TLDS3(A_, R_, V_, L_, S_)                                                                            \
   {                                                                                                              \
@@ -842,8 +849,8 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
   }
 #define EH_TLDS2(A_, R_, V_, L_)                                   \
   {                                                                \
-    if (wide) EH_TLDS3(A_, R_, V_, L_, 2 * kStageRegs)             \
-    else EH_TLDS3(A_, R_, V_, L_, kStageRegs)                      \
+    if (a.dst) EH_TLDS3(A_, R_, V_, L_, true)                      \
+    else EH_TLDS3(A_, R_, V_, L_, false)                           \
   }
 #define EH_TLDS(A_, R_, V_)                     \
   {                                               \

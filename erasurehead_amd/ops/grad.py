@@ -648,7 +648,7 @@ class SparseGradPlan:
     # coefficient 1: ref src/replication.py:56-68), so the device stacks the group's partitions into one
     # unit and the column pass writes the unit's sums straight into every member's message row
     # (SparseArgs::dst) -- no per-partition rows and no encoding launch, the naive plan's work.  Units
-    # up to this many rows are staged whole (grad_sparse.hip csc_tiles_lds STAGE 8); larger ones keep the
+    # up to this many rows are staged whole (grad_sparse.hip csc_tiles_lds UNITS); larger ones keep the
     # partition basis and the encoding.
     UNIT_ROWS = 8192
     MAX_DST = 4  # grad_sparse.hip kSparseMaxDst: replicas per unit
@@ -776,7 +776,7 @@ class SparseGradPlan:
         rb = self.ROW_BLOCK_ROWS
         wgt = self.WG_TILES
         self.wg_tiles = wgt or self.MAX_WG_TILES
-        if self.units is not None:  # a unit is one sub-block of up to UNIT_ROWS rows (csc_tiles_lds STAGE 8)
+        if self.units is not None:  # a unit is one sub-block of up to UNIT_ROWS rows (csc_tiles_lds UNITS)
             rb = max(rb, max(b[0].shape[0] for b in dev_blocks))
         t = self.csc_tables([b[0] for b in dev_blocks], self.d, self.TILE, row_block=rb, wg_tiles=self.wg_tiles,
                             wg_spans=self.WG_SPANS, slots=0 if wgt else self.WG_SLOTS)

@@ -259,7 +259,11 @@ def eval_cases(out):
         del X
 
 
-def sparse_cases(out, names=("covtype", "kc_house_data", "amazon-dataset"), ell_only=False):
+UNITS_PROBE = False  # --units-probe
+
+
+def sparse_cases(out, names=("covtype", "kc_house_data", "amazon-dataset"), ell_only=False, layouts_only=None,
+                 rows="both"):
     import torch
 
     from erasurehead_amd.data.synthetic import REAL_SHAPES, onehot_partitions
@@ -276,10 +280,15 @@ def sparse_cases(out, names=("covtype", "kc_house_data", "amazon-dataset"), ell_
                    "s1_replicas": [[(w, 1.0), ((w + 1) % W, 1.0)] for w in range(W)],  # 8 workers, 2 partitions each
                    # FRC / AGC s = 1: groups {2g, 2g + 1} send the sum of both partitions (merged units when small)
                    "frc_s1": [[(w - w % 2, 1.0), (w - w % 2 + 1, 1.0)] for w in range(W)]}
-        for (layout, msgs), use_ell in [(x, e) for x in layouts.items() for e in ((True,) if ell_only else (True, False))]:
+        if layouts_only:
+            layouts = {k: v for k, v in layouts.items() if k in layouts_only}
+        ells = (True,) if ell_only else ("auto",) if rows == "auto" else (True, False)
+        for (layout, msgs), use_ell in [(x, e) for x in layouts.items() for e in ells]:
             plan = SparseGradPlan(msgs, parts, prec, LOGISTIC, dd, device="cuda", use_ell=use_ell)
             beta = torch.randn(prec.ld(dd), device="cuda", dtype=torch.float64) * 0.1
             G = plan.out_buffer()[0]
+            if UNITS_PROBE and plan.dst is not None:  # timing probe, not a gradient: each unit's first row only
+                plan.dst[:, 1:] = -1
             ms = _time(lambda: plan.run(beta, G))
             kern = ("ell16" if plan.idx16 else "ell32") if plan.ell else "csr"
             r = {"kernel": f"grad_sparse ({kern} rows, CSC{16 if plan.row16 else 32} tiles)", "layout": layout,
@@ -305,16 +314,22 @@ def main():
     ap.add_argument("--precs", default="fp64,fp32", help="--only sweep: precisions")
     ap.add_argument("--sparse-shapes", default="covtype,kc_house_data,amazon-dataset", help="--only sparse: datasets")
     ap.add_argument("--ell-only", action="store_true", help="--only sparse: skip the CSR row pass")
+    ap.add_argument("--sparse-layouts", default=None, help="--only sparse: naive,s1_replicas,frc_s1 (default: all)")
+    ap.add_argument("--units-probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--sparse-rows", default="both", choices=["both", "auto"],
+                    help="--only sparse: both row passes, or the plan's own choice")
     ap.add_argument("--wg-tiles", type=int, default=0, help="--only sparse: tiles per column-pass workgroup (A/B)")
-    ap.add_argument("--row-block", type=int, default=0, help="--only sparse: column-pass sub-block rows (A/B, <= 8192)")
+    ap.add_argument("--row-block", type=int, default=0, help="--only sparse: column-pass sub-block rows (A/B, <= 4096)")
     ap.add_argument("--wg-slots", type=int, default=0, help="--only sparse: workgroup budget of the chip-sized chunks (A/B)")
     ap.add_argument("--no-wg-spans", action="store_true",
                     help="--only sparse: whole 16-tile chunks and the csc_spans launch (A/B of SparseGradPlan.WG_SPANS)")
     a = ap.parse_args()
+    global UNITS_PROBE
+    UNITS_PROBE = a.units_probe
     if a.row_block:
         from erasurehead_amd.ops import SparseGradPlan
 
-        SparseGradPlan.ROW_BLOCK_ROWS = a.row_block  # > 4096: 8 staged residuals per thread (csc_tiles_lds STAGE)
+        SparseGradPlan.ROW_BLOCK_ROWS = a.row_block
     if a.no_wg_spans or a.wg_tiles or a.wg_slots:
         from erasurehead_amd.ops import SparseGradPlan
 
@@ -338,7 +353,8 @@ def main():
         else:
             choice_cases(out, layout=a.layout)
     if a.only in (None, "sparse"):
-        sparse_cases(out, names=tuple(a.sparse_shapes.split(",")), ell_only=a.ell_only)
+        sparse_cases(out, names=tuple(a.sparse_shapes.split(",")), ell_only=a.ell_only,
+                     layouts_only=a.sparse_layouts.split(",") if a.sparse_layouts else None, rows=a.sparse_rows)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         for r in out:

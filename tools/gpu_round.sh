@@ -94,13 +94,8 @@ for s in "${STAGES[@]}"; do
       done
       run 300 prof_bf16_stream.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bf16_stream" -o run -- \
         python bench.py --no-floor --no-breakdown --precision bf16 --mfma-stream 1 --steps 50 ;;
-    sparseab)  # sparse gradients at the real shapes (naive / cyclic-style / FRC layouts), then covtype with
-               # 8192-row sub-blocks (2 and 1 workgroups per CU), then the sparse suite rows
+    sparseab)  # sparse gradients at the real shapes (naive / cyclic-style / FRC layouts), then the sparse suite rows
       run 600 sparse.log python -u tools/bench_kernels.py --only sparse --out "$OUT/sparse.jsonl"
-      run 300 sparse_rb8k.log python -u tools/bench_kernels.py --only sparse --sparse-shapes covtype --ell-only \
-        --row-block 8192 --out "$OUT/sparse_rb8k.jsonl"
-      run 300 sparse_rb8k_s256.log python -u tools/bench_kernels.py --only sparse --sparse-shapes covtype --ell-only \
-        --row-block 8192 --wg-slots 256 --out "$OUT/sparse_rb8k_s256.jsonl"
       run 900 suite_sparse.log python -u tools/bench_suite.py --out "$OUT/suite" \
         --only naive_covtype,agc_covtype,ls_kc_house_naive,ls_kc_house_agc_k6,naive_amazon,agc_amazon ;;
     rccl)  # the RCCL self-loop comm path under the kernel tracer (RCCL kernel names in the stats)
