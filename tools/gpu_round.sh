@@ -129,7 +129,7 @@ for s in "${STAGES[@]}"; do
         done
         [ -z "$want" ] && { log "skip pass $i: none of $grp listed"; continue; }
         run 180 "pmcs_$i.log" timeout -s KILL 170 rocprofv3 --pmc $want --output-format csv -d "$OUT/pmcs" -o "p$i" -- \
-          python tools/bench_kernels.py --only sparse --sparse-shapes covtype --ell-only --out /tmp/sparse_pmc.jsonl
+          python tools/bench_kernels.py --only sparse --sparse-shapes covtype --ell-only --sparse-layouts naive --out /tmp/sparse_pmc.jsonl
       done
       python tools/pmc_summary.py "$OUT/pmcs" --by-kernel > "$OUT/pmcs_summary.json" ;;
     rehearse)
