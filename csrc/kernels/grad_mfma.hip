@@ -16,7 +16,8 @@
 // so the products keep fp32 accuracy while X stays exact bf16; accumulation is fp32 in the MFMA.
 // (A two-term split measured ~1e-5 absolute error on O(10) gradients: 10x the VALU kernel's.)
 //
-// Data movement: the workgroup (8 waves) streams its row range through a 2-stage LDS ring with
+// Data movement (grad_staged_mfma; grad_vring_mfma below is the same ring fed through registers, the
+// default for packed bundles): the workgroup (8 waves) streams its row range through a 2-stage LDS ring with
 // 16-byte LDS-DMA (global_load_lds, lds_dma.h) exactly like grad_dense_staged; a stage is 32 rows
 // (64 KB at d = 1000) + their labels.  GEMM1 reads its B operand (X rows, k = columns) with
 // ds_read_b128; GEMM2 needs X with k = rows, read through gfx950's transposing ds_read_b64_tr_b16
@@ -430,6 +431,178 @@ grad_stream_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
   }
 }
 
+// ---- VGPR-staged ring (R <= 4, packed terms, 32-row stages) ---------------------------------------
+// grad_staged_mfma's LDS ring and arithmetic, but every stage is loaded into registers two stages ahead
+// -- whole 1 KB blocks per wave instruction, full 128-byte lines, the LDS-DMA form's block map -- and
+// copied into its LDS buffer with ds_write_b128 once the compute of the stage before has freed it.  Two
+// stages (128 KB per CU) are in flight while a third is computed, against the LDS-DMA ring's one (its
+// stream alone: 311 us per 2 GB).  Buffer loads past a partial stage's rows return zeros (finite data;
+// residual 0 there), so every stage issues the same loads and the compiler waits only for the older one.
+constexpr int kVrPieces = 8;  // 1 KB blocks per wave per stage at ld <= 1024 (32 rows x 2 KB / 8 waves)
+// The stage loads are inline asm, counted by the kernel (lds_dma.h's reason): through the builtins the
+// compiler merged the loop's entry and back-edge states conservatively and waited vmcnt(0) for both
+// register sets at every other stage.  base: wave-uniform stage address; off: this lane's byte offset.
+__device__ __forceinline__ uint4 vr_load16(const unsigned char* base, int off) {
+  uint4 v;
+  asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=v"(v) : "v"(off), "s"(base) : "memory");
+  return v;
+}
+__device__ __forceinline__ float vr_load4(const float* base, int off) {
+  float v;
+  asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(off), "s"(base) : "memory");
+  return v;
+}
+// NSET register sets: NSET stages in flight while one is computed (NSET x 32 VGPRs of stage data)
+template <int LOSS, int NSET>
+__global__ void __launch_bounds__(512)
+grad_vring_mfma(const Segment* __restrict__ segs, const Task* __restrict__ tasks, const float* __restrict__ beta,
+                float* __restrict__ slab, int ld, int R, const int* __restrict__ gate, int probe) {
+  constexpr int S = 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  if (gate_closed(gate)) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Task lead = tasks[blockIdx.x * R];  // slot 0 of a bundle is always a real task
+  const Segment ls = segs[lead.seg];
+  const unsigned char* __restrict__ X = static_cast<const unsigned char*>(ls.X);
+  const float* __restrict__ Y = static_cast<const float*>(ls.y);
+  const int rowbytes = ld * 2;
+  // every stage buffer holds all kVrPieces blocks, so the copies into it are unconditional (a branch per
+  // block let the compiler sink the prologue's loads into it, and the loop's waits went conservative)
+  constexpr int data_bytes = kMfNW * kVrPieces * 1024;
+  constexpr int buf_bytes = data_bytes + 256;
+  const int nrows = lead.row_end - lead.row_begin;
+  const int nst = (nrows + S - 1) / S;
+  float* zred = reinterpret_cast<float*>(smem_raw + 2 * buf_bytes);  // [wave][16][32] partial Zᵀ
+  __bf16* rres = reinterpret_cast<__bf16*>(zred + kMfNW * 16 * S);     // [16][32] residual terms
+  const int fi = lane & 15, fq = fi >> 2, fp = fi & 3, fg = lane >> 4;
+
+  const int rm = tid / S, rn = tid % S;  // residual role (replica rm, stage row rn) of the first 4 * S threads
+  const bool rrole = tid < 4 * S;
+  float rcoef = 0.f;
+  if (rrole && rm < R) {
+    const Task tq = tasks[blockIdx.x * R + rm];
+    if (tq.seg >= 0) rcoef = static_cast<float>(segs[tq.seg].coef);
+  }
+  // GEMM1 A fragments (packed): A[m = lane & 15][k] = term m & 3 of beta[k] for replica m >> 2 < R
+  const bool rep_ok = ((lane & 15) >> 2) < R && (lane & 3) < kMfSplit;
+  bf16x8 bfr[kMfKPW];
+#pragma unroll
+  for (int kk = 0; kk < kMfKPW; ++kk) {
+    const int k0 = (w * kMfKPW + kk) * 32 + 8 * fg;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __bf16 t[kMfSplit];
+      split_bf16(rep_ok && k0 + j < ld ? beta[k0 + j] : 0.f, t);
+      const int sm = lane & 3;
+      bfr[kk][j] = sm == 0 ? t[0] : sm == 1 ? t[1] : t[2];
+    }
+  }
+  f32x4 g[kMfTPW];
+#pragma unroll
+  for (int t = 0; t < kMfTPW; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int slab_row = -1;  // lane group fg holds replica fg's G
+  if (fg < R) {
+    const Task tq = tasks[blockIdx.x * R + fg];
+    if (tq.seg >= 0) slab_row = tq.slab;
+  }
+
+  // stage t into registers, 9 loads per wave: (stages past the last repeat it and are never stored; pieces
+  // past a partial stage's rows are clamped onto its last 16 valid bytes, grad_staged_mfma's rule)
+  auto load = [&](int t, uint4 (&xr)[kVrPieces], float& yv) {
+    const int tc = __builtin_amdgcn_readfirstlane(min(t, nst - 1));
+    const long long r0 = lead.row_begin + static_cast<long long>(tc) * S;
+    const int ns = min(S, static_cast<int>(lead.row_end - r0));
+    const unsigned char* base = X + r0 * rowbytes;
+    const int last = ns * rowbytes - 16;
+#pragma unroll
+    for (int j = 0; j < kVrPieces; ++j) xr[j] = vr_load16(base, min((w + kMfNW * j) * 1024 + lane * 16, last));
+    yv = vr_load4(Y + r0, 4 * min(lane & (S - 1), ns - 1));
+  };
+  auto store = [&](int t, const uint4 (&xr)[kVrPieces], float yv) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSET - 1) * (kVrPieces + 1)) : "memory");  // this set landed
+    unsigned char* buf = smem_raw + (t & 1) * buf_bytes;
+#pragma unroll
+    for (int j = 0; j < kVrPieces; ++j) *reinterpret_cast<uint4*>(buf + (w + kMfNW * j) * 1024 + lane * 16) = xr[j];
+    // the labels by every wave (the same values; a store under a branch let the compiler sink the load)
+    reinterpret_cast<float*>(buf + data_bytes)[lane & (S - 1)] = yv;
+  };
+  auto compute = [&](int t) {
+    const unsigned char* buf = smem_raw + (t & 1) * buf_bytes;
+    const float* lab = reinterpret_cast<const float*>(buf + data_bytes);
+    const int ns = min(S, nrows - t * S);
+    f32x4 z[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kk = 0; kk < kMfKPW; ++kk) {
+      const int kstep = w * kMfKPW + kk;
+      if (kstep * 32 >= ld) break;  // wave-uniform
+      const int col = min(kstep * 32 + 8 * fg, ld - 8);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        z[nt] = mma(bfr[kk], *reinterpret_cast<const bf16x8*>(buf + (16 * nt + fi) * rowbytes + col * 2), z[nt]);
+    }
+    float* zw = zred + w * 16 * S;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) zw[fg * S + 16 * nt + fi] = (z[nt][2] + z[nt][1]) + z[nt][0];
+    __syncthreads();
+    if (rrole) {
+      float zs = 0.f;
+#pragma unroll
+      for (int v = 0; v < kMfNW; ++v) zs += zred[(v * 16 + rm) * S + rn];
+      const float r = rm < R && rn < ns ? residual_hw<LOSS>(zs, lab[rn], rcoef) : 0.f;
+      __bf16 tt[kMfSplit];
+      split_bf16(r, tt);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rres[(4 * rm + q) * S + rn] = q < kMfSplit ? tt[q < kMfSplit ? q : 0] : __bf16(0.f);
+    }
+    __syncthreads();
+    const bf16x8 ar = *reinterpret_cast<const bf16x8*>(rres + fi * S + 8 * fg);
+#pragma unroll
+    for (int tt = 0; tt < kMfTPW; ++tt) {
+      const int c0 = (w * kMfTPW + tt) * 16;
+      if (c0 >= ld) break;  // wave-uniform
+      const unsigned char* a0 = buf + (8 * fg + fq) * rowbytes + (c0 + 4 * fp) * 2;
+      const bf16x4 t0 = tr_read(a0);
+      const bf16x4 t1 = tr_read(a0 + 4 * rowbytes);
+      g[tt] = mma(ar, bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]}, g[tt]);
+    }
+  };
+  // NSET register sets, the loop unrolled by NSET so each is named statically.  The copy of stage t
+  // follows compute(t - 1) -- the buffer it reuses, t - 2's, was freed by the barrier before compute(t - 1)
+  // -- and stages t + 1 .. t + NSET are in flight while stage t is computed.
+  uint4 xs[NSET][kVrPieces];
+  float ys[NSET];
+#pragma unroll
+  for (int k = 0; k < NSET; ++k) ys[k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMfKPW; ++k) asm volatile("" ::"v"(bfr[k]));
+  asm volatile("" ::"v"(rcoef), "v"(slab_row));
+  // the setup's loads done, and its arithmetic kept here, before the counted loads (scheduled past them it
+  // brought a compiler wait for beta -- vmcnt(0) -- behind the first stages' loads)
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < NSET; ++k) load(k, xs[k], ys[k]);
+  for (int t = 0; t < nst; t += NSET) {
+#pragma unroll
+    for (int k = 0; k < NSET; ++k) {
+      if (t + k >= nst) break;  // block-uniform
+      store(t + k, xs[k], ys[k]);
+      load(t + k + NSET, xs[k], ys[k]);
+      __syncthreads();  // stage t + k in LDS; zred and the residuals of the stage before consumed
+      if (probe != 1) compute(t + k);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the repeated loads past the last stage
+#pragma unroll
+  for (int tt = 0; tt < kMfTPW; ++tt) {
+    const int c0 = (w * kMfTPW + tt) * 16;
+    if (c0 >= ld) break;
+    const int col = c0 + fi;
+    if (slab_row >= 0 && col < ld) slab[static_cast<long long>(slab_row) * ld + col] = (g[tt][2] + g[tt][1]) + g[tt][0];
+  }
+}
+
 // ---- layout probes (tests/test_kernels_gpu.py checks them with exact integer data) ---------------
 // C[16][16] = A[16][32] · B[32][16] through one v_mfma_f32_16x16x32_bf16 with the fragment maps
 // the kernel above assumes.
@@ -481,10 +654,12 @@ void set_mfma_probe(int mode) { g_mfma_probe = mode == 1 || mode == 2 ? mode : 0
 // the packed-term form for R <= 4 (default) or the three-MFMA form, for A/B
 static bool g_mfma_pack = true;
 void set_mfma_pack(bool on) { g_mfma_pack = on; }
-// packed bundles (R <= 4) through the VGPR stream (grad_stream_mfma: 1 nt loads, 2 default-policy loads) or
-// the LDS-DMA stage ring (0), for A/B
-static int g_mfma_stream = 0;
-void set_mfma_stream(int mode) { g_mfma_stream = mode == 1 || mode == 2 ? mode : 0; }
+// packed bundles (R <= 4) through the VGPR stream (grad_stream_mfma: 1 nt loads, 2 default-policy loads), the
+// VGPR-staged ring (grad_vring_mfma: 3 two register sets, the default; 4 three) or the LDS-DMA stage ring (0).
+// At the N = 1 rank shape (2 GB, two alternating reps on two boxes, profiles/round6/bf16ab/rows_ab*.jsonl):
+// 0: 315.3-320.4 us, 3: 312.4-314.7, 4: 318.8-319.0 (stream alone 307.6-310.2 / 301.0-303.3 / 305.1-307.3).
+static int g_mfma_stream = 3;
+void set_mfma_stream(int mode) { g_mfma_stream = mode >= 1 && mode <= 4 ? mode : 0; }
 
 bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds) {
   if (ld < 8 || ld > kMfNW * kMfKPW * 32 || ld % 8) return false;
@@ -512,7 +687,19 @@ hipError_t grad_mfma_launch(int loss, const Segment* segs, const Task* tasks, in
   size_t lds = 0;
   if (!mfma_geometry(ld, &rows, &pieces, &nstage, &lds)) return hipErrorInvalidValue;
   const bool pack = R <= 4 && g_mfma_pack;
-  if (pack && g_mfma_stream && g_mfma_probe == 0) {  // (ld <= 1024, ld % 8 == 0: mfma_geometry above)
+  if (pack && (g_mfma_stream == 3 || g_mfma_stream == 4) && rows == 32 && g_mfma_probe != 2) {  // (ld <= 1024)
+    auto kern = g_mfma_stream == 3 ? (loss == kLogistic ? grad_vring_mfma<kLogistic, 2> : grad_vring_mfma<kLeastSquares, 2>)
+                                   : (loss == kLogistic ? grad_vring_mfma<kLogistic, 3> : grad_vring_mfma<kLeastSquares, 3>);
+    constexpr int vlds = 2 * (kMfNW * kVrPieces * 1024 + 256) + kMfNW * 16 * 32 * 4 + 16 * 32 * 2;
+    static_assert(vlds <= 160 * 1024, "two stage buffers + partial Z + residuals");
+    const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, vlds);
+    if (ea != hipSuccess) return ea;
+    hipLaunchKernelGGL(kern, dim3(ntasks / R), dim3(64 * kMfNW), vlds, st, segs, tasks, beta, slab, ld, R, gate,
+                       g_mfma_probe);
+    return hipGetLastError();
+  }
+  if (pack && (g_mfma_stream == 1 || g_mfma_stream == 2) && g_mfma_probe == 0) {  // (ld <= 1024, ld % 8 == 0)
     auto kern = g_mfma_stream == 1 ? (loss == kLogistic ? grad_stream_mfma<kLogistic, kStreamAux>
                                                         : grad_stream_mfma<kLeastSquares, kStreamAux>)
                                    : (loss == kLogistic ? grad_stream_mfma<kLogistic, 0> : grad_stream_mfma<kLeastSquares, 0>);
