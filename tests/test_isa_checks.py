@@ -121,3 +121,29 @@ def test_wide_row_bundles_do_not_spill(tmp_path):
     assert len(wide) >= 24, sorted(wide)  # 3 storage types x 2 losses x (256 threads x R in 1..3, 512 x R = 1)
     bad = {n: r for n, r in wide.items() if r[1] > 0}
     assert not bad, bad
+
+
+@pytest.mark.skipif(not os.path.exists(OBJDUMP), reason="llvm-objdump not installed")
+def test_vgpr_ring_waits_only_for_its_oldest_register_set(tmp_path):
+    """grad_vring_mfma (the default bf16 packed bundles) counts its own stage loads (inline asm,
+    9 per stage and wave): once the pipeline has started, the only vector-memory loads are those 9-load
+    groups, every copy into the ring waits vmcnt((NSET - 1) * 9) -- the other sets stay in flight --
+    and no vmcnt(0) appears before the loop ends."""
+    checked = 0
+    for co in _code_objects(tmp_path):
+        for name, body in _functions(co):
+            if "grad_vring_mfma" not in name:
+                continue
+            nset = int(re.search(r"grad_vring_mfmaILi\d+ELi(\d+)E", name).group(1))
+            checked += 1
+            body = [l.split("//")[0].strip() for l in body]
+            first = next(i for i, l in enumerate(body) if l.startswith("global_load_dwordx4") and l.endswith(" nt"))
+            # the loop: from the first ring copy to the last barrier
+            last = max(i for i, l in enumerate(body) if l.startswith("s_barrier"))
+            waits = [l for l in body[first:last] if l.startswith("s_waitcnt") and "vmcnt" in l]
+            assert waits, name
+            want = f"vmcnt({(nset - 1) * 9})"
+            assert all(want in w for w in waits), (name, waits)
+            loads = [l.split()[0] for l in body[first:last] if VMEM_LOAD.match(l.split()[0])]
+            assert loads.count("global_load_dwordx4") == 8 * loads.count("global_load_dword"), (name, loads[:12])
+    assert checked >= 4, f"only {checked} grad_vring_mfma instantiations found"
