@@ -16,8 +16,8 @@
 // so the products keep fp32 accuracy while X stays exact bf16; accumulation is fp32 in the MFMA.
 // (A two-term split measured ~1e-5 absolute error on O(10) gradients: 10x the VALU kernel's.)
 //
-// Data movement (grad_staged_mfma; grad_vring_mfma below is the same ring fed through registers, the
-// default for packed bundles): the workgroup (8 waves) streams its row range through a 2-stage LDS ring with
+// Data movement (grad_staged_mfma; grad_vring_mfma below is the same ring fed through registers, an A/B):
+// the workgroup (8 waves) streams its row range through a 2-stage LDS ring with
 // 16-byte LDS-DMA (global_load_lds, lds_dma.h) exactly like grad_dense_staged; a stage is 32 rows
 // (64 KB at d = 1000) + their labels.  GEMM1 reads its B operand (X rows, k = columns) with
 // ds_read_b128; GEMM2 needs X with k = rows, read through gfx950's transposing ds_read_b64_tr_b16
@@ -655,10 +655,11 @@ void set_mfma_probe(int mode) { g_mfma_probe = mode == 1 || mode == 2 ? mode : 0
 static bool g_mfma_pack = true;
 void set_mfma_pack(bool on) { g_mfma_pack = on; }
 // packed bundles (R <= 4) through the VGPR stream (grad_stream_mfma: 1 nt loads, 2 default-policy loads), the
-// VGPR-staged ring (grad_vring_mfma: 3 two register sets, the default; 4 three) or the LDS-DMA stage ring (0).
-// At the N = 1 rank shape (2 GB, two alternating reps on two boxes, profiles/round6/bf16ab/rows_ab*.jsonl):
-// 0: 315.3-320.4 us, 3: 312.4-314.7, 4: 318.8-319.0 (stream alone 307.6-310.2 / 301.0-303.3 / 305.1-307.3).
-static int g_mfma_stream = 3;
+// VGPR-staged ring (grad_vring_mfma: 3 two register sets, 4 three) or the LDS-DMA stage ring (0, the default).
+// At the N = 1 rank shape (2 GB; profiles/round6/bf16ab/rows_ab*.jsonl, ring_vs_vring_r8e.jsonl): on two boxes
+// 0: 315.3-320.4 us, 3: 312.4-314.7, 4: 318.8-319.0 (stream alone 307.6-310.2 / 301.0-303.3 / 305.1-307.3);
+// on a third, four alternating reps, 0: 312.9-316.2, 3: 314.0-319.3.  Within the box-to-box spread: no default.
+static int g_mfma_stream = 0;
 void set_mfma_stream(int mode) { g_mfma_stream = mode >= 1 && mode <= 4 ? mode : 0; }
 
 bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds) {

@@ -125,7 +125,7 @@ def test_wide_row_bundles_do_not_spill(tmp_path):
 
 @pytest.mark.skipif(not os.path.exists(OBJDUMP), reason="llvm-objdump not installed")
 def test_vgpr_ring_waits_only_for_its_oldest_register_set(tmp_path):
-    """grad_vring_mfma (the default bf16 packed bundles) counts its own stage loads (inline asm,
+    """grad_vring_mfma (the bf16 packed bundles' VGPR-staged ring, an A/B) counts its own stage loads (inline asm,
     9 per stage and wave): once the pipeline has started, the only vector-memory loads are those 9-load
     groups, every copy into the ring waits vmcnt((NSET - 1) * 9) -- the other sets stay in flight --
     and no vmcnt(0) appears before the loop ends."""

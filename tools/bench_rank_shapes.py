@@ -80,7 +80,7 @@ def build_plan(n_gpus: int, precision: str, shard: str = "partition", rows_overr
 
 
 def one(n_gpus: int, precision: str, shard: str = "partition", rows_override: int = 0, fill: bool = False,
-        slab_mode: int = 1, mfma_rows: int = 32, mfma_probe: int = 0, mfma_stream: int = 3) -> dict:
+        slab_mode: int = 1, mfma_rows: int = 32, mfma_probe: int = 0, mfma_stream: int = 0) -> dict:
     import numpy as np
     import torch
 
@@ -126,8 +126,8 @@ def main():
     ap.add_argument("--slab-mode", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--mfma-rows", type=int, default=32, help="bf16 MFMA bundles: rows per LDS stage (32 / 16)")
     ap.add_argument("--mfma-probe", type=int, default=0, help="bf16 MFMA timing probe: 1 loads only, 2 compute only")
-    ap.add_argument("--mfma-stream", type=int, default=3,
-                    help="bf16 packed bundles: 0 LDS-DMA ring, 1 / 2 VGPR stream, 3 VGPR-staged ring (default), 4 its three-set form")
+    ap.add_argument("--mfma-stream", type=int, default=0,
+                    help="bf16 packed bundles: 0 LDS-DMA ring (default), 1 / 2 VGPR stream, 3 VGPR-staged ring, 4 its three-set form")
     a = ap.parse_args()
     if a.one:
         print(json.dumps(one(a.one, a.precision, a.shard, a.rows, a.fill, a.slab_mode, a.mfma_rows, a.mfma_probe,
