@@ -521,6 +521,10 @@ grad_vring_mfma(const Segment* __restrict__ segs, const Task* __restrict__ tasks
   };
   auto store = [&](int t, const uint4 (&xr)[kVrPieces], float yv) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSET - 1) * (kVrPieces + 1)) : "memory");  // this set landed
+    if (probe >= 3) {  // timing probes: the loads alone (3: with the stage barriers, 4: without)
+      asm volatile("" ::"v"(xr[0].x), "v"(xr[kVrPieces - 1].w), "v"(yv));
+      return;
+    }
     unsigned char* buf = smem_raw + (t & 1) * buf_bytes;
 #pragma unroll
     for (int j = 0; j < kVrPieces; ++j) *reinterpret_cast<uint4*>(buf + (w + kMfNW * j) * 1024 + lane * 16) = xr[j];
@@ -589,8 +593,8 @@ grad_vring_mfma(const Segment* __restrict__ segs, const Task* __restrict__ tasks
       if (t + k >= nst) break;  // block-uniform
       store(t + k, xs[k], ys[k]);
       load(t + k + NSET, xs[k], ys[k]);
-      __syncthreads();  // stage t + k in LDS; zred and the residuals of the stage before consumed
-      if (probe != 1) compute(t + k);
+      if (probe != 4) __syncthreads();  // stage t + k in LDS; zred and the residuals of the stage before consumed
+      if (probe == 0) compute(t + k);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the repeated loads past the last stage
@@ -648,9 +652,10 @@ hipError_t tr_probe_launch(const float* tile, int rowlen, float* out, hipStream_
 static int g_mfma_rows = 32;
 void set_mfma_stage_rows(int rows) { g_mfma_rows = rows == 16 ? 16 : 32; }
 // timing probes of grad_staged_mfma (tools/bench_rank_shapes.py --mfma-probe; results are NOT a
-// gradient): 1 = the LDS-DMA stage stream and barriers only, 2 = the GEMMs / residuals without loads
+// gradient): 1 = the LDS-DMA stage stream and barriers only, 2 = the GEMMs / residuals without loads;
+// grad_vring_mfma also 3 = its loads and barriers (no LDS copies), 4 = its loads alone
 static int g_mfma_probe = 0;
-void set_mfma_probe(int mode) { g_mfma_probe = mode == 1 || mode == 2 ? mode : 0; }
+void set_mfma_probe(int mode) { g_mfma_probe = mode >= 1 && mode <= 4 ? mode : 0; }
 // the packed-term form for R <= 4 (default) or the three-MFMA form, for A/B
 static bool g_mfma_pack = true;
 void set_mfma_pack(bool on) { g_mfma_pack = on; }
