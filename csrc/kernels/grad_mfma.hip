@@ -279,157 +279,10 @@ grad_staged_mfma(const Segment* __restrict__ segs, const Task* __restrict__ task
   }
 }
 
-// ---- VGPR-streamed bundles (R <= 4, packed terms) -------------------------------------------------
-// The LDS-DMA form above is bound by its stage stream: alone it takes 311 of the kernel's 316-318 us
-// per 2 GB, one 64 KB stage in flight per CU.  Here every wave loads ITS column slice of a stage
-// (128 columns x 32 rows = 8 KB) with buffer loads straight into registers, already in GEMM1's
-// B-fragment layout (row lane & 15, 8 consecutive columns), kMsPre stages ahead of the one computed
-// (two in flight: 128 KB per CU); GEMM1 reads the registers, and the wave copies its slice into a
-// private LDS image only for GEMM2's transposing reads of the SAME columns (its own column tiles).  No
-// other wave reads that image, so the only barriers left are the two around the cross-wave residual.
-// MEASURED SLOWER, kept as an A/B (bench.py --mfma-stream): 0.475 ms with nt loads, 0.345 ms with the
-// default policy, against the ring's 0.316 ms (profiles/round6/bf16ab).  The B-fragment layout fixes every
-// load instruction at 16 rows x 64 bytes -- half of each 128-byte line per request -- which only the
-// LDS-DMA stage (whole rows per wave instruction) avoids.
-constexpr int kMsRowPitch = 272;                 // bytes per row of a wave's image: 256 + 16 (spreads the tr reads)
-constexpr int kMsSlice = 32 * kMsRowPitch;       // one stage's image, per wave
-constexpr int kMsLds = kMfNW * kMsSlice + kMfNW * 4 * 32 * 4 + 16 * 32 * 2;  // images + partial z + residuals
-
-// AUX: the loads' cache policy -- nt like every X stream, or the default one: a wave's load instruction
-// covers 16 rows x 64 bytes, so the next K step's load reads the other half of each 128-byte line
-template <int LOSS, int AUX>
-__global__ void __launch_bounds__(512)
-grad_stream_mfma(const Segment* __restrict__ segs, const Task* __restrict__ tasks, const float* __restrict__ beta,
-                 float* __restrict__ slab, int ld, int R, const int* __restrict__ gate) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  if (gate_closed(gate)) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const Task lead = tasks[blockIdx.x * R];  // slot 0 of a bundle is always a real task
-  const Segment ls = segs[lead.seg];
-  const float* __restrict__ Y = static_cast<const float*>(ls.y) + lead.row_begin;
-  const int rowbytes = ld * 2;
-  const int nrows = lead.row_end - lead.row_begin;
-  const int nst = (nrows + 31) / 32;
-  unsigned char* xsw = smem_raw + w * kMsSlice;
-  float* zred = reinterpret_cast<float*>(smem_raw + kMfNW * kMsSlice);  // [wave][replica][32 rows]
-  __bf16* rres = reinterpret_cast<__bf16*>(zred + kMfNW * 4 * 32);      // [4 replica + term][32 rows]
-  const int fi = lane & 15, fg = lane >> 4, fq = fi >> 2, fp = fi & 3;
-
-  // residual role: (replica rm, stage row rn) for the first 128 threads
-  const int rm = tid >> 5, rn = tid & 31;
-  const bool rrole = tid < 128;
-  float rcoef = 0.f;
-  if (rrole && rm < R) {
-    const Task tq = tasks[blockIdx.x * R + rm];
-    if (tq.seg >= 0) rcoef = static_cast<float>(segs[tq.seg].coef);
-  }
-  // GEMM1 A fragments (packed): A[m = lane & 15][k] = term m & 3 of beta[k] for replica m >> 2 < R
-  const bool rep_ok = ((lane & 15) >> 2) < R && (lane & 3) < kMfSplit;
-  bf16x8 bfr[kMfKPW];
-#pragma unroll
-  for (int kk = 0; kk < kMfKPW; ++kk) {
-    const int k0 = (w * kMfKPW + kk) * 32 + 8 * fg;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      __bf16 t[kMfSplit];
-      split_bf16(rep_ok && k0 + j < ld ? beta[k0 + j] : 0.f, t);
-      const int sm = lane & 3;
-      bfr[kk][j] = sm == 0 ? t[0] : sm == 1 ? t[1] : t[2];
-    }
-  }
-  f32x4 g[kMfTPW];
-#pragma unroll
-  for (int t = 0; t < kMfTPW; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int slab_row = -1;  // lane group fg holds replica fg's G
-  if (fg < R) {
-    const Task tq = tasks[blockIdx.x * R + fg];
-    if (tq.seg >= 0) slab_row = tq.slab;
-  }
-  // the byte offset of each of this lane's column groups; columns past ld are clamped onto the row's last 8
-  // (their beta is 0 and their G columns are never stored)
-  int coff[kMfKPW];
-#pragma unroll
-  for (int kk = 0; kk < kMfKPW; ++kk) coff[kk] = min((w * kMfKPW + kk) * 32 + 8 * fg, ld - 8) * 2;
-  const auto rs = make_rsrc(static_cast<const unsigned char*>(ls.X) + static_cast<long long>(lead.row_begin) * rowbytes,
-                            nrows * rowbytes);
-  const auto yrs = make_rsrc(Y, nrows * 4);
-  // stage t's loads: 8 x 16 B per lane, unconditional (rows past the task clamp onto its last row, so the
-  // compiler counts the same loads in every stage and waits only for the oldest), plus one label per lane
-  auto load = [&](int t, uint4 (&xr)[8], float& yv) {
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int row = min(t * 32 + 16 * nt + fi, nrows - 1);
-#pragma unroll
-      for (int kk = 0; kk < kMfKPW; ++kk) xr[nt * kMfKPW + kk] = buf_load16<uint4, AUX>(rs, row * rowbytes + coff[kk]);
-    }
-    yv = buf_load_scalar<float>(yrs, 4 * min(t * 32 + (tid & 31), nrows - 1));  // (a flat load would count in lgkmcnt too)
-  };
-  auto process = [&](int t, const uint4 (&xr)[8], float yv) {
-    const int ns = min(32, nrows - t * 32);
-    f32x4 z[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    // every K step and every column tile, without branches (a K step past ld reads clamped columns against a
-    // zero beta; a tile past ld fills G columns that are never stored): the stage has no control flow for
-    // the compiler's wait counting to merge, so it waits only for the oldest stage's loads
-#pragma unroll
-    for (int kk = 0; kk < kMfKPW; ++kk) {
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        bf16x8 x;
-        __builtin_memcpy(&x, &xr[nt * kMfKPW + kk], 16);
-        z[nt] = mma(bfr[kk], x, z[nt]);
-        // the wave's image of its slice, row-major, for GEMM2's transposing reads
-        *reinterpret_cast<uint4*>(xsw + (16 * nt + fi) * kMsRowPitch + (kk * 32 + 8 * fg) * 2) = xr[nt * kMfKPW + kk];
-      }
-    }
-    // C: lane group fg = replica fg, its three terms in registers 0..2, stage row 16 nt + fi
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) zred[(w * 4 + fg) * 32 + 16 * nt + fi] = (z[nt][2] + z[nt][1]) + z[nt][0];
-    __syncthreads();  // every wave's partial z
-    if (rrole) {
-      float zs = 0.f;
-#pragma unroll
-      for (int v = 0; v < kMfNW; ++v) zs += zred[(v * 4 + rm) * 32 + rn];
-      const float r = rm < R && rn < ns ? residual_hw<LOSS>(zs, yv, rcoef) : 0.f;
-      __bf16 tt[kMfSplit];
-      split_bf16(r, tt);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) rres[(4 * rm + q) * 32 + rn] = q < kMfSplit ? tt[q < kMfSplit ? q : 0] : __bf16(0.f);
-    }
-    __syncthreads();  // the residuals
-    const bf16x8 ar = *reinterpret_cast<const bf16x8*>(rres + fi * 32 + 8 * fg);
-#pragma unroll
-    for (int tt = 0; tt < kMfTPW; ++tt) {
-      const unsigned char* a0 = xsw + (8 * fg + fq) * kMsRowPitch + (tt * 16 + 4 * fp) * 2;
-      const bf16x4 t0 = tr_read(a0);
-      const bf16x4 t1 = tr_read(a0 + 4 * kMsRowPitch);
-      const bf16x8 xb = bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
-      g[tt] = mma(ar, xb, g[tt]);
-    }
-  };
-  // a three-deep register ring, unrolled so every stage's registers are named statically
-  uint4 xa[8], xb[8], xc[8];
-  float ya = 0.f, yb = 0.f, yc = 0.f;
-  load(0, xa, ya);
-  load(1, xb, yb);
-  for (int t = 0; t < nst; t += 3) {
-    load(t + 2, xc, yc);
-    process(t, xa, ya);
-    if (t + 1 >= nst) break;
-    load(t + 3, xa, ya);
-    process(t + 1, xb, yb);
-    if (t + 2 >= nst) break;
-    load(t + 4, xb, yb);
-    process(t + 2, xc, yc);
-  }
-#pragma unroll
-  for (int tt = 0; tt < kMfTPW; ++tt) {
-    const int c0 = (w * kMfTPW + tt) * 16;
-    if (c0 >= ld) break;
-    const int col = c0 + fi;
-    if (slab_row >= 0 && col < ld) slab[static_cast<long long>(slab_row) * ld + col] = (g[tt][2] + g[tt][1]) + g[tt][0];
-  }
-}
+// (A VGPR-streamed form -- every wave loading its column slice of a stage straight into GEMM1's B-fragment
+// registers, a private LDS image for GEMM2 -- measured 0.475 ms with nt loads and 0.345 with the default
+// policy against the ring's 0.316: the fragment layout fixes each load instruction at 16 rows x 64 bytes, half
+// of every 128-byte line per request.  Removed in round 6; docs/PERF_NOTES.md, profiles/round6/bf16ab.)
 
 // ---- VGPR-staged ring (R <= 4, packed terms, 32-row stages) ---------------------------------------
 // grad_staged_mfma's LDS ring and arithmetic, but every stage is loaded into registers two stages ahead
@@ -659,13 +512,13 @@ void set_mfma_probe(int mode) { g_mfma_probe = mode >= 1 && mode <= 4 ? mode : 0
 // the packed-term form for R <= 4 (default) or the three-MFMA form, for A/B
 static bool g_mfma_pack = true;
 void set_mfma_pack(bool on) { g_mfma_pack = on; }
-// packed bundles (R <= 4) through the VGPR stream (grad_stream_mfma: 1 nt loads, 2 default-policy loads), the
-// VGPR-staged ring (grad_vring_mfma: 3 two register sets, 4 three) or the LDS-DMA stage ring (0, the default).
+// packed bundles (R <= 4) through the VGPR-staged ring (grad_vring_mfma: 3 two register sets, 4 three) or the
+// LDS-DMA stage ring (0, the default).
 // At the N = 1 rank shape (2 GB; profiles/round6/bf16ab/rows_ab*.jsonl, ring_vs_vring_r8e.jsonl): on two boxes
 // 0: 315.3-320.4 us, 3: 312.4-314.7, 4: 318.8-319.0 (stream alone 307.6-310.2 / 301.0-303.3 / 305.1-307.3);
 // on a third, four alternating reps, 0: 312.9-316.2, 3: 314.0-319.3.  Within the box-to-box spread: no default.
 static int g_mfma_stream = 0;
-void set_mfma_stream(int mode) { g_mfma_stream = mode >= 1 && mode <= 4 ? mode : 0; }
+void set_mfma_stream(int mode) { g_mfma_stream = mode == 3 || mode == 4 ? mode : 0; }
 
 bool mfma_geometry(int ld, int* rows, int* pieces, int* nstage, size_t* lds) {
   if (ld < 8 || ld > kMfNW * kMfKPW * 32 || ld % 8) return false;
@@ -703,16 +556,6 @@ hipError_t grad_mfma_launch(int loss, const Segment* segs, const Task* tasks, in
     if (ea != hipSuccess) return ea;
     hipLaunchKernelGGL(kern, dim3(ntasks / R), dim3(64 * kMfNW), vlds, st, segs, tasks, beta, slab, ld, R, gate,
                        g_mfma_probe);
-    return hipGetLastError();
-  }
-  if (pack && (g_mfma_stream == 1 || g_mfma_stream == 2) && g_mfma_probe == 0) {  // (ld <= 1024, ld % 8 == 0)
-    auto kern = g_mfma_stream == 1 ? (loss == kLogistic ? grad_stream_mfma<kLogistic, kStreamAux>
-                                                        : grad_stream_mfma<kLeastSquares, kStreamAux>)
-                                   : (loss == kLogistic ? grad_stream_mfma<kLogistic, 0> : grad_stream_mfma<kLeastSquares, 0>);
-    const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, kMsLds);
-    if (ea != hipSuccess) return ea;
-    hipLaunchKernelGGL(kern, dim3(ntasks / R), dim3(64 * kMfNW), kMsLds, st, segs, tasks, beta, slab, ld, R, gate);
     return hipGetLastError();
   }
   auto pick = [&](auto p32l, auto p32q, auto p16l, auto p16q) {

@@ -41,7 +41,7 @@ void set_slab_reduce_mode(int mode);
 void set_mfma_stage_rows(int rows);
 void set_mfma_probe(int mode);  // timing probes only (grad_mfma.hip): 1 stage stream alone, 2 compute alone
 void set_mfma_pack(bool on);    // bf16 MFMA bundles with R <= 4: bf16 terms packed into M (default) or 3 MFMAs
-void set_mfma_stream(int mode);  // packed bf16 bundles: 0 LDS-DMA ring, VGPR stream 1 nt / 2 default loads,
+void set_mfma_stream(int mode);  // packed bf16 bundles: 0 LDS-DMA ring (default),
                                  // VGPR-staged ring 3 (two register sets) / 4 (three)
 // Timeline probe: grad_dense_multi launches write {start, rows done, slab written, XCC} ticks per bundle
 // into `stamps` (int64 [4 * bundles]); nullptr turns it off (tools/probes/bundle_stamps.py).

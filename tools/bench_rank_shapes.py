@@ -125,9 +125,11 @@ def main():
     ap.add_argument("--ab-slab", action="store_true", help="also time the two-stage slab reduction (mode 0)")
     ap.add_argument("--slab-mode", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--mfma-rows", type=int, default=32, help="bf16 MFMA bundles: rows per LDS stage (32 / 16)")
-    ap.add_argument("--mfma-probe", type=int, default=0, help="bf16 MFMA timing probe: 1 loads only, 2 compute only")
+    ap.add_argument("--mfma-probe", type=int, default=0,
+                    help="bf16 MFMA timing probe: 1 loads only, 2 compute only (3 / 4, --mfma-stream 3 / 4: loads with / "
+                         "without the stage barriers, no LDS copies)")
     ap.add_argument("--mfma-stream", type=int, default=0,
-                    help="bf16 packed bundles: 0 LDS-DMA ring (default), 1 / 2 VGPR stream, 3 VGPR-staged ring, 4 its three-set form")
+                    help="bf16 packed bundles: 0 LDS-DMA ring (default), 3 VGPR-staged ring, 4 its three-set form")
     a = ap.parse_args()
     if a.one:
         print(json.dumps(one(a.one, a.precision, a.shard, a.rows, a.fill, a.slab_mode, a.mfma_rows, a.mfma_probe,

@@ -83,17 +83,17 @@ for s in "${STAGES[@]}"; do
       run 600 sparse.log python -u tools/bench_kernels.py --only sparse --out "$OUT/sparse.jsonl"
       run 600 prof_sparse.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_sparse" -o run -- \
         python tools/bench_kernels.py --only sparse --out /tmp/sparse_prof.jsonl ;;
-    bf16ab)  # the bf16 MFMA bundles: LDS-DMA ring vs VGPR stream, kernel alone (rank shape N = 1) and headline
-      for m in ${MFMA_MODES:-0 1 2 0 1 2}; do
+    bf16ab)  # the bf16 MFMA bundles: LDS-DMA ring vs VGPR-staged ring, kernel alone (rank shape N = 1) and headline
+      for m in ${MFMA_MODES:-0 3 0 3}; do
         run 300 "bf16_shape_$m.log" python -u tools/bench_rank_shapes.py --one 1 --precision bf16 --mfma-stream $m
         cat "$OUT/bf16_shape_$m.log" >> "$OUT/bf16_shapes.jsonl"
       done
-      for m in ${MFMA_BENCH:-0 2}; do
+      for m in ${MFMA_BENCH:-0 3}; do
         run 600 "bench_bf16_s$m.log" $BENCH --precision bf16 --mfma-stream $m --steps 100 --warmup 10 \
           && tail -1 "$OUT/bench_bf16_s$m.log" > "$OUT/bench_bf16_s$m.json"
       done
-      run 300 prof_bf16_stream.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bf16_stream" -o run -- \
-        python bench.py --no-floor --no-breakdown --precision bf16 --mfma-stream 1 --steps 50 ;;
+      run 300 prof_bf16_vring.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bf16_vring" -o run -- \
+        python bench.py --no-floor --no-breakdown --precision bf16 --mfma-stream 3 --steps 50 ;;
     sparseab)  # sparse gradients at the real shapes (naive / cyclic-style / FRC layouts), then the sparse suite rows
       run 600 sparse.log python -u tools/bench_kernels.py --only sparse --out "$OUT/sparse.jsonl"
       run 900 suite_sparse.log python -u tools/bench_suite.py --out "$OUT/suite" \
