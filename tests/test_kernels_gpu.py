@@ -258,7 +258,7 @@ def test_sparse_replicas_share_reads_and_match_per_message(native):
 def test_sparse_frc_units_write_every_replica(prec_name, tol, rows, use_ell, native):
     """FRC / AGC messages (each group's members send the sum of the group's partitions, coefficient 1,
     ref src/replication.py:56-68): the device stacks a group's partitions into one unit, the column pass
-    stages the whole unit (<= 4096 rows: 4 residuals per thread, up to 8192: 8) and writes its sums into
+    stages the whole unit (up to 8192 rows, 8 residuals per thread: the UNITS variant) and writes its sums into
     every member's message row -- no partition rows, no encoding launch.  Every row against the scipy
     oracle, bitwise run to run, through plan.run and the native launcher, padding columns untouched."""
     from erasurehead_amd.data.synthetic import onehot_partitions
