@@ -86,6 +86,9 @@ def parse(argv=None):
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl", "loopback"])
     ap.add_argument("--round-timeout", type=float, default=120.0, help="bounds any hang (a round takes ms)")
+    ap.add_argument("--subrun-timeout", type=float, default=20.0,
+                    help="round timeout of every run after the headline (a failed sub-run is found within a few of "
+                         "them and recorded in subrun_failures; the headline keeps --round-timeout)")
     ap.add_argument("--device-loop", default="auto", choices=["auto", "graph", "stream", "off"])
     ap.add_argument("--tie-break", default="permute", choices=["permute", "worker"])
     ap.add_argument("--preflight", type=int, default=1000,
@@ -194,6 +197,11 @@ def main(argv=None) -> int:
     # N > 1: the job checks the exact path its headline will take before anything is timed (preflight
     # round trips per pair, then a bounded integrity-tagged run), stepping down arbiter -> native pump ->
     # RCCL p2p on any failure, in this process (first_contact)
+    # test hook ERASUREHEAD_SABOTAGE=subrun:<spec>: ERASUREHEAD_SABOTAGE=<spec> from the first run after the
+    # headline on (the containment of the sub-runs below)
+    late_sabotage = None
+    if os.environ.get("ERASUREHEAD_SABOTAGE", "").startswith("subrun:"):
+        late_sabotage = os.environ.pop("ERASUREHEAD_SABOTAGE").split(":", 1)[1]
     contact = first_contact(a, make_cfg, env, free, Trainer, TransportError) if env.world > 1 else None
     t_setup = time.perf_counter()
     trainer = Trainer(make_cfg(w0 + a.steps), env)
@@ -314,29 +322,51 @@ def main(argv=None) -> int:
     free(trainer)
     del trainer, res
 
+    # Every run after the headline is contained (Trainer.run_contained: one verdict on every rank): a failure
+    # is recorded in `subrun_failures` and the collective runs after it are skipped on every rank alike, so a
+    # sub-run that breaks on new hardware never costs the headline line.
+    failures = {}
+    a.round_timeout = min(a.round_timeout, a.subrun_timeout)  # make_cfg reads it at every call
+    if late_sabotage:
+        os.environ["ERASUREHEAD_SABOTAGE"] = late_sabotage
+
+    class _SubRunFailed(Exception):
+        pass
+
+    def contained(name: str, tr_, **kw):
+        res_, why_ = tr_.run_contained(**kw)
+        if why_:
+            failures[name] = why_
+            if env.is_master:
+                print(f"[bench] WARNING: {name} run failed ({why_}); the later sub-runs are skipped", file=sys.stderr,
+                      flush=True)
+        return res_, why_ is None
+
     # ---- 2. the same rounds host-driven, instrumented: real wait-for-k path + per-rank breakdown -----
     if not a.no_breakdown:
         headline = reports
         # N > 1: device records too, for the worker half of the round chain (worker_round_start_latency)
         tr = Trainer(make_cfg(w0 + a.steps, device_loop="off", instrument=True, device_records=env.world > 1), env)
-        r = tr.run(timed_start=w0)
-        t = env.allreduce_max(r.timed_seconds if env.is_master else tr.worker_timed_seconds)
-        reports = env.gather_objects(tr.rank_report())
-        if env.world > 1:
-            lat = worker_round_start_latency(env.gather_objects(tr.device_records), w0)
+        r, ok = contained("breakdown", tr, timed_start=w0)
+        if ok:
+            t = env.allreduce_max(r.timed_seconds if env.is_master else tr.worker_timed_seconds)
+            reports = env.gather_objects(tr.rank_report())
+            if env.world > 1:
+                lat = worker_round_start_latency(env.gather_objects(tr.device_records), w0)
+                if env.is_master:
+                    for rep in reports:
+                        if rep["rank"] in lat:
+                            rep["beta_to_round_start_us"] = lat[rep["rank"]]
+            if env.is_master:  # the headline run's device-side master ticks (arbiter: poll / update / release)
+                for rep, h in zip(reports, headline):
+                    rep.update({f"headline_{k}": v for k, v in h.items()
+                                if k.startswith("arbiter_") or k in ("device_round_us", "round_loop")})
             if env.is_master:
-                for rep in reports:
-                    if rep["rank"] in lat:
-                        rep["beta_to_round_start_us"] = lat[rep["rank"]]
-        if env.is_master:  # the headline run's device-side master ticks (arbiter: poll / update / release)
-            for rep, h in zip(reports, headline):
-                rep.update({f"headline_{k}": v for k, v in h.items()
-                            if k.startswith("arbiter_") or k in ("device_round_us", "round_loop")})
-        if env.is_master:
-            out["host_driven_ms_per_step"] = 1e3 * t / a.steps
-            out["host_driven_instrumented"] = True
+                out["host_driven_ms_per_step"] = 1e3 * t / a.steps
+                out["host_driven_instrumented"] = True
         free(tr)
         del tr, r
+
     if env.is_master:
         for rep, k in zip(reports, kernel_iso):
             if k is not None:
@@ -351,7 +381,7 @@ def main(argv=None) -> int:
     # every round (a device spin after its gradient, before its put: ref src/naive.py:141-148), and
     # AGC with a lazy drain (no wait for the tail, stale rounds skipped on the late rank) is timed
     # against naive (which must wait for every worker), each with and without the straggler.
-    if env.world > 1 and not a.no_straggler:
+    if env.world > 1 and not a.no_straggler and not failures:
         S, W = a.straggler_steps, a.workers
         late_rank = env.world - 1
         late_workers = [w for w in range(W) if w % env.world == late_rank]  # parallel/placement.py place_spread
@@ -366,7 +396,11 @@ def main(argv=None) -> int:
             else:
                 extra.update(add_delay=0)
             tr_s = Trainer(make_cfg(warm + steps, naive=naive, **extra), env)
-            r_s = tr_s.run(timed_start=warm)
+            r_s, ok_s = contained(f"{'naive' if naive else 'scheme'}_{'late' if late else 'on_time'}_{extra['shard']}",
+                                  tr_s, timed_start=warm)
+            if not ok_s:
+                free(tr_s)
+                raise _SubRunFailed()
             t_s = env.allreduce_max(r_s.timed_seconds if env.is_master else tr_s.worker_timed_seconds)
             reps = env.gather_objects(tr_s.rank_report())
             rec = None
@@ -378,13 +412,16 @@ def main(argv=None) -> int:
             free(tr_s)
             return rec
 
-        topo = sub_run(a.naive, False, warm=w0, steps=a.steps)  # the headline's warm-up and step count
-        straggler = {
-            "late_rank": late_rank, "late_workers": late_workers, "late_ms": a.late_ms, "placement": "message",
-            "steps": S, "agc_lazy": sub_run(False, True, drain="lazy"),
-            "agc_lazy_no_straggler": sub_run(False, False, drain="lazy"),
-            "naive": sub_run(True, True), "naive_no_straggler": sub_run(True, False)}
-        if env.is_master:
+        try:
+            topo = sub_run(a.naive, False, warm=w0, steps=a.steps)  # the headline's warm-up and step count
+            straggler = {
+                "late_rank": late_rank, "late_workers": late_workers, "late_ms": a.late_ms, "placement": "message",
+                "steps": S, "agc_lazy": sub_run(False, True, drain="lazy"),
+                "agc_lazy_no_straggler": sub_run(False, False, drain="lazy"),
+                "naive": sub_run(True, True), "naive_no_straggler": sub_run(True, False)}
+        except _SubRunFailed:
+            topo = straggler = None
+        if env.is_master and topo is not None and straggler is not None:
             out["message_placement_ms_per_step"] = topo["ms_per_step"]
             out["message_placement"] = topo
             # the straggler-tolerant co-headline: the reference topology (one worker's s+1 partitions per
@@ -401,9 +438,11 @@ def main(argv=None) -> int:
             out["straggler"] = straggler
 
     # ---- 2c. N > 1: the same problem on rank 0's GPU alone, in this job (the scaling denominator) --------
-    if env.world > 1 and a.single_ref:
+    if env.world > 1 and a.single_ref and not failures:
         single = single_gpu_reference(a, make_cfg, env, free, Trainer, clock_rounds)
-        if env.is_master:
+        if env.is_master and isinstance(single, str):  # rank 0's solo run failed: recorded, not collective
+            out["single_gpu_reference_failure"] = single
+        elif env.is_master:
             out["single_gpu_s_per_iter"] = single
             out["single_gpu_definition"] = ("the headline config on rank 0's GPU alone (world 1, every message "
                                             "local), timed in this job right after the N-rank runs")
@@ -414,15 +453,17 @@ def main(argv=None) -> int:
                                          "value_tolerant": "message (the reference topology)"}
 
     # ---- 3. convergence: naive (exact GD) sets the common loss target, then the scheme -------------
-    if not a.no_floor:
+    if not a.no_floor and not failures:
         curves = {}
         for name, naive in (("naive", True), ("scheme", a.naive)):
             if name == "scheme" and a.naive:
                 curves["scheme"] = curves["naive"]
                 continue
             tr2 = Trainer(make_cfg(a.floor_rounds, naive=naive), env)
-            r2 = tr2.run()
+            r2, ok2 = contained(f"floor_{name}", tr2)
             free(tr2)
+            if not ok2:
+                break
             if env.is_master:
                 tr2.cfg.fix_quirks = True  # evaluate on every partition
                 if torch.cuda.is_available():
@@ -431,7 +472,7 @@ def main(argv=None) -> int:
                 ev = evaluate(tr2, r2, write=False)
                 curves[name] = (ev, r2, time.perf_counter() - t_ev)
             del tr2, r2
-        if env.is_master:
+        if env.is_master and "scheme" in curves:
             ev_n, r_n, _ = curves["naive"]
             ev, r2, eval_s = curves["scheme"]
             target = float(ev_n.training_loss[-1]) * 1.01
@@ -458,18 +499,29 @@ def main(argv=None) -> int:
     # and AGC with the lazy drain (no wait for the tail, a worker still busy skips the stale round: the
     # replacement of the reference's send Cancel, ref src/coded.py:178-180) run one after another, each
     # for --floor-rounds rounds, and are compared on wall-clock to the common loss target.
-    if env.world == 1 and not a.no_straggler and not a.no_floor:
-        blk = virtual_straggler_block(a, make_cfg, env, free, Trainer, evaluate,
-                                      out.get("ms_per_step", 0.0) / 1e3 if env.is_master else 0.0)
-        if env.is_master:
+    if env.world == 1 and not a.no_straggler and not a.no_floor and not failures:
+        try:  # one process: nothing collective inside, so a failure here is this rank's alone
+            blk = virtual_straggler_block(a, make_cfg, env, free, Trainer, evaluate,
+                                          out.get("ms_per_step", 0.0) / 1e3 if env.is_master else 0.0)
             out["straggler_virtual"] = blk
+        except Exception as e:  # noqa: BLE001 -- recorded in the JSON, the headline line still prints
+            failures["straggler_virtual"] = f"{type(e).__name__}: {e}"
+            print(f"[bench] WARNING: straggler_virtual failed ({e})", file=sys.stderr, flush=True)
     env.barrier()
+    if env.is_master and failures:
+        out["subrun_failures"] = failures
     if env.is_master:
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
+    if failures and env.world > 1:
+        # a contained failure can leave receives posted on the process group that nothing will match
+        # (gloo cannot cancel them), and its teardown would wait on them: the line is out, leave now
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     env.shutdown()
     return 0
 
@@ -501,7 +553,8 @@ def single_gpu_reference(a, make_cfg, env, free, Trainer, clock_rounds: int):
     """N > 1: rank 0 runs the headline configuration by itself (a world-1 Trainer on its own GPU: every
     message local, the single-process device loop) for --steps timed rounds after the same warm-up,
     while the other ranks wait at a barrier.  Returns its s/iter on rank 0 (None elsewhere): the
-    denominator of the job's own scaling efficiencies, measured on the same node in the same job."""
+    denominator of the job's own scaling efficiencies, measured on the same node in the same job (a failed
+    solo run returns its reason instead)."""
     from erasurehead_amd.parallel.dist import DistEnv
 
     env.barrier()
@@ -510,8 +563,8 @@ def single_gpu_reference(a, make_cfg, env, free, Trainer, clock_rounds: int):
         solo = DistEnv(rank=0, world=1, local_rank=env.local_rank, device=env.device, backend="none")
         w0 = clock_rounds + a.warmup
         tr = Trainer(make_cfg(w0 + a.steps), solo)
-        r = tr.run(timed_start=w0)
-        sec = r.timed_seconds / a.steps
+        r, why = tr.run_contained(timed_start=w0)  # world 1: a verdict of this rank alone
+        sec = r.timed_seconds / a.steps if why is None else why
         free(tr)
         del tr, r
     env.barrier()

@@ -122,6 +122,25 @@ def test_bench_one_gpu_straggler_block(tmp_path):
     assert st["agc_lazy"]["speedup_to_target_vs_naive"] == pytest.approx(nv / lz)
 
 
+def test_bench_subrun_failure_keeps_the_headline(tmp_path):
+    """A run after the headline that fails on every rank alike (here: worker rank 1's round loop raises in
+    the instrumented breakdown run, ERASUREHEAD_SABOTAGE=subrun:raise:1:2) is contained: the JSON line still
+    carries the headline value, names the failed sub-run in `subrun_failures`, and the collective sub-runs
+    after it are skipped on every rank (no hang, exit 0)."""
+    out = tmp_path / "b.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *TINY, "--straggler-steps", "4",
+                        "--subrun-timeout", "3", "--clock-warmup-ms", "0", "--json-out", str(out)],
+                       cwd=str(tmp_path), env=dict(_env(), ERASUREHEAD_SABOTAGE="subrun:raise:1:2"),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["ms_per_step"] > 0
+    assert list(d["subrun_failures"]) == ["breakdown"], d.get("subrun_failures")
+    assert "rank 1" in d["subrun_failures"]["breakdown"] or "test hook" in d["subrun_failures"]["breakdown"]
+    assert "straggler" not in d and "loss_target" not in d and "single_gpu_s_per_iter" not in d
+    assert "host_driven_ms_per_step" not in d
+
+
 def test_bench_world_size_mismatch_fails(tmp_path):
     env = _env()
     env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
