@@ -85,7 +85,8 @@ def parse(argv=None):
     ap.add_argument("--tasks", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl", "loopback"])
-    ap.add_argument("--round-timeout", type=float, default=120.0, help="bounds any hang (a round takes ms)")
+    ap.add_argument("--round-timeout", type=float, default=30.0,
+                    help="bounds any hang (a round takes ms; a gone rank is found within a few of these)")
     ap.add_argument("--subrun-timeout", type=float, default=20.0,
                     help="round timeout of every run after the headline (a failed sub-run is found within a few of "
                          "them and recorded in subrun_failures; the headline keeps --round-timeout)")
@@ -207,14 +208,15 @@ def main(argv=None) -> int:
     trainer = Trainer(make_cfg(w0 + a.steps), env)
     setup_s = time.perf_counter() - t_setup
     res, why = trainer.run_contained(timed_start=w0)
-    if why is not None:  # the headline itself failed after a clean first contact: one rung down, once
-        step = step_down(a, env, trainer, why)
+    while why is not None:  # the headline itself failed after a clean first contact: one rung down and again
+        step = step_down(a, env, trainer, why)  # (raises once nothing is left below)
         if env.is_master:
             print(f"[bench] WARNING: headline run failed ({why}); rebuilding: {step}", file=sys.stderr, flush=True)
         free(trainer)
-        contact = dict(contact or {}, headline_failure=why, headline_step_down=step)
+        contact = dict(contact or {})
+        contact.setdefault("headline_failures", []).append({"failure": why, "step_down": step})
         trainer = Trainer(make_cfg(w0 + a.steps), env)
-        res = trainer.run(timed_start=w0)
+        res, why = trainer.run_contained(timed_start=w0)
     mine = res.timed_seconds if env.is_master else trainer.worker_timed_seconds
     timed = env.allreduce_max(mine)
     sch = trainer.scheme
