@@ -564,11 +564,14 @@ def single_gpu_reference(a, make_cfg, env, free, Trainer, clock_rounds: int):
     if env.is_master:
         solo = DistEnv(rank=0, world=1, local_rank=env.local_rank, device=env.device, backend="none")
         w0 = clock_rounds + a.warmup
-        tr = Trainer(make_cfg(w0 + a.steps), solo)
-        r, why = tr.run_contained(timed_start=w0)  # world 1: a verdict of this rank alone
-        sec = r.timed_seconds / a.steps if why is None else why
-        free(tr)
-        del tr, r
+        try:  # rank 0 alone: whatever fails here must still reach the barrier the others wait at
+            tr = Trainer(make_cfg(w0 + a.steps), solo)
+            r, why = tr.run_contained(timed_start=w0)  # world 1: a verdict of this rank alone
+            sec = r.timed_seconds / a.steps if why is None else why
+            free(tr)
+            del tr, r
+        except Exception as e:  # noqa: BLE001 -- recorded as single_gpu_reference_failure
+            sec = f"{type(e).__name__}: {e}"
     env.barrier()
     return sec
 
