@@ -423,6 +423,15 @@ def main(argv=None) -> int:
                 "naive": sub_run(True, True), "naive_no_straggler": sub_run(True, False)}
         except _SubRunFailed:
             topo = straggler = None
+        except Exception as e:  # noqa: BLE001 -- e.g. a transport that failed to build: its peers fail with it
+            failures["straggler_setup"] = f"rank {env.rank}: {type(e).__name__}: {e}"
+            topo = straggler = None
+        # one view of what failed on every rank (a construction error is raised on each side of its pair)
+        seen = env.gather_objects(dict(failures))  # (the list on rank 0, None elsewhere)
+        merged = env.broadcast_object({k: v for f in seen for k, v in f.items()} if env.is_master else None, 0)
+        failures.update(merged)
+        if failures:
+            topo = straggler = None
         if env.is_master and topo is not None and straggler is not None:
             out["message_placement_ms_per_step"] = topo["ms_per_step"]
             out["message_placement"] = topo
