@@ -43,6 +43,20 @@ __device__ __forceinline__ V buf_load16(__amdgpu_buffer_rsrc_t rs, int byte_off)
   __builtin_memcpy(&out, &v, 16);
   return out;
 }
+// One 4- / 8-byte element stored through a buffer descriptor (past the descriptor's size: dropped).
+template <typename A>
+__device__ __forceinline__ void buf_store(__amdgpu_buffer_rsrc_t rs, int byte_off, A v) {
+  if constexpr (sizeof(A) == 8) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 u;
+    __builtin_memcpy(&u, &v, 8);
+    __builtin_amdgcn_raw_buffer_store_b64(u, rs, byte_off, 0, 0);
+  } else {
+    unsigned u;
+    __builtin_memcpy(&u, &v, 4);
+    __builtin_amdgcn_raw_buffer_store_b32(u, rs, byte_off, 0, 0);
+  }
+}
 template <typename A>
 __device__ __forceinline__ A buf_load_scalar(__amdgpu_buffer_rsrc_t rs, int byte_off) {
   if constexpr (sizeof(A) == 8) {

@@ -650,21 +650,29 @@ __global__ void __launch_bounds__(1024, 2) csc_tiles_lds(const SparseArgs a, con
     const A carry = fl & 1u ? A(0) : prev;       // into this lane's entries before its first flag
     const unsigned cmask = fl ? (fl & (0u - fl)) - 1u : 0xffu;
     // the output rows of sub-block p (wave-uniform): row p, or its shared message rows (SparseArgs::dst)
-    A* __restrict__ gout = static_cast<A*>(a.Gs) + static_cast<long long>(p) * a.ld;
-    long long doff[kSparseMaxDst];
-    int nd = 0;
+    // the output row(s) through buffer descriptors (wave-uniform, in SGPRs): a run's store is one instruction
+    // on the column's 32-bit byte offset, no 64-bit address per lane (UNITS: one descriptor per message row
+    // of the unit; a missing destination gets a zero-size descriptor, its stores dropped)
+    const auto grs = make_rsrc(static_cast<A*>(a.Gs) + static_cast<long long>(p) * a.ld, a.ld * static_cast<int>(sizeof(A)));
+    __amdgpu_buffer_rsrc_t drs[kSparseMaxDst];
+    int nd = 0;  // (a unit's rows come first in its dst entry)
     if constexpr (UNITS) {
 #pragma unroll
       for (int q = 0; q < kSparseMaxDst; ++q) {
         const int r = __builtin_amdgcn_readfirstlane(a.dst[p * kSparseMaxDst + q]);
-        if (r >= 0) doff[nd++] = static_cast<long long>(r) * a.ld;
+        nd += r >= 0 ? 1 : 0;
+        drs[q] = make_rsrc(static_cast<A*>(a.Gs) + static_cast<long long>(r >= 0 ? r : 0) * a.ld,
+                           r >= 0 ? a.ld * static_cast<int>(sizeof(A)) : 0);
       }
     }
     auto put = [&](int col, A val) {
       if constexpr (UNITS) {
-        for (int q = 0; q < nd; ++q) static_cast<A*>(a.Gs)[doff[q] + col] = val;
+        const int off = col * static_cast<int>(sizeof(A));
+#pragma unroll
+        for (int q = 0; q < kSparseMaxDst; ++q)
+          if (q < nd) buf_store(drs[q], off, val);
       } else {
-        gout[col] = val;
+        buf_store(grs, col * static_cast<int>(sizeof(A)), val);
       }
     };
     if (compact) {
