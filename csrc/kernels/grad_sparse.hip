@@ -210,7 +210,9 @@ __global__ void __launch_bounds__(256) csr_rows(const SparseArgs a, const A* __r
   const long long row = gid / G;
   const int sub = threadIdx.x % G;
   if (row >= a.nrows) return;  // whole group exits together (G divides 64)
-  const long long b = a.row_ptr[row], e = a.row_ptr[row + 1];
+  // one-hot rows (the same nnz in every row): the row's entries start at row * nnz, one dependent load less
+  const long long b = a.csr_fixed ? row * a.csr_fixed : a.row_ptr[row];
+  const long long e = a.csr_fixed ? b + a.csr_fixed : a.row_ptr[row + 1];
   const A* __restrict__ vals = static_cast<const A*>(a.vals);
   A z = A(0);
   for (long long q = b + sub; q < e; q += G) z = fma(vals ? vals[q] : A(1), beta[a.col_idx[q]], z);

@@ -71,6 +71,7 @@ struct SparseArgs {
   long long ell_ld;             // ELL row stride (>= nrows; even: the LDS row pass loads row pairs)
   const int* lo;                // [m] category window starts (idx16)
   const long long* row_ptr;     // CSR [nrows + 1]
+  int csr_fixed;                // CSR with the same nnz in every row (one-hot data): that nnz, row_ptr unread; else 0
   const int* col_idx;           // CSR [nnz]
   const void* vals;             // ELL [m][ell_ld] or CSR [nnz] values; nullptr: pattern-only (1.0)
   const void* y;                // [nrows] labels (acc dtype)

@@ -228,7 +228,7 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
                                           std::optional<Tensor> wg, int64_t u_lds, std::optional<Tensor> Gs,
                                           std::optional<Tensor> sub_begin, std::optional<Tensor> runs,
                                           std::optional<Tensor> tkeys, std::optional<Tensor> wspan,
-                                          std::optional<Tensor> wspan_ptr, std::optional<Tensor> dst) {
+                                          std::optional<Tensor> wspan_ptr, std::optional<Tensor> dst, int64_t csr_fixed) {
   for (auto* t : {&y, &u, &crow, &col_ptr, &tiles, &part_entry0, &part_row0, &part_nnz, &head, &tail, &span, &empty})
     need_gpu(*t, "sparse plan operand");
   need(tiles.scalar_type() == at::kInt && tiles.dim() == 2 && tiles.size(1) == 4, "tiles: int32 [n, 4]");
@@ -274,6 +274,8 @@ std::shared_ptr<GradLauncher> make_sparse(int64_t loss, const Tensor& y, const T
     need(row_ptr->scalar_type() == at::kLong && row_ptr->numel() == a.nrows + 1, "row_ptr: int64 [rows + 1]");
     a.row_ptr = reinterpret_cast<const long long*>(row_ptr->data_ptr<int64_t>());
     a.col_idx = col_idx->data_ptr<int>();
+    need(csr_fixed >= 0 && (csr_fixed == 0 || col_idx->numel() == csr_fixed * a.nrows), "csr_fixed: nnz of every row");
+    a.csr_fixed = (int)csr_fixed;
     g->keep.push_back(*row_ptr);
     g->keep.push_back(*col_idx);
   }
@@ -2215,7 +2217,7 @@ void bind_engine(py::module& m) {
                   py::arg("nparts"), py::arg("d"), py::arg("ld"), py::arg("wg") = py::none(), py::arg("u_lds") = 0,
                   py::arg("Gs") = py::none(), py::arg("sub_begin") = py::none(),
                   py::arg("runs") = py::none(), py::arg("tkeys") = py::none(), py::arg("wspan") = py::none(),
-                  py::arg("wspan_ptr") = py::none(), py::arg("dst") = py::none())
+                  py::arg("wspan_ptr") = py::none(), py::arg("dst") = py::none(), py::arg("csr_fixed") = 0)
       .def("set_encode",
            [](GradLauncher& g, const Tensor& ptr, const Tensor& idx, const Tensor& coef, const Tensor& Gb) {
              for (auto* t : {&ptr, &idx, &coef, &Gb}) need_gpu(*t, "encode operand");

@@ -741,6 +741,7 @@ class SparseGradPlan:
         self.u = torch.zeros(max(1, self.nrows), dtype=acc, device=dev)
         nnz_row = np.diff(X.indptr)
         self.ell_idx = self.ell_lo = self.row_ptr = self.col_idx = self.vals = None
+        self.csr_fixed = 0
         beta_lds = self.d * torch.tensor([], dtype=acc).element_size() <= self.ELL_LDS_BYTES
         if use_ell == "auto":
             use_ell = beta_lds
@@ -769,6 +770,9 @@ class SparseGradPlan:
         else:
             self.row_ptr = torch.from_numpy(X.indptr.astype(np.int64)).to(dev)
             self.col_idx = torch.from_numpy(X.indices.astype(np.int32)).to(dev)
+            # one-hot rows: the same nnz everywhere, so the row pass skips its row_ptr load
+            if self.nrows and np.all(nnz_row == nnz_row[0]) and nnz_row[0] > 0:
+                self.csr_fixed = int(nnz_row[0])
             if not self.pattern_only:
                 self.vals = torch.from_numpy(X.data.astype(npacc)).to(dev)
         # residual sub-blocks staged in LDS by the column pass: 4096 rows (32 KB fp64, 16 KB fp32; four
@@ -1015,7 +1019,8 @@ class SparseGradPlan:
                                              self.span, empty, self.nsub, self.d, self.ld,
                                              wg=self.wg if len(self.wg) else None, u_lds=self.u_lds, Gs=self.Gs,
                                              sub_begin=self.sub_begin, runs=self.runs, tkeys=self.tkeys,
-                                             wspan=self.wspan, wspan_ptr=self.wspan_ptr, dst=self.dst)
+                                             wspan=self.wspan, wspan_ptr=self.wspan_ptr, dst=self.dst,
+                                             csr_fixed=self.csr_fixed)
             if not self.identity:
                 L.set_encode(self.enc_ptr, self.enc_idx, self.enc_coef, self.Gb)
             self._launcher = L
