@@ -236,3 +236,27 @@ def test_bench_first_contact_steps_down_on_integrity_failure(tmp_path):
     assert fc["round_loop"] == "native pump"
     assert d["config"]["round_loop"] == "host-driven (native pump)"
     assert d["ms_per_step"] > 0
+
+
+def test_worker_round_start_latency_maps_both_clocks():
+    """bench.worker_round_start_latency: the master's beta(i) put stamp and each worker's round-i start stamp
+    live on different GPU clocks; both are mapped to the host clock through each rank's (tick0, t0, hz)
+    calibration before they are subtracted, unstamped rounds (-1) are skipped, and the median over the
+    rounds from ``first`` on is reported per worker rank in microseconds."""
+    sys.path.insert(0, ROOT)
+    from bench import worker_round_start_latency
+
+    hz0, hz1 = 100e6, 25e6
+    R = 6
+    beta_put = [[-1, -1] for _ in range(R)]
+    rounds = [[-1] * 10 for _ in range(R)]
+    for i in range(R):
+        t_put = 10.0 + i * 1e-3  # host seconds of the master's post-put stamp
+        beta_put[i][1] = 5_000 + (t_put - 2.0) * hz0  # master clock: tick0 5000 at host t0 = 2.0 s
+        rounds[i][9] = 700 + (t_put + (3 + i) * 1e-6 - 4.0) * hz1  # worker: starts 3 + i us later
+    rounds[2][9] = -1  # an unstamped round is skipped
+    recs = [{"rank": 0, "clock": (0, 5_000, 2.0, hz0), "beta_put": beta_put, "probes": []},
+            {"rank": 1, "clock": (0, 700, 4.0, hz1), "rounds": rounds}]
+    lat = worker_round_start_latency(recs, first=1)
+    assert set(lat) == {1}
+    assert abs(lat[1] - 6.5) < 0.05, lat  # rounds 1, 3, 4, 5: 4, 6, 7, 8 us -> median 6.5
