@@ -195,10 +195,12 @@ grad_dense_fused(const Segment* __restrict__ segs, const Task* __restrict__ task
 // profiles/round3/choices), which this halves.
 // stamps (a timeline probe, tools/probes/bundle_stamps.py; nullptr in every production launch): per
 // bundle {start, rows done, slab written, XCC id} in wall_clock64 ticks, one vector store of lane 0 each.
-// Rows in flight per wave of grad_dense_multi: 2 for fp64 / fp32 rows (8 / 4 KB at d = 1000), 6 for
-// bf16 (2 KB rows: 12 KB in flight per wave; 3 waves per SIMD at R = 3, 169 VGPRs and 2 waves with 8).
+// Rows in flight per wave of grad_dense_multi: 2 for fp64 rows (8 KB at d = 1000; 3 measured 1184.5 vs
+// 1181 us at the N = 1 rank shape, 278 VGPRs), 3 for fp32 (4 KB rows: 570-573 vs 588-590 us at N = 1, 81-83
+// vs 84 at N = 8, profiles/round6/fp32_depth; 4 was slower, round 5), 6 for bf16 (2 KB rows: 12 KB in flight
+// per wave; 3 waves per SIMD at R = 3, 169 VGPRs and 2 waves with 8).
 template <typename T>
-constexpr int kMultiDepth = std::is_same<T, bf16_t>::value ? 6 : 2;
+constexpr int kMultiDepth = std::is_same<T, bf16_t>::value ? 6 : std::is_same<T, float>::value ? 3 : 2;
 
 template <typename T, typename A, int CPL, int LOSS, int R, bool FOLD, int EPI = 0>
 __global__ void __launch_bounds__(256)
