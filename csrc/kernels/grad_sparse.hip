@@ -829,7 +829,9 @@ hipError_t grad_sparse_launch(int dtype, int loss, const SparseArgs& a, const vo
       }
 #undef EH_ELL
     } else {
-      constexpr int Gs = 16;
+      // lanes per CSR row: 8 (16 / 8 / 4 at kc_house 13.45 / 13.2 / 13.05 us, amazon 21.4 / 21.2 / 21.7,
+      // covtype 96.7 / 82.7 / 89.0: profiles/round6/sparse/csr_lanes)
+      constexpr int Gs = 8;
       const dim3 grid(static_cast<unsigned>((a.nrows * Gs + 255) / 256));
       if (dtype == 0) {
         if (loss == kLogistic)

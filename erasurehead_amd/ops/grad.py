@@ -641,7 +641,7 @@ class SparseGradPlan:
     WG_SPANS = True  # (False: the csc_spans launch; tools/bench_kernels.py --no-wg-spans, for A/B)
     # beta bytes the ELL row pass stages in LDS (grad_sparse.hip kEllLdsBytes).  ELL rows pay off there
     # (covtype-shaped, 124 KB of fp64 beta: 54.7 vs 105.3 us with CSR rows); a beta that does not fit
-    # leaves ELL one row per thread gathering from L2, which the CSR pass (16 lanes per row) beats on
+    # leaves ELL one row per thread gathering from L2, which the CSR pass (8 lanes per row since round 6) beats on
     # the real shapes (amazon 33.1 vs 37.9 us, kc_house 18.4 vs 18.9: profiles/round4/r5a/breakdown.txt)
     ELL_LDS_BYTES = 148 * 1024
     # FRC / AGC units: a group's replicas all send the SAME message (the sum of the group's partitions,
